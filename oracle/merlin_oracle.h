@@ -1,0 +1,98 @@
+/*
+ * merlin_oracle.h -- TEST INFRASTRUCTURE ONLY (the parity checker).
+ *
+ * Plain-C CPU restatement of the reference's hot path for PPO-2DGrid ("MERLIN"):
+ *   - numpy Generator(PCG64(SeedSequence(seed))) draw model (gymnasium
+ *     `seeding.np_random`, used by `MiniGridEnv._rand_int`),
+ *   - the MERLIN map generators (src/custom_envs/<difficulty>_env.py) on top of the
+ *     minigrid-3.0.0 `place_obj` / `place_agent` / `wall_rect` semantics,
+ *   - `MiniGridEnv.step` reward/done rules, the egocentric 7x7 view with
+ *     wall occlusion (`see_through_walls=False`, base_env.py:39) rendered as
+ *     5 tile classes (RGBImgPartialObsWrapper, scenario_creator.py:48),
+ *   - StuckPenaltyWrapper (src/wrappers/stuck_penalty_wrapper.py:19-57),
+ *   - PPO.compute_gae (src/ppo.py:107-120).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker / CPU baseline -- never as the
+ * product path.  Parity status: the RNG model is pinned against numpy itself;
+ * GAE is pinned against goldens captured from the reference PPO core; the
+ * minigrid-level env semantics are "parity unpinned" (minigrid 3.0.0 is not
+ * installed and the reference's own tests assert nothing) and are
+ * cross-checked against an independent literal Python restatement
+ * (oracle/minigrid_literal.py).
+ */
+#ifndef MERLIN_ORACLE_H
+#define MERLIN_ORACLE_H
+#include <stdint.h>
+
+#define O_MAXS 32
+
+enum { O_EMPTY = 0, O_WALL = 1, O_GOAL = 2 };
+enum { O_EASY = 0, O_MEDIUM = 1, O_MEDIUMHARD = 2, O_HARD = 3, O_HARDEST = 4 };
+/* view tile classes (the only 5 distinct rendered 8x8 tiles) */
+enum { O_T_DARK = 0, O_T_EMPTY = 1, O_T_WALL = 2, O_T_GOAL = 3, O_T_AGENT = 4 };
+
+typedef struct {
+    uint64_t st_hi, st_lo;   /* 128-bit LCG state */
+    uint64_t inc_hi, inc_lo; /* 128-bit increment (odd) */
+    uint32_t has32, buf32;   /* persistent 32-bit half buffer (pcg64_next32) */
+} o_pcg64;
+
+typedef struct {
+    int size, difficulty, max_steps;
+    uint8_t cell[O_MAXS * O_MAXS]; /* minigrid Grid: index y*size + x */
+    int ax, ay, dir, step_count;
+    int gx, gy;
+    o_pcg64 rng;
+    int rng_ready;
+    int fallbacks;     /* number of generator fallbacks to the empty map */
+    int attempts;      /* generator attempts used by the last reset */
+    int error;         /* nonzero: place_obj RecursionError or bad action */
+    /* StuckPenaltyWrapper (unwired in the reference; flag) */
+    int stuck_on, max_stay;
+    double penalty;
+    int last_x, last_y, stay;
+    /* ExplorationBonus (absent in the reference; MERLIN-AMD definition) */
+    int explore_on;
+    double bonus;
+    uint32_t visited[O_MAXS];
+} o_env;
+
+/* ---- RNG ---- */
+void o_seedseq_pcg64(uint64_t seed, o_pcg64 *out);
+uint64_t o_next64(o_pcg64 *r);
+uint32_t o_next32(o_pcg64 *r);
+int64_t o_integers(o_pcg64 *r, int64_t lo, int64_t hi); /* Generator.integers(lo, hi) */
+void o_choice_noreplace(o_pcg64 *r, int64_t pop, int64_t k, int64_t *out_idx);
+
+/* ---- env ---- */
+void o_env_init(o_env *e, int size, int difficulty, int max_steps);
+void o_env_set_stuck(o_env *e, int on, int max_stay, double penalty);
+void o_env_set_explore(o_env *e, int on, double bonus);
+void o_env_reset(o_env *e, int has_seed, uint64_t seed);
+void o_env_step(o_env *e, int64_t action, double *reward, int *terminated, int *truncated);
+void o_env_view_codes(const o_env *e, uint8_t codes[49]);
+int o_is_reachable(const o_env *e, int sx, int sy, int gx, int gy);
+
+/* ---- batched helpers (ctypes-friendly) ---- */
+/* seeds: n envs, env i reset(seed=seeds[i]) once; then `steps` steps with
+ * actions[t*n+i]; auto-reset (unseeded) on done.  Outputs [t][i]. */
+void o_batch_rollout(int n, int size, int difficulty, int max_steps, const uint64_t *seeds,
+                     int steps, const int64_t *actions, int stuck_on, int explore_on,
+                     double explore_bonus,
+                     uint8_t *codes_out /* [(steps+1)][n][49] */,
+                     float *reward_out, uint8_t *term_out, uint8_t *trunc_out,
+                     int32_t *agent_out /* [(steps+1)][n][4]: x,y,dir,step_count */);
+/* grid dump after reset(seed) : cell[size*size]; meta6 = agent x,y,dir, goal x,y, attempts */
+void o_gen_map(int size, int difficulty, uint64_t seed, uint8_t *cells, int32_t *meta6);
+/* expand tile codes to uint8 HWC (56,56,3) using a 5x8x8x3 atlas */
+void o_render(const uint8_t *codes, int n, const uint8_t *atlas, uint8_t *out);
+
+/* GAE, reference op order (src/ppo.py:107-120): single env, length T */
+void o_gae_f32(const float *r, const float *v, const float *d, float last_value, int T,
+               double gamma, double lam, float *adv, float *ret);
+/* [T][N] layout, per-env last values */
+void o_gae_f32_tn(const float *r, const float *v, const float *d, const float *last_value, int T,
+                  int N, double gamma, double lam, float *adv, float *ret);
+
+#endif

@@ -1,0 +1,289 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+Run in the build container (the only place /root/reference exists):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Sources, per fixture:
+  rng_numpy.npz   numpy's own Generator(PCG64(SeedSequence(s))) (the env RNG of
+                  gymnasium seeding.np_random) -- pins the RNG restatements.
+  atlas.npz       oracle/tiles.py (numpy restatement of minigrid render_tile).
+  env_maps.npz    oracle/minigrid_literal.py with numpy's real Generator: maps
+                  after reset(seed) for every generator incl. multi-attempt seeds.
+  env_trace.npz   oracle/minigrid_literal.py rollouts (seeded reset, unseeded
+                  auto-reset), incl. goal hits and truncation.
+  gae_ref.npz     the REFERENCE PPO.compute_gae (src/ppo.py:107-120) and
+                  compute_gae_standard (src/utils/utils_rl.py:11-29), imported
+                  read-only from /root/reference, plus the adv normalisation of
+                  src/ppo.py:125.
+  cnn_ref.npz     the REFERENCE CNNActorCritic (src/actor_critic.py) under
+                  torch.manual_seed: param checksums + act/evaluate outputs.
+  update_ref.npz  one REFERENCE PPO.update (src/ppo.py:122-168) on a small
+                  replay batch, with the randperm draws recorded for replay.
+The reference code itself is never copied into the repo; only its outputs.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import oracle as O  # noqa: E402
+from minigrid_literal import LiteralEnv  # noqa: E402
+from tiles import build_atlas  # noqa: E402
+
+REF = "/root/reference"
+
+
+def gen_rng():
+    seeds = [0, 1, 777, 123456, 2**40 + 5]
+    out = {"seeds": np.array(seeds, dtype=np.uint64)}
+    st = []
+    raw = []
+    ints_lohi = []
+    ints_out = []
+    ch_args = []
+    ch_out = []
+    rs = np.random.RandomState(7)
+    for s in seeds:
+        g = np.random.PCG64(s)
+        S = g.state["state"]
+        st.append([S["state"] >> 64, S["state"] & (2**64 - 1), S["inc"] >> 64, S["inc"] & (2**64 - 1)])
+        raw.append(g.random_raw(64))
+        gen = np.random.default_rng(s)
+        lohi = []
+        vals = []
+        for _ in range(2000):
+            lo = int(rs.randint(0, 40))
+            hi = lo + int(rs.randint(1, 600))
+            lohi.append((lo, hi))
+            vals.append(int(gen.integers(lo, hi)))
+        ints_lohi.append(lohi)
+        ints_out.append(vals)
+        gen = np.random.default_rng(s)
+        args = []
+        outs = np.full((50, 32), -1, dtype=np.int64)
+        for i in range(50):
+            pop = int(rs.randint(1, 32))
+            k = int(rs.randint(1, pop + 1))
+            args.append((pop, k))
+            outs[i, :k] = gen.choice(pop, size=k, replace=False)
+        ch_args.append(args)
+        ch_out.append(outs)
+    out["state_words"] = np.array(st, dtype=np.uint64)
+    out["raw64"] = np.array(raw, dtype=np.uint64)
+    out["int_lohi"] = np.array(ints_lohi, dtype=np.int64)
+    out["int_out"] = np.array(ints_out, dtype=np.int64)
+    out["choice_args"] = np.array(ch_args, dtype=np.int64)
+    out["choice_out"] = np.array(ch_out, dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "rng_numpy.npz"), **out)
+
+
+MAP_CASES = [
+    ("mediumhard", 16, list(range(0, 40)) + [575, 641, 857, 1600, 777, 123456]),
+    ("hard", 16, list(range(0, 12)) + [147, 277]),
+    ("hard", 22, list(range(0, 12)) + [429, 1619]),
+    ("easy", 16, list(range(0, 8))),
+    ("medium", 16, list(range(0, 8))),
+    ("hardest", 16, list(range(0, 8)) + [4, 39]),
+]
+
+
+def gen_maps():
+    recs = {}
+    for diff, size, seeds in MAP_CASES:
+        cells = []
+        meta = []
+        for s in seeds:
+            L = LiteralEnv(size, diff)
+            codes = L.reset(s)
+            cells.append(L.cells())
+            meta.append([L.agent_pos[0], L.agent_pos[1], L.agent_dir, L.goal_pos[0], L.goal_pos[1]])
+        key = f"{diff}_{size}"
+        recs[key + "_seeds"] = np.array(seeds, dtype=np.uint64)
+        recs[key + "_cells"] = np.array(cells, dtype=np.uint8)
+        recs[key + "_meta"] = np.array(meta, dtype=np.int32)
+    np.savez_compressed(os.path.join(HERE, "env_maps.npz"), **recs)
+
+
+TRACE_CASES = [
+    # (difficulty, size, n_envs, T, max_steps, seed_base, p_forward)
+    ("mediumhard", 16, 8, 400, 100, 777, 0.6),
+    ("hard", 22, 4, 300, 0, 4000, 0.6),
+    ("easy", 16, 4, 300, 64, 55, 0.7),
+]
+
+
+def gen_traces():
+    recs = {}
+    rs = np.random.RandomState(11)
+    for diff, size, n, T, max_steps, base, pf in TRACE_CASES:
+        seeds = np.arange(base, base + n, dtype=np.uint64)
+        p = [(1 - pf) / 2, (1 - pf) / 2, pf]
+        acts = rs.choice([0, 1, 2], size=(T, n), p=p).astype(np.int64)
+        codes = np.zeros((T + 1, n, 49), np.uint8)
+        rew = np.zeros((T, n), np.float32)
+        term = np.zeros((T, n), np.uint8)
+        trunc = np.zeros((T, n), np.uint8)
+        agent = np.zeros((T + 1, n, 4), np.int32)
+        for i in range(n):
+            L = LiteralEnv(size, diff, max_steps=(max_steps or None))
+            c = L.reset(int(seeds[i]))
+            codes[0, i] = c.reshape(-1)
+            agent[0, i] = (L.agent_pos[0], L.agent_pos[1], L.agent_dir, L.step_count)
+            for t in range(T):
+                c, r, te, tr = L.step(int(acts[t, i]))
+                rew[t, i], term[t, i], trunc[t, i] = np.float32(r), te, tr
+                if te or tr:
+                    c = L.reset()
+                codes[t + 1, i] = c.reshape(-1)
+                agent[t + 1, i] = (L.agent_pos[0], L.agent_pos[1], L.agent_dir, L.step_count)
+        key = f"{diff}_{size}"
+        recs[key + "_cfg"] = np.array([n, T, max_steps, base], dtype=np.int64)
+        recs[key + "_actions"] = acts
+        recs[key + "_codes"] = codes
+        recs[key + "_reward"] = rew
+        recs[key + "_term"] = term
+        recs[key + "_trunc"] = trunc
+        recs[key + "_agent"] = agent
+        print(f"trace {key}: terms={int(term.sum())} truncs={int(trunc.sum())}")
+    np.savez_compressed(os.path.join(HERE, "env_trace.npz"), **recs)
+
+
+def _import_reference():
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from src.actor_critic import CNNActorCritic
+    from src.ppo import PPO
+    from src.utils.utils_rl import compute_gae_standard
+
+    return PPO, CNNActorCritic, compute_gae_standard
+
+
+def gen_gae():
+    import torch
+
+    PPO, _, gae_std = _import_reference()
+    rs = np.random.RandomState(3)
+    recs = {}
+    for k, (T, p_done) in enumerate([(256, 0.02), (2048, 0.004), (64, 0.3)]):
+        r = (rs.rand(T) < 0.05).astype(np.float32) * rs.rand(T).astype(np.float32)
+        r -= (rs.rand(T) < 0.1).astype(np.float32) * np.float32(0.1)
+        v = rs.randn(T).astype(np.float32)
+        d = (rs.rand(T) < p_done).astype(np.float32)
+        d[T // 2] = 1.0
+        last = float(np.float32(rs.randn()))
+        self_ = types.SimpleNamespace(gamma=0.99, lam=0.95)
+        adv, ret = PPO.compute_gae(self_, torch.from_numpy(r), torch.from_numpy(v), torch.from_numpy(d), last)
+        adv_n = (adv - adv.mean()) / (adv.std() + 1e-8)
+        a_std, r_std = gae_std(r, v, d, last, gamma=0.995, lam=0.95)
+        recs[f"c{k}_r"], recs[f"c{k}_v"], recs[f"c{k}_d"] = r, v, d
+        recs[f"c{k}_last"] = np.float32(last)
+        recs[f"c{k}_adv"] = adv.numpy()
+        recs[f"c{k}_ret"] = ret.numpy()
+        recs[f"c{k}_advnorm"] = adv_n.numpy()
+        recs[f"c{k}_adv995"] = a_std.astype(np.float32)
+        recs[f"c{k}_ret995"] = np.asarray(r_std, dtype=np.float32)
+    recs["ncases"] = np.int64(3)
+    np.savez_compressed(os.path.join(HERE, "gae_ref.npz"), **recs)
+
+
+def _param_checksums(model):
+    keys = []
+    sums = []
+    for name, p in model.state_dict().items():
+        keys.append(name)
+        t = p.detach().double()
+        sums.append([t.sum().item(), t.abs().sum().item(), float(t.reshape(-1)[0].item())])
+    return np.array(keys), np.array(sums, dtype=np.float64)
+
+
+def gen_cnn():
+    import torch
+
+    _, CNNActorCritic, _ = _import_reference()
+    atlas = build_atlas()
+    rs = np.random.RandomState(5)
+    codes = rs.randint(0, 4, size=(16, 49)).astype(np.uint8)
+    codes[:, 45] = 4  # agent tile at view (3, 6)
+    imgs = O.render(codes, atlas)
+    torch.manual_seed(0)
+    ac = CNNActorCritic((56, 56, 3), 3)
+    keys, sums = _param_checksums(ac)
+    obs = torch.from_numpy(imgs.astype(np.float32))
+    acts = torch.from_numpy(rs.randint(0, 3, size=16).astype(np.int64))
+    with torch.no_grad():
+        a_det, lp_det, v_det = ac.act(obs, deterministic=True)
+        lp_ev, ent_ev, v_ev = ac.evaluate(obs, acts)
+        logits = ac.actor(ac.actor_extractor(obs.permute(0, 3, 1, 2)))
+    np.savez_compressed(
+        os.path.join(HERE, "cnn_ref.npz"),
+        seed=np.int64(0), codes=codes, keys=keys, sums=sums, actions=acts.numpy(),
+        act_action=a_det.numpy(), act_logp=lp_det.numpy(), act_value=v_det.numpy(),
+        ev_logp=lp_ev.numpy(), ev_entropy=ent_ev.numpy(), ev_value=v_ev.numpy(),
+        logits=logits.numpy(),
+    )
+
+
+def gen_update():
+    import torch
+
+    PPO, _, _ = _import_reference()
+    atlas = build_atlas()
+    B, MB, EPOCHS = 64, 16, 2
+    rs = np.random.RandomState(9)
+    codes = rs.randint(0, 4, size=(B, 49)).astype(np.uint8)
+    codes[:, 45] = 4
+    imgs = O.render(codes, atlas)
+
+    class _StubEnv:  # the reference PPO accepts any gym-like env; only reset/action_space are used
+        action_space = types.SimpleNamespace(n=3)
+
+        def reset(self, seed=None):
+            return imgs[0].copy(), {}
+
+    torch.manual_seed(0)
+    agent = PPO(_StubEnv(), lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=EPOCHS,
+                batch_size=B, minibatch_size=MB, vf_coef=0.5, ent_coef=0.05, device="cpu")
+    keys, sums0 = _param_checksums(agent.ac)
+    actions = rs.randint(0, 3, size=B).astype(np.int64)
+    with torch.no_grad():
+        lp, _, v = agent.ac.evaluate(torch.from_numpy(imgs.astype(np.float32)), torch.from_numpy(actions))
+    rewards = ((rs.rand(B) < 0.1) * rs.rand(B)).astype(np.float32)
+    dones = (rs.rand(B) < 0.05).astype(np.float32)
+    for t in range(B):
+        agent.buffer.add(torch.from_numpy(imgs[t].astype(np.float32)), torch.tensor(actions[t]), lp[t], v[t],
+                         torch.tensor(rewards[t]), torch.tensor(dones[t]))
+    last_value = float(v[0].item())
+    torch.manual_seed(1234)
+    perms = np.stack([torch.randperm(B).numpy() for _ in range(EPOCHS)])
+    torch.manual_seed(1234)
+    stats = agent.update(last_value)
+    keys1, sums1 = _param_checksums(agent.ac)
+    assert (keys1 == keys).all()
+    np.savez_compressed(
+        os.path.join(HERE, "update_ref.npz"),
+        cfg=np.array([B, MB, EPOCHS], dtype=np.int64), codes=codes, actions=actions,
+        logp=lp.numpy(), values=v.numpy(), rewards=rewards, dones=dones,
+        last_value=np.float32(last_value), perms=perms, keys=keys, sums0=sums0, sums1=sums1,
+        stat_names=np.array(sorted(stats)), stat_vals=np.array([stats[k] for k in sorted(stats)]),
+        hparams=np.array([3e-4, 0.99, 0.95, 0.2, 0.5, 0.05]),
+    )
+
+
+if __name__ == "__main__":
+    np.savez_compressed(os.path.join(HERE, "atlas.npz"), atlas=build_atlas())
+    gen_rng()
+    gen_maps()
+    gen_traces()
+    gen_gae()
+    gen_cnn()
+    gen_update()
+    print("golden fixtures written to", HERE)
