@@ -1,0 +1,247 @@
+#!/usr/bin/env python
+"""bench.py -- BASELINE.json metric: env-steps/sec (rollout + GAE + PPO update),
+4096 envs per GPU, 16x16 mediumhard (configs[1]; configs[2] when launched on 8 ranks).
+
+One "step" = one PPO iteration of the reference loop (src/ppo.py:64-168) over the
+vectorised envs: reset all envs, T=256 env steps x N envs of act -> env-step (HIP),
+GAE + whole-batch advantage normalisation (HIP), then 10 epochs x 8 minibatches of
+N*T/8 with clip_grad_norm_(0.5) + Adam (PyTorch-ROCm fp32, the reference's precision).
+ppo_train.py defaults otherwise (lr 3e-4, gamma .99, lam .95, clip .2, vf .5, ent .05).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank r owns envs [r*N, (r+1)*N) seeded 777 + global index (weak scaling); the update
+all-reduces the f32 gradient once per optimizer step and the advantage moments once
+per iteration over RCCL.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ppo-2dgrid_amd"))
+# MIOpen: heuristic ("immediate") solver choice instead of a per-shape Find that compiles and
+# times every candidate kernel (minutes per new batch shape on a fresh box).  Startup-only
+# setting; the convolutions computed are the same fp32 convolutions.
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+os.environ.setdefault("MIOPEN_LOG_LEVEL", "3")
+
+# Algorithmic work per unit:
+#   k_env_step, per env-step: action 8 + agent state r/w 32 + wall rows 64 + episode
+#   accumulators r/w 24 + obs codes 32 + reward 4 + done 4  = 168 B
+ENV_STEP_BYTES = 168
+#   full iteration, per env-step: rollout forward of both towers 9.94 MFLOP
+#   + 10 epochs x fwd+bwd 25.67 MFLOP (conv1 needs no input gradient)
+FWD_MACS = 2 * (1_038_336 + 819_200 + 331_776 + 294_912) + 512 * 3 + 512
+BWD_MACS = 2 * FWD_MACS - 2 * 1_038_336
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (vector == f32 MFMA rate)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--k-steps", type=int, default=256)
+    ap.add_argument("--epochs", type=int, default=10)
+    ap.add_argument("--minibatches", type=int, default=8)
+    ap.add_argument("--difficulty", default="mediumhard")
+    ap.add_argument("--size", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-tiers", action="store_true")
+    return ap.parse_args()
+
+
+def env_only_tier(torch, MerlinVecEnv, n, T, difficulty, size, device):
+    """Tier E: env dynamics + obs codes only, actions pre-generated.
+    (a) one launch steps all T steps with state on chip; (b) T single-step launches."""
+    env = MerlinVecEnv(n, difficulty=difficulty, size=size, seed=4242, device=device)
+    env.reset()
+    g = torch.Generator(device=device)
+    g.manual_seed(7)
+    acts = torch.randint(0, 3, (T, n), device=device, generator=g)
+    obs = torch.empty((T, n, 8), dtype=torch.int32, device=device)
+    rew = torch.empty((T, n), dtype=torch.float32, device=device)
+    done = torch.empty((T, n), dtype=torch.float32, device=device)
+    for _ in range(2):
+        env.step_into(acts, obs, rew, None, None, done, n_steps=T, action_stride=n)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        env.step_into(acts, obs, rew, None, None, done, n_steps=T, action_stride=n)
+    e1.record()
+    torch.cuda.synchronize()
+    fused = reps * T * n / (e0.elapsed_time(e1) / 1e3)
+    e0.record()
+    for t in range(T):
+        env.step_into(acts[t], obs[t], rew[t], None, None, done[t])
+    e1.record()
+    torch.cuda.synchronize()
+    single = T * n / (e0.elapsed_time(e1) / 1e3)
+    env.errors()
+    env.close()
+    return fused, single
+
+
+def cpu_baseline():
+    """The oracle's CPU port of the reference loop (oracle/ppo_cpu.py), N=1 env,
+    batch 2048, 10 epochs x 8 minibatches of 256: one iteration (~5 s on 8 cores)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import torch
+
+    import ppo_cpu  # noqa: E402  (baseline leg only)
+
+    steps, secs = ppo_cpu.run_iterations(n_iter=1)
+    return {"value": round(steps / secs, 2), "unit": "env-steps/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": "1 PPO iteration of the reference loop on CPU: 1 mediumhard 16x16 env (C oracle + RGB "
+                      "render), batch 2048, 10 epochs x 8 minibatches of 256, fp32 torch CNN (cfg 1 shape)"}
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of k_env_step from the committed rocprofv3 --pmc pass
+    (profiles/*env_step_pmc*.json, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*env_step_pmc*.json")))
+    if not files:
+        return None
+    try:
+        return json.load(open(files[-1])).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def heartbeat(state):
+    import threading
+
+    def run():
+        t0 = time.time()
+        while True:
+            time.sleep(45)
+            print(f"[bench] alive {time.time() - t0:.0f}s phase={state.get('phase')}", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
+def main():
+    args = parse()
+    state = {"phase": "init"}
+    heartbeat(state)
+    import torch
+    import torch.distributed as dist
+
+    from merlin import MerlinVecEnv
+    from merlin.distributed import DataParallel
+    from merlin.ppo import PPO
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dp = DataParallel.init_from_env("nccl" if world > 1 else None, device)
+
+    N, T = args.num_envs, args.k_steps
+    B = N * T
+    env = MerlinVecEnv(N, difficulty=args.difficulty, size=args.size, seed=777, device=device,
+                       env_offset=rank * N)
+    torch.manual_seed(777)
+    agent = PPO(env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=args.epochs, batch_size=B,
+                minibatch_size=B // args.minibatches, vf_coef=0.5, ent_coef=0.05, device=device, dp=dp)
+
+    state["phase"] = "warmup"
+    for _ in range(args.warmup):
+        agent.update(agent.collect_rollouts())
+    torch.cuda.synchronize()
+    if dp.enabled:
+        dist.barrier()
+
+    state["phase"] = "timed"
+    agent.env_step_events = []
+    ph = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        lv = agent.collect_rollouts()
+        e1.record()
+        agent.update(lv)
+        e2.record()
+        ph.append((e0, e1, e2))
+    torch.cuda.synchronize()
+    if dp.enabled:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dp.enabled:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ev = agent.env_step_events
+    agent.env_step_events = None
+    step_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    rollout_ms = sum(a.elapsed_time(b) for a, b, _ in ph) / len(ph)
+    update_ms = sum(b.elapsed_time(c) for _, b, c in ph) / len(ph)
+    value = args.steps * B * world / elapsed
+
+    if rank != 0:
+        if dp.enabled:
+            dist.barrier()
+        return
+    achieved = ENV_STEP_BYTES * N / (step_ms / 1e3) / 1e9
+    traffic = pmc_traffic()
+    flop_per_step = 2 * FWD_MACS + args.epochs * 2 * (FWD_MACS + BWD_MACS)
+    loop_tflops = value / world * flop_per_step / 1e12
+    out = {
+        "metric": "env-steps/sec (rollout+GAE+PPO update), 4096 envs, 16x16 mediumhard",
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: procedurally generated mediumhard maps (numpy-PCG64-exact, seeds 777+i), "
+                "random-init CNNActorCritic",
+        "config": {"workload": f"{args.difficulty} {args.size}x{args.size}, {N} envs/GPU x k_steps {T}, "
+                               f"{args.epochs} epochs x {args.minibatches} minibatches of {B // args.minibatches}",
+                   "num_envs_per_gpu": N, "k_steps": T, "global_batch": B * world,
+                   "parallelism": f"dp{world}" if world > 1 else "single"},
+        "roofline": {"kernel": "k_env_step", "bound": "hbm", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": traffic, "bytes_per_env_step": ENV_STEP_BYTES, "envs_per_launch": N,
+                     "avg_launch_us": round(step_ms * 1e3, 2)},
+        "roofline_loop": {"bound": "mfma", "achieved": round(loop_tflops, 2), "peak": FP32_PEAK_TFLOPS,
+                          "unit": "TFLOP/s", "frac": round(loop_tflops / FP32_PEAK_TFLOPS, 4),
+                          "flop_per_env_step": flop_per_step},
+        "phases_ms": {"rollout": round(rollout_ms, 2), "update": round(update_ms, 2)},
+    }
+    state["phase"] = "tiers"
+    if not args.no_tiers:
+        fused, single = env_only_tier(torch, MerlinVecEnv, N, T, args.difficulty, args.size, device)
+        out["tiers"] = {"env_only_fused_T_steps_per_launch": round(fused, 1),
+                        "env_only_one_step_per_launch": round(single, 1),
+                        "rollout_only": round(B / (rollout_ms / 1e3), 1),
+                        "full_loop_per_gpu": round(value / world, 1)}
+    state["phase"] = "cpu_baseline"
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    print(json.dumps(out), flush=True)
+    if dp.enabled:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

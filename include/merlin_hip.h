@@ -1,0 +1,162 @@
+/*
+ * merlin_hip.h -- C ABI of libmerlin_hip.so, the MI355X (gfx950) hot path of
+ * PPO-2DGrid ("MERLIN"): batched MiniGrid step/reset dynamics, the occluded
+ * 7x7 egocentric observation, reward/done rules, the RGB tile expansion, and
+ * GAE(lambda) + advantage normalisation.
+ *
+ * Conventions
+ *   - Plain C types only; every device pointer is caller-allocated (e.g. a
+ *     torch tensor's data_ptr()) and every call is stream-ordered on `stream`
+ *     (a hipStream_t passed as void*; NULL = the null stream).  Calls marked
+ *     [sync] synchronise that stream.
+ *   - The env context owns only per-env state (grid bitmasks, agent, RNG,
+ *     episode accumulators) in device memory.
+ *   - Every entry point returns 0 (MERLIN_OK) or a MERLIN_E* code; nothing
+ *     throws across the ABI.  merlin_last_error() gives a thread-local message.
+ *   - Not re-entrant per context; one host thread per device.
+ *
+ * Reference interfaces replaced (paths relative to the reference checkout):
+ *   merlin_env_create    gym.make(env_id, size=..) + wrapper chain
+ *                        src/scenario_creator/scenario_creator.py:35-57,
+ *                        BaseCustomEnv.__init__ src/custom_envs/base_env.py:15-41
+ *   merlin_env_seed      gymnasium Env.reset(seed=s) -> seeding.np_random(s)
+ *                        (ppo/ppo_train.py:48 `env.reset(seed=base_seed + ep)`)
+ *   merlin_env_reset     env.reset() src/ppo.py:35,65,96 -> MiniGridEnv.reset ->
+ *                        <Difficulty>Env._gen_grid (medium_hard_env.py:12-45,
+ *                        hard_env.py:11-73, easy/medium/hardest_env.py)
+ *   merlin_env_step      env.step(action.item()) src/ppo.py:76 ->
+ *                        ThreeActionWrapper.action (three_action_wrapper.py:16-17)
+ *                        -> MiniGridEnv.step [+ StuckPenaltyWrapper.step
+ *                        stuck_penalty_wrapper.py:29-57]; done = term or trunc
+ *                        (src/ppo.py:77); auto-reset on done (src/ppo.py:93-98)
+ *   obs codes            RGBImgPartialObsWrapper.observation -> get_pov_render
+ *                        (gen_obs_grid + process_vis), selected at
+ *                        scenario_creator.py:48
+ *   merlin_obs_expand_*  Grid.render tile blit + ImgObsWrapper
+ *                        (scenario_creator.py:50), PPO._obs_to_tensor
+ *                        src/ppo.py:58-62, CNNActorCritic._format_obs
+ *                        src/actor_critic.py:43-46 and the /255 of
+ *                        CNNFeatureExtractor.forward src/actor_critic.py:20-21
+ *   merlin_gae           PPO.compute_gae src/ppo.py:107-120
+ *                        (== compute_gae_standard src/utils/utils_rl.py:11-29)
+ *   merlin_adv_normalize (adv - adv.mean()) / (adv.std() + 1e-8) src/ppo.py:125
+ */
+#ifndef MERLIN_HIP_H
+#define MERLIN_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MERLIN_ABI_VERSION 1
+
+#define MERLIN_OK 0
+#define MERLIN_E_INVALID 1     /* bad argument / config */
+#define MERLIN_E_HIP 2         /* a HIP runtime call failed */
+#define MERLIN_E_DEVICE 3      /* device-side error flag raised (see merlin_env_errors) */
+#define MERLIN_E_UNSUPPORTED 4 /* e.g. grid size > 32 */
+
+/* difficulty ids (ScenarioCreator difficulties, src/config/scenario.yaml) */
+#define MERLIN_EASY 0
+#define MERLIN_MEDIUM 1
+#define MERLIN_MEDIUMHARD 2
+#define MERLIN_HARD 3
+#define MERLIN_HARDEST 4
+
+/* device error bits reported by merlin_env_errors */
+#define MERLIN_DEVERR_BAD_ACTION 1u  /* action not in {0,1,2}: ThreeActionWrapper IndexError */
+#define MERLIN_DEVERR_PLACE_OBJ 2u   /* place_obj max_tries exceeded: RecursionError */
+
+/* observation layouts for merlin_obs_expand_f32 */
+#define MERLIN_LAYOUT_NCHW 0 /* [n][3][56][56]: what CNNActorCritic._format_obs hands the convs */
+#define MERLIN_LAYOUT_NHWC 1 /* [n][56][56][3]: the RolloutBuffer / gym observation layout */
+
+/* Observation codes: one 7x7 view per env = 49 tile classes (0 dark-empty,
+ * 1 lit empty, 2 lit wall, 3 lit goal, 4 agent), 4 bits each, cell (vi,vj)
+ * at nibble vj*7+vi, packed into MERLIN_OBS_WORDS uint32 words (32 B). */
+#define MERLIN_OBS_WORDS 8
+#define MERLIN_OBS_TILES 5
+#define MERLIN_TILE_PX 8
+#define MERLIN_VIEW 7
+
+typedef struct merlin_env merlin_env;
+
+typedef struct {
+    int32_t num_envs;          /* envs in this context (this rank's shard) */
+    int32_t size;              /* grid side, 5..32 (reference: 16, base_env.py:17) */
+    int32_t difficulty;        /* MERLIN_* difficulty id */
+    int32_t max_steps;         /* <= 0: 4*size^2 (base_env.py:32-33) */
+    int32_t stuck_penalty;     /* 1: StuckPenaltyWrapper semantics (off in the reference chain) */
+    int32_t max_stay;          /* StuckPenaltyWrapper.max_stay (default 3) */
+    double penalty;            /* StuckPenaltyWrapper.penalty (default -0.1) */
+    int32_t exploration_bonus; /* 1: +bonus on the first visit of a cell per episode */
+    double bonus;
+} merlin_env_config;
+
+/* Library */
+int merlin_version(void);
+const char *merlin_last_error(void);
+/* [host] the 5 tiles (uint8[5][8][8][3]) the library renders with, computed at
+ * load time by the library's own restatement of minigrid's render_tile. */
+int merlin_tile_atlas(uint8_t *out_host);
+
+/* Env context */
+int merlin_env_create(const merlin_env_config *cfg, merlin_env **out);
+int merlin_env_destroy(merlin_env *env);
+/* Seed env i with seeds_host[i] (numpy SeedSequence -> PCG64, as gymnasium
+ * reset(seed=...)); takes effect at the next merlin_env_reset of that env. */
+int merlin_env_seed(merlin_env *env, const uint64_t *seeds_host, int32_t n, void *stream);
+/* Reset the envs whose mask_dev[i] != 0 (mask_dev NULL = all), writing their
+ * observation codes to obs_dev[i][8]; others' obs rows are left untouched. */
+int merlin_env_reset(merlin_env *env, const uint8_t *mask_dev, uint32_t *obs_dev, void *stream);
+/* Advance all envs n_steps times.  Step t reads actions_dev[t*action_stride + i]
+ * (int64, values 0 left / 1 right / 2 forward) and writes, at row t*num_envs+i:
+ *   obs_dev[..][8]  observation after the step (after the auto-reset if done),
+ *   reward_dev f32, terminated_dev u8, truncated_dev u8, done_dev f32 (term|trunc),
+ *   ep_return_dev f64 / ep_length_dev i32 (the finished episode's totals; valid
+ *   where done).  Any output pointer may be NULL.  autoreset=0 leaves a done env
+ *   in its terminal state (gym semantics: the caller must reset it). */
+int merlin_env_step(merlin_env *env, const int64_t *actions_dev, int32_t n_steps,
+                    int64_t action_stride, uint32_t *obs_dev, float *reward_dev,
+                    uint8_t *terminated_dev, uint8_t *truncated_dev, float *done_dev,
+                    double *ep_return_dev, int32_t *ep_length_dev, int32_t autoreset,
+                    void *stream);
+/* [sync] copy env state to host: walls uint32[N][size] (bit x of row y = wall at
+ * (x,y)); agent int32[N][8] = (x, y, dir, step_count, goal_x, goal_y, stay, 0);
+ * rng uint64[N][5] = (state_hi, state_lo, inc_hi, inc_lo, has32<<32|buf32).
+ * Any pointer may be NULL. */
+int merlin_env_get_state(merlin_env *env, uint32_t *walls_host, int32_t *agent_host,
+                         uint64_t *rng_host, void *stream);
+/* [sync] read-and-clear the device error bits and the fallback-map counter. */
+int merlin_env_errors(merlin_env *env, uint32_t *flags_host, uint32_t *fallbacks_host,
+                      void *stream);
+int merlin_env_num_envs(const merlin_env *env);
+int merlin_env_size(const merlin_env *env);
+
+/* Observation expansion: out[k] = RGB image of codes_dev[index_dev ? index_dev[k] : k],
+ * k < n.  f32: values are tile bytes * scale (scale = 1/255 folds
+ * CNNFeatureExtractor's /255), layout MERLIN_LAYOUT_*.  u8: NHWC bytes, exactly
+ * the RGBImgPartialObsWrapper(tile_size=8) frame. */
+int merlin_obs_expand_f32(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
+                          float *out_dev, float scale, int32_t layout, void *stream);
+int merlin_obs_expand_u8(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
+                         uint8_t *out_dev, void *stream);
+
+/* GAE over [T][N] (row t, env i at t*N+i), truncation treated as terminal
+ * (done = term or trunc).  stats_dev (nullable) receives double[3] =
+ * (count, sum adv, sum adv^2) of this call's advantages -- the per-rank
+ * partial that multi-GPU callers all-reduce before merlin_adv_normalize. */
+int merlin_gae(const float *reward_dev, const float *value_dev, const float *done_dev,
+               const float *last_value_dev, float *adv_dev, float *ret_dev, int32_t T, int32_t N,
+               double gamma, double lam, double *stats_dev, void *stream);
+/* out[k] = (adv[k] - mean) / (std_unbiased + 1e-8) with mean/std from
+ * stats_dev = (count, sum, sum of squares); out may alias adv. */
+int merlin_adv_normalize(const float *adv_dev, int64_t n, const double *stats_dev, float *out_dev,
+                         void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

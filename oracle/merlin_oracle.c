@@ -630,3 +630,26 @@ void o_gae_f32_tn(const float *r, const float *v, const float *d, const float *l
         }
     }
 }
+
+/* ------------------------------------------------------------------------ */
+#include <stdlib.h>
+
+o_env *o_env_new(int size, int difficulty, int max_steps) {
+    o_env *e = (o_env *)malloc(sizeof(o_env));
+    o_env_init(e, size, difficulty, max_steps);
+    return e;
+}
+
+void o_env_free(o_env *e) { free(e); }
+
+void o_env_reset_codes(o_env *e, int has_seed, uint64_t seed, uint8_t codes[49]) {
+    o_env_reset(e, has_seed, seed);
+    o_env_view_codes(e, codes);
+}
+
+double o_env_step_codes(o_env *e, int64_t action, uint8_t codes[49], int *terminated, int *truncated) {
+    double r;
+    o_env_step(e, action, &r, terminated, truncated);
+    o_env_view_codes(e, codes);
+    return r;
+}

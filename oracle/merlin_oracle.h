@@ -95,4 +95,15 @@ void o_gae_f32(const float *r, const float *v, const float *d, float last_value,
 void o_gae_f32_tn(const float *r, const float *v, const float *d, const float *last_value, int T,
                   int N, double gamma, double lam, float *adv, float *ret);
 
+/* ---- single-env handle API (bench.py cpu_baseline / tests) ---- */
+#ifndef MERLIN_ORACLE_HANDLE_API
+#define MERLIN_ORACLE_HANDLE_API
+o_env *o_env_new(int size, int difficulty, int max_steps);
+void o_env_free(o_env *e);
+/* reset (seeded if has_seed) and write the 49 view codes */
+void o_env_reset_codes(o_env *e, int has_seed, uint64_t seed, uint8_t codes[49]);
+/* step and write the next view codes; returns reward (f64) */
+double o_env_step_codes(o_env *e, int64_t action, uint8_t codes[49], int *terminated, int *truncated);
+#endif
+
 #endif

@@ -1,0 +1,466 @@
+// merlin_capi.hip -- host side of libmerlin_hip.so: the extern "C" ABI declared
+// in include/merlin_hip.h, env-context lifetime, numpy SeedSequence seeding and
+// the library's own restatement of minigrid's tile renderer (the atlas).
+#include <math.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "merlin_internal.h"
+
+struct merlin_env {
+    merlin::EnvDev dev;
+    int device;
+    bool has_state;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(MERLIN_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                  \
+    do {                                               \
+        hipError_t _e = (expr);                        \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// numpy SeedSequence(seed).generate_state(4, uint64) -> PCG64 seeding
+// (numpy/random/bit_generator.pyx mix_entropy / generate_state,
+//  numpy/random/_pcg64.pyx -> pcg64_set_seed -> pcg_setseq_128_srandom_r).
+struct U128 {
+    uint64_t hi, lo;
+};
+
+U128 mul128(U128 a, U128 b) {
+    const unsigned __int128 x = ((unsigned __int128)a.hi << 64) | a.lo;
+    const unsigned __int128 y = ((unsigned __int128)b.hi << 64) | b.lo;
+    const unsigned __int128 z = x * y;
+    return {(uint64_t)(z >> 64), (uint64_t)z};
+}
+
+U128 add128(U128 a, U128 b) {
+    const unsigned __int128 x = ((unsigned __int128)a.hi << 64) | a.lo;
+    const unsigned __int128 y = ((unsigned __int128)b.hi << 64) | b.lo;
+    const unsigned __int128 z = x + y;
+    return {(uint64_t)(z >> 64), (uint64_t)z};
+}
+
+void seed_pcg64(uint64_t seed, U128 &state, U128 &inc) {
+    uint32_t ent[2];
+    int n = 0;
+    if (seed == 0) ent[n++] = 0;
+    for (uint64_t s = seed; s; s >>= 32) ent[n++] = (uint32_t)s;
+    uint32_t pool[4];
+    uint32_t hc = 0x43b0d7e5u;
+    auto hashmix = [&hc](uint32_t v) {
+        v ^= hc;
+        hc *= 0x931e8875u;
+        v *= hc;
+        v ^= v >> 16;
+        return v;
+    };
+    auto mix = [](uint32_t x, uint32_t y) {
+        uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;
+        return r ^ (r >> 16);
+    };
+    for (int i = 0; i < 4; i++) pool[i] = hashmix(i < n ? ent[i] : 0u);
+    for (int s = 0; s < 4; s++)
+        for (int d = 0; d < 4; d++)
+            if (s != d) pool[d] = mix(pool[d], hashmix(pool[s]));
+    uint32_t w[8];
+    uint32_t hb = 0x8b51f9ddu;
+    for (int i = 0; i < 8; i++) {
+        uint32_t v = pool[i & 3] ^ hb;
+        hb *= 0x58f38dedu;
+        v *= hb;
+        w[i] = v ^ (v >> 16);
+    }
+    const uint64_t v0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), v1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+    const uint64_t v2 = (uint64_t)w[4] | ((uint64_t)w[5] << 32), v3 = (uint64_t)w[6] | ((uint64_t)w[7] << 32);
+    const U128 initstate{v0, v1}, initseq{v2, v3};
+    inc = {(initseq.hi << 1) | (initseq.lo >> 63), (initseq.lo << 1) | 1u};
+    const U128 mult{0x2360ed051fc65da4ULL, 0x4385df649fccf645ULL};
+    state = inc;  // step from state 0: 0 * mult + inc
+    state = add128(state, initstate);
+    state = add128(mul128(state, mult), inc);
+}
+
+// ---------------------------------------------------------------------------
+// minigrid 3.0.0 Grid.render_tile(obj, agent_dir, highlight, tile_size=8, subdivs=3)
+// with minigrid.utils.rendering fill_coords / point_in_rect / point_in_triangle /
+// rotate_fn / highlight_img / downsample, keeping numpy's dtypes: float32
+// triangle vertices and their dot products, float64 sample points, uint8
+// canvas, float64 means, truncating cast into the uint8 frame.
+struct Tri {
+    float ax, ay, v0x, v0y, v1x, v1y, dot00, dot01, dot11, inv;
+    Tri() {
+        const float a[2] = {0.12f, 0.19f}, b[2] = {0.87f, 0.50f}, c[2] = {0.12f, 0.81f};
+        ax = a[0];
+        ay = a[1];
+        v0x = c[0] - a[0];
+        v0y = c[1] - a[1];
+        v1x = b[0] - a[0];
+        v1y = b[1] - a[1];
+        dot00 = v0x * v0x + v0y * v0y;
+        dot01 = v0x * v1x + v0y * v1y;
+        dot11 = v1x * v1x + v1y * v1y;
+        const float den = dot00 * dot11 - dot01 * dot01;
+        inv = 1.0f / den;
+    }
+    bool in(double x, double y) const {
+        const double v2x = x - (double)ax, v2y = y - (double)ay;
+        const double dot02 = (double)v0x * v2x + (double)v0y * v2y;
+        const double dot12 = (double)v1x * v2x + (double)v1y * v2y;
+        const double u = ((double)dot11 * dot02 - (double)dot01 * dot12) * (double)inv;
+        const double v = ((double)dot00 * dot12 - (double)dot01 * dot02) * (double)inv;
+        return (u >= 0) && (v >= 0) && (u + v) < 1;
+    }
+};
+
+void render_tile(int obj /*0 none 1 wall 2 goal*/, bool agent, bool highlight, uint8_t out[8][8][3]) {
+    static uint8_t img[24][24][3];
+    memset(img, 0, sizeof(img));
+    auto fill_rect = [](double xmin, double xmax, double ymin, double ymax, const uint8_t col[3]) {
+        for (int y = 0; y < 24; y++)
+            for (int x = 0; x < 24; x++) {
+                const double yf = (y + 0.5) / 24, xf = (x + 0.5) / 24;
+                if (xf >= xmin && xf <= xmax && yf >= ymin && yf <= ymax) memcpy(img[y][x], col, 3);
+            }
+    };
+    const uint8_t grey[3] = {100, 100, 100}, green[3] = {0, 255, 0}, red[3] = {255, 0, 0};
+    fill_rect(0, 0.031, 0, 1, grey);
+    fill_rect(0, 1, 0, 0.031, grey);
+    if (obj == 1) fill_rect(0, 1, 0, 1, grey);
+    if (obj == 2) fill_rect(0, 1, 0, 1, green);
+    if (agent) {
+        const Tri tri;
+        const double theta = 0.5 * M_PI * 3;  // agent_dir = 3 in get_pov_render
+        const double c = cos(-theta), s = sin(-theta);
+        for (int y = 0; y < 24; y++)
+            for (int x = 0; x < 24; x++) {
+                const double yf = (y + 0.5) / 24, xf = (x + 0.5) / 24;
+                const double px = xf - 0.5, py = yf - 0.5;
+                const double x2 = (0.5 + px * c) - py * s;
+                const double y2 = (0.5 + py * c) + px * s;
+                if (tri.in(x2, y2)) memcpy(img[y][x], red, 3);
+            }
+    }
+    if (highlight)
+        for (int y = 0; y < 24; y++)
+            for (int x = 0; x < 24; x++)
+                for (int k = 0; k < 3; k++) {
+                    const uint8_t p = img[y][x][k];
+                    double v = (double)p + 0.30 * (double)(uint8_t)(255 - p);
+                    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+                    img[y][x][k] = (uint8_t)v;
+                }
+    for (int Y = 0; Y < 8; Y++)
+        for (int X = 0; X < 8; X++)
+            for (int k = 0; k < 3; k++) {
+                double m[3];
+                for (int sy = 0; sy < 3; sy++) {
+                    const uint8_t *r0 = img[3 * Y + sy][3 * X];
+                    m[sy] = (((double)r0[k] + (double)r0[3 + k]) + (double)r0[6 + k]) / 3.0;
+                }
+                out[Y][X][k] = (uint8_t)(((m[0] + m[1]) + m[2]) / 3.0);
+            }
+}
+
+uint8_t g_atlas[MERLIN_OBS_TILES][8][8][3];
+std::once_flag g_atlas_once;
+
+void build_atlas() {
+    std::call_once(g_atlas_once, [] {
+        render_tile(0, false, false, g_atlas[0]);  // not visible: empty, no highlight
+        render_tile(0, false, true, g_atlas[1]);   // visible empty
+        render_tile(1, false, true, g_atlas[2]);   // visible wall
+        render_tile(2, false, true, g_atlas[3]);   // visible goal
+        render_tile(0, true, true, g_atlas[4]);    // agent (view cell (3,6), agent_dir 3)
+    });
+}
+
+// per-device one-time init: atlas upload + GAE partials workspace
+struct DeviceWs {
+    bool ready = false;
+    double *partials = nullptr;
+    int max_partials = 0;
+};
+constexpr int MAX_DEV = 64;
+DeviceWs g_dev[MAX_DEV];
+std::mutex g_dev_mu;
+constexpr int WS_PARTIALS = 1 << 16;
+
+int device_ws(DeviceWs **out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= MAX_DEV) return fail(MERLIN_E_UNSUPPORTED, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    DeviceWs &w = g_dev[dev];
+    if (!w.ready) {
+        build_atlas();
+        HIP_TRY(merlin::upload_atlas(&g_atlas[0][0][0][0]));
+        HIP_TRY(hipMalloc(&w.partials, sizeof(double) * 2 * WS_PARTIALS));
+        w.max_partials = WS_PARTIALS;
+        w.ready = true;
+    }
+    *out = &w;
+    return MERLIN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int merlin_version(void) { return MERLIN_ABI_VERSION; }
+
+const char *merlin_last_error(void) { return g_err.c_str(); }
+
+int merlin_tile_atlas(uint8_t *out_host) {
+    if (!out_host) return fail(MERLIN_E_INVALID, "null output");
+    build_atlas();
+    memcpy(out_host, g_atlas, sizeof(g_atlas));
+    return MERLIN_OK;
+}
+
+int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
+    if (!cfg || !out) return fail(MERLIN_E_INVALID, "null argument");
+    *out = nullptr;
+    if (cfg->num_envs <= 0) return fail(MERLIN_E_INVALID, "num_envs must be > 0");
+    if (cfg->size < 5 || cfg->size > 32)
+        return fail(MERLIN_E_UNSUPPORTED, "grid size must be in [5, 32]");
+    if (cfg->difficulty < MERLIN_EASY || cfg->difficulty > MERLIN_HARDEST)
+        return fail(MERLIN_E_INVALID, "unknown difficulty");
+    if (cfg->difficulty == MERLIN_HARDEST && cfg->size < 9)
+        return fail(MERLIN_E_UNSUPPORTED, "hardest needs size >= 9 (integers(2, mid-1))");
+    if (cfg->difficulty == MERLIN_HARD && cfg->size < 6)
+        return fail(MERLIN_E_UNSUPPORTED, "hard needs size >= 6");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    merlin_env *e = new merlin_env();
+    merlin::EnvDev &d = e->dev;
+    d.n = cfg->num_envs;
+    d.size = cfg->size;
+    d.sp = cfg->size <= 16 ? 16 : 32;
+    d.difficulty = cfg->difficulty;
+    d.max_steps = cfg->max_steps > 0 ? cfg->max_steps : 4 * cfg->size * cfg->size;
+    d.stuck_on = cfg->stuck_penalty ? 1 : 0;
+    d.max_stay = cfg->max_stay > 0 ? cfg->max_stay : 3;
+    d.penalty = cfg->penalty;
+    d.explore_on = cfg->exploration_bonus ? 1 : 0;
+    d.bonus = cfg->bonus;
+    (void)hipGetDevice(&e->device);
+    const size_t n = (size_t)d.n;
+    hipError_t err = hipSuccess;
+    auto alloc = [&](void **p, size_t bytes) {
+        if (err == hipSuccess) err = hipMalloc(p, bytes);
+        if (err == hipSuccess) err = hipMemset(*p, 0, bytes);
+    };
+    alloc((void **)&d.walls, n * d.sp * sizeof(uint32_t));
+    alloc((void **)&d.agent, n * sizeof(uint4));
+    alloc((void **)&d.rng_s, n * sizeof(ulonglong2));
+    alloc((void **)&d.rng_i, n * sizeof(ulonglong2));
+    alloc((void **)&d.rng_b, n * sizeof(uint2));
+    alloc((void **)&d.ep_ret, n * sizeof(double));
+    alloc((void **)&d.ep_len, n * sizeof(int32_t));
+    alloc((void **)&d.err, 2 * sizeof(uint32_t));
+    if (d.explore_on) alloc((void **)&d.visited, n * d.sp * sizeof(uint32_t));
+    if (err != hipSuccess) {
+        merlin_env_destroy(e);
+        return hip_fail(err, "hipMalloc(env state)");
+    }
+    *out = e;
+    return MERLIN_OK;
+}
+
+int merlin_env_destroy(merlin_env *e) {
+    if (!e) return MERLIN_OK;
+    merlin::EnvDev &d = e->dev;
+    void *ptrs[] = {d.walls, d.agent, d.rng_s, d.rng_i, d.rng_b, d.ep_ret, d.ep_len, d.err, d.visited};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    delete e;
+    return MERLIN_OK;
+}
+
+int merlin_env_num_envs(const merlin_env *e) { return e ? e->dev.n : -1; }
+int merlin_env_size(const merlin_env *e) { return e ? e->dev.size : -1; }
+
+int merlin_env_seed(merlin_env *e, const uint64_t *seeds, int32_t n, void *stream) {
+    if (!e || !seeds) return fail(MERLIN_E_INVALID, "null argument");
+    if (n != e->dev.n) return fail(MERLIN_E_INVALID, "seed count must equal num_envs");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t N = (size_t)n;
+    ulonglong2 *st = new ulonglong2[N];
+    ulonglong2 *inc = new ulonglong2[N];
+    for (size_t i = 0; i < N; i++) {
+        U128 a, b;
+        seed_pcg64(seeds[i], a, b);
+        st[i] = make_ulonglong2(a.lo, a.hi);
+        inc[i] = make_ulonglong2(b.lo, b.hi);
+    }
+    hipError_t err = hipMemcpyAsync(e->dev.rng_s, st, N * sizeof(ulonglong2), hipMemcpyHostToDevice, s);
+    if (err == hipSuccess)
+        err = hipMemcpyAsync(e->dev.rng_i, inc, N * sizeof(ulonglong2), hipMemcpyHostToDevice, s);
+    if (err == hipSuccess) err = hipMemsetAsync(e->dev.rng_b, 0, N * sizeof(uint2), s);
+    if (err == hipSuccess) err = hipStreamSynchronize(s);  // host staging buffers are freed below
+    delete[] st;
+    delete[] inc;
+    if (err != hipSuccess) return hip_fail(err, "merlin_env_seed");
+    return MERLIN_OK;
+}
+
+int merlin_env_reset(merlin_env *e, const uint8_t *mask, uint32_t *obs, void *stream) {
+    if (!e) return fail(MERLIN_E_INVALID, "null env");
+    HIP_TRY(merlin::launch_env_reset(e->dev, mask, obs, (hipStream_t)stream));
+    if (!mask) e->has_state = true;
+    return MERLIN_OK;
+}
+
+int merlin_env_step(merlin_env *e, const int64_t *actions, int32_t n_steps, int64_t action_stride,
+                    uint32_t *obs, float *reward, uint8_t *term, uint8_t *trunc, float *done,
+                    double *ep_ret, int32_t *ep_len, int32_t autoreset, void *stream) {
+    if (!e || !actions) return fail(MERLIN_E_INVALID, "null argument");
+    if (!e->has_state) return fail(MERLIN_E_INVALID, "merlin_env_step before merlin_env_reset");
+    if (n_steps <= 0) return MERLIN_OK;
+    if (action_stride < e->dev.n && n_steps > 1)
+        return fail(MERLIN_E_INVALID, "action_stride must be >= num_envs");
+    merlin::StepOut o;
+    o.actions = actions;
+    o.action_stride = action_stride;
+    o.n_steps = n_steps;
+    o.autoreset = autoreset;
+    o.obs = obs;
+    o.reward = reward;
+    o.term = term;
+    o.trunc = trunc;
+    o.done = done;
+    o.ep_ret_out = ep_ret;
+    o.ep_len_out = ep_len;
+    HIP_TRY(merlin::launch_env_step(e->dev, o, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_env_get_state(merlin_env *e, uint32_t *walls, int32_t *agent, uint64_t *rng, void *stream) {
+    if (!e) return fail(MERLIN_E_INVALID, "null env");
+    hipStream_t s = (hipStream_t)stream;
+    const merlin::EnvDev &d = e->dev;
+    const size_t n = (size_t)d.n;
+    if (walls) {
+        uint32_t *tmp = new uint32_t[n * d.sp];
+        hipError_t err = hipMemcpyAsync(tmp, d.walls, n * d.sp * 4, hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess) err = hipStreamSynchronize(s);
+        if (err == hipSuccess)
+            for (size_t i = 0; i < n; i++)
+                for (int y = 0; y < d.size; y++) walls[i * d.size + y] = tmp[i * d.sp + y];
+        delete[] tmp;
+        if (err != hipSuccess) return hip_fail(err, "get_state(walls)");
+    }
+    if (agent) {
+        uint4 *tmp = new uint4[n];
+        hipError_t err = hipMemcpyAsync(tmp, d.agent, n * sizeof(uint4), hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess) err = hipStreamSynchronize(s);
+        if (err == hipSuccess)
+            for (size_t i = 0; i < n; i++) {
+                int32_t *a = agent + i * 8;
+                a[0] = tmp[i].x & 0xff;
+                a[1] = (tmp[i].x >> 8) & 0xff;
+                a[2] = (tmp[i].x >> 16) & 3;
+                a[3] = (int32_t)tmp[i].y;
+                a[4] = tmp[i].z & 0xff;
+                a[5] = (tmp[i].z >> 8) & 0xff;
+                a[6] = (int32_t)(tmp[i].w >> 16);
+                a[7] = 0;
+            }
+        delete[] tmp;
+        if (err != hipSuccess) return hip_fail(err, "get_state(agent)");
+    }
+    if (rng) {
+        ulonglong2 *a = new ulonglong2[n], *b = new ulonglong2[n];
+        uint2 *c = new uint2[n];
+        hipError_t err = hipMemcpyAsync(a, d.rng_s, n * sizeof(ulonglong2), hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess) err = hipMemcpyAsync(b, d.rng_i, n * sizeof(ulonglong2), hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess) err = hipMemcpyAsync(c, d.rng_b, n * sizeof(uint2), hipMemcpyDeviceToHost, s);
+        if (err == hipSuccess) err = hipStreamSynchronize(s);
+        if (err == hipSuccess)
+            for (size_t i = 0; i < n; i++) {
+                uint64_t *r = rng + i * 5;
+                r[0] = a[i].y;
+                r[1] = a[i].x;
+                r[2] = b[i].y;
+                r[3] = b[i].x;
+                r[4] = ((uint64_t)c[i].x << 32) | c[i].y;
+            }
+        delete[] a;
+        delete[] b;
+        delete[] c;
+        if (err != hipSuccess) return hip_fail(err, "get_state(rng)");
+    }
+    return MERLIN_OK;
+}
+
+int merlin_env_errors(merlin_env *e, uint32_t *flags, uint32_t *fallbacks, void *stream) {
+    if (!e) return fail(MERLIN_E_INVALID, "null env");
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, e->dev.err, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemsetAsync(e->dev.err, 0, sizeof(h), s));
+    if (flags) *flags = h[0];
+    if (fallbacks) *fallbacks = h[1];
+    return MERLIN_OK;
+}
+
+int merlin_obs_expand_f32(const uint32_t *codes, const int64_t *index, int64_t n, float *out, float scale,
+                          int32_t layout, void *stream) {
+    if ((!codes || !out) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (layout != MERLIN_LAYOUT_NCHW && layout != MERLIN_LAYOUT_NHWC)
+        return fail(MERLIN_E_INVALID, "unknown layout");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_obs_expand_f32(codes, index, n, out, scale, layout, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_obs_expand_u8(const uint32_t *codes, const int64_t *index, int64_t n, uint8_t *out, void *stream) {
+    if ((!codes || !out) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_obs_expand_u8(codes, index, n, out, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_gae(const float *rew, const float *val, const float *done, const float *last, float *adv,
+               float *ret, int32_t T, int32_t N, double gamma, double lam, double *stats, void *stream) {
+    if (!rew || !val || !done || !last || !adv || !ret) return fail(MERLIN_E_INVALID, "null argument");
+    if (T <= 0 || N <= 0) return fail(MERLIN_E_INVALID, "T and N must be > 0");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    if (stats && merlin::gae_partials_needed(T, N) > ws->max_partials)
+        return fail(MERLIN_E_UNSUPPORTED, "too many envs for the GAE stats workspace");
+    HIP_TRY(merlin::launch_gae(rew, val, done, last, adv, ret, T, N, gamma, lam, stats, ws->partials,
+                               ws->max_partials, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_adv_normalize(const float *adv, int64_t n, const double *stats, float *out, void *stream) {
+    if (!adv || !stats || !out) return fail(MERLIN_E_INVALID, "null argument");
+    HIP_TRY(merlin::launch_adv_normalize(adv, n, stats, out, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+}  // extern "C"

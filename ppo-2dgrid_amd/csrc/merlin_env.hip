@@ -1,0 +1,654 @@
+// merlin_env.hip -- batched MiniGrid dynamics for the MERLIN envs on gfx950.
+//
+// One thread owns one env (the envs are independent; a wave = 64 envs).  The
+// env's wall rows are staged into a per-thread LDS column (rows[r][lane]) so
+// that the data-dependent row reads of the 7x7 view, the forward-cell test and
+// the rejection-sampling occupancy tests are LDS reads, not scattered global
+// loads; the rows reach HBM again only after a reset rewrote them.  The step
+// loop keeps agent state in registers across n_steps (the env-only rollout
+// runs many steps per launch).
+//
+// Semantics follow the reference (paths relative to its checkout):
+//   step    MiniGridEnv.step via ThreeActionWrapper (three_action_wrapper.py:16-17),
+//           reward 1 - 0.9*step/max_steps in f64, done = term or trunc (src/ppo.py:77),
+//           StuckPenaltyWrapper.step (stuck_penalty_wrapper.py:29-57) when enabled
+//   reset   MiniGridEnv.reset -> _gen_grid of easy_env.py:19-39, medium_env.py:19-33,
+//           medium_hard_env.py:12-45 (+ _is_reachable :47-74), hard_env.py:11-73,
+//           hardest_env.py:20-70, drawing from numpy's PCG64 with the Lemire
+//           bounded-integer model (bit-exact with Generator.integers / choice)
+//   view    gen_obs_grid (get_view_exts, Grid.slice, rotate_left^(dir+1),
+//           process_vis with see_through_walls=False, base_env.py:39) and the
+//           get_pov_render tile classes (RGBImgPartialObsWrapper, scenario_creator.py:48)
+#include "merlin_internal.h"
+
+namespace merlin {
+namespace {
+
+constexpr int BLK = 64;  // one wave per block: the env count (4096) is small, spread it over CUs
+
+// ---------------------------------------------------------------------------
+// numpy PCG64 + bounded integers
+struct Rng {
+    uint64_t slo, shi, ilo, ihi;
+    uint32_t has, buf;
+};
+
+__device__ __forceinline__ uint64_t rng_next64(Rng &r) {
+    // state = state * 0x2360ed051fc65da44385df649fccf645 + inc (mod 2^128), then XSL-RR
+    const uint64_t MLO = 0x4385df649fccf645ULL, MHI = 0x2360ed051fc65da4ULL;
+    uint64_t lo = r.slo * MLO;
+    uint64_t hi = __umul64hi(r.slo, MLO) + r.slo * MHI + r.shi * MLO;
+    uint64_t nlo = lo + r.ilo;
+    hi += r.ihi + (nlo < lo ? 1ULL : 0ULL);
+    r.slo = nlo;
+    r.shi = hi;
+    uint64_t x = hi ^ nlo;
+    unsigned rot = (unsigned)(hi >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+__device__ __forceinline__ uint32_t rng_next32(Rng &r) {
+    if (r.has) {
+        r.has = 0;
+        return r.buf;
+    }
+    uint64_t v = rng_next64(r);
+    r.has = 1;
+    r.buf = (uint32_t)(v >> 32);
+    return (uint32_t)v;
+}
+
+// buffered_bounded_lemire_uint32(rng = range - 1)
+__device__ __forceinline__ uint32_t rng_lemire(Rng &r, uint32_t rng_incl) {
+    const uint32_t excl = rng_incl + 1u;
+    uint64_t m = (uint64_t)rng_next32(r) * excl;
+    uint32_t left = (uint32_t)m;
+    if (left < excl) {
+        const uint32_t thresh = (0xffffffffu - rng_incl) % excl;
+        while (left < thresh) {
+            m = (uint64_t)rng_next32(r) * excl;
+            left = (uint32_t)m;
+        }
+    }
+    return (uint32_t)(m >> 32);
+}
+
+// Generator.integers(lo, hi)
+__device__ __forceinline__ int rng_int(Rng &r, int lo, int hi) {
+    uint32_t rng = (uint32_t)(hi - lo - 1);
+    if (rng == 0u) return lo;
+    return lo + (int)rng_lemire(r, rng);
+}
+
+__device__ __forceinline__ Rng load_rng(const EnvDev &E, int i) {
+    ulonglong2 s = E.rng_s[i], c = E.rng_i[i];
+    uint2 b = E.rng_b[i];
+    Rng r;
+    r.slo = s.x;
+    r.shi = s.y;
+    r.ilo = c.x;
+    r.ihi = c.y;
+    r.has = b.x;
+    r.buf = b.y;
+    return r;
+}
+
+__device__ __forceinline__ void store_rng(const EnvDev &E, int i, const Rng &r) {
+    E.rng_s[i] = make_ulonglong2(r.slo, r.shi);
+    E.rng_b[i] = make_uint2(r.has, r.buf);
+}
+
+// ---------------------------------------------------------------------------
+// Per-thread grid view over the LDS column + generator state.
+template <int SP>
+struct Grid {
+    uint32_t (*rows)[BLK];  // LDS [SP][BLK]; this thread owns column `lane`
+    int lane, S;
+    int ax, ay, dir;
+    int gx, gy;
+    bool goal_set;
+    uint32_t err;
+
+    __device__ __forceinline__ uint32_t row(int y) const { return rows[y][lane]; }
+    __device__ __forceinline__ void set_row(int y, uint32_t v) { rows[y][lane] = v; }
+    __device__ __forceinline__ bool wall(int x, int y) const { return (row(y) >> x) & 1u; }
+    __device__ __forceinline__ void set_wall(int x, int y) { set_row(y, row(y) | (1u << x)); }
+    __device__ __forceinline__ void clear_wall(int x, int y) { set_row(y, row(y) & ~(1u << x)); }
+    __device__ __forceinline__ uint32_t full() const { return S >= 32 ? 0xffffffffu : ((1u << S) - 1u); }
+    __device__ __forceinline__ bool occupied(int x, int y) const {
+        return wall(x, y) || (goal_set && x == gx && y == gy);
+    }
+
+    // Grid(W,H) + wall_rect(0,0,W,H)
+    __device__ void walled() {
+        const uint32_t edge = 1u | (1u << (S - 1));
+#pragma unroll
+        for (int y = 0; y < SP; y++)
+            if (y < S) set_row(y, (y == 0 || y == S - 1) ? full() : edge);
+        goal_set = false;
+    }
+
+    // MiniGridEnv.place_obj: x then y; reject occupied cells and agent_pos.
+    // kind: 0 none (agent), 1 wall, 2 goal.  max_tries < 0 = unbounded.
+    __device__ bool place(Rng &r, int kind, int tx, int ty, int sw, int sh, int max_tries, int &px,
+                          int &py) {
+        const int xe = min(tx + sw, S), ye = min(ty + sh, S);
+        int tries = 0;
+        for (;;) {
+            if (max_tries >= 0 && tries > max_tries) {
+                err |= MERLIN_DEVERR_PLACE_OBJ;
+                return false;
+            }
+            tries++;
+            int x = rng_int(r, tx, xe);
+            int y = rng_int(r, ty, ye);
+            if (occupied(x, y)) continue;
+            if (x == ax && y == ay) continue;
+            if (kind == 1) set_wall(x, y);
+            if (kind == 2) {
+                gx = x;
+                gy = y;
+                goal_set = true;
+            }
+            px = x;
+            py = y;
+            return true;
+        }
+    }
+
+    // MiniGridEnv.place_agent(top, size, rand_dir=True)
+    __device__ void place_agent(Rng &r, int tx, int ty, int sw, int sh) {
+        int x, y;
+        ax = -1;
+        ay = -1;
+        place(r, 0, tx, ty, sw, sh, -1, x, y);
+        ax = x;
+        ay = y;
+        dir = rng_int(r, 0, 4);
+    }
+
+    __device__ void place_goal(Rng &r) {
+        int x, y;
+        place(r, 2, 0, 0, S, S, -1, x, y);
+    }
+
+    // _is_reachable (medium_hard_env.py:47-74): the BFS's boolean equals "goal in
+    // the 4-connected component of non-wall cells containing the agent"; computed
+    // as a bit-parallel flood fill over row masks (Gauss-Seidel sweeps in registers).
+    __device__ bool reachable() const {
+        uint32_t F[SP], R[SP];
+        const uint32_t fm = full();
+#pragma unroll
+        for (int y = 0; y < SP; y++) {
+            F[y] = (y < S) ? (~row(y) & fm) : 0u;
+            R[y] = (y == ay) ? (1u << ax) : 0u;
+        }
+        for (int it = 0; it < SP * SP; it++) {
+            uint32_t changed = 0u;
+#pragma unroll
+            for (int y = 0; y < SP; y++) {
+                uint32_t n = R[y] | (R[y] << 1) | (R[y] >> 1);
+                if (y > 0) n |= R[y - 1];
+                if (y < SP - 1) n |= R[y + 1];
+                n &= F[y];
+                changed |= n ^ R[y];
+                R[y] = n;
+            }
+#pragma unroll
+            for (int y = SP - 1; y >= 0; y--) {
+                uint32_t n = R[y] | (R[y] << 1) | (R[y] >> 1);
+                if (y > 0) n |= R[y - 1];
+                if (y < SP - 1) n |= R[y + 1];
+                n &= F[y];
+                changed |= n ^ R[y];
+                R[y] = n;
+            }
+            uint32_t hit = 0u;
+#pragma unroll
+            for (int y = 0; y < SP; y++) hit |= (y == gy) ? ((R[y] >> gx) & 1u) : 0u;
+            if (hit) return true;
+            if (!changed) return false;
+        }
+        return false;
+    }
+
+    __device__ void fallback(Rng &r, uint32_t *fallbacks) {
+        atomicAdd(fallbacks, 1u);
+        walled();
+        place_agent(r, 0, 0, S, S);
+        place_goal(r);
+    }
+
+    // EasyEnv._gen_grid (easy_env.py:19-39): put_obj(Goal, W-5, H-5) may sit on the agent
+    __device__ void gen_easy(Rng &r) {
+        walled();
+        place_agent(r, 0, 0, S, S);
+        gx = S - 5;
+        gy = S - 5;
+        goal_set = true;
+    }
+
+    // MediumEnv._gen_grid (medium_env.py:19-33)
+    __device__ void gen_medium(Rng &r) {
+        walled();
+        place_agent(r, 0, 0, S, S);
+        place_goal(r);
+    }
+
+    // MediumHardEnv._gen_grid (medium_hard_env.py:12-45); on a retry the previous
+    // attempt's agent_pos still blocks wall placement (place_agent resets it later).
+    __device__ void gen_mediumhard(Rng &r, uint32_t *fallbacks) {
+        const int playable = (S - 2) * (S - 2);
+        const int min_obs = (playable * 10) / 100;  // int(playable * 0.10)
+        const int max_obs = (playable * 20) / 100;  // int(playable * 0.20)
+        for (int attempt = 0; attempt < 100; attempt++) {
+            walled();
+            int n = rng_int(r, max(1, min_obs), max(1, max_obs) + 1);
+            for (int k = 0; k < n; k++) {
+                int x, y;
+                if (!place(r, 1, 0, 0, S, S, 100, x, y)) return;
+            }
+            place_agent(r, 0, 0, S, S);
+            place_goal(r);
+            if (reachable()) return;
+        }
+        fallback(r, fallbacks);
+    }
+
+    // HardEnv._gen_grid (hard_env.py:11-73), agent_start_pos None, random_goal True
+    __device__ void gen_hard(Rng &r, uint32_t *fallbacks) {
+        const int mid = S / 2;
+        const bool large = S > 10;
+        for (int attempt = 0; attempt < 100; attempt++) {
+            walled();
+            const int k = large ? rng_int(r, 2, 6) : 1;
+            // choice(range(1, S-1), k, replace=False): Floyd + tail shuffle (pop <= 10000)
+            const int pop = S - 2;
+            int idx[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 5; q++) {
+                if (q < k) {
+                    const int j = pop - k + q;
+                    int val = (j == 0) ? 0 : (int)rng_lemire(r, (uint32_t)j);
+                    bool dup = false;
+#pragma unroll
+                    for (int p = 0; p < 5; p++) dup |= (p < q) && (idx[p] == val);
+                    idx[q] = dup ? j : val;
+                }
+            }
+#pragma unroll
+            for (int i = 4; i >= 1; i--) {
+                if (i < k) {
+                    const int j = (int)rng_lemire(r, (uint32_t)i);
+                    int a = 0;
+#pragma unroll
+                    for (int p = 0; p < 5; p++) a = (p == j) ? idx[p] : a;
+                    const int b = idx[i];
+#pragma unroll
+                    for (int p = 0; p < 5; p++) idx[p] = (p == j) ? b : idx[p];
+                    idx[i] = a;
+                }
+            }
+            uint32_t gap_rows = 0u;  // bit i = row i is a gap
+#pragma unroll
+            for (int p = 0; p < 5; p++)
+                if (p < k) gap_rows |= 1u << (idx[p] + 1);
+            for (int i = 1; i < S - 1; i++)
+                if (!((gap_rows >> i) & 1u)) set_wall(mid, i);
+            if (large) {
+                const int extra = rng_int(r, 6, 13);
+                for (int w = 0; w < extra; w++) {
+                    for (int t = 0; t < 10; t++) {
+                        int x = rng_int(r, 1, S - 1);
+                        int y = rng_int(r, 1, S - 1);
+                        if (x != mid && !wall(x, y)) {  // no goal placed yet
+                            set_wall(x, y);
+                            break;
+                        }
+                    }
+                }
+            }
+            int x, y;
+            place(r, 2, mid + 1, 0, S - mid - 1, S, -1, x, y);
+            place_agent(r, 1, 1, mid - 1, S - 2);
+            if (reachable()) return;
+        }
+        fallback(r, fallbacks);
+    }
+
+    // HardestEnv._gen_grid (hardest_env.py:20-70)
+    __device__ void gen_hardest(Rng &r, uint32_t *fallbacks) {
+        const int mx = S / 2, my = S / 2;
+        for (int attempt = 0; attempt < 100; attempt++) {
+            walled();
+            for (int y = 1; y < S - 1; y++) set_wall(mx, y);
+            set_row(my, full());  // x in [1, S-1) plus the border bits already set
+            clear_wall(mx, rng_int(r, 2, my - 1));
+            clear_wall(mx, rng_int(r, my + 1, S - 2));
+            clear_wall(rng_int(r, 2, mx - 1), my);
+            clear_wall(rng_int(r, mx + 1, S - 2), my);
+            const int nobs = rng_int(r, 6, 13);
+            for (int k = 0; k < nobs; k++) {
+                int x = rng_int(r, 1, S - 1);
+                int y = rng_int(r, 1, S - 1);
+                if (!wall(x, y) && x != mx && y != my) set_wall(x, y);
+            }
+            place_agent(r, 0, 0, S, S);
+            place_goal(r);
+            if (reachable()) return;
+        }
+        fallback(r, fallbacks);
+    }
+
+    // MiniGridEnv.reset body: agent_pos=(-1,-1); _gen_grid(W,H)
+    __device__ void generate(Rng &r, int difficulty, uint32_t *fallbacks) {
+        ax = -1;
+        ay = -1;
+        dir = 0;
+        goal_set = false;
+        switch (difficulty) {
+            case MERLIN_EASY: gen_easy(r); break;
+            case MERLIN_MEDIUM: gen_medium(r); break;
+            case MERLIN_MEDIUMHARD: gen_mediumhard(r, fallbacks); break;
+            case MERLIN_HARD: gen_hard(r, fallbacks); break;
+            default: gen_hardest(r, fallbacks); break;
+        }
+    }
+};
+
+__device__ __forceinline__ uint32_t bitrev7(uint32_t v) { return __brev(v) >> 25; }
+
+// gen_obs_grid + get_pov_render tile classes -> 8 packed nibble words.
+template <int SP>
+__device__ __forceinline__ void view_codes(const Grid<SP> &G, uint32_t out[MERLIN_OBS_WORDS]) {
+    const int S = G.S, ax = G.ax, ay = G.ay, dir = G.dir;
+    // get_view_exts (top-left of the 7x7 world window)
+    int tx, ty;
+    if (dir == 0) {
+        tx = ax;
+        ty = ay - 3;
+    } else if (dir == 1) {
+        tx = ax - 3;
+        ty = ay;
+    } else if (dir == 2) {
+        tx = ax - 6;
+        ty = ay - 3;
+    } else {
+        tx = ax - 3;
+        ty = ay - 6;
+    }
+    // Grid.slice: out-of-bounds cells read as Wall
+    const uint64_t hi_ones = ~0ULL << (S + 8);
+    uint32_t win[7];
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+        const int y = ty + r;
+        const bool in = (y >= 0) && (y < S);
+        const uint32_t row = in ? G.row(in ? y : 0) : 0xffffffffu;
+        const uint64_t w = ((uint64_t)row << 8) | 0xffULL | hi_ones;
+        win[r] = (uint32_t)(w >> (tx + 8)) & 0x7fu;  // bit c = cell (c, r) of the slice
+    }
+    // rotate_left applied k = (dir+1) mod 4 times: built from transpose / row flip / bit reverse
+    uint32_t tr[7];
+#pragma unroll
+    for (int x = 0; x < 7; x++) {
+        uint32_t v = 0u;
+#pragma unroll
+        for (int y = 0; y < 7; y++) v |= ((win[y] >> x) & 1u) << y;
+        tr[x] = v;
+    }
+    const int k = (dir + 1) & 3;
+    const bool odd = k & 1, flip = (k == 1) || (k == 2), rev = (k >= 2);
+    uint32_t V[7];  // V[j] bit i = view cell (i, j) is a wall
+#pragma unroll
+    for (int b = 0; b < 7; b++) {
+        uint32_t m = flip ? (odd ? tr[6 - b] : win[6 - b]) : (odd ? tr[b] : win[b]);
+        V[b] = rev ? bitrev7(m) : m;
+    }
+    // goal position in view: view(vi,vj) <- world(agent + (6-vj)*F + (vi-3)*R)
+    const int Fx = (dir == 0) - (dir == 2), Fy = (dir == 1) - (dir == 3);
+    const int Rx = -Fy, Ry = Fx;  // DIR_TO_VEC[(dir+1)%4]
+    const int dx = G.gx - ax, dy = G.gy - ay;
+    const int gvj = 6 - (dx * Fx + dy * Fy), gvi = 3 + (dx * Rx + dy * Ry);
+    const bool ginv = G.goal_set && gvi >= 0 && gvi < 7 && gvj >= 0 && gvj < 7;
+    // Grid.process_vis(agent_pos=(3,6)) as row bit-ops (walls opaque, goal/empty transparent)
+    uint32_t m[7] = {0u, 0u, 0u, 0u, 0u, 0u, 1u << 3};
+#pragma unroll
+    for (int j = 6; j >= 0; j--) {
+        const uint32_t T = ~V[j] & 0x7fu;
+        uint32_t M = m[j];
+#pragma unroll
+        for (int s = 0; s < 6; s++) M |= (M & T & 0x3fu) << 1;  // left-to-right pass
+        const uint32_t e1 = M & T & 0x3fu;
+#pragma unroll
+        for (int s = 0; s < 6; s++) M |= (M & T & 0x7eu) >> 1;  // right-to-left pass
+        const uint32_t e2 = M & T & 0x7eu;
+        m[j] = M;
+        if (j > 0) m[j - 1] |= e1 | (e1 << 1) | e2 | (e2 >> 1);
+    }
+#pragma unroll
+    for (int w = 0; w < MERLIN_OBS_WORDS; w++) out[w] = 0u;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const int kk = j * 7 + i;
+            uint32_t c;
+            if (i == 3 && j == 6) {
+                c = 4u;  // agent tile (its own cell is set to None, agent_dir=3)
+            } else {
+                const bool vis = (m[j] >> i) & 1u;
+                const bool wl = (V[j] >> i) & 1u;
+                const bool gl = ginv && gvi == i && gvj == j;
+                c = !vis ? 0u : (wl ? 2u : (gl ? 3u : 1u));
+            }
+            out[kk >> 3] |= c << ((kk & 7) * 4);
+        }
+    }
+}
+
+template <int SP>
+__device__ __forceinline__ void load_rows(const EnvDev &E, int i, Grid<SP> &G) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(E.walls + (size_t)i * SP);
+#pragma unroll
+    for (int q = 0; q < SP / 4; q++) {
+        const uint4 v = src[q];
+        G.set_row(4 * q + 0, v.x);
+        G.set_row(4 * q + 1, v.y);
+        G.set_row(4 * q + 2, v.z);
+        G.set_row(4 * q + 3, v.w);
+    }
+}
+
+template <int SP>
+__device__ __forceinline__ void store_rows(const EnvDev &E, int i, const Grid<SP> &G) {
+    uint4 *dst = reinterpret_cast<uint4 *>(E.walls + (size_t)i * SP);
+#pragma unroll
+    for (int q = 0; q < SP / 4; q++) {
+        const int y = 4 * q;
+        dst[q] = make_uint4(y + 0 < G.S ? G.row(y + 0) : 0u, y + 1 < G.S ? G.row(y + 1) : 0u,
+                            y + 2 < G.S ? G.row(y + 2) : 0u, y + 3 < G.S ? G.row(y + 3) : 0u);
+    }
+}
+
+__device__ __forceinline__ void store_obs(uint32_t *obs, size_t row, const uint32_t w[8]) {
+    uint4 *d = reinterpret_cast<uint4 *>(obs + row * MERLIN_OBS_WORDS);
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+__device__ __forceinline__ uint4 pack_agent(int ax, int ay, int dir, int steps, int gx, int gy,
+                                            int lx, int ly, int stay) {
+    return make_uint4((uint32_t)ax | ((uint32_t)ay << 8) | ((uint32_t)dir << 16), (uint32_t)steps,
+                      (uint32_t)gx | ((uint32_t)gy << 8),
+                      (uint32_t)lx | ((uint32_t)ly << 8) | ((uint32_t)min(stay, 65535) << 16));
+}
+
+// Post-reset bookkeeping shared by the reset kernel and the auto-reset path.
+template <int SP>
+__device__ __forceinline__ void on_reset(const EnvDev &E, int i, const Grid<SP> &G) {
+    E.ep_ret[i] = 0.0;
+    E.ep_len[i] = 0;
+    if (E.explore_on) {
+        uint32_t *vis = E.visited + (size_t)i * SP;
+        for (int y = 0; y < SP; y++) vis[y] = (y == G.ay) ? (1u << G.ax) : 0u;
+    }
+}
+
+template <int SP>
+__global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__restrict__ mask,
+                                                  uint32_t *__restrict__ obs) {
+    __shared__ uint32_t rows[SP][BLK];
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * BLK + lane;
+    if (i >= E.n) return;
+    if (mask && !mask[i]) return;
+    Grid<SP> G;
+    G.rows = rows;
+    G.lane = lane;
+    G.S = E.size;
+    G.err = 0u;
+    Rng r = load_rng(E, i);
+    G.generate(r, E.difficulty, E.err + 1);
+    store_rng(E, i, r);
+    store_rows(E, i, G);
+    E.agent[i] = pack_agent(G.ax, G.ay, G.dir, 0, G.gx, G.gy, G.ax, G.ay, 0);
+    on_reset(E, i, G);
+    if (G.err) atomicOr(E.err, G.err);
+    uint32_t w[MERLIN_OBS_WORDS];
+    view_codes(G, w);
+    if (obs) store_obs(obs, (size_t)i, w);
+}
+
+template <int SP>
+__global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
+    __shared__ uint32_t rows[SP][BLK];
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * BLK + lane;
+    if (i >= E.n) return;
+    Grid<SP> G;
+    G.rows = rows;
+    G.lane = lane;
+    G.S = E.size;
+    G.err = 0u;
+    G.goal_set = true;
+    load_rows(E, i, G);
+    const uint4 st = E.agent[i];
+    G.ax = st.x & 0xff;
+    G.ay = (st.x >> 8) & 0xff;
+    G.dir = (st.x >> 16) & 3;
+    int steps = (int)st.y;
+    G.gx = st.z & 0xff;
+    G.gy = (st.z >> 8) & 0xff;
+    int lx = st.w & 0xff, ly = (st.w >> 8) & 0xff, stay = (int)(st.w >> 16);
+    double ep_ret = E.ep_ret[i];
+    int ep_len = E.ep_len[i];
+    bool rows_dirty = false, rng_loaded = false;
+    Rng r;
+    const size_t N = (size_t)E.n;
+
+    for (int t = 0; t < O.n_steps; t++) {
+        const int64_t a = O.actions[(size_t)t * O.action_stride + i];
+        steps += 1;
+        const int fx = G.ax + ((G.dir == 0) - (G.dir == 2));
+        const int fy = G.ay + ((G.dir == 1) - (G.dir == 3));
+        const bool fwall = G.wall(fx, fy);
+        const bool fgoal = (fx == G.gx) && (fy == G.gy);
+        double rew = 0.0;
+        bool term = false;
+        if (a == 0) {
+            G.dir = (G.dir + 3) & 3;
+        } else if (a == 1) {
+            G.dir = (G.dir + 1) & 3;
+        } else if (a == 2) {
+            if (!fwall) {  // None or Goal (can_overlap)
+                G.ax = fx;
+                G.ay = fy;
+            }
+            if (fgoal) {
+                term = true;
+                rew = 1.0 - 0.9 * ((double)steps / (double)E.max_steps);  // MiniGridEnv._reward
+            }
+        } else {
+            G.err |= MERLIN_DEVERR_BAD_ACTION;
+        }
+        const bool trunc = steps >= E.max_steps;
+        if (E.stuck_on) {  // StuckPenaltyWrapper.step
+            stay = (G.ax == lx && G.ay == ly) ? stay + 1 : 0;
+            if (stay >= E.max_stay) rew += E.penalty;
+            lx = G.ax;
+            ly = G.ay;
+        }
+        if (E.explore_on) {  // ExplorationBonus (MERLIN-AMD definition; absent in the reference)
+            uint32_t *vrow = E.visited + (size_t)i * SP + G.ay;
+            const uint32_t bit = 1u << G.ax, v = *vrow;
+            if (!(v & bit)) {
+                *vrow = v | bit;
+                rew += E.bonus;
+            }
+        }
+        const bool done = term || trunc;
+        ep_ret += rew;
+        ep_len += 1;
+        const size_t row = (size_t)t * N + i;
+        if (O.reward) O.reward[row] = (float)rew;
+        if (O.term) O.term[row] = term;
+        if (O.trunc) O.trunc[row] = trunc;
+        if (O.done) O.done[row] = done ? 1.0f : 0.0f;
+        if (done) {
+            if (O.ep_ret_out) O.ep_ret_out[row] = ep_ret;
+            if (O.ep_len_out) O.ep_len_out[row] = ep_len;
+        }
+        if (done && O.autoreset) {
+            if (!rng_loaded) {
+                r = load_rng(E, i);
+                rng_loaded = true;
+            }
+            G.generate(r, E.difficulty, E.err + 1);
+            rows_dirty = true;
+            steps = 0;
+            stay = 0;
+            lx = G.ax;
+            ly = G.ay;
+            ep_ret = 0.0;
+            ep_len = 0;
+            if (E.explore_on) {
+                uint32_t *vis = E.visited + (size_t)i * SP;
+                for (int y = 0; y < SP; y++) vis[y] = (y == G.ay) ? (1u << G.ax) : 0u;
+            }
+        }
+        if (O.obs) {
+            uint32_t w[MERLIN_OBS_WORDS];
+            view_codes(G, w);
+            store_obs(O.obs, row, w);
+        }
+    }
+    E.agent[i] = pack_agent(G.ax, G.ay, G.dir, steps, G.gx, G.gy, lx, ly, stay);
+    E.ep_ret[i] = ep_ret;
+    E.ep_len[i] = ep_len;
+    if (rows_dirty) store_rows(E, i, G);
+    if (rng_loaded) store_rng(E, i, r);
+    if (G.err) atomicOr(E.err, G.err);
+}
+
+}  // namespace
+
+hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s) {
+    const dim3 grid((E.n + BLK - 1) / BLK), block(BLK);
+    if (E.sp == 16)
+        hipLaunchKernelGGL(k_env_reset<16>, grid, block, 0, s, E, mask, obs);
+    else
+        hipLaunchKernelGGL(k_env_reset<32>, grid, block, 0, s, E, mask, obs);
+    return hipGetLastError();
+}
+
+hipError_t launch_env_step(const EnvDev &E, const StepOut &O, hipStream_t s) {
+    const dim3 grid((E.n + BLK - 1) / BLK), block(BLK);
+    if (E.sp == 16)
+        hipLaunchKernelGGL(k_env_step<16>, grid, block, 0, s, E, O);
+    else
+        hipLaunchKernelGGL(k_env_step<32>, grid, block, 0, s, E, O);
+    return hipGetLastError();
+}
+
+}  // namespace merlin

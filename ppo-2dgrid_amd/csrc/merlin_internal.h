@@ -1,0 +1,68 @@
+// merlin_internal.h -- shared declarations between the HIP translation units of
+// libmerlin_hip.so (not part of the public ABI; see include/merlin_hip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "merlin_hip.h"
+
+namespace merlin {
+
+// Env state in HBM, structure-of-arrays, one slot per env (index i < n):
+//   walls   uint32[n][SP]   row bitmasks (bit x of row y = wall at (x, y)); SP = 16 or 32
+//   agent   uint4[n]        x: ax | ay<<8 | dir<<16   y: step_count
+//                           z: gx | gy<<8             w: last_x | last_y<<8 | stay<<16
+//   rng_s   ulonglong2[n]   PCG64 128-bit state (x = low 64, y = high 64)
+//   rng_i   ulonglong2[n]   PCG64 increment
+//   rng_b   uint2[n]        (has32, buf32) -- numpy's persistent 32-bit half buffer
+//   ep_ret  double[n]       running episode return (src/ppo.py:88 accumulates a Python float)
+//   ep_len  int32[n]
+//   visited uint32[n][SP]   exploration-bonus visit bitmask (only if enabled)
+//   err     uint32[2]       device error bits, fallback-map counter
+struct EnvDev {
+    int n, size, sp, difficulty, max_steps;
+    int stuck_on, max_stay;
+    double penalty;
+    int explore_on;
+    double bonus;
+    uint32_t *walls;
+    uint4 *agent;
+    ulonglong2 *rng_s;
+    ulonglong2 *rng_i;
+    uint2 *rng_b;
+    double *ep_ret;
+    int32_t *ep_len;
+    uint32_t *visited;
+    uint32_t *err;
+};
+
+struct StepOut {
+    const int64_t *actions;
+    int64_t action_stride;
+    int n_steps;
+    int autoreset;
+    uint32_t *obs;
+    float *reward;
+    uint8_t *term;
+    uint8_t *trunc;
+    float *done;
+    double *ep_ret_out;
+    int32_t *ep_len_out;
+};
+
+hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s);
+hipError_t launch_env_step(const EnvDev &E, const StepOut &O, hipStream_t s);
+hipError_t upload_atlas(const uint8_t *atlas_host);
+hipError_t launch_obs_expand_f32(const uint32_t *codes, const int64_t *index, int64_t n, float *out,
+                                 float scale, int layout, hipStream_t s);
+hipError_t launch_obs_expand_u8(const uint32_t *codes, const int64_t *index, int64_t n, uint8_t *out,
+                                hipStream_t s);
+hipError_t launch_gae(const float *rew, const float *val, const float *done, const float *last,
+                      float *adv, float *ret, int T, int N, double gamma, double lam, double *stats,
+                      double *partials, int max_partials, hipStream_t s);
+hipError_t launch_adv_normalize(const float *adv, int64_t n, const double *stats, float *out,
+                                hipStream_t s);
+int gae_partials_needed(int T, int N);
+
+}  // namespace merlin

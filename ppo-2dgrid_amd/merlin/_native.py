@@ -1,0 +1,166 @@
+"""ctypes binding of lib/libmerlin_hip.so (the C ABI in include/merlin_hip.h).
+
+There is no CPU or PyTorch fallback: if the HIP library is missing or fails to
+load, importing anything that needs it raises ``MerlinNativeError`` with the
+build command.  All device-pointer arguments are torch CUDA(HIP) tensors; every
+call is ordered on torch's current stream of the tensor's device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # loads the HIP runtime that libmerlin_hip.so links against (same soname)
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("MERLIN_HIP_LIB", os.path.join(PKG_ROOT, "lib", "libmerlin_hip.so"))
+
+MERLIN_OK = 0
+LAYOUT_NCHW = 0
+LAYOUT_NHWC = 1
+OBS_WORDS = 8
+DEVERR_BAD_ACTION = 1
+DEVERR_PLACE_OBJ = 2
+
+DIFFICULTY_IDS = {"easy": 0, "medium": 1, "mediumhard": 2, "hard": 3, "hardest": 4}
+
+
+class MerlinNativeError(RuntimeError):
+    pass
+
+
+class EnvConfig(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32),
+        ("size", C.c_int32),
+        ("difficulty", C.c_int32),
+        ("max_steps", C.c_int32),
+        ("stuck_penalty", C.c_int32),
+        ("max_stay", C.c_int32),
+        ("penalty", C.c_double),
+        ("exploration_bonus", C.c_int32),
+        ("bonus", C.c_double),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MerlinNativeError(
+            f"HIP library not found at {LIB_PATH}; build it with "
+            f"`make -C {PKG_ROOT}` (hipcc --offload-arch=gfx950)")
+    try:
+        L = C.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the runtime image
+        raise MerlinNativeError(f"failed to load {LIB_PATH}: {e}") from e
+    vp, i32, i64, u64p = C.c_void_p, C.c_int32, C.c_int64, C.POINTER(C.c_uint64)
+    L.merlin_version.restype = C.c_int
+    L.merlin_last_error.restype = C.c_char_p
+    L.merlin_tile_atlas.argtypes = [vp]
+    L.merlin_env_create.argtypes = [C.POINTER(EnvConfig), C.POINTER(vp)]
+    L.merlin_env_destroy.argtypes = [vp]
+    L.merlin_env_seed.argtypes = [vp, u64p, i32, vp]
+    L.merlin_env_reset.argtypes = [vp, vp, vp, vp]
+    L.merlin_env_step.argtypes = [vp, vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, i32, vp]
+    L.merlin_env_get_state.argtypes = [vp, vp, vp, vp, vp]
+    L.merlin_env_errors.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), vp]
+    L.merlin_obs_expand_f32.argtypes = [vp, vp, i64, vp, C.c_float, i32, vp]
+    L.merlin_obs_expand_u8.argtypes = [vp, vp, i64, vp, vp]
+    L.merlin_gae.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, C.c_double, C.c_double, vp, vp]
+    L.merlin_adv_normalize.argtypes = [vp, i64, vp, vp, vp]
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = (
+    "merlin_version", "merlin_last_error", "merlin_tile_atlas", "merlin_env_create",
+    "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step",
+    "merlin_env_get_state", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
+    "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
+)
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != MERLIN_OK:
+        msg = lib().merlin_last_error().decode(errors="replace")
+        raise MerlinNativeError(f"{what or 'merlin call'} failed (code {rc}): {msg}")
+
+
+def ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise MerlinNativeError("merlin HIP kernels need device (cuda/hip) tensors; got a CPU tensor")
+    if not t.is_contiguous():
+        raise MerlinNativeError("merlin HIP kernels need contiguous tensors")
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_of(t: torch.Tensor):
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def tile_atlas():
+    """uint8[5, 8, 8, 3]: the library's own render of minigrid's 5 reachable tiles."""
+    import numpy as np
+
+    a = np.zeros((5, 8, 8, 3), dtype=np.uint8)
+    check(lib().merlin_tile_atlas(a.ctypes.data_as(C.c_void_p)), "merlin_tile_atlas")
+    return a
+
+
+# ---------------------------------------------------------------------------
+# observation expansion / GAE wrappers (device tensors)
+
+def expand_obs(codes: torch.Tensor, index: torch.Tensor | None = None, out: torch.Tensor | None = None,
+               scale: float = 1.0, layout: str = "nchw") -> torch.Tensor:
+    """codes int32[*, 8] -> float32 [n, 3, 56, 56] (nchw) or [n, 56, 56, 3] (nhwc)."""
+    n = int(index.numel()) if index is not None else int(codes.shape[0])
+    lay = LAYOUT_NCHW if layout == "nchw" else LAYOUT_NHWC
+    shape = (n, 3, 56, 56) if lay == LAYOUT_NCHW else (n, 56, 56, 3)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=codes.device)
+    assert out.shape == shape and out.dtype == torch.float32
+    assert codes.dtype == torch.int32 and codes.shape[-1] == OBS_WORDS
+    if index is not None:
+        assert index.dtype == torch.int64
+    check(lib().merlin_obs_expand_f32(ptr(codes), ptr(index), n, ptr(out), float(scale), lay,
+                                      stream_of(codes)), "merlin_obs_expand_f32")
+    return out
+
+
+def expand_obs_u8(codes: torch.Tensor, index: torch.Tensor | None = None) -> torch.Tensor:
+    """codes int32[*, 8] -> uint8 [n, 56, 56, 3]: the RGBImgPartialObsWrapper frame."""
+    n = int(index.numel()) if index is not None else int(codes.shape[0])
+    out = torch.empty((n, 56, 56, 3), dtype=torch.uint8, device=codes.device)
+    check(lib().merlin_obs_expand_u8(ptr(codes), ptr(index), n, ptr(out), stream_of(codes)),
+          "merlin_obs_expand_u8")
+    return out
+
+
+def gae(rewards, values, dones, last_value, gamma, lam, adv=None, ret=None, stats=None):
+    """[T, N] (or [T]) f32 device tensors -> (adv, returns); stats (f64[3]) receives
+    (count, sum, sum of squares) of adv when given."""
+    T = int(rewards.shape[0])
+    N = int(rewards.numel() // T)
+    adv = torch.empty_like(rewards) if adv is None else adv
+    ret = torch.empty_like(rewards) if ret is None else ret
+    last = last_value.reshape(-1).to(torch.float32).contiguous()
+    assert last.numel() == N
+    for t in (rewards, values, dones):
+        assert t.dtype == torch.float32 and t.numel() == T * N
+    check(lib().merlin_gae(ptr(rewards), ptr(values), ptr(dones), ptr(last), ptr(adv), ptr(ret), T, N,
+                           float(gamma), float(lam), ptr(stats), stream_of(rewards)), "merlin_gae")
+    return adv, ret
+
+
+def adv_normalize(adv: torch.Tensor, stats: torch.Tensor, out: torch.Tensor | None = None):
+    out = torch.empty_like(adv) if out is None else out
+    check(lib().merlin_adv_normalize(ptr(adv), int(adv.numel()), ptr(stats), ptr(out), stream_of(adv)),
+          "merlin_adv_normalize")
+    return out

@@ -1,0 +1,246 @@
+"""PPO with the reference's API (src/ppo.py) and a GPU-resident vectorised hot path.
+
+``PPO(env, lr, gamma, lam, clip_eps, update_epochs, batch_size, minibatch_size,
+vf_coef, ent_coef, device)`` with ``collect_rollouts() -> last value``,
+``compute_gae(rewards, values, dones, last_value) -> (adv, returns)``,
+``update(last_value) -> dict(pi_loss, v_loss, entropy, kl, clipfrac, gradnorm)`` and
+``train(total_steps)`` as in src/ppo.py:10-175; ``.ac``, ``.batch_size``,
+``.episode_returns``, ``.episode_lengths`` and ``._obs_to_tensor`` as used by
+ppo/ppo_train.py.
+
+Env kinds:
+  * ``MerlinVecEnv`` (N envs) or ``MerlinEnv`` (N = 1): the vectorised path.  Each
+    iteration steps T = batch_size / N times; per step one HIP observation expansion,
+    one policy forward (PyTorch) and one HIP env-step kernel that writes reward / done /
+    next observation straight into the [T][N] rollout storage.  GAE, the advantage
+    moments and the normalisation are HIP kernels; minibatch observations are
+    re-expanded from the 32-B codes by index (no 37.6 KB/step f32 frame storage).
+  * any other gym-style env: the reference's batch-1 loop with f32 frame storage
+    (src/ppo.py:64-105), GAE / normalisation still on the HIP kernels.
+
+Semantics kept from the reference: the env is reset at the start of every rollout
+(ppo.py:65), done = terminated or truncated with no bootstrap through truncation
+(ppo.py:77,113), returns from the un-normalised advantages (ppo.py:119), unbiased
+std normalisation over the whole batch (ppo.py:125), randperm minibatches over the
+flattened batch (ppo.py:132-134), unclipped value loss, clip_grad_norm_(0.5), Adam.
+Per-minibatch scalars are accumulated on the device and read back once per update
+instead of six .item() syncs per minibatch (ppo.py:158-163).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.optim as optim
+
+from . import _native as nat
+from .actor_critic import CNNActorCritic, MLPActorCritic
+from .distributed import DataParallel
+from .envs import MerlinEnv, MerlinVecEnv
+from .metrics.ppo_metrics import aggregate_ppo_update_metrics
+from .rollout_buffer import CodeRolloutBuffer, RolloutBuffer
+
+INV255 = 1.0 / 255.0
+
+
+class PPO:
+    def __init__(self, env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=10,
+                 batch_size=2048, minibatch_size=256, vf_coef=0.5, ent_coef=0.01, device="cuda",
+                 *, dp: DataParallel | None = None, perm_fn=None):
+        self.env = env
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise nat.MerlinNativeError("merlin.PPO runs its hot path as HIP kernels; pass a GPU device")
+        self.gamma, self.lam, self.clip_eps = gamma, lam, clip_eps
+        self.update_epochs = update_epochs
+        self.minibatch_size = minibatch_size
+        self.vf_coef, self.ent_coef = vf_coef, ent_coef
+        self.dp = dp if dp is not None else DataParallel()
+        self.perm_fn = perm_fn  # tests replay recorded permutations through this hook
+        self.env_step_events = None  # bench.py: list collecting (start, end) HIP events per env-step launch
+        self.episode_returns: list[float] = []
+        self.episode_lengths: list[int] = []
+
+        self.vec = env.vec if isinstance(env, MerlinEnv) else env if isinstance(env, MerlinVecEnv) else None
+        act_dim = env.action_space.n
+        if self.vec is not None:
+            N = self.vec.num_envs
+            if batch_size % N:
+                raise ValueError(f"batch_size {batch_size} must be a multiple of num_envs {N}")
+            self.num_envs, self.k_steps = N, batch_size // N
+            self.batch_size = batch_size
+            self.use_cnn = True
+            self.obs_shape = (56, 56, 3)
+            self.ac = CNNActorCritic(self.obs_shape, act_dim).to(self.device)
+            self.buf = CodeRolloutBuffer(self.k_steps, N, self.device)
+            self._obs_step = torch.empty((N, 3, 56, 56), dtype=torch.float32, device=self.device)
+            self._mb_obs = None
+        else:
+            sample_obs, _ = env.reset()
+            self.num_envs, self.k_steps, self.batch_size = 1, batch_size, batch_size
+            if sample_obs.ndim == 1:
+                self.use_cnn = False
+                self.obs_shape = (int(np.prod(sample_obs.shape)),)
+                self.ac = MLPActorCritic(self.obs_shape[0], act_dim).to(self.device)
+            else:
+                self.use_cnn = True
+                self.obs_shape = sample_obs.shape
+                self.ac = CNNActorCritic(self.obs_shape, act_dim).to(self.device)
+            self.buffer = RolloutBuffer(batch_size, self.obs_shape, self.device, is_discrete=True)
+        self.optimizer = optim.Adam(self.ac.parameters(), lr=lr)
+        self.dp.attach(self.ac)
+        self._params = [p for p in self.ac.parameters() if p.requires_grad]
+
+    # ------------------------------------------------------------------ helpers
+    def _obs_to_tensor(self, state):
+        """ppo.py:58-62: one frame -> f32 [1, ...] on the device."""
+        state_t = torch.as_tensor(np.asarray(state), dtype=torch.float32, device=self.device)
+        return state_t.unsqueeze(0) if self.use_cnn else state_t.view(1, -1)
+
+    def _perm(self, n: int, epoch: int) -> torch.Tensor:
+        if self.perm_fn is not None:
+            return self.perm_fn(n, epoch).to(self.device)
+        return torch.randperm(n, device=self.device)
+
+    # ----------------------------------------------------------------- rollouts
+    def collect_rollouts(self):
+        if self.vec is None:
+            return self._collect_rollouts_single()
+        buf, env = self.buf, self.vec
+        T = buf.T
+        env.reset(out=buf.codes[0])  # ppo.py:65: every rollout starts from a fresh reset
+        obs = self._obs_step
+        with torch.no_grad():
+            for t in range(T):
+                nat.expand_obs(buf.codes[t], out=obs, scale=INV255)
+                action, logp, value = self.ac.act(obs, prescaled=True)
+                buf.actions[t].copy_(action)
+                buf.logprobs[t].copy_(logp)
+                buf.values[t].copy_(value)
+                ev = self.env_step_events
+                if ev is not None:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
+                              buf.ep_return[t], buf.ep_length[t])
+                if ev is not None:
+                    e1.record()
+                    ev.append((e0, e1))
+            nat.expand_obs(buf.codes[T], out=obs, scale=INV255)
+            _, _, last_value = self.ac.act(obs, prescaled=True)
+            buf.last_value.copy_(last_value)
+        self._record_episodes()
+        env.errors()
+        return float(last_value[0].item()) if self.num_envs == 1 else buf.last_value
+
+    def _record_episodes(self):
+        done = self.buf.dones > 0  # finished episodes in (step, env) order
+        rets = self.buf.ep_return[done]
+        lens = self.buf.ep_length[done]
+        self.episode_returns.extend(rets.cpu().tolist())
+        self.episode_lengths.extend(int(x) for x in lens.cpu().tolist())
+
+    def _collect_rollouts_single(self):
+        """Reference loop (ppo.py:64-105) for a generic gym env."""
+        state, _ = self.env.reset()
+        total_steps, ep_return, ep_length = 0, 0.0, 0
+        while total_steps < self.batch_size:
+            state_t = self._obs_to_tensor(state)
+            with torch.no_grad():
+                action, logp, value = self.ac.act(state_t, deterministic=False)
+            next_state, reward, terminated, truncated, _ = self.env.step(action.item())
+            done = terminated or truncated
+            self.buffer.add(state_t.squeeze(0), action.squeeze(), logp.squeeze(), value.squeeze(),
+                            torch.tensor(reward, dtype=torch.float32, device=self.device),
+                            torch.tensor(done, dtype=torch.float32, device=self.device))
+            ep_return += reward
+            ep_length += 1
+            state = next_state
+            total_steps += 1
+            if done:
+                self.episode_returns.append(ep_return)
+                self.episode_lengths.append(ep_length)
+                state, _ = self.env.reset()
+                ep_return, ep_length = 0.0, 0
+        with torch.no_grad():
+            _, _, v = self.ac.act(self._obs_to_tensor(state))
+        return v.item()
+
+    # ---------------------------------------------------------------------- GAE
+    def compute_gae(self, rewards, values, dones, last_value, stats=None):
+        """ppo.py:107-120 on the HIP kernel; [T] or [T, N] device tensors."""
+        lv = torch.as_tensor(last_value, dtype=torch.float32, device=rewards.device).reshape(-1)
+        return nat.gae(rewards.contiguous(), values.contiguous(), dones.contiguous(), lv, self.gamma,
+                       self.lam, stats=stats)
+
+    def _advantages(self, rewards, values, dones, last_value, adv_out=None, ret_out=None):
+        """GAE + whole-batch normalisation (ppo.py:124-125); across ranks the moments are
+        all-reduced first so every rank normalises with the global batch statistics."""
+        stats = torch.zeros(3, dtype=torch.float64, device=rewards.device)
+        lv = torch.as_tensor(last_value, dtype=torch.float32, device=rewards.device).reshape(-1)
+        adv, ret = nat.gae(rewards, values, dones, lv, self.gamma, self.lam, adv=adv_out, ret=ret_out,
+                           stats=stats)
+        self.dp.allreduce_sum_(stats)
+        return nat.adv_normalize(adv, stats), ret
+
+    # ------------------------------------------------------------------- update
+    def update(self, last_value=None):
+        if self.vec is not None:
+            buf = self.buf
+            lv = buf.last_value if last_value is None else last_value
+            adv_n, ret = self._advantages(buf.rewards, buf.values, buf.dones, lv, buf.adv, buf.returns)
+            B = buf.T * buf.N
+            return self._sgd(B, buf.flat_codes, None, buf.actions.reshape(B), buf.logprobs.reshape(B),
+                             adv_n.reshape(B), ret.reshape(B))
+        states, actions, logp_old, rewards, values_old, dones = self.buffer.get()
+        adv_n, ret = self._advantages(rewards, values_old, dones, last_value)
+        return self._sgd(states.shape[0], None, states, actions, logp_old, adv_n, ret)
+
+    def _minibatch_obs(self, codes, states, mb_idx):
+        if codes is None:
+            return states[mb_idx], False
+        n = mb_idx.numel()
+        if self._mb_obs is None or self._mb_obs.shape[0] < n:
+            self._mb_obs = torch.empty((n, 3, 56, 56), dtype=torch.float32, device=self.device)
+        out = self._mb_obs[:n]
+        nat.expand_obs(codes, index=mb_idx, out=out, scale=INV255)
+        return out, True
+
+    def _sgd(self, B, codes, states, actions, logp_old, adv, returns):
+        totals = torch.zeros(6, dtype=torch.float64, device=self.device)
+        nb = 0
+        for epoch in range(self.update_epochs):
+            idxs = self._perm(B, epoch)
+            for start in range(0, B, self.minibatch_size):
+                mb_idx = idxs[start:start + self.minibatch_size]
+                obs, pre = self._minibatch_obs(codes, states, mb_idx)
+                lp_old, a_mb, ret_mb = logp_old[mb_idx], adv[mb_idx], returns[mb_idx]
+                logp_new, entropy, values = self.ac.evaluate(obs, actions[mb_idx], prescaled=pre)
+                values = values.squeeze(-1)
+                ratio = torch.exp(logp_new - lp_old)
+                surr1 = ratio * a_mb
+                surr2 = torch.clamp(ratio, 1 - self.clip_eps, 1 + self.clip_eps) * a_mb
+                pi_loss = -torch.min(surr1, surr2).mean()
+                v_loss = ((values - ret_mb) ** 2).mean()
+                ent = entropy.mean()
+                loss = pi_loss + self.vf_coef * v_loss - self.ent_coef * ent
+                with torch.no_grad():
+                    approx_kl = (lp_old - logp_new).mean()
+                    clipfrac = (torch.abs(ratio - 1.0) > self.clip_eps).float().mean()
+                self.dp.zero_grad(self.optimizer)
+                loss.backward()
+                self.dp.allreduce_grads()
+                grad_norm = torch.nn.utils.clip_grad_norm_(self._params, 0.5)
+                self.optimizer.step()
+                with torch.no_grad():
+                    totals += torch.stack([pi_loss.detach(), v_loss.detach(), ent.detach(), approx_kl,
+                                           clipfrac, grad_norm.detach()]).double()
+                nb += 1
+        t = totals.cpu().tolist()
+        return aggregate_ppo_update_metrics(*t, nb)
+
+    def train(self, total_steps=100_000):
+        steps_done = 0
+        while steps_done < total_steps:
+            last_value = self.collect_rollouts()
+            self.update(last_value)
+            steps_done += self.batch_size
