@@ -40,6 +40,12 @@
  *   merlin_gae           PPO.compute_gae src/ppo.py:107-120
  *                        (== compute_gae_standard src/utils/utils_rl.py:11-29)
  *   merlin_adv_normalize (adv - adv.mean()) / (adv.std() + 1e-8) src/ppo.py:125
+ *   merlin_conv1_lut_*   the first Conv2d(3,32,k8,s4)+ReLU of both CNNFeatureExtractor
+ *                        towers (src/actor_critic.py:9-10,20-21) evaluated from the
+ *                        tile codes, and its weight/bias gradient
+ *   merlin_tower_*       the data-movement stages around the conv2/conv3 GEMMs of the
+ *                        towers (actor_critic.py:11-14): conv1 -> conv2 im2col from codes,
+ *                        conv2 bias+ReLU -> conv3 im2col, and their backward passes
  */
 #ifndef MERLIN_HIP_H
 #define MERLIN_HIP_H
@@ -155,6 +161,41 @@ int merlin_gae(const float *reward_dev, const float *value_dev, const float *don
  * stats_dev = (count, sum, sum of squares); out may alias adv. */
 int merlin_adv_normalize(const float *adv_dev, int64_t n, const double *stats_dev, float *out_dev,
                          void *stream);
+
+/* conv1 from tile codes (both towers at once).  tables_dev: float[towers][32][4][20]
+ * = P[co][slot=(dy,dx)][class*4 + quarter], the conv1 weights contracted with the
+ * /255-scaled atlas (see csrc/merlin_conv1.hip); bias_dev float[towers][32].
+ * out_dev float[towers][n][32][13][13] = relu(conv1(frame_k)) with frame_k the frame
+ * of codes_dev[index_dev ? index_dev[k] : k]. */
+int merlin_conv1_lut_fwd(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
+                         const float *tables_dev, const float *bias_dev, int32_t towers,
+                         float *out_dev, void *stream);
+/* Backward: dz = grad * (act > 0) with act/grad float[towers][n][32][13][13];
+ * writes dtables_dev float[towers][32][4][20] and dbias_dev float[towers][32]
+ * (overwritten, not accumulated). */
+int merlin_conv1_lut_bwd(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
+                         const float *act_dev, const float *grad_dev, int32_t towers,
+                         float *dtables_dev, float *dbias_dev, void *stream);
+
+/* Tower stages (towers = 1 or 2; n frames; K orders are (ky, kx, ci)).
+ * conv2_im2col_fwd: A2[t][k*25 + p2][(ky*4+kx)*32 + ci] = relu(conv1 of frame k)[ci]
+ *   at (2*oy+ky, 2*ox+kx), p2 = oy*5+ox; tables/bias as merlin_conv1_lut_fwd.
+ * conv2_im2col_bwd: dtables/dbias of that map given dA2 (same layout); the ReLU mask
+ *   is recomputed from the tables.
+ * conv3_im2col_fwd: A3[t][k*9 + p3][(ky*3+kx)*64 + ci] = relu(Z2[t][k*25 + (oy+ky)*5
+ *   + ox+kx][ci] + b2[t][ci]), p3 = oy*3+ox.
+ * conv3_col2im_bwd: dZ2 = [Z2 + b2 > 0] * col2im(dA3). */
+int merlin_tower_conv2_im2col_fwd(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
+                                  const float *tables_dev, const float *bias_dev, int32_t towers,
+                                  float *A2_dev, void *stream);
+int merlin_tower_conv2_im2col_bwd(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
+                                  const float *tables_dev, const float *bias_dev,
+                                  const float *dA2_dev, int32_t towers, float *dtables_dev,
+                                  float *dbias_dev, void *stream);
+int merlin_tower_conv3_im2col_fwd(const float *Z2_dev, const float *b2_dev, int64_t n,
+                                  int32_t towers, float *A3_dev, void *stream);
+int merlin_tower_conv3_col2im_bwd(const float *dA3_dev, const float *Z2_dev, const float *b2_dev,
+                                  int64_t n, int32_t towers, float *dZ2_dev, void *stream);
 
 #ifdef __cplusplus
 }

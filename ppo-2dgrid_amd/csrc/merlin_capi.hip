@@ -195,11 +195,14 @@ struct DeviceWs {
     bool ready = false;
     double *partials = nullptr;
     int max_partials = 0;
+    float *conv1_slabs = nullptr;
+    int max_slabs = 0;
 };
 constexpr int MAX_DEV = 64;
 DeviceWs g_dev[MAX_DEV];
 std::mutex g_dev_mu;
 constexpr int WS_PARTIALS = 1 << 16;
+constexpr int WS_SLABS = 1024;  // conv1 backward: per-block partial slabs (1024 x 2 towers x 2592 floats)
 
 int device_ws(DeviceWs **out) {
     int dev = 0;
@@ -212,6 +215,8 @@ int device_ws(DeviceWs **out) {
         HIP_TRY(merlin::upload_atlas(&g_atlas[0][0][0][0]));
         HIP_TRY(hipMalloc(&w.partials, sizeof(double) * 2 * WS_PARTIALS));
         w.max_partials = WS_PARTIALS;
+        HIP_TRY(hipMalloc(&w.conv1_slabs, sizeof(float) * (size_t)WS_SLABS * merlin::conv1_slab_floats(2)));
+        w.max_slabs = WS_SLABS;
         w.ready = true;
     }
     *out = &w;
@@ -460,6 +465,62 @@ int merlin_gae(const float *rew, const float *val, const float *done, const floa
 int merlin_adv_normalize(const float *adv, int64_t n, const double *stats, float *out, void *stream) {
     if (!adv || !stats || !out) return fail(MERLIN_E_INVALID, "null argument");
     HIP_TRY(merlin::launch_adv_normalize(adv, n, stats, out, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_conv1_lut_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
+                         const float *bias, int32_t towers, float *out, void *stream) {
+    if ((!codes || !tables || !bias || !out) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_conv1_lut_fwd(codes, index, n, tables, bias, towers, out, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_conv1_lut_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *act,
+                         const float *grad, int32_t towers, float *dtables, float *dbias, void *stream) {
+    if (!dtables || !dbias || ((!codes || !act || !grad) && n > 0)) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_conv1_lut_bwd(codes, index, n, act, grad, towers, dtables, dbias, ws->conv1_slabs,
+                                         ws->max_slabs, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_conv2_im2col_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
+                                  const float *bias, int32_t towers, float *A2, void *stream) {
+    if ((!codes || !tables || !bias || !A2) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_conv1_im2col_fwd(codes, index, n, tables, bias, towers, A2, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_conv2_im2col_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
+                                  const float *bias, const float *dA2, int32_t towers, float *dtables,
+                                  float *dbias, void *stream) {
+    if (!dtables || !dbias || ((!codes || !tables || !bias || !dA2) && n > 0))
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_conv1_im2col_bwd(codes, index, n, tables, bias, dA2, towers, dtables, dbias,
+                                            ws->conv1_slabs, ws->max_slabs, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_conv3_im2col_fwd(const float *Z2, const float *b2, int64_t n, int32_t towers, float *A3,
+                                  void *stream) {
+    if ((!Z2 || !b2 || !A3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    HIP_TRY(merlin::launch_im2col3_fwd(Z2, b2, n, towers, A3, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_conv3_col2im_bwd(const float *dA3, const float *Z2, const float *b2, int64_t n, int32_t towers,
+                                  float *dZ2, void *stream) {
+    if ((!dA3 || !Z2 || !b2 || !dZ2) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    HIP_TRY(merlin::launch_col2im3_bwd(dA3, Z2, b2, n, towers, dZ2, (hipStream_t)stream));
     return MERLIN_OK;
 }
 

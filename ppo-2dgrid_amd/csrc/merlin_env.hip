@@ -356,12 +356,37 @@ struct Grid {
     }
 };
 
+// Map generation runs only on reset: keep it out of line so the step loop's state stays
+// in registers (the generator's Grid object lives in its own frame).
+struct GenOut {
+    int ax, ay, dir, gx, gy;
+    uint32_t err;
+};
+
+template <int SP>
+__device__ __noinline__ void generate_map(uint32_t (*rows)[BLK], int lane, int S, int difficulty, Rng &r,
+                                          uint32_t *fallbacks, GenOut &o) {
+    Grid<SP> G;
+    G.rows = rows;
+    G.lane = lane;
+    G.S = S;
+    G.err = 0u;
+    G.generate(r, difficulty, fallbacks);
+    o.ax = G.ax;
+    o.ay = G.ay;
+    o.dir = G.dir;
+    o.gx = G.gx;
+    o.gy = G.gy;
+    o.err = G.err;
+}
+
 __device__ __forceinline__ uint32_t bitrev7(uint32_t v) { return __brev(v) >> 25; }
 
 // gen_obs_grid + get_pov_render tile classes -> 8 packed nibble words.
 template <int SP>
-__device__ __forceinline__ void view_codes(const Grid<SP> &G, uint32_t out[MERLIN_OBS_WORDS]) {
-    const int S = G.S, ax = G.ax, ay = G.ay, dir = G.dir;
+__device__ __forceinline__ void view_codes(const uint32_t (*rows)[BLK], int lane, int S, int ax, int ay, int dir,
+                                           int goal_x, int goal_y, bool goal_set,
+                                           uint32_t out[MERLIN_OBS_WORDS]) {
     // get_view_exts (top-left of the 7x7 world window)
     int tx, ty;
     if (dir == 0) {
@@ -384,7 +409,7 @@ __device__ __forceinline__ void view_codes(const Grid<SP> &G, uint32_t out[MERLI
     for (int r = 0; r < 7; r++) {
         const int y = ty + r;
         const bool in = (y >= 0) && (y < S);
-        const uint32_t row = in ? G.row(in ? y : 0) : 0xffffffffu;
+        const uint32_t row = in ? rows[in ? y : 0][lane] : 0xffffffffu;
         const uint64_t w = ((uint64_t)row << 8) | 0xffULL | hi_ones;
         win[r] = (uint32_t)(w >> (tx + 8)) & 0x7fu;  // bit c = cell (c, r) of the slice
     }
@@ -408,9 +433,9 @@ __device__ __forceinline__ void view_codes(const Grid<SP> &G, uint32_t out[MERLI
     // goal position in view: view(vi,vj) <- world(agent + (6-vj)*F + (vi-3)*R)
     const int Fx = (dir == 0) - (dir == 2), Fy = (dir == 1) - (dir == 3);
     const int Rx = -Fy, Ry = Fx;  // DIR_TO_VEC[(dir+1)%4]
-    const int dx = G.gx - ax, dy = G.gy - ay;
+    const int dx = goal_x - ax, dy = goal_y - ay;
     const int gvj = 6 - (dx * Fx + dy * Fy), gvi = 3 + (dx * Rx + dy * Ry);
-    const bool ginv = G.goal_set && gvi >= 0 && gvi < 7 && gvj >= 0 && gvj < 7;
+    const bool ginv = goal_set && gvi >= 0 && gvi < 7 && gvj >= 0 && gvj < 7;
     // Grid.process_vis(agent_pos=(3,6)) as row bit-ops (walls opaque, goal/empty transparent)
     uint32_t m[7] = {0u, 0u, 0u, 0u, 0u, 0u, 1u << 3};
 #pragma unroll
@@ -448,26 +473,26 @@ __device__ __forceinline__ void view_codes(const Grid<SP> &G, uint32_t out[MERLI
 }
 
 template <int SP>
-__device__ __forceinline__ void load_rows(const EnvDev &E, int i, Grid<SP> &G) {
+__device__ __forceinline__ void load_rows(const EnvDev &E, int i, uint32_t (*rows)[BLK], int lane) {
     const uint4 *src = reinterpret_cast<const uint4 *>(E.walls + (size_t)i * SP);
 #pragma unroll
     for (int q = 0; q < SP / 4; q++) {
         const uint4 v = src[q];
-        G.set_row(4 * q + 0, v.x);
-        G.set_row(4 * q + 1, v.y);
-        G.set_row(4 * q + 2, v.z);
-        G.set_row(4 * q + 3, v.w);
+        rows[4 * q + 0][lane] = v.x;
+        rows[4 * q + 1][lane] = v.y;
+        rows[4 * q + 2][lane] = v.z;
+        rows[4 * q + 3][lane] = v.w;
     }
 }
 
 template <int SP>
-__device__ __forceinline__ void store_rows(const EnvDev &E, int i, const Grid<SP> &G) {
+__device__ __forceinline__ void store_rows(const EnvDev &E, int i, const uint32_t (*rows)[BLK], int lane, int S) {
     uint4 *dst = reinterpret_cast<uint4 *>(E.walls + (size_t)i * SP);
 #pragma unroll
     for (int q = 0; q < SP / 4; q++) {
         const int y = 4 * q;
-        dst[q] = make_uint4(y + 0 < G.S ? G.row(y + 0) : 0u, y + 1 < G.S ? G.row(y + 1) : 0u,
-                            y + 2 < G.S ? G.row(y + 2) : 0u, y + 3 < G.S ? G.row(y + 3) : 0u);
+        dst[q] = make_uint4(y + 0 < S ? rows[y + 0][lane] : 0u, y + 1 < S ? rows[y + 1][lane] : 0u,
+                            y + 2 < S ? rows[y + 2][lane] : 0u, y + 3 < S ? rows[y + 3][lane] : 0u);
     }
 }
 
@@ -486,13 +511,9 @@ __device__ __forceinline__ uint4 pack_agent(int ax, int ay, int dir, int steps, 
 
 // Post-reset bookkeeping shared by the reset kernel and the auto-reset path.
 template <int SP>
-__device__ __forceinline__ void on_reset(const EnvDev &E, int i, const Grid<SP> &G) {
-    E.ep_ret[i] = 0.0;
-    E.ep_len[i] = 0;
-    if (E.explore_on) {
-        uint32_t *vis = E.visited + (size_t)i * SP;
-        for (int y = 0; y < SP; y++) vis[y] = (y == G.ay) ? (1u << G.ax) : 0u;
-    }
+__device__ __forceinline__ void reset_visited(const EnvDev &E, int i, int ax, int ay) {
+    uint32_t *vis = E.visited + (size_t)i * SP;
+    for (int y = 0; y < SP; y++) vis[y] = (y == ay) ? (1u << ax) : 0u;
 }
 
 template <int SP>
@@ -503,20 +524,18 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
     const int i = blockIdx.x * BLK + lane;
     if (i >= E.n) return;
     if (mask && !mask[i]) return;
-    Grid<SP> G;
-    G.rows = rows;
-    G.lane = lane;
-    G.S = E.size;
-    G.err = 0u;
     Rng r = load_rng(E, i);
-    G.generate(r, E.difficulty, E.err + 1);
+    GenOut g;
+    generate_map<SP>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
     store_rng(E, i, r);
-    store_rows(E, i, G);
-    E.agent[i] = pack_agent(G.ax, G.ay, G.dir, 0, G.gx, G.gy, G.ax, G.ay, 0);
-    on_reset(E, i, G);
-    if (G.err) atomicOr(E.err, G.err);
+    store_rows<SP>(E, i, rows, lane, E.size);
+    E.agent[i] = pack_agent(g.ax, g.ay, g.dir, 0, g.gx, g.gy, g.ax, g.ay, 0);
+    E.ep_ret[i] = 0.0;
+    E.ep_len[i] = 0;
+    if (E.explore_on) reset_visited<SP>(E, i, g.ax, g.ay);
+    if (g.err) atomicOr(E.err, g.err);
     uint32_t w[MERLIN_OBS_WORDS];
-    view_codes(G, w);
+    view_codes<SP>(rows, lane, E.size, g.ax, g.ay, g.dir, g.gx, g.gy, true, w);
     if (obs) store_obs(obs, (size_t)i, w);
 }
 
@@ -526,23 +545,16 @@ __global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
     const int lane = threadIdx.x;
     const int i = blockIdx.x * BLK + lane;
     if (i >= E.n) return;
-    Grid<SP> G;
-    G.rows = rows;
-    G.lane = lane;
-    G.S = E.size;
-    G.err = 0u;
-    G.goal_set = true;
-    load_rows(E, i, G);
+    const int S = E.size;
+    load_rows<SP>(E, i, rows, lane);
     const uint4 st = E.agent[i];
-    G.ax = st.x & 0xff;
-    G.ay = (st.x >> 8) & 0xff;
-    G.dir = (st.x >> 16) & 3;
+    int ax = st.x & 0xff, ay = (st.x >> 8) & 0xff, dir = (st.x >> 16) & 3;
     int steps = (int)st.y;
-    G.gx = st.z & 0xff;
-    G.gy = (st.z >> 8) & 0xff;
+    int gx = st.z & 0xff, gy = (st.z >> 8) & 0xff;
     int lx = st.w & 0xff, ly = (st.w >> 8) & 0xff, stay = (int)(st.w >> 16);
     double ep_ret = E.ep_ret[i];
     int ep_len = E.ep_len[i];
+    uint32_t err = 0u;
     bool rows_dirty = false, rng_loaded = false;
     Rng r;
     const size_t N = (size_t)E.n;
@@ -550,38 +562,38 @@ __global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
     for (int t = 0; t < O.n_steps; t++) {
         const int64_t a = O.actions[(size_t)t * O.action_stride + i];
         steps += 1;
-        const int fx = G.ax + ((G.dir == 0) - (G.dir == 2));
-        const int fy = G.ay + ((G.dir == 1) - (G.dir == 3));
-        const bool fwall = G.wall(fx, fy);
-        const bool fgoal = (fx == G.gx) && (fy == G.gy);
+        const int fx = ax + ((dir == 0) - (dir == 2));
+        const int fy = ay + ((dir == 1) - (dir == 3));
+        const bool fwall = (rows[fy][lane] >> fx) & 1u;
+        const bool fgoal = (fx == gx) && (fy == gy);
         double rew = 0.0;
         bool term = false;
         if (a == 0) {
-            G.dir = (G.dir + 3) & 3;
+            dir = (dir + 3) & 3;
         } else if (a == 1) {
-            G.dir = (G.dir + 1) & 3;
+            dir = (dir + 1) & 3;
         } else if (a == 2) {
             if (!fwall) {  // None or Goal (can_overlap)
-                G.ax = fx;
-                G.ay = fy;
+                ax = fx;
+                ay = fy;
             }
             if (fgoal) {
                 term = true;
                 rew = 1.0 - 0.9 * ((double)steps / (double)E.max_steps);  // MiniGridEnv._reward
             }
         } else {
-            G.err |= MERLIN_DEVERR_BAD_ACTION;
+            err |= MERLIN_DEVERR_BAD_ACTION;
         }
         const bool trunc = steps >= E.max_steps;
         if (E.stuck_on) {  // StuckPenaltyWrapper.step
-            stay = (G.ax == lx && G.ay == ly) ? stay + 1 : 0;
+            stay = (ax == lx && ay == ly) ? stay + 1 : 0;
             if (stay >= E.max_stay) rew += E.penalty;
-            lx = G.ax;
-            ly = G.ay;
+            lx = ax;
+            ly = ay;
         }
         if (E.explore_on) {  // ExplorationBonus (MERLIN-AMD definition; absent in the reference)
-            uint32_t *vrow = E.visited + (size_t)i * SP + G.ay;
-            const uint32_t bit = 1u << G.ax, v = *vrow;
+            uint32_t *vrow = E.visited + (size_t)i * SP + ay;
+            const uint32_t bit = 1u << ax, v = *vrow;
             if (!(v & bit)) {
                 *vrow = v | bit;
                 rew += E.bonus;
@@ -604,31 +616,35 @@ __global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
                 r = load_rng(E, i);
                 rng_loaded = true;
             }
-            G.generate(r, E.difficulty, E.err + 1);
+            GenOut g;
+            generate_map<SP>(rows, lane, S, E.difficulty, r, E.err + 1, g);
+            ax = g.ax;
+            ay = g.ay;
+            dir = g.dir;
+            gx = g.gx;
+            gy = g.gy;
+            err |= g.err;
             rows_dirty = true;
             steps = 0;
             stay = 0;
-            lx = G.ax;
-            ly = G.ay;
+            lx = ax;
+            ly = ay;
             ep_ret = 0.0;
             ep_len = 0;
-            if (E.explore_on) {
-                uint32_t *vis = E.visited + (size_t)i * SP;
-                for (int y = 0; y < SP; y++) vis[y] = (y == G.ay) ? (1u << G.ax) : 0u;
-            }
+            if (E.explore_on) reset_visited<SP>(E, i, ax, ay);
         }
         if (O.obs) {
             uint32_t w[MERLIN_OBS_WORDS];
-            view_codes(G, w);
+            view_codes<SP>(rows, lane, S, ax, ay, dir, gx, gy, true, w);
             store_obs(O.obs, row, w);
         }
     }
-    E.agent[i] = pack_agent(G.ax, G.ay, G.dir, steps, G.gx, G.gy, lx, ly, stay);
+    E.agent[i] = pack_agent(ax, ay, dir, steps, gx, gy, lx, ly, stay);
     E.ep_ret[i] = ep_ret;
     E.ep_len[i] = ep_len;
-    if (rows_dirty) store_rows(E, i, G);
+    if (rows_dirty) store_rows<SP>(E, i, rows, lane, S);
     if (rng_loaded) store_rng(E, i, r);
-    if (G.err) atomicOr(E.err, G.err);
+    if (err) atomicOr(E.err, err);
 }
 
 }  // namespace

@@ -64,5 +64,19 @@ hipError_t launch_gae(const float *rew, const float *val, const float *done, con
 hipError_t launch_adv_normalize(const float *adv, int64_t n, const double *stats, float *out,
                                 hipStream_t s);
 int gae_partials_needed(int T, int N);
+int conv1_slab_floats(int towers);
+hipError_t launch_conv1_lut_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
+                                const float *bias, int towers, float *out, hipStream_t s);
+hipError_t launch_conv1_lut_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *act,
+                                const float *grad, int towers, float *dtables, float *dbias, float *slabs,
+                                int max_slabs, hipStream_t s);
+hipError_t launch_conv1_im2col_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
+                                   const float *bias, int T, float *A2, hipStream_t s);
+hipError_t launch_conv1_im2col_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
+                                   const float *bias, const float *dA2, int T, float *dtables, float *dbias,
+                                   float *slabs, int max_slabs, hipStream_t s);
+hipError_t launch_im2col3_fwd(const float *Z2, const float *b2, int64_t n, int T, float *A3, hipStream_t s);
+hipError_t launch_col2im3_bwd(const float *dA3, const float *Z2, const float *b2, int64_t n, int T, float *dZ2,
+                              hipStream_t s);
 
 }  // namespace merlin

@@ -73,6 +73,12 @@ def lib():
     L.merlin_obs_expand_u8.argtypes = [vp, vp, i64, vp, vp]
     L.merlin_gae.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, C.c_double, C.c_double, vp, vp]
     L.merlin_adv_normalize.argtypes = [vp, i64, vp, vp, vp]
+    L.merlin_conv1_lut_fwd.argtypes = [vp, vp, i64, vp, vp, i32, vp, vp]
+    L.merlin_conv1_lut_bwd.argtypes = [vp, vp, i64, vp, vp, i32, vp, vp, vp]
+    L.merlin_tower_conv2_im2col_fwd.argtypes = [vp, vp, i64, vp, vp, i32, vp, vp]
+    L.merlin_tower_conv2_im2col_bwd.argtypes = [vp, vp, i64, vp, vp, vp, i32, vp, vp, vp]
+    L.merlin_tower_conv3_im2col_fwd.argtypes = [vp, vp, i64, i32, vp, vp]
+    L.merlin_tower_conv3_col2im_bwd.argtypes = [vp, vp, vp, i64, i32, vp, vp]
     _lib = L
     return L
 
@@ -82,6 +88,8 @@ EXPORTED_SYMBOLS = (
     "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step",
     "merlin_env_get_state", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
     "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
+    "merlin_conv1_lut_fwd", "merlin_conv1_lut_bwd", "merlin_tower_conv2_im2col_fwd",
+    "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
 )
 
 
@@ -163,4 +171,69 @@ def adv_normalize(adv: torch.Tensor, stats: torch.Tensor, out: torch.Tensor | No
     out = torch.empty_like(adv) if out is None else out
     check(lib().merlin_adv_normalize(ptr(adv), int(adv.numel()), ptr(stats), ptr(out), stream_of(adv)),
           "merlin_adv_normalize")
+    return out
+
+
+def conv1_lut_fwd(codes: torch.Tensor, index: torch.Tensor | None, tables: torch.Tensor, bias: torch.Tensor,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """relu(conv1(frame)) of each tower from tile codes: tables f32[T, 32, 4, 20], bias f32[T, 32]
+    -> f32[T, n, 32, 13, 13]."""
+    T = int(tables.shape[0])
+    n = int(index.numel()) if index is not None else int(codes.shape[0])
+    if out is None:
+        out = torch.empty((T, n, 32, 13, 13), dtype=torch.float32, device=codes.device)
+    assert tables.shape == (T, 32, 4, 20) and bias.shape == (T, 32) and out.shape == (T, n, 32, 13, 13)
+    check(lib().merlin_conv1_lut_fwd(ptr(codes), ptr(index), n, ptr(tables), ptr(bias), T, ptr(out),
+                                     stream_of(codes)), "merlin_conv1_lut_fwd")
+    return out
+
+
+def conv1_lut_bwd(codes: torch.Tensor, index: torch.Tensor | None, act: torch.Tensor, grad: torch.Tensor):
+    """(dtables f32[T, 32, 4, 20], dbias f32[T, 32]) for dz = grad * (act > 0)."""
+    T = int(act.shape[0])
+    n = int(act.shape[1])
+    dt = torch.empty((T, 32, 4, 20), dtype=torch.float32, device=act.device)
+    db = torch.empty((T, 32), dtype=torch.float32, device=act.device)
+    check(lib().merlin_conv1_lut_bwd(ptr(codes), ptr(index), n, ptr(act), ptr(grad), T, ptr(dt), ptr(db),
+                                     stream_of(act)), "merlin_conv1_lut_bwd")
+    return dt, db
+
+
+# -- tower stages around the conv2 / conv3 GEMMs -------------------------------------------
+def conv2_im2col_fwd(codes, index, tables, bias):
+    """-> A2 f32[T, n*25, 512]: conv2's im2col rows of relu(conv1) built from tile codes."""
+    T = int(tables.shape[0])
+    n = int(index.numel()) if index is not None else int(codes.shape[0])
+    out = torch.empty((T, n * 25, 512), dtype=torch.float32, device=codes.device)
+    check(lib().merlin_tower_conv2_im2col_fwd(ptr(codes), ptr(index), n, ptr(tables), ptr(bias), T, ptr(out),
+                                              stream_of(codes)), "merlin_tower_conv2_im2col_fwd")
+    return out
+
+
+def conv2_im2col_bwd(codes, index, tables, bias, dA2):
+    T = int(tables.shape[0])
+    n = int(dA2.shape[1]) // 25
+    dt = torch.empty((T, 32, 4, 20), dtype=torch.float32, device=dA2.device)
+    db = torch.empty((T, 32), dtype=torch.float32, device=dA2.device)
+    check(lib().merlin_tower_conv2_im2col_bwd(ptr(codes), ptr(index), n, ptr(tables), ptr(bias), ptr(dA2), T,
+                                              ptr(dt), ptr(db), stream_of(dA2)), "merlin_tower_conv2_im2col_bwd")
+    return dt, db
+
+
+def conv3_im2col_fwd(Z2, b2):
+    """Z2 f32[T, n*25, 64], b2 f32[T, 64] -> A3 f32[T, n*9, 576] (bias + ReLU fused)."""
+    T = int(Z2.shape[0])
+    n = int(Z2.shape[1]) // 25
+    out = torch.empty((T, n * 9, 576), dtype=torch.float32, device=Z2.device)
+    check(lib().merlin_tower_conv3_im2col_fwd(ptr(Z2), ptr(b2), n, T, ptr(out), stream_of(Z2)),
+          "merlin_tower_conv3_im2col_fwd")
+    return out
+
+
+def conv3_col2im_bwd(dA3, Z2, b2):
+    T = int(Z2.shape[0])
+    n = int(Z2.shape[1]) // 25
+    out = torch.empty_like(Z2)
+    check(lib().merlin_tower_conv3_col2im_bwd(ptr(dA3), ptr(Z2), ptr(b2), n, T, ptr(out), stream_of(Z2)),
+          "merlin_tower_conv3_col2im_bwd")
     return out

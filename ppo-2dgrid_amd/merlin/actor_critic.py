@@ -19,6 +19,14 @@ and update never materialise an extra scaled copy of the observation batch.
 The categorical head is computed directly with log_softmax instead of building a
 torch.distributions.Categorical per call (same formulas: log-prob of the
 normalised logits, entropy = -sum p*log p).
+
+``act_codes`` / ``evaluate_codes`` take the packed 7x7 tile codes of the GPU envs
+instead of frames.  Every frame is a blit of 5 atlas tiles, so each tower's first
+Conv2d(3,32,k8,s4) equals bias + a sum of 4 entries of a [32][4 slots][20] table P
+(W1 contracted with the /255-scaled atlas); P is formed here with an einsum (autograd
+turns dP into dW1) and the lookups / their transposed histogram run in the HIP library
+(merlin_conv1_lut_fwd/bwd, csrc/merlin_conv1.hip).  Same function, fp32 sums in a
+different order; conv2..heads are the reference modules unchanged.
 """
 from __future__ import annotations
 
@@ -71,6 +79,69 @@ def _entropy(logp_all: torch.Tensor, probs: torch.Tensor) -> torch.Tensor:
     return -(lp * probs).sum(-1)
 
 
+class _Conv1FromCodes(torch.autograd.Function):
+    """relu(conv1) of both towers from tile codes (HIP lookup / histogram kernels)."""
+
+    @staticmethod
+    def forward(ctx, tables, bias, codes, index):
+        from . import _native as nat
+
+        a1 = nat.conv1_lut_fwd(codes, index, tables.detach().contiguous(), bias.detach().contiguous())
+        ctx.save_for_backward(a1, codes, index if index is not None else codes.new_empty(0))
+        ctx.has_index = index is not None
+        return a1
+
+    @staticmethod
+    def backward(ctx, grad):
+        from . import _native as nat
+
+        a1, codes, index = ctx.saved_tensors
+        dt, db = nat.conv1_lut_bwd(codes, index if ctx.has_index else None, a1, grad.contiguous())
+        return dt, db, None, None
+
+
+class _Conv2Im2colFromCodes(torch.autograd.Function):
+    """A2 = im2col(relu(conv1(frames))) of both towers, straight from tile codes."""
+
+    @staticmethod
+    def forward(ctx, tables, bias, codes, index):
+        from . import _native as nat
+
+        t, b = tables.detach().contiguous(), bias.detach().contiguous()
+        A2 = nat.conv2_im2col_fwd(codes, index, t, b)
+        ctx.save_for_backward(t, b, codes, index if index is not None else codes.new_empty(0))
+        ctx.has_index = index is not None
+        return A2
+
+    @staticmethod
+    def backward(ctx, dA2):
+        from . import _native as nat
+
+        t, b, codes, index = ctx.saved_tensors
+        dt, db = nat.conv2_im2col_bwd(codes, index if ctx.has_index else None, t, b, dA2.contiguous())
+        return dt, db, None, None
+
+
+class _Conv3Im2col(torch.autograd.Function):
+    """A3 = im2col(relu(Z2 + b2)) of both towers (conv2's bias + ReLU fused)."""
+
+    @staticmethod
+    def forward(ctx, Z2, b2):
+        from . import _native as nat
+
+        Z2, b2 = Z2.contiguous(), b2.detach().contiguous()
+        ctx.save_for_backward(Z2, b2)
+        return nat.conv3_im2col_fwd(Z2, b2)
+
+    @staticmethod
+    def backward(ctx, dA3):
+        from . import _native as nat
+
+        Z2, b2 = ctx.saved_tensors
+        dZ2 = nat.conv3_col2im_bwd(dA3.contiguous(), Z2, b2)
+        return dZ2, dZ2.sum(dim=1)
+
+
 class CNNActorCritic(nn.Module):
     def __init__(self, obs_shape, act_dim, hidden_dim=512):
         super().__init__()
@@ -79,6 +150,69 @@ class CNNActorCritic(nn.Module):
         self.critic_extractor = CNNFeatureExtractor(c, h, w)
         self.actor = _head(self.actor_extractor.output_dim, hidden_dim, act_dim, 0.01)
         self.critic = _head(self.critic_extractor.output_dim, hidden_dim, 1, 1.0)
+        self._atlas = None  # f32 [5, 3, 8, 8] / 255 on the model's device (codes path only)
+        self.codes_impl = "gemm"  # "gemm" (tower as hipBLASLt GEMMs) | "lut_nchw" (conv1 LUT + MIOpen convs)
+
+    # -- tile-code path (GPU envs) --------------------------------------------------
+    def _atlas_on(self, device):
+        if self._atlas is None or self._atlas.device != device:
+            from . import _native as nat
+
+            a = torch.from_numpy(nat.tile_atlas()).permute(0, 3, 1, 2).float() / 255.0
+            self._atlas = a.contiguous().to(device)
+        return self._atlas
+
+    def conv1_tables(self):
+        """P[t][co][slot][bin] (t: actor, critic; slot = 2*dy + dx; bin = 4*class + 2*qy + qx)."""
+        c1a, c1c = self.actor_extractor.network[0], self.critic_extractor.network[0]
+        W = torch.stack([c1a.weight, c1c.weight]).view(2, 32, 3, 2, 4, 2, 4)  # t o c dy ky dx kx
+        A = self._atlas_on(c1a.weight.device).view(5, 3, 2, 4, 2, 4)  # cls c qy ky qx kx
+        P = torch.einsum("tocakbl,zcekfl->toabzef", W, A)
+        return P.reshape(2, 32, 4, 20), torch.stack([c1a.bias, c1c.bias])
+
+    def _forward_codes(self, codes, index=None):
+        """Both towers from tile codes as GEMMs (csrc/merlin_tower.hip for the data movement):
+        A2 = im2col(relu(conv1)) -> Z2 = A2 @ W2t -> A3 = im2col(relu(Z2 + b2)) ->
+        relu(A3 @ W3t + b3) -> fc1 (columns permuted to the (position, channel) row order)
+        -> heads.  The GEMMs are batched over the two towers (hipBLASLt fp32)."""
+        if self.codes_impl == "lut_nchw":
+            return self._forward_codes_nchw(codes, index)
+        ea, ec = self.actor_extractor.network, self.critic_extractor.network
+        n = index.numel() if index is not None else codes.shape[0]
+        tables, b1 = self.conv1_tables()
+        A2 = _Conv2Im2colFromCodes.apply(tables, b1, codes, index)  # [2, n*25, 512]
+        W2t = torch.stack([ea[2].weight, ec[2].weight]).permute(0, 3, 4, 2, 1).reshape(2, 512, 64)
+        Z2 = torch.bmm(A2, W2t)  # [2, n*25, 64]
+        A3 = _Conv3Im2col.apply(Z2, torch.stack([ea[2].bias, ec[2].bias]))  # [2, n*9, 576]
+        W3t = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64)
+        b3 = torch.stack([ea[4].bias, ec[4].bias]).unsqueeze(1)
+        a3 = torch.relu(torch.baddbmm(b3, A3, W3t)).view(2, n, 576)  # rows (p3, co)
+        fa, fc = self.actor[0], self.critic[0]
+        W4 = torch.stack([fa.weight, fc.weight])  # [2, hidden, 576] in (co, p3) order
+        W4p = W4.view(2, W4.shape[1], 64, 9).transpose(2, 3).reshape(2, W4.shape[1], 576)
+        h = torch.relu(torch.baddbmm(torch.stack([fa.bias, fc.bias]).unsqueeze(1), a3, W4p.transpose(1, 2)))
+        logits = F.linear(h[0], self.actor[2].weight, self.actor[2].bias)
+        value = F.linear(h[1], self.critic[2].weight, self.critic[2].bias).squeeze(-1)
+        return logits, value
+
+    def _forward_codes_nchw(self, codes, index=None):
+        tables, bias = self.conv1_tables()
+        a1 = _Conv1FromCodes.apply(tables, bias, codes, index)
+        fa = self.actor_extractor.network[2:](a1[0])
+        fc = self.critic_extractor.network[2:](a1[1])
+        return self.actor(fa), self.critic(fc).squeeze(-1)
+
+    def act_codes(self, codes, deterministic=False, index=None):
+        logits, value = self._forward_codes(codes, index)
+        logp_all, probs = _categorical(logits)
+        action = _sample_or_argmax(logits, logp_all, probs, deterministic)
+        return action, logp_all.gather(-1, action.unsqueeze(-1)).squeeze(-1), value
+
+    def evaluate_codes(self, codes, actions, index=None):
+        logits, value = self._forward_codes(codes, index)
+        logp_all, probs = _categorical(logits)
+        logp = logp_all.gather(-1, actions.long().unsqueeze(-1)).squeeze(-1)
+        return logp, _entropy(logp_all, probs), value
 
     def _format_obs(self, x):
         # NHWC observations (the gym frame layout) -> NCHW for the convs

@@ -45,7 +45,7 @@ INV255 = 1.0 / 255.0
 class PPO:
     def __init__(self, env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=10,
                  batch_size=2048, minibatch_size=256, vf_coef=0.5, ent_coef=0.01, device="cuda",
-                 *, dp: DataParallel | None = None, perm_fn=None):
+                 *, dp: DataParallel | None = None, perm_fn=None, conv1_from_codes: bool = True):
         self.env = env
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -57,6 +57,9 @@ class PPO:
         self.dp = dp if dp is not None else DataParallel()
         self.perm_fn = perm_fn  # tests replay recorded permutations through this hook
         self.env_step_events = None  # bench.py: list collecting (start, end) HIP events per env-step launch
+        # vectorised path: evaluate conv1 from the tile codes (merlin_conv1_lut_*) instead of
+        # expanding 37.6 KB frames and running the generic convolution
+        self.conv1_from_codes = conv1_from_codes
         self.episode_returns: list[float] = []
         self.episode_lengths: list[int] = []
 
@@ -111,8 +114,7 @@ class PPO:
         obs = self._obs_step
         with torch.no_grad():
             for t in range(T):
-                nat.expand_obs(buf.codes[t], out=obs, scale=INV255)
-                action, logp, value = self.ac.act(obs, prescaled=True)
+                action, logp, value = self._act(buf.codes[t], obs)
                 buf.actions[t].copy_(action)
                 buf.logprobs[t].copy_(logp)
                 buf.values[t].copy_(value)
@@ -125,12 +127,17 @@ class PPO:
                 if ev is not None:
                     e1.record()
                     ev.append((e0, e1))
-            nat.expand_obs(buf.codes[T], out=obs, scale=INV255)
-            _, _, last_value = self.ac.act(obs, prescaled=True)
+            _, _, last_value = self._act(buf.codes[T], obs)
             buf.last_value.copy_(last_value)
         self._record_episodes()
         env.errors()
         return float(last_value[0].item()) if self.num_envs == 1 else buf.last_value
+
+    def _act(self, codes, obs_scratch):
+        if self.conv1_from_codes:
+            return self.ac.act_codes(codes)
+        nat.expand_obs(codes, out=obs_scratch, scale=INV255)
+        return self.ac.act(obs_scratch, prescaled=True)
 
     def _record_episodes(self):
         done = self.buf.dones > 0  # finished episodes in (step, env) order
@@ -212,9 +219,12 @@ class PPO:
             idxs = self._perm(B, epoch)
             for start in range(0, B, self.minibatch_size):
                 mb_idx = idxs[start:start + self.minibatch_size]
-                obs, pre = self._minibatch_obs(codes, states, mb_idx)
                 lp_old, a_mb, ret_mb = logp_old[mb_idx], adv[mb_idx], returns[mb_idx]
-                logp_new, entropy, values = self.ac.evaluate(obs, actions[mb_idx], prescaled=pre)
+                if codes is not None and self.conv1_from_codes:
+                    logp_new, entropy, values = self.ac.evaluate_codes(codes, actions[mb_idx], index=mb_idx)
+                else:
+                    obs, pre = self._minibatch_obs(codes, states, mb_idx)
+                    logp_new, entropy, values = self.ac.evaluate(obs, actions[mb_idx], prescaled=pre)
                 values = values.squeeze(-1)
                 ratio = torch.exp(logp_new - lp_old)
                 surr1 = ratio * a_mb
