@@ -32,10 +32,9 @@ sys.path.insert(0, os.path.join(REPO, "ppo-2dgrid_amd"))
 os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 os.environ.setdefault("MIOPEN_LOG_LEVEL", "3")
 
-# Algorithmic work per unit:
-#   k_env_step, per env-step: action 8 + agent state r/w 32 + wall rows 64 + episode
-#   accumulators r/w 24 + obs codes 32 + reward 4 + done 4  = 168 B
-ENV_STEP_BYTES = 168
+# Algorithmic work per unit: each hand-written kernel's bytes per launch are
+# recorded by merlin._native.KernelTimer next to its HIP events (k_env_step: 168 B per
+# env-step; k_conv1_im2col_fwd/bwd: 102,400 B + 40 B per frame; ...);
 #   full iteration, per env-step: rollout forward of both towers 9.94 MFLOP
 #   + 10 epochs x fwd+bwd 25.67 MFLOP (conv1 needs no input gradient)
 FWD_MACS = 2 * (1_038_336 + 819_200 + 331_776 + 294_912) + 512 * 3 + 512
@@ -108,16 +107,40 @@ def cpu_baseline():
                       "render), batch 2048, 10 epochs x 8 minibatches of 256, fp32 torch CNN (cfg 1 shape)"}
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of k_env_step from the committed rocprofv3 --pmc pass
-    (profiles/*env_step_pmc*.json, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*env_step_pmc*.json")))
-    if not files:
-        return None
-    try:
-        return json.load(open(files[-1])).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+def pmc_traffic(kernel: str):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 --pmc passes
+    (profiles/*_pmc.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE)."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(f)).get(kernel)
+        except Exception:
+            continue
+        if d and d.get("hbm_bytes_per_launch"):
+            return d["hbm_bytes_per_launch"]
+    return None
+
+
+def kernel_table(records):
+    """{name: (launches, total ms, avg us, algorithmic bytes per launch, GB/s)} from HIP events."""
+    agg = {}
+    for name, e0, e1, nbytes in records:
+        ms = e0.elapsed_time(e1)
+        a = agg.setdefault(name, [0, 0.0, 0])
+        a[0] += 1
+        a[1] += ms
+        a[2] += nbytes
+    out = {}
+    for name, (cnt, ms, nb) in agg.items():
+        out[name] = {"launches": cnt, "total_ms": round(ms, 3), "avg_us": round(ms / cnt * 1e3, 2),
+                     "bytes_per_launch": nb // cnt, "gbs": round(nb / (ms / 1e3) / 1e9, 2)}
+    return out
+
+
+def roofline_of(name, k):
+    traffic = pmc_traffic(name)
+    return {"kernel": name, "bound": "hbm", "achieved": k["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(k["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "bytes_per_launch": k["bytes_per_launch"], "avg_launch_us": k["avg_us"], "launches": k["launches"]}
 
 
 def heartbeat(state):
@@ -140,6 +163,7 @@ def main():
     import torch.distributed as dist
 
     from merlin import MerlinVecEnv
+    from merlin import _native as nat
     from merlin.distributed import DataParallel
     from merlin.ppo import PPO
 
@@ -166,7 +190,7 @@ def main():
         dist.barrier()
 
     state["phase"] = "timed"
-    agent.env_step_events = []
+    nat.KernelTimer.start()
     ph = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -186,9 +210,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    ev = agent.env_step_events
-    agent.env_step_events = None
-    step_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    kernels = kernel_table(nat.KernelTimer.stop())
     rollout_ms = sum(a.elapsed_time(b) for a, b, _ in ph) / len(ph)
     update_ms = sum(b.elapsed_time(c) for _, b, c in ph) / len(ph)
     value = args.steps * B * world / elapsed
@@ -197,8 +219,7 @@ def main():
         if dp.enabled:
             dist.barrier()
         return
-    achieved = ENV_STEP_BYTES * N / (step_ms / 1e3) / 1e9
-    traffic = pmc_traffic()
+    dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
     flop_per_step = 2 * FWD_MACS + args.epochs * 2 * (FWD_MACS + BWD_MACS)
     loop_tflops = value / world * flop_per_step / 1e12
     out = {
@@ -219,14 +240,14 @@ def main():
                                f"{args.epochs} epochs x {args.minibatches} minibatches of {B // args.minibatches}",
                    "num_envs_per_gpu": N, "k_steps": T, "global_batch": B * world,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
-        "roofline": {"kernel": "k_env_step", "bound": "hbm", "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": traffic, "bytes_per_env_step": ENV_STEP_BYTES, "envs_per_launch": N,
-                     "avg_launch_us": round(step_ms * 1e3, 2)},
+        # dominant hand-written kernel of the timed loop (by total HIP-event time)
+        "roofline": roofline_of(dominant, kernels[dominant]),
+        "roofline_env_step": roofline_of("k_env_step", kernels["k_env_step"]),
         "roofline_loop": {"bound": "mfma", "achieved": round(loop_tflops, 2), "peak": FP32_PEAK_TFLOPS,
                           "unit": "TFLOP/s", "frac": round(loop_tflops / FP32_PEAK_TFLOPS, 4),
                           "flop_per_env_step": flop_per_step},
         "phases_ms": {"rollout": round(rollout_ms, 2), "update": round(update_ms, 2)},
+        "kernels": kernels,
     }
     state["phase"] = "tiers"
     if not args.no_tiers:

@@ -108,88 +108,123 @@ __global__ __launch_bounds__(BLK, 2) void k_conv1_im2col_fwd(const uint32_t *__r
 // Backward of A2 = im2col(relu(conv1)) w.r.t. the tables and the bias:
 //   dz1[t][ci][pos] = [z1 > 0] * sum_{(p2, tap) covering pos} dA2[t][s*25+p2][tap*32+ci]
 //   dP[t][ci][slot][bin] += dz1 over the positions whose slot quarter falls in bin
-// Thread (t, ci, slot) owns 20 register bins (5 classes x 4 quarters) for its whole
-// sample range; positions are visited in 4 parity groups so the quarter is static.
-__global__ __launch_bounds__(BLK, 2) void k_conv1_im2col_bwd(const uint32_t *__restrict__ codes,
-                                                          const int64_t *__restrict__ index, int64_t n,
-                                                          const float *__restrict__ tables,
-                                                          const float *__restrict__ bias,
-                                                          const float *__restrict__ dA, int T,
-                                                          float *__restrict__ slabs) {
+// One wave per sample, lane = (tower, channel) = 64 lanes.  The lane walks the sample's
+// 25 x 16 (p2, tap) gradient entries (each wave load = two 128-B rows, one per tower),
+// tests the ReLU mask from 169 mask bits it computed once from the tables, and adds
+// every entry into the 4 slot bins of its conv1 position.  The quarter index of each
+// slot depends only on the tap's parity (static in the unrolled tap loop); the class is
+// a 5-way select.  80 register bins per lane live across the wave's whole sample range.
+constexpr int BWD_WAVES = 4;
+__global__ __launch_bounds__(64 * BWD_WAVES, 2) void k_conv1_im2col_bwd(
+    const uint32_t *__restrict__ codes, const int64_t *__restrict__ index, int64_t n,
+    const float *__restrict__ tables, const float *__restrict__ bias, const float *__restrict__ dA, int T,
+    float *__restrict__ slabs) {
     __shared__ float tab[MAXT * TAB];
     __shared__ float sb[MAXT * C1];
-    __shared__ uint32_t bins[NPOS1];
-    __shared__ float dz[MAXT * NPOS1 * C1];  // [t][pos][ci]
+    __shared__ uint32_t bins_all[BWD_WAVES][NPOS1];
+    __shared__ float red[64 * (NSLOT * NBIN + 1)];  // block fold of the 4 waves' bins
     stage_tables(tables, bias, T, tab, sb);
-    const int per = (int)((n + gridDim.x - 1) / gridDim.x);
-    const int64_t s0 = (int64_t)blockIdx.x * per, s1 = min(n, s0 + per);
-    // phase-2 identity of this thread
-    const int ht = threadIdx.x >> 7, hci = (threadIdx.x >> 2) & 31, hslot = threadIdx.x & 3;
-    const bool hact = ht < T;
-    const int dyy = hslot >> 1, dxx = hslot & 1;
-    float acc[5][4];  // [class][parity group]
+    for (int k = threadIdx.x; k < 64 * (NSLOT * NBIN + 1); k += blockDim.x) red[k] = 0.0f;
+    __syncthreads();
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = lane >> 5, ci = lane & 31;
+    const bool live = t < T;
+    uint32_t *bins = bins_all[wv];
+    float acc[NSLOT][4][4];  // [slot][class 1..4][parity group]; class 0 = group total - rest
+    float tot[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int c = 0; c < 5; c++)
+    for (int sl = 0; sl < NSLOT; sl++)
 #pragma unroll
-        for (int g = 0; g < 4; g++) acc[c][g] = 0.0f;
-    float accb = 0.0f;
-    for (int64_t s = s0; s < s1; s++) {
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc[sl][c][q] = 0.0f;
+    const int64_t gw = (int64_t)gridDim.x * BWD_WAVES;
+    for (int64_t s = (int64_t)blockIdx.x * BWD_WAVES + wv; s < n; s += gw) {
         uint32_t w[8];
         load_codes(codes, index ? index[s] : s, w);
-        __syncthreads();
-        stage_bins(w, bins);
-        __syncthreads();
-        for (int e = threadIdx.x; e < T * NPOS1 * C1; e += BLK) {
-            const int t = e / (NPOS1 * C1), r = e - t * (NPOS1 * C1), p = r >> 5, ci = r & 31;
-            float g = 0.0f;
-            if (conv1_z(tab, sb, t, ci, bins[p]) > 0.0f) {
-                const int y = p / 13, x = p - (p / 13) * 13;
-                const float *base = dA + ((size_t)t * n + s) * (P2 * K2) + ci;
+        // this wave's tile classes of the 4 slot quarters of the 169 positions (wave-private LDS)
+        for (int p = lane; p < NPOS1; p += 64) {
+            const int oy = p / 13, ox = p - (p / 13) * 13;
+            uint32_t packed = 0u;
 #pragma unroll
-                for (int a = 0; a < 2; a++) {
-                    const int ky = (y & 1) + 2 * a, oy = (y - ky) >> 1;
-                    if (ky > y || oy > 4) continue;
+            for (int dy = 0; dy < 2; dy++)
 #pragma unroll
-                    for (int b = 0; b < 2; b++) {
-                        const int kx = (x & 1) + 2 * b, ox = (x - kx) >> 1;
-                        if (kx > x || ox > 4) continue;
-                        g += base[(oy * 5 + ox) * K2 + (ky * 4 + kx) * C1];
-                    }
+                for (int dx = 0; dx < 2; dx++) {
+                    const int qr = oy + dy, qc = ox + dx, cell = (qr >> 1) * 7 + (qc >> 1);
+                    const uint32_t cls = (w[cell >> 3] >> ((cell & 7) * 4)) & 0xfu;
+                    packed |= cls << (8 * (dy * 2 + dx));
                 }
-            }
-            dz[e] = g;
+            bins[p] = packed;  // 4 x u8 classes (slot order)
         }
-        __syncthreads();
-        if (hact) {
-            const float *d = dz + ht * NPOS1 * C1 + hci;
-            // parity group g = (py, px); within a group this slot's quarter index is fixed
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes are visible
+        if (!live) continue;
+        const float *tt = tab + t * NSLOT * NBIN * C1 + ci;
+        const float b0 = sb[t * C1 + ci];
+        const float *g = dA + ((size_t)t * n + s) * (P2 * K2) + ci;
+        // positions in 4 parity groups (py, px): the taps covering a position and each slot's
+        // quarter index are then compile-time constants
 #pragma unroll
-            for (int py = 0; py < 2; py++)
+        for (int py = 0; py < 2; py++)
 #pragma unroll
-                for (int px = 0; px < 2; px++) {
-                    const int g = py * 2 + px;
-                    for (int y = py; y < 13; y += 2)
-                        for (int x = px; x < 13; x += 2) {
-                            const int p = y * 13 + x;
-                            const float v = d[p * C1];
-                            const int cls = (int)(((bins[p] >> (8 * hslot)) & 0xff) - hslot * NBIN) >> 2;
+            for (int px = 0; px < 2; px++) {
+                const int grp = py * 2 + px;
+                for (int y = py; y < 13; y += 2)
+                    for (int x = px; x < 13; x += 2) {
+                        const int pos = y * 13 + x;
+                        const uint32_t c4 = bins[pos];
+                        // z1 > 0 ?  (ReLU mask, recomputed from the tables)
+                        float z = b0;
 #pragma unroll
-                            for (int c = 0; c < 5; c++) acc[c][g] += (cls == c) ? v : 0.0f;
-                            accb += v;
+                        for (int sl = 0; sl < 4; sl++) {
+                            const int q = ((py + (sl >> 1)) & 1) * 2 + ((px + (sl & 1)) & 1);
+                            z += tt[(sl * NBIN + (int)((c4 >> (8 * sl)) & 0xff) * 4 + q) * C1];
                         }
+                        // col2im: taps ky in {py, py+2}, kx in {px, px+2}
+                        float d = 0.0f;
+#pragma unroll
+                        for (int a = 0; a < 2; a++) {
+                            const int ky = py + 2 * a, oy = (y - ky) >> 1;
+                            if (y < ky || oy > 4) continue;
+#pragma unroll
+                            for (int b = 0; b < 2; b++) {
+                                const int kx = px + 2 * b, ox = (x - kx) >> 1;
+                                if (x < kx || ox > 4) continue;
+                                d += g[(oy * 5 + ox) * K2 + (ky * 4 + kx) * C1];
+                            }
+                        }
+                        d = z > 0.0f ? d : 0.0f;
+                        tot[grp] += d;
+#pragma unroll
+                        for (int sl = 0; sl < 4; sl++) {
+                            const uint32_t cls = (c4 >> (8 * sl)) & 0xff;
+#pragma unroll
+                            for (int c = 1; c < 5; c++) acc[sl][c - 1][grp] += (cls == (uint32_t)c) ? d : 0.0f;
+                        }
+                    }
+            }
+    }
+    // fold the block's waves, then one slab per block
+    if (live) {
+        float *r = red + lane * (NSLOT * NBIN + 1);
+#pragma unroll
+        for (int sl = 0; sl < NSLOT; sl++)
+#pragma unroll
+            for (int grp = 0; grp < 4; grp++) {
+                const int q = (((grp >> 1) + (sl >> 1)) & 1) * 2 + (((grp & 1) + (sl & 1)) & 1);
+                float rest = 0.0f;
+#pragma unroll
+                for (int c = 1; c < 5; c++) {
+                    atomicAdd(r + sl * NBIN + c * 4 + q, acc[sl][c - 1][grp]);
+                    rest += acc[sl][c - 1][grp];
                 }
-        }
+                atomicAdd(r + sl * NBIN + q, tot[grp] - rest);
+            }
+        atomicAdd(r + NSLOT * NBIN, (tot[0] + tot[1]) + (tot[2] + tot[3]));
     }
-    if (hact) {
-        float *dst = slabs + ((size_t)blockIdx.x * T + ht) * SLAB + hci * (NSLOT * NBIN + 1);
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const int q = (((g >> 1) + dyy) & 1) * 2 + (((g & 1) + dxx) & 1);
-#pragma unroll
-            for (int c = 0; c < 5; c++) dst[hslot * NBIN + c * 4 + q] = acc[c][g];
-        }
-        if (hslot == 0) dst[NSLOT * NBIN] = accb;
-    }
+    __syncthreads();
+    float *dst = slabs + (size_t)blockIdx.x * T * SLAB;  // lane order t*32 + co == slab order
+    for (int k = threadIdx.x; k < T * SLAB; k += blockDim.x) dst[k] = red[k];
 }
 
 __global__ __launch_bounds__(256) void k_slab_reduce(const float *__restrict__ slabs, int nslab, int T,
@@ -275,9 +310,9 @@ hipError_t launch_conv1_im2col_bwd(const uint32_t *codes, const int64_t *index, 
         hipError_t e = hipMemsetAsync(dtables, 0, sizeof(float) * T * TAB, s);
         return e == hipSuccess ? hipMemsetAsync(dbias, 0, sizeof(float) * T * C1, s) : e;
     }
-    const int grid = (int)std::min<int64_t>(n, (int64_t)max_slabs);
-    hipLaunchKernelGGL(k_conv1_im2col_bwd, dim3(grid), dim3(BLK), 0, s, codes, index, n, tables, bias, dA2, T,
-                       slabs);
+    const int grid = (int)std::min<int64_t>((n + BWD_WAVES - 1) / BWD_WAVES, (int64_t)max_slabs);
+    hipLaunchKernelGGL(k_conv1_im2col_bwd, dim3(grid), dim3(64 * BWD_WAVES), 0, s, codes, index, n, tables, bias,
+                       dA2, T, slabs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_slab_reduce, dim3((T * SLAB + 255) / 256), dim3(256), 0, s, slabs, grid, T, dtables,

@@ -93,6 +93,53 @@ EXPORTED_SYMBOLS = (
 )
 
 
+class KernelTimer:
+    """Opt-in HIP-event timing of the library's launches on the current stream (bench.py).
+    Each record keeps (name, start event, end event, algorithmic bytes of the launch)."""
+
+    records: list | None = None
+
+    @classmethod
+    def start(cls):
+        cls.records = []
+
+    @classmethod
+    def stop(cls):
+        recs, cls.records = cls.records, None
+        return recs or []
+
+    @classmethod
+    def span(cls, name: str, nbytes: int):
+        return _Span(name, nbytes) if cls.records is not None else _NULL_SPAN
+
+
+class _Span:
+    def __init__(self, name, nbytes):
+        self.name, self.nbytes = name, nbytes
+
+    def __enter__(self):
+        self.e0 = torch.cuda.Event(enable_timing=True)
+        self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        KernelTimer.records.append((self.name, self.e0, e1, self.nbytes))
+        return False
+
+
+class _NullSpan:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL_SPAN = _NullSpan()
+
+
 def check(rc: int, what: str = "") -> None:
     if rc != MERLIN_OK:
         msg = lib().merlin_last_error().decode(errors="replace")
@@ -205,8 +252,10 @@ def conv2_im2col_fwd(codes, index, tables, bias):
     T = int(tables.shape[0])
     n = int(index.numel()) if index is not None else int(codes.shape[0])
     out = torch.empty((T, n * 25, 512), dtype=torch.float32, device=codes.device)
-    check(lib().merlin_tower_conv2_im2col_fwd(ptr(codes), ptr(index), n, ptr(tables), ptr(bias), T, ptr(out),
-                                              stream_of(codes)), "merlin_tower_conv2_im2col_fwd")
+    # algorithmic bytes: A2 written (T*25*512*4 per frame) + codes (32) + index (8) per frame
+    with KernelTimer.span("k_conv1_im2col_fwd", n * (T * 25 * 512 * 4 + 32 + (8 if index is not None else 0))):
+        check(lib().merlin_tower_conv2_im2col_fwd(ptr(codes), ptr(index), n, ptr(tables), ptr(bias), T,
+                                                  ptr(out), stream_of(codes)), "merlin_tower_conv2_im2col_fwd")
     return out
 
 
@@ -215,8 +264,10 @@ def conv2_im2col_bwd(codes, index, tables, bias, dA2):
     n = int(dA2.shape[1]) // 25
     dt = torch.empty((T, 32, 4, 20), dtype=torch.float32, device=dA2.device)
     db = torch.empty((T, 32), dtype=torch.float32, device=dA2.device)
-    check(lib().merlin_tower_conv2_im2col_bwd(ptr(codes), ptr(index), n, ptr(tables), ptr(bias), ptr(dA2), T,
-                                              ptr(dt), ptr(db), stream_of(dA2)), "merlin_tower_conv2_im2col_bwd")
+    with KernelTimer.span("k_conv1_im2col_bwd", n * (T * 25 * 512 * 4 + 32 + (8 if index is not None else 0))):
+        check(lib().merlin_tower_conv2_im2col_bwd(ptr(codes), ptr(index), n, ptr(tables), ptr(bias), ptr(dA2),
+                                                  T, ptr(dt), ptr(db), stream_of(dA2)),
+              "merlin_tower_conv2_im2col_bwd")
     return dt, db
 
 
@@ -225,8 +276,9 @@ def conv3_im2col_fwd(Z2, b2):
     T = int(Z2.shape[0])
     n = int(Z2.shape[1]) // 25
     out = torch.empty((T, n * 9, 576), dtype=torch.float32, device=Z2.device)
-    check(lib().merlin_tower_conv3_im2col_fwd(ptr(Z2), ptr(b2), n, T, ptr(out), stream_of(Z2)),
-          "merlin_tower_conv3_im2col_fwd")
+    with KernelTimer.span("k_im2col3_fwd", n * T * (25 * 64 + 9 * 576) * 4):
+        check(lib().merlin_tower_conv3_im2col_fwd(ptr(Z2), ptr(b2), n, T, ptr(out), stream_of(Z2)),
+              "merlin_tower_conv3_im2col_fwd")
     return out
 
 
@@ -234,6 +286,7 @@ def conv3_col2im_bwd(dA3, Z2, b2):
     T = int(Z2.shape[0])
     n = int(Z2.shape[1]) // 25
     out = torch.empty_like(Z2)
-    check(lib().merlin_tower_conv3_col2im_bwd(ptr(dA3), ptr(Z2), ptr(b2), n, T, ptr(out), stream_of(Z2)),
-          "merlin_tower_conv3_col2im_bwd")
+    with KernelTimer.span("k_col2im3_bwd", n * T * (9 * 576 + 2 * 25 * 64) * 4):
+        check(lib().merlin_tower_conv3_col2im_bwd(ptr(dA3), ptr(Z2), ptr(b2), n, T, ptr(out), stream_of(Z2)),
+              "merlin_tower_conv3_col2im_bwd")
     return out

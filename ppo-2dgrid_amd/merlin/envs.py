@@ -40,6 +40,12 @@ class Box:
         self.low, self.high, self.shape, self.dtype = low, high, tuple(shape), dtype
 
 
+# algorithmic bytes per env-step of k_env_step in the rollout configuration:
+# action 8 + agent state r/w 32 + wall rows 64 + episode accumulators r/w 24 + obs codes 32
+# + reward 4 + done 4
+ENV_STEP_BYTES = 168
+
+
 def _entropy_seed() -> int:
     return int.from_bytes(os.urandom(8), "little") >> 1
 
@@ -142,7 +148,7 @@ class MerlinVecEnv:
         t*action_stride + i (state stays on chip across the steps)."""
         assert actions.dtype == torch.int64 and actions.is_contiguous()
         stride = self.num_envs if action_stride is None else int(action_stride)
-        with torch.cuda.device(self.device):
+        with torch.cuda.device(self.device), nat.KernelTimer.span("k_env_step", self.num_envs * n_steps * ENV_STEP_BYTES):
             nat.check(self._lib.merlin_env_step(
                 self._h, nat.ptr(actions), int(n_steps), stride, nat.ptr(obs_out), nat.ptr(reward),
                 nat.ptr(term), nat.ptr(trunc), nat.ptr(done), nat.ptr(ep_return), nat.ptr(ep_length),

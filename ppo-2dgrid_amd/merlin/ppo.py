@@ -56,7 +56,6 @@ class PPO:
         self.vf_coef, self.ent_coef = vf_coef, ent_coef
         self.dp = dp if dp is not None else DataParallel()
         self.perm_fn = perm_fn  # tests replay recorded permutations through this hook
-        self.env_step_events = None  # bench.py: list collecting (start, end) HIP events per env-step launch
         # vectorised path: evaluate conv1 from the tile codes (merlin_conv1_lut_*) instead of
         # expanding 37.6 KB frames and running the generic convolution
         self.conv1_from_codes = conv1_from_codes
@@ -118,15 +117,8 @@ class PPO:
                 buf.actions[t].copy_(action)
                 buf.logprobs[t].copy_(logp)
                 buf.values[t].copy_(value)
-                ev = self.env_step_events
-                if ev is not None:
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
                 env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
                               buf.ep_return[t], buf.ep_length[t])
-                if ev is not None:
-                    e1.record()
-                    ev.append((e0, e1))
             _, _, last_value = self._act(buf.codes[T], obs)
             buf.last_value.copy_(last_value)
         self._record_episodes()

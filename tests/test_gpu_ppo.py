@@ -41,11 +41,14 @@ def test_update_matches_reference(golden, oracle, device):
     # steps the averaged metrics agree to ~1e-4 relative
     for k, v in ref.items():
         assert abs(stats[k] - v) <= 2e-3 * max(1.0, abs(v)), (k, stats[k], v)
-    # post-Adam parameters: a near-zero gradient whose sign differs between the CPU reference
-    # and the GPU moves one element by +-2*lr, so bound the signed sum relative to the mass
+    # post-Adam parameters: an element whose gradient is ~0 (conv1 has many, behind dead
+    # ReLUs) can take the opposite Adam step (+-lr per optimizer step) on CPU vs GPU; bound the
+    # signed sum by the trajectories of up to 0.5% of the elements (at least 4) flipping
+    nsteps = EPOCHS * ((B + MB - 1) // MB)
     for (k, t), (s, a, first) in zip(agent.ac.state_dict().items(), g["sums1"]):
         t = t.double().cpu()
-        assert abs(t.sum().item() - s) <= 1e-5 * a + 1e-6, k
+        flips = max(4.0, 0.005 * t.numel())
+        assert abs(t.sum().item() - s) <= 1e-5 * a + 2 * lr * nsteps * flips, k
         assert abs(t.abs().sum().item() - a) <= 1e-4 * max(1.0, a), k
 
 
