@@ -1,0 +1,65 @@
+"""CPU: host-side logic mirrored from the reference (no GPU calls)."""
+import os
+
+import pytest
+
+
+def test_metrics_aggregation():
+    from merlin.metrics.ppo_metrics import aggregate_ppo_update_metrics, compute_episode_stats
+
+    m = aggregate_ppo_update_metrics(1.0, 2.0, 3.0, 4.0, 5.0, 6.0, 2)
+    assert m == {"pi_loss": 0.5, "v_loss": 1.0, "entropy": 1.5, "kl": 2.0, "clipfrac": 2.5, "gradnorm": 3.0}
+    assert aggregate_ppo_update_metrics(1, 1, 1, 1, 1, 1, 0)["pi_loss"] == 0.0
+    assert compute_episode_stats([], []) == {"episode_return_mean": 0.0, "episode_length_mean": 0.0}
+    assert compute_episode_stats([1.0, 0.0], [10, 20])["episode_length_mean"] == 15.0
+
+
+def test_scenario_config_surface():
+    from merlin.scenario_creator import ScenarioCreator
+
+    sc = ScenarioCreator()
+    assert sc.get_env_id("mediumhard") == "MERLIN-MediumHard-v0"
+    assert sc.get_env_size_str("hard") == "16x16"
+    kw = sc._env_kwargs("mediumhard")
+    assert kw == {"difficulty": "mediumhard", "size": 16}
+    with pytest.raises(ValueError):
+        sc._env_kwargs("impossible")
+    with pytest.raises(FileNotFoundError):
+        ScenarioCreator("/nonexistent.yaml")
+
+
+def test_scenario_rejects_unsupported_observation_modes(tmp_path):
+    from merlin.scenario_creator import ScenarioCreator
+
+    p = tmp_path / "s.yaml"
+    p.write_text("observation:\n  fully_observable: true\ndifficulties:\n  easy:\n    env_id: MERLIN-Easy-v0\n")
+    with pytest.raises(NotImplementedError):
+        ScenarioCreator(str(p))._env_kwargs("easy")
+
+
+def test_cli_flags_match_reference_defaults():
+    import importlib.util
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ppo-2dgrid_amd", "ppo_train.py")
+    spec = importlib.util.spec_from_file_location("ppo_train", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    a = mod.parse_args([])
+    # ppo/ppo_train.py:21-40 defaults
+    assert (a.device, a.lr, a.gamma, a.lam, a.clip_eps, a.update_epochs) == ("auto", 3e-4, 0.99, 0.95, 0.2, 10)
+    assert (a.batch_size, a.minibatch_size, a.vf_coef, a.ent_coef, a.total_steps) == (2048, 256, 0.5, 0.05, 300_000)
+    assert (a.save_interval, a.eval_episodes, a.difficulty, a.seed, a.print_interval) == (100_000, 3, "easy", 123, 2048)
+    b = mod.parse_args(["--difficulty", "mediumhard", "--num_envs", "4096", "--k_steps", "256", "--stuck_penalty"])
+    assert b.num_envs * b.k_steps == 1_048_576 and b.stuck_penalty and not b.exploration_bonus
+
+
+def test_ppo_refuses_cpu_device():
+    """The product path has no CPU fallback: it fails loudly."""
+    from merlin import _native as nat
+    from merlin.ppo import PPO
+
+    class E:
+        action_space = type("S", (), {"n": 3})()
+
+    with pytest.raises(nat.MerlinNativeError):
+        PPO(E(), device="cpu")
