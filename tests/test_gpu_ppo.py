@@ -48,8 +48,9 @@ def test_update_matches_reference(golden, oracle, device):
     for (k, t), (s, a, first) in zip(agent.ac.state_dict().items(), g["sums1"]):
         t = t.double().cpu()
         flips = max(4.0, 0.005 * t.numel())
-        assert abs(t.sum().item() - s) <= 1e-5 * a + 2 * lr * nsteps * flips, k
-        assert abs(t.abs().sum().item() - a) <= 1e-4 * max(1.0, a), k
+        allow = 2 * lr * nsteps * flips
+        assert abs(t.sum().item() - s) <= 1e-5 * a + allow, k
+        assert abs(t.abs().sum().item() - a) <= 1e-5 * a + allow, k
 
 
 def test_code_path_sgd_matches_frame_path(golden, oracle, device):
