@@ -99,6 +99,9 @@ typedef struct {
     double penalty;            /* StuckPenaltyWrapper.penalty (default -0.1) */
     int32_t exploration_bonus; /* 1: +bonus on the first visit of a cell per episode */
     double bonus;
+    int32_t reseed_each_reset; /* 1: every reset regenerates from the seeded RNG state, i.e.
+                                  env.reset(seed=task_seed) on every episode as FOMAML's
+                                  collect_trajectory does (src/fomaml.py:63,92) */
 } merlin_env_config;
 
 /* Library */

@@ -265,6 +265,7 @@ int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
     d.penalty = cfg->penalty;
     d.explore_on = cfg->exploration_bonus ? 1 : 0;
     d.bonus = cfg->bonus;
+    d.reseed = cfg->reseed_each_reset ? 1 : 0;
     (void)hipGetDevice(&e->device);
     const size_t n = (size_t)d.n;
     hipError_t err = hipSuccess;

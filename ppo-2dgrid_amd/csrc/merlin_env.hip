@@ -527,7 +527,7 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
     Rng r = load_rng(E, i);
     GenOut g;
     generate_map<SP>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
-    store_rng(E, i, r);
+    if (!E.reseed) store_rng(E, i, r);
     store_rows<SP>(E, i, rows, lane, E.size);
     E.agent[i] = pack_agent(g.ax, g.ay, g.dir, 0, g.gx, g.gy, g.ax, g.ay, 0);
     E.ep_ret[i] = 0.0;
@@ -612,8 +612,8 @@ __global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
             if (O.ep_len_out) O.ep_len_out[row] = ep_len;
         }
         if (done && O.autoreset) {
-            if (!rng_loaded) {
-                r = load_rng(E, i);
+            if (!rng_loaded || E.reseed) {
+                r = load_rng(E, i);  // reseed mode: always restart from the seeded state
                 rng_loaded = true;
             }
             GenOut g;
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
     E.ep_ret[i] = ep_ret;
     E.ep_len[i] = ep_len;
     if (rows_dirty) store_rows<SP>(E, i, rows, lane, S);
-    if (rng_loaded) store_rng(E, i, r);
+    if (rng_loaded && !E.reseed) store_rng(E, i, r);
     if (err) atomicOr(E.err, err);
 }
 

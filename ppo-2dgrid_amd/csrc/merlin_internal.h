@@ -26,6 +26,7 @@ struct EnvDev {
     double penalty;
     int explore_on;
     double bonus;
+    int reseed;  // never persist the advanced RNG state: every reset = reset(seed=...)
     uint32_t *walls;
     uint4 *agent;
     ulonglong2 *rng_s;

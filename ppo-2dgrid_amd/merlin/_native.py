@@ -40,6 +40,7 @@ class EnvConfig(C.Structure):
         ("penalty", C.c_double),
         ("exploration_bonus", C.c_int32),
         ("bonus", C.c_double),
+        ("reseed_each_reset", C.c_int32),
     ]
 
 

@@ -64,7 +64,8 @@ class MerlinVecEnv:
     def __init__(self, num_envs: int, difficulty: str = "mediumhard", size: int = 16,
                  max_steps: int | None = None, seed: int | None = None, device="cuda",
                  stuck_penalty: bool = False, max_stay: int = 3, penalty: float = -0.1,
-                 exploration_bonus: bool = False, bonus: float = 0.01, env_offset: int = 0):
+                 exploration_bonus: bool = False, bonus: float = 0.01, env_offset: int = 0,
+                 seeds=None, reseed_each_reset: bool = False):
         if difficulty not in nat.DIFFICULTY_IDS:
             raise ValueError(f"Unknown difficulty: {difficulty}")
         self.device = torch.device(device)
@@ -80,7 +81,7 @@ class MerlinVecEnv:
         self.observation_space = self.single_observation_space
         cfg = nat.EnvConfig(self.num_envs, self.size, nat.DIFFICULTY_IDS[difficulty], self.max_steps,
                             int(stuck_penalty), int(max_stay), float(penalty), int(exploration_bonus),
-                            float(bonus))
+                            float(bonus), int(reseed_each_reset))
         self._lib = nat.lib()
         with torch.cuda.device(self.device):
             h = C.c_void_p()
@@ -88,6 +89,8 @@ class MerlinVecEnv:
         self._h = h
         self._seed_pending = seed
         self._seeded_once = False
+        if seeds is not None:
+            self.seed_each(seeds)
         self.obs = torch.zeros((self.num_envs, nat.OBS_WORDS), dtype=torch.int32, device=self.device)
         # per-step scratch outputs for the gym-style step()
         n = self.num_envs
@@ -115,6 +118,15 @@ class MerlinVecEnv:
     def seed(self, seed: int) -> None:
         seeds = (np.arange(self.num_envs, dtype=np.uint64) + np.uint64(self.env_offset)
                  + np.uint64(seed))
+        with torch.cuda.device(self.device):
+            nat.check(self._lib.merlin_env_seed(self._h, seeds.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                                self.num_envs, self._stream), "merlin_env_seed")
+        self._seeded_once = True
+
+    def seed_each(self, seeds) -> None:
+        """Seed env i with seeds[i] (e.g. FOMAML task seeds)."""
+        seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64))
+        assert seeds.shape == (self.num_envs,)
         with torch.cuda.device(self.device):
             nat.check(self._lib.merlin_env_seed(self._h, seeds.ctypes.data_as(C.POINTER(C.c_uint64)),
                                                 self.num_envs, self._stream), "merlin_env_seed")

@@ -1,0 +1,162 @@
+"""First-order MAML over MERLIN tasks (src/fomaml.py of the reference), batched over tasks.
+
+Reference semantics kept (src/fomaml.py:9-223):
+  * a task = one map seed; ``collect_trajectory`` resets the env with ``seed=task_seed`` at
+    the start and after every done (:63,92), so every episode replays the same map --
+    here a MerlinVecEnv with one env per task and ``reseed_each_reset``;
+  * inner loop: fast policy = copy of the meta policy, support rollout of k steps, loss =
+    PPO clipped surrogate + 0.5 value MSE - 0.05 entropy with GAE(gamma .995, lam .95),
+    advantages normalised per task and returns = values + *normalised* advantages
+    (:110-156), clip_grad_norm_(0.5), one SGD(lr_inner) step (:176-182);
+  * query rollout with the adapted policy, its loss gradient added into the meta
+    gradient (:187-202); meta gradient / n_tasks, clip_grad_norm_(0.5), Adam(lr_outer)
+    (:207-212); returns (avg query loss, avg query episode reward, avg query episode
+    length, the last task's query stats) (:214-223).
+MI355X batching: the support rollouts of all tasks run with the meta weights in one vector
+env (fast == meta before the inner step); the per-task fast policies are stacked tensors
+(merlin.batched_policy), so the inner step, the query rollouts and the query gradients of
+all tasks are single batched launches; GAE is the HIP kernel ([k][tasks] layout).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.optim as optim
+
+from . import _native as nat
+from . import batched_policy as bp
+from .actor_critic import CNNActorCritic
+from .envs import MerlinVecEnv
+
+INV255 = 1.0 / 255.0
+
+
+class FOMAML:
+    def __init__(self, scenario_creator, lr_inner=0.01, lr_outer=3e-4, device="cuda", difficulty="medium"):
+        self.sc = scenario_creator
+        self.difficulty = difficulty
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise nat.MerlinNativeError("merlin.FOMAML runs its rollouts/GAE as HIP kernels; pass a GPU device")
+        self.lr_inner = lr_inner
+        self.env_kwargs = self.sc._env_kwargs(difficulty)
+        self.meta_policy = CNNActorCritic((56, 56, 3), 3).to(self.device)
+        self.meta_optimizer = optim.Adam(self.meta_policy.parameters(), lr=lr_outer)
+        self.gamma, self.lam = 0.995, 0.95
+        self.vf_coef, self.ent_coef, self.clip_eps = 0.5, 0.05, 0.2
+        self._env = None
+
+    # ------------------------------------------------------------------ envs
+    def _task_env(self, task_seeds) -> MerlinVecEnv:
+        G = len(task_seeds)
+        if self._env is None or self._env.num_envs != G:
+            if self._env is not None:
+                self._env.close()
+            self._env = MerlinVecEnv(G, device=self.device, reseed_each_reset=True, **self.env_kwargs)
+        self._env.seed_each(np.asarray(task_seeds, dtype=np.uint64))
+        return self._env
+
+    # ------------------------------------------------------------ rollouts
+    @torch.no_grad()
+    def collect_trajectory(self, env: MerlinVecEnv, params, steps: int):
+        """k steps of every task in parallel (collect_trajectory, src/fomaml.py:54-108).
+        params: stacked per-task weights (bp.stack_params) or None for the meta policy."""
+        G = env.num_envs
+        dev = self.device
+        codes = torch.empty((steps + 1, G, 8), dtype=torch.int32, device=dev)
+        act = torch.empty((steps, G), dtype=torch.int64, device=dev)
+        logp = torch.empty((steps, G), dtype=torch.float32, device=dev)
+        val = torch.empty((steps, G), dtype=torch.float32, device=dev)
+        rew = torch.empty((steps, G), dtype=torch.float32, device=dev)
+        done = torch.empty((steps, G), dtype=torch.float32, device=dev)
+        epr = torch.empty((steps, G), dtype=torch.float64, device=dev)
+        epl = torch.empty((steps, G), dtype=torch.int32, device=dev)
+        env.reset(out=codes[0])  # = env.reset(seed=task_seed)
+        frames = torch.empty((G, 3, 56, 56), dtype=torch.float32, device=dev)
+        for t in range(steps):
+            if params is None:
+                a, lp, v = self.meta_policy.act_codes(codes[t])
+            else:
+                nat.expand_obs(codes[t], out=frames, scale=INV255)
+                a, lp, v = bp.act(params, frames.unsqueeze(1))
+                a, lp, v = a[:, 0], lp[:, 0], v[:, 0]
+            act[t], logp[t], val[t] = a, lp, v
+            env.step_into(act[t], codes[t + 1], rew[t], None, None, done[t], epr[t], epl[t])
+        if params is None:
+            _, _, last = self.meta_policy.act_codes(codes[steps])
+        else:
+            nat.expand_obs(codes[steps], out=frames, scale=INV255)
+            _, _, last = bp.act(params, frames.unsqueeze(1))
+            last = last[:, 0]
+        env.errors()
+        d = done > 0
+        return {"codes": codes, "act": act, "logp": logp, "val": val, "rew": rew, "done": done, "last_val": last,
+                "ep_rews": epr[d].cpu().tolist(), "ep_lens": epl[d].cpu().tolist()}
+
+    # ---------------------------------------------------------------- loss
+    def compute_loss(self, batch, params):
+        """Per-task losses (compute_loss, src/fomaml.py:110-156) -> (sum over tasks, stats per task)."""
+        k, G = batch["rew"].shape
+        adv, _ = nat.gae(batch["rew"].contiguous(), batch["val"].contiguous(), batch["done"].contiguous(),
+                         batch["last_val"].float().contiguous(), self.gamma, self.lam)
+        adv_n = (adv - adv.mean(dim=0, keepdim=True)) / (adv.std(dim=0, keepdim=True) + 1e-8)  # per task
+        ret = (batch["val"] + adv_n).detach()
+        frames = nat.expand_obs(batch["codes"][:k].reshape(k * G, 8), scale=INV255)
+        frames = frames.view(k, G, 3, 56, 56).transpose(0, 1)  # [G, k, ...]
+        new_logp, ent, new_val = bp.evaluate(params, frames, batch["act"].t())
+        old_logp = batch["logp"].t()
+        a_t, r_t = adv_n.t(), ret.t()
+        ratio = torch.exp(new_logp - old_logp)
+        surr1 = ratio * a_t
+        surr2 = torch.clamp(ratio, 1.0 - self.clip_eps, 1.0 + self.clip_eps) * a_t
+        pi_loss = -torch.min(surr1, surr2).mean(dim=1)
+        v_loss = ((new_val - r_t) ** 2).mean(dim=1)
+        ent_m = ent.mean(dim=1)
+        loss = pi_loss + self.vf_coef * v_loss - self.ent_coef * ent_m  # [G]
+        with torch.no_grad():
+            kl = (old_logp - new_logp).mean(dim=1)
+            clipfrac = (torch.abs(ratio - 1.0) > self.clip_eps).float().mean(dim=1)
+        stats = {"loss": loss.detach(), "pi_loss": pi_loss.detach(), "v_loss": v_loss.detach(),
+                 "entropy": ent_m.detach(), "kl": kl, "clipfrac": clipfrac}
+        return loss.sum(), stats
+
+    @staticmethod
+    def _clip_per_task(grads: dict, max_norm: float):
+        """clip_grad_norm_ applied to each task's parameter set independently."""
+        G = next(iter(grads.values())).shape[0]
+        sq = torch.zeros(G, dtype=torch.float32, device=next(iter(grads.values())).device)
+        for g in grads.values():
+            sq += g.reshape(G, -1).pow(2).sum(dim=1)
+        norm = sq.sqrt()
+        coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+        return {k: g * coef.view(G, *([1] * (g.dim() - 1))) for k, g in grads.items()}, norm
+
+    # ------------------------------------------------------------ meta step
+    def meta_train_step(self, task_seeds, k_support=50, k_query=50):
+        G = len(task_seeds)
+        env = self._task_env(task_seeds)
+        self.meta_optimizer.zero_grad()
+        names = [n for n, _ in self.meta_policy.named_parameters()]
+        # inner loop: all fast policies start as the meta policy -> batched support rollout
+        support = self.collect_trajectory(env, None, k_support)
+        fast = bp.stack_params(self.meta_policy, G)
+        loss_s, _ = self.compute_loss(support, fast)
+        grads = dict(zip(names, torch.autograd.grad(loss_s, [fast[n] for n in names])))
+        grads, _ = self._clip_per_task(grads, 0.5)
+        with torch.no_grad():
+            adapted = {n: (fast[n] - self.lr_inner * grads[n]).detach().requires_grad_(True) for n in names}
+        # outer loop: query rollouts with each task's adapted policy
+        query = self.collect_trajectory(env, adapted, k_query)
+        loss_q, qstats = self.compute_loss(query, adapted)
+        qgrads = torch.autograd.grad(loss_q, [adapted[n] for n in names])
+        for (n, p), g in zip(self.meta_policy.named_parameters(), qgrads):
+            p.grad = g.sum(dim=0) / G  # sum of the tasks' fast grads / n_tasks (:198-209)
+        torch.nn.utils.clip_grad_norm_(self.meta_policy.parameters(), max_norm=0.5)
+        self.meta_optimizer.step()
+        avg_loss = float(qstats["loss"].mean().item())
+        if query["ep_rews"]:
+            avg_rew, avg_steps = float(np.mean(query["ep_rews"])), float(np.mean(query["ep_lens"]))
+        else:
+            avg_rew, avg_steps = 0.0, float(k_query)
+        last = {k: float(v[-1].item()) for k, v in qstats.items() if k != "loss"}
+        return avg_loss, avg_rew, avg_steps, last
