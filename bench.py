@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import argparse
 import glob
+
+import numpy as np
 import json
 import os
 import sys
@@ -56,7 +58,40 @@ def parse():
     ap.add_argument("--size", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tiers", action="store_true")
+    ap.add_argument("--fomaml", action="store_true",
+                    help="cfg 5 instead: FOMAML meta-iterations, tasks_per_batch=32 x k_steps=256")
+    ap.add_argument("--tasks", type=int, default=32)
     return ap.parse_args()
+
+
+def fomaml_bench(args):
+    """BASELINE cfg 5: one meta-iteration = 32 tasks x (256 support + 256 query) env steps,
+    inner SGD step per task, meta Adam step (merlin.fomaml, batched over tasks)."""
+    import torch
+
+    from merlin import ScenarioCreator
+    from merlin.fomaml import FOMAML
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(42)
+    fm = FOMAML(ScenarioCreator(), lr_inner=0.01, lr_outer=3e-4, device=dev, difficulty=args.difficulty)
+    rs = np.random.RandomState(42)
+    seeds = lambda: rs.choice(100000, args.tasks, replace=False)  # noqa: E731
+    for _ in range(args.warmup):
+        fm.meta_train_step(seeds(), k_support=args.k_steps, k_query=args.k_steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fm.meta_train_step(seeds(), k_support=args.k_steps, k_query=args.k_steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    steps = args.steps * args.tasks * 2 * args.k_steps
+    print(json.dumps({"metric": "FOMAML env-steps/sec (support+query rollouts, inner SGD, meta Adam)",
+                      "value": round(steps / el, 1), "unit": "env-steps/s", "n_gpus": 1, "steps": args.steps,
+                      "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 2),
+                      "higher_is_better": True, "dtype": "fp32", "data": "synthetic",
+                      "config": {"workload": f"FOMAML {args.difficulty} tasks_per_batch={args.tasks} "
+                                             f"k_steps={args.k_steps}"}}), flush=True)
 
 
 def env_only_tier(torch, MerlinVecEnv, n, T, difficulty, size, device):
@@ -159,6 +194,8 @@ def main():
     args = parse()
     state = {"phase": "init"}
     heartbeat(state)
+    if args.fomaml:
+        return fomaml_bench(args)
     import torch
     import torch.distributed as dist
 

@@ -98,9 +98,14 @@ def test_meta_step_matches_serial_reference(device):
     torch.nn.utils.clip_grad_norm_(meta.parameters(), max_norm=0.5)
     torch.optim.Adam(meta.parameters(), lr=3e-4).step()
     assert abs(avg_loss - float(np.mean(qlosses))) <= 1e-4 * max(1.0, abs(avg_loss))
+    # the clipped meta gradients (left in .grad by both) agree to fp32 tolerance; the Adam
+    # step itself (lr * g / |g| for a first step) can differ by sign where a gradient is
+    # exactly 0 on one path (dead ReLU) and +-1e-12 on the other, so bound it by 2*lr
+    gnorm = torch.sqrt(sum((p.grad ** 2).sum() for p in meta.parameters())).item()
     for (n, a), b in zip(fm.meta_policy.named_parameters(), meta.parameters()):
-        # one Adam step from zero moments moves every element by ~lr*sign(g): compare the update
-        d_mine, d_ref = (a - dict(meta0.named_parameters())[n]), (b - dict(meta0.named_parameters())[n])
-        agree = (torch.sign(d_mine) == torch.sign(d_ref)).float().mean().item()
-        assert agree > 0.99, (n, agree)
-        assert (d_mine - d_ref).abs().max().item() <= 2 * 3e-4 + 1e-6, n
+        # tensors whose gradient is itself a near-cancellation (the value-head bias: mean of
+        # new_vals - vals - normalised adv) are judged against the global gradient norm
+        scale = max(b.grad.norm().item(), 1e-3 * gnorm)
+        rel = ((a.grad - b.grad).norm().item()) / scale
+        assert rel < 1e-4, (n, rel)
+        assert (a - b).abs().max().item() <= 2 * 3e-4 + 1e-6, n
