@@ -45,7 +45,10 @@
  *                        tile codes, and its weight/bias gradient
  *   merlin_tower_*       the data-movement stages around the conv2/conv3 GEMMs of the
  *                        towers (actor_critic.py:11-14): conv1 -> conv2 im2col from codes,
- *                        conv2 bias+ReLU -> conv3 im2col, and their backward passes
+ *                        conv2 bias+ReLU -> conv3 im2col, and their backward passes;
+ *                        merlin_tower_conv2_lut_*: Conv2d(3,32,k8,s4)+ReLU+Conv2d(32,64,k4,s2)
+ *                        of both towers (actor_critic.py:9-12) as table lookups from the
+ *                        tile codes, and the table gradient
  */
 #ifndef MERLIN_HIP_H
 #define MERLIN_HIP_H
@@ -199,6 +202,31 @@ int merlin_tower_conv3_im2col_fwd(const float *Z2_dev, const float *b2_dev, int6
                                   int32_t towers, float *A3_dev, void *stream);
 int merlin_tower_conv3_col2im_bwd(const float *dA3_dev, const float *Z2_dev, const float *b2_dev,
                                   int64_t n, int32_t towers, float *dZ2_dev, void *stream);
+/* Same, writing dZ2 chunk-major, dZ2c[t][ci/4][k*25 + p2][ci%4] (the histogram's input),
+ * and absmax_dev[0] = float bits of max |dZ2| (the histogram's fixed-point scale). */
+int merlin_tower_conv3_col2im_bwd_chunked(const float *dA3_dev, const float *Z2_dev,
+                                          const float *b2_dev, int64_t n, int32_t towers,
+                                          float *dZ2c_dev, uint32_t *absmax_dev, void *stream);
+
+/* conv1 + conv2 as table lookups (csrc/merlin_conv2lut.hip has the derivation).
+ * tables_dev float[towers][rows][64], rows = merlin_tower_conv2_lut_rows() = 2720:
+ *   row = base(type) + 4*v + j for conv2 tap (ky, kx), type = (ky&1, kx&1) with bases
+ *   0 / 20 / 120 / 220 for (0,0) / (0,1) / (1,0) / (1,1), j = 2*(ky>>1) + (kx>>1), and v
+ *   the classes of the tiles the tap's conv1 position covers, in base 5 (row-major tiles).
+ *   Row content: W2[:, :, ky, kx] applied to relu(conv1) of that tile combination.
+ * lut_fwd: Z2[t][k*25 + p2][co] = sum over the 16 taps of tables[t][row(tap, p2, frame k)][co]
+ *   (conv2 of relu(conv1(frame k)), no conv2 bias), frame k = codes[index ? index[k] : k].
+ * lut_bwd: dtables[t][row][co] = sum of dZ2 over the (k, p2) that read row at some tap,
+ *   given dZ2 chunk-major and its max |dZ2| (float bits, >= the true max) as written by
+ *   merlin_tower_conv3_col2im_bwd_chunked; summed in 64-bit fixed point (exact,
+ *   order-independent), overwritten, not accumulated.  A non-finite max gives NaN. */
+int merlin_tower_conv2_lut_rows(void);
+int merlin_tower_conv2_lut_fwd(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
+                               const float *tables_dev, int32_t towers, float *Z2_dev,
+                               void *stream);
+int merlin_tower_conv2_lut_bwd(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
+                               const float *dZ2c_dev, const uint32_t *absmax_dev, int32_t towers,
+                               float *dtables_dev, void *stream);
 
 #ifdef __cplusplus
 }

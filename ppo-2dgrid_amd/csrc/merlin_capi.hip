@@ -197,6 +197,7 @@ struct DeviceWs {
     int max_partials = 0;
     float *conv1_slabs = nullptr;
     int max_slabs = 0;
+    void *lut2_slabs = nullptr;  // conv2 table histogram: per-block 4-channel u64 slices
 };
 constexpr int MAX_DEV = 64;
 DeviceWs g_dev[MAX_DEV];
@@ -217,6 +218,7 @@ int device_ws(DeviceWs **out) {
         w.max_partials = WS_PARTIALS;
         HIP_TRY(hipMalloc(&w.conv1_slabs, sizeof(float) * (size_t)WS_SLABS * merlin::conv1_slab_floats(2)));
         w.max_slabs = WS_SLABS;
+        HIP_TRY(hipMalloc(&w.lut2_slabs, merlin::conv2_lut_slab_bytes(2, merlin::conv2_lut_fblocks(INT64_MAX / 64))));
         w.ready = true;
     }
     *out = &w;
@@ -521,7 +523,37 @@ int merlin_tower_conv3_im2col_fwd(const float *Z2, const float *b2, int64_t n, i
 int merlin_tower_conv3_col2im_bwd(const float *dA3, const float *Z2, const float *b2, int64_t n, int32_t towers,
                                   float *dZ2, void *stream) {
     if ((!dA3 || !Z2 || !b2 || !dZ2) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
-    HIP_TRY(merlin::launch_col2im3_bwd(dA3, Z2, b2, n, towers, dZ2, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_col2im3_bwd(dA3, Z2, b2, n, towers, 0, dZ2, nullptr, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_conv3_col2im_bwd_chunked(const float *dA3, const float *Z2, const float *b2, int64_t n,
+                                          int32_t towers, float *dZ2c, uint32_t *absmax, void *stream) {
+    if (!absmax || ((!dA3 || !Z2 || !b2 || !dZ2c) && n > 0)) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_col2im3_bwd(dA3, Z2, b2, n, towers, 1, dZ2c, absmax, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_conv2_lut_rows(void) { return merlin::conv2_lut_rows(); }
+
+int merlin_tower_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
+                               int32_t towers, float *Z2, void *stream) {
+    if ((!codes || !tables || !Z2) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_conv2_lut_fwd(codes, index, n, tables, towers, Z2, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_conv2_lut_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *dZ2c,
+                               const uint32_t *absmax, int32_t towers, float *dtables, void *stream) {
+    if (!dtables || ((!codes || !dZ2c || !absmax) && n > 0)) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_conv2_lut_bwd(codes, index, n, dZ2c, absmax, towers, dtables, ws->lut2_slabs,
+                                         (hipStream_t)stream));
     return MERLIN_OK;
 }
 

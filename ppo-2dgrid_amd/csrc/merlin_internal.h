@@ -77,7 +77,14 @@ hipError_t launch_conv1_im2col_bwd(const uint32_t *codes, const int64_t *index, 
                                    const float *bias, const float *dA2, int T, float *dtables, float *dbias,
                                    float *slabs, int max_slabs, hipStream_t s);
 hipError_t launch_im2col3_fwd(const float *Z2, const float *b2, int64_t n, int T, float *A3, hipStream_t s);
-hipError_t launch_col2im3_bwd(const float *dA3, const float *Z2, const float *b2, int64_t n, int T, float *dZ2,
-                              hipStream_t s);
+hipError_t launch_col2im3_bwd(const float *dA3, const float *Z2, const float *b2, int64_t n, int T, int chunked,
+                              float *dZ2, uint32_t *absmax, hipStream_t s);
+int conv2_lut_rows();
+int conv2_lut_fblocks(int64_t n);
+size_t conv2_lut_slab_bytes(int towers, int fblocks);
+hipError_t launch_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
+                                int towers, float *Z2, hipStream_t s);
+hipError_t launch_conv2_lut_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *dZ2c,
+                                const uint32_t *absmax, int towers, float *dT, void *slabs, hipStream_t s);
 
 }  // namespace merlin

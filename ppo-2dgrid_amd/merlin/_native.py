@@ -80,6 +80,10 @@ def lib():
     L.merlin_tower_conv2_im2col_bwd.argtypes = [vp, vp, i64, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_tower_conv3_im2col_fwd.argtypes = [vp, vp, i64, i32, vp, vp]
     L.merlin_tower_conv3_col2im_bwd.argtypes = [vp, vp, vp, i64, i32, vp, vp]
+    L.merlin_tower_conv3_col2im_bwd_chunked.argtypes = [vp, vp, vp, i64, i32, vp, vp, vp]
+    L.merlin_tower_conv2_lut_rows.restype = C.c_int
+    L.merlin_tower_conv2_lut_fwd.argtypes = [vp, vp, i64, vp, i32, vp, vp]
+    L.merlin_tower_conv2_lut_bwd.argtypes = [vp, vp, i64, vp, vp, i32, vp, vp]
     _lib = L
     return L
 
@@ -91,6 +95,8 @@ EXPORTED_SYMBOLS = (
     "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
     "merlin_conv1_lut_fwd", "merlin_conv1_lut_bwd", "merlin_tower_conv2_im2col_fwd",
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
+    "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
+    "merlin_tower_conv2_lut_bwd",
 )
 
 
@@ -291,3 +297,53 @@ def conv3_col2im_bwd(dA3, Z2, b2):
         check(lib().merlin_tower_conv3_col2im_bwd(ptr(dA3), ptr(Z2), ptr(b2), n, T, ptr(out), stream_of(Z2)),
               "merlin_tower_conv3_col2im_bwd")
     return out
+
+
+def conv3_col2im_bwd_chunked(dA3, Z2, b2):
+    """(dZ2c, absmax): dZ2 = [Z2 + b2 > 0] * col2im(dA3) chunk-major f32[T, 16, n*25, 4] (conv2_lut_bwd's
+    input) and int32[1] = float bits of max |dZ2| (the histogram's fixed-point scale)."""
+    T = int(Z2.shape[0])
+    n = int(Z2.shape[1]) // 25
+    out = torch.empty((T, 16, n * 25, 4), dtype=torch.float32, device=Z2.device)
+    absmax = torch.empty(1, dtype=torch.int32, device=Z2.device)
+    with KernelTimer.span("k_col2im3_bwd", n * T * (9 * 576 + 2 * 25 * 64) * 4):
+        check(lib().merlin_tower_conv3_col2im_bwd_chunked(ptr(dA3), ptr(Z2), ptr(b2), n, T, ptr(out), ptr(absmax),
+                                                          stream_of(Z2)), "merlin_tower_conv3_col2im_bwd_chunked")
+    return out, absmax
+
+
+LUT2_ROWS = 2720
+
+
+def conv2_lut_fwd(codes, index, tables):
+    """Z2 f32[T, n*25, 64] = conv2(relu(conv1(frame))) (no conv2 bias) by table lookups;
+    tables f32[T, 2720, 64] (merlin.actor_critic.conv2_tables)."""
+    T = int(tables.shape[0])
+    n = int(index.numel()) if index is not None else int(codes.shape[0])
+    assert tables.shape == (T, LUT2_ROWS, 64) and tables.dtype == torch.float32
+    assert codes.dtype == torch.int32 and codes.shape[-1] == OBS_WORDS
+    if index is not None:
+        assert index.dtype == torch.int64
+    out = torch.empty((T, n * 25, 64), dtype=torch.float32, device=codes.device)
+    # algorithmic bytes per frame: codes 32 (+ index 8) + Z2 written T*25*64*4; the
+    # 16 table rows per output position are L2-resident gathers (reported separately)
+    with KernelTimer.span("k_conv2_lut_fwd", n * (T * 25 * 64 * 4 + 32 + (8 if index is not None else 0))):
+        check(lib().merlin_tower_conv2_lut_fwd(ptr(codes), ptr(index), n, ptr(tables), T, ptr(out),
+                                               stream_of(codes)), "merlin_tower_conv2_lut_fwd")
+    return out
+
+
+def conv2_lut_bwd(codes, index, dZ2c, absmax=None):
+    """dtables f32[T, 2720, 64] from chunk-major dZ2c f32[T, 16, n*25, 4]; absmax int32[1] = float
+    bits of an upper bound on max |dZ2c| (computed here when not given)."""
+    T = int(dZ2c.shape[0])
+    n = int(dZ2c.shape[2]) // 25
+    if absmax is None:
+        absmax = dZ2c.abs().amax().reshape(1).view(torch.int32) if dZ2c.numel() else \
+            torch.zeros(1, dtype=torch.int32, device=dZ2c.device)
+    dt = torch.empty((T, LUT2_ROWS, 64), dtype=torch.float32, device=dZ2c.device)
+    # algorithmic bytes per frame: dZ2 read once (T*25*64*4) + codes/index per 4-channel slice block
+    with KernelTimer.span("k_conv2_lut_hist", n * (T * 25 * 64 * 4 + 16 * T * (32 + (8 if index is not None else 0)))):
+        check(lib().merlin_tower_conv2_lut_bwd(ptr(codes), ptr(index), n, ptr(dZ2c), ptr(absmax), T, ptr(dt),
+                                               stream_of(dZ2c)), "merlin_tower_conv2_lut_bwd")
+    return dt

@@ -142,6 +142,55 @@ class _Conv3Im2col(torch.autograd.Function):
         return dZ2, dZ2.sum(dim=1)
 
 
+class _Conv2LutTower(torch.autograd.Function):
+    """A3 = im2col(relu(conv2(relu(conv1(frame))) + b2)) of both towers from tile codes, with
+    conv1 + conv2 as lookups in the tables T (csrc/merlin_conv2lut.hip); backward returns
+    dT (a histogram of dZ2 over the rows each position read) and db2."""
+
+    @staticmethod
+    def forward(ctx, T2, b2, codes, index):
+        from . import _native as nat
+
+        b2c = b2.detach().contiguous()
+        Z2 = nat.conv2_lut_fwd(codes, index, T2.detach().contiguous())
+        ctx.save_for_backward(Z2, b2c, codes, index if index is not None else codes.new_empty(0))
+        ctx.has_index = index is not None
+        return nat.conv3_im2col_fwd(Z2, b2c)
+
+    @staticmethod
+    def backward(ctx, dA3):
+        from . import _native as nat
+
+        Z2, b2, codes, index = ctx.saved_tensors
+        dZ2c, absmax = nat.conv3_col2im_bwd_chunked(dA3.contiguous(), Z2, b2)
+        dT = nat.conv2_lut_bwd(codes, index if ctx.has_index else None, dZ2c, absmax)
+        # every output position reads exactly one row of tap (0, 0) (rows 0, 4, .., 16)
+        return dT, dT[:, 0:20:4, :].sum(1), None, None
+
+
+def _lut2_h1_index():
+    """Per conv1-position parity type (yp, xp), in table order ee, eo, oe, oo: the flat
+    indices (slot*20 + 4*class + 2*qy + qx) into P[t][co] of the 4 slot terms of every tile
+    combination v (tiles (ar, ac), ar <= yp, ac <= xp, row-major, class digits base 5)."""
+    out = []
+    for yp, xp in ((0, 0), (0, 1), (1, 0), (1, 1)):
+        tiles = [(ar, ac) for ar in range(yp + 1) for ac in range(xp + 1)]
+        V = 5 ** len(tiles)
+        idx = torch.empty((V, 4), dtype=torch.long)
+        for v in range(V):
+            digits = [(v // 5 ** (len(tiles) - 1 - i)) % 5 for i in range(len(tiles))]
+            for dy in range(2):
+                for dx in range(2):
+                    tile = tiles.index(((yp + dy) >> 1, (xp + dx) >> 1))
+                    qy, qx = (yp + dy) & 1, (xp + dx) & 1
+                    idx[v, 2 * dy + dx] = (2 * dy + dx) * 20 + 4 * digits[tile] + 2 * qy + qx
+        out.append(((yp, xp), idx))
+    return out
+
+
+_LUT2_H1 = _lut2_h1_index()
+
+
 class CNNActorCritic(nn.Module):
     def __init__(self, obs_shape, act_dim, hidden_dim=512):
         super().__init__()
@@ -151,7 +200,10 @@ class CNNActorCritic(nn.Module):
         self.actor = _head(self.actor_extractor.output_dim, hidden_dim, act_dim, 0.01)
         self.critic = _head(self.critic_extractor.output_dim, hidden_dim, 1, 1.0)
         self._atlas = None  # f32 [5, 3, 8, 8] / 255 on the model's device (codes path only)
-        self.codes_impl = "gemm"  # "gemm" (tower as hipBLASLt GEMMs) | "lut_nchw" (conv1 LUT + MIOpen convs)
+        self._lut2_idx = None
+        # "lut2": conv1+conv2 as table lookups, conv3/fc as hipBLASLt GEMMs (default)
+        # "gemm": conv1 lookups, conv2/conv3/fc as GEMMs | "lut_nchw": conv1 lookups + MIOpen convs
+        self.codes_impl = "lut2"
 
     # -- tile-code path (GPU envs) --------------------------------------------------
     def _atlas_on(self, device):
@@ -170,20 +222,32 @@ class CNNActorCritic(nn.Module):
         P = torch.einsum("tocakbl,zcekfl->toabzef", W, A)
         return P.reshape(2, 32, 4, 20), torch.stack([c1a.bias, c1c.bias])
 
-    def _forward_codes(self, codes, index=None):
-        """Both towers from tile codes as GEMMs (csrc/merlin_tower.hip for the data movement):
-        A2 = im2col(relu(conv1)) -> Z2 = A2 @ W2t -> A3 = im2col(relu(Z2 + b2)) ->
-        relu(A3 @ W3t + b3) -> fc1 (columns permuted to the (position, channel) row order)
-        -> heads.  The GEMMs are batched over the two towers (hipBLASLt fp32)."""
-        if self.codes_impl == "lut_nchw":
-            return self._forward_codes_nchw(codes, index)
+    def conv2_tables(self):
+        """T2[t][row][co] (t: actor, critic; 2720 rows, csrc/merlin_conv2lut.hip layout):
+        W2[:, :, ky, kx] applied to relu(conv1) of each tile combination, from P and b1 by
+        differentiable ops, so autograd maps dT2 to the conv1 and conv2 weight gradients."""
+        P, b1 = self.conv1_tables()
+        Pf = P.reshape(2, 32, 80)
+        if self._lut2_idx is None or self._lut2_idx[0][1].device != Pf.device:
+            self._lut2_idx = [(k, idx.to(Pf.device)) for k, idx in _LUT2_H1]
+        ea, ec = self.actor_extractor.network, self.critic_extractor.network
+        W2 = torch.stack([ea[2].weight, ec[2].weight])  # [2, co 64, ci 32, ky 4, kx 4]
+        parts = []
+        for (yp, xp), idx in self._lut2_idx:
+            H = torch.relu(b1.unsqueeze(-1) + Pf[:, :, idx].sum(-1))  # [2, 32, V]
+            Wsel = W2[:, :, :, yp::2, xp::2].permute(0, 2, 3, 4, 1).reshape(2, 32, 256)  # ci, (a, b), co
+            parts.append(torch.bmm(H.transpose(1, 2), Wsel).reshape(2, -1, 64))  # rows 4*v + j
+        return torch.cat(parts, 1)
+
+    def _forward_codes_lut2(self, codes, index=None):
         ea, ec = self.actor_extractor.network, self.critic_extractor.network
         n = index.numel() if index is not None else codes.shape[0]
-        tables, b1 = self.conv1_tables()
-        A2 = _Conv2Im2colFromCodes.apply(tables, b1, codes, index)  # [2, n*25, 512]
-        W2t = torch.stack([ea[2].weight, ec[2].weight]).permute(0, 3, 4, 2, 1).reshape(2, 512, 64)
-        Z2 = torch.bmm(A2, W2t)  # [2, n*25, 64]
-        A3 = _Conv3Im2col.apply(Z2, torch.stack([ea[2].bias, ec[2].bias]))  # [2, n*9, 576]
+        A3 = _Conv2LutTower.apply(self.conv2_tables(), torch.stack([ea[2].bias, ec[2].bias]), codes, index)
+        return self._tower_tail(A3, n)
+
+    def _tower_tail(self, A3, n):
+        """conv3 (GEMM on the im2col rows A3 [2, n*9, 576]) -> fc1 -> heads."""
+        ea, ec = self.actor_extractor.network, self.critic_extractor.network
         W3t = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64)
         b3 = torch.stack([ea[4].bias, ec[4].bias]).unsqueeze(1)
         a3 = torch.relu(torch.baddbmm(b3, A3, W3t)).view(2, n, 576)  # rows (p3, co)
@@ -194,6 +258,24 @@ class CNNActorCritic(nn.Module):
         logits = F.linear(h[0], self.actor[2].weight, self.actor[2].bias)
         value = F.linear(h[1], self.critic[2].weight, self.critic[2].bias).squeeze(-1)
         return logits, value
+
+    def _forward_codes(self, codes, index=None):
+        """Both towers from tile codes as GEMMs (csrc/merlin_tower.hip for the data movement):
+        A2 = im2col(relu(conv1)) -> Z2 = A2 @ W2t -> A3 = im2col(relu(Z2 + b2)) ->
+        relu(A3 @ W3t + b3) -> fc1 (columns permuted to the (position, channel) row order)
+        -> heads.  The GEMMs are batched over the two towers (hipBLASLt fp32)."""
+        if self.codes_impl == "lut2":
+            return self._forward_codes_lut2(codes, index)
+        if self.codes_impl == "lut_nchw":
+            return self._forward_codes_nchw(codes, index)
+        ea, ec = self.actor_extractor.network, self.critic_extractor.network
+        n = index.numel() if index is not None else codes.shape[0]
+        tables, b1 = self.conv1_tables()
+        A2 = _Conv2Im2colFromCodes.apply(tables, b1, codes, index)  # [2, n*25, 512]
+        W2t = torch.stack([ea[2].weight, ec[2].weight]).permute(0, 3, 4, 2, 1).reshape(2, 512, 64)
+        Z2 = torch.bmm(A2, W2t)  # [2, n*25, 64]
+        A3 = _Conv3Im2col.apply(Z2, torch.stack([ea[2].bias, ec[2].bias]))  # [2, n*9, 576]
+        return self._tower_tail(A3, n)
 
     def _forward_codes_nchw(self, codes, index=None):
         tables, bias = self.conv1_tables()
