@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--size", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tiers", action="store_true")
+    ap.add_argument("--no-dedup", action="store_true",
+                    help="evaluate the towers on every minibatch sample (no distinct-frame grouping)")
     ap.add_argument("--fomaml", action="store_true",
                     help="cfg 5 instead: FOMAML meta-iterations, tasks_per_batch=32 x k_steps=256")
     ap.add_argument("--tasks", type=int, default=32)
@@ -217,7 +219,8 @@ def main():
                        env_offset=rank * N)
     torch.manual_seed(777)
     agent = PPO(env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=args.epochs, batch_size=B,
-                minibatch_size=B // args.minibatches, vf_coef=0.5, ent_coef=0.05, device=device, dp=dp)
+                minibatch_size=B // args.minibatches, vf_coef=0.5, ent_coef=0.05, device=device, dp=dp,
+                dedup=not args.no_dedup)
 
     state["phase"] = "warmup"
     for _ in range(args.warmup):
@@ -284,6 +287,9 @@ def main():
                           "unit": "TFLOP/s", "frac": round(loop_tflops / FP32_PEAK_TFLOPS, 4),
                           "flop_per_env_step": flop_per_step},
         "phases_ms": {"rollout": round(rollout_ms, 2), "update": round(update_ms, 2)},
+        # towers evaluated once per distinct observation of a minibatch (merlin/dedup.py)
+        "distinct_frames_per_sample": (round(agent.last_distinct_frac, 4)
+                                       if agent.last_distinct_frac is not None else None),
         "kernels": kernels,
     }
     state["phase"] = "tiers"

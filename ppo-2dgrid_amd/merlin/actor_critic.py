@@ -290,8 +290,15 @@ class CNNActorCritic(nn.Module):
         action = _sample_or_argmax(logits, logp_all, probs, deterministic)
         return action, logp_all.gather(-1, action.unsqueeze(-1)).squeeze(-1), value
 
-    def evaluate_codes(self, codes, actions, index=None):
-        logits, value = self._forward_codes(codes, index)
+    def evaluate_codes(self, codes, actions, index=None, groups=None):
+        """groups = (rep_idx, inv) (merlin.dedup.FrameGroups.minibatch): the towers run on the
+        distinct frames rep_idx only and sample k takes row inv[k] (same values and gradients)."""
+        if groups is not None:
+            rep_idx, inv = groups
+            logits, value = self._forward_codes(codes, rep_idx)
+            logits, value = logits[inv], value[inv]
+        else:
+            logits, value = self._forward_codes(codes, index)
         logp_all, probs = _categorical(logits)
         logp = logp_all.gather(-1, actions.long().unsqueeze(-1)).squeeze(-1)
         return logp, _entropy(logp_all, probs), value

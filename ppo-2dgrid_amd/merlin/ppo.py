@@ -45,7 +45,8 @@ INV255 = 1.0 / 255.0
 class PPO:
     def __init__(self, env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=10,
                  batch_size=2048, minibatch_size=256, vf_coef=0.5, ent_coef=0.01, device="cuda",
-                 *, dp: DataParallel | None = None, perm_fn=None, conv1_from_codes: bool = True):
+                 *, dp: DataParallel | None = None, perm_fn=None, conv1_from_codes: bool = True,
+                 dedup: bool = True):
         self.env = env
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -59,6 +60,9 @@ class PPO:
         # vectorised path: evaluate conv1 from the tile codes (merlin_conv1_lut_*) instead of
         # expanding 37.6 KB frames and running the generic convolution
         self.conv1_from_codes = conv1_from_codes
+        # evaluate each distinct observation of a minibatch once (merlin/dedup.py)
+        self.dedup = dedup
+        self.last_distinct_frac = None  # distinct frames / samples over the last update
         self.episode_returns: list[float] = []
         self.episode_lengths: list[int] = []
 
@@ -207,13 +211,26 @@ class PPO:
     def _sgd(self, B, codes, states, actions, logp_old, adv, returns):
         totals = torch.zeros(6, dtype=torch.float64, device=self.device)
         nb = 0
+        use_codes = codes is not None and self.conv1_from_codes
+        groups = None
+        if use_codes and self.dedup:
+            from .dedup import FrameGroups
+
+            groups = FrameGroups(codes)
+            if not groups.ok:  # a 64-bit hash collision: evaluate every sample this update
+                groups = None
+        distinct = torch.zeros((), dtype=torch.int64, device=self.device)
         for epoch in range(self.update_epochs):
             idxs = self._perm(B, epoch)
             for start in range(0, B, self.minibatch_size):
                 mb_idx = idxs[start:start + self.minibatch_size]
                 lp_old, a_mb, ret_mb = logp_old[mb_idx], adv[mb_idx], returns[mb_idx]
-                if codes is not None and self.conv1_from_codes:
-                    logp_new, entropy, values = self.ac.evaluate_codes(codes, actions[mb_idx], index=mb_idx)
+                if use_codes:
+                    g = groups.minibatch(mb_idx) if groups is not None else None
+                    if g is not None:
+                        distinct += g[0].numel()
+                    logp_new, entropy, values = self.ac.evaluate_codes(codes, actions[mb_idx], index=mb_idx,
+                                                                       groups=g)
                 else:
                     obs, pre = self._minibatch_obs(codes, states, mb_idx)
                     logp_new, entropy, values = self.ac.evaluate(obs, actions[mb_idx], prescaled=pre)
@@ -238,6 +255,8 @@ class PPO:
                                            clipfrac, grad_norm.detach()]).double()
                 nb += 1
         t = totals.cpu().tolist()
+        if groups is not None:
+            self.last_distinct_frac = float(distinct.item()) / float(self.update_epochs * B)
         return aggregate_ppo_update_metrics(*t, nb)
 
     def train(self, total_steps=100_000):

@@ -63,3 +63,45 @@ def test_ppo_refuses_cpu_device():
 
     with pytest.raises(nat.MerlinNativeError):
         PPO(E(), device="cpu")
+
+
+def test_frame_groups_exact_on_cpu():
+    """merlin.dedup: groups are exactly the sets of equal code rows (CPU tensors)."""
+    import torch
+
+    from merlin.dedup import FrameGroups, hash_codes
+
+    g = torch.Generator().manual_seed(5)
+    base = torch.randint(-2**31, 2**31 - 1, (37, 8), generator=g, dtype=torch.int64).to(torch.int32)
+    pick = torch.randint(0, 37, (1000,), generator=g)
+    codes = base[pick].contiguous()
+    fg = FrameGroups(codes)
+    assert fg.ok and fg.num_groups == torch.unique(pick).numel()
+    assert torch.equal(codes[fg.rep[fg.uid]], codes)
+    # same group <=> same row
+    same_uid = fg.uid[:, None] == fg.uid[None, :]
+    same_row = (codes[:, None, :] == codes[None, :, :]).all(-1)
+    assert torch.equal(same_uid, same_row)
+    mb = torch.randperm(1000, generator=g)[:300]
+    rep_idx, inv = fg.minibatch(mb)
+    assert torch.equal(codes[rep_idx[inv]], codes[mb])
+    assert rep_idx.numel() == torch.unique(pick[mb]).numel()
+    # a word flip changes the hash
+    c2 = codes.clone()
+    c2[0, 3] ^= 1
+    assert hash_codes(c2)[0] != hash_codes(codes)[0]
+
+
+def test_frame_groups_detect_collision():
+    """A forced hash collision is caught by the word-for-word check (ok=False)."""
+    import torch
+
+    import merlin.dedup as D
+
+    codes = torch.tensor([[1, 2, 3, 4, 5, 6, 7, 8], [8, 7, 6, 5, 4, 3, 2, 1]], dtype=torch.int32)
+    orig = D.hash_codes
+    try:
+        D.hash_codes = lambda c: torch.zeros(c.shape[0], dtype=torch.int64)
+        assert not D.FrameGroups(codes).ok
+    finally:
+        D.hash_codes = orig
