@@ -216,17 +216,18 @@ int merlin_tower_conv3_col2im_bwd_chunked(const float *dA3_dev, const float *Z2_
  *   Row content: W2[:, :, ky, kx] applied to relu(conv1) of that tile combination.
  * lut_fwd: Z2[t][k*25 + p2][co] = sum over the 16 taps of tables[t][row(tap, p2, frame k)][co]
  *   (conv2 of relu(conv1(frame k)), no conv2 bias), frame k = codes[index ? index[k] : k].
- * lut_bwd: dtables[t][row][co] = sum of dZ2 over the (k, p2) that read row at some tap,
- *   given dZ2 chunk-major and its max |dZ2| (float bits, >= the true max) as written by
+ * lut_bwd: dtables[t][row][co] = sum of dZ2 over the (k, p2) that read row at some tap, for
+ *   frame k = codes_dev[k] (the minibatch's own rows, no index), given dZ2 chunk-major and its
+ *   max |dZ2| (float bits, >= the true max) as written by
  *   merlin_tower_conv3_col2im_bwd_chunked; summed in 64-bit fixed point (exact,
  *   order-independent), overwritten, not accumulated.  A non-finite max gives NaN. */
 int merlin_tower_conv2_lut_rows(void);
 int merlin_tower_conv2_lut_fwd(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
                                const float *tables_dev, int32_t towers, float *Z2_dev,
                                void *stream);
-int merlin_tower_conv2_lut_bwd(const uint32_t *codes_dev, const int64_t *index_dev, int64_t n,
-                               const float *dZ2c_dev, const uint32_t *absmax_dev, int32_t towers,
-                               float *dtables_dev, void *stream);
+int merlin_tower_conv2_lut_bwd(const uint32_t *codes_dev, int64_t n, const float *dZ2c_dev,
+                               const uint32_t *absmax_dev, int32_t towers, float *dtables_dev,
+                               void *stream);
 
 #ifdef __cplusplus
 }

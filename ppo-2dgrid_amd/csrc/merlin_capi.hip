@@ -545,14 +545,14 @@ int merlin_tower_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int6
     return MERLIN_OK;
 }
 
-int merlin_tower_conv2_lut_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *dZ2c,
-                               const uint32_t *absmax, int32_t towers, float *dtables, void *stream) {
+int merlin_tower_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
+                               int32_t towers, float *dtables, void *stream) {
     if (!dtables || ((!codes || !dZ2c || !absmax) && n > 0)) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     DeviceWs *ws = nullptr;
     int rc = device_ws(&ws);
     if (rc) return rc;
-    HIP_TRY(merlin::launch_conv2_lut_bwd(codes, index, n, dZ2c, absmax, towers, dtables, ws->lut2_slabs,
+    HIP_TRY(merlin::launch_conv2_lut_bwd(codes, n, dZ2c, absmax, towers, dtables, ws->lut2_slabs,
                                          (hipStream_t)stream));
     return MERLIN_OK;
 }

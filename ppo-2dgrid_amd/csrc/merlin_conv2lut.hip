@@ -134,7 +134,7 @@ __global__ __launch_bounds__(64 * FWD_WAVES) void k_conv2_lut_fwd(const uint32_t
 // sums are exact and order-independent, so the result is bitwise reproducible.
 // Scale 2^K with K = 62 - ceil(log2(n*25 + 1)) - e, max|dZ2| < 2^e (from k_col2im3_bwd):
 // no partial or total sum of a row can overflow, and each term is rounded to 2^-K.
-constexpr int HIST_WAVES = 16, HIST_G = 8, HCH = 4, NHCHUNK = C2 / HCH;
+constexpr int HIST_WAVES = 16, HIST_G = 4, HCH = 4, NHCHUNK = C2 / HCH;
 constexpr int HSLICE = NROW * HCH;  // u64 per slice table (87,040 B)
 
 __device__ __forceinline__ int fixed_exp(uint32_t absmax_bits, int64_t n) {
@@ -146,50 +146,103 @@ __device__ __forceinline__ int fixed_exp(uint32_t absmax_bits, int64_t n) {
     return 62 - lg - e;
 }
 
-__global__ __launch_bounds__(64 * HIST_WAVES) void k_conv2_lut_hist(const uint32_t *__restrict__ codes,
-                                                                   const int64_t *__restrict__ index, int64_t n,
+// round(g * 2^K) from the float's bits (|g| * 2^K < 2^38 by the choice of K)
+__device__ __forceinline__ long long to_fixed(float g, int K) {
+    const uint32_t bits = __float_as_uint(g);
+    int E = (bits >> 23) & 0xff;
+    uint32_t m = bits & 0x7fffffu;
+    if (E) m |= 0x800000u; else E = 1;
+    const int sh = E - 150 + K;
+    long long q;
+    if (sh >= 0) q = (long long)m << sh;
+    else if (sh > -26) q = (long long)((m + (1u << (-sh - 1))) >> (-sh));
+    else q = 0;
+    return (bits >> 31) ? -q : q;
+}
+
+// codes here are the minibatch's own rows (the caller gathers them once), so a wave's group
+// of frames is one contiguous 128-B read; the next group's dZ2 slice and code words are
+// loaded into registers while the current group is accumulated.
+__global__ __launch_bounds__(64 * HIST_WAVES) void k_conv2_lut_hist(const uint32_t *__restrict__ codes, int64_t n,
                                                                    const float *__restrict__ dZ2c,
                                                                    const uint32_t *__restrict__ absmax, int fblocks,
                                                                    unsigned long long *__restrict__ slabs) {
     __shared__ unsigned long long tab[HSLICE];
-    __shared__ uint8_t cls_all[HIST_WAVES][HIST_G * 49 + 8];
-    __shared__ __align__(16) float g_all[HIST_WAVES][HIST_G * P2 * HCH];
+    __shared__ uint32_t words_all[HIST_WAVES][HIST_G * MERLIN_OBS_WORDS];
+    // per frame, per parity type and 2x2-tile window origin (r, c) in 0..5: the type's table
+    // row base + 4 v (rows of tap j are that + j)
+    __shared__ uint16_t rb_all[HIST_WAVES][HIST_G * 4 * 36];
+    // the group's dZ2 slice already in fixed point: [frame][position][channel] as int64
+    __shared__ __align__(16) long long q_all[HIST_WAVES][HIST_G * P2 * HCH];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tc = blockIdx.x / fblocks, fb = blockIdx.x - tc * fblocks;  // tc = tower*16 + chunk
-    uint8_t *cls = cls_all[wv];
-    float *gl = g_all[wv];
+    uint32_t *words = words_all[wv];
+    uint16_t *rb = rb_all[wv];
+    long long *qs = q_all[wv];
     for (int k = threadIdx.x; k < HSLICE; k += blockDim.x) tab[k] = 0ull;
-    const double scale = ldexp(1.0, fixed_exp(*absmax, n));
+    const int K = fixed_exp(*absmax, n);
     __syncthreads();
     // this lane's tap: type (yp, xp), tap index j within the type, tile offset (a, b)
     const int k = lane >> 2, c = lane & 3, ky = k >> 2, kx = k & 3;
-    const int yp = ky & 1, xp = kx & 1, a = ky >> 1, b = kx >> 1, j = 2 * a + b;
-    const int base = yp ? (xp ? 220 : 120) : (xp ? 20 : 0);
+    const int type = 2 * (ky & 1) + (kx & 1), a = ky >> 1, b = kx >> 1, j = 2 * a + b;
     int64_t per = (n + fblocks - 1) / fblocks;
     per = (per + HIST_G - 1) / HIST_G * HIST_G;
     const int64_t f0 = (int64_t)fb * per, f1 = std::min<int64_t>(n, f0 + per);
-    const float *src0 = dZ2c + (size_t)tc * n * (P2 * HCH);
-    for (int64_t g = f0 + (int64_t)wv * HIST_G; g < f1; g += (int64_t)HIST_WAVES * HIST_G) {
+    const float4 *src0 = reinterpret_cast<const float4 *>(dZ2c) + (size_t)tc * n * P2;
+    const int64_t stride = (int64_t)HIST_WAVES * HIST_G;
+    float4 pg0 = make_float4(0.f, 0.f, 0.f, 0.f), pg1 = pg0;
+    uint32_t pw = 0u;
+    auto prefetch = [&](int64_t gg) {
+        const int nf = (int)std::min<int64_t>(HIST_G, f1 - gg);
+        const float4 *src = src0 + (size_t)gg * P2;
+        if (lane < nf * P2) pg0 = src[lane];
+        if (lane + 64 < nf * P2) pg1 = src[lane + 64];
+        if (lane < nf * MERLIN_OBS_WORDS) pw = codes[gg * MERLIN_OBS_WORDS + lane];
+    };
+    int64_t g = f0 + (int64_t)wv * HIST_G;
+    if (g < f1) prefetch(g);
+    for (; g < f1; g += stride) {
         const int nf = (int)std::min<int64_t>(HIST_G, f1 - g);
-        const float4 *src = reinterpret_cast<const float4 *>(src0 + (size_t)g * (P2 * HCH));
-        float4 *g4 = reinterpret_cast<float4 *>(gl);
-        for (int e = lane; e < nf * P2; e += 64) g4[e] = src[e];
-        stage_classes(codes, index, g, nf, lane, cls);  // ends with the wave's LDS writes visible
+        if (lane < nf * P2) {
+            longlong2 *d = reinterpret_cast<longlong2 *>(qs + lane * HCH);
+            d[0] = make_longlong2(to_fixed(pg0.x, K), to_fixed(pg0.y, K));
+            d[1] = make_longlong2(to_fixed(pg0.z, K), to_fixed(pg0.w, K));
+        }
+        if (lane + 64 < nf * P2) {
+            longlong2 *d = reinterpret_cast<longlong2 *>(qs + (lane + 64) * HCH);
+            d[0] = make_longlong2(to_fixed(pg1.x, K), to_fixed(pg1.y, K));
+            d[1] = make_longlong2(to_fixed(pg1.z, K), to_fixed(pg1.w, K));
+        }
+        if (lane < nf * MERLIN_OBS_WORDS) words[lane] = pw;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes are visible to it
+        __builtin_amdgcn_wave_barrier();
+        if (g + stride < f1) prefetch(g + stride);
+        for (int e = lane; e < nf * 4 * 36; e += 64) {
+            const int f = e / 144, r = e - f * 144, ty = r / 36, w = r - ty * 36, wr = w / 6, wc = w - wr * 6;
+            const uint32_t *fw = words + f * MERLIN_OBS_WORDS;
+            auto cls = [&](int cell) { return (int)min((fw[cell >> 3] >> ((cell & 7) * 4)) & 0xfu, 4u); };
+            const int cell = wr * 7 + wc;
+            const int c00 = cls(cell);
+            int v, base;
+            if (ty == 0) { v = c00; base = 0; }
+            else if (ty == 1) { v = 5 * c00 + cls(cell + 1); base = 20; }
+            else if (ty == 2) { v = 5 * c00 + cls(cell + 7); base = 120; }
+            else { v = 125 * c00 + 25 * cls(cell + 1) + 5 * cls(cell + 7) + cls(cell + 8); base = 220; }
+            rb[e] = (uint16_t)(base + 4 * v);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
         for (int f = 0; f < nf; f++) {
-            const uint8_t *cf = cls + f * 49 + a * 7 + b;
-            const float *gf = gl + f * (P2 * HCH) + c;
-#pragma unroll 5
+            const uint16_t *rf = rb + f * 144 + type * 36 + a * 6 + b;
+            const long long *qf = qs + f * (P2 * HCH) + c;
+            unsigned long long *tc0 = tab + j * HCH + c;
+#pragma unroll
             for (int p = 0; p < P2; p++) {
-                const int py = p / 5, px = p - (p / 5) * 5;
-                const float gv = gf[p * HCH];
-                const uint8_t *cw = cf + py * 7 + px;
-                const int c00 = cw[0], c01 = cw[1], c10 = cw[7], c11 = cw[8];
-                int v = c00;
-                v = xp ? 5 * v + c01 : v;
-                v = yp ? 5 * v + c10 : v;
-                v = (xp & yp) ? 5 * v + c11 : v;
-                const long long q = __double2ll_rn((double)gv * scale);
-                if (q != 0) atomicAdd(&tab[(base + 4 * v + j) * HCH + c], (unsigned long long)q);
+                const long long q = qf[p * HCH];  // constant offsets: immediate ds_read fields
+                const int row = rf[(p / 5) * 6 + p % 5];
+                if (q != 0) atomicAdd(tc0 + row * HCH, (unsigned long long)q);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -239,13 +292,13 @@ int conv2_lut_fblocks(int64_t n) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(8, (n + 255) / 256));
 }
 
-hipError_t launch_conv2_lut_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *dZ2c,
-                                const uint32_t *absmax, int towers, float *dT, void *slabs, hipStream_t s) {
+hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
+                                int towers, float *dT, void *slabs, hipStream_t s) {
     if (n <= 0) return hipMemsetAsync(dT, 0, sizeof(float) * towers * NROW * C2, s);
     const int fblocks = conv2_lut_fblocks(n);
     auto *sl = reinterpret_cast<unsigned long long *>(slabs);
     hipLaunchKernelGGL(k_conv2_lut_hist, dim3(towers * NHCHUNK * fblocks), dim3(64 * HIST_WAVES), 0, s, codes,
-                       index, n, dZ2c, absmax, fblocks, sl);
+                       n, dZ2c, absmax, fblocks, sl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_conv2_lut_fold, dim3((towers * NROW * C2 + 255) / 256), dim3(256), 0, s, sl, absmax, n,

@@ -84,7 +84,7 @@ int conv2_lut_fblocks(int64_t n);
 size_t conv2_lut_slab_bytes(int towers, int fblocks);
 hipError_t launch_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
                                 int towers, float *Z2, hipStream_t s);
-hipError_t launch_conv2_lut_bwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *dZ2c,
-                                const uint32_t *absmax, int towers, float *dT, void *slabs, hipStream_t s);
+hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
+                                int towers, float *dT, void *slabs, hipStream_t s);
 
 }  // namespace merlin

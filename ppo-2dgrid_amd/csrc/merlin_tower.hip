@@ -262,21 +262,15 @@ __global__ __launch_bounds__(BLK) void k_im2col3_fwd(const float4 *__restrict__ 
 }
 
 // dZ2[t][s*25+p2][ci] = [Z2 + b2 > 0] * sum_{(p3, tap) covering p2} dA3[t][s*9+p3][tap*64+ci]
-// chunked != 0 writes dZ2 chunk-major, [t][ci/4][s*25+p2][ci%4] (the conv2 table histogram's
-// input) and raises *absmax (float bits) to max |dZ2| (the histogram's fixed-point scale).
 __global__ __launch_bounds__(BLK) void k_col2im3_bwd(const float4 *__restrict__ dA3, const float4 *__restrict__ Z2,
-                                                     const float *__restrict__ b2, int64_t n, int T, int chunked,
-                                                     float4 *__restrict__ dZ2, uint32_t *__restrict__ absmax) {
-    float amax = 0.0f;
+                                                     const float *__restrict__ b2, int64_t n, int T,
+                                                     float4 *__restrict__ dZ2) {
     for (int64_t ts = blockIdx.x; ts < (int64_t)T * n; ts += gridDim.x) {
         const int t = (int)(ts / n);
-        const int64_t s = ts - (int64_t)t * n;
         const float4 *base = dA3 + ts * (P3 * K3 / 4);
         const float4 *bb = reinterpret_cast<const float4 *>(b2 + t * C2);
         for (int e = threadIdx.x; e < P2 * C2 / 4; e += BLK) {
-            // chunked: consecutive threads walk the positions of one 4-channel chunk
-            const int p2 = chunked ? e % P2 : e >> 4, ci4 = chunked ? e / P2 : e & 15;
-            const int y = p2 / 5, x = p2 - (p2 / 5) * 5;
+            const int p2 = e >> 4, ci4 = e & 15, y = p2 / 5, x = p2 - (p2 / 5) * 5;
             float4 g = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             for (int oy = max(0, y - 2); oy <= min(2, y); oy++)
                 for (int ox = max(0, x - 2); ox <= min(2, x); ox++) {
@@ -287,24 +281,64 @@ __global__ __launch_bounds__(BLK) void k_col2im3_bwd(const float4 *__restrict__ 
                     g.z += v.z;
                     g.w += v.w;
                 }
-            const float4 z = Z2[ts * (P2 * C2 / 4) + p2 * 16 + ci4];
+            const float4 z = Z2[ts * (P2 * C2 / 4) + e];
+            const float4 b = bb[ci4];
+            dZ2[ts * (P2 * C2 / 4) + e] =
+                make_float4(z.x + b.x > 0.0f ? g.x : 0.0f, z.y + b.y > 0.0f ? g.y : 0.0f,
+                            z.z + b.z > 0.0f ? g.z : 0.0f, z.w + b.w > 0.0f ? g.w : 0.0f);
+        }
+    }
+}
+
+// Same map, written chunk-major dZ2c[t][ci/4][s*25+p2][ci%4] (the conv2 table histogram's
+// input), raising *absmax (float bits) to max |dZ2| (the histogram's fixed-point scale).
+// A block takes CF consecutive frames of one tower: their dA3 rows (CF x 20.7 KB) are staged
+// in LDS with coalesced loads, and each 4-channel chunk's CF x 25 outputs are one contiguous
+// run of the destination.
+constexpr int CF = 2;
+__global__ __launch_bounds__(BLK) void k_col2im3_bwd_chunked(const float4 *__restrict__ dA3,
+                                                             const float4 *__restrict__ Z2,
+                                                             const float *__restrict__ b2, int64_t n, int T,
+                                                             float4 *__restrict__ dZ2c,
+                                                             uint32_t *__restrict__ absmax) {
+    __shared__ float4 tile[CF * P3 * K3 / 4];
+    float amax = 0.0f;
+    const int64_t groups = (n + CF - 1) / CF;
+    for (int64_t tg = blockIdx.x; tg < (int64_t)T * groups; tg += gridDim.x) {
+        const int t = (int)(tg / groups);
+        const int64_t s0 = (tg - (int64_t)t * groups) * CF;
+        const int nf = (int)std::min<int64_t>(CF, n - s0);
+        const float4 *src = dA3 + ((size_t)t * n + s0) * (P3 * K3 / 4);
+        __syncthreads();  // previous group's tile consumed
+        for (int e = threadIdx.x; e < nf * (P3 * K3 / 4); e += BLK) tile[e] = src[e];
+        __syncthreads();
+        const float4 *bb = reinterpret_cast<const float4 *>(b2 + t * C2);
+        for (int e = threadIdx.x; e < 16 * nf * P2; e += BLK) {
+            const int ci4 = e / (nf * P2), r = e - ci4 * (nf * P2), f = r / P2, p2 = r - f * P2;
+            const int y = p2 / 5, x = p2 - (p2 / 5) * 5;
+            const float4 *tf = tile + f * (P3 * K3 / 4);
+            float4 g = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            for (int oy = max(0, y - 2); oy <= min(2, y); oy++)
+                for (int ox = max(0, x - 2); ox <= min(2, x); ox++) {
+                    const int tap = (y - oy) * 3 + (x - ox);
+                    const float4 v = tf[(oy * 3 + ox) * (K3 / 4) + tap * (C2 / 4) + ci4];
+                    g.x += v.x;
+                    g.y += v.y;
+                    g.z += v.z;
+                    g.w += v.w;
+                }
+            const float4 z = Z2[((size_t)t * n + s0 + f) * (P2 * C2 / 4) + p2 * 16 + ci4];
             const float4 b = bb[ci4];
             const float4 d = make_float4(z.x + b.x > 0.0f ? g.x : 0.0f, z.y + b.y > 0.0f ? g.y : 0.0f,
                                          z.z + b.z > 0.0f ? g.z : 0.0f, z.w + b.w > 0.0f ? g.w : 0.0f);
-            if (chunked) {
-                dZ2[(((size_t)t * 16 + ci4) * n + s) * P2 + p2] = d;
-                amax = fmaxf(amax, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
-            } else {
-                dZ2[(size_t)ts * (P2 * C2 / 4) + p2 * 16 + ci4] = d;
-            }
+            dZ2c[(((size_t)t * 16 + ci4) * n + s0 + f) * P2 + p2] = d;
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
         }
     }
-    if (chunked) {
-        // NaN/inf propagate as a non-finite max (the histogram then returns NaN)
-        for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
-        if (amax != amax) amax = __int_as_float(0x7f800000);
-        if ((threadIdx.x & 63) == 0) atomicMax(absmax, __float_as_uint(amax));
-    }
+    // NaN/inf propagate as a non-finite max (the histogram then returns NaN)
+    for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+    if (amax != amax) amax = __int_as_float(0x7f800000);
+    if ((threadIdx.x & 63) == 0) atomicMax(absmax, __float_as_uint(amax));
 }
 
 int grid_cap(int64_t rows) { return (int)std::max<int64_t>(1, std::min<int64_t>(rows, 256 * 16)); }
@@ -348,12 +382,17 @@ hipError_t launch_col2im3_bwd(const float *dA3, const float *Z2, const float *b2
                               float *dZ2, uint32_t *absmax, hipStream_t s) {
     if (chunked) {
         hipError_t e = hipMemsetAsync(absmax, 0, sizeof(uint32_t), s);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess || n <= 0) return e;
+        const int64_t groups = (n + CF - 1) / CF;
+        hipLaunchKernelGGL(k_col2im3_bwd_chunked, dim3(grid_cap((int64_t)T * groups)), dim3(BLK), 0, s,
+                           reinterpret_cast<const float4 *>(dA3), reinterpret_cast<const float4 *>(Z2), b2, n,
+                           T, reinterpret_cast<float4 *>(dZ2), absmax);
+        return hipGetLastError();
     }
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_col2im3_bwd, dim3(grid_cap((int64_t)T * n)), dim3(BLK), 0, s,
                        reinterpret_cast<const float4 *>(dA3), reinterpret_cast<const float4 *>(Z2), b2, n, T,
-                       chunked, reinterpret_cast<float4 *>(dZ2), absmax);
+                       reinterpret_cast<float4 *>(dZ2));
     return hipGetLastError();
 }
 

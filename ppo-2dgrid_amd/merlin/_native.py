@@ -83,7 +83,7 @@ def lib():
     L.merlin_tower_conv3_col2im_bwd_chunked.argtypes = [vp, vp, vp, i64, i32, vp, vp, vp]
     L.merlin_tower_conv2_lut_rows.restype = C.c_int
     L.merlin_tower_conv2_lut_fwd.argtypes = [vp, vp, i64, vp, i32, vp, vp]
-    L.merlin_tower_conv2_lut_bwd.argtypes = [vp, vp, i64, vp, vp, i32, vp, vp]
+    L.merlin_tower_conv2_lut_bwd.argtypes = [vp, i64, vp, vp, i32, vp, vp]
     _lib = L
     return L
 
@@ -333,17 +333,19 @@ def conv2_lut_fwd(codes, index, tables):
     return out
 
 
-def conv2_lut_bwd(codes, index, dZ2c, absmax=None):
-    """dtables f32[T, 2720, 64] from chunk-major dZ2c f32[T, 16, n*25, 4]; absmax int32[1] = float
-    bits of an upper bound on max |dZ2c| (computed here when not given)."""
+def conv2_lut_bwd(codes, dZ2c, absmax=None):
+    """dtables f32[T, 2720, 64] from chunk-major dZ2c f32[T, 16, n*25, 4] of frames codes[0:n]
+    (the minibatch's own code rows); absmax int32[1] = float bits of an upper bound on
+    max |dZ2c| (computed here when not given)."""
     T = int(dZ2c.shape[0])
     n = int(dZ2c.shape[2]) // 25
+    assert codes.dtype == torch.int32 and codes.shape[-1] == OBS_WORDS and codes.shape[0] >= n
     if absmax is None:
         absmax = dZ2c.abs().amax().reshape(1).view(torch.int32) if dZ2c.numel() else \
             torch.zeros(1, dtype=torch.int32, device=dZ2c.device)
     dt = torch.empty((T, LUT2_ROWS, 64), dtype=torch.float32, device=dZ2c.device)
-    # algorithmic bytes per frame: dZ2 read once (T*25*64*4) + codes/index per 4-channel slice block
-    with KernelTimer.span("k_conv2_lut_hist", n * (T * 25 * 64 * 4 + 16 * T * (32 + (8 if index is not None else 0)))):
-        check(lib().merlin_tower_conv2_lut_bwd(ptr(codes), ptr(index), n, ptr(dZ2c), ptr(absmax), T, ptr(dt),
+    # algorithmic bytes per frame: dZ2 read once (T*25*64*4) + its code row per 4-channel slice block
+    with KernelTimer.span("k_conv2_lut_hist", n * (T * 25 * 64 * 4 + 16 * T * 32)):
+        check(lib().merlin_tower_conv2_lut_bwd(ptr(codes), n, ptr(dZ2c), ptr(absmax), T, ptr(dt),
                                                stream_of(dZ2c)), "merlin_tower_conv2_lut_bwd")
     return dt

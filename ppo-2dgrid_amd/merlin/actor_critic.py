@@ -152,18 +152,19 @@ class _Conv2LutTower(torch.autograd.Function):
         from . import _native as nat
 
         b2c = b2.detach().contiguous()
-        Z2 = nat.conv2_lut_fwd(codes, index, T2.detach().contiguous())
-        ctx.save_for_backward(Z2, b2c, codes, index if index is not None else codes.new_empty(0))
-        ctx.has_index = index is not None
+        if index is not None:  # the minibatch's code rows, gathered once (32 B per frame)
+            codes = codes.index_select(0, index)
+        Z2 = nat.conv2_lut_fwd(codes, None, T2.detach().contiguous())
+        ctx.save_for_backward(Z2, b2c, codes)
         return nat.conv3_im2col_fwd(Z2, b2c)
 
     @staticmethod
     def backward(ctx, dA3):
         from . import _native as nat
 
-        Z2, b2, codes, index = ctx.saved_tensors
+        Z2, b2, codes = ctx.saved_tensors
         dZ2c, absmax = nat.conv3_col2im_bwd_chunked(dA3.contiguous(), Z2, b2)
-        dT = nat.conv2_lut_bwd(codes, index if ctx.has_index else None, dZ2c, absmax)
+        dT = nat.conv2_lut_bwd(codes, dZ2c, absmax)
         # every output position reads exactly one row of tap (0, 0) (rows 0, 4, .., 16)
         return dT, dT[:, 0:20:4, :].sum(1), None, None
 
@@ -296,7 +297,8 @@ class CNNActorCritic(nn.Module):
         if groups is not None:
             rep_idx, inv = groups
             logits, value = self._forward_codes(codes, rep_idx)
-            logits, value = logits[inv], value[inv]
+            # index_select: its backward is one index_add (advanced indexing's is a sort)
+            logits, value = logits.index_select(0, inv), value.index_select(0, inv)
         else:
             logits, value = self._forward_codes(codes, index)
         logp_all, probs = _categorical(logits)

@@ -42,4 +42,5 @@ for name, cd in (("env", flat), ):
     g = torch.randn(2, 16, MB * 25, 4, device=dev)
     g[g < 0] = 0
     print(name, "fwd ms", timeit(lambda: nat.conv2_lut_fwd(cd, idx, T2)), flush=True)
-    print(name, "hist ms", timeit(lambda: nat.conv2_lut_bwd(cd, idx, g)), flush=True)
+    cm = cd.index_select(0, idx)
+    print(name, "hist ms", timeit(lambda: nat.conv2_lut_bwd(cm, g)), flush=True)

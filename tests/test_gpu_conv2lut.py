@@ -71,7 +71,7 @@ def test_lut_histogram_matches_index_add(device, n, use_index):
     g = torch.randn(2, n * 25, 64, device=device)
     g[g.abs() < 0.3] = 0.0  # ReLU-masked zeros, as col2im3 produces
     dZ2c = g.view(2, n * 25, 16, 4).permute(0, 2, 1, 3).contiguous()
-    dT = nat.conv2_lut_bwd(codes, idx, dZ2c)
+    dT = nat.conv2_lut_bwd(codes.index_select(0, idx) if use_index else codes, dZ2c)
     sel = idx.cpu().numpy() if use_index else np.arange(n)
     rows = torch.from_numpy(lut2_rows(c49[sel])).to(device).reshape(n * 25, 16)
     ref = torch.zeros(2, 2720, 64, dtype=torch.float64, device=device)
