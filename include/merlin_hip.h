@@ -49,6 +49,12 @@
  *                        merlin_tower_conv2_lut_*: Conv2d(3,32,k8,s4)+ReLU+Conv2d(32,64,k4,s2)
  *                        of both towers (actor_critic.py:9-12) as table lookups from the
  *                        tile codes, and the table gradient
+ *   merlin_tower_window_*, merlin_segment_sum: the same conv2 and the following
+ *                        Conv2d(64,64,k3,s1)+ReLU (actor_critic.py:13-14) evaluated once per
+ *                        distinct receptive-field window of an update, and the fixed-order
+ *                        segmented sums of their backward pass (merlin/windows.py)
+ *   merlin_tower_bias_relu / _relu_bwd / _head_bwd: the ReLU + bias epilogues of the
+ *                        conv3 / fc1 GEMMs and the heads' backward (actor_critic.py:14-41)
  */
 #ifndef MERLIN_HIP_H
 #define MERLIN_HIP_H
@@ -228,6 +234,51 @@ int merlin_tower_conv2_lut_fwd(const uint32_t *codes_dev, const int64_t *index_d
 int merlin_tower_conv2_lut_bwd(const uint32_t *codes_dev, int64_t n, const float *dZ2c_dev,
                                const uint32_t *absmax_dev, int32_t towers, float *dtables_dev,
                                void *stream);
+
+/* Receptive-field windows (csrc/merlin_window.hip; the plan is built by merlin/windows.py).
+ * window_lut:   Z2w[t][w][co] = sum over the 16 taps of tables[t][rows[w][tap]][co]
+ *               (rows int32[n_windows][16]: conv2 table rows as merlin_tower_conv2_lut_fwd's)
+ * window_conv3: Y3[t][k*9 + p3][co] = relu(b3[t][co] + sum over tap = ky*3 + kx of
+ *               Q[t][wid[g*25 + (oy+ky)*5 + ox+kx]][tap][co]), g = groups ? groups[k] : k,
+ *               p3 = oy*3 + ox; Q float[towers][n_windows][9][64], wid int32[*][25]
+ * segment_sum:  out[t][key[e]][:] = sum over the nnz entries e (keys ascending) of
+ *               src[t][row(e)][:], each destination summed in entry order (no atomics);
+ *               row(e) = idx[e], or with slot_dev slot[idx[e] / sub] * sub + idx[e] % sub,
+ *               entries whose slot is -1 skipped.  Items of item_len entries; fix_dev
+ *               int32[n_fix][4] = (dst, first item, last item, carry slot in the first item)
+ *               for destinations spanning items; carry_dev float[towers][ceil(nnz /
+ *               item_len)][2][64] scratch.  out float[towers][out_rows][64] is overwritten
+ *               (rows without entries = 0). */
+int merlin_tower_window_lut(const int32_t *rows_dev, int64_t n_windows, const float *tables_dev,
+                            int32_t towers, float *Z2w_dev, void *stream);
+int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
+                              const int64_t *groups_dev, int64_t n, const float *b3_dev,
+                              int32_t towers, float *Y3_dev, void *stream);
+int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *idx_dev,
+                       const int32_t *key_dev, int64_t nnz, const int32_t *slot_dev, int32_t sub,
+                       int64_t item_len, const int32_t *fix_dev, int64_t n_fix, int32_t towers,
+                       float *out_dev, int64_t out_rows, float *carry_dev, void *stream);
+
+/* Tower GEMM epilogues (csrc/merlin_head.hip): towers = 1 or 2, `rows` per tower; cols (hidden)
+ * a multiple of 4 dividing 1024 (4 x a divisor of 256).  Column sums use a per-device library
+ * workspace: calls on one device must be stream-ordered with each other.
+ * bias_relu: z[t][r][c] = relu(z[t][r][c] + bias[t][c]) in place (NaN propagates), after a
+ *            plain GEMM (conv3 / fc1 of CNNFeatureExtractor / the heads, actor_critic.py:9-41)
+ * relu_bwd:  dz = [y > 0] * dy (dz may alias dy), dbias[t][c] = sum over r of dz[t][r][c]
+ * head_bwd:  the heads' backward through fc1's ReLU (actor_critic.py:30-41): h float[2][n][hidden]
+ *            = relu(fc1) of the actor / critic tower, dlogits float[n][act_dim], dvalue float[n],
+ *            w_actor float[act_dim][hidden], w_critic float[hidden] ->
+ *            dz[0][k] = [h0 > 0] * (dlogits[k] . w_actor), dz[1][k] = [h1 > 0] * dvalue[k] * w_critic,
+ *            dbias float[2][hidden] = sum_k dz[t][k], dw_actor = dlogits^T h0, dw_critic = dvalue^T h1
+ *            (fixed-order sums; act_dim <= 8). */
+int merlin_tower_bias_relu(float *z_dev, const float *bias_dev, int64_t rows, int32_t cols, int32_t towers,
+                           void *stream);
+int merlin_tower_relu_bwd(const float *y_dev, const float *dy_dev, float *dz_dev, int64_t rows, int32_t cols,
+                          int32_t towers, float *dbias_dev, void *stream);
+int merlin_tower_head_bwd(const float *h_dev, const float *dlogits_dev, const float *dvalue_dev,
+                          const float *w_actor_dev, const float *w_critic_dev, int64_t n, int32_t hidden,
+                          int32_t act_dim, float *dz_dev, float *dbias_dev, float *dw_actor_dev,
+                          float *dw_critic_dev, void *stream);
 
 #ifdef __cplusplus
 }

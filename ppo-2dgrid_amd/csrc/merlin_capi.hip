@@ -198,6 +198,7 @@ struct DeviceWs {
     float *conv1_slabs = nullptr;
     int max_slabs = 0;
     void *lut2_slabs = nullptr;  // conv2 table histogram: per-block 4-channel u64 slices
+    float *epi_work = nullptr;   // GEMM epilogues: per-block column-sum partials
 };
 constexpr int MAX_DEV = 64;
 DeviceWs g_dev[MAX_DEV];
@@ -219,6 +220,7 @@ int device_ws(DeviceWs **out) {
         HIP_TRY(hipMalloc(&w.conv1_slabs, sizeof(float) * (size_t)WS_SLABS * merlin::conv1_slab_floats(2)));
         w.max_slabs = WS_SLABS;
         HIP_TRY(hipMalloc(&w.lut2_slabs, merlin::conv2_lut_slab_bytes(2, merlin::conv2_lut_fblocks(INT64_MAX / 64))));
+        HIP_TRY(hipMalloc(&w.epi_work, sizeof(float) * merlin::epilogue_work_floats()));
         w.ready = true;
     }
     *out = &w;
@@ -554,6 +556,70 @@ int merlin_tower_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ
     if (rc) return rc;
     HIP_TRY(merlin::launch_conv2_lut_bwd(codes, n, dZ2c, absmax, towers, dtables, ws->lut2_slabs,
                                          (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_window_lut(const int32_t *rows, int64_t nw, const float *tables, int32_t towers, float *Z2w,
+                            void *stream) {
+    if ((!rows || !tables || !Z2w) && nw > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_window_lut(rows, nw, tables, towers, Z2w, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
+                              const float *b3, int32_t towers, float *Y3, void *stream) {
+    if ((!Q || !wid || !b3 || !Y3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_segment_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
+                       const int32_t *slot, int32_t sub, int64_t item_len, const int32_t *fix, int64_t n_fix,
+                       int32_t towers, float *out, int64_t out_rows, float *carry, void *stream) {
+    if (!out && out_rows > 0) return fail(MERLIN_E_INVALID, "null output");
+    if (nnz > 0 && (!src || !idx || !key || !carry)) return fail(MERLIN_E_INVALID, "null argument");
+    if (n_fix > 0 && !fix) return fail(MERLIN_E_INVALID, "null fix-up list");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (item_len <= 0 || sub <= 0) return fail(MERLIN_E_INVALID, "item_len and sub must be > 0");
+    HIP_TRY(merlin::launch_seg_sum(src, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
+                                   out_rows, carry, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_bias_relu(float *z, const float *bias, int64_t rows, int32_t cols, int32_t towers, void *stream) {
+    if ((!z || !bias) && rows > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (cols <= 0 || cols % 4) return fail(MERLIN_E_INVALID, "cols must be a positive multiple of 4");
+    HIP_TRY(merlin::launch_bias_relu(z, bias, rows, cols, towers, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_relu_bwd(const float *y, const float *dy, float *dz, int64_t rows, int32_t cols, int32_t towers,
+                          float *dbias, void *stream) {
+    if (!dbias || ((!y || !dy || !dz) && rows > 0)) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (!merlin::epilogue_cols_ok(cols)) return fail(MERLIN_E_UNSUPPORTED, "cols must be 4 x a divisor of 256");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_relu_bwd_colsum(y, dy, dz, rows, cols, towers, dbias, ws->epi_work, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *w_actor,
+                          const float *w_critic, int64_t n, int32_t hidden, int32_t act_dim, float *dz, float *dbias,
+                          float *dw_actor, float *dw_critic, void *stream) {
+    if (!dbias || !dw_actor || !dw_critic || ((!h || !dlogits || !dvalue || !w_actor || !w_critic || !dz) && n > 0))
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (act_dim < 1 || act_dim > merlin::epilogue_max_act()) return fail(MERLIN_E_UNSUPPORTED, "act_dim must be 1..8");
+    if (!merlin::epilogue_cols_ok(hidden)) return fail(MERLIN_E_UNSUPPORTED, "hidden must be 4 x a divisor of 256");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_head_bwd(h, dlogits, dvalue, w_actor, w_critic, n, hidden, act_dim, dz, dbias, dw_actor,
+                                    dw_critic, ws->epi_work, (hipStream_t)stream));
     return MERLIN_OK;
 }
 

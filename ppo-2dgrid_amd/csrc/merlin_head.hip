@@ -1,0 +1,241 @@
+// merlin_head.hip -- the memory-bound epilogues around the towers' conv3 / fc1 GEMMs and the
+// heads' backward (src/actor_critic.py:14-18 conv3 + ReLU, :30-41 Linear(576, 512) -> ReLU ->
+// Linear(512, act_dim | 1)), so that no full-size activation is touched more than once per
+// direction outside the GEMMs:
+//   k_bias_relu        Z = relu(Z + b) in place after a plain GEMM (instead of baddbmm's
+//                      bias broadcast copy + a separate relu_ pass)
+//   k_relu_bwd_colsum  dZ = [Y > 0] * dY and the bias gradient (column sums) in one pass
+//   k_head_bwd         fc1's ReLU mask applied to the heads' input gradient, fused with the
+//                      heads' weight gradients and fc1's bias gradient: one read of h, one
+//                      write of dz per tower (instead of two select-backward zero fills, an
+//                      add, a where and a reduction over [2, n, 512])
+// Column sums are per-block partials folded in a fixed order (bitwise reproducible).
+#include <algorithm>
+
+#include "merlin_internal.h"
+
+namespace merlin {
+namespace {
+
+constexpr int EBLK = 256;
+constexpr int MAXA = 8;  // act_dim limit of the fused head backward
+
+__device__ __forceinline__ float relu_nan(float v) { return v != v ? v : fmaxf(v, 0.0f); }  // torch.relu keeps NaN
+__device__ __forceinline__ float4 f4_zero() { return make_float4(0.0f, 0.0f, 0.0f, 0.0f); }
+__device__ __forceinline__ void f4_add(float4 &a, const float4 b) {
+    a.x += b.x;
+    a.y += b.y;
+    a.z += b.z;
+    a.w += b.w;
+}
+__device__ __forceinline__ float4 f4_mask(const float4 y, const float4 g) {
+    return make_float4(y.x > 0.0f ? g.x : 0.0f, y.y > 0.0f ? g.y : 0.0f, y.z > 0.0f ? g.z : 0.0f,
+                       y.w > 0.0f ? g.w : 0.0f);
+}
+
+// Z[t][r][:] = relu(Z[t][r][:] + b[t][:]), c4 = cols / 4
+__global__ __launch_bounds__(EBLK) void k_bias_relu(float4 *__restrict__ Z, const float4 *__restrict__ b,
+                                                    int64_t rows, int c4, int64_t total4) {
+    for (int64_t e = (int64_t)blockIdx.x * EBLK + threadIdx.x; e < total4; e += (int64_t)gridDim.x * EBLK) {
+        const int64_t tr = e / c4;
+        const int c = (int)(e - tr * c4), t = (int)(tr / rows);
+        const float4 bb = b[t * c4 + c];
+        float4 v = Z[e];
+        v.x = relu_nan(v.x + bb.x);
+        v.y = relu_nan(v.y + bb.y);
+        v.z = relu_nan(v.z + bb.z);
+        v.w = relu_nan(v.w + bb.w);
+        Z[e] = v;
+    }
+}
+
+// Block (b, t): rows [b*per, min(rows, (b+1)*per)) of tower t.  Thread = (row lane r0, column
+// group c); c4 divides EBLK, so EBLK / c4 rows are in flight per iteration and every wave
+// load is a run of whole rows.  partials[t][b][c4] = the block's column sums of dZ.
+__global__ __launch_bounds__(EBLK) void k_relu_bwd_colsum(const float4 *__restrict__ Y, const float4 *dY,
+                                                          float4 *dZ, int64_t rows, int c4, int64_t per,
+                                                          float4 *__restrict__ partials) {
+    __shared__ float4 red[EBLK];
+    const int t = blockIdx.y, R = EBLK / c4;
+    const int c = threadIdx.x % c4, r0 = threadIdx.x / c4;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = std::min<int64_t>(rows, lo + per);
+    const size_t base = (size_t)t * rows * c4;
+    float4 acc = f4_zero();
+    for (int64_t r = lo + r0; r < hi; r += R) {
+        const size_t e = base + (size_t)r * c4 + c;
+        const float4 d = f4_mask(Y[e], dY[e]);
+        dZ[e] = d;
+        f4_add(acc, d);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < c4) {
+        float4 s = red[threadIdx.x];
+        for (int k = 1; k < R; k++) f4_add(s, red[threadIdx.x + k * c4]);
+        partials[((size_t)t * gridDim.x + blockIdx.x) * c4 + threadIdx.x] = s;
+    }
+}
+
+// out[t][c] = sum over b (ascending) of partials[t][b][c]
+__global__ __launch_bounds__(256) void k_fold_cols(const float *__restrict__ partials, int nblk, int cols, int T,
+                                                   float *__restrict__ out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= T * cols) return;
+    const int t = k / cols, c = k - t * cols;
+    float acc = 0.0f;
+    for (int b = 0; b < nblk; b++) acc += partials[((size_t)t * nblk + b) * cols + c];
+    out[k] = acc;
+}
+
+// Heads backward with fc1's ReLU mask, h [2][n][H] = relu(fc1) of the actor / critic tower:
+//   tower 0: dz[0][k] = [h0 > 0] * (sum_j dlogits[k][j] * Wa[j]),  dWa[j] += dlogits[k][j] * h0[k]
+//   tower 1: dz[1][k] = [h1 > 0] * (dvalue[k] * wc),               dwc    += dvalue[k] * h1[k]
+//   db4[t] += dz[t][k]
+// partials[t][b][(1 + A) * H4] (float4): tower 0 = (db4_0, dWa rows 0..A-1), tower 1 = (db4_1, dwc).
+__global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h, const float *__restrict__ dlogits,
+                                                   const float *__restrict__ dvalue, const float4 *__restrict__ wa,
+                                                   const float4 *__restrict__ wc, int64_t n, int H4, int A,
+                                                   int64_t per, float4 *__restrict__ dz,
+                                                   float4 *__restrict__ partials) {
+    __shared__ float4 red[EBLK];
+    const int t = blockIdx.y, R = EBLK / H4;
+    const int c = threadIdx.x % H4, r0 = threadIdx.x / H4;
+    const int nw = t == 0 ? A : 1;
+    float4 w[MAXA], accw[MAXA];
+#pragma unroll
+    for (int j = 0; j < MAXA; j++) {
+        w[j] = j < nw ? (t == 0 ? wa[j * H4 + c] : wc[c]) : f4_zero();
+        accw[j] = f4_zero();
+    }
+    float4 acc = f4_zero();
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = std::min<int64_t>(n, lo + per);
+    const size_t base = (size_t)t * n * H4;
+    for (int64_t r = lo + r0; r < hi; r += R) {
+        const size_t e = base + (size_t)r * H4 + c;
+        const float4 hv = h[e];
+        float4 g = f4_zero();
+        if (t == 0) {
+#pragma unroll
+            for (int j = 0; j < MAXA; j++) {
+                if (j < A) {
+                    const float d = dlogits[r * A + j];
+                    g.x += d * w[j].x;
+                    g.y += d * w[j].y;
+                    g.z += d * w[j].z;
+                    g.w += d * w[j].w;
+                    accw[j].x += d * hv.x;
+                    accw[j].y += d * hv.y;
+                    accw[j].z += d * hv.z;
+                    accw[j].w += d * hv.w;
+                }
+            }
+        } else {
+            const float d = dvalue[r];
+            g = make_float4(d * w[0].x, d * w[0].y, d * w[0].z, d * w[0].w);
+            accw[0].x += d * hv.x;
+            accw[0].y += d * hv.y;
+            accw[0].z += d * hv.z;
+            accw[0].w += d * hv.w;
+        }
+        const float4 o = f4_mask(hv, g);
+        dz[e] = o;
+        f4_add(acc, o);
+    }
+    float4 *dst = partials + ((size_t)t * gridDim.x + blockIdx.x) * (size_t)(1 + A) * H4;
+#pragma unroll
+    for (int q = 0; q < 1 + MAXA; q++) {
+        if (q <= nw) {  // block-uniform
+            __syncthreads();
+            red[threadIdx.x] = q == 0 ? acc : accw[q > 0 ? q - 1 : 0];
+            __syncthreads();
+            if (threadIdx.x < H4) {
+                float4 s = red[threadIdx.x];
+                for (int k = 1; k < R; k++) f4_add(s, red[threadIdx.x + k * H4]);
+                dst[(size_t)q * H4 + threadIdx.x] = s;
+            }
+        }
+    }
+}
+
+// db4[2][H], dWa[A][H], dwc[H] from the head partials (ascending block order)
+__global__ __launch_bounds__(256) void k_head_fold(const float *__restrict__ partials, int nblk, int H, int A,
+                                                   float *__restrict__ db4, float *__restrict__ dwa,
+                                                   float *__restrict__ dwc) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int S = (1 + A) * H;
+    int t, off;
+    if (k < S) {
+        t = 0;
+        off = k;
+    } else if (k < S + 2 * H) {
+        t = 1;
+        off = k - S;
+    } else {
+        return;
+    }
+    float acc = 0.0f;
+    for (int b = 0; b < nblk; b++) acc += partials[((size_t)t * nblk + b) * S + off];
+    if (off < H)
+        db4[t * H + off] = acc;
+    else if (t == 0)
+        dwa[off - H] = acc;
+    else
+        dwc[off - H] = acc;
+}
+
+int blocks_for(int64_t rows) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(EPI_MAX_BLOCKS, (rows + 31) / 32));
+}
+
+}  // namespace
+
+size_t epilogue_work_floats() { return (size_t)2 * EPI_MAX_BLOCKS * (1 + MAXA) * 1024; }
+
+bool epilogue_cols_ok(int cols) { return cols > 0 && cols % 4 == 0 && cols / 4 <= EBLK && EBLK % (cols / 4) == 0; }
+
+int epilogue_max_act() { return MAXA; }
+
+hipError_t launch_bias_relu(float *Z, const float *b, int64_t rows, int cols, int T, hipStream_t s) {
+    const int64_t total4 = (int64_t)T * rows * (cols / 4);
+    if (total4 <= 0) return hipSuccess;
+    const int grid = (int)std::min<int64_t>((total4 + EBLK - 1) / EBLK, 256 * 16);
+    hipLaunchKernelGGL(k_bias_relu, dim3(grid), dim3(EBLK), 0, s, reinterpret_cast<float4 *>(Z),
+                       reinterpret_cast<const float4 *>(b), rows, cols / 4, total4);
+    return hipGetLastError();
+}
+
+hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, int64_t rows, int cols, int T,
+                                  float *dbias, float *work, hipStream_t s) {
+    if (rows <= 0) return hipMemsetAsync(dbias, 0, sizeof(float) * T * cols, s);
+    const int nblk = blocks_for(rows);
+    const int64_t per = (rows + nblk - 1) / nblk;
+    hipLaunchKernelGGL(k_relu_bwd_colsum, dim3(nblk, T), dim3(EBLK), 0, s, reinterpret_cast<const float4 *>(Y),
+                       reinterpret_cast<const float4 *>(dY), reinterpret_cast<float4 *>(dZ), rows, cols / 4, per,
+                       reinterpret_cast<float4 *>(work));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_fold_cols, dim3((T * cols + 255) / 256), dim3(256), 0, s, work, nblk, cols, T, dbias);
+    return hipGetLastError();
+}
+
+hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
+                           const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
+                           float *work, hipStream_t s) {
+    if (n <= 0) {
+        hipError_t e = hipMemsetAsync(db4, 0, sizeof(float) * 2 * H, s);
+        if (e == hipSuccess) e = hipMemsetAsync(dwa, 0, sizeof(float) * A * H, s);
+        return e == hipSuccess ? hipMemsetAsync(dwc, 0, sizeof(float) * H, s) : e;
+    }
+    const int nblk = blocks_for(n);
+    const int64_t per = (n + nblk - 1) / nblk;
+    hipLaunchKernelGGL(k_head_bwd, dim3(nblk, 2), dim3(EBLK), 0, s, reinterpret_cast<const float4 *>(h), dlogits,
+                       dvalue, reinterpret_cast<const float4 *>(wa), reinterpret_cast<const float4 *>(wc), n, H / 4,
+                       A, per, reinterpret_cast<float4 *>(dz), reinterpret_cast<float4 *>(work));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int total = (1 + A) * H + 2 * H;
+    hipLaunchKernelGGL(k_head_fold, dim3((total + 255) / 256), dim3(256), 0, s, work, nblk, H, A, db4, dwa, dwc);
+    return hipGetLastError();
+}
+
+}  // namespace merlin

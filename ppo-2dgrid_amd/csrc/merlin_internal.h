@@ -87,4 +87,24 @@ hipError_t launch_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int
 hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
                                 int towers, float *dT, void *slabs, hipStream_t s);
 
+hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s);
+hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
+                               const float *b3, int T, float *Y3, hipStream_t s);
+hipError_t launch_seg_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
+                          const int32_t *slot, int S, int64_t L, const int32_t *fix, int64_t nfix, int T, float *out,
+                          int64_t out_rows, float *carry, hipStream_t s);
+
+// GEMM epilogues (merlin_head.hip); partial sums use a per-device workspace of
+// epilogue_work_floats() floats
+constexpr int EPI_MAX_BLOCKS = 512;
+size_t epilogue_work_floats();
+bool epilogue_cols_ok(int cols);
+int epilogue_max_act();
+hipError_t launch_bias_relu(float *Z, const float *b, int64_t rows, int cols, int T, hipStream_t s);
+hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, int64_t rows, int cols, int T,
+                                  float *dbias, float *work, hipStream_t s);
+hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
+                           const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
+                           float *work, hipStream_t s);
+
 }  // namespace merlin

@@ -1,0 +1,232 @@
+// merlin_window.hip -- conv2 and conv3 of both CNN towers evaluated once per distinct
+// receptive-field window of an update's frames (src/actor_critic.py:11-14), and the
+// fixed-order segmented sums of their backward passes.
+//
+// conv2 output (py, px) of a frame depends only on the frame's 3x3 tile-class window at
+// (py, px) (its 16 conv2 table rows, merlin_conv2lut.hip), and convolution + ReLU are
+// translation invariant, so merlin/windows.py numbers the distinct windows of a rollout once
+// per update and each minibatch runs
+//   Z2w[t][w]     = sum over the 16 taps of T2[t][rows[w][tap]]                    k_window_lut
+//   Q[t][w][tap]  = relu(Z2w[t][w] + b2[t]) . W3[t][:, :, tap]        (a small GEMM in torch)
+//   Y3[t][u*9+p3] = relu(b3[t] + sum over the 9 taps of Q[t][wid[g_u][p3+tap]][tap])  k_window_conv3
+// instead of building conv3's 576-wide im2col rows (3.3 GB per minibatch) and their GEMM.
+// Backward:
+//   dQ[t][w*9+tap] = sum of dZ3[t][u*9+p3] over the (u, p3) that read Q[t][w][tap]
+//   dT2[t][row]    = sum of dZ2w[t][w] over the (w, tap) that read T2[t][row]
+// are segmented sums over entry lists sorted by destination once per update: k_seg_sum cuts a
+// list into items of L entries, one wave per item, adding each destination's entries in list
+// order; a destination whose entries span items gets the items' partial sums added in item
+// order by k_seg_fix.  No atomics: bitwise reproducible.
+#include <algorithm>
+
+#include "merlin_internal.h"
+
+namespace merlin {
+namespace {
+
+constexpr int NROW = 2720;  // conv2 table rows per tower (merlin_conv2lut.hip)
+
+__device__ __forceinline__ void f4_add(float4 &a, const float4 b) {
+    a.x += b.x;
+    a.y += b.y;
+    a.z += b.z;
+    a.w += b.w;
+}
+__device__ __forceinline__ float relu_nan(float v) { return v != v ? v : fmaxf(v, 0.0f); }  // torch.relu keeps NaN
+
+// Z2w[t][w][c4] = sum_{k<16} T2[t][rows[w][k]][c4], taps in k_conv2_lut_fwd's order
+__global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ rows, int64_t nw,
+                                                    const float4 *__restrict__ tab, int T,
+                                                    float4 *__restrict__ Z2w) {
+    const int64_t total = (int64_t)T * nw * 16;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int c = (int)(e & 15);
+        const int64_t tw = e >> 4;
+        const int t = (int)(tw / nw);
+        const int32_t *r = rows + (tw - (int64_t)t * nw) * 16;
+        const float4 *tt = tab + (size_t)t * NROW * 16 + c;
+        float4 v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = tt[r[k] * 16];
+        float4 acc = v[0];
+#pragma unroll
+        for (int k = 1; k < 16; k++) f4_add(acc, v[k]);
+        Z2w[e] = acc;
+    }
+}
+
+// Y3[t][u*9 + p3][c4] = relu(b3[t][c4] + sum_tap Q[t][wid[g*25 + p2(p3, tap)]][tap][c4]); 16
+// consecutive lanes read one 256-B row of Q per tap
+__global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__ Q, int64_t nw,
+                                                      const int32_t *__restrict__ wid,
+                                                      const int64_t *__restrict__ groups, int64_t n,
+                                                      const float4 *__restrict__ b3, int T,
+                                                      float4 *__restrict__ Y3) {
+    const int64_t total = (int64_t)T * n * 9 * 16;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int c = (int)(e & 15);
+        const int64_t r = e >> 4, tu = r / 9;
+        const int p3 = (int)(r - tu * 9), t = (int)(tu / n);
+        const int64_t u = tu - (int64_t)t * n;
+        const int32_t *wr = wid + (groups ? groups[u] : u) * 25;
+        const int oy = p3 / 3, ox = p3 - 3 * (p3 / 3);
+        const float4 *qt = Q + (size_t)t * nw * 9 * 16 + c;
+        float4 v[9];
+#pragma unroll
+        for (int tap = 0; tap < 9; tap++) {
+            const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+            v[tap] = qt[((size_t)wr[(oy + ky) * 5 + ox + kx] * 9 + tap) * 16];
+        }
+        float4 acc = v[0];
+#pragma unroll
+        for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
+        const float4 b = b3[t * 16 + c];
+        Y3[e] = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
+                            relu_nan(acc.w + b.w));
+    }
+}
+
+// One wave per item of L entries; lane = (tower t, float2 column c2), so one wave load reads
+// one entry's 256-B row of each tower.  The wave loads 64 entries' (idx, key) at a time,
+// resolves their source rows (through slot[] when given: -1 = not in this minibatch), and
+// walks the valid ones in order, SEG_UNROLL row loads in flight (issued unconditionally:
+// a select around a load would make hipcc wait for each load in turn), flushing a
+// destination's sum when the key changes.  The item's first / last destination, when it
+// continues in the neighbouring item, goes to carry[t][item][0 / 1] instead of out.
+constexpr int SEG_WAVES = 4, SEG_UNROLL = 8;
+__global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float2 *__restrict__ src, int64_t src_rows,
+                                                           const int32_t *__restrict__ idx,
+                                                           const int32_t *__restrict__ key, int64_t nnz,
+                                                           const int32_t *__restrict__ slot, int S, int64_t L,
+                                                           int64_t nitems, int T, float2 *__restrict__ out,
+                                                           int64_t out_rows, float2 *__restrict__ carry) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int t = lane >> 5, c2 = lane & 31;
+    const bool live = t < T;
+    const float2 *srct = src + (size_t)(live ? t : 0) * src_rows * 32 + c2;
+    const float2 zero = make_float2(0.0f, 0.0f);
+    for (int64_t it = (int64_t)blockIdx.x * SEG_WAVES + wv; it < nitems; it += (int64_t)gridDim.x * SEG_WAVES) {
+        const int64_t e0 = it * L, e1 = std::min<int64_t>(nnz, e0 + L);
+        const int kfirst = key[e0], klast = key[e1 - 1];
+        const bool xfirst = e0 > 0 && key[e0 - 1] == kfirst;
+        const bool xlast = e1 < nnz && key[e1] == klast;
+        const bool to_head_last = kfirst == klast && xlast;
+        float2 head = zero, tail = zero, acc = zero;
+        int cur = -1;
+        auto flush = [&]() {
+            if (cur == kfirst && (xfirst || to_head_last))
+                head = acc;
+            else if (cur == klast && xlast)
+                tail = acc;
+            else if (live)
+                out[((size_t)t * out_rows + cur) * 32 + c2] = acc;
+        };
+        for (int64_t base = e0; base < e1; base += 64) {
+            int row = -1, k = -1;
+            if (base + lane < e1) {
+                const int v = idx[base + lane];
+                k = key[base + lane];
+                if (slot) {
+                    const int q = v / S;
+                    const int s = slot[q];
+                    row = s >= 0 ? s * S + (v - q * S) : -1;
+                } else {
+                    row = v;
+                }
+            }
+            unsigned long long m = __ballot(row >= 0);
+            while (m) {
+                int rq[SEG_UNROLL], kq[SEG_UNROLL];
+#pragma unroll
+                for (int q = 0; q < SEG_UNROLL; q++) {
+                    const int j = m ? __builtin_ctzll(m) : -1;  // wave-uniform
+                    if (m) m &= m - 1;
+                    rq[q] = j >= 0 ? __shfl(row, j) : 0;
+                    kq[q] = j >= 0 ? __shfl(k, j) : -1;
+                }
+                float2 vq[SEG_UNROLL];
+#pragma unroll
+                for (int q = 0; q < SEG_UNROLL; q++) vq[q] = srct[(size_t)rq[q] * 32];
+#pragma unroll
+                for (int q = 0; q < SEG_UNROLL; q++) {
+                    if (kq[q] < 0) break;
+                    if (kq[q] != cur) {
+                        if (cur >= 0) flush();
+                        cur = kq[q];
+                        acc = vq[q];
+                    } else {
+                        acc.x += vq[q].x;
+                        acc.y += vq[q].y;
+                    }
+                }
+            }
+        }
+        if (cur >= 0) flush();
+        if (live) {
+            float2 *cr = carry + ((size_t)t * nitems + it) * 64 + c2;
+            cr[0] = head;
+            cr[32] = tail;
+        }
+    }
+}
+
+// fix rows (dst, j0, j1, slot0): out[t][dst] = carry[t][j0][slot0] + sum_{j0 < j <= j1} carry[t][j][0]
+__global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carry, int64_t nitems,
+                                                 const int4 *__restrict__ fix, int64_t nfix, int T,
+                                                 float2 *__restrict__ out, int64_t out_rows) {
+    const int lane = threadIdx.x & 63, t = lane >> 5, c2 = lane & 31;
+    for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nfix; f += (int64_t)gridDim.x * 4) {
+        if (t >= T) continue;
+        const int4 x = fix[f];
+        const float2 *ct = carry + (size_t)t * nitems * 64 + c2;
+        float2 acc = ct[(size_t)x.y * 64 + x.w * 32];
+#pragma unroll 8
+        for (int j = x.y + 1; j <= x.z; j++) {
+            const float2 v = ct[(size_t)j * 64];
+            acc.x += v.x;
+            acc.y += v.y;
+        }
+        out[((size_t)t * out_rows + x.x) * 32 + c2] = acc;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s) {
+    const int64_t total = (int64_t)T * nw * 16;
+    if (total <= 0) return hipSuccess;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(k_window_lut, dim3(grid), dim3(256), 0, s, rows, nw, reinterpret_cast<const float4 *>(tab), T,
+                       reinterpret_cast<float4 *>(Z2w));
+    return hipGetLastError();
+}
+
+hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
+                               const float *b3, int T, float *Y3, hipStream_t s) {
+    const int64_t total = (int64_t)T * n * 9 * 16;
+    if (total <= 0) return hipSuccess;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
+    hipLaunchKernelGGL(k_window_conv3, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4 *>(Q), nw, wid,
+                       groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3));
+    return hipGetLastError();
+}
+
+hipError_t launch_seg_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
+                          const int32_t *slot, int S, int64_t L, const int32_t *fix, int64_t nfix, int T, float *out,
+                          int64_t out_rows, float *carry, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
+    if (e != hipSuccess || nnz <= 0) return e;
+    const int64_t nitems = (nnz + L - 1) / L;
+    const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
+    hipLaunchKernelGGL(k_seg_sum, dim3(grid), dim3(64 * SEG_WAVES), 0, s, reinterpret_cast<const float2 *>(src),
+                       src_rows, idx, key, nnz, slot, S, L, nitems, T, reinterpret_cast<float2 *>(out), out_rows,
+                       reinterpret_cast<float2 *>(carry));
+    e = hipGetLastError();
+    if (e != hipSuccess || nfix <= 0) return e;
+    const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);
+    hipLaunchKernelGGL(k_seg_fix, dim3(gfix), dim3(256), 0, s, reinterpret_cast<const float2 *>(carry), nitems,
+                       reinterpret_cast<const int4 *>(fix), nfix, T, reinterpret_cast<float2 *>(out), out_rows);
+    return hipGetLastError();
+}
+
+}  // namespace merlin

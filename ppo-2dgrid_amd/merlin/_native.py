@@ -84,6 +84,12 @@ def lib():
     L.merlin_tower_conv2_lut_rows.restype = C.c_int
     L.merlin_tower_conv2_lut_fwd.argtypes = [vp, vp, i64, vp, i32, vp, vp]
     L.merlin_tower_conv2_lut_bwd.argtypes = [vp, i64, vp, vp, i32, vp, vp]
+    L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
+    L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
+    L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, vp]
+    L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
+    L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
+    L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -96,7 +102,8 @@ EXPORTED_SYMBOLS = (
     "merlin_conv1_lut_fwd", "merlin_conv1_lut_bwd", "merlin_tower_conv2_im2col_fwd",
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
-    "merlin_tower_conv2_lut_bwd",
+    "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
+    "merlin_segment_sum", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
 )
 
 
@@ -117,7 +124,10 @@ class KernelTimer:
 
     @classmethod
     def span(cls, name: str, nbytes: int):
-        return _Span(name, nbytes) if cls.records is not None else _NULL_SPAN
+        # no events inside a HIP-graph capture (the captured rollout, merlin/ppo.py)
+        if cls.records is None or torch.cuda.is_current_stream_capturing():
+            return _NULL_SPAN
+        return _Span(name, nbytes)
 
 
 class _Span:
@@ -349,3 +359,93 @@ def conv2_lut_bwd(codes, dZ2c, absmax=None):
         check(lib().merlin_tower_conv2_lut_bwd(ptr(codes), n, ptr(dZ2c), ptr(absmax), T, ptr(dt),
                                                stream_of(dZ2c)), "merlin_tower_conv2_lut_bwd")
     return dt
+
+
+# -- receptive-field windows (merlin/windows.py, csrc/merlin_window.hip) -----------------------
+def window_lut(rows, tables):
+    """Z2w f32[T, nw, 64]: the sum of the 16 conv2-table rows rows[w] (int32 [nw, 16]) of
+    tables f32[T, 2720, 64] for every window w."""
+    T, nw = int(tables.shape[0]), int(rows.shape[0])
+    assert tables.shape == (T, LUT2_ROWS, 64) and tables.dtype == torch.float32
+    assert rows.dtype == torch.int32 and rows.shape == (nw, 16)
+    out = torch.empty((T, nw, 64), dtype=torch.float32, device=tables.device)
+    # algorithmic bytes: row indices + Z2w written (table rows are L2-resident gathers)
+    with KernelTimer.span("k_window_lut", nw * (64 + T * 256)):
+        check(lib().merlin_tower_window_lut(ptr(rows), nw, ptr(tables), T, ptr(out), stream_of(tables)),
+              "merlin_tower_window_lut")
+    return out
+
+
+def window_conv3(Q, wid, groups, b3):
+    """Y3 f32[T, n*9, 64] = relu(conv3) rows (k, p3) of frames groups[k] from
+    Q f32[T, nw, 576], the per-window, per-tap conv3 partial sums (merlin/windows.py)."""
+    T, nw = int(Q.shape[0]), int(Q.shape[1])
+    n = int(groups.numel())
+    assert Q.shape[2] == 576 and Q.dtype == torch.float32 and b3.shape == (T, 64)
+    assert wid.dtype == torch.int32 and wid.shape[1] == 25 and groups.dtype == torch.int64
+    out = torch.empty((T, n * 9, 64), dtype=torch.float32, device=Q.device)
+    # algorithmic bytes: Y3 written, the frames' ids and window ids, Q read once (its 81 row
+    # gathers per frame and tower are L2 / Infinity-Cache hits)
+    with KernelTimer.span("k_window_conv3", T * n * 9 * 256 + n * 108 + T * nw * 576 * 4):
+        check(lib().merlin_tower_window_conv3(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
+                                              stream_of(Q)), "merlin_tower_window_conv3")
+    return out
+
+
+def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum"):
+    """out f32[T, out_rows, 64]: out[t][key] = the sum, in entry order, of src[t][row(e)] over
+    the plan's entries e with that key (merlin.windows.SegmentPlan); row(e) = idx[e], or
+    slot[idx[e] // sub] * sub + idx[e] % sub with entries whose slot is -1 skipped."""
+    T, src_rows = int(src.shape[0]), int(src.shape[1])
+    assert src.shape[2] == 64 and src.dtype == torch.float32
+    assert plan.max_key < out_rows
+    if slot is not None:
+        assert slot.dtype == torch.int32
+    out = torch.empty((T, out_rows, 64), dtype=torch.float32, device=src.device)
+    carry = torch.empty((T, max(plan.nitems, 1), 2, 64), dtype=torch.float32, device=src.device)
+    # algorithmic bytes: the entry lists (+ slot lookups), src read once, out written
+    nb = plan.nnz * (8 + (4 if slot is not None else 0)) + T * (src_rows + out_rows) * 256
+    with KernelTimer.span(name, nb):
+        check(lib().merlin_segment_sum(ptr(src), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz, ptr(slot),
+                                       int(sub), plan.item_len, ptr(plan.fix), int(plan.fix.shape[0]), T, ptr(out),
+                                       int(out_rows), ptr(carry), stream_of(src)), "merlin_segment_sum")
+    return out
+
+
+# -- GEMM epilogues (csrc/merlin_head.hip) -------------------------------------------------------
+def bias_relu_(z, bias):
+    """z f32[T, rows, cols] = relu(z + bias[t]) in place (bias f32[T, cols])."""
+    T, rows, cols = (int(x) for x in z.shape)
+    assert z.dtype == torch.float32 and bias.shape == (T, cols) and bias.dtype == torch.float32
+    with KernelTimer.span("k_bias_relu", 2 * z.numel() * 4):
+        check(lib().merlin_tower_bias_relu(ptr(z), ptr(bias), rows, cols, T, stream_of(z)), "merlin_tower_bias_relu")
+    return z
+
+
+def relu_bwd(y, dy, out=None):
+    """(dz, dbias): dz = [y > 0] * dy (out may be dy itself), dbias f32[T, cols] = column sums of dz."""
+    T, rows, cols = (int(x) for x in y.shape)
+    assert dy.shape == y.shape and y.dtype == dy.dtype == torch.float32
+    dz = torch.empty_like(dy) if out is None else out
+    db = torch.empty((T, cols), dtype=torch.float32, device=y.device)
+    with KernelTimer.span("k_relu_bwd_colsum", 3 * y.numel() * 4):
+        check(lib().merlin_tower_relu_bwd(ptr(y), ptr(dy), ptr(dz), rows, cols, T, ptr(db), stream_of(y)),
+              "merlin_tower_relu_bwd")
+    return dz, db
+
+
+def head_bwd(h, dlogits, dvalue, w_actor, w_critic):
+    """Heads backward through fc1's ReLU: h f32[2, n, H] = relu(fc1) of both towers, dlogits
+    f32[n, A], dvalue f32[n], w_actor f32[A, H], w_critic f32[1, H] or [H] ->
+    (dz f32[2, n, H], dbias f32[2, H], dw_actor f32[A, H], dw_critic f32[H])."""
+    _, n, H = (int(x) for x in h.shape)
+    A = int(w_actor.shape[0])
+    assert h.shape[0] == 2 and dlogits.shape == (n, A) and dvalue.numel() == n and w_critic.numel() == H
+    dz = torch.empty_like(h)
+    db = torch.empty((2, H), dtype=torch.float32, device=h.device)
+    dwa = torch.empty((A, H), dtype=torch.float32, device=h.device)
+    dwc = torch.empty((H,), dtype=torch.float32, device=h.device)
+    with KernelTimer.span("k_head_bwd", 2 * h.numel() * 4 + n * (A + 1) * 4):
+        check(lib().merlin_tower_head_bwd(ptr(h), ptr(dlogits), ptr(dvalue), ptr(w_actor), ptr(w_critic), n, H, A,
+                                          ptr(dz), ptr(db), ptr(dwa), ptr(dwc), stream_of(h)), "merlin_tower_head_bwd")
+    return dz, db, dwa, dwc

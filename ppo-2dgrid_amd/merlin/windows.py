@@ -1,0 +1,190 @@
+"""Receptive-field windows: conv2 and conv3 of both towers evaluated once per distinct window.
+
+Every observation is a 7x7 blit of 5 atlas tiles and the towers' convolutions
+(src/actor_critic.py:9-14) are translation invariant, so conv2's output at position (py, px)
+of a frame is a function of the frame's 3x3 tile-class window at (py, px) alone (conv1 k8/s4
+then conv2 k4/s2 see 20 px: tiles py..py+2, the third by its first half).  A bench rollout
+of 1,048,576 frames holds 5,411 distinct windows (scripts/probe_windows.py), so each update
+numbers them once (WindowPlan) and every minibatch evaluates
+
+  Z2w[t][w]     = conv2(relu(conv1)) of window w: its 16 conv2-table rows summed
+                  (merlin_tower_window_lut; tables from CNNActorCritic.conv2_tables)
+  Q[t][w][tap]  = relu(Z2w[t][w] + b2[t]) . W3[t][:, :, tap]    one [windows, 64] x [64, 576] GEMM
+  Y3[t][u, p3]  = relu(b3[t] + sum over the 9 taps of Q[t][wid[u][p3 + tap]][tap])
+                  (merlin_tower_window_conv3) = relu(conv3) of distinct frame u at p3
+
+instead of conv3's im2col rows and GEMMs over every (frame, position).  Backward, autograd
+runs through the tables and the GEMM, and the adjoints of the two gathers are segmented sums
+over lists sorted once per update (merlin_segment_sum: fixed order, no atomics):
+
+  dQ[t][w][tap] = sum of dZ3[t][u, p3] over the minibatch's (u, p3) whose window at p3 + tap
+                  is w (the list holds every distinct frame of the rollout; a slot table
+                  skips the frames outside the minibatch)
+  dT2[t][row]   = sum of dZ2w[t][w] over the (w, tap) that read table row `row`
+
+Same function and gradients as the reference towers, fp32 sums regrouped.  The minibatch's
+frames are its distinct observations (merlin/dedup.py); fc1 and the heads run on them.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as nat
+
+# conv3 output p3 = (oy, ox) and tap = (ky, kx) -> conv2 position (oy + ky) * 5 + (ox + kx)
+P2_OF = [[(p // 3 + k // 3) * 5 + p % 3 + k % 3 for k in range(9)] for p in range(9)]
+ITEM_LEN = 1024      # entries per wave of the dQ lists (81 per distinct frame of the rollout)
+HIST_ITEM_LEN = 256  # of the dT2 lists (16 per window)
+
+
+def unpack_classes(codes: torch.Tensor) -> torch.Tensor:
+    """int32 [n, 8] observation codes -> int64 [n, 7, 7] tile classes (cell r*7 + c is nibble
+    cell % 8 of word cell // 8, include/merlin_hip.h; clamped to 4 like the kernels)."""
+    shifts = torch.arange(0, 32, 4, dtype=torch.int32, device=codes.device)
+    nib = (codes.unsqueeze(-1) >> shifts) & 0xF
+    return nib.reshape(codes.shape[0], 64)[:, :49].to(torch.int64).clamp_(max=4).view(-1, 7, 7)
+
+
+def window_keys(cls: torch.Tensor) -> torch.Tensor:
+    """[n, 7, 7] classes -> int64 [n, 25]: the 3x3 window at each conv2 position as 9 base-5
+    digits, window tile (0, 0) most significant."""
+    k = torch.zeros((cls.shape[0], 5, 5), dtype=torch.int64, device=cls.device)
+    for a in range(3):
+        for b in range(3):
+            k = k * 5 + cls[:, a:a + 5, b:b + 5]
+    return k.reshape(-1, 25)
+
+
+def window_rows(keys: torch.Tensor) -> torch.Tensor:
+    """int64 [m] window keys -> int32 [m, 16]: the conv2 table row each tap 4*ky + kx reads
+    (row layout of csrc/merlin_conv2lut.hip, tap_rows)."""
+    d = [(keys // 5 ** (8 - i)) % 5 for i in range(9)]  # d[3a + b] = class of window tile (a, b)
+    rows = []
+    for ky in range(4):
+        for kx in range(4):
+            i, j = 3 * (ky >> 1) + (kx >> 1), 2 * (ky >> 1) + (kx >> 1)
+            if not ky & 1 and not kx & 1:
+                r = 4 * d[i] + j
+            elif not ky & 1:
+                r = 20 + 4 * (5 * d[i] + d[i + 1]) + j
+            elif not kx & 1:
+                r = 120 + 4 * (5 * d[i] + d[i + 3]) + j
+            else:
+                r = 220 + 4 * (125 * d[i] + 25 * d[i + 1] + 5 * d[i + 3] + d[i + 4]) + j
+            rows.append(r)
+    return torch.stack(rows, 1).to(torch.int32)
+
+
+class SegmentPlan:
+    """A destination-sorted entry list for merlin_segment_sum: out[key[e]] = sum of src[row(e)]
+    over the entries e of that key, in list order.  The list is cut into items of item_len
+    entries (one wave each); `fix` rows (dst, first item, last item, carry slot of the first
+    item) name the destinations whose entries span items: their items' partial sums are added
+    in item order."""
+
+    def __init__(self, key_sorted: torch.Tensor, idx_sorted: torch.Tensor, item_len: int = ITEM_LEN):
+        dev = key_sorted.device
+        n = int(key_sorted.numel())
+        L = int(item_len)
+        self.nnz, self.item_len = n, L
+        self.nitems = (n + L - 1) // L
+        self.key = key_sorted.to(torch.int32).contiguous()
+        self.idx = idx_sorted.to(torch.int32).contiguous()
+        if n == 0:
+            self.fix = torch.zeros((0, 4), dtype=torch.int32, device=dev)
+            self.max_key, self.num_segments = -1, 0
+            return
+        new = torch.ones(n, dtype=torch.bool, device=dev)
+        new[1:] = key_sorted[1:] != key_sorted[:-1]
+        start = torch.nonzero(new).squeeze(1)
+        end = torch.cat([start[1:], start.new_tensor([n])])
+        j0, j1 = start // L, (end - 1) // L
+        x = j1 > j0
+        self.fix = torch.stack([key_sorted[start[x]].long(), j0[x], j1[x], (start[x] != j0[x] * L).long()],
+                               1).to(torch.int32).contiguous()
+        self.max_key = int(key_sorted[-1])
+        self.num_segments = int(start.numel())
+
+
+class MinibatchWindows:
+    """One minibatch's distinct frames: groups int64 [U] (frame ids of the plan, ascending),
+    inv int64 [n] (sample -> position in groups), slot int32 [F] (frame id -> position or -1)."""
+
+    def __init__(self, groups: torch.Tensor, inv: torch.Tensor, slot: torch.Tensor):
+        self.groups, self.inv, self.slot = groups, inv, slot
+
+
+class WindowPlan:
+    """Per-update numbering of the receptive-field windows of a rollout's distinct frames
+    (frame id = merlin.dedup.FrameGroups group id) and the two backward entry lists."""
+
+    def __init__(self, codes: torch.Tensor, frame_groups, item_len: int = ITEM_LEN,
+                 hist_item_len: int = HIST_ITEM_LEN):
+        dev = codes.device
+        self.frame_groups = frame_groups
+        rep = codes.index_select(0, frame_groups.rep)  # one code row per distinct frame
+        F = int(rep.shape[0])
+        uniq, inv = torch.unique(window_keys(unpack_classes(rep)).reshape(-1), return_inverse=True)
+        nw = int(uniq.numel())
+        self.num_frames, self.num_windows = F, nw
+        self.wid = inv.view(F, 25).to(torch.int32).contiguous()
+        self.rows = window_rows(uniq).contiguous()
+        assert int(self.rows.max()) < nat.LUT2_ROWS
+        # dT2 lists: entry (w, tap) -> table row rows[w][tap]; source row w of dZ2w
+        hk, ho = torch.sort(self.rows.reshape(-1), stable=True)
+        self.hist = SegmentPlan(hk, ho // 16, hist_item_len)
+        # dQ lists: entry (frame g, p3, tap) -> Q row wid[g][p3 + tap] * 9 + tap; source dZ3 row g*9 + p3
+        p2 = torch.tensor(P2_OF, dtype=torch.int64, device=dev)
+        dst = (self.wid[:, p2] * 9 + torch.arange(9, dtype=torch.int32, device=dev)).reshape(-1)
+        dk, do = torch.sort(dst, stable=True)
+        self.conv3 = SegmentPlan(dk, do // 9, item_len)
+
+    def minibatch(self, mb_idx: torch.Tensor) -> MinibatchWindows:
+        g, inv = torch.unique(self.frame_groups.uid[mb_idx], return_inverse=True)
+        slot = torch.full((self.num_frames,), -1, dtype=torch.int32, device=g.device)
+        slot[g] = torch.arange(g.numel(), dtype=torch.int32, device=g.device)
+        return MinibatchWindows(g, inv, slot)
+
+
+class _WindowConv2(torch.autograd.Function):
+    """Z2w [2, windows, 64] = conv2(relu(conv1)) of every window (no conv2 bias) from the tables."""
+
+    @staticmethod
+    def forward(ctx, T2, plan):
+        ctx.plan = plan
+        return nat.window_lut(plan.rows, T2.detach().contiguous())
+
+    @staticmethod
+    def backward(ctx, dZ2w):
+        dT2 = nat.segment_sum(dZ2w.contiguous(), ctx.plan.hist, nat.LUT2_ROWS, name="k_seg_sum_dT2")
+        return dT2, None
+
+
+class _WindowConv3(torch.autograd.Function):
+    """Y3 [2, U*9, 64] = relu(conv3) rows (u, p3) of the minibatch's distinct frames, from Q."""
+
+    @staticmethod
+    def forward(ctx, Q, b3, plan, mb):
+        Y3 = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous())
+        ctx.save_for_backward(Y3)
+        ctx.plan, ctx.mb = plan, mb
+        return Y3
+
+    @staticmethod
+    def backward(ctx, dY3):
+        (Y3,) = ctx.saved_tensors
+        plan = ctx.plan
+        dZ3, db3 = nat.relu_bwd(Y3, dY3.contiguous())
+        dQ = nat.segment_sum(dZ3, plan.conv3, plan.num_windows * 9, slot=ctx.mb.slot, sub=9, name="k_seg_sum_dQ")
+        return dQ.view(dQ.shape[0], plan.num_windows, 576), db3, None, None
+
+
+def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows) -> torch.Tensor:
+    """relu(conv3(relu(conv2(relu(conv1(frame)))))) of both towers of CNNActorCritic `ac` for the
+    minibatch's distinct frames: [2, U*9, 64], rows (u, p3), channels last."""
+    ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
+    Z2w = _WindowConv2.apply(ac.conv2_tables(), plan)
+    a2w = torch.relu(Z2w + torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1))
+    W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
+    Q = torch.bmm(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
+    return _WindowConv3.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), plan, mb)

@@ -9,8 +9,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$R/gpurun_out/p
 tail -2 "$R/gpurun_out/prof_trace.log"
 if [ -n "$PMC" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_env_step|k_conv1_im2col|k_im2col3|k_col2im3|k_gae|k_adv" -T -f csv \
-        -d "$R/gpurun_out/prof_pmc_$C" -o run -- python "$R/bench.py" $ARGS \
+    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_env_step|k_conv|k_im2col3|k_col2im3|k_gae|k_adv|k_window|k_seg|k_bias_relu|k_relu_bwd|k_head" -T -f csv \
+        -d "$R/gpurun_out/prof_pmc_$C" -o run -- python "$R/bench.py" $ARGS --no-graph \
         > "$R/gpurun_out/prof_pmc_$C.log" 2>&1 || exit $?
     echo "pmc $C done"
   done

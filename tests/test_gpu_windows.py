@@ -1,0 +1,148 @@
+"""GPU: the receptive-field window kernels (csrc/merlin_window.hip) and the window-path update.
+
+merlin_tower_window_lut / _window_conv3 against torch gathers of the same tables on a real
+rollout's windows; merlin_segment_sum against index_add in float64 (skewed lists, with and
+without a minibatch slot map) and bitwise run to run; CNNActorCritic.evaluate_windows against
+the reference-structured frame path (F.conv2d towers on the rendered frames): outputs and every
+parameter gradient; one PPO update with windows against the per-frame lookup path."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rollout_codes(device, N=256, T=32):
+    from merlin import MerlinVecEnv
+
+    env = MerlinVecEnv(N, "mediumhard", seed=777, device=device)
+    codes = torch.zeros((T + 1, N, 8), dtype=torch.int32, device=device)
+    env.reset(out=codes[0])
+    g = torch.Generator(device=device)
+    g.manual_seed(5)
+    for t in range(T):
+        a = torch.randint(0, 3, (N,), device=device, generator=g)
+        env.step_into(a, codes[t + 1], torch.empty(N, device=device), None, None, torch.empty(N, device=device))
+    env.errors()
+    return codes[:T].reshape(-1, 8)
+
+
+def _plan(device):
+    from merlin.dedup import FrameGroups
+    from merlin.windows import WindowPlan
+
+    codes = _rollout_codes(device)
+    fg = FrameGroups(codes)
+    assert fg.ok
+    return codes, WindowPlan(codes, fg)
+
+
+def test_window_lut_and_conv3_match_gathers(device):
+    from merlin import _native as nat
+    from merlin.windows import P2_OF
+
+    codes, plan = _plan(device)
+    torch.manual_seed(0)
+    T2 = torch.randn(2, nat.LUT2_ROWS, 64, device=device)
+    torch.testing.assert_close(nat.window_lut(plan.rows, T2), T2[:, plan.rows.long()].sum(2), rtol=1e-5, atol=1e-5)
+    mb = plan.minibatch(torch.randperm(codes.shape[0], device=device)[:1000])
+    nw = plan.num_windows
+    Q = torch.randn(2, nw, 576, device=device)
+    b3 = torch.randn(2, 64, device=device)
+    Y3 = nat.window_conv3(Q, plan.wid, mb.groups, b3)
+    w = plan.wid[mb.groups].long()[:, torch.tensor(P2_OF, device=device)]
+    ref = torch.relu(Q.view(2, nw, 9, 64)[:, w, torch.arange(9, device=device)].sum(3) + b3[:, None, None])
+    torch.testing.assert_close(Y3.view(2, -1, 9, 64), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,nkeys,L,use_slot", [(1, 3, 4, False), (5000, 37, 64, True),
+                                                (200000, 3000, 1024, True), (70000, 2, 256, False)])
+def test_segment_sum_matches_index_add(device, n, nkeys, L, use_slot):
+    from merlin import _native as nat
+    from merlin.windows import SegmentPlan
+
+    g = torch.Generator(device=device)
+    g.manual_seed(n)
+    keys = (torch.rand(n, device=device, generator=g) ** 3 * nkeys).long()  # long and short lists
+    F_, S = 5000, 9
+    idx = torch.randint(0, F_ * S, (n,), device=device, generator=g)
+    o = torch.sort(keys, stable=True).indices
+    plan = SegmentPlan(keys[o], idx[o], item_len=L)
+    if use_slot:
+        slot = torch.full((F_,), -1, dtype=torch.int32, device=device)
+        chosen = torch.randperm(F_, device=device, generator=g)[:1500]
+        slot[chosen] = torch.arange(1500, dtype=torch.int32, device=device)
+        src = torch.randn(2, 1500 * S, 64, device=device, generator=g)
+        s = slot[idx // S].long()
+        keep = s >= 0
+        rows, kk = s[keep] * S + idx[keep] % S, keys[keep]
+    else:
+        slot = None
+        src = torch.randn(2, F_ * S, 64, device=device, generator=g)
+        rows, kk = idx, keys
+    out = nat.segment_sum(src, plan, nkeys, slot=slot, sub=S)
+    ref = torch.zeros(2, nkeys, 64, dtype=torch.float64, device=device)
+    mag = torch.zeros_like(ref)
+    for t in range(2):
+        ref[t].index_add_(0, kk, src[t, rows].double())
+        mag[t].index_add_(0, kk, src[t, rows].double().abs())
+    err = (out.double() - ref).abs()
+    assert (err <= 1e-5 * mag + 1e-6).all(), (err / (mag + 1e-6)).max().item()
+    assert torch.equal(out, nat.segment_sum(src, plan, nkeys, slot=slot, sub=S))  # fixed order
+
+
+def _loss(lp, ent, v):
+    return -(lp.exp() * 0.7).mean() + 0.5 * (v ** 2).mean() - 0.05 * ent.mean()
+
+
+def test_evaluate_windows_matches_frames(device):
+    from merlin import _native as nat
+    from merlin.actor_critic import CNNActorCritic
+
+    codes, plan = _plan(device)
+    mb_idx = torch.randperm(codes.shape[0], device=device)[:2048]
+    acts = torch.randint(0, 3, (2048,), device=device)
+    torch.manual_seed(12)
+    ac = CNNActorCritic((56, 56, 3), 3).to(device)
+    lp1, e1, v1 = ac.evaluate_windows(plan, plan.minibatch(mb_idx), acts)
+    _loss(lp1, e1, v1).backward()
+    g1 = [p.grad.clone() for p in ac.parameters()]
+    ac.zero_grad()
+    frames = nat.expand_obs(codes, index=mb_idx, scale=1.0 / 255.0)
+    lp2, e2, v2 = ac.evaluate(frames, acts, prescaled=True)
+    _loss(lp2, e2, v2).backward()
+    g2 = [p.grad.clone() for p in ac.parameters()]
+    torch.testing.assert_close(lp1, lp2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(e1, e2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(v1, v2, rtol=1e-5, atol=1e-5)
+    for (name, _), a, b in zip(ac.named_parameters(), g1, g2):
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+        assert rel < 1e-4, (name, rel)
+
+
+def test_window_update_matches_lookup_path(device):
+    """PPO.update through the windows == through per-frame table lookups, same rollout."""
+    from merlin import MerlinVecEnv
+    from merlin.ppo import PPO
+
+    N, T = 256, 32
+    res = []
+    for windows in (True, False):
+        env = MerlinVecEnv(N, "mediumhard", seed=777, device=device)
+        torch.manual_seed(3)
+        g = torch.Generator(device=device)
+        g.manual_seed(11)
+        agent = PPO(env, batch_size=N * T, minibatch_size=N * T // 4, update_epochs=2, ent_coef=0.05,
+                    device=device, windows=windows,
+                    perm_fn=lambda n, e: torch.randperm(n, device=device, generator=g))
+        torch.manual_seed(4)
+        stats = agent.update(agent.collect_rollouts())
+        res.append((stats, [p.detach().clone() for p in agent.ac.parameters()], agent.last_num_windows))
+    (s1, p1, nw), (s2, p2, none) = res
+    assert none is None and 0 < nw < 25 * N * T, nw
+    for k in s1:
+        tol = 4.0 / (N * T // 4) if k == "clipfrac" else 1e-4 * max(1.0, abs(s2[k]))
+        assert abs(s1[k] - s2[k]) <= tol, (k, s1[k], s2[k])
+    for a, b in zip(p1, p2):
+        d = (a - b).abs()
+        assert d.max().item() <= 2 * 3e-4 * 8
+        assert (d > 5e-5).float().mean().item() < 0.05
