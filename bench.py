@@ -42,10 +42,13 @@ os.environ.setdefault("MIOPEN_LOG_LEVEL", "3")
 FWD_MACS = 2 * (1_038_336 + 819_200 + 331_776 + 294_912) + 512 * 3 + 512
 BWD_MACS = 2 * FWD_MACS - 2 * 1_038_336
 # What this implementation runs on the matrix/vector FP32 units: conv1+conv2 are table
-# lookups (no MACs), so per evaluated frame the GEMMs are conv3 + fc1 + heads of both towers;
-# backward = input grad + weight grad of each (2x).  Frames evaluated: every rollout frame
-# once, and every distinct frame of every minibatch once per optimizer step (merlin/dedup.py).
+# lookups (no MACs), so per rollout frame the GEMMs are conv3 + fc1 + heads of both towers;
+# in the update fc1 + heads run once per distinct frame of a minibatch (merlin/dedup.py) and
+# conv3 once per distinct receptive-field window of the rollout (merlin/windows.py: the
+# [windows, 64] x [64, 576] product per tower); backward = input grad + weight grad (2x).
 GEMM_FWD_MACS = 2 * (331_776 + 294_912) + 512 * 3 + 512
+FC_FWD_MACS = 2 * 294_912 + 512 * 3 + 512
+WINDOW_FWD_MACS = 2 * 64 * 576  # per window per minibatch
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (vector == f32 MFMA rate)
 
@@ -65,6 +68,9 @@ def parse():
     ap.add_argument("--no-tiers", action="store_true")
     ap.add_argument("--no-dedup", action="store_true",
                     help="evaluate the towers on every minibatch sample (no distinct-frame grouping)")
+    ap.add_argument("--no-windows", action="store_true",
+                    help="conv2/conv3 per (frame, position) table lookups instead of per distinct window")
+    ap.add_argument("--no-graph", action="store_true", help="launch the rollout eagerly (no captured HIP graph)")
     ap.add_argument("--fomaml", action="store_true",
                     help="cfg 5 instead: FOMAML meta-iterations, tasks_per_batch=32 x k_steps=256")
     ap.add_argument("--tasks", type=int, default=32)
@@ -132,6 +138,40 @@ def env_only_tier(torch, MerlinVecEnv, n, T, difficulty, size, device):
     env.errors()
     env.close()
     return fused, single
+
+
+def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=8):
+    """Tier E at HBM scale: 2M envs (0.35 GB of env state and outputs per step),
+    T single-step k_env_step launches on pre-generated actions, 168 algorithmic bytes per
+    env-step (merlin.envs.ENV_STEP_BYTES); at the bench's 4096 envs the kernel is latency-bound
+    (64 waves on 256 CUs), here it streams."""
+    from merlin.envs import ENV_STEP_BYTES
+
+    env = MerlinVecEnv(n, difficulty=difficulty, size=size, seed=31337, device=device)
+    env.reset()
+    g = torch.Generator(device=device)
+    g.manual_seed(9)
+    acts = torch.randint(0, 3, (T, n), device=device, generator=g)
+    obs = torch.empty((T, n, 8), dtype=torch.int32, device=device)
+    rew = torch.empty((T, n), dtype=torch.float32, device=device)
+    done = torch.empty((T, n), dtype=torch.float32, device=device)
+    env.step_into(acts[0], obs[0], rew[0], None, None, done[0])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for t in range(T):
+        env.step_into(acts[t], obs[t], rew[t], None, None, done[t])
+    e1.record()
+    torch.cuda.synchronize()
+    sec = e0.elapsed_time(e1) / 1e3
+    env.errors()
+    env.close()
+    rate = T * n / sec
+    gbs = rate * ENV_STEP_BYTES / 1e9
+    return {"kernel": "k_env_step", "num_envs": n, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_env_step_large"),
+            "env_steps_per_s": round(rate, 1), "bytes_per_launch": n * ENV_STEP_BYTES,
+            "avg_launch_us": round(sec / T * 1e6, 2), "launches": T}
 
 
 def cpu_baseline():
@@ -225,7 +265,7 @@ def main():
     torch.manual_seed(777)
     agent = PPO(env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=args.epochs, batch_size=B,
                 minibatch_size=B // args.minibatches, vf_coef=0.5, ent_coef=0.05, device=device, dp=dp,
-                dedup=not args.no_dedup)
+                dedup=not args.no_dedup, windows=not args.no_windows, rollout_graph=not args.no_graph)
 
     state["phase"] = "warmup"
     for _ in range(args.warmup):
@@ -267,7 +307,11 @@ def main():
     dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
     ref_flop_per_step = 2 * FWD_MACS + args.epochs * 2 * (FWD_MACS + BWD_MACS)
     frac = agent.last_distinct_frac if agent.last_distinct_frac is not None else 1.0
-    exec_flop_per_step = 2 * GEMM_FWD_MACS * (1 + 3 * args.epochs * frac)
+    if agent.last_num_windows is not None:
+        upd = 3 * args.epochs * (FC_FWD_MACS * frac + WINDOW_FWD_MACS * agent.last_num_windows * args.minibatches / B)
+    else:
+        upd = 3 * args.epochs * GEMM_FWD_MACS * frac
+    exec_flop_per_step = 2 * (GEMM_FWD_MACS + upd)
     loop_tflops = value / world * exec_flop_per_step / 1e12
     out = {
         "metric": "env-steps/sec (rollout+GAE+PPO update), 4096 envs, 16x16 mediumhard",
@@ -289,7 +333,9 @@ def main():
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         # dominant hand-written kernel of the timed loop (by total HIP-event time)
         "roofline": roofline_of(dominant, kernels[dominant]),
-        "roofline_env_step": roofline_of("k_env_step", kernels["k_env_step"]),
+        # the env-step kernel inside the timed loop (absent when the rollout replays as a graph:
+        # no per-kernel events inside it); the HBM-scale measurement is tiers.env_only_2M_envs
+        "roofline_env_step": roofline_of("k_env_step", kernels["k_env_step"]) if "k_env_step" in kernels else None,
         # whole iteration against the FP32 peak, counting the FLOPs actually executed
         # (GEMMs of conv3/fc1/heads on the evaluated frames); the reference formulation's
         # count is given for comparison (reference-equivalent rate = value x that)
@@ -302,6 +348,9 @@ def main():
         # towers evaluated once per distinct observation of a minibatch (merlin/dedup.py)
         "distinct_frames_per_sample": (round(agent.last_distinct_frac, 4)
                                        if agent.last_distinct_frac is not None else None),
+        # conv2/conv3 evaluated once per distinct receptive-field window (merlin/windows.py)
+        "windows_per_update": agent.last_num_windows,
+        "rollout_graph": agent._graph is not None,
         "kernels": kernels,
     }
     state["phase"] = "tiers"
@@ -310,6 +359,7 @@ def main():
         out["tiers"] = {"env_only_fused_T_steps_per_launch": round(fused, 1),
                         "env_only_one_step_per_launch": round(single, 1),
                         "rollout_only": round(B / (rollout_ms / 1e3), 1),
+                        "env_only_2M_envs": env_large_tier(torch, MerlinVecEnv, args.difficulty, args.size, device),
                         "full_loop_per_gpu": round(value / world, 1)}
     state["phase"] = "cpu_baseline"
     if world == 1 and not args.no_cpu_baseline:

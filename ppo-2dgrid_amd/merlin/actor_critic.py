@@ -27,6 +27,10 @@ Conv2d(3,32,k8,s4) equals bias + a sum of 4 entries of a [32][4 slots][20] table
 turns dP into dW1) and the lookups / their transposed histogram run in the HIP library
 (merlin_conv1_lut_fwd/bwd, csrc/merlin_conv1.hip).  Same function, fp32 sums in a
 different order; conv2..heads are the reference modules unchanged.
+
+``evaluate_windows`` (the update's path) evaluates conv2 and conv3 once per distinct
+receptive-field window of the rollout (merlin/windows.py, csrc/merlin_window.hip) and fc1 +
+the heads once per distinct frame of the minibatch.
 """
 from __future__ import annotations
 
@@ -71,7 +75,10 @@ def _categorical(logits: torch.Tensor):
 def _sample_or_argmax(logits: torch.Tensor, logp_all: torch.Tensor, probs: torch.Tensor, deterministic: bool):
     if deterministic:
         return torch.argmax(logits, dim=1)
-    return torch.multinomial(probs.reshape(-1, probs.shape[-1]), 1, True).reshape(probs.shape[:-1])
+    # one Categorical(probs) sample per row by exponential races, argmax_i p_i / E_i with
+    # E_i ~ Exp(1): the form torch.multinomial uses for a single sample, without its host-side
+    # validity check, so the rollout can be captured as a HIP graph (merlin/ppo.py)
+    return (probs / torch.empty_like(probs).exponential_()).argmax(dim=-1)
 
 
 def _entropy(logp_all: torch.Tensor, probs: torch.Tensor) -> torch.Tensor:
@@ -169,6 +176,79 @@ class _Conv2LutTower(torch.autograd.Function):
         return dT, dT[:, 0:20:4, :].sum(1), None, None
 
 
+def _splitk_bmm_tn(X, dY, chunks):
+    """X^T @ dY for X [T, M, K], dY [T, M, N] with the long M reduction split into `chunks`
+    batched GEMMs plus a sum: hipBLASLt runs the plain tall-skinny product at about half the
+    FP32 rate on these shapes (scripts/probe_gemm2.py), the split form at ~105-125 TFLOP/s."""
+    T, M, K = X.shape
+    N = dY.shape[2]
+    c = M // chunks
+    if chunks <= 1 or c < 1024:
+        return torch.bmm(X.transpose(1, 2), dY)
+    head = torch.bmm(X[:, : c * chunks].reshape(T * chunks, c, K).transpose(1, 2),
+                     dY[:, : c * chunks].reshape(T * chunks, c, N)).view(T, chunks, K, N).sum(1)
+    if c * chunks < M:
+        head = head + torch.bmm(X[:, c * chunks:].transpose(1, 2), dY[:, c * chunks:])
+    return head
+
+
+class _BiasReluBmm(torch.autograd.Function):
+    """relu(X @ W + b) over both towers (X [T, M, K], W [T, K, N], b [T, 1, N]): a plain bmm and
+    the in-place bias + ReLU epilogue (merlin_tower_bias_relu); backward: the ReLU mask and the
+    bias gradient in one HIP pass (merlin_tower_relu_bwd), the input gradient as a bmm and the
+    weight gradient as the split-K product."""
+
+    @staticmethod
+    def forward(ctx, X, W, b, chunks):
+        from . import _native as nat
+
+        Y = nat.bias_relu_(torch.bmm(X, W), b.detach().reshape(b.shape[0], -1).contiguous())
+        ctx.save_for_backward(X, W, Y)
+        ctx.chunks = chunks
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        from . import _native as nat
+
+        X, W, Y = ctx.saved_tensors
+        dZ, db = nat.relu_bwd(Y, dY.contiguous())
+        dX = torch.bmm(dZ, W.transpose(1, 2)) if ctx.needs_input_grad[0] else None
+        dW = _splitk_bmm_tn(X, dZ, ctx.chunks)
+        return dX, dW, db.unsqueeze(1), None
+
+
+class _TowerHead(torch.autograd.Function):
+    """fc1 -> ReLU -> heads of both towers (actor_critic.py:30-41) on a3 [2, n, 576] (rows
+    (p3, co), W4's columns permuted to match, W4p [2, H, 576]): one bmm + the bias/ReLU
+    epilogue, then the two small heads.  Backward: the heads' backward, fc1's ReLU mask, fc1's
+    bias gradient and the heads' weight gradients in one HIP pass over h
+    (merlin_tower_head_bwd), then fc1's input gradient (bmm) and weight gradient (split-K)."""
+
+    @staticmethod
+    def forward(ctx, a3, W4p, b4, Wa, ba, Wc, bc):
+        from . import _native as nat
+
+        h = nat.bias_relu_(torch.bmm(a3, W4p.transpose(1, 2)), b4.detach().contiguous())
+        logits = torch.addmm(ba, h[0], Wa.t())
+        value = torch.addmm(bc, h[1], Wc.t()).squeeze(-1)
+        ctx.save_for_backward(a3, W4p, h, Wa, Wc)
+        return logits, value
+
+    @staticmethod
+    def backward(ctx, dlogits, dvalue):
+        from . import _native as nat
+
+        a3, W4p, h, Wa, Wc = ctx.saved_tensors
+        n = h.shape[1]
+        dlogits = h.new_zeros(n, Wa.shape[0]) if dlogits is None else dlogits.contiguous()
+        dvalue = h.new_zeros(n) if dvalue is None else dvalue.contiguous()
+        dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
+        da3 = torch.bmm(dz, W4p) if ctx.needs_input_grad[0] else None
+        dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
+        return da3, dW4p, db4, dWa, dlogits.sum(0), dWc.view_as(Wc), dvalue.sum(0, keepdim=True)
+
+
 def _lut2_h1_index():
     """Per conv1-position parity type (yp, xp), in table order ee, eo, oe, oo: the flat
     indices (slot*20 + 4*class + 2*qy + qx) into P[t][co] of the 4 slot terms of every tile
@@ -251,14 +331,16 @@ class CNNActorCritic(nn.Module):
         ea, ec = self.actor_extractor.network, self.critic_extractor.network
         W3t = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64)
         b3 = torch.stack([ea[4].bias, ec[4].bias]).unsqueeze(1)
-        a3 = torch.relu(torch.baddbmm(b3, A3, W3t)).view(2, n, 576)  # rows (p3, co)
+        a3 = _BiasReluBmm.apply(A3, W3t, b3, 64).view(2, n, 576)  # rows (p3, co)
+        return self._tower_head(a3, n)
+
+    def _tower_head(self, a3, n):
+        """fc1 (W4's columns permuted to the (p3, co) order of a3 [2, n, 576]) -> ReLU -> heads."""
         fa, fc = self.actor[0], self.critic[0]
         W4 = torch.stack([fa.weight, fc.weight])  # [2, hidden, 576] in (co, p3) order
         W4p = W4.view(2, W4.shape[1], 64, 9).transpose(2, 3).reshape(2, W4.shape[1], 576)
-        h = torch.relu(torch.baddbmm(torch.stack([fa.bias, fc.bias]).unsqueeze(1), a3, W4p.transpose(1, 2)))
-        logits = F.linear(h[0], self.actor[2].weight, self.actor[2].bias)
-        value = F.linear(h[1], self.critic[2].weight, self.critic[2].bias).squeeze(-1)
-        return logits, value
+        return _TowerHead.apply(a3, W4p, torch.stack([fa.bias, fc.bias]), self.actor[2].weight, self.actor[2].bias,
+                                self.critic[2].weight, self.critic[2].bias)
 
     def _forward_codes(self, codes, index=None):
         """Both towers from tile codes as GEMMs (csrc/merlin_tower.hip for the data movement):
@@ -285,6 +367,39 @@ class CNNActorCritic(nn.Module):
         fc = self.critic_extractor.network[2:](a1[1])
         return self.actor(fa), self.critic(fc).squeeze(-1)
 
+    def rollout_pack(self):
+        """The weights of the acting path in the layouts its kernels and GEMMs read, built once
+        per rollout (the weights do not change while acting): conv1+conv2 tables, conv3 as
+        [2, 576, 64], fc1 with columns permuted to (p3, co) as [2, 576, H], biases stacked."""
+        ea, ec = self.actor_extractor.network, self.critic_extractor.network
+        fa, fc = self.actor[0], self.critic[0]
+        W4 = torch.stack([fa.weight, fc.weight])
+        H = W4.shape[1]
+        return {
+            "T2": self.conv2_tables().contiguous(),
+            "b2": torch.stack([ea[2].bias, ec[2].bias]).contiguous(),
+            "W3t": torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64).contiguous(),
+            "b3": torch.stack([ea[4].bias, ec[4].bias]).contiguous(),
+            "W4t": W4.view(2, H, 64, 9).transpose(2, 3).reshape(2, H, 576).transpose(1, 2).contiguous(),
+            "b4": torch.stack([fa.bias, fc.bias]).contiguous(),
+        }
+
+    @torch.no_grad()
+    def act_codes_packed(self, codes, pack, deterministic=False):
+        """act_codes with the layouts of rollout_pack(): conv1+conv2 lookups, conv3 / fc1 as
+        plain bmm + the HIP bias/ReLU epilogue, the heads, the categorical sample."""
+        from . import _native as nat
+
+        n = codes.shape[0]
+        A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
+        a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
+        h = nat.bias_relu_(torch.bmm(a3, pack["W4t"]), pack["b4"])
+        logits = torch.addmm(self.actor[2].bias, h[0], self.actor[2].weight.t())
+        value = torch.addmm(self.critic[2].bias, h[1], self.critic[2].weight.t()).squeeze(-1)
+        logp_all, probs = _categorical(logits)
+        action = _sample_or_argmax(logits, logp_all, probs, deterministic)
+        return action, logp_all.gather(-1, action.unsqueeze(-1)).squeeze(-1), value
+
     def act_codes(self, codes, deterministic=False, index=None):
         logits, value = self._forward_codes(codes, index)
         logp_all, probs = _categorical(logits)
@@ -301,6 +416,19 @@ class CNNActorCritic(nn.Module):
             logits, value = logits.index_select(0, inv), value.index_select(0, inv)
         else:
             logits, value = self._forward_codes(codes, index)
+        logp_all, probs = _categorical(logits)
+        logp = logp_all.gather(-1, actions.long().unsqueeze(-1)).squeeze(-1)
+        return logp, _entropy(logp_all, probs), value
+
+    def evaluate_windows(self, plan, mb, actions):
+        """evaluate_codes for one minibatch of the update through its receptive-field windows
+        (merlin/windows.py): conv2 / conv3 once per distinct window of the rollout, fc1 and the
+        heads once per distinct frame of the minibatch (mb.groups); sample k takes row mb.inv[k]."""
+        from .windows import tower_conv3
+
+        n = int(mb.groups.numel())
+        logits, value = self._tower_head(tower_conv3(self, plan, mb).view(2, n, 576), n)
+        logits, value = logits.index_select(0, mb.inv), value.index_select(0, mb.inv)
         logp_all, probs = _categorical(logits)
         logp = logp_all.gather(-1, actions.long().unsqueeze(-1)).squeeze(-1)
         return logp, _entropy(logp_all, probs), value

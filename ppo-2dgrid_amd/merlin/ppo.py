@@ -15,6 +15,8 @@ Env kinds:
     next observation straight into the [T][N] rollout storage.  GAE, the advantage
     moments and the normalisation are HIP kernels; minibatch observations are
     re-expanded from the 32-B codes by index (no 37.6 KB/step f32 frame storage).
+    The update evaluates conv2 / conv3 once per distinct receptive-field window of the
+    rollout and fc1 + heads once per distinct frame of a minibatch (merlin/windows.py).
   * any other gym-style env: the reference's batch-1 loop with f32 frame storage
     (src/ppo.py:64-105), GAE / normalisation still on the HIP kernels.
 
@@ -27,6 +29,8 @@ Per-minibatch scalars are accumulated on the device and read back once per updat
 instead of six .item() syncs per minibatch (ppo.py:158-163).
 """
 from __future__ import annotations
+
+import warnings
 
 import numpy as np
 import torch
@@ -46,7 +50,7 @@ class PPO:
     def __init__(self, env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=10,
                  batch_size=2048, minibatch_size=256, vf_coef=0.5, ent_coef=0.01, device="cuda",
                  *, dp: DataParallel | None = None, perm_fn=None, conv1_from_codes: bool = True,
-                 dedup: bool = True):
+                 dedup: bool = True, windows: bool = True, rollout_graph: bool = True):
         self.env = env
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -63,6 +67,12 @@ class PPO:
         # evaluate each distinct observation of a minibatch once (merlin/dedup.py)
         self.dedup = dedup
         self.last_distinct_frac = None  # distinct frames / samples over the last update
+        # conv2 / conv3 once per distinct receptive-field window of the update (merlin/windows.py)
+        self.windows = windows
+        self.last_num_windows = None
+        # after one eager rollout, replay the vectorised rollout as one captured HIP graph
+        self.rollout_graph = rollout_graph
+        self._graph = None
         self.episode_returns: list[float] = []
         self.episode_lengths: list[int] = []
 
@@ -111,29 +121,57 @@ class PPO:
     def collect_rollouts(self):
         if self.vec is None:
             return self._collect_rollouts_single()
+        if self._graph is not None:
+            self._graph.replay()
+        else:
+            self._rollout_body()
+            if self.rollout_graph and self.conv1_from_codes:
+                self._capture_rollout()
+        self._record_episodes()
+        self.vec.errors()
+        lv = self.buf.last_value
+        return float(lv[0].item()) if self.num_envs == 1 else lv
+
+    def _rollout_body(self):
+        """ppo.py:64-105 for N envs: reset (ppo.py:65: every rollout starts from a fresh
+        reset), T x (act -> env step writing into the [T][N] storage), bootstrap value."""
         buf, env = self.buf, self.vec
         T = buf.T
-        env.reset(out=buf.codes[0])  # ppo.py:65: every rollout starts from a fresh reset
-        obs = self._obs_step
+        env.reset(out=buf.codes[0])
         with torch.no_grad():
+            pack = self.ac.rollout_pack() if self.conv1_from_codes else None
             for t in range(T):
-                action, logp, value = self._act(buf.codes[t], obs)
+                action, logp, value = self._act(buf.codes[t], pack)
                 buf.actions[t].copy_(action)
                 buf.logprobs[t].copy_(logp)
                 buf.values[t].copy_(value)
                 env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
                               buf.ep_return[t], buf.ep_length[t])
-            _, _, last_value = self._act(buf.codes[T], obs)
+            _, _, last_value = self._act(buf.codes[T], pack)
             buf.last_value.copy_(last_value)
-        self._record_episodes()
-        env.errors()
-        return float(last_value[0].item()) if self.num_envs == 1 else buf.last_value
 
-    def _act(self, codes, obs_scratch):
-        if self.conv1_from_codes:
-            return self.ac.act_codes(codes)
-        nat.expand_obs(codes, out=obs_scratch, scale=INV255)
-        return self.ac.act(obs_scratch, prescaled=True)
+    def _capture_rollout(self):
+        """Record _rollout_body as one HIP graph (torch.cuda.graph; the env and lookup kernels
+        launch on the capturing stream through the C ABI, the sampler's RNG offsets advance per
+        replay).  Storage, env state and weights are read in place, so every replay is a fresh
+        rollout with the current weights, launched as one graph instead of ~10k kernels."""
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                self._rollout_body()
+        except Exception as e:  # an op this stack cannot capture: keep launching eagerly
+            warnings.warn(f"rollout graph capture failed, rollouts stay eager: {e}")
+            self.rollout_graph = False
+            torch.cuda.synchronize(self.device)
+            return
+        self._graph = g
+
+    def _act(self, codes, pack):
+        if pack is not None:
+            return self.ac.act_codes_packed(codes, pack)
+        nat.expand_obs(codes, out=self._obs_step, scale=INV255)
+        return self.ac.act(self._obs_step, prescaled=True)
 
     def _record_episodes(self):
         done = self.buf.dones > 0  # finished episodes in (step, env) order
@@ -212,20 +250,29 @@ class PPO:
         totals = torch.zeros(6, dtype=torch.float64, device=self.device)
         nb = 0
         use_codes = codes is not None and self.conv1_from_codes
-        groups = None
+        groups = plan = None
         if use_codes and self.dedup:
             from .dedup import FrameGroups
 
             groups = FrameGroups(codes)
             if not groups.ok:  # a 64-bit hash collision: evaluate every sample this update
                 groups = None
+            elif self.windows:
+                from .windows import WindowPlan
+
+                plan = WindowPlan(codes, groups)
+                self.last_num_windows = plan.num_windows
         distinct = torch.zeros((), dtype=torch.int64, device=self.device)
         for epoch in range(self.update_epochs):
             idxs = self._perm(B, epoch)
             for start in range(0, B, self.minibatch_size):
                 mb_idx = idxs[start:start + self.minibatch_size]
                 lp_old, a_mb, ret_mb = logp_old[mb_idx], adv[mb_idx], returns[mb_idx]
-                if use_codes:
+                if plan is not None:
+                    mbw = plan.minibatch(mb_idx)
+                    distinct += mbw.groups.numel()
+                    logp_new, entropy, values = self.ac.evaluate_windows(plan, mbw, actions[mb_idx])
+                elif use_codes:
                     g = groups.minibatch(mb_idx) if groups is not None else None
                     if g is not None:
                         distinct += g[0].numel()

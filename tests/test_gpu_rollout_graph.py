@@ -1,0 +1,60 @@
+"""GPU: the acting path with per-rollout weight layouts (CNNActorCritic.act_codes_packed) ==
+act_codes, and the captured rollout (PPO._capture_rollout: one HIP graph per rollout) == eager
+launches: its observations, rewards and dones replay bit-exact through an eager env fed its
+actions, its log-probs / values re-evaluate to the stored ones with the weights of that
+rollout, and every replay draws fresh actions."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_packed_act_matches_act_codes(device):
+    from merlin.actor_critic import CNNActorCritic
+    from test_gpu_conv2lut import _codes
+
+    _, codes = _codes(device, 700, seed=3)
+    torch.manual_seed(4)
+    ac = CNNActorCritic((56, 56, 3), 3).to(device)
+    with torch.no_grad():
+        a1, lp1, v1 = ac.act_codes(codes, deterministic=True)
+        a2, lp2, v2 = ac.act_codes_packed(codes, ac.rollout_pack(), deterministic=True)
+    same = a1 == a2
+    assert same.float().mean() > 0.99
+    torch.testing.assert_close(lp1[same], lp2[same], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(v1, v2, rtol=1e-5, atol=1e-5)
+
+
+def test_graph_rollout_matches_eager_env(device):
+    from merlin import MerlinVecEnv
+    from merlin.ppo import PPO
+
+    N, T = 256, 16
+    env = MerlinVecEnv(N, "mediumhard", seed=777, device=device, max_steps=12)
+    mirror = MerlinVecEnv(N, "mediumhard", seed=777, device=device, max_steps=12)
+    torch.manual_seed(0)
+    agent = PPO(env, batch_size=N * T, minibatch_size=N * T // 4, update_epochs=1, ent_coef=0.05, device=device)
+    buf = agent.buf
+    seen = []
+    for it in range(3):
+        lv = agent.collect_rollouts()
+        assert agent._graph is not None  # captured after the first (eager) rollout
+        codes = torch.zeros_like(buf.codes)
+        rew, done = torch.zeros_like(buf.rewards), torch.zeros_like(buf.dones)
+        mirror.reset(out=codes[0])
+        for t in range(T):
+            mirror.step_into(buf.actions[t].contiguous(), codes[t + 1], rew[t], None, None, done[t])
+        assert torch.equal(codes, buf.codes)
+        assert torch.equal(rew, buf.rewards) and torch.equal(done, buf.dones)
+        assert (done.sum(0) >= 1).all()  # max_steps 12 < T: every env auto-reset inside the graph
+        with torch.no_grad():
+            for t in (0, T // 2, T - 1):
+                lp, _, v = agent.ac.evaluate_codes(buf.codes[t], buf.actions[t])
+                torch.testing.assert_close(lp, buf.logprobs[t], rtol=1e-5, atol=1e-5)
+                torch.testing.assert_close(v, buf.values[t], rtol=1e-5, atol=1e-5)
+            _, _, v = agent.ac.act_codes(buf.codes[T])
+            torch.testing.assert_close(v, buf.last_value, rtol=1e-5, atol=1e-5)
+        seen.append(buf.actions.clone())
+        agent.update(lv)  # new weights: the next replay must read them in place
+    assert not torch.equal(seen[1], seen[2])
+    mirror.errors()
