@@ -61,6 +61,7 @@ __global__ __launch_bounds__(EBLK) void k_relu_bwd_colsum(const float4 *__restri
     const int64_t lo = (int64_t)blockIdx.x * per, hi = std::min<int64_t>(rows, lo + per);
     const size_t base = (size_t)t * rows * c4;
     float4 acc = f4_zero();
+#pragma unroll 4
     for (int64_t r = lo + r0; r < hi; r += R) {
         const size_t e = base + (size_t)r * c4 + c;
         const float4 d = f4_mask(Y[e], dY[e]);
@@ -76,15 +77,40 @@ __global__ __launch_bounds__(EBLK) void k_relu_bwd_colsum(const float4 *__restri
     }
 }
 
-// out[t][c] = sum over b (ascending) of partials[t][b][c]
-__global__ __launch_bounds__(256) void k_fold_cols(const float *__restrict__ partials, int nblk, int cols, int T,
-                                                   float *__restrict__ out) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= T * cols) return;
-    const int t = k / cols, c = k - t * cols;
+// Fold of per-block partials: output k (< total) is the sum over blocks b of
+// partials[(t * nblk + b) * S + off] with (t, off) = locate(k).  A block takes 32 outputs; its
+// 8 slices of 32 threads each sum every 8th block (8 loads in flight), then slice 0 adds the
+// 8 slice sums in order: fixed order, and no thread walks all nblk partials serially.
+constexpr int FOLD_COLS = 32, FOLD_SLICES = 8;
+template <typename Locate, typename Store>
+__device__ __forceinline__ void fold_partials(const float *__restrict__ partials, int nblk, int S, int total,
+                                              Locate locate, Store store) {
+    __shared__ float red[FOLD_SLICES][FOLD_COLS];
+    const int c = threadIdx.x % FOLD_COLS, z = threadIdx.x / FOLD_COLS;
+    const int k = blockIdx.x * FOLD_COLS + c;
     float acc = 0.0f;
-    for (int b = 0; b < nblk; b++) acc += partials[((size_t)t * nblk + b) * cols + c];
-    out[k] = acc;
+    if (k < total) {
+        int t, off;
+        locate(k, t, off);
+        const float *p = partials + (size_t)t * nblk * S + off;
+#pragma unroll 8
+        for (int b = z; b < nblk; b += FOLD_SLICES) acc += p[(size_t)b * S];
+    }
+    red[z][c] = acc;
+    __syncthreads();
+    if (z == 0 && k < total) {
+        float sum = red[0][c];
+        for (int q = 1; q < FOLD_SLICES; q++) sum += red[q][c];
+        store(k, sum);
+    }
+}
+
+// out[t][c] = sum over blocks of partials[t][b][c]
+__global__ __launch_bounds__(FOLD_COLS * FOLD_SLICES) void k_fold_cols(const float *__restrict__ partials, int nblk,
+                                                                       int cols, int T, float *__restrict__ out) {
+    fold_partials(
+        partials, nblk, cols, T * cols, [&](int k, int &t, int &off) { t = k / cols; off = k - t * cols; },
+        [&](int k, float v) { out[k] = v; });
 }
 
 // Heads backward with fc1's ReLU mask, h [2][n][H] = relu(fc1) of the actor / critic tower:
@@ -110,6 +136,7 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
     float4 acc = f4_zero();
     const int64_t lo = (int64_t)blockIdx.x * per, hi = std::min<int64_t>(n, lo + per);
     const size_t base = (size_t)t * n * H4;
+#pragma unroll 2
     for (int64_t r = lo + r0; r < hi; r += R) {
         const size_t e = base + (size_t)r * H4 + c;
         const float4 hv = h[e];
@@ -157,30 +184,28 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
     }
 }
 
-// db4[2][H], dWa[A][H], dwc[H] from the head partials (ascending block order)
-__global__ __launch_bounds__(256) void k_head_fold(const float *__restrict__ partials, int nblk, int H, int A,
-                                                   float *__restrict__ db4, float *__restrict__ dwa,
-                                                   float *__restrict__ dwc) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+// db4[2][H], dWa[A][H], dwc[H] from the head partials: tower 0's rows are (db4_0, dWa), tower
+// 1's (db4_1, dwc)
+__global__ __launch_bounds__(FOLD_COLS * FOLD_SLICES) void k_head_fold(const float *__restrict__ partials, int nblk,
+                                                                       int H, int A, float *__restrict__ db4,
+                                                                       float *__restrict__ dwa,
+                                                                       float *__restrict__ dwc) {
     const int S = (1 + A) * H;
-    int t, off;
-    if (k < S) {
-        t = 0;
-        off = k;
-    } else if (k < S + 2 * H) {
-        t = 1;
-        off = k - S;
-    } else {
-        return;
-    }
-    float acc = 0.0f;
-    for (int b = 0; b < nblk; b++) acc += partials[((size_t)t * nblk + b) * S + off];
-    if (off < H)
-        db4[t * H + off] = acc;
-    else if (t == 0)
-        dwa[off - H] = acc;
-    else
-        dwc[off - H] = acc;
+    fold_partials(
+        partials, nblk, S, S + 2 * H,
+        [&](int k, int &t, int &off) {
+            t = k < S ? 0 : 1;
+            off = k < S ? k : k - S;
+        },
+        [&](int k, float v) {
+            const int t = k < S ? 0 : 1, off = k < S ? k : k - S;
+            if (off < H)
+                db4[t * H + off] = v;
+            else if (t == 0)
+                dwa[off - H] = v;
+            else
+                dwc[off - H] = v;
+        });
 }
 
 int blocks_for(int64_t rows) {
@@ -214,7 +239,8 @@ hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, in
                        reinterpret_cast<float4 *>(work));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_fold_cols, dim3((T * cols + 255) / 256), dim3(256), 0, s, work, nblk, cols, T, dbias);
+    hipLaunchKernelGGL(k_fold_cols, dim3((T * cols + FOLD_COLS - 1) / FOLD_COLS), dim3(FOLD_COLS * FOLD_SLICES), 0, s,
+                       work, nblk, cols, T, dbias);
     return hipGetLastError();
 }
 
@@ -234,7 +260,8 @@ hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dv
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int total = (1 + A) * H + 2 * H;
-    hipLaunchKernelGGL(k_head_fold, dim3((total + 255) / 256), dim3(256), 0, s, work, nblk, H, A, db4, dwa, dwc);
+    hipLaunchKernelGGL(k_head_fold, dim3((total + FOLD_COLS - 1) / FOLD_COLS), dim3(FOLD_COLS * FOLD_SLICES), 0, s,
+                       work, nblk, H, A, db4, dwa, dwc);
     return hipGetLastError();
 }
 

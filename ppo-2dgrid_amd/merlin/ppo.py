@@ -265,11 +265,13 @@ class PPO:
         distinct = torch.zeros((), dtype=torch.int64, device=self.device)
         for epoch in range(self.update_epochs):
             idxs = self._perm(B, epoch)
-            for start in range(0, B, self.minibatch_size):
+            # one host read per epoch for the minibatches' distinct-frame groups (merlin/windows.py)
+            mbws = plan.epoch_minibatches(idxs, self.minibatch_size) if plan is not None else None
+            for k, start in enumerate(range(0, B, self.minibatch_size)):
                 mb_idx = idxs[start:start + self.minibatch_size]
                 lp_old, a_mb, ret_mb = logp_old[mb_idx], adv[mb_idx], returns[mb_idx]
                 if plan is not None:
-                    mbw = plan.minibatch(mb_idx)
+                    mbw = mbws[k]
                     distinct += mbw.groups.numel()
                     logp_new, entropy, values = self.ac.evaluate_windows(plan, mbw, actions[mb_idx])
                 elif use_codes:

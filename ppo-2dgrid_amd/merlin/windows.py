@@ -139,6 +139,24 @@ class WindowPlan:
         dk, do = torch.sort(dst, stable=True)
         self.conv3 = SegmentPlan(dk, do // 9, item_len)
 
+    def epoch_minibatches(self, idxs: torch.Tensor, minibatch_size: int) -> list:
+        """MinibatchWindows of every minibatch idxs[k*mb:(k+1)*mb] of one epoch's permutation,
+        grouped by one sort and one host read for the whole epoch (a torch.unique per
+        minibatch would stall the host at every optimizer step).  Same groups as minibatch()."""
+        dev, B, F = idxs.device, int(idxs.numel()), self.num_frames
+        nmb = (B + minibatch_size - 1) // minibatch_size
+        mb_of = torch.arange(B, device=dev) // minibatch_size
+        uniq, inv = torch.unique(mb_of * F + self.frame_groups.uid[idxs], return_inverse=True)
+        counts = torch.bincount(uniq // F, minlength=nmb).tolist()
+        out, off = [], 0
+        for m, c in enumerate(counts):
+            g = uniq[off:off + c] % F
+            slot = torch.full((F,), -1, dtype=torch.int32, device=dev)
+            slot[g] = torch.arange(c, dtype=torch.int32, device=dev)
+            out.append(MinibatchWindows(g, inv[m * minibatch_size:(m + 1) * minibatch_size] - off, slot))
+            off += c
+        return out
+
     def minibatch(self, mb_idx: torch.Tensor) -> MinibatchWindows:
         g, inv = torch.unique(self.frame_groups.uid[mb_idx], return_inverse=True)
         slot = torch.full((self.num_frames,), -1, dtype=torch.int32, device=g.device)

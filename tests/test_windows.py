@@ -134,3 +134,22 @@ def test_window_towers_match_frame_convs(golden):
     dZ2w = torch.randn(2, plan.num_windows, 64, dtype=torch.float64)
     (T2[:, plan.rows.long()].sum(2) * dZ2w).sum().backward()
     torch.testing.assert_close(emulate_segment_sum(plan.hist, dZ2w, 2720), T2.grad)
+
+
+def test_epoch_minibatches_match_per_minibatch_grouping():
+    """WindowPlan.epoch_minibatches (one sort per epoch) == minibatch() on every chunk."""
+    from merlin.dedup import FrameGroups
+    from merlin.windows import WindowPlan
+
+    rs = np.random.RandomState(7)
+    base = rs.randint(0, 5, size=(40, 49)).astype(np.uint8)
+    codes = torch.from_numpy(pack(base[rs.randint(0, 40, size=1000)]))
+    plan = WindowPlan(codes, FrameGroups(codes))
+    idxs = torch.randperm(1000, generator=torch.Generator().manual_seed(1))
+    for mbs in (128, 300, 1000):
+        got = plan.epoch_minibatches(idxs, mbs)
+        assert len(got) == (1000 + mbs - 1) // mbs
+        for k, m in enumerate(got):
+            ref = plan.minibatch(idxs[k * mbs:(k + 1) * mbs])
+            assert torch.equal(m.groups, ref.groups) and torch.equal(m.inv, ref.inv)
+            assert torch.equal(m.slot, ref.slot)
