@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--size", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tiers", action="store_true")
+    ap.add_argument("--env-tier-only", action="store_true",
+                    help="only the HBM-scale env tier (2M envs; for the k_env_step rocprofv3 --pmc pass)")
     ap.add_argument("--no-dedup", action="store_true",
                     help="evaluate the towers on every minibatch sample (no distinct-frame grouping)")
     ap.add_argument("--no-windows", action="store_true",
@@ -189,9 +191,15 @@ def cpu_baseline():
                       "render), batch 2048, 10 epochs x 8 minibatches of 256, fp32 torch CNN (cfg 1 shape)"}
 
 
+# bench names -> rocprofv3 kernel names: the dQ and dT2 segmented sums are one kernel; the
+# PMC summary keeps its largest-grid launches, which are the dQ ones (2048 blocks vs ~90)
+PMC_ALIAS = {"k_seg_sum_dQ": "k_seg_sum"}
+
+
 def pmc_traffic(kernel: str):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 --pmc passes
     (profiles/*_pmc.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE)."""
+    kernel = PMC_ALIAS.get(kernel, kernel)
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
         try:
             d = json.load(open(f)).get(kernel)
@@ -247,6 +255,11 @@ def main():
     import torch.distributed as dist
 
     from merlin import MerlinVecEnv
+    if args.env_tier_only:
+        torch.cuda.set_device(0)
+        print(json.dumps(env_large_tier(torch, MerlinVecEnv, args.difficulty, args.size, torch.device("cuda", 0))),
+              flush=True)
+        return
     from merlin import _native as nat
     from merlin.distributed import DataParallel
     from merlin.ppo import PPO

@@ -248,7 +248,8 @@ int merlin_tower_conv2_lut_bwd(const uint32_t *codes_dev, int64_t n, const float
  *               int32[n_fix][4] = (dst, first item, last item, carry slot in the first item)
  *               for destinations spanning items; carry_dev float[towers][ceil(nnz /
  *               item_len)][2][64] scratch.  out float[towers][out_rows][64] is overwritten
- *               (rows without entries = 0). */
+ *               (rows without entries = 0), or with accumulate != 0 the sums are added to it
+ *               (a list split by source block into several calls sums in call order). */
 int merlin_tower_window_lut(const int32_t *rows_dev, int64_t n_windows, const float *tables_dev,
                             int32_t towers, float *Z2w_dev, void *stream);
 int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
@@ -257,7 +258,33 @@ int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32
 int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *idx_dev,
                        const int32_t *key_dev, int64_t nnz, const int32_t *slot_dev, int32_t sub,
                        int64_t item_len, const int32_t *fix_dev, int64_t n_fix, int32_t towers,
-                       float *out_dev, int64_t out_rows, float *carry_dev, void *stream);
+                       float *out_dev, int64_t out_rows, float *carry_dev, int32_t accumulate,
+                       void *stream);
+
+/* PPO minibatch loss (src/ppo.py:136-150), per distinct frame u < n_frames of the minibatch:
+ *   logits float[n_frames][act_dim] (act_dim <= 8), value float[n_frames]; the frame's samples
+ *   are order[offs[u] .. offs[u+1]) (int32 CSR, offs[n_frames] = n_samples, every frame owns
+ *   >= 1 sample), frame_of int64[n_samples] maps a sample to its frame (frame_of[order[k]] =
+ *   the u whose range holds k), and sample i reads actions / logp_old / adv / ret at
+ *   sample_index[i] (int64; NULL = i).  With logp = log_softmax(logits), ratio = exp(logp[a] -
+ *   logp_old),
+ *   loss = -mean(min(ratio*A, clamp(ratio, 1-clip_eps, 1+clip_eps)*A)) + vf_coef*mean((v-R)^2)
+ *          - ent_coef*mean(entropy)
+ * writes loss float[1], dlogits float[n_frames][act_dim] and dvalue float[n_frames] = d loss /
+ * d (logits, value) summed over each frame's samples (fixed order; torch.min / clamp
+ * subgradients), and adds (-mean(min(...)), mean((v-R)^2), mean(entropy), mean(logp_old -
+ * logp), mean(|ratio-1| > clip_eps)) to stats double[5] (NULL: not written).  workspace double[
+ * merlin_ppo_loss_workspace(n_samples)].  An action outside [0, act_dim) makes the loss NaN.
+ * bias_actor float[act_dim] / bias_critic float[1] (NULL = 0) are added to logits / value
+ * first, and dbias_actor / dbias_critic (NULL: not written) get their gradients. */
+int64_t merlin_ppo_loss_workspace(int64_t n_samples);
+int merlin_ppo_loss(const float *logits_dev, const float *value_dev, const float *bias_actor_dev,
+                    const float *bias_critic_dev, int64_t n_frames, int32_t act_dim, const int32_t *offs_dev,
+                    const int32_t *order_dev, const int64_t *frame_of_dev, int64_t n_samples,
+                    const int64_t *sample_index_dev, const int64_t *actions_dev, const float *logp_old_dev,
+                    const float *adv_dev, const float *ret_dev, double clip_eps, double vf_coef, double ent_coef,
+                    float *dlogits_dev, float *dvalue_dev, float *dbias_actor_dev, float *dbias_critic_dev,
+                    float *loss_dev, double *stats_dev, double *workspace_dev, void *stream);
 
 /* Tower GEMM epilogues (csrc/merlin_head.hip): towers = 1 or 2, `rows` per tower; cols (hidden)
  * a multiple of 4 dividing 1024 (4 x a divisor of 256).  Column sums use a per-device library

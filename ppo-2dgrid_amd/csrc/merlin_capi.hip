@@ -577,14 +577,39 @@ int merlin_tower_window_conv3(const float *Q, int64_t nw, const int32_t *wid, co
 
 int merlin_segment_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
                        const int32_t *slot, int32_t sub, int64_t item_len, const int32_t *fix, int64_t n_fix,
-                       int32_t towers, float *out, int64_t out_rows, float *carry, void *stream) {
+                       int32_t towers, float *out, int64_t out_rows, float *carry, int32_t accumulate,
+                       void *stream) {
     if (!out && out_rows > 0) return fail(MERLIN_E_INVALID, "null output");
     if (nnz > 0 && (!src || !idx || !key || !carry)) return fail(MERLIN_E_INVALID, "null argument");
     if (n_fix > 0 && !fix) return fail(MERLIN_E_INVALID, "null fix-up list");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (item_len <= 0 || sub <= 0) return fail(MERLIN_E_INVALID, "item_len and sub must be > 0");
     HIP_TRY(merlin::launch_seg_sum(src, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
-                                   out_rows, carry, (hipStream_t)stream));
+                                   out_rows, carry, accumulate ? 1 : 0, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int64_t merlin_ppo_loss_workspace(int64_t n_samples) { return merlin::ppo_loss_workspace_doubles(n_samples); }
+
+int merlin_ppo_loss(const float *logits, const float *value, const float *bias_actor, const float *bias_critic,
+                    int64_t n_frames, int32_t act_dim, const int32_t *offs, const int32_t *order,
+                    const int64_t *frame_of, int64_t n_samples, const int64_t *sample_index, const int64_t *actions,
+                    const float *logp_old, const float *adv, const float *ret, double clip_eps, double vf_coef,
+                    double ent_coef, float *dlogits, float *dvalue, float *dbias_actor, float *dbias_critic,
+                    float *loss, double *stats, double *workspace, void *stream) {
+    if (n_frames < 0 || n_samples < 0) return fail(MERLIN_E_INVALID, "negative size");
+    if (n_frames > n_samples) return fail(MERLIN_E_INVALID, "every frame needs at least one sample");
+    if (act_dim < 1 || act_dim > 8) return fail(MERLIN_E_INVALID, "act_dim must be in [1, 8]");
+    if (!workspace) return fail(MERLIN_E_INVALID, "null workspace");
+    if (n_frames > 0 && (!logits || !value || !offs || !dlogits || !dvalue))
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (n_samples > 0 && (!order || !frame_of || !actions || !logp_old || !adv || !ret))
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (n_samples > INT32_MAX) return fail(MERLIN_E_INVALID, "n_samples exceeds int32");
+    HIP_TRY(merlin::launch_ppo_loss(logits, value, bias_actor, bias_critic, n_frames, act_dim, offs, order, frame_of,
+                                    n_samples, sample_index, actions, logp_old, adv, ret, clip_eps, vf_coef, ent_coef,
+                                    dlogits, dvalue, dbias_actor, dbias_critic, loss, stats, workspace,
+                                    (hipStream_t)stream));
     return MERLIN_OK;
 }
 

@@ -90,9 +90,16 @@ hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *d
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
                                const float *b3, int T, float *Y3, hipStream_t s);
+int64_t ppo_loss_workspace_doubles(int64_t n_samples);
+hipError_t launch_ppo_loss(const float *logits, const float *value, const float *bias_a, const float *bias_c,
+                           int64_t U, int A, const int32_t *offs, const int32_t *order, const int64_t *inv, int64_t n,
+                           const int64_t *sample_index, const int64_t *actions, const float *lp_old, const float *adv,
+                           const float *ret, double clip_eps, double vf_coef, double ent_coef, float *dlogits,
+                           float *dvalue, float *dbias_a, float *dbias_c, float *loss, double *stats,
+                           double *workspace, hipStream_t s);
 hipError_t launch_seg_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
                           const int32_t *slot, int S, int64_t L, const int32_t *fix, int64_t nfix, int T, float *out,
-                          int64_t out_rows, float *carry, hipStream_t s);
+                          int64_t out_rows, float *carry, int acc_out, hipStream_t s);
 
 // GEMM epilogues (merlin_head.hip); partial sums use a per-device workspace of
 // epilogue_work_floats() floats

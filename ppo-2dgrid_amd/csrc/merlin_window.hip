@@ -92,14 +92,17 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
 // walks the valid ones in order, SEG_UNROLL row loads in flight (issued unconditionally:
 // a select around a load would make hipcc wait for each load in turn), flushing a
 // destination's sum when the key changes.  The item's first / last destination, when it
-// continues in the neighbouring item, goes to carry[t][item][0 / 1] instead of out.
+// continues in the neighbouring item, goes to carry[t][item][0 / 1] instead of out.  With
+// acc_out the sums are added to out (one writer per destination per launch), so a list split
+// by source block into several launches (merlin/windows.py) accumulates in block order.
 constexpr int SEG_WAVES = 4, SEG_UNROLL = 8;
 __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float2 *__restrict__ src, int64_t src_rows,
                                                            const int32_t *__restrict__ idx,
                                                            const int32_t *__restrict__ key, int64_t nnz,
                                                            const int32_t *__restrict__ slot, int S, int64_t L,
                                                            int64_t nitems, int T, float2 *__restrict__ out,
-                                                           int64_t out_rows, float2 *__restrict__ carry) {
+                                                           int64_t out_rows, float2 *__restrict__ carry,
+                                                           int acc_out) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int t = lane >> 5, c2 = lane & 31;
     const bool live = t < T;
@@ -118,8 +121,15 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float2 *__rest
                 head = acc;
             else if (cur == klast && xlast)
                 tail = acc;
-            else if (live)
-                out[((size_t)t * out_rows + cur) * 32 + c2] = acc;
+            else if (live) {
+                float2 *o = out + ((size_t)t * out_rows + cur) * 32 + c2;
+                if (acc_out) {
+                    const float2 p = *o;
+                    *o = make_float2(p.x + acc.x, p.y + acc.y);
+                } else {
+                    *o = acc;
+                }
+            }
         };
         for (int64_t base = e0; base < e1; base += 64) {
             int row = -1, k = -1;
@@ -173,7 +183,7 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float2 *__rest
 // fix rows (dst, j0, j1, slot0): out[t][dst] = carry[t][j0][slot0] + sum_{j0 < j <= j1} carry[t][j][0]
 __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carry, int64_t nitems,
                                                  const int4 *__restrict__ fix, int64_t nfix, int T,
-                                                 float2 *__restrict__ out, int64_t out_rows) {
+                                                 float2 *__restrict__ out, int64_t out_rows, int acc_out) {
     const int lane = threadIdx.x & 63, t = lane >> 5, c2 = lane & 31;
     for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nfix; f += (int64_t)gridDim.x * 4) {
         if (t >= T) continue;
@@ -186,7 +196,13 @@ __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carr
             acc.x += v.x;
             acc.y += v.y;
         }
-        out[((size_t)t * out_rows + x.x) * 32 + c2] = acc;
+        float2 *o = out + ((size_t)t * out_rows + x.x) * 32 + c2;
+        if (acc_out) {
+            const float2 p = *o;
+            *o = make_float2(p.x + acc.x, p.y + acc.y);
+        } else {
+            *o = acc;
+        }
     }
 }
 
@@ -213,19 +229,20 @@ hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, c
 
 hipError_t launch_seg_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
                           const int32_t *slot, int S, int64_t L, const int32_t *fix, int64_t nfix, int T, float *out,
-                          int64_t out_rows, float *carry, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
+                          int64_t out_rows, float *carry, int acc_out, hipStream_t s) {
+    hipError_t e = acc_out ? hipSuccess : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
     if (e != hipSuccess || nnz <= 0) return e;
     const int64_t nitems = (nnz + L - 1) / L;
     const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
     hipLaunchKernelGGL(k_seg_sum, dim3(grid), dim3(64 * SEG_WAVES), 0, s, reinterpret_cast<const float2 *>(src),
                        src_rows, idx, key, nnz, slot, S, L, nitems, T, reinterpret_cast<float2 *>(out), out_rows,
-                       reinterpret_cast<float2 *>(carry));
+                       reinterpret_cast<float2 *>(carry), acc_out);
     e = hipGetLastError();
     if (e != hipSuccess || nfix <= 0) return e;
     const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);
     hipLaunchKernelGGL(k_seg_fix, dim3(gfix), dim3(256), 0, s, reinterpret_cast<const float2 *>(carry), nitems,
-                       reinterpret_cast<const int4 *>(fix), nfix, T, reinterpret_cast<float2 *>(out), out_rows);
+                       reinterpret_cast<const int4 *>(fix), nfix, T, reinterpret_cast<float2 *>(out), out_rows,
+                       acc_out);
     return hipGetLastError();
 }
 

@@ -86,10 +86,14 @@ def lib():
     L.merlin_tower_conv2_lut_bwd.argtypes = [vp, i64, vp, vp, i32, vp, vp]
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
-    L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, vp]
+    L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
+    L.merlin_ppo_loss_workspace.argtypes = [i64]
+    L.merlin_ppo_loss_workspace.restype = i64
+    L.merlin_ppo_loss.argtypes = [vp, vp, vp, vp, i64, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp, C.c_double,
+                                  C.c_double, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -104,6 +108,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
     "merlin_segment_sum", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
+    "merlin_ppo_loss_workspace", "merlin_ppo_loss",
 )
 
 
@@ -392,23 +397,31 @@ def window_conv3(Q, wid, groups, b3):
     return out
 
 
-def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum"):
+def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum", out=None,
+                accumulate: bool = False, carry=None):
     """out f32[T, out_rows, 64]: out[t][key] = the sum, in entry order, of src[t][row(e)] over
     the plan's entries e with that key (merlin.windows.SegmentPlan); row(e) = idx[e], or
-    slot[idx[e] // sub] * sub + idx[e] % sub with entries whose slot is -1 skipped."""
+    slot[idx[e] // sub] * sub + idx[e] % sub with entries whose slot is -1 skipped.  With
+    accumulate the sums are added to `out` (a list split over source blocks, in call order)."""
     T, src_rows = int(src.shape[0]), int(src.shape[1])
     assert src.shape[2] == 64 and src.dtype == torch.float32
     assert plan.max_key < out_rows
     if slot is not None:
         assert slot.dtype == torch.int32
-    out = torch.empty((T, out_rows, 64), dtype=torch.float32, device=src.device)
-    carry = torch.empty((T, max(plan.nitems, 1), 2, 64), dtype=torch.float32, device=src.device)
+    if out is None:
+        assert not accumulate
+        out = torch.empty((T, out_rows, 64), dtype=torch.float32, device=src.device)
+    assert out.shape == (T, out_rows, 64) and out.dtype == torch.float32 and out.is_contiguous()
+    need = T * max(plan.nitems, 1) * 128
+    if carry is None or carry.numel() < need:
+        carry = torch.empty(need, dtype=torch.float32, device=src.device)
     # algorithmic bytes: the entry lists (+ slot lookups), src read once, out written
     nb = plan.nnz * (8 + (4 if slot is not None else 0)) + T * (src_rows + out_rows) * 256
     with KernelTimer.span(name, nb):
         check(lib().merlin_segment_sum(ptr(src), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz, ptr(slot),
                                        int(sub), plan.item_len, ptr(plan.fix), int(plan.fix.shape[0]), T, ptr(out),
-                                       int(out_rows), ptr(carry), stream_of(src)), "merlin_segment_sum")
+                                       int(out_rows), ptr(carry), int(bool(accumulate)), stream_of(src)),
+              "merlin_segment_sum")
     return out
 
 
@@ -449,3 +462,46 @@ def head_bwd(h, dlogits, dvalue, w_actor, w_critic):
         check(lib().merlin_tower_head_bwd(ptr(h), ptr(dlogits), ptr(dvalue), ptr(w_actor), ptr(w_critic), n, H, A,
                                           ptr(dz), ptr(db), ptr(dwa), ptr(dwc), stream_of(h)), "merlin_tower_head_bwd")
     return dz, db, dwa, dwc
+
+
+# -- PPO loss (csrc/merlin_loss.hip) -------------------------------------------------------------
+def ppo_loss(logits, value, offs, order, frame_of, sample_index, actions, logp_old, adv, ret, clip_eps, vf_coef,
+             ent_coef, stats=None, bias_actor=None, bias_critic=None):
+    """(loss f32[], dlogits f32[U, A], dvalue f32[U], dbias_actor f32[A] | None, dbias_critic f32[1] |
+    None): the PPO minibatch loss of src/ppo.py:136-150 over the samples of U distinct frames (CSR
+    offs int32[U+1] / order int32[n], frame_of int64[n] = the frame of sample i; sample i reads
+    actions / logp_old / adv / ret at sample_index[i]) and its gradient per frame.  With the
+    heads' biases given, logits / value exclude them and their gradients are returned too.
+    stats f64[>=5], when given, gets (pi_loss, v_loss, entropy, approx_kl, clipfrac) added."""
+    U, A = (int(x) for x in logits.shape)
+    n = int(order.numel())
+    assert logits.dtype == value.dtype == torch.float32 and value.shape == (U,)
+    assert offs.dtype == order.dtype == torch.int32 and offs.shape == (U + 1,)
+    assert frame_of.dtype == torch.int64 and frame_of.numel() == n and U <= n
+    assert actions.dtype == torch.int64 and logp_old.dtype == adv.dtype == ret.dtype == torch.float32
+    if sample_index is not None:
+        assert sample_index.dtype == torch.int64 and sample_index.numel() == n
+    if stats is not None:
+        assert stats.dtype == torch.float64 and stats.numel() >= 5 and stats.is_contiguous()
+    dev = logits.device
+    dlogits = torch.empty((U, A), dtype=torch.float32, device=dev)
+    dvalue = torch.empty((U,), dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    dba = dbc = None
+    if bias_actor is not None:
+        assert bias_actor.shape == (A,) and bias_actor.dtype == torch.float32
+        bias_actor = bias_actor.detach().contiguous()
+        dba = torch.empty((A,), dtype=torch.float32, device=dev)
+    if bias_critic is not None:
+        assert bias_critic.numel() == 1 and bias_critic.dtype == torch.float32
+        bias_critic = bias_critic.detach().contiguous()
+        dbc = torch.empty((1,), dtype=torch.float32, device=dev)
+    ws = torch.empty(max(int(lib().merlin_ppo_loss_workspace(n)), 1), dtype=torch.float64, device=dev)
+    with KernelTimer.span("k_ppo_loss", U * (4 * A + 4) * 2 + n * (4 + 8 + 8 + 12)):
+        check(lib().merlin_ppo_loss(ptr(logits.contiguous()), ptr(value.contiguous()), ptr(bias_actor),
+                                    ptr(bias_critic), U, A, ptr(offs), ptr(order), ptr(frame_of), n,
+                                    ptr(sample_index), ptr(actions.contiguous()), ptr(logp_old.contiguous()),
+                                    ptr(adv.contiguous()), ptr(ret.contiguous()), float(clip_eps), float(vf_coef),
+                                    float(ent_coef), ptr(dlogits), ptr(dvalue), ptr(dba), ptr(dbc), ptr(loss),
+                                    ptr(stats), ptr(ws), stream_of(logits)), "merlin_ppo_loss")
+    return loss, dlogits, dvalue, dba, dbc

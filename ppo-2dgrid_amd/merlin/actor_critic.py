@@ -185,8 +185,13 @@ def _splitk_bmm_tn(X, dY, chunks):
     c = M // chunks
     if chunks <= 1 or c < 1024:
         return torch.bmm(X.transpose(1, 2), dY)
-    head = torch.bmm(X[:, : c * chunks].reshape(T * chunks, c, K).transpose(1, 2),
-                     dY[:, : c * chunks].reshape(T * chunks, c, N)).view(T, chunks, K, N).sum(1)
+    # per tower the first c*chunks rows are a view [chunks, c, K] (merging the tower and chunk
+    # dims would copy both operands whenever M % chunks != 0: 2 x 0.1 ms per call at the bench size)
+    part = X.new_empty((T, chunks, K, N))
+    for t in range(T):
+        torch.bmm(X[t, : c * chunks].view(chunks, c, K).transpose(1, 2), dY[t, : c * chunks].view(chunks, c, N),
+                  out=part[t])
+    head = part.sum(1)
     if c * chunks < M:
         head = head + torch.bmm(X[:, c * chunks:].transpose(1, 2), dY[:, c * chunks:])
     return head
@@ -230,9 +235,10 @@ class _TowerHead(torch.autograd.Function):
         from . import _native as nat
 
         h = nat.bias_relu_(torch.bmm(a3, W4p.transpose(1, 2)), b4.detach().contiguous())
-        logits = torch.addmm(ba, h[0], Wa.t())
-        value = torch.addmm(bc, h[1], Wc.t()).squeeze(-1)
+        logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
+        value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)
         ctx.save_for_backward(a3, W4p, h, Wa, Wc)
+        ctx.head_bias = (ba is not None, bc is not None)
         return logits, value
 
     @staticmethod
@@ -246,7 +252,9 @@ class _TowerHead(torch.autograd.Function):
         dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
         da3 = torch.bmm(dz, W4p) if ctx.needs_input_grad[0] else None
         dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
-        return da3, dW4p, db4, dWa, dlogits.sum(0), dWc.view_as(Wc), dvalue.sum(0, keepdim=True)
+        dba = dlogits.sum(0) if ctx.head_bias[0] else None
+        dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
+        return da3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc
 
 
 def _lut2_h1_index():
@@ -334,13 +342,14 @@ class CNNActorCritic(nn.Module):
         a3 = _BiasReluBmm.apply(A3, W3t, b3, 64).view(2, n, 576)  # rows (p3, co)
         return self._tower_head(a3, n)
 
-    def _tower_head(self, a3, n):
+    def _tower_head(self, a3, n, head_bias: bool = True):
         """fc1 (W4's columns permuted to the (p3, co) order of a3 [2, n, 576]) -> ReLU -> heads."""
         fa, fc = self.actor[0], self.critic[0]
         W4 = torch.stack([fa.weight, fc.weight])  # [2, hidden, 576] in (co, p3) order
         W4p = W4.view(2, W4.shape[1], 64, 9).transpose(2, 3).reshape(2, W4.shape[1], 576)
-        return _TowerHead.apply(a3, W4p, torch.stack([fa.bias, fc.bias]), self.actor[2].weight, self.actor[2].bias,
-                                self.critic[2].weight, self.critic[2].bias)
+        ba, bc = (self.actor[2].bias, self.critic[2].bias) if head_bias else (None, None)
+        return _TowerHead.apply(a3, W4p, torch.stack([fa.bias, fc.bias]), self.actor[2].weight, ba,
+                                self.critic[2].weight, bc)
 
     def _forward_codes(self, codes, index=None):
         """Both towers from tile codes as GEMMs (csrc/merlin_tower.hip for the data movement):
@@ -420,14 +429,20 @@ class CNNActorCritic(nn.Module):
         logp = logp_all.gather(-1, actions.long().unsqueeze(-1)).squeeze(-1)
         return logp, _entropy(logp_all, probs), value
 
-    def evaluate_windows(self, plan, mb, actions):
-        """evaluate_codes for one minibatch of the update through its receptive-field windows
-        (merlin/windows.py): conv2 / conv3 once per distinct window of the rollout, fc1 and the
-        heads once per distinct frame of the minibatch (mb.groups); sample k takes row mb.inv[k]."""
+    def heads_windows(self, plan, mb, head_bias: bool = True):
+        """(logits [U, act_dim], value [U]) of the minibatch's distinct frames mb.groups through
+        the receptive-field windows (merlin/windows.py): conv2 / conv3 once per distinct window of
+        the rollout, fc1 and the heads once per distinct frame.  head_bias=False leaves the heads'
+        biases out (merlin.ppo's fused loss adds them and returns their gradients)."""
         from .windows import tower_conv3
 
         n = int(mb.groups.numel())
-        logits, value = self._tower_head(tower_conv3(self, plan, mb).view(2, n, 576), n)
+        return self._tower_head(tower_conv3(self, plan, mb).view(2, n, 576), n, head_bias)
+
+    def evaluate_windows(self, plan, mb, actions):
+        """evaluate_codes for one minibatch of the update through heads_windows; sample k takes
+        frame row mb.inv[k]."""
+        logits, value = self.heads_windows(plan, mb)
         logits, value = logits.index_select(0, mb.inv), value.index_select(0, mb.inv)
         logp_all, probs = _categorical(logits)
         logp = logp_all.gather(-1, actions.long().unsqueeze(-1)).squeeze(-1)

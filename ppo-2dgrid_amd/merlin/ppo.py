@@ -46,6 +46,26 @@ from .rollout_buffer import CodeRolloutBuffer, RolloutBuffer
 INV255 = 1.0 / 255.0
 
 
+class _PPOLoss(torch.autograd.Function):
+    """The minibatch loss of src/ppo.py:136-150 from per-distinct-frame logits / values (the
+    heads' outputs without their biases) and the heads' biases: one HIP pass (merlin_ppo_loss)
+    computes the loss, its gradient per frame and for the biases, and the update statistics
+    (added to `stats`); backward only scales the stored gradients."""
+
+    @staticmethod
+    def forward(ctx, logits, value, bias_actor, bias_critic, mb, sample_index, actions, logp_old, adv, ret, clip_eps,
+                vf_coef, ent_coef, stats):
+        loss, dlogits, dvalue, dba, dbc = nat.ppo_loss(
+            logits.detach(), value.detach(), mb.offs, mb.order, mb.inv, sample_index, actions, logp_old, adv, ret,
+            clip_eps, vf_coef, ent_coef, stats, bias_actor=bias_actor, bias_critic=bias_critic)
+        ctx.save_for_backward(dlogits, dvalue, dba, dbc.view_as(bias_critic))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        return tuple(d * g for d in ctx.saved_tensors) + (None,) * 10
+
+
 class PPO:
     def __init__(self, env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=10,
                  batch_size=2048, minibatch_size=256, vf_coef=0.5, ent_coef=0.01, device="cuda",
@@ -102,7 +122,8 @@ class PPO:
                 self.obs_shape = sample_obs.shape
                 self.ac = CNNActorCritic(self.obs_shape, act_dim).to(self.device)
             self.buffer = RolloutBuffer(batch_size, self.obs_shape, self.device, is_discrete=True)
-        self.optimizer = optim.Adam(self.ac.parameters(), lr=lr)
+        # torch's fused Adam: one multi-tensor kernel per step instead of the foreach chain (~9)
+        self.optimizer = optim.Adam(self.ac.parameters(), lr=lr, fused=True)
         self.dp.attach(self.ac)
         self._params = [p for p in self.ac.parameters() if p.requires_grad]
 
@@ -262,50 +283,56 @@ class PPO:
 
                 plan = WindowPlan(codes, groups)
                 self.last_num_windows = plan.num_windows
-        distinct = torch.zeros((), dtype=torch.int64, device=self.device)
+        distinct = 0
         for epoch in range(self.update_epochs):
             idxs = self._perm(B, epoch)
             # one host read per epoch for the minibatches' distinct-frame groups (merlin/windows.py)
             mbws = plan.epoch_minibatches(idxs, self.minibatch_size) if plan is not None else None
             for k, start in enumerate(range(0, B, self.minibatch_size)):
                 mb_idx = idxs[start:start + self.minibatch_size]
-                lp_old, a_mb, ret_mb = logp_old[mb_idx], adv[mb_idx], returns[mb_idx]
                 if plan is not None:
+                    # distinct frames only: merlin_ppo_loss sums each frame's samples (mb.offs/order)
+                    # and adds the statistics to totals[:5] on the device
                     mbw = mbws[k]
-                    distinct += mbw.groups.numel()
-                    logp_new, entropy, values = self.ac.evaluate_windows(plan, mbw, actions[mb_idx])
-                elif use_codes:
-                    g = groups.minibatch(mb_idx) if groups is not None else None
-                    if g is not None:
-                        distinct += g[0].numel()
-                    logp_new, entropy, values = self.ac.evaluate_codes(codes, actions[mb_idx], index=mb_idx,
-                                                                       groups=g)
+                    distinct += int(mbw.groups.numel())
+                    logits, values = self.ac.heads_windows(plan, mbw, head_bias=False)
+                    loss = _PPOLoss.apply(logits, values, self.ac.actor[2].bias, self.ac.critic[2].bias, mbw, mb_idx,
+                                          actions, logp_old, adv, returns, self.clip_eps, self.vf_coef,
+                                          self.ent_coef, totals)
                 else:
-                    obs, pre = self._minibatch_obs(codes, states, mb_idx)
-                    logp_new, entropy, values = self.ac.evaluate(obs, actions[mb_idx], prescaled=pre)
-                values = values.squeeze(-1)
-                ratio = torch.exp(logp_new - lp_old)
-                surr1 = ratio * a_mb
-                surr2 = torch.clamp(ratio, 1 - self.clip_eps, 1 + self.clip_eps) * a_mb
-                pi_loss = -torch.min(surr1, surr2).mean()
-                v_loss = ((values - ret_mb) ** 2).mean()
-                ent = entropy.mean()
-                loss = pi_loss + self.vf_coef * v_loss - self.ent_coef * ent
-                with torch.no_grad():
-                    approx_kl = (lp_old - logp_new).mean()
-                    clipfrac = (torch.abs(ratio - 1.0) > self.clip_eps).float().mean()
+                    lp_old, a_mb, ret_mb = logp_old[mb_idx], adv[mb_idx], returns[mb_idx]
+                    if use_codes:
+                        g = groups.minibatch(mb_idx) if groups is not None else None
+                        if g is not None:
+                            distinct += int(g[0].numel())
+                        logp_new, entropy, values = self.ac.evaluate_codes(codes, actions[mb_idx], index=mb_idx,
+                                                                           groups=g)
+                    else:
+                        obs, pre = self._minibatch_obs(codes, states, mb_idx)
+                        logp_new, entropy, values = self.ac.evaluate(obs, actions[mb_idx], prescaled=pre)
+                    values = values.squeeze(-1)
+                    ratio = torch.exp(logp_new - lp_old)
+                    surr1 = ratio * a_mb
+                    surr2 = torch.clamp(ratio, 1 - self.clip_eps, 1 + self.clip_eps) * a_mb
+                    pi_loss = -torch.min(surr1, surr2).mean()
+                    v_loss = ((values - ret_mb) ** 2).mean()
+                    ent = entropy.mean()
+                    loss = pi_loss + self.vf_coef * v_loss - self.ent_coef * ent
+                    with torch.no_grad():
+                        approx_kl = (lp_old - logp_new).mean()
+                        clipfrac = (torch.abs(ratio - 1.0) > self.clip_eps).float().mean()
+                        totals[:5] += torch.stack([pi_loss.detach(), v_loss.detach(), ent.detach(), approx_kl,
+                                                   clipfrac]).double()
                 self.dp.zero_grad(self.optimizer)
                 loss.backward()
                 self.dp.allreduce_grads()
                 grad_norm = torch.nn.utils.clip_grad_norm_(self._params, 0.5)
                 self.optimizer.step()
-                with torch.no_grad():
-                    totals += torch.stack([pi_loss.detach(), v_loss.detach(), ent.detach(), approx_kl,
-                                           clipfrac, grad_norm.detach()]).double()
+                totals[5:].add_(grad_norm.detach())
                 nb += 1
         t = totals.cpu().tolist()
         if groups is not None:
-            self.last_distinct_frac = float(distinct.item()) / float(self.update_epochs * B)
+            self.last_distinct_frac = float(distinct) / float(self.update_epochs * B)
         return aggregate_ppo_update_metrics(*t, nb)
 
     def train(self, total_steps=100_000):

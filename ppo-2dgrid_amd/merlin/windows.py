@@ -18,8 +18,9 @@ runs through the tables and the GEMM, and the adjoints of the two gathers are se
 over lists sorted once per update (merlin_segment_sum: fixed order, no atomics):
 
   dQ[t][w][tap] = sum of dZ3[t][u, p3] over the minibatch's (u, p3) whose window at p3 + tap
-                  is w (the list holds every distinct frame of the rollout; a slot table
-                  skips the frames outside the minibatch)
+                  is w (the lists hold every distinct frame of the rollout, one list per
+                  block of frame ids so that each pass gathers from 1/DQ_BLOCKS of dZ3; a
+                  slot table skips the frames outside the minibatch)
   dT2[t][row]   = sum of dZ2w[t][w] over the (w, tap) that read table row `row`
 
 Same function and gradients as the reference towers, fp32 sums regrouped.  The minibatch's
@@ -34,6 +35,14 @@ from . import _native as nat
 # conv3 output p3 = (oy, ox) and tap = (ky, kx) -> conv2 position (oy + ky) * 5 + (ox + kx)
 P2_OF = [[(p // 3 + k // 3) * 5 + p % 3 + k % 3 for k in range(9)] for p in range(9)]
 ITEM_LEN = 1024      # entries per wave of the dQ lists (81 per distinct frame of the rollout)
+# The dQ entries gather 256-B rows of dZ3 ([2, U*9, 64]: 322 MB at the bench size), each row
+# once per tap (9x); sorted by destination alone the re-reads miss the 256 MB MALL (rocprofv3:
+# 3.7 GB of HBM traffic per call, 0.57 ms).  The lists can be split by blocks of frame ids (a
+# minibatch numbers its distinct frames in ascending id, so block b's pass reads a contiguous
+# 1/dq_blocks of dZ3) with the blocks' sums added in block order; measured on MI355X, 8 blocks
+# of 256-entry items took 0.78 ms per minibatch (8 launches, each latency-bound on the
+# idx -> slot -> row chain), so the default stays one list.
+DQ_BLOCKS = 1
 HIST_ITEM_LEN = 256  # of the dT2 lists (16 per window)
 
 
@@ -108,10 +117,17 @@ class SegmentPlan:
 
 class MinibatchWindows:
     """One minibatch's distinct frames: groups int64 [U] (frame ids of the plan, ascending),
-    inv int64 [n] (sample -> position in groups), slot int32 [F] (frame id -> position or -1)."""
+    inv int64 [n] (sample -> position in groups), slot int32 [F] (frame id -> position or -1),
+    and the samples of each frame as CSR: order int32 [n] (sample positions grouped by frame,
+    ascending within a frame), offs int32 [U+1] (merlin_ppo_loss sums per frame in that order)."""
 
-    def __init__(self, groups: torch.Tensor, inv: torch.Tensor, slot: torch.Tensor):
+    def __init__(self, groups: torch.Tensor, inv: torch.Tensor, slot: torch.Tensor, order=None, offs=None):
         self.groups, self.inv, self.slot = groups, inv, slot
+        self.order, self.offs = order, offs
+
+
+def _frame_csr(starts: torch.Tensor, n: int) -> torch.Tensor:
+    return torch.cat([starts, starts.new_tensor([n])]).to(torch.int32)
 
 
 class WindowPlan:
@@ -119,7 +135,7 @@ class WindowPlan:
     (frame id = merlin.dedup.FrameGroups group id) and the two backward entry lists."""
 
     def __init__(self, codes: torch.Tensor, frame_groups, item_len: int = ITEM_LEN,
-                 hist_item_len: int = HIST_ITEM_LEN):
+                 hist_item_len: int = HIST_ITEM_LEN, dq_blocks: int = DQ_BLOCKS):
         dev = codes.device
         self.frame_groups = frame_groups
         rep = codes.index_select(0, frame_groups.rep)  # one code row per distinct frame
@@ -133,35 +149,59 @@ class WindowPlan:
         # dT2 lists: entry (w, tap) -> table row rows[w][tap]; source row w of dZ2w
         hk, ho = torch.sort(self.rows.reshape(-1), stable=True)
         self.hist = SegmentPlan(hk, ho // 16, hist_item_len)
-        # dQ lists: entry (frame g, p3, tap) -> Q row wid[g][p3 + tap] * 9 + tap; source dZ3 row g*9 + p3
+        # dQ lists: entry (frame g, p3, tap) -> Q row wid[g][p3 + tap] * 9 + tap; source dZ3 row
+        # g*9 + p3; one destination-sorted list per block of frame ids (DQ_BLOCKS)
         p2 = torch.tensor(P2_OF, dtype=torch.int64, device=dev)
-        dst = (self.wid[:, p2] * 9 + torch.arange(9, dtype=torch.int32, device=dev)).reshape(-1)
-        dk, do = torch.sort(dst, stable=True)
-        self.conv3 = SegmentPlan(dk, do // 9, item_len)
+        dst = (self.wid[:, p2].long() * 9 + torch.arange(9, dtype=torch.int64, device=dev)).reshape(-1)
+        nd, nb = nw * 9, max(1, min(int(dq_blocks), F))
+        blk = torch.arange(F, dtype=torch.int64, device=dev) * nb // F
+        dk, do = torch.sort(blk.repeat_interleave(81) * nd + dst, stable=True)
+        self.conv3_blocks = []
+        off = 0
+        for b, c in enumerate(torch.bincount(blk, minlength=nb).mul_(81).tolist()):
+            if c:
+                self.conv3_blocks.append(SegmentPlan(dk[off:off + c] - b * nd, do[off:off + c] // 9, item_len))
+            off += c
 
     def epoch_minibatches(self, idxs: torch.Tensor, minibatch_size: int) -> list:
         """MinibatchWindows of every minibatch idxs[k*mb:(k+1)*mb] of one epoch's permutation,
-        grouped by one sort and one host read for the whole epoch (a torch.unique per
+        grouped by one stable sort and one host read for the whole epoch (a torch.unique per
         minibatch would stall the host at every optimizer step).  Same groups as minibatch()."""
         dev, B, F = idxs.device, int(idxs.numel()), self.num_frames
         nmb = (B + minibatch_size - 1) // minibatch_size
         mb_of = torch.arange(B, device=dev) // minibatch_size
-        uniq, inv = torch.unique(mb_of * F + self.frame_groups.uid[idxs], return_inverse=True)
+        sk, perm = torch.sort(mb_of * F + self.frame_groups.uid[idxs], stable=True)
+        new = torch.ones(B, dtype=torch.bool, device=dev)
+        new[1:] = sk[1:] != sk[:-1]
+        inv = torch.empty(B, dtype=torch.int64, device=dev)
+        inv[perm] = torch.cumsum(new, 0) - 1
+        starts = torch.nonzero(new).squeeze(1)  # first sorted position of each (minibatch, frame)
+        uniq = sk[starts]
         counts = torch.bincount(uniq // F, minlength=nmb).tolist()
         out, off = [], 0
         for m, c in enumerate(counts):
+            lo, hi = m * minibatch_size, min(B, (m + 1) * minibatch_size)
             g = uniq[off:off + c] % F
             slot = torch.full((F,), -1, dtype=torch.int32, device=dev)
             slot[g] = torch.arange(c, dtype=torch.int32, device=dev)
-            out.append(MinibatchWindows(g, inv[m * minibatch_size:(m + 1) * minibatch_size] - off, slot))
+            # sorted positions lo..hi hold exactly this minibatch's samples (mb_of is the major key)
+            order = (perm[lo:hi] - lo).to(torch.int32)
+            out.append(MinibatchWindows(g, inv[lo:hi] - off, slot, order, _frame_csr(starts[off:off + c] - lo, hi - lo)))
             off += c
         return out
 
     def minibatch(self, mb_idx: torch.Tensor) -> MinibatchWindows:
-        g, inv = torch.unique(self.frame_groups.uid[mb_idx], return_inverse=True)
+        n = int(mb_idx.numel())
+        sk, perm = torch.sort(self.frame_groups.uid[mb_idx], stable=True)
+        new = torch.ones(n, dtype=torch.bool, device=mb_idx.device)
+        new[1:] = sk[1:] != sk[:-1]
+        starts = torch.nonzero(new).squeeze(1)
+        g = sk[starts]
+        inv = torch.empty(n, dtype=torch.int64, device=mb_idx.device)
+        inv[perm] = torch.cumsum(new, 0) - 1
         slot = torch.full((self.num_frames,), -1, dtype=torch.int32, device=g.device)
         slot[g] = torch.arange(g.numel(), dtype=torch.int32, device=g.device)
-        return MinibatchWindows(g, inv, slot)
+        return MinibatchWindows(g, inv, slot, perm.to(torch.int32), _frame_csr(starts, n))
 
 
 class _WindowConv2(torch.autograd.Function):
@@ -193,7 +233,11 @@ class _WindowConv3(torch.autograd.Function):
         (Y3,) = ctx.saved_tensors
         plan = ctx.plan
         dZ3, db3 = nat.relu_bwd(Y3, dY3.contiguous())
-        dQ = nat.segment_sum(dZ3, plan.conv3, plan.num_windows * 9, slot=ctx.mb.slot, sub=9, name="k_seg_sum_dQ")
+        dQ = torch.zeros((dZ3.shape[0], plan.num_windows * 9, 64), dtype=dZ3.dtype, device=dZ3.device)
+        carry = dZ3.new_empty(dZ3.shape[0] * max([p.nitems for p in plan.conv3_blocks] + [1]) * 128)
+        for b, part in enumerate(plan.conv3_blocks):  # source blocks, summed in block order
+            nat.segment_sum(dZ3, part, plan.num_windows * 9, slot=ctx.mb.slot, sub=9, name="k_seg_sum_dQ",
+                            out=dQ, accumulate=b > 0, carry=carry)
         return dQ.view(dQ.shape[0], plan.num_windows, 576), db3, None, None
 
 

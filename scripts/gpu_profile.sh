@@ -14,6 +14,13 @@ if [ -n "$PMC" ]; then
         > "$R/gpurun_out/prof_pmc_$C.log" 2>&1 || exit $?
     echo "pmc $C done"
   done
+  # the HBM-scale env tier alone (2M envs): k_env_step's per-launch HBM bytes -> k_env_step_large
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "k_env_step" -T -f csv \
+        -d "$R/gpurun_out/prof_pmcenv_$C" -o run -- python "$R/bench.py" --env-tier-only \
+        > "$R/gpurun_out/prof_pmcenv_$C.log" 2>&1 || exit $?
+    echo "pmc env $C done"
+  done
 fi
 find "$R/gpurun_out" -name "*.csv" | head -20
 if [ -n "$LAYERS" ]; then

@@ -36,23 +36,32 @@ def stats(tag):
 
 def pmc(tag):
     res = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        src = os.path.join(OUT, f"prof_pmc_{counter}", "run_counter_collection.csv")
-        if not os.path.exists(src):
-            continue
-        per = {}
-        for r in csv.DictReader(open(src)):
-            per.setdefault(r["Kernel_Name"], []).append((int(r["Grid_Size"]), float(r["Counter_Value"])))
-        for k, vals in per.items():
-            g = max(v[0] for v in vals)
-            big = [v[1] for v in vals if v[0] == g]
-            d = res.setdefault(k, {"grid": g, "launches": len(big)})
-            d[counter.lower() + "_kb"] = sum(big) / len(big)
+    # prof_pmc_*: the bench loop; prof_pmcenv_*: bench.py --env-tier-only (2M envs), whose
+    # k_env_step launches are keyed k_env_step_large (bench.py tiers.env_only_2M_envs)
+    for pre, rename in (("prof_pmc_", {}), ("prof_pmcenv_", {"k_env_step": "k_env_step_large"})):
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            src = os.path.join(OUT, f"{pre}{counter}", "run_counter_collection.csv")
+            if os.path.exists(src):
+                collect(res, src, counter, rename)
     for k, d in res.items():
         if "fetch_size_kb" in d and "write_size_kb" in d:
             d["hbm_bytes_per_launch"] = int((2 * d["fetch_size_kb"] + d["write_size_kb"]) * 1024)
     if res:
         json.dump(res, open(os.path.join(REPO, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
+
+
+def collect(res, src, counter, rename):
+    per = {}
+    for r in csv.DictReader(open(src)):
+        name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").strip()
+        name = name.split("::")[-1]
+        name = rename.get(name, name)
+        per.setdefault(name, []).append((int(r["Grid_Size"]), float(r["Counter_Value"])))
+    for k, vals in per.items():
+        g = max(v[0] for v in vals)
+        big = [v[1] for v in vals if v[0] == g]
+        d = res.setdefault(k, {"grid": g, "launches": len(big)})
+        d[counter.lower() + "_kb"] = sum(big) / len(big)
 
 
 if __name__ == "__main__":

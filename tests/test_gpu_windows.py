@@ -88,6 +88,13 @@ def test_segment_sum_matches_index_add(device, n, nkeys, L, use_slot):
     err = (out.double() - ref).abs()
     assert (err <= 1e-5 * mag + 1e-6).all(), (err / (mag + 1e-6)).max().item()
     assert torch.equal(out, nat.segment_sum(src, plan, nkeys, slot=slot, sub=S))  # fixed order
+    # accumulate: a second list added onto the first's sums, exactly the fp32 sum of the two
+    keys2 = torch.randint(0, nkeys, (n,), device=device, generator=g)
+    o2 = torch.sort(keys2, stable=True).indices
+    plan2 = SegmentPlan(keys2[o2], idx[o2], item_len=L)
+    out2 = nat.segment_sum(src, plan2, nkeys, slot=slot, sub=S)
+    both = nat.segment_sum(src, plan2, nkeys, slot=slot, sub=S, out=out.clone(), accumulate=True)
+    assert torch.equal(both, out + out2)
 
 
 def _loss(lp, ent, v):

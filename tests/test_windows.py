@@ -108,7 +108,7 @@ def test_window_towers_match_frame_convs(golden):
     c[:, 45] = 4
     c = np.concatenate([c, c[:5]])  # repeated observations share a frame id
     codes = torch.from_numpy(pack(c))
-    plan = WindowPlan(codes, FrameGroups(codes), item_len=16, hist_item_len=8)
+    plan = WindowPlan(codes, FrameGroups(codes), item_len=16, hist_item_len=8, dq_blocks=3)
     assert plan.num_frames == 12
     mb_idx = torch.tensor([0, 3, 12, 5, 7, 14, 9, 3])
     mb = plan.minibatch(mb_idx)
@@ -129,7 +129,8 @@ def test_window_towers_match_frame_convs(golden):
     g = torch.randn(2, mb.groups.numel(), 9, 64, dtype=torch.float64)
     (Y3 * g).sum().backward()
     dZ3 = torch.where(Y3 > 0, g, torch.zeros((), dtype=g.dtype)).reshape(2, -1, 64).detach()
-    dQ = emulate_segment_sum(plan.conv3, dZ3, plan.num_windows * 9, slot=mb.slot, sub=9)
+    assert len(plan.conv3_blocks) == 3
+    dQ = sum(emulate_segment_sum(part, dZ3, plan.num_windows * 9, slot=mb.slot, sub=9) for part in plan.conv3_blocks)
     torch.testing.assert_close(dQ.view_as(Q), Q.grad)
     dZ2w = torch.randn(2, plan.num_windows, 64, dtype=torch.float64)
     (T2[:, plan.rows.long()].sum(2) * dZ2w).sum().backward()
@@ -153,3 +154,10 @@ def test_epoch_minibatches_match_per_minibatch_grouping():
             ref = plan.minibatch(idxs[k * mbs:(k + 1) * mbs])
             assert torch.equal(m.groups, ref.groups) and torch.equal(m.inv, ref.inv)
             assert torch.equal(m.slot, ref.slot)
+            assert torch.equal(m.order, ref.order) and torch.equal(m.offs, ref.offs)
+            # CSR: frame u's samples are order[offs[u]:offs[u+1]], ascending, all with inv == u
+            o, f = m.order.long(), m.offs.long()
+            assert f[0] == 0 and f[-1] == o.numel() and bool((f[1:] > f[:-1]).all())
+            frame_of = torch.repeat_interleave(torch.arange(f.numel() - 1), f[1:] - f[:-1])
+            assert torch.equal(m.inv[o], frame_of)
+            assert bool((o[1:] > o[:-1])[frame_of[1:] == frame_of[:-1]].all())
