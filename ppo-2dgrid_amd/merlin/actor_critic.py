@@ -280,6 +280,50 @@ def _lut2_h1_index():
 _LUT2_H1 = _lut2_h1_index()
 
 
+def _lut2_gather_matrix():
+    """(G f32 [680, 80], part int64 [680]): the 680 tile combinations of the four parity types
+    in table order (row 4*v + j of T2), G[v][k] = how often P's flat entry k enters combination
+    v's conv1 sum (Pf[:, :, idx].sum(-1) == Pf @ G.T), part[v] = its parity type."""
+    G = torch.cat([torch.zeros(idx.shape[0], 80).scatter_add_(1, idx, torch.ones(idx.shape, dtype=torch.float32))
+                   for _, idx in _LUT2_H1])
+    part = torch.cat([torch.full((idx.shape[0],), p, dtype=torch.int64) for p, (_, idx) in enumerate(_LUT2_H1)])
+    return G, part
+
+
+class _Conv2Tables(torch.autograd.Function):
+    """T2 [2, 2720, 64] from P [2, 32, 80], b1 [2, 32], W2 [2, 64, 32, 4, 4] in a handful of
+    kernels, forward and backward written out (the autograd graph of the per-parity-type
+    formulation, CNNActorCritic._conv2_tables_autograd, ran ~25 forward and ~90 backward kernels
+    per optimizer step, four of them sort-based index_put backwards):
+      HT   = relu(G @ P[t]^T + b1[t])                 [2, 680, 32]  conv1 of every combination
+      X    = HT @ Wall[t]                             [2, 680, 1024] all four tap-parity blocks
+      T2   = X[:, v, part(v)]                         the block of each combination's own type
+    Wall[t][ci][(yp, xp, a, b, co)] = W2[t][co][ci][2a + yp][2b + xp]; X computes the three other
+    blocks too (89 MFLOP per call, negligible) so one bmm replaces eight."""
+
+    @staticmethod
+    def forward(ctx, P, b1, W2, G, part):
+        HT = torch.matmul(G, P.transpose(1, 2))
+        HT = torch.relu_(HT.add_(b1.unsqueeze(1)))
+        Wall = W2.reshape(2, 64, 32, 2, 2, 2, 2).permute(0, 2, 4, 6, 3, 5, 1).reshape(2, 32, 1024)
+        X = torch.bmm(HT, Wall).view(2, -1, 4, 256)
+        ar = torch.arange(part.numel(), device=part.device)
+        ctx.save_for_backward(HT, Wall, G, part, ar)
+        return X[:, ar, part].reshape(2, -1, 64)
+
+    @staticmethod
+    def backward(ctx, dT2):
+        HT, Wall, G, part, ar = ctx.saved_tensors
+        V = part.numel()
+        dX = dT2.new_zeros((2, V, 4, 256))
+        dX[:, ar, part] = dT2.reshape(2, V, 256)
+        dX = dX.view(2, V, 1024)
+        dWall = torch.bmm(HT.transpose(1, 2), dX)
+        dW2 = dWall.view(2, 32, 2, 2, 2, 2, 64).permute(0, 6, 1, 4, 2, 5, 3).reshape(2, 64, 32, 4, 4)
+        dH = torch.bmm(dX, Wall.transpose(1, 2)).mul_(HT > 0)
+        return torch.matmul(dH.transpose(1, 2), G), dH.sum(1), dW2, None, None
+
+
 class CNNActorCritic(nn.Module):
     def __init__(self, obs_shape, act_dim, hidden_dim=512):
         super().__init__()
@@ -290,6 +334,7 @@ class CNNActorCritic(nn.Module):
         self.critic = _head(self.critic_extractor.output_dim, hidden_dim, 1, 1.0)
         self._atlas = None  # f32 [5, 3, 8, 8] / 255 on the model's device (codes path only)
         self._lut2_idx = None
+        self._lut2_gather = None
         # "lut2": conv1+conv2 as table lookups, conv3/fc as hipBLASLt GEMMs (default)
         # "gemm": conv1 lookups, conv2/conv3/fc as GEMMs | "lut_nchw": conv1 lookups + MIOpen convs
         self.codes_impl = "lut2"
@@ -313,8 +358,19 @@ class CNNActorCritic(nn.Module):
 
     def conv2_tables(self):
         """T2[t][row][co] (t: actor, critic; 2720 rows, csrc/merlin_conv2lut.hip layout):
-        W2[:, :, ky, kx] applied to relu(conv1) of each tile combination, from P and b1 by
-        differentiable ops, so autograd maps dT2 to the conv1 and conv2 weight gradients."""
+        W2[:, :, ky, kx] applied to relu(conv1) of each tile combination (_Conv2Tables: autograd
+        maps dT2 to the conv1 and conv2 weight gradients)."""
+        P, b1 = self.conv1_tables()
+        if self._lut2_gather is None or self._lut2_gather[0].device != P.device or self._lut2_gather[0].dtype != P.dtype:
+            G, part = _lut2_gather_matrix()
+            self._lut2_gather = (G.to(device=P.device, dtype=P.dtype), part.to(P.device))
+        ea, ec = self.actor_extractor.network, self.critic_extractor.network
+        W2 = torch.stack([ea[2].weight, ec[2].weight])  # [2, co 64, ci 32, ky 4, kx 4]
+        return _Conv2Tables.apply(P.reshape(2, 32, 80), b1, W2, *self._lut2_gather)
+
+    def _conv2_tables_autograd(self):
+        """conv2_tables as plain differentiable torch ops, one bmm per parity type (the
+        definition _Conv2Tables is tested against)."""
         P, b1 = self.conv1_tables()
         Pf = P.reshape(2, 32, 80)
         if self._lut2_idx is None or self._lut2_idx[0][1].device != Pf.device:

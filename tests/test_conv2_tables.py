@@ -103,3 +103,22 @@ def test_histogram_gradient_equals_conv_gradients(golden):
     for a, b in zip(mine, ref):
         for u, v in zip(a, b):
             torch.testing.assert_close(u, v, rtol=1e-9, atol=1e-9)
+
+
+def test_conv2_tables_function_matches_autograd_definition(golden):
+    """_Conv2Tables (explicit forward/backward) == the per-parity-type autograd formulation:
+    the table and the conv1 / conv2 weight and bias gradients, float64."""
+    ac, _ = _model(5, golden, torch.float64)
+    g = torch.Generator().manual_seed(3)
+    dT = torch.randn(2, 2720, 64, dtype=torch.float64, generator=g)
+    grads = []
+    for fn in (ac.conv2_tables, ac._conv2_tables_autograd):
+        ac.zero_grad(set_to_none=True)
+        T = fn()
+        T.backward(dT)
+        grads.append([T.detach()] + [p.grad.clone() for p in (ac.actor_extractor.network[0].weight,
+                                                             ac.critic_extractor.network[0].bias,
+                                                             ac.actor_extractor.network[2].weight,
+                                                             ac.critic_extractor.network[2].weight)])
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-12, atol=1e-12)
