@@ -261,6 +261,19 @@ int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *id
                        float *out_dev, int64_t out_rows, float *carry_dev, int32_t accumulate,
                        void *stream);
 
+/* Acting tail (src/actor_critic.py:48-55 act, src/ppo.py:69-71): z float[2][n][hidden] = fc1's
+ * pre-activation of the actor / critic tower, b4 float[2][hidden]; h = relu(z + b4); logits =
+ * w_actor float[act_dim][hidden] . h0 + b_actor, value = w_critic float[hidden] . h1 + b_critic[0];
+ * action int64[n] = argmax(logits) when deterministic, else a Categorical(logits) draw (exponential
+ * races on a counter-based generator keyed by seed, *epoch_dev (NULL = 0; bump it to redraw in
+ * a replayed graph), step and the env index); logp float[n] = log_softmax(logits)[action],
+ * value float[n].  hidden % 4 == 0, act_dim <= 8. */
+int merlin_act_heads(const float *z_dev, const float *b4_dev, int64_t n, int32_t hidden,
+                     const float *w_actor_dev, const float *b_actor_dev, const float *w_critic_dev,
+                     const float *b_critic_dev, int32_t act_dim, int32_t deterministic, uint64_t seed,
+                     const int64_t *epoch_dev, int64_t step, int64_t *action_dev, float *logp_dev,
+                     float *value_dev, void *stream);
+
 /* PPO minibatch loss (src/ppo.py:136-150), per distinct frame u < n_frames of the minibatch:
  *   logits float[n_frames][act_dim] (act_dim <= 8), value float[n_frames]; the frame's samples
  *   are order[offs[u] .. offs[u+1]) (int32 CSR, offs[n_frames] = n_samples, every frame owns

@@ -589,6 +589,21 @@ int merlin_segment_sum(const float *src, int64_t src_rows, const int32_t *idx, c
     return MERLIN_OK;
 }
 
+int merlin_act_heads(const float *z, const float *b4, int64_t n, int32_t hidden, const float *w_actor,
+                     const float *b_actor, const float *w_critic, const float *b_critic, int32_t act_dim,
+                     int32_t deterministic, uint64_t seed, const int64_t *epoch, int64_t step, int64_t *action,
+                     float *logp, float *value, void *stream) {
+    if (n < 0) return fail(MERLIN_E_INVALID, "negative size");
+    if (act_dim < 1 || act_dim > 8) return fail(MERLIN_E_INVALID, "act_dim must be in [1, 8]");
+    if (hidden <= 0 || hidden % 4) return fail(MERLIN_E_INVALID, "hidden must be a positive multiple of 4");
+    if (n > 0 && (!z || !b4 || !w_actor || !b_actor || !w_critic || !b_critic || !action || !logp || !value))
+        return fail(MERLIN_E_INVALID, "null argument");
+    HIP_TRY(merlin::launch_act_heads(z, b4, n, hidden, w_actor, b_actor, w_critic, b_critic, act_dim,
+                                     deterministic ? 1 : 0, seed, epoch, step, action, logp, value,
+                                     (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
 int64_t merlin_ppo_loss_workspace(int64_t n_samples) { return merlin::ppo_loss_workspace_doubles(n_samples); }
 
 int merlin_ppo_loss(const float *logits, const float *value, const float *bias_actor, const float *bias_critic,

@@ -90,6 +90,7 @@ def lib():
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
+    L.merlin_act_heads.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, i32, i32, C.c_uint64, vp, i64, vp, vp, vp, vp]
     L.merlin_ppo_loss_workspace.argtypes = [i64]
     L.merlin_ppo_loss_workspace.restype = i64
     L.merlin_ppo_loss.argtypes = [vp, vp, vp, vp, i64, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp, C.c_double,
@@ -108,7 +109,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
     "merlin_segment_sum", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
-    "merlin_ppo_loss_workspace", "merlin_ppo_loss",
+    "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
 )
 
 
@@ -505,3 +506,29 @@ def ppo_loss(logits, value, offs, order, frame_of, sample_index, actions, logp_o
                                     float(ent_coef), ptr(dlogits), ptr(dvalue), ptr(dba), ptr(dbc), ptr(loss),
                                     ptr(stats), ptr(ws), stream_of(logits)), "merlin_ppo_loss")
     return loss, dlogits, dvalue, dba, dbc
+
+
+# -- acting tail (csrc/merlin_act.hip) -----------------------------------------------------------
+def act_heads(z, b4, w_actor, b_actor, w_critic, b_critic, deterministic=False, seed=0, epoch=None, step=0,
+              out=None):
+    """(action int64[n], logp f32[n], value f32[n]) from fc1's pre-activation z f32[2, n, H]:
+    relu(z + b4) -> heads -> log_softmax -> argmax or a Categorical draw keyed by (seed, epoch[0],
+    step, env).  out = (action, logp, value) tensors to write in place (the rollout storage)."""
+    T, n, H = (int(x) for x in z.shape)
+    A = int(w_actor.shape[0])
+    assert T == 2 and z.dtype == torch.float32 and b4.shape == (2, H) and w_actor.shape == (A, H)
+    assert w_critic.numel() == H and b_critic.numel() == 1 and b_actor.numel() == A
+    if epoch is not None:
+        assert epoch.dtype == torch.int64 and epoch.is_cuda
+    dev = z.device
+    if out is None:
+        out = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.float32, device=dev),
+               torch.empty(n, dtype=torch.float32, device=dev))
+    action, logp, value = out
+    assert action.dtype == torch.int64 and logp.dtype == value.dtype == torch.float32
+    assert action.numel() == logp.numel() == value.numel() == n
+    with KernelTimer.span("k_act_heads", z.numel() * 4 + n * 16):
+        check(lib().merlin_act_heads(ptr(z), ptr(b4), n, H, ptr(w_actor), ptr(b_actor), ptr(w_critic), ptr(b_critic), A,
+                                     int(bool(deterministic)), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(epoch), int(step),
+                                     ptr(action), ptr(logp), ptr(value), stream_of(z)), "merlin_act_heads")
+    return action, logp, value

@@ -450,20 +450,19 @@ class CNNActorCritic(nn.Module):
         }
 
     @torch.no_grad()
-    def act_codes_packed(self, codes, pack, deterministic=False):
-        """act_codes with the layouts of rollout_pack(): conv1+conv2 lookups, conv3 / fc1 as
-        plain bmm + the HIP bias/ReLU epilogue, the heads, the categorical sample."""
+    def act_codes_packed(self, codes, pack, deterministic=False, seed=0, epoch=None, step=0, out=None):
+        """act_codes with the layouts of rollout_pack(): conv1+conv2 lookups, conv3 as a plain bmm
+        + the HIP bias/ReLU epilogue, fc1 as a plain bmm, then fc1's bias/ReLU, the heads, the
+        log-probs and the categorical draw in one HIP pass (merlin_act_heads; draws keyed by
+        (seed, epoch[0], step, env)).  out = (action, logp, value) tensors to write in place."""
         from . import _native as nat
 
         n = codes.shape[0]
         A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
         a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
-        h = nat.bias_relu_(torch.bmm(a3, pack["W4t"]), pack["b4"])
-        logits = torch.addmm(self.actor[2].bias, h[0], self.actor[2].weight.t())
-        value = torch.addmm(self.critic[2].bias, h[1], self.critic[2].weight.t()).squeeze(-1)
-        logp_all, probs = _categorical(logits)
-        action = _sample_or_argmax(logits, logp_all, probs, deterministic)
-        return action, logp_all.gather(-1, action.unsqueeze(-1)).squeeze(-1), value
+        z = torch.bmm(a3, pack["W4t"])
+        return nat.act_heads(z, pack["b4"], self.actor[2].weight, self.actor[2].bias, self.critic[2].weight,
+                             self.critic[2].bias, deterministic, seed=seed, epoch=epoch, step=step, out=out)
 
     def act_codes(self, codes, deterministic=False, index=None):
         logits, value = self._forward_codes(codes, index)

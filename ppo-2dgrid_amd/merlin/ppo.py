@@ -93,6 +93,11 @@ class PPO:
         # after one eager rollout, replay the vectorised rollout as one captured HIP graph
         self.rollout_graph = rollout_graph
         self._graph = None
+        # acting draws: counter-based (merlin_act_heads), keyed by this seed (torch.manual_seed's,
+        # read without consuming the RNG), the rollout counter below (bumped inside the captured
+        # graph: every replay draws afresh), the step and the env
+        self._act_seed = int(torch.initial_seed())
+        self._act_epoch = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.episode_returns: list[float] = []
         self.episode_lengths: list[int] = []
 
@@ -160,15 +165,13 @@ class PPO:
         T = buf.T
         env.reset(out=buf.codes[0])
         with torch.no_grad():
+            self._act_epoch.add_(1)
             pack = self.ac.rollout_pack() if self.conv1_from_codes else None
             for t in range(T):
-                action, logp, value = self._act(buf.codes[t], pack)
-                buf.actions[t].copy_(action)
-                buf.logprobs[t].copy_(logp)
-                buf.values[t].copy_(value)
+                self._act(buf.codes[t], pack, t, out=(buf.actions[t], buf.logprobs[t], buf.values[t]))
                 env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
                               buf.ep_return[t], buf.ep_length[t])
-            _, _, last_value = self._act(buf.codes[T], pack)
+            _, _, last_value = self._act(buf.codes[T], pack, T)
             buf.last_value.copy_(last_value)
 
     def _capture_rollout(self):
@@ -188,11 +191,16 @@ class PPO:
             return
         self._graph = g
 
-    def _act(self, codes, pack):
+    def _act(self, codes, pack, step, out=None):
         if pack is not None:
-            return self.ac.act_codes_packed(codes, pack)
+            return self.ac.act_codes_packed(codes, pack, seed=self._act_seed, epoch=self._act_epoch, step=step,
+                                            out=out)
         nat.expand_obs(codes, out=self._obs_step, scale=INV255)
-        return self.ac.act(self._obs_step, prescaled=True)
+        res = self.ac.act(self._obs_step, prescaled=True)
+        if out is not None:
+            for dst, src in zip(out, res):
+                dst.copy_(src)
+        return res
 
     def _record_episodes(self):
         done = self.buf.dones > 0  # finished episodes in (step, env) order
