@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define MERLIN_ABI_VERSION 1
+#define MERLIN_ABI_VERSION 2
 
 #define MERLIN_OK 0
 #define MERLIN_E_INVALID 1     /* bad argument / config */
@@ -112,6 +112,13 @@ typedef struct {
                                   env.reset(seed=task_seed) on every episode as FOMAML's
                                   collect_trajectory does (src/fomaml.py:63,92) */
 } merlin_env_config;
+
+/* [host] Layout check for bindings that restate merlin_env_config (ctypes, cgo, ...): returns
+ * sizeof(merlin_env_config) and writes the byte offset of its first min(n_fields,
+ * MERLIN_ENV_CONFIG_FIELDS) fields, in declaration order, to offsets_host (nullable).
+ * merlin_env_create reads all MERLIN_ENV_CONFIG_FIELDS fields: a binding must match. */
+#define MERLIN_ENV_CONFIG_FIELDS 10
+int64_t merlin_env_config_layout(int64_t *offsets_host, int32_t n_fields);
 
 /* Library */
 int merlin_version(void);
@@ -266,12 +273,16 @@ int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *id
  * w_actor float[act_dim][hidden] . h0 + b_actor, value = w_critic float[hidden] . h1 + b_critic[0];
  * action int64[n] = argmax(logits) when deterministic, else a Categorical(logits) draw (exponential
  * races on a counter-based generator keyed by seed, *epoch_dev (NULL = 0; bump it to redraw in
- * a replayed graph), step and the env index); logp float[n] = log_softmax(logits)[action],
- * value float[n].  hidden % 4 == 0, act_dim <= 8. */
+ * a replayed graph), step and the global env index env_offset + k, so data-parallel shards draw
+ * what one process over the concatenated envs draws); logp float[n] = log_softmax(logits)[action],
+ * value float[n].  hidden % 4 == 0, act_dim <= 8.  Non-finite logits (where the reference's
+ * Categorical(logits) raises) give action -1, which merlin_env_step flags as
+ * MERLIN_DEVERR_BAD_ACTION. */
 int merlin_act_heads(const float *z_dev, const float *b4_dev, int64_t n, int32_t hidden,
                      const float *w_actor_dev, const float *b_actor_dev, const float *w_critic_dev,
                      const float *b_critic_dev, int32_t act_dim, int32_t deterministic, uint64_t seed,
-                     const int64_t *epoch_dev, int64_t step, int64_t *action_dev, float *logp_dev,
+                     const int64_t *epoch_dev, int64_t step, int64_t env_offset, int64_t *action_dev,
+                     float *logp_dev,
                      float *value_dev, void *stream);
 
 /* PPO minibatch loss (src/ppo.py:136-150), per distinct frame u < n_frames of the minibatch:

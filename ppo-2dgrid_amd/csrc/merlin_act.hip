@@ -8,9 +8,11 @@
 // Lane 0 forms logp = logits - logsumexp(logits) and draws the action by exponential races,
 // argmax_j p_j / E_j with E_j ~ Exp(1) (the law of Categorical(logits).sample(); torch's
 // multinomial uses the same race), from a counter-based generator keyed by (seed, *epoch,
-// step, env, j): no RNG state, so the rollout replays as a HIP graph with a fresh draw per
+// step, global env index = env_offset + env, j: a data-parallel shard draws what one process
+// over the concatenated envs would): no RNG state, so the rollout replays as a HIP graph with a fresh draw per
 // replay once the caller bumps *epoch.  deterministic = argmax of the logits (first maximum,
-// as torch.argmax).  Writes action int64, logp[action] and value straight into the rollout
+// as torch.argmax).  Non-finite logits give action -1 (see below).  Writes action int64,
+// logp[action] and value straight into the rollout
 // storage: the 2 head GEMMs + ~17 small torch kernels + 3 copies of the per-step tail become one
 // launch.
 #include <algorithm>
@@ -50,7 +52,8 @@ __global__ __launch_bounds__(64 * ACT_WAVES) void k_act_heads(const float4 *__re
                                                               const float4 *__restrict__ wc,
                                                               const float *__restrict__ bc, int A, int det,
                                                               uint64_t seed, const int64_t *__restrict__ epoch,
-                                                              int64_t step, int64_t *__restrict__ action,
+                                                              int64_t step, int64_t env_offset,
+                                                              int64_t *__restrict__ action,
                                                               float *__restrict__ logp, float *__restrict__ value) {
     const int lane = threadIdx.x & 63;
     const uint64_t ep = epoch ? (uint64_t)epoch[0] : 0ull;
@@ -104,7 +107,7 @@ __global__ __launch_bounds__(64 * ACT_WAVES) void k_act_heads(const float4 *__re
                     if (j < A) {
                         // log(p_j / E_j) = logp_j - log(-log u)
                         const double sc = (double)(zl[j] - lse) - log(-log(uniform01(seed, ep, (uint64_t)step,
-                                                                                    (uint64_t)k, j)));
+                                                                                    (uint64_t)(env_offset + k), j)));
                         if (sc > best) {
                             best = sc;
                             a = j;
@@ -116,6 +119,10 @@ __global__ __launch_bounds__(64 * ACT_WAVES) void k_act_heads(const float4 *__re
 #pragma unroll
             for (int j = 1; j < MAXA; j++)
                 if (j == a) la = zl[j] - lse;
+            // non-finite logits (a diverged update): Categorical(logits) raises in the reference;
+            // here the action is the sentinel -1, which the next env step rejects
+            // (MERLIN_DEVERR_BAD_ACTION, read once per rollout by merlin_env_errors)
+            if (!isfinite(lse)) a = -1;
             action[k] = a;
             logp[k] = la;
             value[k] = acc[MAXA] + bc[0];
@@ -127,12 +134,14 @@ __global__ __launch_bounds__(64 * ACT_WAVES) void k_act_heads(const float4 *__re
 
 hipError_t launch_act_heads(const float *z, const float *b4, int64_t n, int H, const float *wa, const float *ba,
                             const float *wc, const float *bc, int A, int det, uint64_t seed, const int64_t *epoch,
-                            int64_t step, int64_t *action, float *logp, float *value, hipStream_t s) {
+                            int64_t step, int64_t env_offset, int64_t *action, float *logp, float *value,
+                            hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((n + ACT_WAVES - 1) / ACT_WAVES, 256 * 8);
     hipLaunchKernelGGL(k_act_heads, dim3(grid), dim3(64 * ACT_WAVES), 0, s, reinterpret_cast<const float4 *>(z),
                        reinterpret_cast<const float4 *>(b4), n, H / 4, reinterpret_cast<const float4 *>(wa), ba,
-                       reinterpret_cast<const float4 *>(wc), bc, A, det, seed, epoch, step, action, logp, value);
+                       reinterpret_cast<const float4 *>(wc), bc, A, det, seed, epoch, step, env_offset, action, logp,
+                       value);
     return hipGetLastError();
 }
 

@@ -242,6 +242,18 @@ int merlin_tile_atlas(uint8_t *out_host) {
     return MERLIN_OK;
 }
 
+int64_t merlin_env_config_layout(int64_t *offsets_host, int32_t n_fields) {
+    const int64_t off[MERLIN_ENV_CONFIG_FIELDS] = {
+        (int64_t)offsetof(merlin_env_config, num_envs),     (int64_t)offsetof(merlin_env_config, size),
+        (int64_t)offsetof(merlin_env_config, difficulty),   (int64_t)offsetof(merlin_env_config, max_steps),
+        (int64_t)offsetof(merlin_env_config, stuck_penalty), (int64_t)offsetof(merlin_env_config, max_stay),
+        (int64_t)offsetof(merlin_env_config, penalty),      (int64_t)offsetof(merlin_env_config, exploration_bonus),
+        (int64_t)offsetof(merlin_env_config, bonus),        (int64_t)offsetof(merlin_env_config, reseed_each_reset)};
+    if (offsets_host)
+        for (int i = 0; i < n_fields && i < MERLIN_ENV_CONFIG_FIELDS; i++) offsets_host[i] = off[i];
+    return (int64_t)sizeof(merlin_env_config);
+}
+
 int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
     if (!cfg || !out) return fail(MERLIN_E_INVALID, "null argument");
     *out = nullptr;
@@ -591,15 +603,15 @@ int merlin_segment_sum(const float *src, int64_t src_rows, const int32_t *idx, c
 
 int merlin_act_heads(const float *z, const float *b4, int64_t n, int32_t hidden, const float *w_actor,
                      const float *b_actor, const float *w_critic, const float *b_critic, int32_t act_dim,
-                     int32_t deterministic, uint64_t seed, const int64_t *epoch, int64_t step, int64_t *action,
-                     float *logp, float *value, void *stream) {
+                     int32_t deterministic, uint64_t seed, const int64_t *epoch, int64_t step, int64_t env_offset,
+                     int64_t *action, float *logp, float *value, void *stream) {
     if (n < 0) return fail(MERLIN_E_INVALID, "negative size");
     if (act_dim < 1 || act_dim > 8) return fail(MERLIN_E_INVALID, "act_dim must be in [1, 8]");
     if (hidden <= 0 || hidden % 4) return fail(MERLIN_E_INVALID, "hidden must be a positive multiple of 4");
     if (n > 0 && (!z || !b4 || !w_actor || !b_actor || !w_critic || !b_critic || !action || !logp || !value))
         return fail(MERLIN_E_INVALID, "null argument");
     HIP_TRY(merlin::launch_act_heads(z, b4, n, hidden, w_actor, b_actor, w_critic, b_critic, act_dim,
-                                     deterministic ? 1 : 0, seed, epoch, step, action, logp, value,
+                                     deterministic ? 1 : 0, seed, epoch, step, env_offset, action, logp, value,
                                      (hipStream_t)stream));
     return MERLIN_OK;
 }

@@ -63,6 +63,8 @@ def lib():
     L.merlin_version.restype = C.c_int
     L.merlin_last_error.restype = C.c_char_p
     L.merlin_tile_atlas.argtypes = [vp]
+    L.merlin_env_config_layout.argtypes = [C.POINTER(C.c_int64), i32]
+    L.merlin_env_config_layout.restype = i64
     L.merlin_env_create.argtypes = [C.POINTER(EnvConfig), C.POINTER(vp)]
     L.merlin_env_destroy.argtypes = [vp]
     L.merlin_env_seed.argtypes = [vp, u64p, i32, vp]
@@ -90,17 +92,38 @@ def lib():
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
-    L.merlin_act_heads.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, i32, i32, C.c_uint64, vp, i64, vp, vp, vp, vp]
+    L.merlin_act_heads.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp,
+                                   vp]
     L.merlin_ppo_loss_workspace.argtypes = [i64]
     L.merlin_ppo_loss_workspace.restype = i64
     L.merlin_ppo_loss.argtypes = [vp, vp, vp, vp, i64, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp, C.c_double,
                                   C.c_double, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]
+    check_env_config_layout(L)
     _lib = L
     return L
 
 
+def env_config_layout(L=None):
+    """(sizeof, field offsets) of the C merlin_env_config, from the library itself."""
+    L = L or lib()
+    nf = len(EnvConfig._fields_)
+    offs = (C.c_int64 * nf)()
+    size = int(L.merlin_env_config_layout(offs, nf))
+    return size, [int(o) for o in offs]
+
+
+def check_env_config_layout(L) -> None:
+    """The ctypes EnvConfig must be byte-identical to include/merlin_hip.h's merlin_env_config:
+    merlin_env_create reads every field, so a shorter binding would be read past its end."""
+    size, offs = env_config_layout(L)
+    mine = [getattr(EnvConfig, f).offset for f, _ in EnvConfig._fields_]
+    if size != C.sizeof(EnvConfig) or offs != mine:
+        raise MerlinNativeError(f"EnvConfig layout mismatch: C sizeof {size} offsets {offs}, "
+                                f"ctypes sizeof {C.sizeof(EnvConfig)} offsets {mine}")
+
+
 EXPORTED_SYMBOLS = (
-    "merlin_version", "merlin_last_error", "merlin_tile_atlas", "merlin_env_create",
+    "merlin_version", "merlin_last_error", "merlin_tile_atlas", "merlin_env_config_layout", "merlin_env_create",
     "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step",
     "merlin_env_get_state", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
     "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
@@ -510,14 +533,20 @@ def ppo_loss(logits, value, offs, order, frame_of, sample_index, actions, logp_o
 
 # -- acting tail (csrc/merlin_act.hip) -----------------------------------------------------------
 def act_heads(z, b4, w_actor, b_actor, w_critic, b_critic, deterministic=False, seed=0, epoch=None, step=0,
-              out=None):
+              out=None, env_offset=0):
     """(action int64[n], logp f32[n], value f32[n]) from fc1's pre-activation z f32[2, n, H]:
     relu(z + b4) -> heads -> log_softmax -> argmax or a Categorical draw keyed by (seed, epoch[0],
-    step, env).  out = (action, logp, value) tensors to write in place (the rollout storage)."""
+    step, env_offset + env): the global env index, so data-parallel shards draw like one process.  out = (action, logp, value) tensors to write in place (the rollout storage).
+    A draw (deterministic=False) needs the epoch counter: the key has no hidden state, so the
+    caller advances it (merlin.PPO bumps it once per rollout) or every call repeats its draws.
+    Non-finite logits give action -1 (the env step then raises MERLIN_DEVERR_BAD_ACTION)."""
     T, n, H = (int(x) for x in z.shape)
     A = int(w_actor.shape[0])
     assert T == 2 and z.dtype == torch.float32 and b4.shape == (2, H) and w_actor.shape == (A, H)
     assert w_critic.numel() == H and b_critic.numel() == 1 and b_actor.numel() == A
+    if not deterministic and epoch is None:
+        raise ValueError("act_heads: a sampled action needs an epoch counter tensor (int64[1] on the device) "
+                         "that the caller advances between rollouts; without it every call repeats its draws")
     if epoch is not None:
         assert epoch.dtype == torch.int64 and epoch.is_cuda
     dev = z.device
@@ -530,5 +559,6 @@ def act_heads(z, b4, w_actor, b_actor, w_critic, b_critic, deterministic=False, 
     with KernelTimer.span("k_act_heads", z.numel() * 4 + n * 16):
         check(lib().merlin_act_heads(ptr(z), ptr(b4), n, H, ptr(w_actor), ptr(b_actor), ptr(w_critic), ptr(b_critic), A,
                                      int(bool(deterministic)), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(epoch), int(step),
+                                     int(env_offset),
                                      ptr(action), ptr(logp), ptr(value), stream_of(z)), "merlin_act_heads")
     return action, logp, value

@@ -450,11 +450,11 @@ class CNNActorCritic(nn.Module):
         }
 
     @torch.no_grad()
-    def act_codes_packed(self, codes, pack, deterministic=False, seed=0, epoch=None, step=0, out=None):
+    def act_codes_packed(self, codes, pack, deterministic=False, seed=0, epoch=None, step=0, out=None, env_offset=0):
         """act_codes with the layouts of rollout_pack(): conv1+conv2 lookups, conv3 as a plain bmm
         + the HIP bias/ReLU epilogue, fc1 as a plain bmm, then fc1's bias/ReLU, the heads, the
         log-probs and the categorical draw in one HIP pass (merlin_act_heads; draws keyed by
-        (seed, epoch[0], step, env)).  out = (action, logp, value) tensors to write in place."""
+        (seed, epoch[0], step, env_offset + env)).  out = (action, logp, value) tensors to write in place."""
         from . import _native as nat
 
         n = codes.shape[0]
@@ -462,7 +462,8 @@ class CNNActorCritic(nn.Module):
         a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
         z = torch.bmm(a3, pack["W4t"])
         return nat.act_heads(z, pack["b4"], self.actor[2].weight, self.actor[2].bias, self.critic[2].weight,
-                             self.critic[2].bias, deterministic, seed=seed, epoch=epoch, step=step, out=out)
+                             self.critic[2].bias, deterministic, seed=seed, epoch=epoch, step=step, out=out,
+                             env_offset=env_offset)
 
     def act_codes(self, codes, deterministic=False, index=None):
         logits, value = self._forward_codes(codes, index)

@@ -213,7 +213,8 @@ class MerlinVecEnv:
         if raise_on_error and flags.value:
             what = []
             if flags.value & nat.DEVERR_BAD_ACTION:
-                what.append("action outside {0,1,2} (ThreeActionWrapper IndexError)")
+                what.append("action outside {0,1,2} (ThreeActionWrapper IndexError; -1 = the policy's "
+                            "logits were non-finite, merlin_act_heads)")
             if flags.value & nat.DEVERR_PLACE_OBJ:
                 what.append("place_obj rejection sampling failed (RecursionError)")
             raise nat.MerlinNativeError("device env error: " + "; ".join(what))

@@ -95,7 +95,9 @@ class PPO:
         self._graph = None
         # acting draws: counter-based (merlin_act_heads), keyed by this seed (torch.manual_seed's,
         # read without consuming the RNG), the rollout counter below (bumped inside the captured
-        # graph: every replay draws afresh), the step and the env
+        # graph: every replay draws afresh), the step and the GLOBAL env index (env_offset + i):
+        # ranks of a data-parallel run draw independently, exactly as one process over the
+        # concatenated envs would
         self._act_seed = int(torch.initial_seed())
         self._act_epoch = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.episode_returns: list[float] = []
@@ -176,9 +178,11 @@ class PPO:
 
     def _capture_rollout(self):
         """Record _rollout_body as one HIP graph (torch.cuda.graph; the env and lookup kernels
-        launch on the capturing stream through the C ABI, the sampler's RNG offsets advance per
-        replay).  Storage, env state and weights are read in place, so every replay is a fresh
-        rollout with the current weights, launched as one graph instead of ~10k kernels."""
+        launch on the capturing stream through the C ABI).  The action draws are counter-based
+        (merlin_act_heads): the graph bumps the rollout counter _act_epoch on the device at the
+        start of every replay, so each replay draws afresh.  Storage, env state and weights are
+        read in place, so every replay is a fresh rollout with the current weights, launched as
+        one graph instead of ~10k kernels."""
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         try:
@@ -194,7 +198,7 @@ class PPO:
     def _act(self, codes, pack, step, out=None):
         if pack is not None:
             return self.ac.act_codes_packed(codes, pack, seed=self._act_seed, epoch=self._act_epoch, step=step,
-                                            out=out)
+                                            out=out, env_offset=self.vec.env_offset)
         nat.expand_obs(codes, out=self._obs_step, scale=INV255)
         res = self.ac.act(self._obs_step, prescaled=True)
         if out is not None:

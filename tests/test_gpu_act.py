@@ -78,3 +78,47 @@ def test_act_heads_writes_into_storage(device):
     torch.cuda.synchronize()
     assert bool((act[0] == -1).all()) and bool((lp[0] == 9.0).all()) and bool((val[0] == 9.0).all())
     assert bool(((act[1] >= 0) & (act[1] < A)).all()) and bool((lp[1] <= 0).all())
+
+
+def test_act_heads_non_finite_logits_give_sentinel_and_env_rejects_it(device):
+    """A diverged policy (NaN / inf logits) must not silently act: the reference's
+    Categorical(logits) raises; merlin_act_heads writes action -1 and the next env step raises
+    MERLIN_DEVERR_BAD_ACTION through MerlinVecEnv.errors()."""
+    from merlin import MerlinVecEnv
+    from merlin import _native as nat
+
+    n, H, A = 64, 64, 3
+    z, b4, wa, ba, wc, bc = _inputs(device, n, H, A, 13)
+    z[0, 5, 3] = float("nan")
+    z[0, 9, :] = float("inf")
+    epoch = torch.zeros(1, dtype=torch.int64, device=device)
+    for det in (True, False):
+        action, _, _ = nat.act_heads(z, b4, wa, ba, wc, bc, deterministic=det, seed=1, epoch=epoch)
+        assert int(action[5]) == -1 and int(action[9]) == -1
+        ok = torch.ones(n, dtype=torch.bool, device=device)
+        ok[5] = ok[9] = False
+        assert bool(((action[ok] >= 0) & (action[ok] < A)).all())
+    env = MerlinVecEnv(n, "mediumhard", seed=3, device=device)
+    env.reset()
+    env.step(action)
+    with pytest.raises(nat.MerlinNativeError, match="non-finite"):
+        env.errors()
+
+
+def test_act_heads_keys_on_the_global_env_index(device):
+    """data-parallel ranks (same torch seed on every rank, ppo_train.py set_seed) must not
+    share sampling noise.  The draw is keyed by env_offset + env: rank r (env_offset r*n) draws
+    differently from rank 0 for identical logits, and exactly what one process over the 2n
+    concatenated envs draws for those envs."""
+    from merlin import _native as nat
+
+    n, H, A = 4096, 64, 3
+    z, b4, wa, ba, wc, bc = _inputs(device, n, H, A, 17)
+    z = z[:, :1].expand(2, n, H).contiguous()  # identical logits for every env
+    epoch = torch.full((1,), 3, dtype=torch.int64, device=device)
+    r0, _, _ = nat.act_heads(z, b4, wa, ba, wc, bc, seed=9, epoch=epoch, step=2, env_offset=0)
+    r1, _, _ = nat.act_heads(z, b4, wa, ba, wc, bc, seed=9, epoch=epoch, step=2, env_offset=n)
+    assert (r0 != r1).float().mean() > 0.2
+    zz = torch.cat([z, z], 1)
+    both, _, _ = nat.act_heads(zz, b4, wa, ba, wc, bc, seed=9, epoch=epoch, step=2)
+    assert torch.equal(both[:n], r0) and torch.equal(both[n:], r1)

@@ -59,46 +59,3 @@ def test_graph_rollout_matches_eager_env(device):
     assert not torch.equal(seen[1], seen[2])
     mirror.errors()
 
-
-def test_act_heads_matches_torch_and_samples_the_policy(device):
-    """merlin_act_heads: relu(z + b4) -> heads -> log_softmax == torch; deterministic = argmax;
-    the draws follow softmax(logits) (per-env empirical frequencies over many keys) and change
-    with the epoch counter."""
-    from merlin import _native as nat
-
-    g = torch.Generator(device=device)
-    g.manual_seed(5)
-    n, H, A = 3000, 512, 3
-    z = torch.randn(2, n, H, device=device, generator=g)
-    b4 = torch.randn(2, H, device=device, generator=g) * 0.1
-    wa = torch.randn(A, H, device=device, generator=g) * 0.05
-    ba = torch.randn(A, device=device, generator=g)
-    wc = torch.randn(1, H, device=device, generator=g) * 0.05
-    bc = torch.randn(1, device=device, generator=g)
-    h = torch.relu(z + b4[:, None])
-    logits = h[0] @ wa.t() + ba
-    logp_all = torch.log_softmax(logits, -1)
-    value = (h[1] @ wc.t()).squeeze(-1) + bc
-    a, lp, v = nat.act_heads(z, b4, wa, ba, wc, bc, deterministic=True)
-    assert torch.equal(a, logits.argmax(-1))
-    torch.testing.assert_close(lp, logp_all.gather(-1, a[:, None]).squeeze(-1), rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(v, value, rtol=1e-5, atol=1e-5)
-    # sampling: same frame for every env -> frequencies over 3000 envs x 20 steps ~ softmax
-    zz = z[:, :1].expand(2, n, H).contiguous()
-    p = torch.softmax(h[0, :1] @ wa.t() + ba, -1)[0]
-    epoch = torch.zeros(1, dtype=torch.int64, device=device)
-    counts = torch.zeros(A, device=device)
-    first = None
-    for step in range(20):
-        a, lp, _ = nat.act_heads(zz, b4, wa, ba, wc, bc, seed=123, epoch=epoch, step=step)
-        counts += torch.bincount(a, minlength=A).float()
-        torch.testing.assert_close(lp, torch.log(p)[a], rtol=1e-5, atol=1e-5)
-        if first is None:
-            first = a.clone()
-    freq = counts / counts.sum()
-    assert (freq - p).abs().max() < 0.01, (freq, p)  # 60k draws: sd < 0.002
-    a0, _, _ = nat.act_heads(zz, b4, wa, ba, wc, bc, seed=123, epoch=epoch, step=0)
-    assert torch.equal(a0, first)  # same key, same draw
-    epoch += 1
-    a1, _, _ = nat.act_heads(zz, b4, wa, ba, wc, bc, seed=123, epoch=epoch, step=0)
-    assert not torch.equal(a1, first)

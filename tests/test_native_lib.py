@@ -5,6 +5,7 @@ import re
 import subprocess
 
 import numpy as np
+import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "merlin_hip.h")
@@ -42,7 +43,7 @@ def test_library_has_gfx950_code_object():
 def test_version_and_atlas(golden):
     from merlin import _native as nat
 
-    assert nat.lib().merlin_version() == 1
+    assert nat.lib().merlin_version() == 2
     # the library's own C++ restatement of render_tile == the numpy restatement golden
     assert (nat.tile_atlas() == golden("atlas")["atlas"]).all()
 
@@ -59,3 +60,36 @@ def test_errors_are_reported_not_thrown():
     assert rc == 1 and b"num_envs" in L.merlin_last_error()
     cfg = nat.EnvConfig(4, 40, 2, 0, 0, 3, -0.1, 0, 0.0)
     assert L.merlin_env_create(C.byref(cfg), C.byref(h)) == 4  # size > 32 unsupported
+
+
+def test_act_heads_draw_requires_epoch_counter():
+    """a sampled action without the epoch counter would repeat its draws every call."""
+    import torch
+
+    from merlin import _native as nat
+
+    z = torch.zeros(2, 4, 8)
+    b4 = torch.zeros(2, 8)
+    wa, ba, wc, bc = torch.zeros(3, 8), torch.zeros(3), torch.zeros(1, 8), torch.zeros(1)
+    with pytest.raises(ValueError, match="epoch"):
+        nat.act_heads(z, b4, wa, ba, wc, bc, deterministic=False)
+
+
+def test_env_config_binding_matches_the_c_struct():
+    """VERDICT r1 boundary defect: the ctypes restatement of merlin_env_config (the one
+    INTEGRATION.md tells a reference maintainer to paste) must have the C struct's size and field
+    offsets; merlin_env_create reads every field."""
+    import ctypes as C
+
+    from merlin import _native as nat
+
+    size, offs = nat.env_config_layout()
+    assert size == C.sizeof(nat.EnvConfig)
+    assert offs == [getattr(nat.EnvConfig, f).offset for f, _ in nat.EnvConfig._fields_]
+    hdr = open(HEADER).read()
+    assert int(re.search(r"#define MERLIN_ENV_CONFIG_FIELDS (\d+)", hdr).group(1)) == len(nat.EnvConfig._fields_)
+    # the binding printed in INTEGRATION.md declares the same fields in the same order
+    doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = doc[doc.index("class MerlinEnvConfig"):]
+    block = block[:block.index("]")]
+    assert re.findall(r'\("(\w+)"', block) == [f for f, _ in nat.EnvConfig._fields_]
