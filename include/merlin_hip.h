@@ -257,18 +257,6 @@ int merlin_tower_conv2_lut_bwd(const uint32_t *codes_dev, int64_t n, const float
  *               item_len)][2][64] scratch.  out float[towers][out_rows][64] is overwritten
  *               (rows without entries = 0), or with accumulate != 0 the sums are added to it
  *               (a list split by source block into several calls sums in call order). */
-/* dq_hot: the hot-window rows of the same dQ, each dZ3 row read once: dQ[t][hot_windows[s]*9 + tap]
- *               = sum of dZ3_dev[t][u*9 + p3] over the frames u < n_frames and p3 with
- *               hot_slots[u*32 + p2(p3, tap)] == s (hot_slots int16[n_frames][32]: the hot slot
- *               0..n_hot-1 of the frame's window at conv2 position p2 < 25, or -1; n_hot <= 192).
- *               Only those n_hot*9 rows of dQ_dev float[towers][out_rows][64] are written (the
- *               rest, e.g. the cold windows' rows from merlin_segment_sum, are left as they are).
- *               Sums in LDS, one writer per accumulator, partials added in a fixed order:
- *               reproducible.  workspace float[merlin_tower_window_dq_hot_workspace(...)]. */
-int64_t merlin_tower_window_dq_hot_workspace(int64_t n_frames, int32_t towers, int32_t n_hot);
-int merlin_tower_window_dq_hot(const float *dZ3_dev, int64_t n_frames, const int16_t *hot_slots_dev,
-                               const int32_t *hot_windows_dev, int32_t n_hot, int32_t towers,
-                               float *workspace_dev, float *dQ_dev, int64_t out_rows, void *stream);
 int merlin_tower_window_lut(const int32_t *rows_dev, int64_t n_windows, const float *tables_dev,
                             int32_t towers, float *Z2w_dev, void *stream);
 int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,

@@ -601,24 +601,6 @@ int merlin_segment_sum(const float *src, int64_t src_rows, const int32_t *idx, c
     return MERLIN_OK;
 }
 
-int64_t merlin_tower_window_dq_hot_workspace(int64_t n_frames, int32_t towers, int32_t n_hot) {
-    if (n_frames <= 0 || n_hot <= 0) return 0;
-    return (int64_t)merlin::dq_hot_part_floats(n_frames, towers, n_hot);
-}
-
-int merlin_tower_window_dq_hot(const float *dZ3, int64_t n_frames, const int16_t *hot_slots, const int32_t *hot_windows,
-                               int32_t n_hot, int32_t towers, float *workspace, float *dQ, int64_t out_rows,
-                               void *stream) {
-    if (n_frames < 0 || n_hot < 0) return fail(MERLIN_E_INVALID, "negative size");
-    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    if (n_hot > merlin::dq_hot_max()) return fail(MERLIN_E_INVALID, "n_hot exceeds the LDS accumulator capacity");
-    if (n_frames > 0 && n_hot > 0 && (!dZ3 || !hot_slots || !hot_windows || !workspace || !dQ))
-        return fail(MERLIN_E_INVALID, "null argument");
-    HIP_TRY(merlin::launch_dq_hot(dZ3, n_frames, hot_slots, hot_windows, n_hot, towers, workspace, dQ, out_rows,
-                                  (hipStream_t)stream));
-    return MERLIN_OK;
-}
-
 int merlin_act_heads(const float *z, const float *b4, int64_t n, int32_t hidden, const float *w_actor,
                      const float *b_actor, const float *w_critic, const float *b_critic, int32_t act_dim,
                      int32_t deterministic, uint64_t seed, const int64_t *epoch, int64_t step, int64_t env_offset,

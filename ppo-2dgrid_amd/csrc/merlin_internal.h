@@ -90,11 +90,6 @@ hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *d
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
                                const float *b3, int T, float *Y3, hipStream_t s);
-int dq_hot_chunks(int64_t U, int T);
-size_t dq_hot_part_floats(int64_t U, int T, int nhot);
-int dq_hot_max();
-hipError_t launch_dq_hot(const float *dZ3, int64_t U, const int16_t *hs, const int32_t *hot_w, int nhot, int T,
-                         float *part, float *out, int64_t out_rows, hipStream_t s);
 hipError_t launch_act_heads(const float *z, const float *b4, int64_t n, int H, const float *wa, const float *ba,
                             const float *wc, const float *bc, int A, int det, uint64_t seed, const int64_t *epoch,
                             int64_t step, int64_t env_offset, int64_t *action, float *logp, float *value,

@@ -206,149 +206,7 @@ __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carr
     }
 }
 
-// ---- dQ of the hot windows: scatter into LDS accumulators ------------------------------------
-// The dQ gather above reads each 256-B dZ3 row once per tap (9x), from a table far larger than L2;
-// the windows are very skewed (a bench rollout: the 192 most-entered of ~6k windows take ~85 % of
-// the entries), so their dQ rows are accumulated in LDS instead, each dZ3 row read once:
-//   workgroup = (tower t, channel slice c of DQH_SC channels, chunk of frames), one wave per tap;
-//   the workgroup stages DQH_STEP dZ3 rows (its slice) and their frames' hot slots in LDS, and wave
-//   `tap` adds row (u, p3) into acc[tap][hot slot of window wid(u, p3 + tap)] when that window is
-//   hot.  Each accumulator has one writer wave, which adds in row order: the partial sums are
-//   reproducible.  Partials per chunk go to `part` and k_dq_hot_reduce sums them in chunk order
-//   into the hot windows' dQ rows.  Blocks are numbered so that the DQH_NS slice workgroups of one
-//   (tower, chunk) share an XCD (block b runs on XCD b % 8): each dZ3 row is fetched into that
-//   XCD's L2 once and read by the slices from there.
-constexpr int DQH_SC = 16;                // channels per workgroup
-constexpr int DQH_NS = 64 / DQH_SC;       // slices
-constexpr int DQH_C4 = DQH_SC / 4;        // float4 per row slice
-constexpr int DQH_STEP = 64;              // dZ3 rows per staged step
-constexpr int DQH_FR = 8;                 // frames a step can touch (64 rows of 9)
-constexpr int DQH_HSW = 32;               // int16 hot slots per frame row (25 used)
-constexpr int DQH_THREADS = 9 * 64;
-constexpr int DQH_MAXHOT = 192;
-
-__global__ __launch_bounds__(DQH_THREADS) void k_dq_hot(const float4 *__restrict__ dZ3, int64_t U,
-                                                      const int16_t *__restrict__ hs, int nhot, int chunks, int T,
-                                                      float4 *__restrict__ part) {
-    __shared__ float4 acc[9 * DQH_MAXHOT * DQH_C4];
-    __shared__ float4 stg[2][DQH_STEP * DQH_C4];
-    __shared__ int16_t hsl[2][DQH_FR * DQH_HSW];
-    const int b = blockIdx.x;
-    const int slice = (b >> 3) % DQH_NS;
-    const int r = (b / (8 * DQH_NS)) * 8 + (b & 7);
-    if (r >= T * chunks) return;  // grid padding: whole workgroup, before any barrier
-    const int t = r % T, chunk = r / T;
-    const int tid = threadIdx.x, lane = tid & 63, tap = tid >> 6;
-    for (int i = tid; i < 9 * nhot * DQH_C4; i += DQH_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int64_t u0 = U * chunk / chunks, u1 = U * (chunk + 1) / chunks;
-    const int64_t r0 = u0 * 9, r1 = u1 * 9;
-    const int nsteps = (int)((r1 - r0 + DQH_STEP - 1) / DQH_STEP);
-    const float4 *src = dZ3 + (size_t)t * U * 9 * 16 + slice * DQH_C4;
-    // staging roles: threads [0, 256) one float4 of the rows, [256, 288) 16 B of hot slots
-    float4 vreg = make_float4(0.f, 0.f, 0.f, 0.f);
-    int4 hreg = make_int4(-1, -1, -1, -1);
-    auto gload = [&](int k) {
-        const int64_t s0 = r0 + (int64_t)k * DQH_STEP;
-        if (tid < DQH_STEP * DQH_C4) {
-            const int64_t row = s0 + tid / DQH_C4;
-            vreg = row < r1 ? src[row * 16 + tid % DQH_C4] : make_float4(0.f, 0.f, 0.f, 0.f);
-        } else if (tid < DQH_STEP * DQH_C4 + DQH_FR * DQH_HSW / 8) {
-            const int j = tid - DQH_STEP * DQH_C4;
-            const int64_t u = s0 / 9 + j / (DQH_HSW / 8);
-            hreg = u < u1 ? reinterpret_cast<const int4 *>(hs + u * DQH_HSW)[j % (DQH_HSW / 8)]
-                          : make_int4(-1, -1, -1, -1);
-        }
-    };
-    auto swrite = [&](int buf) {
-        if (tid < DQH_STEP * DQH_C4)
-            stg[buf][tid] = vreg;
-        else if (tid < DQH_STEP * DQH_C4 + DQH_FR * DQH_HSW / 8)
-            reinterpret_cast<int4 *>(hsl[buf])[tid - DQH_STEP * DQH_C4] = hreg;
-    };
-    // per-lane constants: 16 rows per wave-instruction, lane = (row q, float4 c4 of the slice)
-    const int q = lane / DQH_C4, c4 = lane % DQH_C4;
-    const int ky = tap / 3, kx = tap - 3 * ky;
-    float *accw = reinterpret_cast<float *>(acc) + (size_t)tap * nhot * DQH_SC + c4 * 4;
-    if (nsteps > 0) {
-        gload(0);
-        swrite(0);
-    }
-    __syncthreads();
-    for (int k = 0; k < nsteps; k++) {
-        const int buf = k & 1;
-        if (k + 1 < nsteps) gload(k + 1);
-        const int64_t s0 = r0 + (int64_t)k * DQH_STEP;
-        const int64_t ulo = s0 / 9;
-#pragma unroll
-        for (int it = 0; it < DQH_STEP / 16; it++) {
-            const int lr = it * 16 + q;
-            const int64_t row = s0 + lr;
-            const int64_t u = row / 9;
-            const int p3 = (int)(row - u * 9);
-            const int p2 = (p3 / 3 + ky) * 5 + (p3 - 3 * (p3 / 3)) + kx;
-            const int s = row < r1 ? hsl[buf][(int)(u - ulo) * DQH_HSW + p2] : -1;
-            if (s >= 0) {
-                const float4 v = stg[buf][lr * DQH_C4 + c4];
-                float *a = accw + s * DQH_SC;
-                atomicAdd(a + 0, v.x);
-                atomicAdd(a + 1, v.y);
-                atomicAdd(a + 2, v.z);
-                atomicAdd(a + 3, v.w);
-            }
-        }
-        if (k + 1 < nsteps) swrite(buf ^ 1);
-        __syncthreads();
-    }
-    // partial sums of this (tower, chunk, slice): part[t][chunk][tap][slot][64 channels]
-    for (int i = tid; i < 9 * nhot * DQH_C4; i += DQH_THREADS) {
-        const int row = i / DQH_C4;  // tap * nhot + slot
-        part[(((size_t)t * chunks + chunk) * 9 * nhot + row) * 16 + slice * DQH_C4 + i % DQH_C4] = acc[i];
-    }
-}
-
-// dQ[t][hot_w[s] * 9 + tap] = sum over chunks (in order) of part[t][chunk][tap][s]
-__global__ __launch_bounds__(256) void k_dq_hot_reduce(const float4 *__restrict__ part, int chunks, int nhot,
-                                                       const int32_t *__restrict__ hot_w, int T,
-                                                       float4 *__restrict__ out, int64_t out_rows) {
-    const int64_t total = (int64_t)T * 9 * nhot * 16;
-    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-        const int c = (int)(e & 15);
-        const int64_t rr = e >> 4;  // (t, tap, s)
-        const int s = (int)(rr % nhot), tap = (int)((rr / nhot) % 9), t = (int)(rr / (9 * nhot));
-        const float4 *p = part + (((size_t)t * chunks * 9 + tap) * nhot + s) * 16 + c;
-        float4 a = p[0];
-        for (int ch = 1; ch < chunks; ch++) f4_add(a, p[(size_t)ch * 9 * nhot * 16]);
-        out[((size_t)t * out_rows + (int64_t)hot_w[s] * 9 + tap) * 16 + c] = a;
-    }
-}
-
 }  // namespace
-
-int dq_hot_chunks(int64_t U, int T) {
-    // one workgroup per CU: T * DQH_NS * chunks ~ 256, at least a few steps per chunk
-    int c = 256 / (T * DQH_NS);
-    while (c > 1 && U * 9 / c < 4 * DQH_STEP) c >>= 1;
-    return c;
-}
-size_t dq_hot_part_floats(int64_t U, int T, int nhot) { return (size_t)T * dq_hot_chunks(U, T) * 9 * nhot * 64; }
-int dq_hot_max() { return DQH_MAXHOT; }
-
-hipError_t launch_dq_hot(const float *dZ3, int64_t U, const int16_t *hs, const int32_t *hot_w, int nhot, int T,
-                         float *part, float *out, int64_t out_rows, hipStream_t s) {
-    if (U <= 0 || nhot <= 0) return hipSuccess;
-    const int chunks = dq_hot_chunks(U, T);
-    const int work = T * chunks * DQH_NS;  // workgroups doing work
-    const int grid = ((work + 8 * DQH_NS - 1) / (8 * DQH_NS)) * 8 * DQH_NS;
-    hipLaunchKernelGGL(k_dq_hot, dim3(grid), dim3(DQH_THREADS), 0, s, reinterpret_cast<const float4 *>(dZ3), U, hs,
-                       nhot, chunks, T, reinterpret_cast<float4 *>(part));
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int64_t total = (int64_t)T * 9 * nhot * 16;
-    const int g2 = (int)std::min<int64_t>((total + 255) / 256, 256 * 8);
-    hipLaunchKernelGGL(k_dq_hot_reduce, dim3(g2), dim3(256), 0, s, reinterpret_cast<const float4 *>(part), chunks,
-                       nhot, hot_w, T, reinterpret_cast<float4 *>(out), out_rows);
-    return hipGetLastError();
-}
 
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s) {
     const int64_t total = (int64_t)T * nw * 16;

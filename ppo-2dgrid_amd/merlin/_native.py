@@ -89,9 +89,6 @@ def lib():
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
-    L.merlin_tower_window_dq_hot_workspace.argtypes = [i64, i32, i32]
-    L.merlin_tower_window_dq_hot_workspace.restype = i64
-    L.merlin_tower_window_dq_hot.argtypes = [vp, i64, vp, vp, i32, i32, vp, vp, i64, vp]
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
@@ -134,8 +131,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
-    "merlin_segment_sum", "merlin_tower_window_dq_hot_workspace", "merlin_tower_window_dq_hot",
-    "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
+    "merlin_segment_sum", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
 )
 
@@ -450,32 +446,6 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
                                        int(sub), plan.item_len, ptr(plan.fix), int(plan.fix.shape[0]), T, ptr(out),
                                        int(out_rows), ptr(carry), int(bool(accumulate)), stream_of(src)),
               "merlin_segment_sum")
-    return out
-
-
-DQ_HOT_MAX = 192
-HOT_SLOT_WORDS = 32  # int16 hot slots per frame row (25 conv2 positions used)
-
-
-def window_dq_hot(dZ3, hot_slots, hot_windows, out, workspace=None):
-    """Writes the hot windows' rows of dQ (out f32[T, out_rows, 64], rows hot_windows[s]*9 + tap):
-    the sum of dZ3 f32[T, n*9, 64] rows (u, p3) whose window at conv2 position p2(p3, tap) has hot
-    slot s in hot_slots int16[n, 32]; other rows of out are left untouched."""
-    T, rows = int(dZ3.shape[0]), int(dZ3.shape[1])
-    n = rows // 9
-    nhot = int(hot_windows.numel())
-    assert dZ3.shape[2] == 64 and dZ3.dtype == torch.float32 and rows == n * 9
-    assert hot_slots.dtype == torch.int16 and hot_slots.shape == (n, HOT_SLOT_WORDS)
-    assert hot_windows.dtype == torch.int32 and nhot <= DQ_HOT_MAX
-    assert out.dtype == torch.float32 and out.shape[0] == T and out.shape[2] == 64 and out.is_contiguous()
-    need = int(lib().merlin_tower_window_dq_hot_workspace(n, T, nhot))
-    if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(max(need, 1), dtype=torch.float32, device=dZ3.device)
-    # algorithmic bytes: dZ3 read once, the frames' hot slots, the hot rows of dQ written
-    with KernelTimer.span("k_dq_hot", T * rows * 256 + n * HOT_SLOT_WORDS * 2 + T * nhot * 9 * 256):
-        check(lib().merlin_tower_window_dq_hot(ptr(dZ3), n, ptr(hot_slots), ptr(hot_windows), nhot, T,
-                                               ptr(workspace), ptr(out), int(out.shape[1]), stream_of(dZ3)),
-              "merlin_tower_window_dq_hot")
     return out
 
 

@@ -44,12 +44,6 @@ ITEM_LEN = 1024      # entries per wave of the dQ lists (81 per distinct frame o
 # idx -> slot -> row chain), so the default stays one list.
 DQ_BLOCKS = 1
 HIST_ITEM_LEN = 256  # of the dT2 lists (16 per window)
-# dQ of the DQ_HOT most-entered windows is summed in LDS (merlin_tower_window_dq_hot: each dZ3 row
-# read once); the gather list then holds only the other ("cold") windows' entries.  A bench
-# rollout's 192 most-entered windows take ~85 % of the dQ entries.  0 = every window gathered.
-DQ_HOT = 192
-# entries per (frame, p3, tap) land on conv2 position p2 = P2_OF[p3][tap]: how many of the 81 per p2
-NTAPS_OF_P2 = [sum(1 for p in range(9) for k in range(9) if P2_OF[p][k] == q) for q in range(25)]
 
 
 def unpack_classes(codes: torch.Tensor) -> torch.Tensor:
@@ -141,7 +135,7 @@ class WindowPlan:
     (frame id = merlin.dedup.FrameGroups group id) and the two backward entry lists."""
 
     def __init__(self, codes: torch.Tensor, frame_groups, item_len: int = ITEM_LEN,
-                 hist_item_len: int = HIST_ITEM_LEN, dq_blocks: int = DQ_BLOCKS, dq_hot: int = DQ_HOT):
+                 hist_item_len: int = HIST_ITEM_LEN, dq_blocks: int = DQ_BLOCKS):
         dev = codes.device
         self.frame_groups = frame_groups
         rep = codes.index_select(0, frame_groups.rep)  # one code row per distinct frame
@@ -155,39 +149,16 @@ class WindowPlan:
         # dT2 lists: entry (w, tap) -> table row rows[w][tap]; source row w of dZ2w
         hk, ho = torch.sort(self.rows.reshape(-1), stable=True)
         self.hist = SegmentPlan(hk, ho // 16, hist_item_len)
-        # hot windows: the dq_hot windows with the most dQ entries over the rollout's distinct frames;
-        # hot_slots[g][p2] = the hot slot of frame g's window at p2, or -1 (merlin_tower_window_dq_hot)
-        wl = self.wid.long()
-        self.num_hot = min(int(dq_hot), nw, nat.DQ_HOT_MAX)
-        hot_of = torch.full((nw,), -1, dtype=torch.int16, device=dev)
-        if self.num_hot:
-            ntaps = torch.tensor(NTAPS_OF_P2, dtype=torch.float32, device=dev)
-            cnt = torch.zeros(nw, dtype=torch.float32, device=dev).index_add_(0, wl.reshape(-1), ntaps.repeat(F))
-            hot = torch.topk(cnt, self.num_hot).indices
-            hot_of[hot] = torch.arange(self.num_hot, dtype=torch.int16, device=dev)
-            self.hot_windows = hot.to(torch.int32).contiguous()
-            self.hot_slots = torch.full((F, nat.HOT_SLOT_WORDS), -1, dtype=torch.int16, device=dev)
-            self.hot_slots[:, :25] = hot_of[wl]
-        # dQ gather lists: entry (frame g, p3, tap) -> Q row wid[g][p3 + tap] * 9 + tap; source dZ3
-        # row g*9 + p3; the cold windows' entries only, destination-sorted (stable: ascending source
-        # within a destination), one list per block of frame ids (DQ_BLOCKS)
+        # dQ lists: entry (frame g, p3, tap) -> Q row wid[g][p3 + tap] * 9 + tap; source dZ3 row
+        # g*9 + p3; one destination-sorted list per block of frame ids (DQ_BLOCKS)
         p2 = torch.tensor(P2_OF, dtype=torch.int64, device=dev)
-        wsel = wl[:, p2]  # [F, 9 p3, 9 tap]
-        dst = (wsel * 9 + torch.arange(9, dtype=torch.int64, device=dev)).reshape(-1)
-        cold = (hot_of[wsel] < 0).reshape(-1) if self.num_hot else None
+        dst = (self.wid[:, p2].long() * 9 + torch.arange(9, dtype=torch.int64, device=dev)).reshape(-1)
         nd, nb = nw * 9, max(1, min(int(dq_blocks), F))
         blk = torch.arange(F, dtype=torch.int64, device=dev) * nb // F
-        key = blk.repeat_interleave(81) * nd + dst
-        src = torch.arange(F * 81, dtype=torch.int64, device=dev)
-        if cold is not None:
-            key, src = key[cold], src[cold]
-        dk, order = torch.sort(key, stable=True)
-        do = src[order]
-        self.num_cold_entries = int(dk.numel())
+        dk, do = torch.sort(blk.repeat_interleave(81) * nd + dst, stable=True)
         self.conv3_blocks = []
         off = 0
-        bcnt = torch.bincount(dk // nd, minlength=nb).tolist() if dk.numel() else [0] * nb
-        for b, c in enumerate(bcnt):
+        for b, c in enumerate(torch.bincount(blk, minlength=nb).mul_(81).tolist()):
             if c:
                 self.conv3_blocks.append(SegmentPlan(dk[off:off + c] - b * nd, do[off:off + c] // 9, item_len))
             off += c
@@ -264,11 +235,9 @@ class _WindowConv3(torch.autograd.Function):
         dZ3, db3 = nat.relu_bwd(Y3, dY3.contiguous())
         dQ = torch.zeros((dZ3.shape[0], plan.num_windows * 9, 64), dtype=dZ3.dtype, device=dZ3.device)
         carry = dZ3.new_empty(dZ3.shape[0] * max([p.nitems for p in plan.conv3_blocks] + [1]) * 128)
-        for b, part in enumerate(plan.conv3_blocks):  # cold windows: source blocks, summed in block order
+        for b, part in enumerate(plan.conv3_blocks):  # source blocks, summed in block order
             nat.segment_sum(dZ3, part, plan.num_windows * 9, slot=ctx.mb.slot, sub=9, name="k_seg_sum_dQ",
                             out=dQ, accumulate=b > 0, carry=carry)
-        if plan.num_hot:  # hot windows' rows (disjoint from the cold ones)
-            nat.window_dq_hot(dZ3, plan.hot_slots.index_select(0, ctx.mb.groups), plan.hot_windows, dQ)
         return dQ.view(dQ.shape[0], plan.num_windows, 576), db3, None, None
 
 

@@ -158,42 +158,3 @@ def test_window_update_matches_lookup_path(device):
     for d in ds:
         assert d.max().item() <= 2 * 3e-4 * 8
     assert (torch.cat(ds) > 5e-5).float().mean().item() < 0.05
-
-
-@pytest.mark.parametrize("n_mb", [1, 37, 6000])
-def test_dq_hot_matches_index_add(device, n_mb):
-    """merlin_tower_window_dq_hot (LDS accumulation of the hot windows' dQ rows) == index_add in
-    float64 over every (u, p3, tap) with a hot window; rows of cold windows are left untouched;
-    bitwise the same run to run (one writer per accumulator, chunk partials in order)."""
-    from merlin import _native as nat
-    from merlin.windows import P2_OF
-
-    codes, plan = _plan(device)
-    assert 0 < plan.num_hot <= nat.DQ_HOT_MAX
-    g = torch.Generator(device=device)
-    g.manual_seed(n_mb)
-    mb = plan.minibatch(torch.randperm(codes.shape[0], device=device, generator=g)[:n_mb])
-    U = int(mb.groups.numel())
-    dZ3 = torch.randn(2, U * 9, 64, device=device, generator=g)
-    rows = plan.num_windows * 9
-    out = torch.full((2, rows, 64), 7.0, device=device)
-    hs = plan.hot_slots.index_select(0, mb.groups)
-    nat.window_dq_hot(dZ3, hs, plan.hot_windows, out)
-    s = hs[:, :25].long()[:, torch.tensor(P2_OF, device=device)]  # [U, p3, tap]
-    hot = s >= 0
-    u, p3, tap = torch.nonzero(hot, as_tuple=True)
-    dst = plan.hot_windows.long()[s[hot]] * 9 + tap
-    ref = torch.zeros(2, rows, 64, dtype=torch.float64, device=device)
-    mag = torch.zeros_like(ref)
-    for t in range(2):
-        ref[t].index_add_(0, dst, dZ3[t, u * 9 + p3].double())
-        mag[t].index_add_(0, dst, dZ3[t, u * 9 + p3].double().abs())
-    hot_rows = (plan.hot_windows.long()[:, None] * 9 + torch.arange(9, device=device)).reshape(-1)
-    err = (out[:, hot_rows].double() - ref[:, hot_rows]).abs()
-    assert (err <= 1e-5 * mag[:, hot_rows] + 1e-6).all(), (err / (mag[:, hot_rows] + 1e-6)).max().item()
-    cold = torch.ones(rows, dtype=torch.bool, device=device)
-    cold[hot_rows] = False
-    assert bool((out[:, cold] == 7.0).all())
-    again = torch.full_like(out, 7.0)
-    nat.window_dq_hot(dZ3, hs, plan.hot_windows, again)
-    assert torch.equal(out, again)

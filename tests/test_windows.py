@@ -94,29 +94,9 @@ def test_segment_plan_sums_every_destination(n, nkeys, L, skew):
     torch.testing.assert_close(emulate_segment_sum(plan, src_mb, nkeys, slot=slot, sub=4), ref)
 
 
-def emulate_dq_hot(plan, dZ3, groups, out_rows):
-    """Restatement of k_dq_hot + k_dq_hot_reduce: the hot windows' dQ rows, every (u, p3, tap)
-    whose window at P2_OF[p3][tap] has a hot slot adds dZ3 row (u, p3) to row hot_w * 9 + tap."""
-    from merlin.windows import P2_OF
-
-    T = dZ3.shape[0]
-    out = torch.zeros(T, out_rows, dZ3.shape[2], dtype=dZ3.dtype)
-    hs = plan.hot_slots[groups].long()
-    for u in range(groups.numel()):
-        for p3 in range(9):
-            for tap in range(9):
-                s = int(hs[u, P2_OF[p3][tap]])
-                if s >= 0:
-                    out[:, int(plan.hot_windows[s]) * 9 + tap] += dZ3[:, u * 9 + p3]
-    return out
-
-
-@pytest.mark.parametrize("dq_hot", [0, 3, 500])
-def test_window_towers_match_frame_convs(golden, dq_hot):
+def test_window_towers_match_frame_convs(golden):
     """Y3 through windows == relu(conv3(relu(conv2(relu(conv1(frame)))))) of the reference
-    modules; dQ and dT2 from the plan's lists == autograd of the torch gathers.  dQ = the cold
-    windows' gather lists + the hot windows' LDS sums (dq_hot of them; 0: all gathered, 500: all
-    hot, capped at the kernel's capacity or the window count)."""
+    modules; dQ and dT2 from the plan's lists == autograd of the torch gathers."""
     import oracle as O
 
     from merlin.dedup import FrameGroups
@@ -128,12 +108,8 @@ def test_window_towers_match_frame_convs(golden, dq_hot):
     c[:, 45] = 4
     c = np.concatenate([c, c[:5]])  # repeated observations share a frame id
     codes = torch.from_numpy(pack(c))
-    plan = WindowPlan(codes, FrameGroups(codes), item_len=16, hist_item_len=8, dq_blocks=3, dq_hot=dq_hot)
+    plan = WindowPlan(codes, FrameGroups(codes), item_len=16, hist_item_len=8, dq_blocks=3)
     assert plan.num_frames == 12
-    assert plan.num_hot == min(dq_hot, plan.num_windows, 192)
-    if dq_hot:
-        hot_entries = ((plan.hot_slots[:, :25].long() >= 0).float() @ torch.tensor([float(x) for x in _ntaps()])).sum()
-        assert plan.num_cold_entries == 81 * 12 - int(hot_entries)
     mb_idx = torch.tensor([0, 3, 12, 5, 7, 14, 9, 3])
     mb = plan.minibatch(mb_idx)
     ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
@@ -153,21 +129,12 @@ def test_window_towers_match_frame_convs(golden, dq_hot):
     g = torch.randn(2, mb.groups.numel(), 9, 64, dtype=torch.float64)
     (Y3 * g).sum().backward()
     dZ3 = torch.where(Y3 > 0, g, torch.zeros((), dtype=g.dtype)).reshape(2, -1, 64).detach()
-    assert len(plan.conv3_blocks) == (3 if plan.num_hot < plan.num_windows else 0)
+    assert len(plan.conv3_blocks) == 3
     dQ = sum(emulate_segment_sum(part, dZ3, plan.num_windows * 9, slot=mb.slot, sub=9) for part in plan.conv3_blocks)
-    if plan.num_hot:
-        dQ = dQ + emulate_dq_hot(plan, dZ3, mb.groups, plan.num_windows * 9)
     torch.testing.assert_close(dQ.view_as(Q), Q.grad)
     dZ2w = torch.randn(2, plan.num_windows, 64, dtype=torch.float64)
     (T2[:, plan.rows.long()].sum(2) * dZ2w).sum().backward()
     torch.testing.assert_close(emulate_segment_sum(plan.hist, dZ2w, 2720), T2.grad)
-
-
-def _ntaps():
-    from merlin.windows import NTAPS_OF_P2
-
-    assert sum(NTAPS_OF_P2) == 81
-    return NTAPS_OF_P2
 
 
 def test_epoch_minibatches_match_per_minibatch_grouping():
