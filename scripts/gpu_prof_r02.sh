@@ -1,0 +1,17 @@
+#!/bin/bash
+# rocprofv3 kernel trace + stats of the bench at the driver's settings (20 timed steps after 5
+# warmups), then separate PMC passes (FETCH_SIZE, WRITE_SIZE) over the same command.
+R="$GRAFT_REPO_ROOT"; mkdir -p "$R/gpurun_out"
+cd /tmp && export TMPDIR=/tmp
+ARGS="${BENCH_ARGS:---steps 20 --warmup 5 --no-cpu-baseline --no-tiers}"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$R/gpurun_out/prof_trace" -o run -- \
+    python "$R/bench.py" $ARGS > "$R/gpurun_out/prof_trace.log" 2>&1 || exit $?
+tail -c 600 "$R/gpurun_out/prof_trace.log"
+if [ -n "$PMC" ]; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "${PMC_RE:-k_}" -T -f csv \
+        -d "$R/gpurun_out/prof_pmc_$C" -o run -- python "$R/bench.py" $ARGS \
+        > "$R/gpurun_out/prof_pmc_$C.log" 2>&1 || exit $?
+    echo "pmc $C done"
+  done
+fi
