@@ -223,49 +223,6 @@ class _BiasReluBmm(torch.autograd.Function):
         return dX, dW, db.unsqueeze(1), None
 
 
-class DeferredWeightGrad:
-    """fc1's weight gradient (the K = n split-K product a3^T dz of _TowerHead.backward) computed on a
-    side HIP stream, overlapped with the memory-bound rest of the backward pass (conv3's ReLU
-    mask, the window segmented sums, ...) that runs on the main stream meanwhile; it does not
-    depend on them.  At the end of the backward pass (an autograd engine callback, so before
-    loss.backward() returns) the main stream waits for the side stream and the gradient is added
-    to the fc1 weights' .grad exactly as autograd would have accumulated it."""
-
-    def __init__(self):
-        self.stream = None
-        self.params = None
-        self.pending = None
-
-    def launch(self, fn, inputs):
-        main = torch.cuda.current_stream()
-        if self.stream is None or self.stream.device != main.device:
-            self.stream = torch.cuda.Stream(device=main.device)
-        self.stream.wait_stream(main)
-        with torch.cuda.stream(self.stream):
-            out = fn()
-        for t in inputs:  # made on main, read on the side stream: keep their memory until it is done
-            t.record_stream(self.stream)
-        self.pending = (out, self.stream.record_event(), self.params)
-        torch.autograd.Variable._execution_engine.queue_callback(self.finish)
-
-    def finish(self):
-        if self.pending is None:
-            return
-        out, ev, params = self.pending
-        self.pending = None
-        main = torch.cuda.current_stream()
-        main.wait_event(ev)
-        out.record_stream(main)
-        # out = a3^T dz [2, 576 (p3, co), H] -> dW4 [2, H, 576 (co, p3)], the nn.Linear layout
-        T, K, H = out.shape
-        dW = out.view(T, 9, K // 9, H).permute(0, 3, 2, 1).reshape(T, H, K)
-        for t, p in enumerate(params):
-            if p.grad is None:
-                p.grad = dW[t].clone()
-            else:
-                p.grad.add_(dW[t])
-
-
 class _TowerHead(torch.autograd.Function):
     """fc1 -> ReLU -> heads of both towers (actor_critic.py:30-41) on a3 [2, n, 576] (rows
     (p3, co), W4's columns permuted to match, W4p [2, H, 576]): one bmm + the bias/ReLU
@@ -274,10 +231,9 @@ class _TowerHead(torch.autograd.Function):
     (merlin_tower_head_bwd), then fc1's input gradient (bmm) and weight gradient (split-K)."""
 
     @staticmethod
-    def forward(ctx, a3, W4p, b4, Wa, ba, Wc, bc, defer=None):
+    def forward(ctx, a3, W4p, b4, Wa, ba, Wc, bc):
         from . import _native as nat
 
-        ctx.defer = defer
         h = nat.bias_relu_(torch.bmm(a3, W4p.transpose(1, 2)), b4.detach().contiguous())
         logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
         value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)
@@ -295,15 +251,10 @@ class _TowerHead(torch.autograd.Function):
         dvalue = h.new_zeros(n) if dvalue is None else dvalue.contiguous()
         dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
         da3 = torch.bmm(dz, W4p) if ctx.needs_input_grad[0] else None
-        if ctx.defer is not None and da3 is not None:
-            # after da3: on the side stream, overlapped with the rest of the backward pass
-            ctx.defer.launch(lambda: _splitk_bmm_tn(a3, dz, 32), (a3, dz))
-            dW4p = None
-        else:
-            dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
+        dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
         dba = dlogits.sum(0) if ctx.head_bias[0] else None
         dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
-        return da3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc, None
+        return da3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc
 
 
 def _lut2_h1_index():
@@ -387,9 +338,6 @@ class CNNActorCritic(nn.Module):
         # "lut2": conv1+conv2 as table lookups, conv3/fc as hipBLASLt GEMMs (default)
         # "gemm": conv1 lookups, conv2/conv3/fc as GEMMs | "lut_nchw": conv1 lookups + MIOpen convs
         self.codes_impl = "lut2"
-        # fc1's weight gradient on a side stream, overlapped with the conv backward (None: inline)
-        self.defer_fc1_wgrad = True
-        self._defer = DeferredWeightGrad()
 
     # -- tile-code path (GPU envs) --------------------------------------------------
     def _atlas_on(self, device):
@@ -456,12 +404,8 @@ class CNNActorCritic(nn.Module):
         W4 = torch.stack([fa.weight, fc.weight])  # [2, hidden, 576] in (co, p3) order
         W4p = W4.view(2, W4.shape[1], 64, 9).transpose(2, 3).reshape(2, W4.shape[1], 576)
         ba, bc = (self.actor[2].bias, self.critic[2].bias) if head_bias else (None, None)
-        defer = None
-        if self.defer_fc1_wgrad and a3.is_cuda and torch.is_grad_enabled() and fa.weight.requires_grad:
-            defer = self._defer
-            defer.params = (fa.weight, fc.weight)
         return _TowerHead.apply(a3, W4p, torch.stack([fa.bias, fc.bias]), self.actor[2].weight, ba,
-                                self.critic[2].weight, bc, defer)
+                                self.critic[2].weight, bc)
 
     def _forward_codes(self, codes, index=None):
         """Both towers from tile codes as GEMMs (csrc/merlin_tower.hip for the data movement):
