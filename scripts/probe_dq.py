@@ -80,7 +80,42 @@ def main():
     d1 = dZ3[:1].contiguous()
     o1 = out[:1].contiguous()
     print(f"  compacted, one tower: {timeit(lambda: nat.segment_sum(d1, cplan, rows, out=o1)):.1f} us", flush=True)
+    blocks_probe.ctx = {"ck": ck, "ci": ci, "dZ3": dZ3, "rows": rows, "U": U}
+    blocks_probe()
 
 
 if __name__ == "__main__":
     main()
+
+
+def blocks_probe():
+    """Source-blocked compacted lists: block b holds the entries whose minibatch frame u lies in
+    the b-th of nb contiguous u ranges (its dZ3 rows: 1/nb of the table), summed block after block
+    into dQ (accumulate)."""
+    import merlin._native as nat
+    from merlin.windows import SegmentPlan
+    g = blocks_probe.ctx
+    ck, ci, dZ3, rows, U = g["ck"], g["ci"], g["dZ3"], g["rows"], g["U"]
+    out = torch.empty(2, rows, 64, device=dZ3.device)
+    for nb in (1, 2, 3, 4, 8):
+        blk = (ci // 9) * nb // U
+        key = blk * rows + ck.long()
+        k2, o2 = torch.sort(key, stable=True)
+        parts = []
+        cnt = torch.bincount(blk, minlength=nb).tolist()
+        off = 0
+        for b, c in enumerate(cnt):
+            parts.append(SegmentPlan(k2[off:off + c] - b * rows, ci[o2[off:off + c]], 1024))
+            off += c
+
+        def run():
+            for b, p in enumerate(parts):
+                nat.segment_sum(dZ3, p, rows, out=out, accumulate=b > 0)
+        print(f"  compacted, {nb} source blocks (sequential, accumulate): {timeit(run):.1f} us", flush=True)
+        d1 = dZ3[:1].contiguous()
+        o1 = out[:1].contiguous()
+
+        def run1():
+            for b, p in enumerate(parts):
+                nat.segment_sum(d1, p, rows, out=o1, accumulate=b > 0)
+        print(f"     one tower: {timeit(run1):.1f} us", flush=True)
