@@ -84,10 +84,6 @@ def main():
     blocks_probe()
 
 
-if __name__ == "__main__":
-    main()
-
-
 def blocks_probe():
     """Source-blocked compacted lists: block b holds the entries whose minibatch frame u lies in
     the b-th of nb contiguous u ranges (its dZ3 rows: 1/nb of the table), summed block after block
@@ -119,3 +115,7 @@ def blocks_probe():
             for b, p in enumerate(parts):
                 nat.segment_sum(d1, p, rows, out=o1, accumulate=b > 0)
         print(f"     one tower: {timeit(run1):.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
