@@ -115,6 +115,16 @@ def blocks_probe():
             for b, p in enumerate(parts):
                 nat.segment_sum(d1, p, rows, out=o1, accumulate=b > 0)
         print(f"     one tower: {timeit(run1):.1f} us", flush=True)
+        for L in (256, 512, 1024):
+            cat = SegmentPlan(k2, ci[o2], L)  # one launch, keys (block, dst): partial rows per block
+            part = torch.empty(2, nb * rows, 64, device=dZ3.device)
+
+            def run2():
+                nat.segment_sum(dZ3, cat, nb * rows, out=part)
+                torch.sum(part.view(2, nb, rows, 64), 1, out=out)
+            t = timeit(run2)
+            tp = timeit(lambda: nat.segment_sum(dZ3, cat, nb * rows, out=part))
+            print(f"     one launch, block-major items, L={L}: {t:.1f} us (segment_sum alone {tp:.1f})", flush=True)
 
 
 if __name__ == "__main__":
