@@ -86,48 +86,55 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
     }
 }
 
-// One wave per item of L entries; lane = (tower t, float2 column c2), so one wave load reads
-// one entry's 256-B row of each tower.  The wave loads 64 entries' (idx, key) at a time,
-// resolves their source rows (through slot[] when given: -1 = not in this minibatch), and
-// walks the valid ones in order, SEG_UNROLL row loads in flight (issued unconditionally:
-// a select around a load would make hipcc wait for each load in turn), flushing a
-// destination's sum when the key changes.  The item's first / last destination, when it
-// continues in the neighbouring item, goes to carry[t][item][0 / 1] instead of out.  With
-// acc_out the sums are added to out (one writer per destination per launch), so a list split
-// by source block into several launches (merlin/windows.py) accumulates in block order.
+// One wave per item of L entries; lane = (tower t, entry parity q, float4 column c): one wave
+// load reads the 256-B rows of two entries in both towers (1 KB, 16 B per lane).  The wave loads
+// 64 entries' (idx, key) at a time, resolves their source rows (through slot[] when given: -1 = not
+// in this minibatch) and walks the valid ones in order in rounds of two, SEG_UNROLL rounds of row
+// loads in flight (issued unconditionally: a select around a load would make hipcc wait for each
+// load in turn).  Lanes q = 0 / 1 keep partial sums of the even / odd entries of the current
+// destination; when the key changes the two are added (a fixed xor-16 exchange) and the
+// destination's sum is flushed.  The item's first / last destination, when it continues in the
+// neighbouring item, goes to carry[t][item][0 / 1] instead of out.  With acc_out the sums are
+// added to out (one writer per destination per launch), so a list split by source block into
+// several launches (merlin/windows.py) accumulates in block order.
 constexpr int SEG_WAVES = 4, SEG_UNROLL = 8;
-__global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float2 *__restrict__ src, int64_t src_rows,
+__global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__restrict__ src, int64_t src_rows,
                                                            const int32_t *__restrict__ idx,
                                                            const int32_t *__restrict__ key, int64_t nnz,
                                                            const int32_t *__restrict__ slot, int S, int64_t L,
-                                                           int64_t nitems, int T, float2 *__restrict__ out,
-                                                           int64_t out_rows, float2 *__restrict__ carry,
+                                                           int64_t nitems, int T, float4 *__restrict__ out,
+                                                           int64_t out_rows, float4 *__restrict__ carry,
                                                            int acc_out) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int t = lane >> 5, c2 = lane & 31;
+    const int t = lane >> 5, q = (lane >> 4) & 1, c = lane & 15;
     const bool live = t < T;
-    const float2 *srct = src + (size_t)(live ? t : 0) * src_rows * 32 + c2;
-    const float2 zero = make_float2(0.0f, 0.0f);
+    const float4 *srct = src + (size_t)(live ? t : 0) * src_rows * 16 + c;
+    const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int64_t it = (int64_t)blockIdx.x * SEG_WAVES + wv; it < nitems; it += (int64_t)gridDim.x * SEG_WAVES) {
         const int64_t e0 = it * L, e1 = std::min<int64_t>(nnz, e0 + L);
         const int kfirst = key[e0], klast = key[e1 - 1];
         const bool xfirst = e0 > 0 && key[e0 - 1] == kfirst;
         const bool xlast = e1 < nnz && key[e1] == klast;
         const bool to_head_last = kfirst == klast && xlast;
-        float2 head = zero, tail = zero, acc = zero;
+        float4 head = zero, tail = zero, acc = zero;
         int cur = -1;
-        auto flush = [&]() {
+        auto flush = [&]() {  // wave-uniform call sites (keys are uniform)
+            float4 o = acc;
+            o.x += __shfl_xor(acc.x, 16);
+            o.y += __shfl_xor(acc.y, 16);
+            o.z += __shfl_xor(acc.z, 16);
+            o.w += __shfl_xor(acc.w, 16);
             if (cur == kfirst && (xfirst || to_head_last))
-                head = acc;
+                head = o;
             else if (cur == klast && xlast)
-                tail = acc;
-            else if (live) {
-                float2 *o = out + ((size_t)t * out_rows + cur) * 32 + c2;
+                tail = o;
+            else if (live && q == 0) {
+                float4 *d = out + ((size_t)t * out_rows + cur) * 16 + c;
                 if (acc_out) {
-                    const float2 p = *o;
-                    *o = make_float2(p.x + acc.x, p.y + acc.y);
+                    const float4 p = *d;
+                    *d = make_float4(p.x + o.x, p.y + o.y, p.z + o.z, p.w + o.w);
                 } else {
-                    *o = acc;
+                    *d = o;
                 }
             }
         };
@@ -137,45 +144,55 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float2 *__rest
                 const int v = idx[base + lane];
                 k = key[base + lane];
                 if (slot) {
-                    const int q = v / S;
-                    const int s = slot[q];
-                    row = s >= 0 ? s * S + (v - q * S) : -1;
+                    const int g = v / S;
+                    const int sl = slot[g];
+                    row = sl >= 0 ? sl * S + (v - g * S) : -1;
                 } else {
                     row = v;
                 }
             }
             unsigned long long m = __ballot(row >= 0);
             while (m) {
-                int rq[SEG_UNROLL], kq[SEG_UNROLL];
+                int rq[SEG_UNROLL], k0[SEG_UNROLL], k1[SEG_UNROLL];
 #pragma unroll
-                for (int q = 0; q < SEG_UNROLL; q++) {
-                    const int j = m ? __builtin_ctzll(m) : -1;  // wave-uniform
+                for (int u = 0; u < SEG_UNROLL; u++) {
+                    const int j0 = m ? __builtin_ctzll(m) : -1;  // wave-uniform
                     if (m) m &= m - 1;
-                    rq[q] = j >= 0 ? __shfl(row, j) : 0;
-                    kq[q] = j >= 0 ? __shfl(k, j) : -1;
+                    const int j1 = m ? __builtin_ctzll(m) : -1;
+                    if (m) m &= m - 1;
+                    const int r0 = j0 >= 0 ? __shfl(row, j0) : 0;
+                    const int r1 = j1 >= 0 ? __shfl(row, j1) : 0;
+                    k0[u] = j0 >= 0 ? __shfl(k, j0) : -1;
+                    k1[u] = j1 >= 0 ? __shfl(k, j1) : -1;
+                    rq[u] = q ? r1 : r0;
                 }
-                float2 vq[SEG_UNROLL];
+                float4 vq[SEG_UNROLL];
 #pragma unroll
-                for (int q = 0; q < SEG_UNROLL; q++) vq[q] = srct[(size_t)rq[q] * 32];
+                for (int u = 0; u < SEG_UNROLL; u++) vq[u] = srct[(size_t)rq[u] * 16];
 #pragma unroll
-                for (int q = 0; q < SEG_UNROLL; q++) {
-                    if (kq[q] < 0) break;
-                    if (kq[q] != cur) {
+                for (int u = 0; u < SEG_UNROLL; u++) {
+                    if (k0[u] < 0) break;
+                    if (k0[u] != cur) {
                         if (cur >= 0) flush();
-                        cur = kq[q];
-                        acc = vq[q];
-                    } else {
-                        acc.x += vq[q].x;
-                        acc.y += vq[q].y;
+                        cur = k0[u];
+                        acc = zero;
                     }
+                    if (q == 0) f4_add(acc, vq[u]);
+                    if (k1[u] < 0) break;
+                    if (k1[u] != cur) {
+                        flush();
+                        cur = k1[u];
+                        acc = zero;
+                    }
+                    if (q == 1) f4_add(acc, vq[u]);
                 }
             }
         }
         if (cur >= 0) flush();
-        if (live) {
-            float2 *cr = carry + ((size_t)t * nitems + it) * 64 + c2;
+        if (live && q == 0) {
+            float4 *cr = carry + ((size_t)t * nitems + it) * 32 + c;
             cr[0] = head;
-            cr[32] = tail;
+            cr[16] = tail;
         }
     }
 }
@@ -234,9 +251,9 @@ hipError_t launch_seg_sum(const float *src, int64_t src_rows, const int32_t *idx
     if (e != hipSuccess || nnz <= 0) return e;
     const int64_t nitems = (nnz + L - 1) / L;
     const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
-    hipLaunchKernelGGL(k_seg_sum, dim3(grid), dim3(64 * SEG_WAVES), 0, s, reinterpret_cast<const float2 *>(src),
-                       src_rows, idx, key, nnz, slot, S, L, nitems, T, reinterpret_cast<float2 *>(out), out_rows,
-                       reinterpret_cast<float2 *>(carry), acc_out);
+    hipLaunchKernelGGL(k_seg_sum, dim3(grid), dim3(64 * SEG_WAVES), 0, s, reinterpret_cast<const float4 *>(src),
+                       src_rows, idx, key, nnz, slot, S, L, nitems, T, reinterpret_cast<float4 *>(out), out_rows,
+                       reinterpret_cast<float4 *>(carry), acc_out);
     e = hipGetLastError();
     if (e != hipSuccess || nfix <= 0) return e;
     const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);
