@@ -19,12 +19,15 @@
 //   view    gen_obs_grid (get_view_exts, Grid.slice, rotate_left^(dir+1),
 //           process_vis with see_through_walls=False, base_env.py:39) and the
 //           get_pov_render tile classes (RGBImgPartialObsWrapper, scenario_creator.py:48)
+#include <algorithm>
+
 #include "merlin_internal.h"
 
 namespace merlin {
 namespace {
 
-constexpr int BLK = 64;  // one wave per block: the env count (4096) is small, spread it over CUs
+constexpr int BLK = 64;    // reset kernels: one wave per block (map generation is long and divergent)
+constexpr int SBLK = 256;  // step kernel: 4 waves per block
 
 // ---------------------------------------------------------------------------
 // numpy PCG64 + bounded integers
@@ -100,9 +103,9 @@ __device__ __forceinline__ void store_rng(const EnvDev &E, int i, const Rng &r) 
 
 // ---------------------------------------------------------------------------
 // Per-thread grid view over the LDS column + generator state.
-template <int SP>
+template <int SP, int NB>
 struct Grid {
-    uint32_t (*rows)[BLK];  // LDS [SP][BLK]; this thread owns column `lane`
+    uint32_t (*rows)[NB];  // LDS [SP][NB]; this thread owns column `lane`
     int lane, S;
     int ax, ay, dir;
     int gx, gy;
@@ -363,10 +366,10 @@ struct GenOut {
     uint32_t err;
 };
 
-template <int SP>
-__device__ __noinline__ void generate_map(uint32_t (*rows)[BLK], int lane, int S, int difficulty, Rng &r,
+template <int SP, int NB>
+__device__ __noinline__ void generate_map(uint32_t (*rows)[NB], int lane, int S, int difficulty, Rng &r,
                                           uint32_t *fallbacks, GenOut &o) {
-    Grid<SP> G;
+    Grid<SP, NB> G;
     G.rows = rows;
     G.lane = lane;
     G.S = S;
@@ -383,8 +386,8 @@ __device__ __noinline__ void generate_map(uint32_t (*rows)[BLK], int lane, int S
 __device__ __forceinline__ uint32_t bitrev7(uint32_t v) { return __brev(v) >> 25; }
 
 // gen_obs_grid + get_pov_render tile classes -> 8 packed nibble words.
-template <int SP>
-__device__ __forceinline__ void view_codes(const uint32_t (*rows)[BLK], int lane, int S, int ax, int ay, int dir,
+template <int SP, int NB>
+__device__ __forceinline__ void view_codes(const uint32_t (*rows)[NB], int lane, int S, int ax, int ay, int dir,
                                            int goal_x, int goal_y, bool goal_set,
                                            uint32_t out[MERLIN_OBS_WORDS]) {
     // get_view_exts (top-left of the 7x7 world window)
@@ -472,8 +475,8 @@ __device__ __forceinline__ void view_codes(const uint32_t (*rows)[BLK], int lane
     }
 }
 
-template <int SP>
-__device__ __forceinline__ void load_rows(const EnvDev &E, int i, uint32_t (*rows)[BLK], int lane) {
+template <int SP, int NB>
+__device__ __forceinline__ void load_rows(const EnvDev &E, int i, uint32_t (*rows)[NB], int lane) {
     const uint4 *src = reinterpret_cast<const uint4 *>(E.walls + (size_t)i * SP);
 #pragma unroll
     for (int q = 0; q < SP / 4; q++) {
@@ -485,8 +488,8 @@ __device__ __forceinline__ void load_rows(const EnvDev &E, int i, uint32_t (*row
     }
 }
 
-template <int SP>
-__device__ __forceinline__ void store_rows(const EnvDev &E, int i, const uint32_t (*rows)[BLK], int lane, int S) {
+template <int SP, int NB>
+__device__ __forceinline__ void store_rows(const EnvDev &E, int i, const uint32_t (*rows)[NB], int lane, int S) {
     uint4 *dst = reinterpret_cast<uint4 *>(E.walls + (size_t)i * SP);
 #pragma unroll
     for (int q = 0; q < SP / 4; q++) {
@@ -516,6 +519,25 @@ __device__ __forceinline__ void reset_visited(const EnvDev &E, int i, int ax, in
     for (int y = 0; y < SP; y++) vis[y] = (y == ay) ? (1u << ax) : 0u;
 }
 
+// One env's reset: map generation, state, RNG, episode accumulators, first observation.
+template <int SP>
+__device__ __forceinline__ void reset_one(const EnvDev &E, int i, uint32_t (*rows)[BLK], int lane,
+                                          uint32_t *__restrict__ obs) {
+    Rng r = load_rng(E, i);
+    GenOut g;
+    generate_map<SP, BLK>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
+    if (!E.reseed) store_rng(E, i, r);
+    store_rows<SP, BLK>(E, i, rows, lane, E.size);
+    E.agent[i] = pack_agent(g.ax, g.ay, g.dir, 0, g.gx, g.gy, g.ax, g.ay, 0);
+    E.ep_ret[i] = 0.0;
+    E.ep_len[i] = 0;
+    if (E.explore_on) reset_visited<SP>(E, i, g.ax, g.ay);
+    if (g.err) atomicOr(E.err, g.err);
+    uint32_t w[MERLIN_OBS_WORDS];
+    view_codes<SP, BLK>(rows, lane, E.size, g.ax, g.ay, g.dir, g.gx, g.gy, true, w);
+    if (obs) store_obs(obs, (size_t)i, w);
+}
+
 template <int SP>
 __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__restrict__ mask,
                                                   uint32_t *__restrict__ obs) {
@@ -524,29 +546,31 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
     const int i = blockIdx.x * BLK + lane;
     if (i >= E.n) return;
     if (mask && !mask[i]) return;
-    Rng r = load_rng(E, i);
-    GenOut g;
-    generate_map<SP>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
-    if (!E.reseed) store_rng(E, i, r);
-    store_rows<SP>(E, i, rows, lane, E.size);
-    E.agent[i] = pack_agent(g.ax, g.ay, g.dir, 0, g.gx, g.gy, g.ax, g.ay, 0);
-    E.ep_ret[i] = 0.0;
-    E.ep_len[i] = 0;
-    if (E.explore_on) reset_visited<SP>(E, i, g.ax, g.ay);
-    if (g.err) atomicOr(E.err, g.err);
-    uint32_t w[MERLIN_OBS_WORDS];
-    view_codes<SP>(rows, lane, E.size, g.ax, g.ay, g.dir, g.gx, g.gy, true, w);
-    if (obs) store_obs(obs, (size_t)i, w);
+    reset_one<SP>(E, i, rows, lane, obs);
 }
 
+// The auto-resets of a single-step launch, compacted: k_env_step appended the envs whose episode
+// ended to E.rlist, so the resets (rejection sampling + flood fill, thousands of cycles each) run
+// densely packed here instead of stalling a whole 64-env wave of the step kernel per reset.
 template <int SP>
-__global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
+__global__ __launch_bounds__(BLK) void k_env_autoreset(EnvDev E, uint32_t *__restrict__ obs) {
     __shared__ uint32_t rows[SP][BLK];
     const int lane = threadIdx.x;
-    const int i = blockIdx.x * BLK + lane;
+    const uint32_t cnt = *E.rcount;
+    for (uint32_t j = blockIdx.x * BLK + lane; j < cnt; j += gridDim.x * BLK) reset_one<SP>(E, E.rlist[j], rows, lane, obs);
+}
+
+// DEFER (single-step launches with auto-reset): an env whose episode ends is appended to E.rlist
+// and k_env_autoreset, launched next on the stream, regenerates it and writes its observation; the
+// step kernel then writes neither that obs row nor the env's state.
+template <int SP, bool DEFER>
+__global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
+    __shared__ uint32_t rows[SP][SBLK];
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * SBLK + lane;
     if (i >= E.n) return;
     const int S = E.size;
-    load_rows<SP>(E, i, rows, lane);
+    load_rows<SP, SBLK>(E, i, rows, lane);
     const uint4 st = E.agent[i];
     int ax = st.x & 0xff, ay = (st.x >> 8) & 0xff, dir = (st.x >> 16) & 3;
     int steps = (int)st.y;
@@ -611,13 +635,18 @@ __global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
             if (O.ep_ret_out) O.ep_ret_out[row] = ep_ret;
             if (O.ep_len_out) O.ep_len_out[row] = ep_len;
         }
+        if (DEFER && done) {  // O.autoreset, n_steps == 1
+            E.rlist[atomicAdd(E.rcount, 1u)] = i;
+            if (err) atomicOr(E.err, err);
+            return;
+        }
         if (done && O.autoreset) {
             if (!rng_loaded || E.reseed) {
                 r = load_rng(E, i);  // reseed mode: always restart from the seeded state
                 rng_loaded = true;
             }
             GenOut g;
-            generate_map<SP>(rows, lane, S, E.difficulty, r, E.err + 1, g);
+            generate_map<SP, SBLK>(rows, lane, S, E.difficulty, r, E.err + 1, g);
             ax = g.ax;
             ay = g.ay;
             dir = g.dir;
@@ -635,14 +664,14 @@ __global__ __launch_bounds__(BLK) void k_env_step(EnvDev E, StepOut O) {
         }
         if (O.obs) {
             uint32_t w[MERLIN_OBS_WORDS];
-            view_codes<SP>(rows, lane, S, ax, ay, dir, gx, gy, true, w);
+            view_codes<SP, SBLK>(rows, lane, S, ax, ay, dir, gx, gy, true, w);
             store_obs(O.obs, row, w);
         }
     }
     E.agent[i] = pack_agent(ax, ay, dir, steps, gx, gy, lx, ly, stay);
     E.ep_ret[i] = ep_ret;
     E.ep_len[i] = ep_len;
-    if (rows_dirty) store_rows<SP>(E, i, rows, lane, S);
+    if (rows_dirty) store_rows<SP, SBLK>(E, i, rows, lane, S);
     if (rng_loaded && !E.reseed) store_rng(E, i, r);
     if (err) atomicOr(E.err, err);
 }
@@ -658,13 +687,25 @@ hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs,
     return hipGetLastError();
 }
 
-hipError_t launch_env_step(const EnvDev &E, const StepOut &O, hipStream_t s) {
-    const dim3 grid((E.n + BLK - 1) / BLK), block(BLK);
-    if (E.sp == 16)
-        hipLaunchKernelGGL(k_env_step<16>, grid, block, 0, s, E, O);
-    else
-        hipLaunchKernelGGL(k_env_step<32>, grid, block, 0, s, E, O);
+template <int SP>
+static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t s) {
+    const dim3 grid((E.n + SBLK - 1) / SBLK), block(SBLK);
+    if (O.autoreset && O.n_steps == 1) {  // resets deferred to the compacted k_env_autoreset
+        hipError_t e = hipMemsetAsync(E.rcount, 0, sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_env_step<SP, true>), grid, block, 0, s, E, O);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const int rgrid = std::min((E.n + BLK - 1) / BLK, 2048);
+        hipLaunchKernelGGL(k_env_autoreset<SP>, dim3(rgrid), dim3(BLK), 0, s, E, O.obs);
+    } else {
+        hipLaunchKernelGGL((k_env_step<SP, false>), grid, block, 0, s, E, O);
+    }
     return hipGetLastError();
+}
+
+hipError_t launch_env_step(const EnvDev &E, const StepOut &O, hipStream_t s) {
+    return E.sp == 16 ? launch_step_sp<16>(E, O, s) : launch_step_sp<32>(E, O, s);
 }
 
 }  // namespace merlin
