@@ -297,8 +297,7 @@ int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
     alloc((void **)&d.ep_ret, n * sizeof(double));
     alloc((void **)&d.ep_len, n * sizeof(int32_t));
     alloc((void **)&d.err, 2 * sizeof(uint32_t));
-    alloc((void **)&d.rlist, n * sizeof(int32_t));
-    alloc((void **)&d.rcount, sizeof(uint32_t));
+    alloc((void **)&d.rflag, n * sizeof(uint8_t));
     if (d.explore_on) alloc((void **)&d.visited, n * d.sp * sizeof(uint32_t));
     if (err != hipSuccess) {
         merlin_env_destroy(e);
@@ -311,7 +310,7 @@ int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
 int merlin_env_destroy(merlin_env *e) {
     if (!e) return MERLIN_OK;
     merlin::EnvDev &d = e->dev;
-    void *ptrs[] = {d.walls, d.agent, d.rng_s, d.rng_i, d.rng_b, d.ep_ret, d.ep_len, d.err, d.visited, d.rlist, d.rcount};
+    void *ptrs[] = {d.walls, d.agent, d.rng_s, d.rng_i, d.rng_b, d.ep_ret, d.ep_len, d.err, d.visited, d.rflag};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete e;

@@ -549,19 +549,39 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
     reset_one<SP>(E, i, rows, lane, obs);
 }
 
-// The auto-resets of a single-step launch, compacted: k_env_step appended the envs whose episode
-// ended to E.rlist, so the resets (rejection sampling + flood fill, thousands of cycles each) run
-// densely packed here instead of stalling a whole 64-env wave of the step kernel per reset.
+// The auto-resets of a single-step launch, out of the step kernel: k_env_step flagged the envs whose
+// episode ended (E.rflag), and here each one-wave block scans RS_SPAN x 64 envs, packs the flagged
+// ones onto consecutive lanes (ballot + prefix count) and regenerates them 64 at a time, so the map
+// generations (rejection sampling + flood fill, thousands of cycles each) run densely instead of
+// stalling a whole wave of the step kernel per reset.
+constexpr int RS_SPAN = 16;
 template <int SP>
 __global__ __launch_bounds__(BLK) void k_env_autoreset(EnvDev E, uint32_t *__restrict__ obs) {
     __shared__ uint32_t rows[SP][BLK];
+    __shared__ int queue[BLK];
     const int lane = threadIdx.x;
-    const uint32_t cnt = *E.rcount;
-    for (uint32_t j = blockIdx.x * BLK + lane; j < cnt; j += gridDim.x * BLK) reset_one<SP>(E, E.rlist[j], rows, lane, obs);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int nq = 0;  // wave-uniform
+    for (int g = 0; g < RS_SPAN; g++) {
+        const int64_t i = ((int64_t)blockIdx.x * RS_SPAN + g) * BLK + lane;
+        const bool need = i < E.n && E.rflag[i];
+        const unsigned long long m = __ballot(need);
+        const int c = __popcll(m);
+        if (c == 0) continue;
+        if (nq + c > BLK) {  // the queue is full: run it first
+            if (lane < nq) reset_one<SP>(E, queue[lane], rows, lane, obs);
+            nq = 0;
+            __syncthreads();
+        }
+        if (need) queue[nq + __popcll(m & below)] = (int)i;
+        nq += c;
+        __syncthreads();
+    }
+    if (lane < nq) reset_one<SP>(E, queue[lane], rows, lane, obs);
 }
 
-// DEFER (single-step launches with auto-reset): an env whose episode ends is appended to E.rlist
-// and k_env_autoreset, launched next on the stream, regenerates it and writes its observation; the
+// DEFER (single-step launches with auto-reset): an env whose episode ends is flagged in E.rflag and
+// k_env_autoreset, launched next on the stream, regenerates it and writes its observation; the
 // step kernel then writes neither that obs row nor the env's state.
 template <int SP, bool DEFER>
 __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
@@ -635,10 +655,12 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
             if (O.ep_ret_out) O.ep_ret_out[row] = ep_ret;
             if (O.ep_len_out) O.ep_len_out[row] = ep_len;
         }
-        if (DEFER && done) {  // O.autoreset, n_steps == 1
-            E.rlist[atomicAdd(E.rcount, 1u)] = i;
-            if (err) atomicOr(E.err, err);
-            return;
+        if (DEFER) {  // O.autoreset, n_steps == 1
+            E.rflag[i] = done ? 1 : 0;
+            if (done) {
+                if (err) atomicOr(E.err, err);
+                return;
+            }
         }
         if (done && O.autoreset) {
             if (!rng_loaded || E.reseed) {
@@ -690,13 +712,11 @@ hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs,
 template <int SP>
 static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t s) {
     const dim3 grid((E.n + SBLK - 1) / SBLK), block(SBLK);
-    if (O.autoreset && O.n_steps == 1) {  // resets deferred to the compacted k_env_autoreset
-        hipError_t e = hipMemsetAsync(E.rcount, 0, sizeof(uint32_t), s);
-        if (e != hipSuccess) return e;
+    if (O.autoreset && O.n_steps == 1) {  // resets deferred to the packed k_env_autoreset
         hipLaunchKernelGGL((k_env_step<SP, true>), grid, block, 0, s, E, O);
-        e = hipGetLastError();
+        hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        const int rgrid = std::min((E.n + BLK - 1) / BLK, 2048);
+        const int rgrid = (E.n + BLK * RS_SPAN - 1) / (BLK * RS_SPAN);
         hipLaunchKernelGGL(k_env_autoreset<SP>, dim3(rgrid), dim3(BLK), 0, s, E, O.obs);
     } else {
         hipLaunchKernelGGL((k_env_step<SP, false>), grid, block, 0, s, E, O);

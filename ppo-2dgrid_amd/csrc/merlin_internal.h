@@ -20,8 +20,8 @@ namespace merlin {
 //   ep_len  int32[n]
 //   visited uint32[n][SP]   exploration-bonus visit bitmask (only if enabled)
 //   err     uint32[2]       device error bits, fallback-map counter
-//   rlist   int32[n]        envs whose episode ended in the last single-step launch (auto-reset
-//   rcount  uint32[1]       deferred to k_env_autoreset), and their count
+//   rflag   uint8[n]        1 = the env's episode ended in the last single-step launch (its
+//                           auto-reset is deferred to k_env_autoreset)
 struct EnvDev {
     int n, size, sp, difficulty, max_steps;
     int stuck_on, max_stay;
@@ -38,8 +38,7 @@ struct EnvDev {
     int32_t *ep_len;
     uint32_t *visited;
     uint32_t *err;
-    int32_t *rlist;
-    uint32_t *rcount;
+    uint8_t *rflag;
 };
 
 struct StepOut {
