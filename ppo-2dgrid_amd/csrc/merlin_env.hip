@@ -367,8 +367,8 @@ struct GenOut {
 };
 
 template <int SP, int NB>
-__device__ __noinline__ void generate_map(uint32_t (*rows)[NB], int lane, int S, int difficulty, Rng &r,
-                                          uint32_t *fallbacks, GenOut &o) {
+__device__ __forceinline__ void generate_map_inl(uint32_t (*rows)[NB], int lane, int S, int difficulty, Rng &r,
+                                                 uint32_t *fallbacks, GenOut &o) {
     Grid<SP, NB> G;
     G.rows = rows;
     G.lane = lane;
@@ -381,6 +381,13 @@ __device__ __noinline__ void generate_map(uint32_t (*rows)[NB], int lane, int S,
     o.gx = G.gx;
     o.gy = G.gy;
     o.err = G.err;
+}
+
+// out of line for the multi-step kernel, whose step state must stay in registers across a reset
+template <int SP, int NB>
+__device__ __noinline__ void generate_map(uint32_t (*rows)[NB], int lane, int S, int difficulty, Rng &r,
+                                          uint32_t *fallbacks, GenOut &o) {
+    generate_map_inl<SP, NB>(rows, lane, S, difficulty, r, fallbacks, o);
 }
 
 __device__ __forceinline__ uint32_t bitrev7(uint32_t v) { return __brev(v) >> 25; }
@@ -525,7 +532,7 @@ __device__ __forceinline__ void reset_one(const EnvDev &E, int i, uint32_t (*row
                                           uint32_t *__restrict__ obs) {
     Rng r = load_rng(E, i);
     GenOut g;
-    generate_map<SP, BLK>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
+    generate_map_inl<SP, BLK>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
     if (!E.reseed) store_rng(E, i, r);
     store_rows<SP, BLK>(E, i, rows, lane, E.size);
     E.agent[i] = pack_agent(g.ax, g.ay, g.dir, 0, g.gx, g.gy, g.ax, g.ay, 0);
