@@ -557,8 +557,9 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
 }
 
 // The auto-resets of a single-step launch, out of the step kernel: k_env_step flagged the envs whose
-// episode ended (E.rflag), and here each one-wave block scans RS_SPAN x 64 envs, packs the flagged
-// ones onto consecutive lanes (ballot + prefix count) and regenerates them 64 at a time, so the map
+// episode ended (E.rflag), and here each one-wave block takes RS_SPAN x 64 envs (lane l loads the
+// RS_SPAN flags of envs base + RS_SPAN*l .. in one 16-B load), packs the flagged ones onto
+// consecutive lanes (ballot + prefix count) and regenerates them 64 at a time, so the map
 // generations (rejection sampling + flood fill, thousands of cycles each) run densely instead of
 // stalling a whole wave of the step kernel per reset.
 constexpr int RS_SPAN = 16;
@@ -568,10 +569,22 @@ __global__ __launch_bounds__(BLK) void k_env_autoreset(EnvDev E, uint32_t *__res
     __shared__ int queue[BLK];
     const int lane = threadIdx.x;
     const unsigned long long below = (1ull << lane) - 1ull;
+    const int64_t base = ((int64_t)blockIdx.x * BLK + lane) * RS_SPAN;  // this lane's first env
+    uint32_t fl[RS_SPAN / 4] = {0u, 0u, 0u, 0u};
+    if (base + RS_SPAN <= E.n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(E.rflag + base);
+        fl[0] = v.x;
+        fl[1] = v.y;
+        fl[2] = v.z;
+        fl[3] = v.w;
+    } else {
+        for (int b = 0; b < RS_SPAN; b++)
+            if (base + b < E.n) fl[b >> 2] |= (uint32_t)E.rflag[base + b] << (8 * (b & 3));
+    }
     int nq = 0;  // wave-uniform
-    for (int g = 0; g < RS_SPAN; g++) {
-        const int64_t i = ((int64_t)blockIdx.x * RS_SPAN + g) * BLK + lane;
-        const bool need = i < E.n && E.rflag[i];
+#pragma unroll
+    for (int b = 0; b < RS_SPAN; b++) {
+        const bool need = (fl[b >> 2] >> (8 * (b & 3))) & 0xffu;
         const unsigned long long m = __ballot(need);
         const int c = __popcll(m);
         if (c == 0) continue;
@@ -580,7 +593,7 @@ __global__ __launch_bounds__(BLK) void k_env_autoreset(EnvDev E, uint32_t *__res
             nq = 0;
             __syncthreads();
         }
-        if (need) queue[nq + __popcll(m & below)] = (int)i;
+        if (need) queue[nq + __popcll(m & below)] = (int)(base + b);
         nq += c;
         __syncthreads();
     }
