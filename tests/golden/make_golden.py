@@ -19,6 +19,11 @@ Sources, per fixture:
                   torch.manual_seed: param checksums + act/evaluate outputs.
   update_ref.npz  one REFERENCE PPO.update (src/ppo.py:122-168) on a small
                   replay batch, with the randperm draws recorded for replay.
+  fomaml_ref.npz  the REFERENCE FOMAML.compute_loss (src/fomaml.py:110-156) and the
+                  per-task inner SGD step + query-gradient accumulation of
+                  meta_train_step (:158-212) on recorded support / query batches of
+                  3 tasks (the env-free part of a meta step; FOMAML is built with
+                  __new__ because its constructor needs minigrid).
 The reference code itself is never copied into the repo; only its outputs.
 """
 from __future__ import annotations
@@ -278,7 +283,87 @@ def gen_update():
     )
 
 
+def gen_fomaml():
+    import copy
+
+    import torch
+
+    _import_reference()
+    from src.actor_critic import CNNActorCritic
+    from src.fomaml import FOMAML
+
+    atlas = build_atlas()
+    G, K = 3, 24
+    rs = np.random.RandomState(21)
+    ref = FOMAML.__new__(FOMAML)  # the constructor builds a minigrid env; compute_loss needs none
+    ref.device = torch.device("cpu")
+    ref.gamma, ref.lam, ref.vf_coef, ref.ent_coef, ref.clip_eps = 0.995, 0.95, 0.5, 0.05, 0.2
+    lr_inner = 0.01
+    torch.manual_seed(0)
+    meta = CNNActorCritic((56, 56, 3), 3)
+    keys, sums0 = _param_checksums(meta)
+
+    def batch_of(policy):
+        codes = rs.randint(0, 4, size=(K + 1, 49)).astype(np.uint8)
+        codes[:, 45] = 4
+        imgs = torch.from_numpy(O.render(codes, atlas).astype(np.float32))
+        act = torch.from_numpy(rs.randint(0, 3, size=K).astype(np.int64))
+        with torch.no_grad():  # what collect_trajectory stores from policy.act (src/fomaml.py:73-86)
+            lp, _, v = policy.evaluate(imgs[:K], act)
+            _, _, last = policy.act(imgs[K:K + 1])
+        rew = ((rs.rand(K) < 0.15) * rs.rand(K)).astype(np.float32)
+        done = (rs.rand(K) < 0.1).astype(np.float32)
+        done[K // 2] = 1.0
+        b = {"obs": imgs[:K], "act": act, "rew": torch.from_numpy(rew), "val": v, "logp": lp,
+             "done": torch.from_numpy(done), "last_val": last}
+        return codes, b
+
+    rec = {"cfg": np.array([G, K], dtype=np.int64), "lr_inner": np.float64(lr_inner), "keys": keys, "sums0": sums0}
+    meta_grad = {n: torch.zeros_like(p) for n, p in meta.named_parameters()}
+    meta_sd = copy.deepcopy(meta.state_dict())
+    for g in range(G):
+        fast = copy.deepcopy(meta)
+        fast.load_state_dict(meta_sd)
+        sc, sb = batch_of(fast)
+        loss_s, st_s = ref.compute_loss(sb, fast)
+        inner = torch.optim.SGD(fast.parameters(), lr=lr_inner)
+        inner.zero_grad()
+        loss_s.backward()
+        torch.nn.utils.clip_grad_norm_(fast.parameters(), max_norm=0.5)
+        inner.step()
+        qc, qb = batch_of(fast)  # the query rollout runs the adapted policy
+        loss_q, st_q = ref.compute_loss(qb, fast)
+        fast.zero_grad()
+        loss_q.backward()
+        for n, p in fast.named_parameters():
+            meta_grad[n] += p.grad
+        for tag, c, b, loss, st in (("s", sc, sb, loss_s, st_s), ("q", qc, qb, loss_q, st_q)):
+            rec[f"t{g}_{tag}_codes"] = c
+            for k in ("act", "rew", "val", "logp", "done"):
+                rec[f"t{g}_{tag}_{k}"] = b[k].numpy()
+            rec[f"t{g}_{tag}_last_val"] = np.float32(b["last_val"].item())
+            rec[f"t{g}_{tag}_loss"] = np.float64(loss.item())
+            rec[f"t{g}_{tag}_stats"] = np.array([st[k] for k in ("pi_loss", "v_loss", "entropy", "kl", "clipfrac")])
+    # the meta gradient of meta_train_step before its clip / Adam (:205-209): sum / n_tasks; stored
+    # as per-parameter (norm, sum) and 256 fixed sampled elements per parameter
+    names, stats, idx, vals = [], [], [], []
+    for n, gsum in meta_grad.items():
+        gm = (gsum / G).reshape(-1).double()
+        names.append(n)
+        stats.append([gm.norm().item(), gm.sum().item()])
+        sel = np.sort(np.random.RandomState(len(names)).choice(gm.numel(), min(256, gm.numel()), replace=False))
+        idx.append(np.pad(sel, (0, 256 - sel.size), constant_values=-1))
+        vals.append(np.pad(gm.numpy()[sel], (0, 256 - sel.size)))
+    rec.update(grad_names=np.array(names), grad_stats=np.array(stats), grad_idx=np.array(idx, dtype=np.int64),
+               grad_vals=np.array(vals))
+    np.savez_compressed(os.path.join(HERE, "fomaml_ref.npz"), **rec)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # e.g. `make_golden.py gen_fomaml`: only the named fixtures
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     np.savez_compressed(os.path.join(HERE, "atlas.npz"), atlas=build_atlas())
     gen_rng()
     gen_maps()
@@ -286,4 +371,5 @@ if __name__ == "__main__":
     gen_gae()
     gen_cnn()
     gen_update()
+    gen_fomaml()
     print("golden fixtures written to", HERE)

@@ -109,3 +109,80 @@ def test_meta_step_matches_serial_reference(device):
         rel = ((a.grad - b.grad).norm().item()) / scale
         assert rel < 1e-4, (n, rel)
         assert (a - b).abs().max().item() <= 2 * 3e-4 + 1e-6, n
+
+
+def _fixture_batch(fx, tag, G, device):
+    """The fixture's per-task batches as merlin.fomaml's [k][tasks] batch dict (codes packed)."""
+    from test_windows import pack
+
+    codes = np.stack([pack(fx[f"t{g}_{tag}_codes"]) for g in range(G)], 1)  # [k+1, G, 8]
+    b = {"codes": torch.from_numpy(codes).to(device)}
+    for k in ("act", "rew", "val", "logp", "done"):
+        b[k] = torch.from_numpy(np.stack([fx[f"t{g}_{tag}_{k}"] for g in range(G)], 1)).to(device)
+    b["last_val"] = torch.tensor([float(fx[f"t{g}_{tag}_last_val"]) for g in range(G)], device=device)
+    return b
+
+
+def test_loss_and_meta_gradient_match_reference_fixture(golden, device):
+    """Pinned to the reference itself (tests/golden/fomaml_ref.npz, made by importing
+    src/fomaml.py): per task, compute_loss (src/fomaml.py:110-156) on the recorded support batch,
+    the clipped inner SGD step, compute_loss on the recorded query batch with the adapted weights,
+    and the meta gradient sum/n_tasks (:158-209), all through merlin.fomaml's batched path (HIP GAE,
+    stacked per-task weights).  Tolerances: fp32 sums in another order (losses 1e-5 relative,
+    gradients 1e-4 of each parameter's norm)."""
+    from merlin import ScenarioCreator
+    from merlin import batched_policy as bp
+    from merlin.fomaml import FOMAML
+
+    fx = golden("fomaml_ref")
+    G, K = (int(x) for x in fx["cfg"])
+    torch.manual_seed(0)  # the reference's init order: the same weights (cnn_ref checks it)
+    fm = FOMAML(ScenarioCreator(), lr_inner=float(fx["lr_inner"]), lr_outer=3e-4, device=device,
+                difficulty="mediumhard")
+    names = [n for n, _ in fm.meta_policy.named_parameters()]
+    support, query = _fixture_batch(fx, "s", G, device), _fixture_batch(fx, "q", G, device)
+    fast = bp.stack_params(fm.meta_policy, G)
+    loss_s, st_s = fm.compute_loss(support, fast)
+    keys = ("pi_loss", "v_loss", "entropy", "kl", "clipfrac")
+    for g in range(G):
+        assert abs(float(st_s["loss"][g]) - float(fx[f"t{g}_s_loss"])) <= 1e-5 * max(1.0, abs(float(fx[f"t{g}_s_loss"])))
+        for j, k in enumerate(keys):
+            assert abs(float(st_s[k][g]) - float(fx[f"t{g}_s_stats"][j])) <= 1e-5, (g, k)
+    grads = dict(zip(names, torch.autograd.grad(loss_s, [fast[n] for n in names])))
+    grads, _ = fm._clip_per_task(grads, 0.5)
+    with torch.no_grad():
+        adapted = {n: (fast[n] - fm.lr_inner * grads[n]).detach().requires_grad_(True) for n in names}
+    loss_q, st_q = fm.compute_loss(query, adapted)
+    for g in range(G):
+        assert abs(float(st_q["loss"][g]) - float(fx[f"t{g}_q_loss"])) <= 1e-5 * max(1.0, abs(float(fx[f"t{g}_q_loss"])))
+        for j, k in enumerate(keys):
+            assert abs(float(st_q[k][g]) - float(fx[f"t{g}_q_stats"][j])) <= 1e-5, (g, k)
+    qgrads = dict(zip(names, torch.autograd.grad(loss_q, [adapted[n] for n in names])))
+    assert list(fx["grad_names"]) == names
+    gnorm = float(np.sqrt((fx["grad_stats"][:, 0] ** 2).sum()))
+    for i, n in enumerate(names):
+        gm = (qgrads[n].sum(0) / G).reshape(-1).double().cpu()
+        ref_norm = float(fx["grad_stats"][i, 0])
+        scale = max(ref_norm, 1e-3 * gnorm)
+        assert abs(gm.norm().item() - ref_norm) <= 1e-4 * scale, n
+        sel = fx["grad_idx"][i]
+        sel = sel[sel >= 0]
+        err = (gm[torch.from_numpy(sel)] - torch.from_numpy(fx["grad_vals"][i][:sel.size])).abs().max().item()
+        assert err <= 1e-4 * scale, (n, err, scale)
+
+
+def test_meta_step_at_cfg5_size(device):
+    """BASELINE cfg 5 at its stated size: 32 tasks x 256 support + 256 query steps through
+    meta_train_step (batched rollouts, inner SGD, meta Adam): finite outputs, parameters move."""
+    from merlin import ScenarioCreator
+    from merlin.fomaml import FOMAML
+
+    torch.manual_seed(1)
+    fm = FOMAML(ScenarioCreator(), lr_inner=0.01, lr_outer=3e-4, device=device, difficulty="mediumhard")
+    p0 = [p.detach().clone() for p in fm.meta_policy.parameters()]
+    seeds = np.random.RandomState(42).choice(100000, 32, replace=False)
+    avg_loss, avg_rew, avg_steps, stats = fm.meta_train_step(seeds, k_support=256, k_query=256)
+    assert np.isfinite(avg_loss) and np.isfinite(avg_rew) and 0 < avg_steps <= 1024
+    assert all(np.isfinite(v) for v in stats.values())
+    moved = sum(int((a != b).any()) for a, b in zip(p0, fm.meta_policy.parameters()))
+    assert moved == len(p0)
