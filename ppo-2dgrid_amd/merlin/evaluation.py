@@ -1,41 +1,85 @@
-"""Batched deterministic evaluation (ppo/ppo_train.py:43-69 evaluate_policy of the reference).
+"""Batched deterministic evaluation and the checkpoint sweep.
 
-The reference resets its eval env with ``seed = base_seed + ep`` for ep < episodes and runs
-each episode to termination/truncation with the argmax policy, one env step per forward.
-Here all episodes run at once as one ``MerlinVecEnv`` (env ep seeded base_seed + ep, the
-same maps), one batched deterministic forward per step, no auto-reset; finished envs keep
-stepping but their results are frozen at their first done.
+``evaluate_policy``  ppo/ppo_train.py:43-69 of the reference: episode ep is reset with
+                     ``seed = base_seed + ep`` and run to termination/truncation with the argmax
+                     policy.  Here all episodes run at once in one ``MerlinVecEnv`` (env ep seeded
+                     base_seed + ep: the same maps), one batched deterministic forward per step, no
+                     auto-reset; an env's result is frozen at its first done.  Episode returns are
+                     the env's f64 accumulator (the reference sums Python floats), not a sum of the
+                     f32 reward buffer.
+``evaluate_seeds``   the same for an arbitrary list of seeds (src/sweep_checkpoints.py:52-70
+                     evaluate_model: one episode per seed, returns the mean reward and steps).
+``sweep_checkpoints`` src/sweep_checkpoints.py:72-100: every ``*.pth`` of a directory on the fixed
+                     seeds 200000 + i, ranked by mean reward; checkpoints load through
+                     merlin.checkpoints.load_policy (legacy-key remap included).
 """
 from __future__ import annotations
+
+import glob
+import os
 
 import torch
 
 from .envs import MerlinVecEnv
 
+SWEEP_SEED_BASE = 200000  # src/sweep_checkpoints.py:79
+
 
 @torch.no_grad()
-def evaluate_policy(ac, difficulty: str = "mediumhard", episodes: int = 3, seed: int | None = None,
-                    size: int = 16, device="cuda", max_steps: int | None = None, **env_flags):
-    """Returns (rewards list[float], steps list[int]) like the reference's evaluate_policy."""
-    base = 0 if seed is None else int(seed)
-    env = MerlinVecEnv(episodes, difficulty=difficulty, size=size, seed=base, device=device,
-                       max_steps=max_steps, **env_flags)
+def evaluate_seeds(ac, seeds, difficulty: str = "mediumhard", size: int = 16, device="cuda",
+                   max_steps: int | None = None, record: bool = False, **env_flags):
+    """One deterministic episode per seed, all at once -> (rewards list[float], steps list[int])
+    [+ actions int64[T, n] when record: the actions taken, for replay checks]."""
+    seeds = [int(s) for s in seeds]
+    n = len(seeds)
+    env = MerlinVecEnv(n, difficulty=difficulty, size=size, device=device, max_steps=max_steps, seeds=seeds,
+                       **env_flags)
     try:
         obs = env.reset().clone()
-        n = episodes
         total = torch.zeros(n, dtype=torch.float64, device=env.device)
         steps = torch.zeros(n, dtype=torch.int64, device=env.device)
         done = torch.zeros(n, dtype=torch.bool, device=env.device)
+        acts = []
         for _ in range(env.max_steps):
             action, _, _ = ac.act_codes(obs, deterministic=True)
-            obs, rew, term, trunc, _ = env.step(action, autoreset=False)
+            obs, _, term, trunc, info = env.step(action, autoreset=False)
+            if record:
+                acts.append(action.clone())
             live = ~done
-            total += torch.where(live, rew.double(), torch.zeros_like(total))
+            fin = live & (term | trunc)
+            total = torch.where(fin, info["episode_return"], total)
             steps += live.long()
             done |= term | trunc
             if bool(done.all()):
                 break
         env.errors()
-        return total.cpu().tolist(), steps.cpu().tolist()
+        out = (total.cpu().tolist(), steps.cpu().tolist())
+        if record:
+            out = out + (torch.stack(acts).cpu(),)
+        return out
     finally:
         env.close()
+
+
+def evaluate_policy(ac, difficulty: str = "mediumhard", episodes: int = 3, seed: int | None = None,
+                    size: int = 16, device="cuda", max_steps: int | None = None, **env_flags):
+    """Returns (rewards list[float], steps list[int]) like the reference's evaluate_policy."""
+    base = 0 if seed is None else int(seed)
+    return evaluate_seeds(ac, range(base, base + episodes), difficulty=difficulty, size=size, device=device,
+                          max_steps=max_steps, **env_flags)
+
+
+def sweep_checkpoints(model_dir: str, difficulty: str = "mediumhard", tasks: int = 50, size: int = 16,
+                      device="cuda", **env_flags):
+    """[(path, mean reward, mean steps)] of every *.pth in model_dir, best first
+    (src/sweep_checkpoints.py:72-100)."""
+    from .checkpoints import load_policy
+
+    seeds = range(SWEEP_SEED_BASE, SWEEP_SEED_BASE + tasks)
+    results = []
+    for path in sorted(glob.glob(os.path.join(model_dir, "*.pth"))):
+        policy = load_policy(path, device)
+        rew, st = evaluate_seeds(policy, seeds, difficulty=difficulty, size=size, device=device, **env_flags)
+        results.append((path, sum(rew) / len(rew), sum(st) / len(st)))
+    results.sort(key=lambda r: r[1], reverse=True)
+    return results

@@ -90,6 +90,32 @@ class ScalarLog:
         else:
             self.f.write(json.dumps({"tag": tag, "value": float(value), "step": int(step)}) + "\n")
 
+    def add_histogram(self, tag, values, step):
+        values = np.asarray(values, dtype=np.float64)
+        if self.tb is not None:
+            self.tb.add_histogram(tag, values, step)
+        else:
+            counts, edges = np.histogram(values, bins=min(30, max(1, values.size)))
+            self.f.write(json.dumps({"tag": tag, "histogram": {"counts": counts.tolist(), "edges": edges.tolist()},
+                                     "step": int(step)}) + "\n")
+
+    def add_reward_vs_steps(self, tag, lengths, returns, step):
+        """The reference's scatter figure (ppo/ppo_train.py:186-190): a matplotlib figure in
+        TensorBoard, the raw points in the JSONL stand-in."""
+        if self.tb is not None:
+            import matplotlib
+
+            matplotlib.use("Agg")
+            import matplotlib.pyplot as plt
+
+            fig = plt.figure()
+            plt.scatter(lengths, returns, c="green")
+            self.tb.add_figure(tag, fig, step)
+            plt.close(fig)
+        else:
+            self.f.write(json.dumps({"tag": tag, "points": [[float(a), float(b)] for a, b in zip(lengths, returns)],
+                                     "step": int(step)}) + "\n")
+
     def close(self):
         if self.tb is not None:
             self.tb.close()
@@ -177,6 +203,11 @@ def train_minigrid(args):
                   f"V: {update_stats['v_loss']:.4f} | Ent: {update_stats['entropy']:.4f} | "
                   f"KL: {update_stats['kl']:.6f} | Steps: {avg_s:.1f} | T: {elapsed_min:.2f}m | {sps:,.0f} steps/s",
                   flush=True)
+            if len(agent.episode_returns) >= 10:  # ppo/ppo_train.py:184-190
+                writer.add_histogram("hist/episode_rewards", agent.episode_returns[-50:], step_count)
+                writer.add_histogram("hist/episode_lengths", agent.episode_lengths[-50:], step_count)
+                writer.add_reward_vs_steps("fig/reward_vs_steps", agent.episode_lengths[-50:],
+                                           agent.episode_returns[-50:], step_count)
     if lead:
         torch.save(agent.ac.state_dict(), os.path.join(ckpt_subdir, "ppo_model_final.pth"))
         writer.close()

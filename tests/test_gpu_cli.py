@@ -34,6 +34,35 @@ def test_cli_vectorised_run_writes_reference_layout(tmp_path, monkeypatch, devic
     assert (tmp_path / "tb_logs").exists()
 
 
+def test_cli_cfg1_single_env_reference_run(tmp_path):
+    """BASELINE cfg 1, the reference's own CPU-runnable plumbing config, end to end as a user runs it:
+    `ppo_train.py --num_envs 1 --difficulty mediumhard --seed 777 --total_steps 10000` (the loop of
+    ppo/ppo_train.py:112-196: 5 iterations of a 2048-step single-env rollout, 10 epochs x 8 minibatches
+    of 256, a 3-episode deterministic eval per iteration, best / milestone / final checkpoints)."""
+    import json
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ppo-2dgrid_amd",
+                          "ppo_train.py")
+    r = subprocess.run([sys.executable, script, "--difficulty", "mediumhard", "--seed", "777", "--total_steps",
+                        "10000", "--num_envs", "1", "--device", "cuda", "--group_timestamp", "CFG1"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("[")]
+    assert len([ln for ln in lines if "R:" in ln]) == 5, r.stdout[-2000:]  # 5 x 2048 >= 10000
+    assert lines[-1].startswith("[  10240]")
+    d = tmp_path / "checkpoints" / "MERLIN-MediumHard-v0_16x16_mediumhard_CFG1" / "seed_777"
+    names = set(os.listdir(d))
+    assert {"best_model.pth", "ppo_model_10k.pth", "ppo_model_final.pth"} <= names
+    sd = torch.load(d / "ppo_model_final.pth", weights_only=True)
+    assert "actor_extractor.network.0.weight" in sd and "critic.2.bias" in sd
+    tb = tmp_path / "tb_logs" / "MERLIN-MediumHard-v0_16x16_mediumhard_CFG1" / "seed_777"
+    if (tb / "scalars.jsonl").exists():  # no tensorboard in the image: the JSONL stand-in
+        tags = {json.loads(ln)["tag"] for ln in open(tb / "scalars.jsonl")}
+        assert {"reward/avg_eval_reward", "loss/policy_loss", "diagnostics/gradnorm"} <= tags
+
+
 def test_batched_eval_matches_serial_single_env(device):
     from merlin import MerlinEnv
     from merlin.actor_critic import CNNActorCritic
