@@ -262,6 +262,7 @@ class PPO:
             buf = self.buf
             lv = buf.last_value if last_value is None else last_value
             adv_n, ret = self._advantages(buf.rewards, buf.values, buf.dones, lv, buf.adv, buf.returns)
+            self.last_adv_normalized = adv_n  # [T][N], for inspection (the update reads it flat)
             B = buf.T * buf.N
             return self._sgd(B, buf.flat_codes, None, buf.actions.reshape(B), buf.logprobs.reshape(B),
                              adv_n.reshape(B), ret.reshape(B))

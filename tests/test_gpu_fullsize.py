@@ -1,0 +1,63 @@
+"""GPU: the benched update path at the bench's own size (cfg 2: 4096 envs x 256 steps, 8 minibatches of
+131,072, windows over the whole rollout) against the per-frame lookup path on the same rollout: the
+first optimizer step's gradient of every parameter, the update metrics and the parameters after one
+epoch (8 optimizer steps).  Tolerances as tests/test_gpu_windows.py (fp32 sums regrouped)."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fullsize_window_update_matches_lookup_path(device):
+    from merlin import MerlinVecEnv
+    from merlin.ppo import PPO
+
+    N, T, MB = 4096, 256, 8
+    B = N * T
+    env = MerlinVecEnv(N, "mediumhard", seed=777, device=device)
+    torch.manual_seed(777)
+    g = torch.Generator(device=device)
+    perm = None
+
+    def perm_fn(n, epoch):
+        return perm
+
+    agent = PPO(env, batch_size=B, minibatch_size=B // MB, update_epochs=1, ent_coef=0.05, device=device,
+                perm_fn=perm_fn)
+    lv = agent.collect_rollouts()
+    g.manual_seed(11)
+    perm = torch.randperm(B, device=device, generator=g)
+    sd0 = copy.deepcopy(agent.ac.state_dict())
+    opt0 = copy.deepcopy(agent.optimizer.state_dict())
+    results = []
+    for windows in (True, False):
+        agent.ac.load_state_dict(sd0)
+        agent.optimizer.load_state_dict(opt0)
+        agent.windows = windows
+        first = []
+        orig_step = agent.optimizer.step
+
+        def step(*a, **k):
+            if not first:
+                first.append([p.grad.detach().clone() for p in agent._params])
+            return orig_step(*a, **k)
+
+        agent.optimizer.step = step
+        stats = agent.update(lv)
+        agent.optimizer.step = orig_step
+        results.append((stats, first[0], [p.detach().clone() for p in agent.ac.parameters()],
+                        agent.last_num_windows if windows else None, agent.last_distinct_frac))
+    (s1, g1, p1, nw, frac), (s2, g2, p2, _, _) = results
+    assert nw is not None and nw > 1000 and 0.1 < frac <= 1.0, (nw, frac)
+    for (name, _), a, b in zip(agent.ac.named_parameters(), g1, g2):
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+        assert rel < 1e-4, (name, rel)
+    for k in s1:
+        tol = 4.0 / (B // MB) if k == "clipfrac" else 1e-4 * max(1.0, abs(s2[k]))
+        assert abs(s1[k] - s2[k]) <= tol, (k, s1[k], s2[k])
+    ds = [(a - b).abs().flatten() for a, b in zip(p1, p2)]
+    for d in ds:
+        assert d.max().item() <= 2 * 3e-4 * MB
+    assert (torch.cat(ds) > 5e-5).float().mean().item() < 0.05
