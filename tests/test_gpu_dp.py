@@ -84,11 +84,13 @@ def test_two_rank_ppo_equals_one_process_over_concatenated_envs(device, tmp_path
     agent = _agent(env)
     lv = agent.collect_rollouts()
     buf = agent.buf
-    for r in range(2):  # the rank's rollout is its columns of the single run, bit for bit
+    for r in range(2):  # the rank's rollout is its columns of the single run
         for k, v in res[r]["roll"].items():
-            full = getattr(buf, k).cpu()
-            cols = full[:, r * N:(r + 1) * N] if full.dim() >= 2 else full
-            assert torch.equal(v, cols), (r, k)
+            cols = getattr(buf, k).cpu()[:, r * N:(r + 1) * N]
+            if k in ("logprobs", "values"):  # the policy GEMMs run at another batch size: fp32 order
+                torch.testing.assert_close(v, cols, rtol=1e-5, atol=1e-5)
+            else:  # observations, actions, rewards, dones: bit for bit
+                assert torch.equal(v, cols), (r, k)
     stats = agent.update(lv)
     # global-moment normalisation: each rank's advantages == the single run's columns
     for r in range(2):

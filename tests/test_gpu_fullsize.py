@@ -51,9 +51,16 @@ def test_fullsize_window_update_matches_lookup_path(device):
                         agent.last_num_windows if windows else None, agent.last_distinct_frac))
     (s1, g1, p1, nw, frac), (s2, g2, p2, _, _) = results
     assert nw is not None and nw > 1000 and 0.1 < frac <= 1.0, (nw, frac)
+    bad = []
     for (name, _), a, b in zip(agent.ac.named_parameters(), g1, g2):
         rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
-        assert rel < 1e-4, (name, rel)
+        # conv1's weight gradient is the longest reduction (131,072 samples x 169 positions per
+        # tower, ~2.2e7 fp32 terms with cancellation): its summation-order noise is ~sqrt(2.2e7) x
+        # 6e-8 ~ 3e-4 of the terms' magnitude; every other tensor keeps test_gpu_windows' 1e-4
+        tol = 5e-4 if name.endswith("network.0.weight") else 1e-4
+        if rel >= tol:
+            bad.append((name, rel))
+    assert not bad, bad
     for k in s1:
         tol = 4.0 / (B // MB) if k == "clipfrac" else 1e-4 * max(1.0, abs(s2[k]))
         assert abs(s1[k] - s2[k]) <= tol, (k, s1[k], s2[k])
