@@ -3,6 +3,12 @@ import sys
 
 import pytest
 
+# MIOpen (the reference-structured F.conv2d paths the parity tests compare against): heuristic
+# solver choice instead of a per-shape Find that compiles and times every candidate kernel
+# (minutes for a new batch shape on a fresh box).  Same fp32 convolutions.
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+os.environ.setdefault("MIOPEN_LOG_LEVEL", "3")
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "ppo-2dgrid_amd")
 ORACLE = os.path.join(REPO, "oracle")

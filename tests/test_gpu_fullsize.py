@@ -10,6 +10,40 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+def _first_step_grad(agent, sd0, mb, dtype):
+    """The first optimizer step's (clipped) gradient through the reference-structured frame path
+    (the rendered frames through the F.conv2d towers), the loss of src/ppo.py:136-150 on minibatch
+    mb and clip_grad_norm_(0.5) (src/ppo.py:155), in `dtype` (float64: the yardstick; float32: the
+    reference's own formulation and precision)."""
+    from merlin import _native as nat
+    from merlin.actor_critic import CNNActorCritic
+
+    ac = CNNActorCritic((56, 56, 3), 3).to(agent.device)
+    ac.load_state_dict(sd0)
+    ac.to(dtype)
+    buf = agent.buf
+    B = buf.T * buf.N
+    frames = nat.expand_obs(buf.flat_codes, index=mb, scale=1.0 / 255.0).to(dtype)
+    acts = buf.actions.reshape(B)[mb]
+    lp_old = buf.logprobs.reshape(B)[mb].to(dtype)
+    adv = agent.last_adv_normalized.reshape(B)[mb].to(dtype)
+    ret = buf.returns.reshape(B)[mb].to(dtype)
+    logits = ac.actor(ac.actor_extractor(frames, prescaled=True))  # (evaluate() casts its input to f32)
+    v = ac.critic(ac.critic_extractor(frames, prescaled=True)).squeeze(-1)
+    del frames
+    logp_all = logits.log_softmax(-1)
+    lp = logp_all.gather(-1, acts[:, None]).squeeze(-1)
+    ent = -(logp_all.exp() * logp_all).sum(-1)
+    ratio = torch.exp(lp - lp_old)
+    pi = -torch.min(ratio * adv, torch.clamp(ratio, 0.8, 1.2) * adv).mean()
+    loss = pi + 0.5 * ((v - ret) ** 2).mean() - 0.05 * ent.mean()
+    loss.backward()
+    grads = [p.grad for p in ac.parameters()]
+    norm = torch.sqrt(sum((g ** 2).sum() for g in grads))
+    coef = torch.clamp(0.5 / (norm + 1e-6), max=1.0)
+    return [g * coef for g in grads]
+
+
 def test_fullsize_window_update_matches_lookup_path(device):
     from merlin import MerlinVecEnv
     from merlin.ppo import PPO
@@ -50,17 +84,21 @@ def test_fullsize_window_update_matches_lookup_path(device):
         results.append((stats, first[0], [p.detach().clone() for p in agent.ac.parameters()],
                         agent.last_num_windows if windows else None, agent.last_distinct_frac))
     (s1, g1, p1, nw, frac), (s2, g2, p2, _, _) = results
-    assert nw is not None and nw > 1000 and 0.1 < frac <= 1.0, (nw, frac)
-    bad = []
-    for (name, _), a, b in zip(agent.ac.named_parameters(), g1, g2):
-        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
-        # conv1's weight gradient is the longest reduction (131,072 samples x 169 positions per
-        # tower, ~2.2e7 fp32 terms with cancellation): its summation-order noise is ~sqrt(2.2e7) x
-        # 6e-8 ~ 3e-4 of the terms' magnitude; every other tensor keeps test_gpu_windows' 1e-4
-        tol = 5e-4 if name.endswith("network.0.weight") else 1e-4
-        if rel >= tol:
-            bad.append((name, rel))
+    # gradients: each fp32 path against float64, as close as the reference's own fp32 formulation
+    # (the frame path, F.conv2d) is: summation-order noise at this size reaches ~3e-4 on the actor
+    # tower (near-uniform policy: the policy-gradient terms cancel), so a fixed 1e-4 between two
+    # fp32 paths would fail on fp32 itself
+    print("update paths done; float64 / float32 frame-path gradients", flush=True)
+    g64 = _first_step_grad(agent, sd0, perm[: B // MB], torch.float64)
+    print("float64 done", flush=True)
+    g32 = _first_step_grad(agent, sd0, perm[: B // MB], torch.float32)
+    rel = lambda a, b: ((a.double() - b).norm() / b.norm().clamp_min(1e-30)).item()  # noqa: E731
+    table = [(name, rel(a, r), rel(b, r), rel(f, r))
+             for (name, _), a, b, f, r in zip(agent.ac.named_parameters(), g1, g2, g32, g64)]
+    print("\n".join(f"{n:40s} windows {x:.2e} lookup {y:.2e} frames-fp32 {z:.2e}" for n, x, y, z in table))
+    bad = [t for t in table if t[1] > max(2 * t[3], 1e-5) or t[2] > max(2 * t[3], 1e-5)]
     assert not bad, bad
+    assert nw is not None and nw > 1000 and 0.1 < frac <= 1.0, (nw, frac)
     for k in s1:
         tol = 4.0 / (B // MB) if k == "clipfrac" else 1e-4 * max(1.0, abs(s2[k]))
         assert abs(s1[k] - s2[k]) <= tol, (k, s1[k], s2[k])
