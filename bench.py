@@ -109,6 +109,30 @@ def fomaml_bench(args):
                                              f"k_steps={args.k_steps}"}}), flush=True)
 
 
+def fomaml_tier(device, difficulty, tasks=32, k=256, warmup=1, steps=1):
+    """BASELINE cfg 5 inside the default run: meta-iterations of 32 tasks x (256 support + 256
+    query) env steps with the inner SGD step and the meta Adam step (merlin.fomaml, batched over
+    tasks); env-steps/s of the meta step."""
+    import torch
+
+    from merlin import ScenarioCreator
+    from merlin.fomaml import FOMAML
+
+    torch.manual_seed(42)
+    fm = FOMAML(ScenarioCreator(), lr_inner=0.01, lr_outer=3e-4, device=device, difficulty=difficulty)
+    rs = np.random.RandomState(42)
+    for _ in range(warmup):
+        fm.meta_train_step(rs.choice(100000, tasks, replace=False), k_support=k, k_query=k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fm.meta_train_step(rs.choice(100000, tasks, replace=False), k_support=k, k_query=k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(steps * tasks * 2 * k / el, 1), "unit": "env-steps/s", "ms_per_meta_step":
+            round(el / steps * 1e3, 1), "config": f"tasks_per_batch={tasks} k_support=k_query={k}, {difficulty}"}
+
+
 def env_only_tier(torch, MerlinVecEnv, n, T, difficulty, size, device):
     """Tier E: env dynamics + obs codes only, actions pre-generated.
     (a) one launch steps all T steps with state on chip; (b) T single-step launches."""
@@ -177,60 +201,112 @@ def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=8
 
 
 def cpu_baseline():
-    """The oracle's CPU port of the reference loop (oracle/ppo_cpu.py), N=1 env,
-    batch 2048, 10 epochs x 8 minibatches of 256: one iteration (~5 s on 8 cores)."""
+    """The oracle's CPU port of the reference loop (oracle/ppo_cpu.py), N=1 env, batch 2048, 10 epochs x
+    8 minibatches of 256, plus the per-iteration 3-episode deterministic eval of ppo/ppo_train.py:150
+    (BASELINE.md's plan: counted env-steps / wall time without and with the eval; all host threads and
+    1 thread).  One iteration per thread count (~10 s with all threads, ~20-40 s on one)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import torch
 
     import ppo_cpu  # noqa: E402  (baseline leg only)
 
-    steps, secs = ppo_cpu.run_iterations(n_iter=1)
-    return {"value": round(steps / secs, 2), "unit": "env-steps/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": "1 PPO iteration of the reference loop on CPU: 1 mediumhard 16x16 env (C oracle + RGB "
-                      "render), batch 2048, 10 epochs x 8 minibatches of 256, fp32 torch CNN (cfg 1 shape)"}
+    threads = torch.get_num_threads()
+    steps, secs, secs_eval = ppo_cpu.run_iterations(n_iter=1, eval_episodes=3)
+    torch.set_num_threads(1)
+    try:
+        s1, t1, t1e = ppo_cpu.run_iterations(n_iter=1, eval_episodes=3)
+    finally:
+        torch.set_num_threads(threads)
+    return {"value": round(steps / secs, 2), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "value_with_eval": round(steps / secs_eval, 2),
+            "one_thread": {"value": round(s1 / t1, 2), "value_with_eval": round(s1 / t1e, 2), "cores": 1},
+            "sample": "1 PPO iteration of the reference loop on CPU per thread count: 1 mediumhard 16x16 env "
+                      "(C oracle + RGB render), batch 2048, 10 epochs x 8 minibatches of 256, fp32 torch CNN "
+                      "(cfg 1 shape); value_with_eval adds the 3-episode deterministic eval of "
+                      "ppo/ppo_train.py:150"}
 
 
 # bench names -> rocprofv3 kernel names: the dQ and dT2 segmented sums are one kernel; the
-# PMC summary keeps its largest-grid launches, which are the dQ ones (2048 blocks vs ~90)
+# PMC summary keeps its largest-grid launches, which are the dQ ones (2048 blocks vs ~90).  The
+# fc1 GEMMs are hipBLASLt kernels, matched by name prefix (largest grid = the update's, not the
+# rollout's); their PMC key is the full Tensile kernel name.
 PMC_ALIAS = {"k_seg_sum_dQ": "k_seg_sum"}
+PMC_PREFIX = {"gemm_fc1_fwd": "Cijk_Alik_Bljk_S_B_Bias_HA_S_SAV_UserArgs_MT128x128x64"}
+PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 
 
 def pmc_traffic(kernel: str):
-    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 --pmc passes
-    (profiles/*_pmc.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE)."""
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 --pmc passes of the same bench
+    command (profiles/*_pmc.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE)."""
     kernel = PMC_ALIAS.get(kernel, kernel)
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
+    files = [PMC_FILE] if PMC_FILE else sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True)
+    for f in files:
         try:
-            d = json.load(open(f)).get(kernel)
+            dd = json.load(open(f))
         except Exception:
             continue
+        d = dd.get(kernel)
+        if d is None and kernel in PMC_PREFIX:
+            cands = [v for k, v in dd.items() if k.startswith(PMC_PREFIX[kernel])]
+            d = max(cands, key=lambda v: v.get("grid", 0)) if cands else None
         if d and d.get("hbm_bytes_per_launch"):
             return d["hbm_bytes_per_launch"]
     return None
 
 
 def kernel_table(records):
-    """{name: (launches, total ms, avg us, algorithmic bytes per launch, GB/s)} from HIP events."""
+    """{name: launches, total ms, avg us, algorithmic bytes (GB/s) or flops (TFLOP/s) per launch}
+    from HIP events."""
     agg = {}
-    for name, e0, e1, nbytes in records:
+    for name, e0, e1, nbytes, flops in records:
         ms = e0.elapsed_time(e1)
-        a = agg.setdefault(name, [0, 0.0, 0])
+        a = agg.setdefault(name, [0, 0.0, 0, 0])
         a[0] += 1
         a[1] += ms
         a[2] += nbytes
+        a[3] += flops
     out = {}
-    for name, (cnt, ms, nb) in agg.items():
-        out[name] = {"launches": cnt, "total_ms": round(ms, 3), "avg_us": round(ms / cnt * 1e3, 2),
-                     "bytes_per_launch": nb // cnt, "gbs": round(nb / (ms / 1e3) / 1e9, 2)}
+    for name, (cnt, ms, nb, fl) in agg.items():
+        d = {"launches": cnt, "total_ms": round(ms, 3), "avg_us": round(ms / cnt * 1e3, 2)}
+        if fl:
+            d.update(flops_per_launch=fl // cnt, tflops=round(fl / (ms / 1e3) / 1e12, 2))
+        else:
+            d.update(bytes_per_launch=nb // cnt, gbs=round(nb / (ms / 1e3) / 1e9, 2))
+        out[name] = d
     return out
 
 
 def roofline_of(name, k):
     traffic = pmc_traffic(name)
+    if "tflops" in k:  # a hipBLASLt GEMM: f32 MFMA bound
+        return {"kernel": name, "bound": "mfma", "achieved": k["tflops"], "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(k["tflops"] / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "flops_per_launch": k["flops_per_launch"], "avg_launch_us": k["avg_us"], "launches": k["launches"]}
     return {"kernel": name, "bound": "hbm", "achieved": k["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(k["gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
             "bytes_per_launch": k["bytes_per_launch"], "avg_launch_us": k["avg_us"], "launches": k["launches"]}
+
+
+def floor_tier(agent, iters=1):
+    """The update without exploiting repeated observations (no distinct-frame grouping, no
+    receptive-field windows: every minibatch sample through the per-position lookup path), on the
+    agent's current state, after the timed region: env-steps/s of rollout + update."""
+    import torch
+
+    saved = (agent.dedup, agent.windows)
+    out = {}
+    try:
+        for name, (dedup, windows) in (("no_windows", (True, False)), ("no_dedup_no_windows", (False, False))):
+            agent.dedup, agent.windows = dedup, windows
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                agent.update(agent.collect_rollouts())
+            torch.cuda.synchronize()
+            out[name] = round(iters * agent.batch_size / (time.perf_counter() - t0), 1)
+    finally:
+        agent.dedup, agent.windows = saved
+    return out
 
 
 def heartbeat(state):
@@ -318,6 +394,7 @@ def main():
             dist.barrier()
         return
     dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
+    handwritten = max((k for k in kernels if k.startswith("k_")), key=lambda k: kernels[k]["total_ms"])
     ref_flop_per_step = 2 * FWD_MACS + args.epochs * 2 * (FWD_MACS + BWD_MACS)
     frac = agent.last_distinct_frac if agent.last_distinct_frac is not None else 1.0
     if agent.last_num_windows is not None:
@@ -339,13 +416,25 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic: procedurally generated mediumhard maps (numpy-PCG64-exact, seeds 777+i), "
-                "random-init CNNActorCritic",
+                "random-init CNNActorCritic (torch seed 777), timed after the warm-up iterations",
         "config": {"workload": f"{args.difficulty} {args.size}x{args.size}, {N} envs/GPU x k_steps {T}, "
                                f"{args.epochs} epochs x {args.minibatches} minibatches of {B // args.minibatches}",
                    "num_envs_per_gpu": N, "k_steps": T, "global_batch": B * world,
-                   "parallelism": f"dp{world}" if world > 1 else "single"},
-        # dominant hand-written kernel of the timed loop (by total HIP-event time)
+                   "parallelism": f"dp{world}" if world > 1 else "single",
+                   # the training state the number is measured at: the throughput depends on how many
+                   # distinct frames / windows the policy's rollouts hold (distinct_frames_per_sample)
+                   "state": f"iterations {args.warmup + 1}..{args.warmup + args.steps} of a run from random init "
+                            f"(seed 777)"},
+        # the number's data dependence: distinct observations per minibatch sample (1.0 = none repeat)
+        "distinct_frames_per_sample": (round(agent.last_distinct_frac, 4)
+                                       if agent.last_distinct_frac is not None else None),
+        # dominant kernel of the timed loop by total HIP-event time (hand-written kernels and the
+        # fc1 hipBLASLt GEMMs, which are timed the same way)
         "roofline": roofline_of(dominant, kernels[dominant]),
+        # dominant hand-written kernel
+        "roofline_handwritten": roofline_of(handwritten, kernels[handwritten]),
+        # every hipBLASLt GEMM family timed in the loop against the f32 MFMA peak
+        "roofline_gemm": {k: roofline_of(k, v) for k, v in kernels.items() if "tflops" in v},
         # the env-step kernel inside the timed loop (absent when the rollout replays as a graph:
         # no per-kernel events inside it); the HBM-scale measurement is tiers.env_only_2M_envs
         "roofline_env_step": roofline_of("k_env_step", kernels["k_env_step"]) if "k_env_step" in kernels else None,
@@ -358,9 +447,6 @@ def main():
                           "reference_flop_per_env_step": ref_flop_per_step,
                           "reference_equivalent_tflops": round(value / world * ref_flop_per_step / 1e12, 2)},
         "phases_ms": {"rollout": round(rollout_ms, 2), "update": round(update_ms, 2)},
-        # towers evaluated once per distinct observation of a minibatch (merlin/dedup.py)
-        "distinct_frames_per_sample": (round(agent.last_distinct_frac, 4)
-                                       if agent.last_distinct_frac is not None else None),
         # conv2/conv3 evaluated once per distinct receptive-field window (merlin/windows.py)
         "windows_per_update": agent.last_num_windows,
         "rollout_graph": agent._graph is not None,
@@ -368,12 +454,17 @@ def main():
     }
     state["phase"] = "tiers"
     if not args.no_tiers:
+        floors = floor_tier(agent)
         fused, single = env_only_tier(torch, MerlinVecEnv, N, T, args.difficulty, args.size, device)
         out["tiers"] = {"env_only_fused_T_steps_per_launch": round(fused, 1),
                         "env_only_one_step_per_launch": round(single, 1),
                         "rollout_only": round(B / (rollout_ms / 1e3), 1),
                         "env_only_2M_envs": env_large_tier(torch, MerlinVecEnv, args.difficulty, args.size, device),
-                        "full_loop_per_gpu": round(value / world, 1)}
+                        "full_loop_per_gpu": round(value / world, 1),
+                        # the same loop, one iteration each right after the timed region, with the
+                        # observation reuse switched off: the data-independent floor
+                        "full_loop_floor": floors,
+                        "fomaml": fomaml_tier(device, args.difficulty)}
     state["phase"] = "cpu_baseline"
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()

@@ -75,9 +75,23 @@ class CpuEnv:
         return self._frame(), r, bool(te.value), bool(tr.value)
 
 
+def evaluate(ac, env, episodes=3, seed=0, max_steps=1024):
+    """ppo/ppo_train.py:43-69: `episodes` deterministic (argmax) episodes, reset(seed=seed + ep)."""
+    for ep in range(episodes):
+        state = env.reset(seed + ep)
+        for _ in range(max_steps):
+            with torch.no_grad():
+                dist, _ = ac.heads(torch.from_numpy(state.astype(np.float32))[None])
+            state, _, te, tr = env.step(int(dist.probs.argmax(-1).item()))
+            if te or tr:
+                break
+
+
 def run_iterations(n_iter=1, batch=2048, mb=256, epochs=10, lr=3e-4, gamma=0.99, lam=0.95, clip=0.2, vf=0.5,
-                   ent_coef=0.05, seed=777, difficulty="mediumhard"):
-    """Returns (env_steps, seconds) for n_iter rollout+GAE+update iterations on CPU."""
+                   ent_coef=0.05, seed=777, difficulty="mediumhard", eval_episodes=0):
+    """Returns (env_steps, seconds) for n_iter rollout+GAE+update iterations on CPU; with
+    eval_episodes > 0, (env_steps, seconds without the evals, seconds with them): the per-iteration
+    deterministic evaluation of ppo/ppo_train.py:150 on its own env (seed + 999)."""
     torch.manual_seed(seed)
     env = CpuEnv(difficulty)
     ac = CpuActorCritic()
@@ -86,6 +100,8 @@ def run_iterations(n_iter=1, batch=2048, mb=256, epochs=10, lr=3e-4, gamma=0.99,
     acts = torch.zeros(batch, dtype=torch.long)
     logps, vals, rews, dones = (torch.zeros(batch) for _ in range(4))
     state = env.reset(seed)
+    eval_env = CpuEnv(difficulty) if eval_episodes else None
+    t_eval = 0.0
     t0 = time.perf_counter()
     for _ in range(n_iter):
         state = env.reset()
@@ -117,4 +133,11 @@ def run_iterations(n_iter=1, batch=2048, mb=256, epochs=10, lr=3e-4, gamma=0.99,
                 loss.backward()
                 torch.nn.utils.clip_grad_norm_(ac.parameters(), 0.5)
                 opt.step()
-    return n_iter * batch, time.perf_counter() - t0
+        if eval_env is not None:
+            te0 = time.perf_counter()
+            evaluate(ac, eval_env, eval_episodes, seed + 999)
+            t_eval += time.perf_counter() - te0
+    total = time.perf_counter() - t0
+    if eval_env is not None:
+        return n_iter * batch, total - t_eval, total
+    return n_iter * batch, total

@@ -138,7 +138,8 @@ EXPORTED_SYMBOLS = (
 
 class KernelTimer:
     """Opt-in HIP-event timing of the library's launches on the current stream (bench.py).
-    Each record keeps (name, start event, end event, algorithmic bytes of the launch)."""
+    Each record keeps (name, start event, end event, algorithmic bytes, algorithmic flops); the
+    hipBLASLt GEMMs of the towers are timed the same way (flops only)."""
 
     records: list | None = None
 
@@ -152,16 +153,16 @@ class KernelTimer:
         return recs or []
 
     @classmethod
-    def span(cls, name: str, nbytes: int):
+    def span(cls, name: str, nbytes: int, flops: int = 0):
         # no events inside a HIP-graph capture (the captured rollout, merlin/ppo.py)
         if cls.records is None or torch.cuda.is_current_stream_capturing():
             return _NULL_SPAN
-        return _Span(name, nbytes)
+        return _Span(name, nbytes, flops)
 
 
 class _Span:
-    def __init__(self, name, nbytes):
-        self.name, self.nbytes = name, nbytes
+    def __init__(self, name, nbytes, flops=0):
+        self.name, self.nbytes, self.flops = name, nbytes, flops
 
     def __enter__(self):
         self.e0 = torch.cuda.Event(enable_timing=True)
@@ -171,7 +172,7 @@ class _Span:
     def __exit__(self, *exc):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        KernelTimer.records.append((self.name, self.e0, e1, self.nbytes))
+        KernelTimer.records.append((self.name, self.e0, e1, self.nbytes, self.flops))
         return False
 
 

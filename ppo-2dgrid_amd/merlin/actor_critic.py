@@ -176,6 +176,13 @@ class _Conv2LutTower(torch.autograd.Function):
         return dT, dT[:, 0:20:4, :].sum(1), None, None
 
 
+def _gemm_span(name, T, M, N, K):
+    """HIP-event span of a hipBLASLt GEMM batch (T GEMMs of M x N x K) for bench.py's FLOP roofline."""
+    from ._native import KernelTimer
+
+    return KernelTimer.span(name, 0, 2 * T * M * N * K)
+
+
 def _splitk_bmm_tn(X, dY, chunks):
     """X^T @ dY for X [T, M, K], dY [T, M, N] with the long M reduction split into `chunks`
     batched GEMMs plus a sum: hipBLASLt runs the plain tall-skinny product at about half the
@@ -184,13 +191,15 @@ def _splitk_bmm_tn(X, dY, chunks):
     N = dY.shape[2]
     c = M // chunks
     if chunks <= 1 or c < 1024:
-        return torch.bmm(X.transpose(1, 2), dY)
+        with _gemm_span("gemm_wgrad", T, K, N, M):
+            return torch.bmm(X.transpose(1, 2), dY)
     # per tower the first c*chunks rows are a view [chunks, c, K] (merging the tower and chunk
     # dims would copy both operands whenever M % chunks != 0: 2 x 0.1 ms per call at the bench size)
     part = X.new_empty((T, chunks, K, N))
-    for t in range(T):
-        torch.bmm(X[t, : c * chunks].view(chunks, c, K).transpose(1, 2), dY[t, : c * chunks].view(chunks, c, N),
-                  out=part[t])
+    with _gemm_span("gemm_wgrad", T, K, N, c * chunks):
+        for t in range(T):
+            torch.bmm(X[t, : c * chunks].view(chunks, c, K).transpose(1, 2), dY[t, : c * chunks].view(chunks, c, N),
+                      out=part[t])
     head = part.sum(1)
     if c * chunks < M:
         head = head + torch.bmm(X[:, c * chunks:].transpose(1, 2), dY[:, c * chunks:])
@@ -234,7 +243,10 @@ class _TowerHead(torch.autograd.Function):
     def forward(ctx, a3, W4p, b4, Wa, ba, Wc, bc):
         from . import _native as nat
 
-        h = nat.bias_relu_(torch.bmm(a3, W4p.transpose(1, 2)), b4.detach().contiguous())
+        T, n, K = a3.shape
+        with _gemm_span("gemm_fc1_fwd", T, n, W4p.shape[1], K):
+            z = torch.bmm(a3, W4p.transpose(1, 2))
+        h = nat.bias_relu_(z, b4.detach().contiguous())
         logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
         value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)
         ctx.save_for_backward(a3, W4p, h, Wa, Wc)
@@ -250,7 +262,10 @@ class _TowerHead(torch.autograd.Function):
         dlogits = h.new_zeros(n, Wa.shape[0]) if dlogits is None else dlogits.contiguous()
         dvalue = h.new_zeros(n) if dvalue is None else dvalue.contiguous()
         dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
-        da3 = torch.bmm(dz, W4p) if ctx.needs_input_grad[0] else None
+        da3 = None
+        if ctx.needs_input_grad[0]:
+            with _gemm_span("gemm_fc1_dgrad", dz.shape[0], n, W4p.shape[2], dz.shape[2]):
+                da3 = torch.bmm(dz, W4p)
         dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
         dba = dlogits.sum(0) if ctx.head_bias[0] else None
         dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
