@@ -14,7 +14,7 @@ def _first_step_grad(agent, sd0, mb, dtype):
     """The first optimizer step's (clipped) gradient through the reference-structured frame path
     (the rendered frames through the F.conv2d towers), the loss of src/ppo.py:136-150 on minibatch
     mb and clip_grad_norm_(0.5) (src/ppo.py:155), in `dtype` (float64: the yardstick; float32: the
-    reference's own formulation and precision)."""
+    reference's formulation)."""
     from merlin import _native as nat
     from merlin.actor_critic import CNNActorCritic
 
@@ -84,19 +84,18 @@ def test_fullsize_window_update_matches_lookup_path(device):
         results.append((stats, first[0], [p.detach().clone() for p in agent.ac.parameters()],
                         agent.last_num_windows if windows else None, agent.last_distinct_frac))
     (s1, g1, p1, nw, frac), (s2, g2, p2, _, _) = results
-    # gradients: each fp32 path against float64, as close as the reference's own fp32 formulation
-    # (the frame path, F.conv2d) is: summation-order noise at this size reaches ~3e-4 on the actor
-    # tower (near-uniform policy: the policy-gradient terms cancel), so a fixed 1e-4 between two
-    # fp32 paths would fail on fp32 itself
-    print("update paths done; float64 / float32 frame-path gradients", flush=True)
+    # gradients: each fp32 path against the float64 frame-path gradient.  Measured at this size
+    # (profiles/r02_fullsize_grad.log): both paths sit at 2-3e-4 of float64 on the actor tower and
+    # its fc1 (a near-uniform policy: the policy-gradient terms cancel, so fp32 summation noise over
+    # 131,072 samples shows) and 0.2-3e-5 on the critic, windows no further from float64 than the
+    # lookup path.  (The reference-structured fp32 frame path through F.conv2d / MIOpen is NOT a
+    # usable yardstick at this batch: it measured 10-94 % off float64 here.)
+    print("update paths done; float64 frame-path gradients", flush=True)
     g64 = _first_step_grad(agent, sd0, perm[: B // MB], torch.float64)
-    print("float64 done", flush=True)
-    g32 = _first_step_grad(agent, sd0, perm[: B // MB], torch.float32)
     rel = lambda a, b: ((a.double() - b).norm() / b.norm().clamp_min(1e-30)).item()  # noqa: E731
-    table = [(name, rel(a, r), rel(b, r), rel(f, r))
-             for (name, _), a, b, f, r in zip(agent.ac.named_parameters(), g1, g2, g32, g64)]
-    print("\n".join(f"{n:40s} windows {x:.2e} lookup {y:.2e} frames-fp32 {z:.2e}" for n, x, y, z in table))
-    bad = [t for t in table if t[1] > max(2 * t[3], 1e-5) or t[2] > max(2 * t[3], 1e-5)]
+    table = [(name, rel(a, r), rel(b, r)) for (name, _), a, b, r in zip(agent.ac.named_parameters(), g1, g2, g64)]
+    print("\n".join(f"{n:40s} windows {x:.2e} lookup {y:.2e}" for n, x, y in table))
+    bad = [t for t in table if t[1] > 5e-4 or t[2] > 5e-4 or t[1] > 2 * t[2] + 2e-5]
     assert not bad, bad
     assert nw is not None and nw > 1000 and 0.1 < frac <= 1.0, (nw, frac)
     for k in s1:
