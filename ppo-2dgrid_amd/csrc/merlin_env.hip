@@ -61,8 +61,100 @@ __device__ __forceinline__ uint32_t rng_next32(Rng &r) {
     return (uint32_t)v;
 }
 
+// ---------------------------------------------------------------------------
+// The same numpy stream drawn by a whole wave for ONE env (the sparse auto-resets): lane l holds the
+// block's output l, computed in parallel by jumping the LCG ahead l+1 steps,
+//   s_{n+k} = M^k s_n + (M^{k-1} + ... + M + 1) inc   (mod 2^128),
+// so the serial consumer (Lemire, rejection sampling) only reads outputs (readlane), the 128-bit
+// multiplies of the stepping run 64-wide.  The buffered 32-bit half is kept as numpy keeps it.
+struct U128c {
+    uint64_t lo, hi;
+};
+struct JumpTable {
+    U128c mk[64];  // M^(k+1)
+    U128c sk[64];  // sum_{i<=k} M^i
+};
+constexpr JumpTable make_jump_table() {
+    JumpTable t{};
+    const unsigned __int128 M = ((unsigned __int128)0x2360ed051fc65da4ULL << 64) | 0x4385df649fccf645ULL;
+    unsigned __int128 p = 1, sum = 0;
+    for (int k = 0; k < 64; k++) {
+        sum += p;  // sum_{i<=k} M^i
+        p *= M;    // M^(k+1)
+        t.mk[k] = U128c{(uint64_t)p, (uint64_t)(p >> 64)};
+        t.sk[k] = U128c{(uint64_t)sum, (uint64_t)(sum >> 64)};
+    }
+    return t;
+}
+__constant__ JumpTable kJump = make_jump_table();
+
+__device__ __forceinline__ void mul128(uint64_t alo, uint64_t ahi, uint64_t blo, uint64_t bhi, uint64_t &lo,
+                                       uint64_t &hi) {
+    lo = alo * blo;
+    hi = __umul64hi(alo, blo) + alo * bhi + ahi * blo;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+struct WaveRng {
+    uint64_t blo, bhi;  // state the current block was jumped from (uniform)
+    uint64_t ilo, ihi;  // increment (uniform)
+    uint64_t slo, shi;  // this lane's state after block output `lane`
+    uint64_t out;       // this lane's block output
+    int idx;            // next unconsumed block output (uniform)
+    uint32_t has, buf;
+    int lane;
+
+    __device__ __forceinline__ void jump() {  // block outputs 0..63 from (blo, bhi)
+        const U128c m = kJump.mk[lane], c = kJump.sk[lane];
+        uint64_t alo, ahi, clo, chi;
+        mul128(m.lo, m.hi, blo, bhi, alo, ahi);
+        mul128(c.lo, c.hi, ilo, ihi, clo, chi);
+        slo = alo + clo;
+        shi = ahi + chi + (slo < alo ? 1ULL : 0ULL);
+        const uint64_t x = shi ^ slo;
+        const unsigned rot = (unsigned)(shi >> 58);
+        out = (x >> rot) | (x << ((64u - rot) & 63u));
+        idx = 0;
+    }
+    __device__ __forceinline__ uint64_t next64() {
+        if (idx == 64) {
+            blo = readlane64(slo, 63);
+            bhi = readlane64(shi, 63);
+            jump();
+        }
+        return readlane64(out, idx++);
+    }
+    // numpy's state after the consumed outputs
+    __device__ __forceinline__ void state(uint64_t &lo, uint64_t &hi) const {
+        if (idx == 0) {
+            lo = blo;
+            hi = bhi;
+        } else {
+            lo = readlane64(slo, idx - 1);
+            hi = readlane64(shi, idx - 1);
+        }
+    }
+};
+
+__device__ __forceinline__ uint32_t rng_next32(WaveRng &r) {
+    if (r.has) {
+        r.has = 0;
+        return r.buf;
+    }
+    const uint64_t v = r.next64();
+    r.has = 1;
+    r.buf = (uint32_t)(v >> 32);
+    return (uint32_t)v;
+}
+
 // buffered_bounded_lemire_uint32(rng = range - 1)
-__device__ __forceinline__ uint32_t rng_lemire(Rng &r, uint32_t rng_incl) {
+template <class R>
+__device__ __forceinline__ uint32_t rng_lemire(R &r, uint32_t rng_incl) {
     const uint32_t excl = rng_incl + 1u;
     uint64_t m = (uint64_t)rng_next32(r) * excl;
     uint32_t left = (uint32_t)m;
@@ -77,7 +169,8 @@ __device__ __forceinline__ uint32_t rng_lemire(Rng &r, uint32_t rng_incl) {
 }
 
 // Generator.integers(lo, hi)
-__device__ __forceinline__ int rng_int(Rng &r, int lo, int hi) {
+template <class R>
+__device__ __forceinline__ int rng_int(R &r, int lo, int hi) {
     uint32_t rng = (uint32_t)(hi - lo - 1);
     if (rng == 0u) return lo;
     return lo + (int)rng_lemire(r, rng);
@@ -102,18 +195,37 @@ __device__ __forceinline__ void store_rng(const EnvDev &E, int i, const Rng &r) 
 }
 
 // ---------------------------------------------------------------------------
-// Per-thread grid view over the LDS column + generator state.
-template <int SP, int NB>
+// Where a grid's wall rows live while a map is generated:
+//   LdsRows   one thread per env: the env's rows are this thread's column of an LDS array
+//   WaveRows  one wave per env: lane y holds row y (rows read by readlane of a uniform y)
+template <int NB>
+struct LdsRows {
+    static constexpr bool wave = false;
+    uint32_t (*p)[NB];
+    int lane;
+    __device__ __forceinline__ uint32_t row(int y) const { return p[y][lane]; }
+    __device__ __forceinline__ void set_row(int y, uint32_t v) { p[y][lane] = v; }
+};
+struct WaveRows {
+    static constexpr bool wave = true;
+    uint32_t v;
+    int lane;
+    __device__ __forceinline__ uint32_t row(int y) const { return (uint32_t)__builtin_amdgcn_readlane((int)v, y); }
+    __device__ __forceinline__ void set_row(int y, uint32_t val) { v = (lane == y) ? val : v; }
+};
+
+// Grid + generator state over a row store; the generators are the same code for both.
+template <int SP, class Rows>
 struct Grid {
-    uint32_t (*rows)[NB];  // LDS [SP][NB]; this thread owns column `lane`
-    int lane, S;
+    Rows rows;
+    int S;
     int ax, ay, dir;
     int gx, gy;
     bool goal_set;
     uint32_t err;
 
-    __device__ __forceinline__ uint32_t row(int y) const { return rows[y][lane]; }
-    __device__ __forceinline__ void set_row(int y, uint32_t v) { rows[y][lane] = v; }
+    __device__ __forceinline__ uint32_t row(int y) const { return rows.row(y); }
+    __device__ __forceinline__ void set_row(int y, uint32_t v) { rows.set_row(y, v); }
     __device__ __forceinline__ bool wall(int x, int y) const { return (row(y) >> x) & 1u; }
     __device__ __forceinline__ void set_wall(int x, int y) { set_row(y, row(y) | (1u << x)); }
     __device__ __forceinline__ void clear_wall(int x, int y) { set_row(y, row(y) & ~(1u << x)); }
@@ -125,16 +237,21 @@ struct Grid {
     // Grid(W,H) + wall_rect(0,0,W,H)
     __device__ void walled() {
         const uint32_t edge = 1u | (1u << (S - 1));
+        if constexpr (Rows::wave) {
+            const int y = rows.lane;
+            rows.v = y < S ? ((y == 0 || y == S - 1) ? full() : edge) : 0u;
+        } else {
 #pragma unroll
-        for (int y = 0; y < SP; y++)
-            if (y < S) set_row(y, (y == 0 || y == S - 1) ? full() : edge);
+            for (int y = 0; y < SP; y++)
+                if (y < S) set_row(y, (y == 0 || y == S - 1) ? full() : edge);
+        }
         goal_set = false;
     }
 
     // MiniGridEnv.place_obj: x then y; reject occupied cells and agent_pos.
     // kind: 0 none (agent), 1 wall, 2 goal.  max_tries < 0 = unbounded.
-    __device__ bool place(Rng &r, int kind, int tx, int ty, int sw, int sh, int max_tries, int &px,
-                          int &py) {
+    template <class R>
+    __device__ bool place(R &r, int kind, int tx, int ty, int sw, int sh, int max_tries, int &px, int &py) {
         const int xe = min(tx + sw, S), ye = min(ty + sh, S);
         int tries = 0;
         for (;;) {
@@ -160,7 +277,8 @@ struct Grid {
     }
 
     // MiniGridEnv.place_agent(top, size, rand_dir=True)
-    __device__ void place_agent(Rng &r, int tx, int ty, int sw, int sh) {
+    template <class R>
+    __device__ void place_agent(R &r, int tx, int ty, int sw, int sh) {
         int x, y;
         ax = -1;
         ay = -1;
@@ -170,7 +288,8 @@ struct Grid {
         dir = rng_int(r, 0, 4);
     }
 
-    __device__ void place_goal(Rng &r) {
+    template <class R>
+    __device__ void place_goal(R &r) {
         int x, y;
         place(r, 2, 0, 0, S, S, -1, x, y);
     }
@@ -179,6 +298,7 @@ struct Grid {
     // the 4-connected component of non-wall cells containing the agent"; computed
     // as a bit-parallel flood fill over row masks (Gauss-Seidel sweeps in registers).
     __device__ bool reachable() const {
+        if constexpr (Rows::wave) return reachable_wave();
         uint32_t F[SP], R[SP];
         const uint32_t fm = full();
 #pragma unroll
@@ -215,15 +335,35 @@ struct Grid {
         return false;
     }
 
-    __device__ void fallback(Rng &r, uint32_t *fallbacks) {
-        atomicAdd(fallbacks, 1u);
+    // the same fixed point with one row per lane (Jacobi sweeps: lane y reads rows y-1, y+1)
+    __device__ bool reachable_wave() const {
+        const int y = rows.lane;
+        const uint32_t F = y < S ? (~rows.v & full()) : 0u;
+        uint32_t R = y == ay ? (1u << ax) : 0u;
+        for (int it = 0; it < SP * SP; it++) {
+            uint32_t up = (uint32_t)__shfl_up((int)R, 1);
+            uint32_t dn = (uint32_t)__shfl_down((int)R, 1);
+            if (y == 0) up = 0u;
+            if (y == 63) dn = 0u;
+            const uint32_t n = (R | (R << 1) | (R >> 1) | up | dn) & F;
+            if (((uint32_t)__builtin_amdgcn_readlane((int)n, gy) >> gx) & 1u) return true;
+            if (!__ballot(n != R)) return false;
+            R = n;
+        }
+        return false;
+    }
+
+    template <class R>
+    __device__ void fallback(R &r, uint32_t *fallbacks) {
+        if (!Rows::wave || rows.lane == 0) atomicAdd(fallbacks, 1u);
         walled();
         place_agent(r, 0, 0, S, S);
         place_goal(r);
     }
 
     // EasyEnv._gen_grid (easy_env.py:19-39): put_obj(Goal, W-5, H-5) may sit on the agent
-    __device__ void gen_easy(Rng &r) {
+    template <class R>
+    __device__ void gen_easy(R &r) {
         walled();
         place_agent(r, 0, 0, S, S);
         gx = S - 5;
@@ -232,7 +372,8 @@ struct Grid {
     }
 
     // MediumEnv._gen_grid (medium_env.py:19-33)
-    __device__ void gen_medium(Rng &r) {
+    template <class R>
+    __device__ void gen_medium(R &r) {
         walled();
         place_agent(r, 0, 0, S, S);
         place_goal(r);
@@ -240,7 +381,8 @@ struct Grid {
 
     // MediumHardEnv._gen_grid (medium_hard_env.py:12-45); on a retry the previous
     // attempt's agent_pos still blocks wall placement (place_agent resets it later).
-    __device__ void gen_mediumhard(Rng &r, uint32_t *fallbacks) {
+    template <class R>
+    __device__ void gen_mediumhard(R &r, uint32_t *fallbacks) {
         const int playable = (S - 2) * (S - 2);
         const int min_obs = (playable * 10) / 100;  // int(playable * 0.10)
         const int max_obs = (playable * 20) / 100;  // int(playable * 0.20)
@@ -259,7 +401,8 @@ struct Grid {
     }
 
     // HardEnv._gen_grid (hard_env.py:11-73), agent_start_pos None, random_goal True
-    __device__ void gen_hard(Rng &r, uint32_t *fallbacks) {
+    template <class R>
+    __device__ void gen_hard(R &r, uint32_t *fallbacks) {
         const int mid = S / 2;
         const bool large = S > 10;
         for (int attempt = 0; attempt < 100; attempt++) {
@@ -320,7 +463,8 @@ struct Grid {
     }
 
     // HardestEnv._gen_grid (hardest_env.py:20-70)
-    __device__ void gen_hardest(Rng &r, uint32_t *fallbacks) {
+    template <class R>
+    __device__ void gen_hardest(R &r, uint32_t *fallbacks) {
         const int mx = S / 2, my = S / 2;
         for (int attempt = 0; attempt < 100; attempt++) {
             walled();
@@ -344,7 +488,8 @@ struct Grid {
     }
 
     // MiniGridEnv.reset body: agent_pos=(-1,-1); _gen_grid(W,H)
-    __device__ void generate(Rng &r, int difficulty, uint32_t *fallbacks) {
+    template <class R>
+    __device__ void generate(R &r, int difficulty, uint32_t *fallbacks) {
         ax = -1;
         ay = -1;
         dir = 0;
@@ -369,9 +514,9 @@ struct GenOut {
 template <int SP, int NB>
 __device__ __forceinline__ void generate_map_inl(uint32_t (*rows)[NB], int lane, int S, int difficulty, Rng &r,
                                                  uint32_t *fallbacks, GenOut &o) {
-    Grid<SP, NB> G;
-    G.rows = rows;
-    G.lane = lane;
+    Grid<SP, LdsRows<NB>> G;
+    G.rows.p = rows;
+    G.rows.lane = lane;
     G.S = S;
     G.err = 0u;
     G.generate(r, difficulty, fallbacks);
@@ -556,48 +701,78 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
     reset_one<SP>(E, i, rows, lane, obs);
 }
 
-// The auto-resets of a single-step launch, out of the step kernel: k_env_step flagged the envs whose
-// episode ended (E.rflag), and here each one-wave block takes RS_SPAN x 64 envs (lane l loads the
-// RS_SPAN flags of envs base + RS_SPAN*l .. in one 16-B load), packs the flagged ones onto
-// consecutive lanes (ballot + prefix count) and regenerates them 64 at a time, so the map
-// generations (rejection sampling + flood fill, thousands of cycles each) run densely instead of
-// stalling a whole wave of the step kernel per reset.
-constexpr int RS_SPAN = 16;
+// One env's reset by a whole wave: the same generators over WaveRows / WaveRng (lane y holds wall row
+// y, block outputs jumped ahead in parallel, the flood fill one row per lane), then the rows go to
+// HBM in one coalesced store and lane 0 writes the state and the first observation.  Bit-exact
+// with reset_one: the same draws in the same order.
 template <int SP>
-__global__ __launch_bounds__(BLK) void k_env_autoreset(EnvDev E, uint32_t *__restrict__ obs) {
-    __shared__ uint32_t rows[SP][BLK];
-    __shared__ int queue[BLK];
-    const int lane = threadIdx.x;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    const int64_t base = ((int64_t)blockIdx.x * BLK + lane) * RS_SPAN;  // this lane's first env
-    uint32_t fl[RS_SPAN / 4] = {0u, 0u, 0u, 0u};
-    if (base + RS_SPAN <= E.n) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(E.rflag + base);
-        fl[0] = v.x;
-        fl[1] = v.y;
-        fl[2] = v.z;
-        fl[3] = v.w;
-    } else {
-        for (int b = 0; b < RS_SPAN; b++)
-            if (base + b < E.n) fl[b >> 2] |= (uint32_t)E.rflag[base + b] << (8 * (b & 3));
+__device__ void reset_one_wave(const EnvDev &E, int i, uint32_t (*vrows)[1], uint32_t *__restrict__ obs) {
+    const int lane = threadIdx.x & 63;
+    WaveRng r;
+    r.lane = lane;
+    const ulonglong2 st = E.rng_s[i], inc = E.rng_i[i];
+    const uint2 b = E.rng_b[i];
+    r.blo = st.x;
+    r.bhi = st.y;
+    r.ilo = inc.x;
+    r.ihi = inc.y;
+    r.has = b.x;
+    r.buf = b.y;
+    r.jump();
+    Grid<SP, WaveRows> G;
+    G.rows.v = 0u;
+    G.rows.lane = lane;
+    G.S = E.size;
+    G.err = 0u;
+    G.generate(r, E.difficulty, E.err + 1);
+    uint64_t slo, shi;
+    r.state(slo, shi);
+    if (lane < SP) {
+        E.walls[(size_t)i * SP + lane] = lane < E.size ? G.rows.v : 0u;
+        vrows[lane][0] = G.rows.v;
     }
-    int nq = 0;  // wave-uniform
-#pragma unroll
-    for (int b = 0; b < RS_SPAN; b++) {
-        const bool need = (fl[b >> 2] >> (8 * (b & 3))) & 0xffu;
-        const unsigned long long m = __ballot(need);
-        const int c = __popcll(m);
-        if (c == 0) continue;
-        if (nq + c > BLK) {  // the queue is full: run it first
-            if (lane < nq) reset_one<SP>(E, queue[lane], rows, lane, obs);
-            nq = 0;
-            __syncthreads();
+    __syncthreads();  // one-wave block
+    if (lane == 0) {
+        if (!E.reseed) {
+            E.rng_s[i] = make_ulonglong2(slo, shi);
+            E.rng_b[i] = make_uint2(r.has, r.buf);
         }
-        if (need) queue[nq + __popcll(m & below)] = (int)(base + b);
-        nq += c;
-        __syncthreads();
+        E.agent[i] = pack_agent(G.ax, G.ay, G.dir, 0, G.gx, G.gy, G.ax, G.ay, 0);
+        E.ep_ret[i] = 0.0;
+        E.ep_len[i] = 0;
+        if (E.explore_on) reset_visited<SP>(E, i, G.ax, G.ay);
+        if (G.err) atomicOr(E.err, G.err);
+        uint32_t w[MERLIN_OBS_WORDS];
+        view_codes<SP, 1>(vrows, 0, E.size, G.ax, G.ay, G.dir, G.gx, G.gy, true, w);
+        if (obs) store_obs(obs, (size_t)i, w);
     }
-    if (lane < nq) reset_one<SP>(E, queue[lane], rows, lane, obs);
+    __syncthreads();  // vrows is reused by the wave's next reset
+}
+
+// The auto-resets of a single-step launch, out of the step kernel: k_env_step flagged the envs whose
+// episode ended (E.rflag); each one-wave block takes SPAN groups of 64 envs and regenerates the flagged
+// ones one after another, each by the whole wave (reset_one_wave).  Resets are sparse (an episode ends
+// every ~10^2-10^3 steps), so this launch costs about one map generation's latency, and that latency is
+// a wave's, not a thread's (parallel RNG jump-ahead and flood fill).
+template <int SP, int SPAN>
+__global__ __launch_bounds__(BLK) void k_env_autoreset(EnvDev E, uint32_t *__restrict__ obs) {
+    __shared__ uint32_t vrows[SP][1];
+    const int lane = threadIdx.x;
+    bool need[SPAN];
+#pragma unroll
+    for (int g = 0; g < SPAN; g++) {
+        const int64_t i = ((int64_t)blockIdx.x * SPAN + g) * BLK + lane;
+        need[g] = i < E.n && E.rflag[i];
+    }
+    for (int g = 0; g < SPAN; g++) {
+        const int64_t base = ((int64_t)blockIdx.x * SPAN + g) * BLK;
+        unsigned long long m = __ballot(need[g]);
+        while (m) {
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            reset_one_wave<SP>(E, (int)(base + j), vrows, obs);
+        }
+    }
 }
 
 // DEFER (single-step launches with auto-reset): an env whose episode ends is flagged in E.rflag and
@@ -736,8 +911,12 @@ static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t 
         hipLaunchKernelGGL((k_env_step<SP, true>), grid, block, 0, s, E, O);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        const int rgrid = (E.n + BLK * RS_SPAN - 1) / (BLK * RS_SPAN);
-        hipLaunchKernelGGL(k_env_autoreset<SP>, dim3(rgrid), dim3(BLK), 0, s, E, O.obs);
+        if (E.n >= (1 << 18)) {  // many envs: 4 groups of 64 per wave keep the launch small
+            hipLaunchKernelGGL((k_env_autoreset<SP, 4>), dim3((E.n + 4 * BLK - 1) / (4 * BLK)), dim3(BLK), 0, s, E,
+                               O.obs);
+        } else {
+            hipLaunchKernelGGL((k_env_autoreset<SP, 1>), dim3((E.n + BLK - 1) / BLK), dim3(BLK), 0, s, E, O.obs);
+        }
     } else {
         hipLaunchKernelGGL((k_env_step<SP, false>), grid, block, 0, s, E, O);
     }
