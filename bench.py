@@ -166,11 +166,12 @@ def env_only_tier(torch, MerlinVecEnv, n, T, difficulty, size, device):
     return fused, single
 
 
-def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=8):
+def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=16):
     """Tier E at HBM scale: 2M envs (0.35 GB of env state and outputs per step),
     T single-step k_env_step launches on pre-generated actions, 168 algorithmic bytes per
     env-step (merlin.envs.ENV_STEP_BYTES); at the bench's 4096 envs the kernel is latency-bound
-    (64 waves on 256 CUs), here it streams."""
+    (64 waves on 256 CUs), here it streams.  T = 16 = one look-ahead map refill (every 16 step
+    launches, csrc/merlin_env.hip k_env_refill) inside the timed steps."""
     from merlin.envs import ENV_STEP_BYTES
 
     env = MerlinVecEnv(n, difficulty=difficulty, size=size, seed=31337, device=device)

@@ -13,6 +13,7 @@ struct merlin_env {
     merlin::EnvDev dev;
     int device;
     bool has_state;
+    int steps_since_refill;  // merlin_env_step launches since the last look-ahead refill
 };
 
 namespace {
@@ -297,7 +298,11 @@ int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
     alloc((void **)&d.ep_ret, n * sizeof(double));
     alloc((void **)&d.ep_len, n * sizeof(int32_t));
     alloc((void **)&d.err, 2 * sizeof(uint32_t));
-    alloc((void **)&d.rflag, n * sizeof(uint8_t));
+    alloc((void **)&d.pg_walls, n * d.sp * sizeof(uint32_t));
+    alloc((void **)&d.pg_agent, n * sizeof(uint4));
+    alloc((void **)&d.pg_rng_s, n * sizeof(ulonglong2));
+    alloc((void **)&d.pg_rng_b, n * sizeof(uint2));
+    alloc((void **)&d.pg_valid, n * sizeof(uint8_t));
     if (d.explore_on) alloc((void **)&d.visited, n * d.sp * sizeof(uint32_t));
     if (err != hipSuccess) {
         merlin_env_destroy(e);
@@ -310,7 +315,8 @@ int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
 int merlin_env_destroy(merlin_env *e) {
     if (!e) return MERLIN_OK;
     merlin::EnvDev &d = e->dev;
-    void *ptrs[] = {d.walls, d.agent, d.rng_s, d.rng_i, d.rng_b, d.ep_ret, d.ep_len, d.err, d.visited, d.rflag};
+    void *ptrs[] = {d.walls, d.agent, d.rng_s, d.rng_i, d.rng_b, d.ep_ret, d.ep_len, d.err, d.visited,
+                    d.pg_walls, d.pg_agent, d.pg_rng_s, d.pg_rng_b, d.pg_valid};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete e;
@@ -337,6 +343,7 @@ int merlin_env_seed(merlin_env *e, const uint64_t *seeds, int32_t n, void *strea
     if (err == hipSuccess)
         err = hipMemcpyAsync(e->dev.rng_i, inc, N * sizeof(ulonglong2), hipMemcpyHostToDevice, s);
     if (err == hipSuccess) err = hipMemsetAsync(e->dev.rng_b, 0, N * sizeof(uint2), s);
+    if (err == hipSuccess) err = hipMemsetAsync(e->dev.pg_valid, 0, N, s);  // look-ahead maps are stale
     if (err == hipSuccess) err = hipStreamSynchronize(s);  // host staging buffers are freed below
     delete[] st;
     delete[] inc;
@@ -346,7 +353,8 @@ int merlin_env_seed(merlin_env *e, const uint64_t *seeds, int32_t n, void *strea
 
 int merlin_env_reset(merlin_env *e, const uint8_t *mask, uint32_t *obs, void *stream) {
     if (!e) return fail(MERLIN_E_INVALID, "null env");
-    HIP_TRY(merlin::launch_env_reset(e->dev, mask, obs, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_env_reset(e->dev, mask, obs, (hipStream_t)stream));  // + look-ahead refill
+    e->steps_since_refill = 0;
     if (!mask) e->has_state = true;
     return MERLIN_OK;
 }
@@ -371,7 +379,9 @@ int merlin_env_step(merlin_env *e, const int64_t *actions, int32_t n_steps, int6
     o.done = done;
     o.ep_ret_out = ep_ret;
     o.ep_len_out = ep_len;
-    HIP_TRY(merlin::launch_env_step(e->dev, o, (hipStream_t)stream));
+    const bool refill = ++e->steps_since_refill >= merlin::REFILL_EVERY;
+    if (refill) e->steps_since_refill = 0;
+    HIP_TRY(merlin::launch_env_step(e->dev, o, refill, (hipStream_t)stream));
     return MERLIN_OK;
 }
 

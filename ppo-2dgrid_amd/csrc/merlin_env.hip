@@ -61,97 +61,6 @@ __device__ __forceinline__ uint32_t rng_next32(Rng &r) {
     return (uint32_t)v;
 }
 
-// ---------------------------------------------------------------------------
-// The same numpy stream drawn by a whole wave for ONE env (the sparse auto-resets): lane l holds the
-// block's output l, computed in parallel by jumping the LCG ahead l+1 steps,
-//   s_{n+k} = M^k s_n + (M^{k-1} + ... + M + 1) inc   (mod 2^128),
-// so the serial consumer (Lemire, rejection sampling) only reads outputs (readlane), the 128-bit
-// multiplies of the stepping run 64-wide.  The buffered 32-bit half is kept as numpy keeps it.
-struct U128c {
-    uint64_t lo, hi;
-};
-struct JumpTable {
-    U128c mk[64];  // M^(k+1)
-    U128c sk[64];  // sum_{i<=k} M^i
-};
-constexpr JumpTable make_jump_table() {
-    JumpTable t{};
-    const unsigned __int128 M = ((unsigned __int128)0x2360ed051fc65da4ULL << 64) | 0x4385df649fccf645ULL;
-    unsigned __int128 p = 1, sum = 0;
-    for (int k = 0; k < 64; k++) {
-        sum += p;  // sum_{i<=k} M^i
-        p *= M;    // M^(k+1)
-        t.mk[k] = U128c{(uint64_t)p, (uint64_t)(p >> 64)};
-        t.sk[k] = U128c{(uint64_t)sum, (uint64_t)(sum >> 64)};
-    }
-    return t;
-}
-__constant__ JumpTable kJump = make_jump_table();
-
-__device__ __forceinline__ void mul128(uint64_t alo, uint64_t ahi, uint64_t blo, uint64_t bhi, uint64_t &lo,
-                                       uint64_t &hi) {
-    lo = alo * blo;
-    hi = __umul64hi(alo, blo) + alo * bhi + ahi * blo;
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-struct WaveRng {
-    uint64_t blo, bhi;  // state the current block was jumped from (uniform)
-    uint64_t ilo, ihi;  // increment (uniform)
-    uint64_t slo, shi;  // this lane's state after block output `lane`
-    uint64_t out;       // this lane's block output
-    int idx;            // next unconsumed block output (uniform)
-    uint32_t has, buf;
-    int lane;
-
-    __device__ __forceinline__ void jump() {  // block outputs 0..63 from (blo, bhi)
-        const U128c m = kJump.mk[lane], c = kJump.sk[lane];
-        uint64_t alo, ahi, clo, chi;
-        mul128(m.lo, m.hi, blo, bhi, alo, ahi);
-        mul128(c.lo, c.hi, ilo, ihi, clo, chi);
-        slo = alo + clo;
-        shi = ahi + chi + (slo < alo ? 1ULL : 0ULL);
-        const uint64_t x = shi ^ slo;
-        const unsigned rot = (unsigned)(shi >> 58);
-        out = (x >> rot) | (x << ((64u - rot) & 63u));
-        idx = 0;
-    }
-    __device__ __forceinline__ uint64_t next64() {
-        if (idx == 64) {
-            blo = readlane64(slo, 63);
-            bhi = readlane64(shi, 63);
-            jump();
-        }
-        return readlane64(out, idx++);
-    }
-    // numpy's state after the consumed outputs
-    __device__ __forceinline__ void state(uint64_t &lo, uint64_t &hi) const {
-        if (idx == 0) {
-            lo = blo;
-            hi = bhi;
-        } else {
-            lo = readlane64(slo, idx - 1);
-            hi = readlane64(shi, idx - 1);
-        }
-    }
-};
-
-__device__ __forceinline__ uint32_t rng_next32(WaveRng &r) {
-    if (r.has) {
-        r.has = 0;
-        return r.buf;
-    }
-    const uint64_t v = r.next64();
-    r.has = 1;
-    r.buf = (uint32_t)(v >> 32);
-    return (uint32_t)v;
-}
-
 // buffered_bounded_lemire_uint32(rng = range - 1)
 template <class R>
 __device__ __forceinline__ uint32_t rng_lemire(R &r, uint32_t rng_incl) {
@@ -195,26 +104,15 @@ __device__ __forceinline__ void store_rng(const EnvDev &E, int i, const Rng &r) 
 }
 
 // ---------------------------------------------------------------------------
-// Where a grid's wall rows live while a map is generated:
-//   LdsRows   one thread per env: the env's rows are this thread's column of an LDS array
-//   WaveRows  one wave per env: lane y holds row y (rows read by readlane of a uniform y)
+// Where a grid's wall rows live while a map is generated: this thread's column of an LDS array.
 template <int NB>
 struct LdsRows {
-    static constexpr bool wave = false;
     uint32_t (*p)[NB];
     int lane;
     __device__ __forceinline__ uint32_t row(int y) const { return p[y][lane]; }
     __device__ __forceinline__ void set_row(int y, uint32_t v) { p[y][lane] = v; }
 };
-struct WaveRows {
-    static constexpr bool wave = true;
-    uint32_t v;
-    int lane;
-    __device__ __forceinline__ uint32_t row(int y) const { return (uint32_t)__builtin_amdgcn_readlane((int)v, y); }
-    __device__ __forceinline__ void set_row(int y, uint32_t val) { v = (lane == y) ? val : v; }
-};
-
-// Grid + generator state over a row store; the generators are the same code for both.
+// Grid + generator state over a row store.
 template <int SP, class Rows>
 struct Grid {
     Rows rows;
@@ -237,14 +135,9 @@ struct Grid {
     // Grid(W,H) + wall_rect(0,0,W,H)
     __device__ void walled() {
         const uint32_t edge = 1u | (1u << (S - 1));
-        if constexpr (Rows::wave) {
-            const int y = rows.lane;
-            rows.v = y < S ? ((y == 0 || y == S - 1) ? full() : edge) : 0u;
-        } else {
 #pragma unroll
-            for (int y = 0; y < SP; y++)
-                if (y < S) set_row(y, (y == 0 || y == S - 1) ? full() : edge);
-        }
+        for (int y = 0; y < SP; y++)
+            if (y < S) set_row(y, (y == 0 || y == S - 1) ? full() : edge);
         goal_set = false;
     }
 
@@ -298,7 +191,6 @@ struct Grid {
     // the 4-connected component of non-wall cells containing the agent"; computed
     // as a bit-parallel flood fill over row masks (Gauss-Seidel sweeps in registers).
     __device__ bool reachable() const {
-        if constexpr (Rows::wave) return reachable_wave();
         uint32_t F[SP], R[SP];
         const uint32_t fm = full();
 #pragma unroll
@@ -335,27 +227,9 @@ struct Grid {
         return false;
     }
 
-    // the same fixed point with one row per lane (Jacobi sweeps: lane y reads rows y-1, y+1)
-    __device__ bool reachable_wave() const {
-        const int y = rows.lane;
-        const uint32_t F = y < S ? (~rows.v & full()) : 0u;
-        uint32_t R = y == ay ? (1u << ax) : 0u;
-        for (int it = 0; it < SP * SP; it++) {
-            uint32_t up = (uint32_t)__shfl_up((int)R, 1);
-            uint32_t dn = (uint32_t)__shfl_down((int)R, 1);
-            if (y == 0) up = 0u;
-            if (y == 63) dn = 0u;
-            const uint32_t n = (R | (R << 1) | (R >> 1) | up | dn) & F;
-            if (((uint32_t)__builtin_amdgcn_readlane((int)n, gy) >> gx) & 1u) return true;
-            if (!__ballot(n != R)) return false;
-            R = n;
-        }
-        return false;
-    }
-
     template <class R>
     __device__ void fallback(R &r, uint32_t *fallbacks) {
-        if (!Rows::wave || rows.lane == 0) atomicAdd(fallbacks, 1u);
+        atomicAdd(fallbacks, 1u);
         walled();
         place_agent(r, 0, 0, S, S);
         place_goal(r);
@@ -671,14 +545,54 @@ __device__ __forceinline__ void reset_visited(const EnvDev &E, int i, int ax, in
     for (int y = 0; y < SP; y++) vis[y] = (y == ay) ? (1u << ax) : 0u;
 }
 
-// One env's reset: map generation, state, RNG, episode accumulators, first observation.
+// Look-ahead maps.  An env's next map depends only on its RNG stream (MiniGridEnv.reset draws nothing
+// else), so k_env_refill generates it ahead of time into the env's slot (pg_*: the rows, agent, goal
+// and the RNG state after the generation) and a reset just takes the slot: the step kernel never stalls
+// a wave on a map generation (rejection sampling + flood fill, tens of microseconds for one env), and
+// the refill -- which is latency-bound on its slowest env -- runs once per REFILL_EVERY step launches
+// instead of once per step.  A reset whose slot is empty (a second episode end before a refill, or a
+// reseed) generates the same map in place from the env's RNG.  In reseed mode (every reset is
+// reset(seed=task_seed)) the slot is never consumed and the env's RNG never advances.
+template <int SP, int NB, bool INL>
+__device__ __forceinline__ void take_map(const EnvDev &E, int i, uint32_t (*rows)[NB], int lane, GenOut &g) {
+    if (E.pg_valid[i]) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(E.pg_walls + (size_t)i * SP);
+#pragma unroll
+        for (int q = 0; q < SP / 4; q++) {
+            const uint4 v = src[q];
+            rows[4 * q + 0][lane] = v.x;
+            rows[4 * q + 1][lane] = v.y;
+            rows[4 * q + 2][lane] = v.z;
+            rows[4 * q + 3][lane] = v.w;
+        }
+        const uint4 a = E.pg_agent[i];
+        g.ax = a.x & 0xff;
+        g.ay = (a.x >> 8) & 0xff;
+        g.dir = (a.x >> 16) & 3;
+        g.gx = a.z & 0xff;
+        g.gy = (a.z >> 8) & 0xff;
+        g.err = 0u;
+        if (!E.reseed) {
+            E.rng_s[i] = E.pg_rng_s[i];
+            E.rng_b[i] = E.pg_rng_b[i];
+            E.pg_valid[i] = 0;
+        }
+    } else {
+        Rng r = load_rng(E, i);
+        if (INL)
+            generate_map_inl<SP, NB>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
+        else
+            generate_map<SP, NB>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
+        if (!E.reseed) store_rng(E, i, r);
+    }
+}
+
+// One env's reset (merlin_env_reset): its next map, state, episode accumulators, first observation.
 template <int SP>
 __device__ __forceinline__ void reset_one(const EnvDev &E, int i, uint32_t (*rows)[BLK], int lane,
                                           uint32_t *__restrict__ obs) {
-    Rng r = load_rng(E, i);
     GenOut g;
-    generate_map_inl<SP, BLK>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
-    if (!E.reseed) store_rng(E, i, r);
+    take_map<SP, BLK, true>(E, i, rows, lane, g);
     store_rows<SP, BLK>(E, i, rows, lane, E.size);
     E.agent[i] = pack_agent(g.ax, g.ay, g.dir, 0, g.gx, g.gy, g.ax, g.ay, 0);
     E.ep_ret[i] = 0.0;
@@ -701,84 +615,67 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
     reset_one<SP>(E, i, rows, lane, obs);
 }
 
-// One env's reset by a whole wave: the same generators over WaveRows / WaveRng (lane y holds wall row
-// y, block outputs jumped ahead in parallel, the flood fill one row per lane), then the rows go to
-// HBM in one coalesced store and lane 0 writes the state and the first observation.  Bit-exact
-// with reset_one: the same draws in the same order.
+// Fill the empty look-ahead slots: each one-wave block takes RS_SPAN x 64 envs (lane l reads the slot
+// flags of envs base + RS_SPAN*l .. in one 16-B load), packs the empty ones onto consecutive lanes
+// (ballot + prefix count) and generates 64 at a time, one thread per env, from the env's RNG (which
+// stays as it is: the slot holds the state after the generation).
+constexpr int RS_SPAN = 16;
 template <int SP>
-__device__ void reset_one_wave(const EnvDev &E, int i, uint32_t (*vrows)[1], uint32_t *__restrict__ obs) {
-    const int lane = threadIdx.x & 63;
-    WaveRng r;
-    r.lane = lane;
-    const ulonglong2 st = E.rng_s[i], inc = E.rng_i[i];
-    const uint2 b = E.rng_b[i];
-    r.blo = st.x;
-    r.bhi = st.y;
-    r.ilo = inc.x;
-    r.ihi = inc.y;
-    r.has = b.x;
-    r.buf = b.y;
-    r.jump();
-    Grid<SP, WaveRows> G;
-    G.rows.v = 0u;
-    G.rows.lane = lane;
-    G.S = E.size;
-    G.err = 0u;
-    G.generate(r, E.difficulty, E.err + 1);
-    uint64_t slo, shi;
-    r.state(slo, shi);
-    if (lane < SP) {
-        E.walls[(size_t)i * SP + lane] = lane < E.size ? G.rows.v : 0u;
-        vrows[lane][0] = G.rows.v;
-    }
-    __syncthreads();  // one-wave block
-    if (lane == 0) {
-        if (!E.reseed) {
-            E.rng_s[i] = make_ulonglong2(slo, shi);
-            E.rng_b[i] = make_uint2(r.has, r.buf);
-        }
-        E.agent[i] = pack_agent(G.ax, G.ay, G.dir, 0, G.gx, G.gy, G.ax, G.ay, 0);
-        E.ep_ret[i] = 0.0;
-        E.ep_len[i] = 0;
-        if (E.explore_on) reset_visited<SP>(E, i, G.ax, G.ay);
-        if (G.err) atomicOr(E.err, G.err);
-        uint32_t w[MERLIN_OBS_WORDS];
-        view_codes<SP, 1>(vrows, 0, E.size, G.ax, G.ay, G.dir, G.gx, G.gy, true, w);
-        if (obs) store_obs(obs, (size_t)i, w);
-    }
-    __syncthreads();  // vrows is reused by the wave's next reset
-}
-
-// The auto-resets of a single-step launch, out of the step kernel: k_env_step flagged the envs whose
-// episode ended (E.rflag); each one-wave block takes SPAN groups of 64 envs and regenerates the flagged
-// ones one after another, each by the whole wave (reset_one_wave).  Resets are sparse (an episode ends
-// every ~10^2-10^3 steps), so this launch costs about one map generation's latency, and that latency is
-// a wave's, not a thread's (parallel RNG jump-ahead and flood fill).
-template <int SP, int SPAN>
-__global__ __launch_bounds__(BLK) void k_env_autoreset(EnvDev E, uint32_t *__restrict__ obs) {
-    __shared__ uint32_t vrows[SP][1];
-    const int lane = threadIdx.x;
-    bool need[SPAN];
+__device__ __forceinline__ void refill_one(const EnvDev &E, int i, uint32_t (*rows)[BLK], int lane) {
+    Rng r = load_rng(E, i);
+    GenOut g;
+    generate_map_inl<SP, BLK>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
+    uint4 *dst = reinterpret_cast<uint4 *>(E.pg_walls + (size_t)i * SP);
 #pragma unroll
-    for (int g = 0; g < SPAN; g++) {
-        const int64_t i = ((int64_t)blockIdx.x * SPAN + g) * BLK + lane;
-        need[g] = i < E.n && E.rflag[i];
+    for (int q = 0; q < SP / 4; q++) {
+        const int y = 4 * q;
+        dst[q] = make_uint4(y + 0 < E.size ? rows[y + 0][lane] : 0u, y + 1 < E.size ? rows[y + 1][lane] : 0u,
+                            y + 2 < E.size ? rows[y + 2][lane] : 0u, y + 3 < E.size ? rows[y + 3][lane] : 0u);
     }
-    for (int g = 0; g < SPAN; g++) {
-        const int64_t base = ((int64_t)blockIdx.x * SPAN + g) * BLK;
-        unsigned long long m = __ballot(need[g]);
-        while (m) {
-            const int j = __builtin_ctzll(m);
-            m &= m - 1;
-            reset_one_wave<SP>(E, (int)(base + j), vrows, obs);
-        }
-    }
+    E.pg_agent[i] = pack_agent(g.ax, g.ay, g.dir, 0, g.gx, g.gy, g.ax, g.ay, 0);
+    E.pg_rng_s[i] = make_ulonglong2(r.slo, r.shi);
+    E.pg_rng_b[i] = make_uint2(r.has, r.buf);
+    E.pg_valid[i] = 1;
+    if (g.err) atomicOr(E.err, g.err);
 }
 
-// DEFER (single-step launches with auto-reset): an env whose episode ends is flagged in E.rflag and
-// k_env_autoreset, launched next on the stream, regenerates it and writes its observation; the
-// step kernel then writes neither that obs row nor the env's state.
-template <int SP, bool DEFER>
+template <int SP>
+__global__ __launch_bounds__(BLK) void k_env_refill(EnvDev E) {
+    __shared__ uint32_t rows[SP][BLK];
+    __shared__ int queue[BLK];
+    const int lane = threadIdx.x;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const int64_t base = ((int64_t)blockIdx.x * BLK + lane) * RS_SPAN;  // this lane's first env
+    uint32_t fl[RS_SPAN / 4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
+    if (base + RS_SPAN <= E.n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(E.pg_valid + base);
+        fl[0] = v.x;
+        fl[1] = v.y;
+        fl[2] = v.z;
+        fl[3] = v.w;
+    } else {
+        for (int b = 0; b < RS_SPAN; b++)
+            if (base + b < E.n && !E.pg_valid[base + b]) fl[b >> 2] &= ~(0xffu << (8 * (b & 3)));
+    }
+    int nq = 0;  // wave-uniform
+    for (int b = 0; b < RS_SPAN; b++) {
+        const bool need = !((fl[b >> 2] >> (8 * (b & 3))) & 0xffu);
+        const unsigned long long m = __ballot(need);
+        const int c = __popcll(m);
+        if (c == 0) continue;
+        if (nq + c > BLK) {  // the queue is full: run it first
+            if (lane < nq) refill_one<SP>(E, queue[lane], rows, lane);
+            nq = 0;
+            __syncthreads();
+        }
+        if (need) queue[nq + __popcll(m & below)] = (int)(base + b);
+        nq += c;
+        __syncthreads();
+    }
+    if (lane < nq) refill_one<SP>(E, queue[lane], rows, lane);
+}
+
+template <int SP>
 __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
     __shared__ uint32_t rows[SP][SBLK];
     const int lane = threadIdx.x;
@@ -794,8 +691,7 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
     double ep_ret = E.ep_ret[i];
     int ep_len = E.ep_len[i];
     uint32_t err = 0u;
-    bool rows_dirty = false, rng_loaded = false;
-    Rng r;
+    bool rows_dirty = false;
     const size_t N = (size_t)E.n;
 
     for (int t = 0; t < O.n_steps; t++) {
@@ -850,20 +746,9 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
             if (O.ep_ret_out) O.ep_ret_out[row] = ep_ret;
             if (O.ep_len_out) O.ep_len_out[row] = ep_len;
         }
-        if (DEFER) {  // O.autoreset, n_steps == 1
-            E.rflag[i] = done ? 1 : 0;
-            if (done) {
-                if (err) atomicOr(E.err, err);
-                return;
-            }
-        }
         if (done && O.autoreset) {
-            if (!rng_loaded || E.reseed) {
-                r = load_rng(E, i);  // reseed mode: always restart from the seeded state
-                rng_loaded = true;
-            }
             GenOut g;
-            generate_map<SP, SBLK>(rows, lane, S, E.difficulty, r, E.err + 1, g);
+            take_map<SP, SBLK, false>(E, i, rows, lane, g);
             ax = g.ax;
             ay = g.ay;
             dir = g.dir;
@@ -889,11 +774,20 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
     E.ep_ret[i] = ep_ret;
     E.ep_len[i] = ep_len;
     if (rows_dirty) store_rows<SP, SBLK>(E, i, rows, lane, S);
-    if (rng_loaded && !E.reseed) store_rng(E, i, r);
     if (err) atomicOr(E.err, err);
 }
 
 }  // namespace
+
+template <int SP>
+static hipError_t launch_refill_sp(const EnvDev &E, hipStream_t s) {
+    hipLaunchKernelGGL(k_env_refill<SP>, dim3((E.n + BLK * RS_SPAN - 1) / (BLK * RS_SPAN)), dim3(BLK), 0, s, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_env_refill(const EnvDev &E, hipStream_t s) {
+    return E.sp == 16 ? launch_refill_sp<16>(E, s) : launch_refill_sp<32>(E, s);
+}
 
 hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s) {
     const dim3 grid((E.n + BLK - 1) / BLK), block(BLK);
@@ -901,30 +795,18 @@ hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs,
         hipLaunchKernelGGL(k_env_reset<16>, grid, block, 0, s, E, mask, obs);
     else
         hipLaunchKernelGGL(k_env_reset<32>, grid, block, 0, s, E, mask, obs);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    return e != hipSuccess ? e : launch_env_refill(E, s);
 }
 
-template <int SP>
-static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t s) {
+hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s) {
     const dim3 grid((E.n + SBLK - 1) / SBLK), block(SBLK);
-    if (O.autoreset && O.n_steps == 1) {  // resets deferred to the packed k_env_autoreset
-        hipLaunchKernelGGL((k_env_step<SP, true>), grid, block, 0, s, E, O);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        if (E.n >= (1 << 18)) {  // many envs: 4 groups of 64 per wave keep the launch small
-            hipLaunchKernelGGL((k_env_autoreset<SP, 4>), dim3((E.n + 4 * BLK - 1) / (4 * BLK)), dim3(BLK), 0, s, E,
-                               O.obs);
-        } else {
-            hipLaunchKernelGGL((k_env_autoreset<SP, 1>), dim3((E.n + BLK - 1) / BLK), dim3(BLK), 0, s, E, O.obs);
-        }
-    } else {
-        hipLaunchKernelGGL((k_env_step<SP, false>), grid, block, 0, s, E, O);
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_env_step(const EnvDev &E, const StepOut &O, hipStream_t s) {
-    return E.sp == 16 ? launch_step_sp<16>(E, O, s) : launch_step_sp<32>(E, O, s);
+    if (E.sp == 16)
+        hipLaunchKernelGGL(k_env_step<16>, grid, block, 0, s, E, O);
+    else
+        hipLaunchKernelGGL(k_env_step<32>, grid, block, 0, s, E, O);
+    hipError_t e = hipGetLastError();
+    return (e != hipSuccess || !refill) ? e : launch_env_refill(E, s);
 }
 
 }  // namespace merlin

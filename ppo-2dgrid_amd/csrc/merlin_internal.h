@@ -20,8 +20,9 @@ namespace merlin {
 //   ep_len  int32[n]
 //   visited uint32[n][SP]   exploration-bonus visit bitmask (only if enabled)
 //   err     uint32[2]       device error bits, fallback-map counter
-//   rflag   uint8[n]        1 = the env's episode ended in the last single-step launch (its
-//                           auto-reset is deferred to k_env_autoreset)
+//   pg_*    the env's look-ahead map (merlin_env.hip k_env_refill): pg_walls uint32[n][SP],
+//           pg_agent uint4[n] (agent format above), pg_rng_s / pg_rng_b (RNG state after it),
+//           pg_valid uint8[n] (1 = the slot holds the env's next map)
 struct EnvDev {
     int n, size, sp, difficulty, max_steps;
     int stuck_on, max_stay;
@@ -38,8 +39,15 @@ struct EnvDev {
     int32_t *ep_len;
     uint32_t *visited;
     uint32_t *err;
-    uint8_t *rflag;
+    uint32_t *pg_walls;
+    uint4 *pg_agent;
+    ulonglong2 *pg_rng_s;
+    uint2 *pg_rng_b;
+    uint8_t *pg_valid;
 };
+
+// step launches between two look-ahead refills (merlin_env_step)
+constexpr int REFILL_EVERY = 16;
 
 struct StepOut {
     const int64_t *actions;
@@ -56,7 +64,8 @@ struct StepOut {
 };
 
 hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s);
-hipError_t launch_env_step(const EnvDev &E, const StepOut &O, hipStream_t s);
+hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s);
+hipError_t launch_env_refill(const EnvDev &E, hipStream_t s);
 hipError_t upload_atlas(const uint8_t *atlas_host);
 hipError_t launch_obs_expand_f32(const uint32_t *codes, const int64_t *index, int64_t n, float *out,
                                  float scale, int layout, hipStream_t s);
