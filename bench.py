@@ -168,10 +168,14 @@ def env_only_tier(torch, MerlinVecEnv, n, T, difficulty, size, device):
 
 def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=16):
     """Tier E at HBM scale: 2M envs (0.35 GB of env state and outputs per step),
-    T single-step k_env_step launches on pre-generated actions, 168 algorithmic bytes per
-    env-step (merlin.envs.ENV_STEP_BYTES); at the bench's 4096 envs the kernel is latency-bound
-    (64 waves on 256 CUs), here it streams.  T = 16 = one look-ahead map refill (every 16 step
-    launches, csrc/merlin_env.hip k_env_refill) inside the timed steps."""
+    T single-step launches on pre-generated actions, 168 algorithmic bytes per env-step
+    (merlin.envs.ENV_STEP_BYTES); at the bench's 4096 envs the kernel is latency-bound (64 waves on
+    256 CUs), here it streams.  Two timings of the same T steps:
+      roofline   k_env_step alone (autoreset off: no resets, nothing else launched) -> HBM fraction;
+      with_resets  auto-reset on: each launch is k_env_step + k_env_fallback (the resets whose
+                 look-ahead map slot was already used since the last refill -- at 2M envs some every
+                 step, each a one-thread map generation of tens of microseconds) + k_env_refill every
+                 16 launches (T = 16 = one refill inside the timed steps)."""
     from merlin.envs import ENV_STEP_BYTES
 
     env = MerlinVecEnv(n, difficulty=difficulty, size=size, seed=31337, device=device)
@@ -184,13 +188,19 @@ def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=1
     done = torch.empty((T, n), dtype=torch.float32, device=device)
     env.step_into(acts[0], obs[0], rew[0], None, None, done[0])
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for t in range(T):
-        env.step_into(acts[t], obs[t], rew[t], None, None, done[t])
-    e1.record()
-    torch.cuda.synchronize()
-    sec = e0.elapsed_time(e1) / 1e3
+
+    def timed(autoreset):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for t in range(T):
+            env.step_into(acts[t], obs[t], rew[t], None, None, done[t], autoreset=autoreset)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3
+
+    sec_reset = timed(True)
+    resets = int(done.sum())
+    sec = timed(False)  # truncated envs stay done (no reset): same bytes per env-step
     env.errors()
     env.close()
     rate = T * n / sec
@@ -198,7 +208,9 @@ def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=1
     return {"kernel": "k_env_step", "num_envs": n, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_env_step_large"),
             "env_steps_per_s": round(rate, 1), "bytes_per_launch": n * ENV_STEP_BYTES,
-            "avg_launch_us": round(sec / T * 1e6, 2), "launches": T}
+            "avg_launch_us": round(sec / T * 1e6, 2), "launches": T,
+            "with_resets": {"env_steps_per_s": round(T * n / sec_reset, 1),
+                            "us_per_step": round(sec_reset / T * 1e6, 2), "resets": resets}}
 
 
 def cpu_baseline():

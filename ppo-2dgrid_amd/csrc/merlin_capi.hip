@@ -303,6 +303,8 @@ int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
     alloc((void **)&d.pg_rng_s, n * sizeof(ulonglong2));
     alloc((void **)&d.pg_rng_b, n * sizeof(uint2));
     alloc((void **)&d.pg_valid, n * sizeof(uint8_t));
+    alloc((void **)&d.rflag, n * sizeof(uint8_t));
+    alloc((void **)&d.bflag, (n + 255) / 256);
     if (d.explore_on) alloc((void **)&d.visited, n * d.sp * sizeof(uint32_t));
     if (err != hipSuccess) {
         merlin_env_destroy(e);
@@ -316,7 +318,7 @@ int merlin_env_destroy(merlin_env *e) {
     if (!e) return MERLIN_OK;
     merlin::EnvDev &d = e->dev;
     void *ptrs[] = {d.walls, d.agent, d.rng_s, d.rng_i, d.rng_b, d.ep_ret, d.ep_len, d.err, d.visited,
-                    d.pg_walls, d.pg_agent, d.pg_rng_s, d.pg_rng_b, d.pg_valid};
+                    d.pg_walls, d.pg_agent, d.pg_rng_s, d.pg_rng_b, d.pg_valid, d.rflag, d.bflag};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete e;

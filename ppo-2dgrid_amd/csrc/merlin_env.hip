@@ -547,15 +547,17 @@ __device__ __forceinline__ void reset_visited(const EnvDev &E, int i, int ax, in
 
 // Look-ahead maps.  An env's next map depends only on its RNG stream (MiniGridEnv.reset draws nothing
 // else), so k_env_refill generates it ahead of time into the env's slot (pg_*: the rows, agent, goal
-// and the RNG state after the generation) and a reset just takes the slot: the step kernel never stalls
-// a wave on a map generation (rejection sampling + flood fill, tens of microseconds for one env), and
-// the refill -- which is latency-bound on its slowest env -- runs once per REFILL_EVERY step launches
-// instead of once per step.  A reset whose slot is empty (a second episode end before a refill, or a
-// reseed) generates the same map in place from the env's RNG.  In reseed mode (every reset is
+// and the RNG state after the generation) and a reset just takes the slot: the single-step kernel
+// carries no map-generation code (lean registers, no wave stalled on one env's rejection sampling +
+// flood fill), and the refill -- latency-bound on its slowest env -- runs once per REFILL_EVERY step
+// launches instead of once per step.  A reset whose slot is empty (a second episode end before a
+// refill, or a reseed) generates the same map from the env's RNG: in place in the reset and
+// multi-step kernels, in k_env_fallback after a single-step launch.  In reseed mode (every reset is
 // reset(seed=task_seed)) the slot is never consumed and the env's RNG never advances.
-template <int SP, int NB, bool INL>
-__device__ __forceinline__ void take_map(const EnvDev &E, int i, uint32_t (*rows)[NB], int lane, GenOut &g) {
-    if (E.pg_valid[i]) {
+template <int SP, int NB>
+__device__ __forceinline__ bool take_slot(const EnvDev &E, int i, uint32_t (*rows)[NB], int lane, GenOut &g) {
+    if (!E.pg_valid[i]) return false;
+    {
         const uint4 *src = reinterpret_cast<const uint4 *>(E.pg_walls + (size_t)i * SP);
 #pragma unroll
         for (int q = 0; q < SP / 4; q++) {
@@ -577,7 +579,13 @@ __device__ __forceinline__ void take_map(const EnvDev &E, int i, uint32_t (*rows
             E.rng_b[i] = E.pg_rng_b[i];
             E.pg_valid[i] = 0;
         }
-    } else {
+    }
+    return true;
+}
+
+template <int SP, int NB, bool INL>
+__device__ __forceinline__ void take_map(const EnvDev &E, int i, uint32_t (*rows)[NB], int lane, GenOut &g) {
+    if (!take_slot<SP, NB>(E, i, rows, lane, g)) {
         Rng r = load_rng(E, i);
         if (INL)
             generate_map_inl<SP, NB>(rows, lane, E.size, E.difficulty, r, E.err + 1, g);
@@ -675,7 +683,51 @@ __global__ __launch_bounds__(BLK) void k_env_refill(EnvDev E) {
     if (lane < nq) refill_one<SP>(E, queue[lane], rows, lane);
 }
 
+// The resets of a single-step launch whose look-ahead slot was empty: one wave per 64 step blocks reads
+// their block flags, packs the flagged envs of all flagged blocks onto lanes and regenerates them 64 at
+// a time (reset_one: map, state, first observation into the step's obs row), clearing the flags.
+// Generation is latency-bound on one thread, so the envs share one pass instead of one per block.
 template <int SP>
+__global__ __launch_bounds__(BLK) void k_env_fallback(EnvDev E, uint32_t *__restrict__ obs) {
+    __shared__ uint32_t rows[SP][BLK];
+    __shared__ int queue[BLK];
+    const int lane = threadIdx.x;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const int nblocks = (E.n + SBLK - 1) / SBLK;
+    const int b0 = blockIdx.x * BLK;
+    const bool flagged = b0 + lane < nblocks && E.bflag[b0 + lane];
+    unsigned long long bm = __ballot(flagged);
+    if (flagged) E.bflag[b0 + lane] = 0;
+    int nq = 0;  // wave-uniform
+    while (bm) {
+        const int sb = b0 + __builtin_ctzll(bm);
+        bm &= bm - 1;
+        for (int q = 0; q < SBLK / BLK; q++) {
+            const int i = sb * SBLK + q * BLK + lane;
+            const bool need = i < E.n && E.rflag[i];
+            const unsigned long long m = __ballot(need);
+            const int c = __popcll(m);
+            if (c == 0) continue;
+            if (nq + c > BLK) {  // the queue is full: run it first
+                if (lane < nq) reset_one<SP>(E, queue[lane], rows, lane, obs);
+                nq = 0;
+                __syncthreads();
+            }
+            if (need) {
+                E.rflag[i] = 0;
+                queue[nq + __popcll(m & below)] = i;
+            }
+            nq += c;
+            __syncthreads();
+        }
+    }
+    if (lane < nq) reset_one<SP>(E, queue[lane], rows, lane, obs);
+}
+
+// DEFER (single-step launches): a reset takes the env's look-ahead slot; when the slot is empty the env
+// is flagged (rflag, and its 256-env block in bflag) and k_env_fallback, launched next on the stream,
+// generates its map and writes its observation, so this kernel carries no generator (lean registers).
+template <int SP, bool DEFER>
 __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
     __shared__ uint32_t rows[SP][SBLK];
     const int lane = threadIdx.x;
@@ -748,7 +800,16 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
         }
         if (done && O.autoreset) {
             GenOut g;
-            take_map<SP, SBLK, false>(E, i, rows, lane, g);
+            if constexpr (DEFER) {
+                if (!take_slot<SP, SBLK>(E, i, rows, lane, g)) {
+                    E.rflag[i] = 1;
+                    E.bflag[blockIdx.x] = 1;
+                    if (err) atomicOr(E.err, err);
+                    return;
+                }
+            } else {
+                take_map<SP, SBLK, false>(E, i, rows, lane, g);
+            }
             ax = g.ax;
             ay = g.ay;
             dir = g.dir;
@@ -799,13 +860,24 @@ hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs,
     return e != hipSuccess ? e : launch_env_refill(E, s);
 }
 
+template <int SP>
+static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t s) {
+    const int nb = (E.n + SBLK - 1) / SBLK;
+    if (!O.autoreset) {  // no resets: the lean kernel
+        hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
+    } else if (O.n_steps == 1) {  // empty look-ahead slots reset in k_env_fallback
+        hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_env_fallback<SP>, dim3((nb + BLK - 1) / BLK), dim3(BLK), 0, s, E, O.obs);
+    } else {
+        hipLaunchKernelGGL((k_env_step<SP, false>), dim3(nb), dim3(SBLK), 0, s, E, O);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s) {
-    const dim3 grid((E.n + SBLK - 1) / SBLK), block(SBLK);
-    if (E.sp == 16)
-        hipLaunchKernelGGL(k_env_step<16>, grid, block, 0, s, E, O);
-    else
-        hipLaunchKernelGGL(k_env_step<32>, grid, block, 0, s, E, O);
-    hipError_t e = hipGetLastError();
+    hipError_t e = E.sp == 16 ? launch_step_sp<16>(E, O, s) : launch_step_sp<32>(E, O, s);
     return (e != hipSuccess || !refill) ? e : launch_env_refill(E, s);
 }
 

@@ -23,6 +23,8 @@ namespace merlin {
 //   pg_*    the env's look-ahead map (merlin_env.hip k_env_refill): pg_walls uint32[n][SP],
 //           pg_agent uint4[n] (agent format above), pg_rng_s / pg_rng_b (RNG state after it),
 //           pg_valid uint8[n] (1 = the slot holds the env's next map)
+//   rflag   uint8[n]        1 = reset due, its slot was empty (single-step launch; k_env_fallback)
+//   bflag   uint8[ceil(n/256)] 1 = some env of that 256-env step block is flagged
 struct EnvDev {
     int n, size, sp, difficulty, max_steps;
     int stuck_on, max_stay;
@@ -44,6 +46,8 @@ struct EnvDev {
     ulonglong2 *pg_rng_s;
     uint2 *pg_rng_b;
     uint8_t *pg_valid;
+    uint8_t *rflag;
+    uint8_t *bflag;
 };
 
 // step launches between two look-ahead refills (merlin_env_step)

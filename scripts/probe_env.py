@@ -17,7 +17,8 @@ def main():
         env.reset()
         g = torch.Generator(device=dev)
         g.manual_seed(9)
-        T = 12
+        T = 32
+        used = torch.zeros(n, dtype=torch.bool, device=dev)  # slot consumed since the last refill
         acts = torch.randint(0, 3, (T, n), device=dev, generator=g)
         obs = torch.empty((T, n, 8), dtype=torch.int32, device=dev)
         rew = torch.empty((T, n), dtype=torch.float32, device=dev)
@@ -28,8 +29,13 @@ def main():
             env.step_into(acts[t], obs[t], rew[t], None, None, done[t])
             e1.record()
             torch.cuda.synchronize()
-            print(f"n={n} step {t}: resets {int(done[t].sum())} ({float(done[t].mean()) * 100:.3f} %) "
-                  f"step+autoreset {e0.elapsed_time(e1) * 1e3:.1f} us", flush=True)
+            d = done[t] > 0
+            fb = int((d & used).sum())
+            used |= d
+            if (t + 1) % 16 == 0:
+                used.zero_()
+            print(f"n={n} step {t}: resets {int(d.sum())} ({float(done[t].mean()) * 100:.3f} %) "
+                  f"empty-slot resets {fb} step+autoreset {e0.elapsed_time(e1) * 1e3:.1f} us", flush=True)
         env.errors()
         env.close()
 
