@@ -14,4 +14,10 @@ if [ -n "$PMC" ]; then
         > "$R/gpurun_out/prof_pmc_$C.log" 2>&1 || exit $?
     echo "pmc $C done"
   done
+  for C in FETCH_SIZE WRITE_SIZE; do  # the HBM-scale env tier alone (2M envs) -> k_env_step_large
+    timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "k_env_step" -T -f csv \
+        -d "$R/gpurun_out/prof_pmcenv_$C" -o run -- python "$R/bench.py" --env-tier-only \
+        > "$R/gpurun_out/prof_pmcenv_$C.log" 2>&1 || exit $?
+    echo "pmc env $C done"
+  done
 fi

@@ -102,6 +102,10 @@ def _loss(lp, ent, v):
 
 
 def test_evaluate_windows_matches_frames(device):
+    """evaluate_windows (conv2/conv3 once per distinct window) against the reference-structured frame
+    path (rendered frames through the F.conv2d towers) computed in float64: outputs and every
+    parameter's gradient.  (float64 is the yardstick: the fp32 MIOpen path itself drifts by 1e-3 on the
+    conv-1 weight gradient with the FAST find mode the suite runs under, tests/conftest.py.)"""
     from merlin import _native as nat
     from merlin.actor_critic import CNNActorCritic
 
@@ -113,16 +117,22 @@ def test_evaluate_windows_matches_frames(device):
     lp1, e1, v1 = ac.evaluate_windows(plan, plan.minibatch(mb_idx), acts)
     _loss(lp1, e1, v1).backward()
     g1 = [p.grad.clone() for p in ac.parameters()]
-    ac.zero_grad()
-    frames = nat.expand_obs(codes, index=mb_idx, scale=1.0 / 255.0)
-    lp2, e2, v2 = ac.evaluate(frames, acts, prescaled=True)
+    ac64 = CNNActorCritic((56, 56, 3), 3).to(device)
+    ac64.load_state_dict(ac.state_dict())
+    ac64.double()
+    frames = nat.expand_obs(codes, index=mb_idx, scale=1.0 / 255.0).double()
+    logits = ac64.actor(ac64.actor_extractor(frames, prescaled=True))
+    v2 = ac64.critic(ac64.critic_extractor(frames, prescaled=True)).squeeze(-1)
+    logp = logits.log_softmax(-1)
+    lp2 = logp.gather(-1, acts[:, None]).squeeze(-1)
+    e2 = -(logp.exp() * logp).sum(-1)
     _loss(lp2, e2, v2).backward()
-    g2 = [p.grad.clone() for p in ac.parameters()]
-    torch.testing.assert_close(lp1, lp2, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(e1, e2, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(v1, v2, rtol=1e-5, atol=1e-5)
+    g2 = [p.grad for p in ac64.parameters()]
+    torch.testing.assert_close(lp1.double(), lp2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(e1.double(), e2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(v1.double(), v2, rtol=1e-5, atol=1e-5)
     for (name, _), a, b in zip(ac.named_parameters(), g1, g2):
-        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+        rel = ((a.double() - b).norm() / b.norm().clamp_min(1e-30)).item()
         assert rel < 1e-4, (name, rel)
 
 
