@@ -148,6 +148,17 @@ int merlin_env_step(merlin_env *env, const int64_t *actions_dev, int32_t n_steps
                     uint8_t *terminated_dev, uint8_t *truncated_dev, float *done_dev,
                     double *ep_return_dev, int32_t *ep_length_dev, int32_t autoreset,
                     void *stream);
+/* Look-ahead maps (no reference counterpart: an implementation detail of the auto-reset above).
+ * An env's next map depends only on its RNG stream, so it is generated ahead of time into a
+ * per-env slot, and an auto-reset takes the slot instead of generating in the step.
+ * merlin_env_reset refills every slot before it returns; merlin_env_step refills the used slots
+ * every `every` step calls (default 16).  every = 0 hands the refills to the caller:
+ * merlin_env_refill launches one on `stream` -- e.g. on a side stream after each step, joined
+ * before the next step, so the (latency-bound) map generation overlaps the policy forward.  A
+ * reset whose slot is empty generates its map in the step instead; results are identical
+ * either way. */
+int merlin_env_set_refill_interval(merlin_env *env, int32_t every);
+int merlin_env_refill(merlin_env *env, void *stream);
 /* [sync] copy env state to host: walls uint32[N][size] (bit x of row y = wall at
  * (x,y)); agent int32[N][8] = (x, y, dir, step_count, goal_x, goal_y, stay, 0);
  * rng uint64[N][5] = (state_hi, state_lo, inc_hi, inc_lo, has32<<32|buf32).

@@ -14,6 +14,7 @@ struct merlin_env {
     int device;
     bool has_state;
     int steps_since_refill;  // merlin_env_step launches since the last look-ahead refill
+    int refill_every;        // 0: the caller launches refills (merlin_env_refill)
 };
 
 namespace {
@@ -271,6 +272,7 @@ int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
     int rc = device_ws(&ws);
     if (rc) return rc;
     merlin_env *e = new merlin_env();
+    e->refill_every = merlin::REFILL_EVERY;
     merlin::EnvDev &d = e->dev;
     d.n = cfg->num_envs;
     d.size = cfg->size;
@@ -381,9 +383,23 @@ int merlin_env_step(merlin_env *e, const int64_t *actions, int32_t n_steps, int6
     o.done = done;
     o.ep_ret_out = ep_ret;
     o.ep_len_out = ep_len;
-    const bool refill = ++e->steps_since_refill >= merlin::REFILL_EVERY;
+    const bool refill = e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
     if (refill) e->steps_since_refill = 0;
     HIP_TRY(merlin::launch_env_step(e->dev, o, refill, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_env_set_refill_interval(merlin_env *e, int32_t every) {
+    if (!e) return fail(MERLIN_E_INVALID, "null env");
+    if (every < 0) return fail(MERLIN_E_INVALID, "refill interval must be >= 0");
+    e->refill_every = every;
+    e->steps_since_refill = 0;
+    return MERLIN_OK;
+}
+
+int merlin_env_refill(merlin_env *e, void *stream) {
+    if (!e) return fail(MERLIN_E_INVALID, "null env");
+    HIP_TRY(merlin::launch_env_refill(e->dev, false, (hipStream_t)stream));
     return MERLIN_OK;
 }
 

@@ -623,11 +623,11 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
     reset_one<SP>(E, i, rows, lane, obs);
 }
 
-// Fill the empty look-ahead slots: each one-wave block takes RS_SPAN x 64 envs (lane l reads the slot
-// flags of envs base + RS_SPAN*l .. in one 16-B load), packs the empty ones onto consecutive lanes
+// Fill the empty look-ahead slots: each one-wave block takes SPAN x 64 envs (SPAN 16: lane l reads the
+// slot flags of envs base + 16*l .. in one 16-B load), packs the empty ones onto consecutive lanes
 // (ballot + prefix count) and generates 64 at a time, one thread per env, from the env's RNG (which
-// stays as it is: the slot holds the state after the generation).
-constexpr int RS_SPAN = 16;
+// stays as it is: the slot holds the state after the generation).  SPAN 16 for the few slots a step
+// uses, SPAN 1 (one wave per 64 envs, all generating at once) after a full reset used every slot.
 template <int SP>
 __device__ __forceinline__ void refill_one(const EnvDev &E, int i, uint32_t (*rows)[BLK], int lane) {
     Rng r = load_rng(E, i);
@@ -647,26 +647,27 @@ __device__ __forceinline__ void refill_one(const EnvDev &E, int i, uint32_t (*ro
     if (g.err) atomicOr(E.err, g.err);
 }
 
-template <int SP>
+template <int SP, int SPAN>
 __global__ __launch_bounds__(BLK) void k_env_refill(EnvDev E) {
     __shared__ uint32_t rows[SP][BLK];
     __shared__ int queue[BLK];
     const int lane = threadIdx.x;
     const unsigned long long below = (1ull << lane) - 1ull;
-    const int64_t base = ((int64_t)blockIdx.x * BLK + lane) * RS_SPAN;  // this lane's first env
-    uint32_t fl[RS_SPAN / 4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
-    if (base + RS_SPAN <= E.n) {
+    static_assert(SPAN == 1 || SPAN == 16, "refill span");
+    const int64_t base = ((int64_t)blockIdx.x * BLK + lane) * SPAN;  // this lane's first env
+    uint32_t fl[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
+    if (SPAN == 16 && base + SPAN <= E.n) {
         const uint4 v = *reinterpret_cast<const uint4 *>(E.pg_valid + base);
         fl[0] = v.x;
         fl[1] = v.y;
         fl[2] = v.z;
         fl[3] = v.w;
     } else {
-        for (int b = 0; b < RS_SPAN; b++)
+        for (int b = 0; b < SPAN; b++)
             if (base + b < E.n && !E.pg_valid[base + b]) fl[b >> 2] &= ~(0xffu << (8 * (b & 3)));
     }
     int nq = 0;  // wave-uniform
-    for (int b = 0; b < RS_SPAN; b++) {
+    for (int b = 0; b < SPAN; b++) {
         const bool need = !((fl[b >> 2] >> (8 * (b & 3))) & 0xffu);
         const unsigned long long m = __ballot(need);
         const int c = __popcll(m);
@@ -841,13 +842,16 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
 }  // namespace
 
 template <int SP>
-static hipError_t launch_refill_sp(const EnvDev &E, hipStream_t s) {
-    hipLaunchKernelGGL(k_env_refill<SP>, dim3((E.n + BLK * RS_SPAN - 1) / (BLK * RS_SPAN)), dim3(BLK), 0, s, E);
+static hipError_t launch_refill_sp(const EnvDev &E, bool full, hipStream_t s) {
+    if (full)
+        hipLaunchKernelGGL((k_env_refill<SP, 1>), dim3((E.n + BLK - 1) / BLK), dim3(BLK), 0, s, E);
+    else
+        hipLaunchKernelGGL((k_env_refill<SP, 16>), dim3((E.n + BLK * 16 - 1) / (BLK * 16)), dim3(BLK), 0, s, E);
     return hipGetLastError();
 }
 
-hipError_t launch_env_refill(const EnvDev &E, hipStream_t s) {
-    return E.sp == 16 ? launch_refill_sp<16>(E, s) : launch_refill_sp<32>(E, s);
+hipError_t launch_env_refill(const EnvDev &E, bool full, hipStream_t s) {
+    return E.sp == 16 ? launch_refill_sp<16>(E, full, s) : launch_refill_sp<32>(E, full, s);
 }
 
 hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s) {
@@ -857,7 +861,7 @@ hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs,
     else
         hipLaunchKernelGGL(k_env_reset<32>, grid, block, 0, s, E, mask, obs);
     hipError_t e = hipGetLastError();
-    return e != hipSuccess ? e : launch_env_refill(E, s);
+    return e != hipSuccess ? e : launch_env_refill(E, mask == nullptr, s);
 }
 
 template <int SP>
@@ -878,7 +882,7 @@ static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t 
 
 hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s) {
     hipError_t e = E.sp == 16 ? launch_step_sp<16>(E, O, s) : launch_step_sp<32>(E, O, s);
-    return (e != hipSuccess || !refill) ? e : launch_env_refill(E, s);
+    return (e != hipSuccess || !refill) ? e : launch_env_refill(E, false, s);
 }
 
 }  // namespace merlin

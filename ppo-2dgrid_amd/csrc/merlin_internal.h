@@ -69,7 +69,7 @@ struct StepOut {
 
 hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s);
 hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s);
-hipError_t launch_env_refill(const EnvDev &E, hipStream_t s);
+hipError_t launch_env_refill(const EnvDev &E, bool full, hipStream_t s);
 hipError_t upload_atlas(const uint8_t *atlas_host);
 hipError_t launch_obs_expand_f32(const uint32_t *codes, const int64_t *index, int64_t n, float *out,
                                  float scale, int layout, hipStream_t s);

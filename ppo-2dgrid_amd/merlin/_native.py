@@ -70,6 +70,8 @@ def lib():
     L.merlin_env_seed.argtypes = [vp, u64p, i32, vp]
     L.merlin_env_reset.argtypes = [vp, vp, vp, vp]
     L.merlin_env_step.argtypes = [vp, vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, i32, vp]
+    L.merlin_env_set_refill_interval.argtypes = [vp, i32]
+    L.merlin_env_refill.argtypes = [vp, vp]
     L.merlin_env_get_state.argtypes = [vp, vp, vp, vp, vp]
     L.merlin_env_errors.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), vp]
     L.merlin_obs_expand_f32.argtypes = [vp, vp, i64, vp, C.c_float, i32, vp]
@@ -125,6 +127,7 @@ def check_env_config_layout(L) -> None:
 EXPORTED_SYMBOLS = (
     "merlin_version", "merlin_last_error", "merlin_tile_atlas", "merlin_env_config_layout", "merlin_env_create",
     "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step",
+    "merlin_env_set_refill_interval", "merlin_env_refill",
     "merlin_env_get_state", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
     "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
     "merlin_conv1_lut_fwd", "merlin_conv1_lut_bwd", "merlin_tower_conv2_im2col_fwd",

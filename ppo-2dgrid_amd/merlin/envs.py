@@ -166,6 +166,18 @@ class MerlinVecEnv:
                 nat.ptr(term), nat.ptr(trunc), nat.ptr(done), nat.ptr(ep_return), nat.ptr(ep_length),
                 int(bool(autoreset)), self._stream), "merlin_env_step")
 
+    def set_refill_interval(self, every: int) -> None:
+        """Refill the used look-ahead map slots every `every` step calls (default 16); 0 leaves the
+        refills to the caller's refill() (merlin_env_set_refill_interval)."""
+        nat.check(self._lib.merlin_env_set_refill_interval(self._h, int(every)), "merlin_env_set_refill_interval")
+
+    def refill(self) -> None:
+        """Generate the next map of every env whose look-ahead slot was used, on the current stream
+        (merlin_env_refill).  Touches only the slots and reads the envs' RNG: it may run on a side
+        stream beside work that does not step this env, joined before the next step."""
+        with torch.cuda.device(self.device):
+            nat.check(self._lib.merlin_env_refill(self._h, self._stream), "merlin_env_refill")
+
     def step(self, actions: torch.Tensor, autoreset: bool = True):
         """gym-vector style step: returns (obs codes, reward, terminated, truncated, info).
 

@@ -117,6 +117,11 @@ class PPO:
             self.buf = CodeRolloutBuffer(self.k_steps, N, self.device)
             self._obs_step = torch.empty((N, 3, 56, 56), dtype=torch.float32, device=self.device)
             self._mb_obs = None
+            # look-ahead map refills on a side stream after every step, overlapping the next act
+            # (MerlinVecEnv.refill; the env's own every-16-steps refill is switched off)
+            self._refill_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+            if self._refill_stream is not None:
+                self.vec.set_refill_interval(0)
         else:
             sample_obs, _ = env.reset()
             self.num_envs, self.k_steps, self.batch_size = 1, batch_size, batch_size
@@ -162,18 +167,29 @@ class PPO:
 
     def _rollout_body(self):
         """ppo.py:64-105 for N envs: reset (ppo.py:65: every rollout starts from a fresh
-        reset), T x (act -> env step writing into the [T][N] storage), bootstrap value."""
+        reset), T x (act -> env step writing into the [T][N] storage), bootstrap value.
+        After each step the used look-ahead map slots are refilled on a side stream, beside the
+        next act (which reads only the obs codes), and joined before the next step."""
         buf, env = self.buf, self.vec
         T = buf.T
+        main, side = torch.cuda.current_stream(self.device), self._refill_stream
         env.reset(out=buf.codes[0])
         with torch.no_grad():
             self._act_epoch.add_(1)
             pack = self.ac.rollout_pack() if self.conv1_from_codes else None
             for t in range(T):
                 self._act(buf.codes[t], pack, t, out=(buf.actions[t], buf.logprobs[t], buf.values[t]))
+                if side is not None and t > 0:
+                    main.wait_stream(side)
                 env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
                               buf.ep_return[t], buf.ep_length[t])
+                if side is not None:
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        env.refill()
             _, _, last_value = self._act(buf.codes[T], pack, T)
+            if side is not None:
+                main.wait_stream(side)
             buf.last_value.copy_(last_value)
 
     def _capture_rollout(self):

@@ -21,3 +21,7 @@ if [ -n "$PMC" ]; then
     echo "pmc env $C done"
   done
 fi
+# summaries on the box (the raw per-launch CSVs exceed what gpurun copies back), then drop the raw files
+cd "$R" && python scripts/prof_summary.py "${TAG:-r02}" gpurun_out/summary || exit $?
+cp gpurun_out/prof_trace.log gpurun_out/summary/ 2>/dev/null
+rm -f gpurun_out/prof_*/run_kernel_trace.csv gpurun_out/prof_*/run_counter_collection.csv

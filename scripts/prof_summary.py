@@ -1,7 +1,7 @@
 """Turn rocprofv3 outputs under gpurun_out/ into the committed profiles/ summaries.
 
-    python scripts/prof_summary.py <tag>
-writes profiles/<tag>_kernel_stats.md (+ .csv copy) from the --kernel-trace --stats pass and
+    python scripts/prof_summary.py <tag> [dest]
+writes <dest, default profiles>/<tag>_kernel_stats.md (+ .csv copy) from the --kernel-trace --stats pass and
 profiles/<tag>_pmc.json from the FETCH_SIZE / WRITE_SIZE passes: per kernel, the mean over
 its largest-grid launches, HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950:
 FETCH_SIZE counts half of a wide coalesced read stream, MI355X_MICROARCH.md §HBM).
@@ -14,6 +14,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
+DEST = os.path.join(REPO, "profiles")
 
 
 def stats(tag):
@@ -29,9 +30,9 @@ def stats(tag):
     for r in rows[:40]:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
                      f"{float(r['Percentage']):.2f} | {float(r['AverageNs']) / 1e3:.2f} |")
-    os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
-    open(os.path.join(REPO, "profiles", f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
-    shutil.copy(src, os.path.join(REPO, "profiles", f"{tag}_kernel_stats.csv"))
+    os.makedirs(DEST, exist_ok=True)
+    open(os.path.join(DEST, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
+    shutil.copy(src, os.path.join(DEST, f"{tag}_kernel_stats.csv"))
 
 
 def pmc(tag):
@@ -47,7 +48,7 @@ def pmc(tag):
         if "fetch_size_kb" in d and "write_size_kb" in d:
             d["hbm_bytes_per_launch"] = int((2 * d["fetch_size_kb"] + d["write_size_kb"]) * 1024)
     if res:
-        json.dump(res, open(os.path.join(REPO, "profiles", f"{tag}_pmc.json"), "w"), indent=1)
+        json.dump(res, open(os.path.join(DEST, f"{tag}_pmc.json"), "w"), indent=1)
 
 
 def collect(res, src, counter, rename):
@@ -66,6 +67,8 @@ def collect(res, src, counter, rename):
 
 if __name__ == "__main__":
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    if len(sys.argv) > 2:
+        DEST = os.path.abspath(sys.argv[2])
     stats(tag)
     pmc(tag)
     print("wrote profiles for", tag)

@@ -125,6 +125,49 @@ def test_large_batch_vs_oracle(oracle, device, diff, size):
     assert (st["agent_pos"] == oagent[-1][:, 0:2]).all() and (st["agent_dir"] == oagent[-1][:, 2]).all()
 
 
+@pytest.mark.parametrize("mode", ["never", "side_stream_every_step", "every_step", "multistep"])
+def test_lookahead_refill_modes_vs_oracle(oracle, device, mode):
+    """The look-ahead map slots (merlin_env_set_refill_interval / merlin_env_refill) never change
+    results: with no refills at all (every later reset generates in k_env_fallback), a refill on a
+    side stream after every step (PPO's rollout), the library's own refill after every step, and
+    n_steps > 1 launches (resets generate in the step kernel) -- all equal the C oracle.  Short
+    episodes (max_steps 6, forward-biased actions) so envs reset several times per refill window."""
+    n, T, max_steps = 2048, 64, 6
+    rs = np.random.RandomState(5)
+    acts = rs.choice([0, 1, 2], size=(T, n), p=[0.1, 0.1, 0.8]).astype(np.int64)
+    env = make_env(n, "mediumhard", 16, 4242, device, max_steps=max_steps)
+    env.set_refill_interval({"never": 0, "side_stream_every_step": 0, "every_step": 1, "multistep": 16}[mode])
+    env.reset()
+    codes = torch.zeros((T, n, 8), dtype=torch.int32, device=device)
+    rew = torch.zeros((T, n), dtype=torch.float32, device=device)
+    done = torch.zeros((T, n), dtype=torch.float32, device=device)
+    ta = torch.from_numpy(acts).to(device)
+    if mode == "multistep":
+        env.step_into(ta, codes, rew, None, None, done, n_steps=T, action_stride=n)
+    else:
+        main, side = torch.cuda.current_stream(device), torch.cuda.Stream(device)
+        for t in range(T):
+            if mode == "side_stream_every_step" and t > 0:
+                main.wait_stream(side)
+            env.step_into(ta[t].contiguous(), codes[t], rew[t], None, None, done[t])
+            if mode == "side_stream_every_step":
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    env.refill()
+        main.wait_stream(side)
+    torch.cuda.synchronize(device)
+    ocodes, orew, oterm, otrunc, _ = oracle.batch_rollout(np.arange(4242, 4242 + n, dtype=np.uint64), acts,
+                                                          size=16, difficulty="mediumhard", max_steps=max_steps)
+    assert (unpack(codes) == ocodes[1:]).all()
+    assert (rew.cpu().numpy() == orew).all()
+    assert (done.cpu().numpy() == np.maximum(oterm, otrunc)).all()
+    # several resets of one env inside 16 steps (the slot is already used): the fallback path ran
+    per_env = np.maximum(oterm, otrunc)[:16].sum(0)
+    assert (per_env >= 2).sum() > n // 2
+    flags, _ = env.errors()
+    assert flags == 0
+
+
 @pytest.mark.parametrize("stuck,explore", [(True, False), (False, True), (True, True)])
 def test_wrapper_flags_vs_oracle(oracle, device, stuck, explore):
     n, T = 512, 120
