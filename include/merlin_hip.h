@@ -278,6 +278,19 @@ int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *id
                        int64_t item_len, const int32_t *fix_dev, int64_t n_fix, int32_t towers,
                        float *out_dev, int64_t out_rows, float *carry_dev, int32_t accumulate,
                        void *stream);
+/* merlin_segment_sum with two options.  mask_dev (float[towers][src_rows][64], or NULL): each
+ * source row is multiplied by the ReLU mask of the same row of mask_dev (src where mask > 0,
+ * else 0: the ReLU backward of a forward output, fused into the gather).  flags:
+ * MERLIN_SEG_ACCUMULATE as accumulate != 0 above; MERLIN_SEG_NO_FILL leaves the rows of
+ * destinations without any (unskipped) entry untouched instead of zeroing them (the caller
+ * knows which rows are live, e.g. merlin/windows.py's patch sums). */
+#define MERLIN_SEG_ACCUMULATE 1
+#define MERLIN_SEG_NO_FILL 2
+int merlin_segment_sum_masked(const float *src_dev, const float *mask_dev, int64_t src_rows,
+                              const int32_t *idx_dev, const int32_t *key_dev, int64_t nnz,
+                              const int32_t *slot_dev, int32_t sub, int64_t item_len,
+                              const int32_t *fix_dev, int64_t n_fix, int32_t towers, float *out_dev,
+                              int64_t out_rows, float *carry_dev, int32_t flags, void *stream);
 
 /* Acting tail (src/actor_critic.py:48-55 act, src/ppo.py:69-71): z float[2][n][hidden] = fc1's
  * pre-activation of the actor / critic tower, b4 float[2][hidden]; h = relu(z + b4); logits =

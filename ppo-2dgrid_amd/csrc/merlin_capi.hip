@@ -616,18 +616,28 @@ int merlin_tower_window_conv3(const float *Q, int64_t nw, const int32_t *wid, co
     return MERLIN_OK;
 }
 
-int merlin_segment_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
-                       const int32_t *slot, int32_t sub, int64_t item_len, const int32_t *fix, int64_t n_fix,
-                       int32_t towers, float *out, int64_t out_rows, float *carry, int32_t accumulate,
-                       void *stream) {
+int merlin_segment_sum_masked(const float *src, const float *mask, int64_t src_rows, const int32_t *idx,
+                              const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub, int64_t item_len,
+                              const int32_t *fix, int64_t n_fix, int32_t towers, float *out, int64_t out_rows,
+                              float *carry, int32_t flags, void *stream) {
     if (!out && out_rows > 0) return fail(MERLIN_E_INVALID, "null output");
     if (nnz > 0 && (!src || !idx || !key || !carry)) return fail(MERLIN_E_INVALID, "null argument");
     if (n_fix > 0 && !fix) return fail(MERLIN_E_INVALID, "null fix-up list");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (item_len <= 0 || sub <= 0) return fail(MERLIN_E_INVALID, "item_len and sub must be > 0");
-    HIP_TRY(merlin::launch_seg_sum(src, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
-                                   out_rows, carry, accumulate ? 1 : 0, (hipStream_t)stream));
+    if (flags & ~(MERLIN_SEG_ACCUMULATE | MERLIN_SEG_NO_FILL)) return fail(MERLIN_E_INVALID, "unknown flags");
+    HIP_TRY(merlin::launch_seg_sum(src, mask, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
+                                   out_rows, carry, (flags & MERLIN_SEG_ACCUMULATE) ? 1 : 0,
+                                   (flags & MERLIN_SEG_NO_FILL) ? 0 : 1, (hipStream_t)stream));
     return MERLIN_OK;
+}
+
+int merlin_segment_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
+                       const int32_t *slot, int32_t sub, int64_t item_len, const int32_t *fix, int64_t n_fix,
+                       int32_t towers, float *out, int64_t out_rows, float *carry, int32_t accumulate,
+                       void *stream) {
+    return merlin_segment_sum_masked(src, nullptr, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers,
+                                     out, out_rows, carry, accumulate ? MERLIN_SEG_ACCUMULATE : 0, stream);
 }
 
 int merlin_act_heads(const float *z, const float *b4, int64_t n, int32_t hidden, const float *w_actor,

@@ -33,6 +33,11 @@ __device__ __forceinline__ void f4_add(float4 &a, const float4 b) {
     a.w += b.w;
 }
 __device__ __forceinline__ float relu_nan(float v) { return v != v ? v : fmaxf(v, 0.0f); }  // torch.relu keeps NaN
+// ReLU backward (threshold_backward): g where y > 0, else 0
+__device__ __forceinline__ float4 f4_mask(const float4 y, const float4 g) {
+    return make_float4(y.x > 0.0f ? g.x : 0.0f, y.y > 0.0f ? g.y : 0.0f, y.z > 0.0f ? g.z : 0.0f,
+                       y.w > 0.0f ? g.w : 0.0f);
+}
 
 // Z2w[t][w][c4] = sum_{k<16} T2[t][rows[w][k]][c4], taps in k_conv2_lut_fwd's order
 __global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ rows, int64_t nw,
@@ -96,9 +101,13 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
 // destination's sum is flushed.  The item's first / last destination, when it continues in the
 // neighbouring item, goes to carry[t][item][0 / 1] instead of out.  With acc_out the sums are
 // added to out (one writer per destination per launch), so a list split by source block into
-// several launches (merlin/windows.py) accumulates in block order.
+// several launches accumulates in block order.  MASK: each source row is first multiplied by the
+// ReLU mask of the same row of `mask` (the forward's output), i.e. the sums are of
+// threshold_backward(src, mask) rows, never materialised.
 constexpr int SEG_WAVES = 4, SEG_UNROLL = 8;
-__global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__restrict__ src, int64_t src_rows,
+template <bool MASK>
+__global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__restrict__ src,
+                                                           const float4 *__restrict__ mask, int64_t src_rows,
                                                            const int32_t *__restrict__ idx,
                                                            const int32_t *__restrict__ key, int64_t nnz,
                                                            const int32_t *__restrict__ slot, int S, int64_t L,
@@ -109,6 +118,7 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
     const int t = lane >> 5, q = (lane >> 4) & 1, c = lane & 15;
     const bool live = t < T;
     const float4 *srct = src + (size_t)(live ? t : 0) * src_rows * 16 + c;
+    const float4 *maskt = MASK ? mask + (size_t)(live ? t : 0) * src_rows * 16 + c : nullptr;
     const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int64_t it = (int64_t)blockIdx.x * SEG_WAVES + wv; it < nitems; it += (int64_t)gridDim.x * SEG_WAVES) {
         const int64_t e0 = it * L, e1 = std::min<int64_t>(nnz, e0 + L);
@@ -169,6 +179,13 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
                 float4 vq[SEG_UNROLL];
 #pragma unroll
                 for (int u = 0; u < SEG_UNROLL; u++) vq[u] = srct[(size_t)rq[u] * 16];
+                if constexpr (MASK) {
+                    float4 mq[SEG_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < SEG_UNROLL; u++) mq[u] = maskt[(size_t)rq[u] * 16];
+#pragma unroll
+                    for (int u = 0; u < SEG_UNROLL; u++) vq[u] = f4_mask(mq[u], vq[u]);
+                }
 #pragma unroll
                 for (int u = 0; u < SEG_UNROLL; u++) {
                     if (k0[u] < 0) break;
@@ -244,16 +261,25 @@ hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, c
     return hipGetLastError();
 }
 
-hipError_t launch_seg_sum(const float *src, int64_t src_rows, const int32_t *idx, const int32_t *key, int64_t nnz,
-                          const int32_t *slot, int S, int64_t L, const int32_t *fix, int64_t nfix, int T, float *out,
-                          int64_t out_rows, float *carry, int acc_out, hipStream_t s) {
-    hipError_t e = acc_out ? hipSuccess : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
+hipError_t launch_seg_sum(const float *src, const float *mask, int64_t src_rows, const int32_t *idx,
+                          const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
+                          int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,
+                          hipStream_t s) {
+    hipError_t e = (acc_out || !fill) ? hipSuccess
+                                      : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
     if (e != hipSuccess || nnz <= 0) return e;
     const int64_t nitems = (nnz + L - 1) / L;
     const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
-    hipLaunchKernelGGL(k_seg_sum, dim3(grid), dim3(64 * SEG_WAVES), 0, s, reinterpret_cast<const float4 *>(src),
-                       src_rows, idx, key, nnz, slot, S, L, nitems, T, reinterpret_cast<float4 *>(out), out_rows,
-                       reinterpret_cast<float4 *>(carry), acc_out);
+    if (mask)
+        hipLaunchKernelGGL(k_seg_sum<true>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
+                           reinterpret_cast<const float4 *>(src), reinterpret_cast<const float4 *>(mask), src_rows,
+                           idx, key, nnz, slot, S, L, nitems, T, reinterpret_cast<float4 *>(out), out_rows,
+                           reinterpret_cast<float4 *>(carry), acc_out);
+    else
+        hipLaunchKernelGGL(k_seg_sum<false>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
+                           reinterpret_cast<const float4 *>(src), nullptr, src_rows, idx, key, nnz, slot, S, L,
+                           nitems, T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry),
+                           acc_out);
     e = hipGetLastError();
     if (e != hipSuccess || nfix <= 0) return e;
     const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);

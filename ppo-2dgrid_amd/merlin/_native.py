@@ -91,6 +91,8 @@ def lib():
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
+    L.merlin_segment_sum_masked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
+                                            vp]
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
@@ -134,7 +136,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
-    "merlin_segment_sum", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
+    "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
 )
 
@@ -425,14 +427,21 @@ def window_conv3(Q, wid, groups, b3):
     return out
 
 
+SEG_ACCUMULATE, SEG_NO_FILL = 1, 2  # include/merlin_hip.h
+
+
 def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum", out=None,
-                accumulate: bool = False, carry=None):
+                accumulate: bool = False, carry=None, mask=None, fill: bool = True):
     """out f32[T, out_rows, 64]: out[t][key] = the sum, in entry order, of src[t][row(e)] over
     the plan's entries e with that key (merlin.windows.SegmentPlan); row(e) = idx[e], or
     slot[idx[e] // sub] * sub + idx[e] % sub with entries whose slot is -1 skipped.  With
-    accumulate the sums are added to `out` (a list split over source blocks, in call order)."""
+    accumulate the sums are added to `out` (a list split over source blocks, in call order).
+    mask (same shape as src): sum ReLU-backward rows, src where mask > 0 else 0.  fill=False
+    leaves the rows of keys without a live entry unwritten (merlin_segment_sum_masked)."""
     T, src_rows = int(src.shape[0]), int(src.shape[1])
-    assert src.shape[2] == 64 and src.dtype == torch.float32
+    assert src.shape[2] == 64 and src.dtype == torch.float32 and src.is_contiguous()
+    if mask is not None:
+        assert mask.shape == src.shape and mask.dtype == torch.float32 and mask.is_contiguous()
     assert plan.max_key < out_rows
     if slot is not None:
         assert slot.dtype == torch.int32
@@ -443,13 +452,15 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
     need = T * max(plan.nitems, 1) * 128
     if carry is None or carry.numel() < need:
         carry = torch.empty(need, dtype=torch.float32, device=src.device)
-    # algorithmic bytes: the entry lists (+ slot lookups), src read once, out written
-    nb = plan.nnz * (8 + (4 if slot is not None else 0)) + T * (src_rows + out_rows) * 256
+    # algorithmic bytes: the entry lists (+ slot lookups), src (and mask) read once, out written
+    nb = plan.nnz * (8 + (4 if slot is not None else 0)) + T * (src_rows * (2 if mask is not None else 1)
+                                                                 + out_rows) * 256
+    flags = (SEG_ACCUMULATE if accumulate else 0) | (0 if fill else SEG_NO_FILL)
     with KernelTimer.span(name, nb):
-        check(lib().merlin_segment_sum(ptr(src), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz, ptr(slot),
-                                       int(sub), plan.item_len, ptr(plan.fix), int(plan.fix.shape[0]), T, ptr(out),
-                                       int(out_rows), ptr(carry), int(bool(accumulate)), stream_of(src)),
-              "merlin_segment_sum")
+        check(lib().merlin_segment_sum_masked(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz,
+                                              ptr(slot), int(sub), plan.item_len, ptr(plan.fix),
+                                              int(plan.fix.shape[0]), T, ptr(out), int(out_rows), ptr(carry), flags,
+                                              stream_of(src)), "merlin_segment_sum_masked")
     return out
 
 

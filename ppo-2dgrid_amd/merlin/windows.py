@@ -18,9 +18,16 @@ runs through the tables and the GEMM, and the adjoints of the two gathers are se
 over lists sorted once per update (merlin_segment_sum: fixed order, no atomics):
 
   dQ[t][w][tap] = sum of dZ3[t][u, p3] over the minibatch's (u, p3) whose window at p3 + tap
-                  is w (the lists hold every distinct frame of the rollout, one list per
-                  block of frame ids so that each pass gathers from 1/DQ_BLOCKS of dZ3; a
-                  slot table skips the frames outside the minibatch)
+                  is w, dZ3 = [Y3 > 0] * dY3 (conv3's ReLU backward), in two passes over the
+                  5x5-tile patch under each conv3 output (its 9 windows are the patch's 3x3
+                  sub-windows, so (u, p3) with equal patches feed the same 9 destinations):
+     R[t][k]       = sum of dZ3[t][u, p3] over the (u, p3) whose patch is k   (ReLU mask fused:
+                     dY3 and Y3 rows gathered once each, dZ3 never materialised)
+     dQ[t][w][tap] = sum of R[t][k] over the patches k whose sub-window at tap is w
+                  A bench minibatch has ~1M (u, p3) and ~0.5M distinct patches: the first pass
+                  reads each source row once, the second's 9 re-reads hit a table a third of
+                  the size (instead of 81 scattered 256-B row gathers per frame from dZ3)
+  db3[t]        = sum over w of dQ[t][w][tap 0]  (every (u, p3) has one window at p3 + 0)
   dT2[t][row]   = sum of dZ2w[t][w] over the (w, tap) that read table row `row`
 
 Same function and gradients as the reference towers, fp32 sums regrouped.  The minibatch's
@@ -34,15 +41,10 @@ from . import _native as nat
 
 # conv3 output p3 = (oy, ox) and tap = (ky, kx) -> conv2 position (oy + ky) * 5 + (ox + kx)
 P2_OF = [[(p // 3 + k // 3) * 5 + p % 3 + k % 3 for k in range(9)] for p in range(9)]
-ITEM_LEN = 1024      # entries per wave of the dQ lists (81 per distinct frame of the rollout)
-# The dQ entries gather 256-B rows of dZ3 ([2, U*9, 64]: 322 MB at the bench size), each row
-# once per tap (9x); sorted by destination alone the re-reads miss the 256 MB MALL (rocprofv3:
-# 3.7 GB of HBM traffic per call, 0.57 ms).  The lists can be split by blocks of frame ids (a
-# minibatch numbers its distinct frames in ascending id, so block b's pass reads a contiguous
-# 1/dq_blocks of dZ3) with the blocks' sums added in block order; measured on MI355X, 8 blocks
-# of 256-entry items took 0.78 ms per minibatch (8 launches, each latency-bound on the
-# idx -> slot -> row chain), so the default stays one list.
-DQ_BLOCKS = 1
+ITEM_LEN = 1024      # entries per wave of the patch lists (9 per distinct frame) and the dQ lists
+# (The single-pass form -- dQ straight from dZ3, 81 entries per frame each gathering a 256-B row,
+# every row 9 times -- read 5.6 GB per minibatch at the bench size, 0.93 ms, plus a 0.27 ms ReLU
+# backward pass writing dZ3: profiles/r02_kernel_stats.md / r02_pmc.json.)
 HIST_ITEM_LEN = 256  # of the dT2 lists (16 per window)
 
 
@@ -62,6 +64,17 @@ def window_keys(cls: torch.Tensor) -> torch.Tensor:
         for b in range(3):
             k = k * 5 + cls[:, a:a + 5, b:b + 5]
     return k.reshape(-1, 25)
+
+
+def patch_keys(cls: torch.Tensor) -> torch.Tensor:
+    """[n, 7, 7] classes -> int64 [n, 9]: the 5x5-tile patch under each conv3 output p3 =
+    (oy, ox) (conv2 positions oy..oy+2 x ox..ox+2, i.e. tiles oy..oy+4 x ox..ox+4) as 25 base-5
+    digits, patch tile (0, 0) most significant."""
+    k = torch.zeros((cls.shape[0], 3, 3), dtype=torch.int64, device=cls.device)
+    for a in range(5):
+        for b in range(5):
+            k = k * 5 + cls[:, a:a + 3, b:b + 3]
+    return k.reshape(-1, 9)
 
 
 def window_rows(keys: torch.Tensor) -> torch.Tensor:
@@ -135,12 +148,13 @@ class WindowPlan:
     (frame id = merlin.dedup.FrameGroups group id) and the two backward entry lists."""
 
     def __init__(self, codes: torch.Tensor, frame_groups, item_len: int = ITEM_LEN,
-                 hist_item_len: int = HIST_ITEM_LEN, dq_blocks: int = DQ_BLOCKS):
+                 hist_item_len: int = HIST_ITEM_LEN):
         dev = codes.device
         self.frame_groups = frame_groups
         rep = codes.index_select(0, frame_groups.rep)  # one code row per distinct frame
         F = int(rep.shape[0])
-        uniq, inv = torch.unique(window_keys(unpack_classes(rep)).reshape(-1), return_inverse=True)
+        cls = unpack_classes(rep)
+        uniq, inv = torch.unique(window_keys(cls).reshape(-1), return_inverse=True)
         nw = int(uniq.numel())
         self.num_frames, self.num_windows = F, nw
         self.wid = inv.view(F, 25).to(torch.int32).contiguous()
@@ -149,19 +163,24 @@ class WindowPlan:
         # dT2 lists: entry (w, tap) -> table row rows[w][tap]; source row w of dZ2w
         hk, ho = torch.sort(self.rows.reshape(-1), stable=True)
         self.hist = SegmentPlan(hk, ho // 16, hist_item_len)
-        # dQ lists: entry (frame g, p3, tap) -> Q row wid[g][p3 + tap] * 9 + tap; source dZ3 row
-        # g*9 + p3; one destination-sorted list per block of frame ids (DQ_BLOCKS)
+        # patch lists: entry g*9 + p3 (frame g, conv3 output p3) -> its 5x5-tile patch k
+        # (patch_keys: 25 base-5 digits < 5**25 < 2**63), sorted by k; source dY3 / Y3 row
+        # slot[g]*9 + p3 of the minibatch
+        pk, kid = torch.unique(patch_keys(cls).reshape(-1), return_inverse=True)
+        self.num_patches = int(pk.numel())
+        self.kid = kid.view(F, 9).to(torch.int32).contiguous()
+        ks, ko = torch.sort(kid, stable=True)
+        self.patch_plan = SegmentPlan(ks, ko, item_len)
+        # dQ lists: entry (patch k, tap) -> Q row w*9 + tap, w = the window at tap inside k (read
+        # off the patch's first (g, p3)); source R row k
+        first = torch.ones(ks.numel(), dtype=torch.bool, device=dev)
+        first[1:] = ks[1:] != ks[:-1]
+        e = ko[first]  # one (g*9 + p3) per patch, in patch order
         p2 = torch.tensor(P2_OF, dtype=torch.int64, device=dev)
-        dst = (self.wid[:, p2].long() * 9 + torch.arange(9, dtype=torch.int64, device=dev)).reshape(-1)
-        nd, nb = nw * 9, max(1, min(int(dq_blocks), F))
-        blk = torch.arange(F, dtype=torch.int64, device=dev) * nb // F
-        dk, do = torch.sort(blk.repeat_interleave(81) * nd + dst, stable=True)
-        self.conv3_blocks = []
-        off = 0
-        for b, c in enumerate(torch.bincount(blk, minlength=nb).mul_(81).tolist()):
-            if c:
-                self.conv3_blocks.append(SegmentPlan(dk[off:off + c] - b * nd, do[off:off + c] // 9, item_len))
-            off += c
+        subw = self.wid[e // 9].long().gather(1, p2[e % 9])  # [K, 9] window of each tap
+        dst = (subw * 9 + torch.arange(9, dtype=torch.int64, device=dev)).reshape(-1)
+        dk, do = torch.sort(dst, stable=True)
+        self.dq_plan = SegmentPlan(dk, do // 9, item_len)
 
     def epoch_minibatches(self, idxs: torch.Tensor, minibatch_size: int) -> list:
         """MinibatchWindows of every minibatch idxs[k*mb:(k+1)*mb] of one epoch's permutation,
@@ -231,14 +250,20 @@ class _WindowConv3(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dY3):
         (Y3,) = ctx.saved_tensors
-        plan = ctx.plan
-        dZ3, db3 = nat.relu_bwd(Y3, dY3.contiguous())
-        dQ = torch.zeros((dZ3.shape[0], plan.num_windows * 9, 64), dtype=dZ3.dtype, device=dZ3.device)
-        carry = dZ3.new_empty(dZ3.shape[0] * max([p.nitems for p in plan.conv3_blocks] + [1]) * 128)
-        for b, part in enumerate(plan.conv3_blocks):  # source blocks, summed in block order
-            nat.segment_sum(dZ3, part, plan.num_windows * 9, slot=ctx.mb.slot, sub=9, name="k_seg_sum_dQ",
-                            out=dQ, accumulate=b > 0, carry=carry)
-        return dQ.view(dQ.shape[0], plan.num_windows, 576), db3, None, None
+        plan, mb = ctx.plan, ctx.mb
+        T = Y3.shape[0]
+        # pass 1: per-patch sums of the ReLU-masked dY3 rows of this minibatch's frames (rows of
+        # patches absent from the minibatch are left unwritten and skipped below)
+        R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
+                            name="k_seg_sum_R", mask=Y3, fill=False)
+        live = plan.kid.index_select(0, mb.groups).reshape(-1)
+        kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32, device=Y3.device)
+        kmap[live] = live
+        # pass 2: dQ[w][tap] over the live patches
+        dQ = nat.segment_sum(R, plan.dq_plan, plan.num_windows * 9, slot=kmap, sub=1, name="k_seg_sum_dQ")
+        dQ = dQ.view(T, plan.num_windows, 9, 64)
+        db3 = dQ[:, :, 0].sum(1)
+        return dQ.view(T, plan.num_windows, 576), db3, None, None
 
 
 def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows) -> torch.Tensor:

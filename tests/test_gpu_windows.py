@@ -97,6 +97,48 @@ def test_segment_sum_matches_index_add(device, n, nkeys, L, use_slot):
     assert torch.equal(both, out + out2)
 
 
+@pytest.mark.parametrize("L", [16, 1024])
+def test_segment_sum_masked_no_fill(device, L):
+    """merlin_segment_sum_masked: the ReLU mask of a second tensor fused into the gathers, and
+    NO_FILL leaving the rows of keys without a live entry untouched (here a NaN sentinel)."""
+    from merlin import _native as nat
+    from merlin.windows import SegmentPlan
+
+    g = torch.Generator(device=device)
+    g.manual_seed(L)
+    n, nkeys, F_, S = 60000, 9000, 4000, 9
+    keys = (torch.rand(n, device=device, generator=g) ** 2 * nkeys).long()
+    idx = torch.randint(0, F_ * S, (n,), device=device, generator=g)
+    o = torch.sort(keys, stable=True).indices
+    plan = SegmentPlan(keys[o], idx[o], item_len=L)
+    slot = torch.full((F_,), -1, dtype=torch.int32, device=device)
+    chosen = torch.randperm(F_, device=device, generator=g)[:700]
+    slot[chosen] = torch.arange(700, dtype=torch.int32, device=device)
+    src = torch.randn(2, 700 * S, 64, device=device, generator=g)
+    mask = torch.randn(2, 700 * S, 64, device=device, generator=g)
+    out = torch.full((2, nkeys, 64), float("nan"), device=device)
+    nat.segment_sum(src, plan, nkeys, slot=slot, sub=S, mask=mask, fill=False, out=out)
+    s = slot[idx // S].long()
+    keep = s >= 0
+    rows, kk = s[keep] * S + idx[keep] % S, keys[keep]
+    dz = torch.where(mask > 0, src, torch.zeros((), device=device)).double()
+    ref = torch.zeros(2, nkeys, 64, dtype=torch.float64, device=device)
+    mag = torch.zeros_like(ref)
+    for t in range(2):
+        ref[t].index_add_(0, kk, dz[t, rows])
+        mag[t].index_add_(0, kk, dz[t, rows].abs())
+    live = torch.zeros(nkeys, dtype=torch.bool, device=device)
+    live[kk] = True
+    # keys whose entries all fall outside the slot map: untouched, unless they span items (the
+    # fix-up writes their zero carry)
+    spans = torch.zeros(nkeys, dtype=torch.bool, device=device)
+    spans[plan.fix[:, 0].long()] = True
+    assert torch.isnan(out[:, ~live & ~spans]).all()
+    assert (out[:, ~live & spans] == 0).all()
+    err = (out[:, live].double() - ref[:, live]).abs()
+    assert (err <= 1e-5 * mag[:, live] + 1e-6).all()
+
+
 def _loss(lp, ent, v):
     return -(lp.exp() * 0.7).mean() + 0.5 * (v ** 2).mean() - 0.05 * ent.mean()
 

@@ -5,7 +5,8 @@ csrc/merlin_window.hip consume), in float64 with torch gathers standing in for t
   * the segment plans (fixed-length items + fix-ups), restated step by step as k_seg_sum /
     k_seg_fix run them, == index_add, with and without a minibatch slot map;
   * conv2 -> conv3 through the windows == the reference towers' convolutions of the rendered
-    frames, and the plan's backward lists (dQ, dT2) == autograd of the gathers."""
+    frames, and the plan's backward lists (the two dQ passes through the 5x5 patches with the
+    ReLU mask fused, dT2) == autograd of the gathers."""
 import numpy as np
 import pytest
 import torch
@@ -32,10 +33,14 @@ def test_window_rows_match_position_rows():
     assert (rows.numpy() == lut2_rows(c)).all()
 
 
-def emulate_segment_sum(plan, src, out_rows, slot=None, sub=1):
-    """Step-by-step restatement of k_seg_sum + k_seg_fix (csrc/merlin_window.hip)."""
+def emulate_segment_sum(plan, src, out_rows, slot=None, sub=1, mask=None, fill=True):
+    """Step-by-step restatement of k_seg_sum + k_seg_fix (csrc/merlin_window.hip); mask: rows of
+    src where mask > 0 (the MASK variant); fill=False: unwritten rows come back NaN."""
     T, C = src.shape[0], src.shape[2]
-    out = torch.zeros(T, out_rows, C, dtype=src.dtype)
+    if mask is not None:
+        src = torch.where(mask > 0, src, torch.zeros((), dtype=src.dtype))
+    out = torch.zeros(T, out_rows, C, dtype=src.dtype) if fill else torch.full((T, out_rows, C), float("nan"),
+                                                                                 dtype=src.dtype)
     carry = torch.zeros(T, max(plan.nitems, 1), 2, C, dtype=src.dtype)
     key, idx, L, n = plan.key.tolist(), plan.idx.tolist(), plan.item_len, plan.nnz
     for it in range(plan.nitems):
@@ -108,7 +113,7 @@ def test_window_towers_match_frame_convs(golden):
     c[:, 45] = 4
     c = np.concatenate([c, c[:5]])  # repeated observations share a frame id
     codes = torch.from_numpy(pack(c))
-    plan = WindowPlan(codes, FrameGroups(codes), item_len=16, hist_item_len=8, dq_blocks=3)
+    plan = WindowPlan(codes, FrameGroups(codes), item_len=16, hist_item_len=8)
     assert plan.num_frames == 12
     mb_idx = torch.tensor([0, 3, 12, 5, 7, 14, 9, 3])
     mb = plan.minibatch(mb_idx)
@@ -128,10 +133,19 @@ def test_window_towers_match_frame_convs(golden):
             torch.testing.assert_close(Y3[t][mb.inv], ref, rtol=1e-10, atol=1e-10)
     g = torch.randn(2, mb.groups.numel(), 9, 64, dtype=torch.float64)
     (Y3 * g).sum().backward()
-    dZ3 = torch.where(Y3 > 0, g, torch.zeros((), dtype=g.dtype)).reshape(2, -1, 64).detach()
-    assert len(plan.conv3_blocks) == 3
-    dQ = sum(emulate_segment_sum(part, dZ3, plan.num_windows * 9, slot=mb.slot, sub=9) for part in plan.conv3_blocks)
+    # the two passes of _WindowConv3.backward: per-patch sums of the masked rows (patches of frames
+    # outside the minibatch left unwritten = NaN here), then dQ over the live patches only
+    assert plan.num_patches <= 12 * 9 and plan.patch_plan.nnz == 12 * 9 and plan.dq_plan.nnz == plan.num_patches * 9
+    R = emulate_segment_sum(plan.patch_plan, g.reshape(2, -1, 64), plan.num_patches, slot=mb.slot, sub=9,
+                            mask=Y3.detach().reshape(2, -1, 64), fill=False)
+    live = plan.kid[mb.groups].reshape(-1).long()
+    kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32)
+    kmap[live] = live.to(torch.int32)
+    assert torch.isnan(R[:, kmap < 0]).all() and not torch.isnan(R[:, live]).any()
+    dQ = emulate_segment_sum(plan.dq_plan, R, plan.num_windows * 9, slot=kmap, sub=1)
     torch.testing.assert_close(dQ.view_as(Q), Q.grad)
+    dZ3 = torch.where(Y3 > 0, g, torch.zeros((), dtype=g.dtype))
+    torch.testing.assert_close(dQ.view(2, plan.num_windows, 9, 64)[:, :, 0].sum(1), dZ3.sum((1, 2)))  # db3
     dZ2w = torch.randn(2, plan.num_windows, 64, dtype=torch.float64)
     (T2[:, plan.rows.long()].sum(2) * dZ2w).sum().backward()
     torch.testing.assert_close(emulate_segment_sum(plan.hist, dZ2w, 2720), T2.grad)
