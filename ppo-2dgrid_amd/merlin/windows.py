@@ -18,15 +18,19 @@ runs through the tables and the GEMM, and the adjoints of the two gathers are se
 over lists sorted once per update (merlin_segment_sum: fixed order, no atomics):
 
   dQ[t][w][tap] = sum of dZ3[t][u, p3] over the minibatch's (u, p3) whose window at p3 + tap
-                  is w, dZ3 = [Y3 > 0] * dY3 (conv3's ReLU backward), in two passes over the
+                  is w, dZ3 = [Y3 > 0] * dY3 (conv3's ReLU backward), in three passes over the
                   5x5-tile patch under each conv3 output (its 9 windows are the patch's 3x3
-                  sub-windows, so (u, p3) with equal patches feed the same 9 destinations):
-     R[t][k]       = sum of dZ3[t][u, p3] over the (u, p3) whose patch is k   (ReLU mask fused:
-                     dY3 and Y3 rows gathered once each, dZ3 never materialised)
-     dQ[t][w][tap] = sum of R[t][k] over the patches k whose sub-window at tap is w
-                  A bench minibatch has ~1M (u, p3) and ~0.5M distinct patches: the first pass
-                  reads each source row once, the second's 9 re-reads hit a table a third of
-                  the size (instead of 81 scattered 256-B row gathers per frame from dZ3)
+                  sub-windows at tap = (ky, kx), so (u, p3) with equal patches feed the same 9
+                  destinations) and the patch's three 3x5-tile row bands (rows ky..ky+2):
+     R[t][k]        = sum of dZ3[t][u, p3] over the (u, p3) whose patch is k   (ReLU mask fused:
+                      dY3 and Y3 rows gathered once each, dZ3 never materialised)
+     S[t][ky][b]    = sum of R[t][k] over the live patches k whose band ky is b
+     dQ[t][w][tap]  = sum of S[t][ky][b] over the bands b of row ky whose window at column kx
+                      is w
+                  A bench rollout has ~0.5-1M distinct patches but only ~40-70k distinct bands
+                  per ky (and ~6k windows): each source row is read once, each R row 3 times
+                  and the small S table 3 times (instead of 81 scattered 256-B row gathers per
+                  frame from dZ3: 5.6 GB per minibatch)
   db3[t]        = sum over w of dQ[t][w][tap 0]  (every (u, p3) has one window at p3 + 0)
   dT2[t][row]   = sum of dZ2w[t][w] over the (w, tap) that read table row `row`
 
@@ -41,11 +45,20 @@ from . import _native as nat
 
 # conv3 output p3 = (oy, ox) and tap = (ky, kx) -> conv2 position (oy + ky) * 5 + (ox + kx)
 P2_OF = [[(p // 3 + k // 3) * 5 + p % 3 + k % 3 for k in range(9)] for p in range(9)]
-ITEM_LEN = 1024      # entries per wave of the patch lists (9 per distinct frame) and the dQ lists
 # (The single-pass form -- dQ straight from dZ3, 81 entries per frame each gathering a 256-B row,
 # every row 9 times -- read 5.6 GB per minibatch at the bench size, 0.93 ms, plus a 0.27 ms ReLU
 # backward pass writing dZ3: profiles/r02_kernel_stats.md / r02_pmc.json.)
-HIST_ITEM_LEN = 256  # of the dT2 lists (16 per window)
+
+
+def auto_item_len(nnz: int) -> int:
+    """Entries per wave: enough items (~16k, 16 waves per CU) to fill the chip -- a wave walks its
+    item's entries in dependent rounds, so a list of few long items is latency-bound (measured on
+    the bench's band / dQ lists: 1024-entry items 211 / 187 us, 64 / 32-entry items 87 / 50 us,
+    scripts/probe_dq.py) -- between 32 and 1024, a power of two."""
+    L = 32
+    while L < 1024 and L * 2 * 16384 <= nnz:
+        L *= 2
+    return L
 
 
 def unpack_classes(codes: torch.Tensor) -> torch.Tensor:
@@ -77,6 +90,19 @@ def patch_keys(cls: torch.Tensor) -> torch.Tensor:
     return k.reshape(-1, 9)
 
 
+def base5(digits: torch.Tensor) -> torch.Tensor:
+    """int64 [n, m] base-5 digits (most significant first) -> int64 [n] keys."""
+    k = torch.zeros(digits.shape[0], dtype=torch.int64, device=digits.device)
+    for i in range(digits.shape[1]):
+        k = k * 5 + digits[:, i]
+    return k
+
+
+def digits5(keys: torch.Tensor, m: int) -> torch.Tensor:
+    """int64 [n] keys -> int64 [n, m] base-5 digits, most significant first (inverse of base5)."""
+    return torch.stack([(keys // 5 ** (m - 1 - i)) % 5 for i in range(m)], 1)
+
+
 def window_rows(keys: torch.Tensor) -> torch.Tensor:
     """int64 [m] window keys -> int32 [m, 16]: the conv2 table row each tap 4*ky + kx reads
     (row layout of csrc/merlin_conv2lut.hip, tap_rows)."""
@@ -104,10 +130,10 @@ class SegmentPlan:
     item) name the destinations whose entries span items: their items' partial sums are added
     in item order."""
 
-    def __init__(self, key_sorted: torch.Tensor, idx_sorted: torch.Tensor, item_len: int = ITEM_LEN):
+    def __init__(self, key_sorted: torch.Tensor, idx_sorted: torch.Tensor, item_len: int | None = None):
         dev = key_sorted.device
         n = int(key_sorted.numel())
-        L = int(item_len)
+        L = auto_item_len(n) if item_len is None else int(item_len)
         self.nnz, self.item_len = n, L
         self.nitems = (n + L - 1) // L
         self.key = key_sorted.to(torch.int32).contiguous()
@@ -147,8 +173,8 @@ class WindowPlan:
     """Per-update numbering of the receptive-field windows of a rollout's distinct frames
     (frame id = merlin.dedup.FrameGroups group id) and the two backward entry lists."""
 
-    def __init__(self, codes: torch.Tensor, frame_groups, item_len: int = ITEM_LEN,
-                 hist_item_len: int = HIST_ITEM_LEN):
+    def __init__(self, codes: torch.Tensor, frame_groups, item_len: int | None = None,
+                 hist_item_len: int | None = None):
         dev = codes.device
         self.frame_groups = frame_groups
         rep = codes.index_select(0, frame_groups.rep)  # one code row per distinct frame
@@ -171,16 +197,27 @@ class WindowPlan:
         self.kid = kid.view(F, 9).to(torch.int32).contiguous()
         ks, ko = torch.sort(kid, stable=True)
         self.patch_plan = SegmentPlan(ks, ko, item_len)
-        # dQ lists: entry (patch k, tap) -> Q row w*9 + tap, w = the window at tap inside k (read
-        # off the patch's first (g, p3)); source R row k
-        first = torch.ones(ks.numel(), dtype=torch.bool, device=dev)
-        first[1:] = ks[1:] != ks[:-1]
-        e = ko[first]  # one (g*9 + p3) per patch, in patch order
-        p2 = torch.tensor(P2_OF, dtype=torch.int64, device=dev)
-        subw = self.wid[e // 9].long().gather(1, p2[e % 9])  # [K, 9] window of each tap
-        dst = (subw * 9 + torch.arange(9, dtype=torch.int64, device=dev)).reshape(-1)
-        dk, do = torch.sort(dst, stable=True)
-        self.dq_plan = SegmentPlan(dk, do // 9, item_len)
+        # band lists: entry (patch k, ky) -> S row band_off[ky] + (k's band ky); source R row k
+        K = self.num_patches
+        pd = digits5(pk, 25).view(K, 5, 5)
+        bdst, bsrc, wdst, off = [], [], [], 0
+        ar = torch.arange(K, dtype=torch.int64, device=dev)
+        for ky in range(3):
+            ub, bid = torch.unique(base5(pd[:, ky:ky + 3, :].reshape(K, 15)), return_inverse=True)
+            bdst.append(off + bid)
+            bsrc.append(ar)
+            # dQ entries of these bands: (band j, kx) -> Q row w*9 + ky*3 + kx, w = the band's
+            # window at column kx (numbered by searching the sorted window keys)
+            bd = digits5(ub, 15).view(-1, 3, 5)
+            for kx in range(3):
+                w = torch.searchsorted(uniq, base5(bd[:, :, kx:kx + 3].reshape(-1, 9)))
+                wdst.append((w * 9 + ky * 3 + kx, off + torch.arange(ub.numel(), dtype=torch.int64, device=dev)))
+            off += int(ub.numel())
+        self.num_bands = off
+        bk, bo = torch.sort(torch.cat(bdst), stable=True)
+        self.band_plan = SegmentPlan(bk, torch.cat(bsrc)[bo], item_len)
+        dk, do = torch.sort(torch.cat([d for d, _ in wdst]), stable=True)
+        self.dq_plan = SegmentPlan(dk, torch.cat([s for _, s in wdst])[do], item_len)
 
     def epoch_minibatches(self, idxs: torch.Tensor, minibatch_size: int) -> list:
         """MinibatchWindows of every minibatch idxs[k*mb:(k+1)*mb] of one epoch's permutation,
@@ -259,8 +296,9 @@ class _WindowConv3(torch.autograd.Function):
         live = plan.kid.index_select(0, mb.groups).reshape(-1)
         kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32, device=Y3.device)
         kmap[live] = live
-        # pass 2: dQ[w][tap] over the live patches
-        dQ = nat.segment_sum(R, plan.dq_plan, plan.num_windows * 9, slot=kmap, sub=1, name="k_seg_sum_dQ")
+        # pass 2: band sums over the live patches; pass 3: dQ[w][tap] from the bands
+        S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=kmap, sub=1, name="k_seg_sum_S")
+        dQ = nat.segment_sum(S, plan.dq_plan, plan.num_windows * 9, name="k_seg_sum_dQ")
         dQ = dQ.view(T, plan.num_windows, 9, 64)
         db3 = dQ[:, :, 0].sum(1)
         return dQ.view(T, plan.num_windows, 576), db3, None, None

@@ -133,16 +133,19 @@ def test_window_towers_match_frame_convs(golden):
             torch.testing.assert_close(Y3[t][mb.inv], ref, rtol=1e-10, atol=1e-10)
     g = torch.randn(2, mb.groups.numel(), 9, 64, dtype=torch.float64)
     (Y3 * g).sum().backward()
-    # the two passes of _WindowConv3.backward: per-patch sums of the masked rows (patches of frames
-    # outside the minibatch left unwritten = NaN here), then dQ over the live patches only
-    assert plan.num_patches <= 12 * 9 and plan.patch_plan.nnz == 12 * 9 and plan.dq_plan.nnz == plan.num_patches * 9
+    # the three passes of _WindowConv3.backward: per-patch sums of the masked rows (patches of
+    # frames outside the minibatch left unwritten = NaN here), band sums over the live patches,
+    # then dQ from the bands
+    assert plan.num_patches <= 12 * 9 and plan.patch_plan.nnz == 12 * 9
+    assert plan.band_plan.nnz == plan.num_patches * 3 and plan.dq_plan.nnz == plan.num_bands * 3
     R = emulate_segment_sum(plan.patch_plan, g.reshape(2, -1, 64), plan.num_patches, slot=mb.slot, sub=9,
                             mask=Y3.detach().reshape(2, -1, 64), fill=False)
     live = plan.kid[mb.groups].reshape(-1).long()
     kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32)
     kmap[live] = live.to(torch.int32)
     assert torch.isnan(R[:, kmap < 0]).all() and not torch.isnan(R[:, live]).any()
-    dQ = emulate_segment_sum(plan.dq_plan, R, plan.num_windows * 9, slot=kmap, sub=1)
+    S = emulate_segment_sum(plan.band_plan, R, plan.num_bands, slot=kmap, sub=1)
+    dQ = emulate_segment_sum(plan.dq_plan, S, plan.num_windows * 9)
     torch.testing.assert_close(dQ.view_as(Q), Q.grad)
     dZ3 = torch.where(Y3 > 0, g, torch.zeros((), dtype=g.dtype))
     torch.testing.assert_close(dQ.view(2, plan.num_windows, 9, 64)[:, :, 0].sum(1), dZ3.sum((1, 2)))  # db3
