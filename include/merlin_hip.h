@@ -273,20 +273,26 @@ int merlin_tower_window_lut(const int32_t *rows_dev, int64_t n_windows, const fl
 int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
                               const int64_t *groups_dev, int64_t n, const float *b3_dev,
                               int32_t towers, float *Y3_dev, void *stream);
+/* Same, also writing relu_bits_dev uint64[towers][n*9]: bit co of row (k*9 + p3) = Y3 > 0 there. */
+int merlin_tower_window_conv3_bits(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
+                                   const int64_t *groups_dev, int64_t n, const float *b3_dev,
+                                   int32_t towers, float *Y3_dev, uint64_t *relu_bits_dev, void *stream);
 int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *idx_dev,
                        const int32_t *key_dev, int64_t nnz, const int32_t *slot_dev, int32_t sub,
                        int64_t item_len, const int32_t *fix_dev, int64_t n_fix, int32_t towers,
                        float *out_dev, int64_t out_rows, float *carry_dev, int32_t accumulate,
                        void *stream);
-/* merlin_segment_sum with two options.  mask_dev (float[towers][src_rows][64], or NULL): each
- * source row is multiplied by the ReLU mask of the same row of mask_dev (src where mask > 0,
- * else 0: the ReLU backward of a forward output, fused into the gather).  flags:
- * MERLIN_SEG_ACCUMULATE as accumulate != 0 above; MERLIN_SEG_NO_FILL leaves the rows of
+/* merlin_segment_sum with options.  mask_dev (or NULL): each source row is multiplied by a ReLU
+ * mask of the same row (src where mask > 0, else 0: the ReLU backward of a forward output,
+ * fused into the gather); float[towers][src_rows][64], or with MERLIN_SEG_MASK_BITS
+ * uint64[towers][src_rows] (bit ch = channel ch > 0, as merlin_tower_window_conv3_bits writes).
+ * flags: MERLIN_SEG_ACCUMULATE as accumulate != 0 above; MERLIN_SEG_NO_FILL leaves the rows of
  * destinations without any (unskipped) entry untouched instead of zeroing them (the caller
  * knows which rows are live, e.g. merlin/windows.py's patch sums). */
 #define MERLIN_SEG_ACCUMULATE 1
 #define MERLIN_SEG_NO_FILL 2
-int merlin_segment_sum_masked(const float *src_dev, const float *mask_dev, int64_t src_rows,
+#define MERLIN_SEG_MASK_BITS 4
+int merlin_segment_sum_masked(const float *src_dev, const void *mask_dev, int64_t src_rows,
                               const int32_t *idx_dev, const int32_t *key_dev, int64_t nnz,
                               const int32_t *slot_dev, int32_t sub, int64_t item_len,
                               const int32_t *fix_dev, int64_t n_fix, int32_t towers, float *out_dev,

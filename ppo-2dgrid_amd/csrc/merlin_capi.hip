@@ -612,11 +612,19 @@ int merlin_tower_window_conv3(const float *Q, int64_t nw, const int32_t *wid, co
                               const float *b3, int32_t towers, float *Y3, void *stream) {
     if ((!Q || !wid || !b3 || !Y3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, nullptr, (hipStream_t)stream));
     return MERLIN_OK;
 }
 
-int merlin_segment_sum_masked(const float *src, const float *mask, int64_t src_rows, const int32_t *idx,
+int merlin_tower_window_conv3_bits(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
+                                   const float *b3, int32_t towers, float *Y3, uint64_t *relu_bits, void *stream) {
+    if ((!Q || !wid || !b3 || !Y3 || !relu_bits) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_segment_sum_masked(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,
                               const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub, int64_t item_len,
                               const int32_t *fix, int64_t n_fix, int32_t towers, float *out, int64_t out_rows,
                               float *carry, int32_t flags, void *stream) {
@@ -625,8 +633,9 @@ int merlin_segment_sum_masked(const float *src, const float *mask, int64_t src_r
     if (n_fix > 0 && !fix) return fail(MERLIN_E_INVALID, "null fix-up list");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (item_len <= 0 || sub <= 0) return fail(MERLIN_E_INVALID, "item_len and sub must be > 0");
-    if (flags & ~(MERLIN_SEG_ACCUMULATE | MERLIN_SEG_NO_FILL)) return fail(MERLIN_E_INVALID, "unknown flags");
-    HIP_TRY(merlin::launch_seg_sum(src, mask, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
+    if (flags & ~(MERLIN_SEG_ACCUMULATE | MERLIN_SEG_NO_FILL | MERLIN_SEG_MASK_BITS))
+        return fail(MERLIN_E_INVALID, "unknown flags");
+    HIP_TRY(merlin::launch_seg_sum(src, mask, (flags & MERLIN_SEG_MASK_BITS) ? 1 : 0, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
                                    out_rows, carry, (flags & MERLIN_SEG_ACCUMULATE) ? 1 : 0,
                                    (flags & MERLIN_SEG_NO_FILL) ? 0 : 1, (hipStream_t)stream));
     return MERLIN_OK;

@@ -105,7 +105,7 @@ hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *d
 
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                               const float *b3, int T, float *Y3, hipStream_t s);
+                               const float *b3, int T, float *Y3, uint64_t *bits, hipStream_t s);
 hipError_t launch_act_heads(const float *z, const float *b4, int64_t n, int H, const float *wa, const float *ba,
                             const float *wc, const float *bc, int A, int det, uint64_t seed, const int64_t *epoch,
                             int64_t step, int64_t env_offset, int64_t *action, float *logp, float *value,
@@ -117,7 +117,7 @@ hipError_t launch_ppo_loss(const float *logits, const float *value, const float 
                            const float *ret, double clip_eps, double vf_coef, double ent_coef, float *dlogits,
                            float *dvalue, float *dbias_a, float *dbias_c, float *loss, double *stats,
                            double *workspace, hipStream_t s);
-hipError_t launch_seg_sum(const float *src, const float *mask, int64_t src_rows, const int32_t *idx,
+hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,
                           hipStream_t s);

@@ -61,12 +61,15 @@ __global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ 
 }
 
 // Y3[t][u*9 + p3][c4] = relu(b3[t][c4] + sum_tap Q[t][wid[g*25 + p2(p3, tap)]][tap][c4]); 16
-// consecutive lanes read one 256-B row of Q per tap
+// consecutive lanes read one 256-B row of Q per tap.  bits (optional): bit ch of bits[t][u*9 + p3]
+// = (Y3 channel ch > 0), the row's ReLU mask for the backward (16 lanes OR their nibbles together
+// with xor shuffles inside the row's 16-lane group; rows are 16-lane aligned, so the groups are
+// whole and converged).
 __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__ Q, int64_t nw,
                                                       const int32_t *__restrict__ wid,
                                                       const int64_t *__restrict__ groups, int64_t n,
                                                       const float4 *__restrict__ b3, int T,
-                                                      float4 *__restrict__ Y3) {
+                                                      float4 *__restrict__ Y3, uint64_t *__restrict__ bits) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
         const int c = (int)(e & 15);
@@ -86,8 +89,17 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
 #pragma unroll
         for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
         const float4 b = b3[t * 16 + c];
-        Y3[e] = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
-                            relu_nan(acc.w + b.w));
+        const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
+                                     relu_nan(acc.w + b.w));
+        Y3[e] = y;
+        if (bits) {
+            uint64_t v = (uint64_t)((y.x > 0.0f ? 1u : 0u) | (y.y > 0.0f ? 2u : 0u) | (y.z > 0.0f ? 4u : 0u) |
+                                    (y.w > 0.0f ? 8u : 0u))
+                         << (4 * c);
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) v |= __shfl_xor(v, off);
+            if (c == 0) bits[r] = v;
+        }
     }
 }
 
@@ -103,11 +115,13 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
 // added to out (one writer per destination per launch), so a list split by source block into
 // several launches accumulates in block order.  MASK: each source row is first multiplied by the
 // ReLU mask of the same row of `mask` (the forward's output), i.e. the sums are of
-// threshold_backward(src, mask) rows, never materialised.
+// threshold_backward(src, mask) rows, never materialised.  MASK 2: the same mask as one 64-bit
+// word per row (bit ch = mask channel ch > 0, as k_window_conv3 writes it): 8 B per row instead
+// of 256.
 constexpr int SEG_WAVES = 4, SEG_UNROLL = 8;
-template <bool MASK>
+template <int MASK>
 __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__restrict__ src,
-                                                           const float4 *__restrict__ mask, int64_t src_rows,
+                                                           const void *__restrict__ mask, int64_t src_rows,
                                                            const int32_t *__restrict__ idx,
                                                            const int32_t *__restrict__ key, int64_t nnz,
                                                            const int32_t *__restrict__ slot, int S, int64_t L,
@@ -118,7 +132,10 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
     const int t = lane >> 5, q = (lane >> 4) & 1, c = lane & 15;
     const bool live = t < T;
     const float4 *srct = src + (size_t)(live ? t : 0) * src_rows * 16 + c;
-    const float4 *maskt = MASK ? mask + (size_t)(live ? t : 0) * src_rows * 16 + c : nullptr;
+    const float4 *maskt =
+        MASK == 1 ? static_cast<const float4 *>(mask) + (size_t)(live ? t : 0) * src_rows * 16 + c : nullptr;
+    const uint64_t *bitst = MASK == 2 ? static_cast<const uint64_t *>(mask) + (size_t)(live ? t : 0) * src_rows
+                                      : nullptr;
     const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int64_t it = (int64_t)blockIdx.x * SEG_WAVES + wv; it < nitems; it += (int64_t)gridDim.x * SEG_WAVES) {
         const int64_t e0 = it * L, e1 = std::min<int64_t>(nnz, e0 + L);
@@ -179,12 +196,20 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
                 float4 vq[SEG_UNROLL];
 #pragma unroll
                 for (int u = 0; u < SEG_UNROLL; u++) vq[u] = srct[(size_t)rq[u] * 16];
-                if constexpr (MASK) {
+                if constexpr (MASK == 1) {
                     float4 mq[SEG_UNROLL];
 #pragma unroll
                     for (int u = 0; u < SEG_UNROLL; u++) mq[u] = maskt[(size_t)rq[u] * 16];
 #pragma unroll
                     for (int u = 0; u < SEG_UNROLL; u++) vq[u] = f4_mask(mq[u], vq[u]);
+                } else if constexpr (MASK == 2) {
+                    uint32_t mb[SEG_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < SEG_UNROLL; u++) mb[u] = (uint32_t)(bitst[rq[u]] >> (4 * c));
+#pragma unroll
+                    for (int u = 0; u < SEG_UNROLL; u++)
+                        vq[u] = make_float4(mb[u] & 1u ? vq[u].x : 0.0f, mb[u] & 2u ? vq[u].y : 0.0f,
+                                            mb[u] & 4u ? vq[u].z : 0.0f, mb[u] & 8u ? vq[u].w : 0.0f);
                 }
 #pragma unroll
                 for (int u = 0; u < SEG_UNROLL; u++) {
@@ -252,16 +277,16 @@ hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, 
 }
 
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                               const float *b3, int T, float *Y3, hipStream_t s) {
+                               const float *b3, int T, float *Y3, uint64_t *bits, hipStream_t s) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
     hipLaunchKernelGGL(k_window_conv3, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4 *>(Q), nw, wid,
-                       groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3));
+                       groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), bits);
     return hipGetLastError();
 }
 
-hipError_t launch_seg_sum(const float *src, const float *mask, int64_t src_rows, const int32_t *idx,
+hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,
                           hipStream_t s) {
@@ -270,13 +295,16 @@ hipError_t launch_seg_sum(const float *src, const float *mask, int64_t src_rows,
     if (e != hipSuccess || nnz <= 0) return e;
     const int64_t nitems = (nnz + L - 1) / L;
     const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
-    if (mask)
-        hipLaunchKernelGGL(k_seg_sum<true>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
-                           reinterpret_cast<const float4 *>(src), reinterpret_cast<const float4 *>(mask), src_rows,
-                           idx, key, nnz, slot, S, L, nitems, T, reinterpret_cast<float4 *>(out), out_rows,
-                           reinterpret_cast<float4 *>(carry), acc_out);
+    if (mask && mask_bits)
+        hipLaunchKernelGGL(k_seg_sum<2>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
+                           reinterpret_cast<const float4 *>(src), mask, src_rows, idx, key, nnz, slot, S, L, nitems,
+                           T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out);
+    else if (mask)
+        hipLaunchKernelGGL(k_seg_sum<1>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
+                           reinterpret_cast<const float4 *>(src), mask, src_rows, idx, key, nnz, slot, S, L, nitems,
+                           T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out);
     else
-        hipLaunchKernelGGL(k_seg_sum<false>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
+        hipLaunchKernelGGL(k_seg_sum<0>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
                            reinterpret_cast<const float4 *>(src), nullptr, src_rows, idx, key, nnz, slot, S, L,
                            nitems, T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry),
                            acc_out);

@@ -90,6 +90,7 @@ def lib():
     L.merlin_tower_conv2_lut_bwd.argtypes = [vp, i64, vp, vp, i32, vp, vp]
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
+    L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp]
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
     L.merlin_segment_sum_masked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                             vp]
@@ -136,6 +137,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
+    "merlin_tower_window_conv3_bits",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
 )
@@ -411,9 +413,10 @@ def window_lut(rows, tables):
     return out
 
 
-def window_conv3(Q, wid, groups, b3):
+def window_conv3(Q, wid, groups, b3, bits: bool = False):
     """Y3 f32[T, n*9, 64] = relu(conv3) rows (k, p3) of frames groups[k] from
-    Q f32[T, nw, 576], the per-window, per-tap conv3 partial sums (merlin/windows.py)."""
+    Q f32[T, nw, 576], the per-window, per-tap conv3 partial sums (merlin/windows.py).
+    bits: also return the rows' ReLU masks, int64[T, n*9] (bit co = Y3 > 0)."""
     T, nw = int(Q.shape[0]), int(Q.shape[1])
     n = int(groups.numel())
     assert Q.shape[2] == 576 and Q.dtype == torch.float32 and b3.shape == (T, 64)
@@ -421,13 +424,19 @@ def window_conv3(Q, wid, groups, b3):
     out = torch.empty((T, n * 9, 64), dtype=torch.float32, device=Q.device)
     # algorithmic bytes: Y3 written, the frames' ids and window ids, Q read once (its 81 row
     # gathers per frame and tower are L2 / Infinity-Cache hits)
+    if bits:
+        mask = torch.empty((T, n * 9), dtype=torch.int64, device=Q.device)
+        with KernelTimer.span("k_window_conv3", T * n * 9 * 264 + n * 108 + T * nw * 576 * 4):
+            check(lib().merlin_tower_window_conv3_bits(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
+                                                       ptr(mask), stream_of(Q)), "merlin_tower_window_conv3_bits")
+        return out, mask
     with KernelTimer.span("k_window_conv3", T * n * 9 * 256 + n * 108 + T * nw * 576 * 4):
         check(lib().merlin_tower_window_conv3(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
                                               stream_of(Q)), "merlin_tower_window_conv3")
     return out
 
 
-SEG_ACCUMULATE, SEG_NO_FILL = 1, 2  # include/merlin_hip.h
+SEG_ACCUMULATE, SEG_NO_FILL, SEG_MASK_BITS = 1, 2, 4  # include/merlin_hip.h
 
 
 def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum", out=None,
@@ -436,11 +445,15 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
     the plan's entries e with that key (merlin.windows.SegmentPlan); row(e) = idx[e], or
     slot[idx[e] // sub] * sub + idx[e] % sub with entries whose slot is -1 skipped.  With
     accumulate the sums are added to `out` (a list split over source blocks, in call order).
-    mask (same shape as src): sum ReLU-backward rows, src where mask > 0 else 0.  fill=False
-    leaves the rows of keys without a live entry unwritten (merlin_segment_sum_masked)."""
+    mask (same shape as src): sum ReLU-backward rows, src where mask > 0 else 0; or the same mask as
+    int64 [T, src_rows] bit words (window_conv3(bits=True)).  fill=False leaves the rows of keys
+    without a live entry unwritten (merlin_segment_sum_masked)."""
     T, src_rows = int(src.shape[0]), int(src.shape[1])
     assert src.shape[2] == 64 and src.dtype == torch.float32 and src.is_contiguous()
-    if mask is not None:
+    mask_bits = mask is not None and mask.dtype == torch.int64
+    if mask_bits:
+        assert mask.shape == (T, src_rows) and mask.is_contiguous()
+    elif mask is not None:
         assert mask.shape == src.shape and mask.dtype == torch.float32 and mask.is_contiguous()
     assert plan.max_key < out_rows
     if slot is not None:
@@ -453,9 +466,9 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
     if carry is None or carry.numel() < need:
         carry = torch.empty(need, dtype=torch.float32, device=src.device)
     # algorithmic bytes: the entry lists (+ slot lookups), src (and mask) read once, out written
-    nb = plan.nnz * (8 + (4 if slot is not None else 0)) + T * (src_rows * (2 if mask is not None else 1)
-                                                                 + out_rows) * 256
-    flags = (SEG_ACCUMULATE if accumulate else 0) | (0 if fill else SEG_NO_FILL)
+    mrow = 0 if mask is None else (8 if mask_bits else 256)
+    nb = plan.nnz * (8 + (4 if slot is not None else 0)) + T * (src_rows * (256 + mrow) + out_rows * 256)
+    flags = (SEG_ACCUMULATE if accumulate else 0) | (0 if fill else SEG_NO_FILL) | (SEG_MASK_BITS if mask_bits else 0)
     with KernelTimer.span(name, nb):
         check(lib().merlin_segment_sum_masked(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz,
                                               ptr(slot), int(sub), plan.item_len, ptr(plan.fix),

@@ -183,6 +183,18 @@ def _gemm_span(name, T, M, N, K):
     return KernelTimer.span(name, 0, 2 * T * M * N * K)
 
 
+def bias_relu_bmm(X, W, b):
+    """relu(X[t] @ W[t] + b[t]) for every tower t (X [T, M, K], W [T, K, N], b [T, N]): one GEMM per
+    tower with the bias and ReLU in hipBLASLt's epilogue (torch._addmm_activation), bit-identical to
+    the GEMM followed by merlin_tower_bias_relu, without its extra pass over the [T, M, N] output
+    (scripts/probe_gemm3.py: fc1 at the bench size 1247 -> 1135 us; used for fc1, N = 512)."""
+    T, M, _ = X.shape
+    out = X.new_empty((T, M, W.shape[2]))
+    for t in range(T):
+        torch._addmm_activation(b[t], X[t], W[t], out=out[t])
+    return out
+
+
 def _splitk_bmm_tn(X, dY, chunks):
     """X^T @ dY for X [T, M, K], dY [T, M, N] with the long M reduction split into `chunks`
     batched GEMMs plus a sum: hipBLASLt runs the plain tall-skinny product at about half the
@@ -245,8 +257,7 @@ class _TowerHead(torch.autograd.Function):
 
         T, n, K = a3.shape
         with _gemm_span("gemm_fc1_fwd", T, n, W4p.shape[1], K):
-            z = torch.bmm(a3, W4p.transpose(1, 2))
-        h = nat.bias_relu_(z, b4.detach().contiguous())
+            h = bias_relu_bmm(a3, W4p.transpose(1, 2), b4.detach().contiguous())
         logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
         value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)
         ctx.save_for_backward(a3, W4p, h, Wa, Wc)
@@ -474,6 +485,7 @@ class CNNActorCritic(nn.Module):
 
         n = codes.shape[0]
         A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
+        # (conv3's N = 64 GEMM: bmm + k_bias_relu measured faster than the epilogue form here)
         a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
         z = torch.bmm(a3, pack["W4t"])
         return nat.act_heads(z, pack["b4"], self.actor[2].weight, self.actor[2].bias, self.critic[2].weight,

@@ -23,7 +23,8 @@ over lists sorted once per update (merlin_segment_sum: fixed order, no atomics):
                   sub-windows at tap = (ky, kx), so (u, p3) with equal patches feed the same 9
                   destinations) and the patch's three 3x5-tile row bands (rows ky..ky+2):
      R[t][k]        = sum of dZ3[t][u, p3] over the (u, p3) whose patch is k   (ReLU mask fused:
-                      dY3 and Y3 rows gathered once each, dZ3 never materialised)
+                      dY3 rows gathered once each with the 8-B ReLU bit mask that
+                      merlin_tower_window_conv3_bits wrote beside Y3; dZ3 never materialised)
      S[t][ky][b]    = sum of R[t][k] over the live patches k whose band ky is b
      dQ[t][w][tap]  = sum of S[t][ky][b] over the bands b of row ky whose window at column kx
                       is w
@@ -190,7 +191,7 @@ class WindowPlan:
         hk, ho = torch.sort(self.rows.reshape(-1), stable=True)
         self.hist = SegmentPlan(hk, ho // 16, hist_item_len)
         # patch lists: entry g*9 + p3 (frame g, conv3 output p3) -> its 5x5-tile patch k
-        # (patch_keys: 25 base-5 digits < 5**25 < 2**63), sorted by k; source dY3 / Y3 row
+        # (patch_keys: 25 base-5 digits < 5**25 < 2**63), sorted by k; source dY3 row / mask word
         # slot[g]*9 + p3 of the minibatch
         pk, kid = torch.unique(patch_keys(cls).reshape(-1), return_inverse=True)
         self.num_patches = int(pk.numel())
@@ -279,22 +280,22 @@ class _WindowConv3(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, Q, b3, plan, mb):
-        Y3 = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous())
-        ctx.save_for_backward(Y3)
+        Y3, bits = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous(), bits=True)
+        ctx.save_for_backward(bits)
         ctx.plan, ctx.mb = plan, mb
         return Y3
 
     @staticmethod
     def backward(ctx, dY3):
-        (Y3,) = ctx.saved_tensors
+        (bits,) = ctx.saved_tensors
         plan, mb = ctx.plan, ctx.mb
-        T = Y3.shape[0]
+        T = bits.shape[0]
         # pass 1: per-patch sums of the ReLU-masked dY3 rows of this minibatch's frames (rows of
         # patches absent from the minibatch are left unwritten and skipped below)
         R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
-                            name="k_seg_sum_R", mask=Y3, fill=False)
+                            name="k_seg_sum_R", mask=bits, fill=False)
         live = plan.kid.index_select(0, mb.groups).reshape(-1)
-        kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32, device=Y3.device)
+        kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32, device=bits.device)
         kmap[live] = live
         # pass 2: band sums over the live patches; pass 3: dQ[w][tap] from the bands
         S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=kmap, sub=1, name="k_seg_sum_S")

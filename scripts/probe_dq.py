@@ -56,6 +56,10 @@ def main():
     nlive = int((kmap >= 0).sum())
     print(f"F={plan.num_frames} U={U} windows={plan.num_windows} patches={K} live={nlive} bands={plan.num_bands}",
           flush=True)
+    pairs = torch.unique(plan.kid.index_select(0, mb.groups).long() * 9 + torch.arange(9, device=dev)).numel()
+    print(f"minibatch (p3, patch) pairs {pairs} of {U * 9} frame-positions ({U * 9 / pairs:.2f}x)", flush=True)
+    if os.environ.get("PAIRS_ONLY"):
+        return
     dY3 = torch.randn(2, U * 9, 64, device=dev)
     Y3 = torch.randn(2, U * 9, 64, device=dev)
     rows = plan.num_windows * 9

@@ -52,6 +52,23 @@ def test_window_lut_and_conv3_match_gathers(device):
     w = plan.wid[mb.groups].long()[:, torch.tensor(P2_OF, device=device)]
     ref = torch.relu(Q.view(2, nw, 9, 64)[:, w, torch.arange(9, device=device)].sum(3) + b3[:, None, None])
     torch.testing.assert_close(Y3.view(2, -1, 9, 64), ref, rtol=1e-5, atol=1e-5)
+    # the ReLU bit words written beside Y3 (bit co of row r = Y3[t][r][co] > 0), and the masked
+    # segment sum reading them == reading the float mask
+    Y3b, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True)
+    assert torch.equal(Y3b, Y3)
+    shifts = torch.arange(64, device=device, dtype=torch.int64)
+    assert torch.equal((bits.unsqueeze(-1) >> shifts) & 1, (Y3 > 0).long())
+    from merlin.windows import SegmentPlan
+    n = Y3.shape[1]
+    g = torch.Generator(device=device)
+    g.manual_seed(3)
+    keys = torch.randint(0, 500, (n,), device=device, generator=g)
+    o = torch.sort(keys, stable=True).indices
+    sp = SegmentPlan(keys[o], o)
+    dY = torch.randn_like(Y3)
+    a = nat.segment_sum(dY, sp, 500, mask=Y3)
+    b = nat.segment_sum(dY, sp, 500, mask=bits)
+    assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("n,nkeys,L,use_slot", [(1, 3, 4, False), (5000, 37, 64, True),
