@@ -413,19 +413,23 @@ def window_lut(rows, tables):
     return out
 
 
-def window_conv3(Q, wid, groups, b3, bits: bool = False):
+def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None):
     """Y3 f32[T, n*9, 64] = relu(conv3) rows (k, p3) of frames groups[k] from
     Q f32[T, nw, 576], the per-window, per-tap conv3 partial sums (merlin/windows.py).
-    bits: also return the rows' ReLU masks, int64[T, n*9] (bit co = Y3 > 0)."""
+    bits: also return the rows' ReLU masks, int64[T, n*9] (bit co = Y3 > 0).  rows >= n: the
+    outputs hold `rows` frames, those past n zero (Y3) / unwritten (bits)."""
     T, nw = int(Q.shape[0]), int(Q.shape[1])
     n = int(groups.numel())
-    assert Q.shape[2] == 576 and Q.dtype == torch.float32 and b3.shape == (T, 64)
+    R = n if rows is None else int(rows)
+    assert Q.shape[2] == 576 and Q.dtype == torch.float32 and b3.shape == (T, 64) and R >= n
     assert wid.dtype == torch.int32 and wid.shape[1] == 25 and groups.dtype == torch.int64
-    out = torch.empty((T, n * 9, 64), dtype=torch.float32, device=Q.device)
+    out = torch.empty((T, R * 9, 64), dtype=torch.float32, device=Q.device)
+    if R > n:
+        out[:, n * 9:].zero_()
     # algorithmic bytes: Y3 written, the frames' ids and window ids, Q read once (its 81 row
     # gathers per frame and tower are L2 / Infinity-Cache hits)
     if bits:
-        mask = torch.empty((T, n * 9), dtype=torch.int64, device=Q.device)
+        mask = torch.empty((T, R * 9), dtype=torch.int64, device=Q.device)
         with KernelTimer.span("k_window_conv3", T * n * 9 * 264 + n * 108 + T * nw * 576 * 4):
             check(lib().merlin_tower_window_conv3_bits(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
                                                        ptr(mask), stream_of(Q)), "merlin_tower_window_conv3_bits")

@@ -255,8 +255,10 @@ class _TowerHead(torch.autograd.Function):
     def forward(ctx, a3, W4p, b4, Wa, ba, Wc, bc):
         from . import _native as nat
 
+        from .gemm_tuning import tuned
+
         T, n, K = a3.shape
-        with _gemm_span("gemm_fc1_fwd", T, n, W4p.shape[1], K):
+        with _gemm_span("gemm_fc1_fwd", T, n, W4p.shape[1], K), tuned():
             h = bias_relu_bmm(a3, W4p.transpose(1, 2), b4.detach().contiguous())
         logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
         value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)
@@ -267,6 +269,7 @@ class _TowerHead(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dlogits, dvalue):
         from . import _native as nat
+        from .gemm_tuning import tuned
 
         a3, W4p, h, Wa, Wc = ctx.saved_tensors
         n = h.shape[1]
@@ -275,9 +278,10 @@ class _TowerHead(torch.autograd.Function):
         dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
         da3 = None
         if ctx.needs_input_grad[0]:
-            with _gemm_span("gemm_fc1_dgrad", dz.shape[0], n, W4p.shape[2], dz.shape[2]):
+            with _gemm_span("gemm_fc1_dgrad", dz.shape[0], n, W4p.shape[2], dz.shape[2]), tuned():
                 da3 = torch.bmm(dz, W4p)
-        dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
+        with tuned():
+            dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
         dba = dlogits.sum(0) if ctx.head_bias[0] else None
         dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
         return da3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc
@@ -485,9 +489,12 @@ class CNNActorCritic(nn.Module):
 
         n = codes.shape[0]
         A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
+        from .gemm_tuning import tuned
+
         # (conv3's N = 64 GEMM: bmm + k_bias_relu measured faster than the epilogue form here)
-        a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
-        z = torch.bmm(a3, pack["W4t"])
+        with tuned():
+            a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
+            z = torch.bmm(a3, pack["W4t"])
         return nat.act_heads(z, pack["b4"], self.actor[2].weight, self.actor[2].bias, self.critic[2].weight,
                              self.critic[2].bias, deterministic, seed=seed, epoch=epoch, step=step, out=out,
                              env_offset=env_offset)
@@ -517,10 +524,13 @@ class CNNActorCritic(nn.Module):
         the receptive-field windows (merlin/windows.py): conv2 / conv3 once per distinct window of
         the rollout, fc1 and the heads once per distinct frame.  head_bias=False leaves the heads'
         biases out (merlin.ppo's fused loss adds them and returns their gradients)."""
+        from .gemm_tuning import padded_rows
         from .windows import tower_conv3
 
         n = int(mb.groups.numel())
-        return self._tower_head(tower_conv3(self, plan, mb).view(2, n, 576), n, head_bias)
+        npad = padded_rows(n)  # fc1's rows on a tuned GEMM shape (merlin/gemm_tuning.py); zero rows past n
+        logits, value = self._tower_head(tower_conv3(self, plan, mb, npad).view(2, npad, 576), npad, head_bias)
+        return (logits[:n], value[:n]) if npad != n else (logits, value)
 
     def evaluate_windows(self, plan, mb, actions):
         """evaluate_codes for one minibatch of the update through heads_windows; sample k takes

@@ -1,0 +1,77 @@
+"""Pre-tuned GEMM solutions for the update's fc1 GEMMs on gfx950 (PyTorch TunableOp).
+
+hipBLASLt's heuristic pick for the fc1 shapes runs at ~110-120 TFLOP/s of the 157.3 fp32 MFMA
+peak; an exhaustive search over the hipBLASLt and rocBLAS solutions finds faster kernels for the
+forward (bias+ReLU epilogue, per tower) and the split-K weight-gradient chunks
+(scripts/probe_tunable.py: 1271 -> 1042 us and 1240 -> 976 us at 115,712 frames).  The search runs
+offline (scripts/tune_gemms.py on an MI355X) and its results ship as a TunableOp CSV
+(tuning/gemm_gfx950.csv).  The file is read once with tuning OFF, and TunableOp dispatch is
+switched on only around the GEMMs it was made for (`with tuned():` in merlin/actor_critic.py: the
+update's fc1 and the rollout's conv3 / fc1): there a shape found in the file runs the recorded
+solution, any other runs PyTorch's default; every other GEMM of the process takes PyTorch's
+usual path.  Nothing is timed or written at run time.  The file's validator lines (PyTorch / HIP /
+hipBLASLt / rocBLAS versions, gfx950) make TunableOp reject it on any other stack.
+
+The update's frame counts vary per minibatch, so fc1's row count is padded up to the next tuned
+row count when one lies within ROW_BUCKET (zero rows: they add exact zeros to the weight
+gradient, and their outputs are dropped); otherwise, and whenever the file is off, no padding.
+MERLIN_GEMM_TUNING=0 switches it off.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+import re
+
+import torch
+
+TUNED_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "gemm_gfx950.csv")
+ROW_BUCKET = 2048
+_state = {"on": False, "tried": False, "rows": ()}
+
+
+def enable(path: str = TUNED_FILE) -> bool:
+    """Load the tuned solutions (once per process); True when they are in use."""
+    if _state["tried"]:
+        return _state["on"]
+    _state["tried"] = True
+    if os.environ.get("MERLIN_GEMM_TUNING", "1") == "0" or not torch.cuda.is_available() or not os.path.exists(path):
+        return False
+    if not torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.startswith("gfx950"):
+        return False
+    import torch.cuda.tunable as tunable
+
+    tunable.tuning_enable(False)
+    tunable.set_filename(path)
+    _state["on"] = bool(tunable.read_file(path))
+    tunable.enable(False)  # dispatch only inside tuned()
+    if _state["on"]:
+        _state["rows"] = tuple(sorted({int(m.group(1)) for m in re.finditer(r"tn_512_(\d+)_576_ld", open(path).read())}))
+    return _state["on"]
+
+
+@contextlib.contextmanager
+def tuned():
+    """TunableOp dispatch (recorded solutions, no tuning) for the GEMMs inside the block."""
+    if not _state["on"]:
+        yield
+        return
+    import torch.cuda.tunable as tunable
+
+    tunable.enable(True)
+    try:
+        yield
+    finally:
+        tunable.enable(False)
+
+
+def active() -> bool:
+    return _state["on"]
+
+
+def padded_rows(n: int) -> int:
+    """The tuned fc1 row count to pad n frames to (n itself when none lies within ROW_BUCKET)."""
+    for r in _state["rows"]:
+        if n <= r < n + ROW_BUCKET:
+            return r
+    return n

@@ -120,6 +120,10 @@ class PPO:
             # look-ahead map refills on a side stream after every step, overlapping the next act
             # (MerlinVecEnv.refill; the env's own every-16-steps refill is switched off)
             self._refill_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+            if self.device.type == "cuda":
+                from . import gemm_tuning
+
+                gemm_tuning.enable()  # pre-tuned fc1 GEMM solutions on gfx950 (merlin/gemm_tuning.py)
             if self._refill_stream is not None:
                 self.vec.set_refill_interval(0)
         else:

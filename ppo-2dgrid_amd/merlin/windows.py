@@ -279,8 +279,9 @@ class _WindowConv3(torch.autograd.Function):
     """Y3 [2, U*9, 64] = relu(conv3) rows (u, p3) of the minibatch's distinct frames, from Q."""
 
     @staticmethod
-    def forward(ctx, Q, b3, plan, mb):
-        Y3, bits = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous(), bits=True)
+    def forward(ctx, Q, b3, plan, mb, rows):
+        Y3, bits = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous(), bits=True,
+                                    rows=rows)
         ctx.save_for_backward(bits)
         ctx.plan, ctx.mb = plan, mb
         return Y3
@@ -302,15 +303,16 @@ class _WindowConv3(torch.autograd.Function):
         dQ = nat.segment_sum(S, plan.dq_plan, plan.num_windows * 9, name="k_seg_sum_dQ")
         dQ = dQ.view(T, plan.num_windows, 9, 64)
         db3 = dQ[:, :, 0].sum(1)
-        return dQ.view(T, plan.num_windows, 576), db3, None, None
+        return dQ.view(T, plan.num_windows, 576), db3, None, None, None
 
 
-def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows) -> torch.Tensor:
+def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = None) -> torch.Tensor:
     """relu(conv3(relu(conv2(relu(conv1(frame)))))) of both towers of CNNActorCritic `ac` for the
-    minibatch's distinct frames: [2, U*9, 64], rows (u, p3), channels last."""
+    minibatch's distinct frames: [2, U*9, 64], rows (u, p3), channels last ([2, rows*9, 64] with
+    zero rows past U when rows is given)."""
     ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
     Z2w = _WindowConv2.apply(ac.conv2_tables(), plan)
     a2w = torch.relu(Z2w + torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1))
     W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
     Q = torch.bmm(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
-    return _WindowConv3.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), plan, mb)
+    return _WindowConv3.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), plan, mb, rows)
