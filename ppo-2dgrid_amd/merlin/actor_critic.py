@@ -258,7 +258,7 @@ class _TowerHead(torch.autograd.Function):
         from .gemm_tuning import tuned
 
         T, n, K = a3.shape
-        with _gemm_span("gemm_fc1_fwd", T, n, W4p.shape[1], K), tuned():
+        with _gemm_span("gemm_fc1_fwd", T, n, W4p.shape[1], K), tuned("fwd"):
             h = bias_relu_bmm(a3, W4p.transpose(1, 2), b4.detach().contiguous())
         logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
         value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)

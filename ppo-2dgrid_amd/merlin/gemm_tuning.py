@@ -51,9 +51,9 @@ def enable(path: str = TUNED_FILE) -> bool:
 
 
 @contextlib.contextmanager
-def tuned():
+def tuned(which: str = ""):
     """TunableOp dispatch (recorded solutions, no tuning) for the GEMMs inside the block."""
-    if not _state["on"]:
+    if not _state["on"] or which in os.environ.get("MERLIN_UNTUNED", "").split(","):
         yield
         return
     import torch.cuda.tunable as tunable

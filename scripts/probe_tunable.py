@@ -22,6 +22,7 @@ def timeit(fn, reps=20):
 
 
 def main():
+    from merlin import _native as nat
     from merlin.actor_critic import _splitk_bmm_tn, bias_relu_bmm
 
     dev = torch.device("cuda", 0)
@@ -33,6 +34,8 @@ def main():
     fl = 2 * 2 * U * K * H
     cases = {
         "fwd": lambda: bias_relu_bmm(a3, W.transpose(1, 2), b),
+        "fwd_bmm+k_bias_relu": lambda: nat.bias_relu_(torch.bmm(a3, W.transpose(1, 2)), b),
+        "fwd_2mm+k_bias_relu": lambda: nat.bias_relu_(torch.stack([a3[t] @ W[t].t() for t in range(2)]), b),
         "dgrad": lambda: torch.bmm(dz, W),
         "wgrad": lambda: _splitk_bmm_tn(a3, dz, 32),
     }
@@ -50,7 +53,6 @@ def main():
         d = float((f() - ref[k]).abs().max())
         print(f"{k}: default {base[k]:.0f} us ({fl / base[k] / 1e6:.0f} TF)  tuned {t:.0f} us "
               f"({fl / t / 1e6:.0f} TF)  max|diff| {d:.3g}", flush=True)
-    torch.cuda.tunable.write_file()
 
 
 if __name__ == "__main__":
