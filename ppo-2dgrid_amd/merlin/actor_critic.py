@@ -255,10 +255,10 @@ class _TowerHead(torch.autograd.Function):
     def forward(ctx, a3, W4p, b4, Wa, ba, Wc, bc):
         from . import _native as nat
 
-        from .gemm_tuning import tuned
-
         T, n, K = a3.shape
-        with _gemm_span("gemm_fc1_fwd", T, n, W4p.shape[1], K), tuned("fwd"):
+        # (the forward keeps hipBLASLt's own pick: the searched solution measured faster alone
+        # but slower in the update, rocprofv3 profiles/r02_tuning_ab.md)
+        with _gemm_span("gemm_fc1_fwd", T, n, W4p.shape[1], K):
             h = bias_relu_bmm(a3, W4p.transpose(1, 2), b4.detach().contiguous())
         logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
         value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)

@@ -46,7 +46,7 @@ def enable(path: str = TUNED_FILE) -> bool:
     _state["on"] = bool(tunable.read_file(path))
     tunable.enable(False)  # dispatch only inside tuned()
     if _state["on"]:
-        _state["rows"] = tuple(sorted({int(m.group(1)) for m in re.finditer(r"tn_512_(\d+)_576_ld", open(path).read())}))
+        _state["rows"] = tuple(sorted({int(m.group(1)) for m in re.finditer(r"nn_576_(\d+)_512_B_2", open(path).read())}))
     return _state["on"]
 
 
@@ -71,7 +71,7 @@ def active() -> bool:
 
 def padded_rows(n: int) -> int:
     """The tuned fc1 row count to pad n frames to (n itself when none lies within ROW_BUCKET)."""
-    for r in _state["rows"]:
+    for r in _state["rows"]:  # (row counts of the dgrad entries: nn_576_<rows>_512)
         if n <= r < n + ROW_BUCKET:
             return r
     return n

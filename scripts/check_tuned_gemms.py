@@ -21,7 +21,7 @@ def main():
     from merlin.actor_critic import _splitk_bmm_tn, bias_relu_bmm
 
     dev = torch.device("cuda", 0)
-    rows = sorted({int(m.group(1)) for m in re.finditer(r"tn_512_(\d+)_576_ld", open(gemm_tuning.TUNED_FILE).read())})
+    rows = sorted({int(m.group(1)) for m in re.finditer(r"nn_576_(\d+)_512_B_2", open(gemm_tuning.TUNED_FILE).read())})
     g = torch.Generator(device=dev)
     g.manual_seed(0)
     W = torch.randn(2, 512, 576, device=dev, generator=g) * 0.05
