@@ -280,8 +280,9 @@ class _TowerHead(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             with _gemm_span("gemm_fc1_dgrad", dz.shape[0], n, W4p.shape[2], dz.shape[2]), tuned():
                 da3 = torch.bmm(dz, W4p)
-        with tuned():
-            dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
+        # (the split-K wgrad keeps hipBLASLt's pick: the searched solutions were faster in the
+        # tuning loop, slower inside the update)
+        dW4p = _splitk_bmm_tn(a3, dz, 32).transpose(1, 2)
         dba = dlogits.sum(0) if ctx.head_bias[0] else None
         dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
         return da3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc

@@ -1,10 +1,13 @@
 """Pre-tuned GEMM solutions for the update's fc1 GEMMs on gfx950 (PyTorch TunableOp).
 
 hipBLASLt's heuristic pick for the fc1 shapes runs at ~110-120 TFLOP/s of the 157.3 fp32 MFMA
-peak; an exhaustive search over the hipBLASLt and rocBLAS solutions finds faster kernels for the
-forward (bias+ReLU epilogue, per tower) and the split-K weight-gradient chunks
-(scripts/probe_tunable.py: 1271 -> 1042 us and 1240 -> 976 us at 115,712 frames).  The search runs
-offline (scripts/tune_gemms.py on an MI355X) and its results ship as a TunableOp CSV
+peak.  An exhaustive search over the hipBLASLt and rocBLAS solutions (scripts/tune_gemms.py,
+offline on an MI355X) finds faster kernels in its timing loop for all three fc1 GEMMs, but inside
+the update (inputs just written by the previous kernel, other work between the calls) only two
+held up: the input-gradient GEMM (a rocBLAS solution: 965-1020 -> 917 us per minibatch) and the
+rollout's fixed-shape conv3 / fc1 GEMMs (62 -> 44 us and 40 -> 38 us per step); the searched
+forward and split-K weight-gradient solutions measured 6-20 % slower there than hipBLASLt's own
+pick (profiles/r02_tuning_ab.md) and are not shipped.  The kept results ship as a TunableOp CSV
 (tuning/gemm_gfx950.csv).  The file is read once with tuning OFF, and TunableOp dispatch is
 switched on only around the GEMMs it was made for (`with tuned():` in merlin/actor_critic.py: the
 update's fc1 and the rollout's conv3 / fc1): there a shape found in the file runs the recorded
@@ -53,7 +56,7 @@ def enable(path: str = TUNED_FILE) -> bool:
 @contextlib.contextmanager
 def tuned(which: str = ""):
     """TunableOp dispatch (recorded solutions, no tuning) for the GEMMs inside the block."""
-    if not _state["on"] or which in os.environ.get("MERLIN_UNTUNED", "").split(","):
+    if not _state["on"] or (which and which in os.environ.get("MERLIN_UNTUNED", "").split(",")):
         yield
         return
     import torch.cuda.tunable as tunable
