@@ -30,7 +30,8 @@ import torch
 
 TUNED_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "gemm_gfx950.csv")
 ROW_BUCKET = 2048
-_state = {"on": False, "tried": False, "rows": ()}
+WINDOW_BUCKET = 256  # the window GEMMs' row count (distinct windows of an update) is padded to this
+_state = {"on": False, "tried": False, "rows": (), "windows": ()}
 
 
 def enable(path: str = TUNED_FILE) -> bool:
@@ -49,7 +50,9 @@ def enable(path: str = TUNED_FILE) -> bool:
     _state["on"] = bool(tunable.read_file(path))
     tunable.enable(False)  # dispatch only inside tuned()
     if _state["on"]:
-        _state["rows"] = tuple(sorted({int(m.group(1)) for m in re.finditer(r"nn_576_(\d+)_512_B_2", open(path).read())}))
+        text = open(path).read()
+        _state["rows"] = tuple(sorted({int(m.group(1)) for m in re.finditer(r"nn_576_(\d+)_512_B_2", text)}))
+        _state["windows"] = tuple(sorted({int(m.group(1)) for m in re.finditer(r"nn_576_(\d+)_64_B_2", text)}))
     return _state["on"]
 
 
@@ -70,6 +73,14 @@ def tuned(which: str = ""):
 
 def active() -> bool:
     return _state["on"]
+
+
+def padded_windows(n: int) -> int:
+    """The tuned window-GEMM row count to pad n windows to (n when none lies within WINDOW_BUCKET)."""
+    for r in _state["windows"]:
+        if n <= r < n + WINDOW_BUCKET:
+            return r
+    return n
 
 
 def padded_rows(n: int) -> int:

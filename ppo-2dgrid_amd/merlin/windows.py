@@ -262,17 +262,48 @@ class WindowPlan:
 
 
 class _WindowConv2(torch.autograd.Function):
-    """Z2w [2, windows, 64] = conv2(relu(conv1)) of every window (no conv2 bias) from the tables."""
+    """Z2w [2, windows, 64] = conv2(relu(conv1)) of every window (no conv2 bias) from the tables
+    ([2, nw_pad, 64] with zero rows past the windows when the window GEMMs are padded to a tuned
+    shape, merlin/gemm_tuning.py)."""
 
     @staticmethod
-    def forward(ctx, T2, plan):
+    def forward(ctx, T2, plan, nw_pad):
         ctx.plan = plan
-        return nat.window_lut(plan.rows, T2.detach().contiguous())
+        Z = nat.window_lut(plan.rows, T2.detach().contiguous())
+        if nw_pad > Z.shape[1]:
+            Zp = Z.new_zeros((Z.shape[0], nw_pad, 64))
+            Zp[:, :Z.shape[1]] = Z
+            Z = Zp
+        return Z
 
     @staticmethod
     def backward(ctx, dZ2w):
         dT2 = nat.segment_sum(dZ2w.contiguous(), ctx.plan.hist, nat.LUT2_ROWS, name="k_seg_sum_dT2")
-        return dT2, None
+        return dT2, None, None
+
+
+class _TunedBmm(torch.autograd.Function):
+    """A @ B (batched) with the forward and both backward GEMMs on the pre-tuned solutions
+    (merlin/gemm_tuning.py; autograd's own bmm backward would run outside tuned())."""
+
+    @staticmethod
+    def forward(ctx, A, B):
+        from .gemm_tuning import tuned
+
+        ctx.save_for_backward(A, B)
+        with tuned():
+            return torch.bmm(A, B)
+
+    @staticmethod
+    def backward(ctx, dC):
+        from .gemm_tuning import tuned
+
+        A, B = ctx.saved_tensors
+        dC = dC.contiguous()
+        with tuned():
+            dA = torch.bmm(dC, B.transpose(1, 2)) if ctx.needs_input_grad[0] else None
+            dB = torch.bmm(A.transpose(1, 2), dC) if ctx.needs_input_grad[1] else None
+        return dA, dB
 
 
 class _WindowConv3(torch.autograd.Function):
@@ -283,6 +314,7 @@ class _WindowConv3(torch.autograd.Function):
         Y3, bits = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous(), bits=True,
                                     rows=rows)
         ctx.save_for_backward(bits)
+        ctx.nw_q = Q.shape[1]
         ctx.plan, ctx.mb = plan, mb
         return Y3
 
@@ -300,19 +332,22 @@ class _WindowConv3(torch.autograd.Function):
         kmap[live] = live
         # pass 2: band sums over the live patches; pass 3: dQ[w][tap] from the bands
         S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=kmap, sub=1, name="k_seg_sum_S")
-        dQ = nat.segment_sum(S, plan.dq_plan, plan.num_windows * 9, name="k_seg_sum_dQ")
-        dQ = dQ.view(T, plan.num_windows, 9, 64)
+        nw = ctx.nw_q  # Q's rows (the windows, padded)
+        dQ = nat.segment_sum(S, plan.dq_plan, nw * 9, name="k_seg_sum_dQ")
+        dQ = dQ.view(T, nw, 9, 64)
         db3 = dQ[:, :, 0].sum(1)
-        return dQ.view(T, plan.num_windows, 576), db3, None, None, None
+        return dQ.view(T, nw, 576), db3, None, None, None
 
 
 def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = None) -> torch.Tensor:
     """relu(conv3(relu(conv2(relu(conv1(frame)))))) of both towers of CNNActorCritic `ac` for the
     minibatch's distinct frames: [2, U*9, 64], rows (u, p3), channels last ([2, rows*9, 64] with
     zero rows past U when rows is given)."""
+    from .gemm_tuning import padded_windows
+
     ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
-    Z2w = _WindowConv2.apply(ac.conv2_tables(), plan)
+    Z2w = _WindowConv2.apply(ac.conv2_tables(), plan, padded_windows(plan.num_windows))
     a2w = torch.relu(Z2w + torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1))
     W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
-    Q = torch.bmm(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
+    Q = _TunedBmm.apply(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
     return _WindowConv3.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), plan, mb, rows)

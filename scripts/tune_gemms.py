@@ -27,6 +27,10 @@ def main():
                                                   "gemm_gfx950.csv"))
     ap.add_argument("--inp", default=None, help="results to start from (default: --out if it exists)")
     ap.add_argument("--ms", type=int, default=10, help="max tuning ms per solution")
+    ap.add_argument("--windows", action="store_true", help="also the window GEMMs, --wlo..--whi windows")
+    ap.add_argument("--wlo", type=int, default=4096)
+    ap.add_argument("--whi", type=int, default=9984)
+    ap.add_argument("--no-rows", action="store_true", help="skip the fc1 row counts")
     args = ap.parse_args()
     from merlin.actor_critic import _splitk_bmm_tn, bias_relu_bmm
     from merlin.gemm_tuning import ROW_BUCKET
@@ -53,8 +57,20 @@ def main():
     torch.bmm(torch.randn(2, n, 576, device=dev), W.transpose(1, 2))
     torch.cuda.synchronize()
     print(f"rollout shapes ({n} envs) tuned, {time.time() - t0:.0f} s", flush=True)
+    if args.windows:
+        from merlin.gemm_tuning import WINDOW_BUCKET
+
+        W3r = torch.randn(2, 64, 576, device=dev)
+        for nw in range(args.wlo, args.whi + 1, WINDOW_BUCKET):  # merlin/windows.py _TunedBmm shapes
+            a2w = torch.randn(2, nw, 64, device=dev)
+            dQ = torch.randn(2, nw, 576, device=dev)
+            torch.bmm(a2w, W3r)
+            torch.bmm(dQ, W3r.transpose(1, 2))
+            torch.bmm(a2w.transpose(1, 2), dQ)
+        torch.cuda.synchronize()
+        print(f"window GEMMs tuned, {time.time() - t0:.0f} s", flush=True)
     lo = (args.lo + ROW_BUCKET - 1) // ROW_BUCKET * ROW_BUCKET
-    for npad in range(lo, args.hi + 1, ROW_BUCKET):
+    for npad in ([] if args.no_rows else range(lo, args.hi + 1, ROW_BUCKET)):
         a3 = torch.randn(2, npad, K, device=dev)
         dz = torch.randn(2, npad, H, device=dev)
         bias_relu_bmm(a3, W.transpose(1, 2), b)
