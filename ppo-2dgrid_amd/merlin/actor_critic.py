@@ -278,7 +278,7 @@ class _TowerHead(torch.autograd.Function):
         dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
         da3 = None
         if ctx.needs_input_grad[0]:
-            with _gemm_span("gemm_fc1_dgrad", dz.shape[0], n, W4p.shape[2], dz.shape[2]), tuned():
+            with _gemm_span("gemm_fc1_dgrad", dz.shape[0], n, W4p.shape[2], dz.shape[2]), tuned("dgrad"):
                 da3 = torch.bmm(dz, W4p)
         # (the split-K wgrad keeps hipBLASLt's pick: the searched solutions were faster in the
         # tuning loop, slower inside the update)
@@ -493,7 +493,7 @@ class CNNActorCritic(nn.Module):
         from .gemm_tuning import tuned
 
         # (conv3's N = 64 GEMM: bmm + k_bias_relu measured faster than the epilogue form here)
-        with tuned():
+        with tuned("rollout"):
             a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
             z = torch.bmm(a3, pack["W4t"])
         return nat.act_heads(z, pack["b4"], self.actor[2].weight, self.actor[2].bias, self.critic[2].weight,

@@ -1,25 +1,26 @@
 """Pre-tuned GEMM solutions for the update's fc1 GEMMs on gfx950 (PyTorch TunableOp).
 
-hipBLASLt's heuristic pick for the fc1 shapes runs at ~110-120 TFLOP/s of the 157.3 fp32 MFMA
-peak.  An exhaustive search over the hipBLASLt and rocBLAS solutions (scripts/tune_gemms.py,
-offline on an MI355X) finds faster kernels in its timing loop for all three fc1 GEMMs, but inside
-the update (inputs just written by the previous kernel, other work between the calls) only two
-held up: the input-gradient GEMM (a rocBLAS solution: 965-1020 -> 917 us per minibatch) and the
-rollout's fixed-shape conv3 / fc1 GEMMs (62 -> 44 us and 40 -> 38 us per step); the searched
+hipBLASLt's heuristic pick for the update's fc1 shapes runs at ~110-120 TFLOP/s of the 157.3
+fp32 MFMA peak.  An exhaustive search over the hipBLASLt and rocBLAS solutions
+(scripts/tune_gemms.py, offline on an MI355X) finds faster kernels in its timing loop for all
+three fc1 GEMMs and the window GEMMs, but inside the update most did not hold up: the searched
 forward and split-K weight-gradient solutions measured 6-20 % slower there than hipBLASLt's own
-pick (profiles/r02_tuning_ab.md) and are not shipped.  The kept results ship as a TunableOp CSV
-(tuning/gemm_gfx950.csv).  The file is read once with tuning OFF, and TunableOp dispatch is
-switched on only around the GEMMs it was made for (`with tuned():` in merlin/actor_critic.py: the
-update's fc1 and the rollout's conv3 / fc1): there a shape found in the file runs the recorded
-solution, any other runs PyTorch's default; every other GEMM of the process takes PyTorch's
-usual path.  Nothing is timed or written at run time.  The file's validator lines (PyTorch / HIP /
-hipBLASLt / rocBLAS versions, gfx950) make TunableOp reject it on any other stack.
+pick (profiles/r02_tuning_ab.md), and with the searched input-gradient solution (a rocBLAS
+global-split kernel, 965-1,020 -> 908 us per minibatch) -- together with the searched window
+GEMMs, or alone -- the training loop turned non-finite after 10-38 iterations while every
+checked call (each tuned GEMM re-run on the default path and compared, which serialises the
+stream) agreed to 5e-7 and the same loop without them ran 60 iterations clean
+(scripts/debug_nan.py).  So only the rollout's fixed-shape conv3 / fc1 GEMMs ship (rocBLAS
+solutions, 62 -> 44 us and 40 -> 38 us per step, clean over 45+ iterations), as a TunableOp CSV
+(tuning/gemm_gfx950.csv).  The machinery below (row / window padding to tuned counts, tuned
+window GEMMs) stays for shapes a future file may hold.
 
-The update's frame counts vary per minibatch, so fc1's row count is padded up to the next tuned
-row count when one lies within ROW_BUCKET (zero rows: they add exact zeros to the weight
-gradient, and their outputs are dropped); otherwise, and whenever the file is off, no padding.
-MERLIN_GEMM_TUNING=0 switches it off.
-"""
+The file is read once with tuning OFF, and TunableOp dispatch is switched on only around the
+GEMMs it was made for (`with tuned(which):`); there a shape found in the file runs the recorded
+solution, any other runs PyTorch's default, and every other GEMM of the process takes PyTorch's
+usual path.  Nothing is timed or written at run time.  The file's validator lines (PyTorch /
+HIP / hipBLASLt / rocBLAS versions, gfx950) make TunableOp reject it on any other stack.
+MERLIN_GEMM_TUNING=0 switches it off; MERLIN_UNTUNED=rollout,dgrad,window switches groups off."""
 from __future__ import annotations
 
 import contextlib
@@ -59,7 +60,8 @@ def enable(path: str = TUNED_FILE) -> bool:
 @contextlib.contextmanager
 def tuned(which: str = ""):
     """TunableOp dispatch (recorded solutions, no tuning) for the GEMMs inside the block."""
-    if not _state["on"] or (which and which in os.environ.get("MERLIN_UNTUNED", "").split(",")):
+    if (not _state["on"] or (which and which in os.environ.get("MERLIN_UNTUNED", "").split(","))
+            or os.environ.get("MERLIN_PAD_ONLY")):  # (testing: the padding without the tuned dispatch)
         yield
         return
     import torch.cuda.tunable as tunable
@@ -77,6 +79,8 @@ def active() -> bool:
 
 def padded_windows(n: int) -> int:
     """The tuned window-GEMM row count to pad n windows to (n when none lies within WINDOW_BUCKET)."""
+    if "window" in os.environ.get("MERLIN_UNTUNED", "").split(","):
+        return n
     for r in _state["windows"]:
         if n <= r < n + WINDOW_BUCKET:
             return r
@@ -85,6 +89,8 @@ def padded_windows(n: int) -> int:
 
 def padded_rows(n: int) -> int:
     """The tuned fc1 row count to pad n frames to (n itself when none lies within ROW_BUCKET)."""
+    if "dgrad" in os.environ.get("MERLIN_UNTUNED", "").split(","):
+        return n
     for r in _state["rows"]:  # (row counts of the dgrad entries: nn_576_<rows>_512)
         if n <= r < n + ROW_BUCKET:
             return r

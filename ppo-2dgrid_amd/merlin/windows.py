@@ -291,7 +291,7 @@ class _TunedBmm(torch.autograd.Function):
         from .gemm_tuning import tuned
 
         ctx.save_for_backward(A, B)
-        with tuned():
+        with tuned("window"):
             return torch.bmm(A, B)
 
     @staticmethod
@@ -300,7 +300,7 @@ class _TunedBmm(torch.autograd.Function):
 
         A, B = ctx.saved_tensors
         dC = dC.contiguous()
-        with tuned():
+        with tuned("window"):
             dA = torch.bmm(dC, B.transpose(1, 2)) if ctx.needs_input_grad[0] else None
             dB = torch.bmm(A.transpose(1, 2), dC) if ctx.needs_input_grad[1] else None
         return dA, dB
