@@ -282,6 +282,29 @@ class _WindowConv2(torch.autograd.Function):
         return dT2, None, None
 
 
+def _colsum(x):
+    """x [T, n, C] (rows may be strided) -> [T, C] column sums as a ones-row GEMM: torch's reduce
+    over dim 1 of these [2, ~6.5k, 64] shapes takes ~50 us, the GEMM a few."""
+    ones = x.new_ones((x.shape[0], 1, x.shape[1]))
+    return torch.bmm(ones, x).squeeze(1)
+
+
+class _BiasRelu(torch.autograd.Function):
+    """relu(Z + b[:, None]) for Z [T, n, C], b [T, C]; backward's bias gradient by _colsum."""
+
+    @staticmethod
+    def forward(ctx, Z, b):
+        A = torch.relu(Z + b.unsqueeze(1))
+        ctx.save_for_backward(A)
+        return A
+
+    @staticmethod
+    def backward(ctx, dA):
+        (A,) = ctx.saved_tensors
+        dZ = torch.where(A > 0, dA, torch.zeros((), dtype=dA.dtype, device=dA.device))
+        return dZ, _colsum(dZ)
+
+
 class _TunedBmm(torch.autograd.Function):
     """A @ B (batched) with the forward and both backward GEMMs on the pre-tuned solutions
     (merlin/gemm_tuning.py; autograd's own bmm backward would run outside tuned())."""
@@ -335,7 +358,7 @@ class _WindowConv3(torch.autograd.Function):
         nw = ctx.nw_q  # Q's rows (the windows, padded)
         dQ = nat.segment_sum(S, plan.dq_plan, nw * 9, name="k_seg_sum_dQ")
         dQ = dQ.view(T, nw, 9, 64)
-        db3 = dQ[:, :, 0].sum(1)
+        db3 = _colsum(dQ[:, :, 0])
         return dQ.view(T, nw, 576), db3, None, None, None
 
 
@@ -347,7 +370,7 @@ def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = N
 
     ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
     Z2w = _WindowConv2.apply(ac.conv2_tables(), plan, padded_windows(plan.num_windows))
-    a2w = torch.relu(Z2w + torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1))
+    a2w = _BiasRelu.apply(Z2w, torch.stack([ea[2].bias, ec[2].bias]))
     W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
     Q = _TunedBmm.apply(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
     return _WindowConv3.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), plan, mb, rows)

@@ -54,6 +54,11 @@ def main():
             rows.append((ka.self_device_time_total / steps, ka.count / steps, ka.key, str(ka.input_shapes)[:110]))
     for t, c, k, sh in sorted(rows, reverse=True)[:40]:
         print(f"{t:8.1f} us {c:5.1f}x {k:28s} {sh}", flush=True)
+    print("-- by op --", flush=True)
+    byop = [(ka.self_device_time_total / steps, ka.count / steps, ka.key) for ka in p.key_averages()
+            if ka.self_device_time_total > 0]
+    for t, c, k in sorted(byop, reverse=True)[:45]:
+        print(f"{t:8.1f} us {c:6.1f}x {k}", flush=True)
 
 
 if __name__ == "__main__":
