@@ -273,6 +273,15 @@ int merlin_tower_window_lut(const int32_t *rows_dev, int64_t n_windows, const fl
 int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
                               const int64_t *groups_dev, int64_t n, const float *b3_dev,
                               int32_t towers, float *Y3_dev, void *stream);
+/* conv3 of the acting path from a table over every possible 3x3 tile window:
+ * Qall_dev float[towers][merlin_tower_all_windows() = 5^9][9][64] (Q of merlin_tower_window_conv3
+ * for window id = the window's 9 tile classes in base 5, tile (0,0) most significant; built once
+ * per rollout, merlin/actor_critic.py rollout_pack);
+ * Y3[t][k*9 + p3][co] = relu(b3[t][co] + sum over the 9 taps of Qall[t][id of frame k's window at
+ * p3 + tap][tap][co]) for frames codes_dev[k] (8 words of tile-class nibbles, merlin_env_step). */
+int64_t merlin_tower_all_windows(void);
+int merlin_tower_codes_conv3(const uint32_t *codes_dev, int64_t n, const float *Qall_dev,
+                             const float *b3_dev, int32_t towers, float *Y3_dev, void *stream);
 /* Same, also writing relu_bits_dev uint64[towers][n*9]: bit co of row (k*9 + p3) = Y3 > 0 there. */
 int merlin_tower_window_conv3_bits(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
                                    const int64_t *groups_dev, int64_t n, const float *b3_dev,

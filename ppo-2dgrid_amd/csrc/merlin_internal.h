@@ -117,6 +117,8 @@ hipError_t launch_ppo_loss(const float *logits, const float *value, const float 
                            const float *ret, double clip_eps, double vf_coef, double ent_coef, float *dlogits,
                            float *dvalue, float *dbias_a, float *dbias_c, float *loss, double *stats,
                            double *workspace, hipStream_t s);
+hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, const float *b3, int T, float *Y3,
+                              hipStream_t s);
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,

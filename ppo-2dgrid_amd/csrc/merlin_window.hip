@@ -103,6 +103,50 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
     }
 }
 
+// The acting path's conv3 from a table over EVERY possible 3x3 tile window (5^9 = 1,953,125 rows, built
+// once per rollout from the fixed weights): Y3[t][u*9 + p3][c4] = relu(b3[t][c4] + sum_tap
+// Qall[t][key(u, p2(p3, tap))][tap][c4]), key = the frame's 3x3 tile classes at conv2 position p2 as 9
+// base-5 digits, tile (0, 0) most significant (merlin/windows.py window_keys) -- computed from the
+// frame's 49 class nibbles in registers, so conv2's lookups, conv3's im2col and its GEMM all drop out.
+constexpr int64_t ALL_WINDOWS = 1953125;
+__global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict__ codes, int64_t n,
+                                                     const float4 *__restrict__ Q, const float4 *__restrict__ b3,
+                                                     int T, float4 *__restrict__ Y3) {
+    const int64_t total = (int64_t)T * n * 9 * 16;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int c = (int)(e & 15);
+        const int64_t r = e >> 4, tu = r / 9;
+        const int p3 = (int)(r - tu * 9), t = (int)(tu / n);
+        const int64_t u = tu - (int64_t)t * n;
+        const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + u * 8);
+        const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + u * 8 + 4);
+        const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        auto cls = [&](int y, int x) -> uint32_t {  // tile class, clamped to 4 like the other kernels
+            const int cell = y * 7 + x;
+            return min((w[cell >> 3] >> (4 * (cell & 7))) & 15u, 4u);
+        };
+        const int oy = p3 / 3, ox = p3 - 3 * (p3 / 3);
+        const float4 *qt = Q + (size_t)t * ALL_WINDOWS * 9 * 16 + c;
+        float4 v[9];
+#pragma unroll
+        for (int tap = 0; tap < 9; tap++) {
+            const int wy = oy + tap / 3, wx = ox + tap - 3 * (tap / 3);
+            uint32_t key = 0;
+#pragma unroll
+            for (int a = 0; a < 3; a++)
+#pragma unroll
+                for (int b = 0; b < 3; b++) key = key * 5u + cls(wy + a, wx + b);
+            v[tap] = qt[((size_t)key * 9 + tap) * 16];
+        }
+        float4 acc = v[0];
+#pragma unroll
+        for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
+        const float4 b = b3[t * 16 + c];
+        Y3[e] = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
+                            relu_nan(acc.w + b.w));
+    }
+}
+
 // One wave per item of L entries; lane = (tower t, entry parity q, float4 column c): one wave
 // load reads the 256-B rows of two entries in both towers (1 KB, 16 B per lane).  The wave loads
 // 64 entries' (idx, key) at a time, resolves their source rows (through slot[] when given: -1 = not
@@ -283,6 +327,16 @@ hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, c
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
     hipLaunchKernelGGL(k_window_conv3, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4 *>(Q), nw, wid,
                        groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, const float *b3, int T, float *Y3,
+                              hipStream_t s) {
+    const int64_t total = (int64_t)T * n * 9 * 16;
+    if (total <= 0) return hipSuccess;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
+    hipLaunchKernelGGL(k_codes_conv3, dim3(grid), dim3(256), 0, s, codes, n, reinterpret_cast<const float4 *>(Q),
+                       reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3));
     return hipGetLastError();
 }
 

@@ -91,6 +91,8 @@ def lib():
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp]
+    L.merlin_tower_all_windows.restype = i64
+    L.merlin_tower_codes_conv3.argtypes = [vp, i64, vp, vp, i32, vp, vp]
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
     L.merlin_segment_sum_masked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                             vp]
@@ -137,7 +139,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
-    "merlin_tower_window_conv3_bits",
+    "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
 )
@@ -437,6 +439,25 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
     with KernelTimer.span("k_window_conv3", T * n * 9 * 256 + n * 108 + T * nw * 576 * 4):
         check(lib().merlin_tower_window_conv3(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
                                               stream_of(Q)), "merlin_tower_window_conv3")
+    return out
+
+
+ALL_WINDOWS = 5 ** 9  # merlin_tower_all_windows()
+
+
+def codes_conv3(codes, Qall, b3):
+    """Y3 f32[T, n*9, 64]: relu(conv3) rows (k, p3) of frames codes[k] (int32 [n, 8]) from Qall
+    f32[T, 5**9, 576], the per-window, per-tap conv3 partial sums of every possible window
+    (merlin_tower_codes_conv3)."""
+    T, n = int(Qall.shape[0]), int(codes.shape[0])
+    assert Qall.shape == (T, ALL_WINDOWS, 576) and Qall.dtype == torch.float32 and Qall.is_contiguous()
+    assert codes.dtype == torch.int32 and codes.shape[1] == 8 and codes.is_contiguous() and b3.shape == (T, 64)
+    out = torch.empty((T, n * 9, 64), dtype=torch.float32, device=Qall.device)
+    # algorithmic bytes: codes + Y3 written + the 81 Q rows of every frame and tower (random rows of a
+    # 9 GB table: HBM)
+    with KernelTimer.span("k_codes_conv3", n * 32 + T * n * 9 * 256 * 10):
+        check(lib().merlin_tower_codes_conv3(ptr(codes), n, ptr(Qall), ptr(b3), T, ptr(out), stream_of(Qall)),
+              "merlin_tower_codes_conv3")
     return out
 
 

@@ -366,6 +366,7 @@ class CNNActorCritic(nn.Module):
         self._atlas = None  # f32 [5, 3, 8, 8] / 255 on the model's device (codes path only)
         self._lut2_idx = None
         self._lut2_gather = None
+        self._all_rows = None  # int32 [5**9, 16] table rows of every window (acting path)
         # "lut2": conv1+conv2 as table lookups, conv3/fc as hipBLASLt GEMMs (default)
         # "gemm": conv1 lookups, conv2/conv3/fc as GEMMs | "lut_nchw": conv1 lookups + MIOpen convs
         self.codes_impl = "lut2"
@@ -463,18 +464,34 @@ class CNNActorCritic(nn.Module):
         fc = self.critic_extractor.network[2:](a1[1])
         return self.actor(fa), self.critic(fc).squeeze(-1)
 
+    def _all_window_rows(self, device):
+        """int32 [5**9, 16]: the conv2 table rows of every possible 3x3 tile window, window id =
+        its 9 classes in base 5 (merlin/windows.py window_rows), built once per device."""
+        if self._all_rows is None or self._all_rows.device != device:
+            from . import _native as nat
+            from .windows import window_rows
+
+            self._all_rows = window_rows(torch.arange(nat.ALL_WINDOWS, dtype=torch.int64, device=device)).contiguous()
+        return self._all_rows
+
     def rollout_pack(self):
         """The weights of the acting path in the layouts its kernels and GEMMs read, built once
-        per rollout (the weights do not change while acting): conv1+conv2 tables, conv3 as
-        [2, 576, 64], fc1 with columns permuted to (p3, co) as [2, 576, H], biases stacked."""
+        per rollout (the weights do not change while acting): conv2 (from the conv1+conv2 tables)
+        and conv3's per-tap products for EVERY possible 3x3 tile window, Qall [2, 5**9, 576] (9 GB:
+        conv2 + ReLU of all 1,953,125 windows and one [5**9, 64] x [64, 576] GEMM per tower, a few
+        ms per rollout), fc1 with columns permuted to (p3, co) as [2, 576, H], biases stacked."""
+        from . import _native as nat
+
         ea, ec = self.actor_extractor.network, self.critic_extractor.network
         fa, fc = self.actor[0], self.critic[0]
         W4 = torch.stack([fa.weight, fc.weight])
         H = W4.shape[1]
+        T2 = self.conv2_tables().contiguous()
+        Z2 = nat.window_lut(self._all_window_rows(T2.device), T2)  # [2, 5**9, 64]
+        a2 = torch.relu_(Z2.add_(torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1)))
+        W3r = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 2, 3, 4, 1).reshape(2, 64, 576)
         return {
-            "T2": self.conv2_tables().contiguous(),
-            "b2": torch.stack([ea[2].bias, ec[2].bias]).contiguous(),
-            "W3t": torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64).contiguous(),
+            "Qall": torch.bmm(a2, W3r),  # [2, windows, (ky, kx, co)]
             "b3": torch.stack([ea[4].bias, ec[4].bias]).contiguous(),
             "W4t": W4.view(2, H, 64, 9).transpose(2, 3).reshape(2, H, 576).transpose(1, 2).contiguous(),
             "b4": torch.stack([fa.bias, fc.bias]).contiguous(),
@@ -482,19 +499,17 @@ class CNNActorCritic(nn.Module):
 
     @torch.no_grad()
     def act_codes_packed(self, codes, pack, deterministic=False, seed=0, epoch=None, step=0, out=None, env_offset=0):
-        """act_codes with the layouts of rollout_pack(): conv1+conv2 lookups, conv3 as a plain bmm
-        + the HIP bias/ReLU epilogue, fc1 as a plain bmm, then fc1's bias/ReLU, the heads, the
-        log-probs and the categorical draw in one HIP pass (merlin_act_heads; draws keyed by
-        (seed, epoch[0], step, env_offset + env)).  out = (action, logp, value) tensors to write in place."""
+        """act_codes with the layouts of rollout_pack(): conv1+conv2+conv3 from the all-windows
+        table (merlin_tower_codes_conv3: 81 table rows per frame and tower), fc1 as a plain bmm,
+        then fc1's bias/ReLU, the heads, the log-probs and the categorical draw in one HIP pass
+        (merlin_act_heads; draws keyed by (seed, epoch[0], step, env_offset + env)).
+        out = (action, logp, value) tensors to write in place."""
         from . import _native as nat
-
-        n = codes.shape[0]
-        A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
         from .gemm_tuning import tuned
 
-        # (conv3's N = 64 GEMM: bmm + k_bias_relu measured faster than the epilogue form here)
+        n = codes.shape[0]
+        a3 = nat.codes_conv3(codes, pack["Qall"], pack["b3"]).view(2, n, 576)
         with tuned("rollout"):
-            a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
             z = torch.bmm(a3, pack["W4t"])
         return nat.act_heads(z, pack["b4"], self.actor[2].weight, self.actor[2].bias, self.critic[2].weight,
                              self.critic[2].bias, deterministic, seed=seed, epoch=epoch, step=step, out=out,

@@ -25,6 +25,28 @@ def test_packed_act_matches_act_codes(device):
     torch.testing.assert_close(v1, v2, rtol=1e-5, atol=1e-5)
 
 
+def test_codes_conv3_matches_im2col_path(device):
+    """merlin_tower_codes_conv3 over the all-windows table of rollout_pack() == conv2 lookups ->
+    conv3 im2col -> GEMM -> bias + ReLU (the per-frame path of evaluate_codes) on the same frames."""
+    from merlin import _native as nat
+    from merlin.actor_critic import CNNActorCritic
+    from test_gpu_conv2lut import _codes
+
+    _, codes = _codes(device, 900, seed=5)
+    torch.manual_seed(6)
+    ac = CNNActorCritic((56, 56, 3), 3).to(device)
+    ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
+    with torch.no_grad():
+        pack = ac.rollout_pack()
+        assert pack["Qall"].shape == (2, nat.ALL_WINDOWS, 576)
+        Y3 = nat.codes_conv3(codes, pack["Qall"], pack["b3"])
+        A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, ac.conv2_tables().contiguous()),
+                                  torch.stack([ea[2].bias, ec[2].bias]).contiguous())
+        W3t = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64)
+        ref = torch.relu(torch.bmm(A3, W3t) + torch.stack([ea[4].bias, ec[4].bias]).unsqueeze(1))
+    torch.testing.assert_close(Y3, ref, rtol=1e-5, atol=1e-5)
+
+
 def test_graph_rollout_matches_eager_env(device):
     from merlin import MerlinVecEnv
     from merlin.ppo import PPO
