@@ -42,11 +42,14 @@ os.environ.setdefault("MIOPEN_LOG_LEVEL", "3")
 FWD_MACS = 2 * (1_038_336 + 819_200 + 331_776 + 294_912) + 512 * 3 + 512
 BWD_MACS = 2 * FWD_MACS - 2 * 1_038_336
 # What this implementation runs on the matrix/vector FP32 units: conv1+conv2 are table
-# lookups (no MACs), so per rollout frame the GEMMs are conv3 + fc1 + heads of both towers;
-# in the update fc1 + heads run once per distinct frame of a minibatch (merlin/dedup.py) and
-# conv3 once per distinct receptive-field window of the rollout (merlin/windows.py: the
-# [windows, 64] x [64, 576] product per tower); backward = input grad + weight grad (2x).
-GEMM_FWD_MACS = 2 * (331_776 + 294_912) + 512 * 3 + 512
+# lookups (no MACs); per rollout frame fc1 + heads of both towers, and per rollout conv3's
+# all-windows table (one [5^9, 64] x [64, 576] product per tower, merlin/actor_critic.py
+# rollout_pack); in the update fc1 + heads run once per distinct frame of a minibatch
+# (merlin/dedup.py) and conv3 once per distinct receptive-field window of the rollout
+# (merlin/windows.py: the [windows, 64] x [64, 576] product per tower); backward = input grad +
+# weight grad (2x).
+GEMM_FWD_MACS = 2 * (331_776 + 294_912) + 512 * 3 + 512  # the per-frame formulation (no windows)
+ROLLOUT_TABLE_MACS = 2 * 5 ** 9 * 64 * 576  # per rollout
 FC_FWD_MACS = 2 * 294_912 + 512 * 3 + 512
 WINDOW_FWD_MACS = 2 * 64 * 576  # per window per minibatch
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -267,6 +270,18 @@ def pmc_traffic(kernel: str):
     return None
 
 
+def gather_note(name, k):
+    """k_window_conv3 reads no HBM to speak of: every output row sums 9 rows of the per-minibatch Q
+    table (~15 MB per tower, L2 / Infinity-Cache resident), so its bound is the cache gather rate
+    (MI355X_MICROARCH.md 'Indexed rows': 16.8-18.8 TB/s for L2-resident rows), not HBM."""
+    if name != "k_window_conv3":
+        return {}
+    gathered = 9 * k["bytes_per_launch"]  # ~ 9 Q rows of 256 B per written Y3 row
+    tbs = gathered / (k["avg_us"] * 1e-6) / 1e12
+    return {"cache_gather": {"bytes_per_launch": gathered, "achieved_tbs": round(tbs, 2),
+                             "guide_l2_gather_tbs": [16.8, 18.8], "frac_of_18_8": round(tbs / 18.8, 3)}}
+
+
 def kernel_table(records):
     """{name: launches, total ms, avg us, algorithmic bytes (GB/s) or flops (TFLOP/s) per launch}
     from HIP events."""
@@ -414,7 +429,7 @@ def main():
         upd = 3 * args.epochs * (FC_FWD_MACS * frac + WINDOW_FWD_MACS * agent.last_num_windows * args.minibatches / B)
     else:
         upd = 3 * args.epochs * GEMM_FWD_MACS * frac
-    exec_flop_per_step = 2 * (GEMM_FWD_MACS + upd)
+    exec_flop_per_step = 2 * (FC_FWD_MACS + ROLLOUT_TABLE_MACS / B + upd)
     loop_tflops = value / world * exec_flop_per_step / 1e12
     out = {
         "metric": "env-steps/sec (rollout+GAE+PPO update), 4096 envs, 16x16 mediumhard",
@@ -445,7 +460,8 @@ def main():
         # fc1 hipBLASLt GEMMs, which are timed the same way)
         "roofline": roofline_of(dominant, kernels[dominant]),
         # dominant hand-written kernel
-        "roofline_handwritten": roofline_of(handwritten, kernels[handwritten]),
+        "roofline_handwritten": dict(roofline_of(handwritten, kernels[handwritten]),
+                                     **gather_note(handwritten, kernels[handwritten])),
         # every hipBLASLt GEMM family timed in the loop against the f32 MFMA peak
         "roofline_gemm": {k: roofline_of(k, v) for k, v in kernels.items() if "tflops" in v},
         # the env-step kernel inside the timed loop (absent when the rollout replays as a graph:

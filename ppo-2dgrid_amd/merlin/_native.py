@@ -453,9 +453,9 @@ def codes_conv3(codes, Qall, b3):
     assert Qall.shape == (T, ALL_WINDOWS, 576) and Qall.dtype == torch.float32 and Qall.is_contiguous()
     assert codes.dtype == torch.int32 and codes.shape[1] == 8 and codes.is_contiguous() and b3.shape == (T, 64)
     out = torch.empty((T, n * 9, 64), dtype=torch.float32, device=Qall.device)
-    # algorithmic bytes: codes + Y3 written + the 81 Q rows of every frame and tower (random rows of a
-    # 9 GB table: HBM)
-    with KernelTimer.span("k_codes_conv3", n * 32 + T * n * 9 * 256 * 10):
+    # algorithmic bytes: codes read + Y3 written (the 81 Qall rows per frame and tower come from the
+    # few thousand windows a rollout holds: cache-resident gathers, rocprofv3 PMC ~38 MB per launch)
+    with KernelTimer.span("k_codes_conv3", n * 32 + T * n * 9 * 256):
         check(lib().merlin_tower_codes_conv3(ptr(codes), n, ptr(Qall), ptr(b3), T, ptr(out), stream_of(Qall)),
               "merlin_tower_codes_conv3")
     return out
