@@ -317,10 +317,12 @@ class PPO:
                 plan = WindowPlan(codes, groups)
                 self.last_num_windows = plan.num_windows
         distinct = 0
+        perms = [self._perm(B, epoch) for epoch in range(self.update_epochs)]  # drawn in epoch order
+        # one host read per update for every minibatch's distinct-frame groups (merlin/windows.py)
+        all_mbws = plan.update_minibatches(perms, self.minibatch_size) if plan is not None else None
         for epoch in range(self.update_epochs):
-            idxs = self._perm(B, epoch)
-            # one host read per epoch for the minibatches' distinct-frame groups (merlin/windows.py)
-            mbws = plan.epoch_minibatches(idxs, self.minibatch_size) if plan is not None else None
+            idxs = perms[epoch]
+            mbws = all_mbws[epoch] if all_mbws is not None else None
             for k, start in enumerate(range(0, B, self.minibatch_size)):
                 mb_idx = idxs[start:start + self.minibatch_size]
                 if plan is not None:

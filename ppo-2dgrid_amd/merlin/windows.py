@@ -146,7 +146,8 @@ class SegmentPlan:
         new = torch.ones(n, dtype=torch.bool, device=dev)
         new[1:] = key_sorted[1:] != key_sorted[:-1]
         start = torch.nonzero(new).squeeze(1)
-        end = torch.cat([start[1:], start.new_tensor([n])])
+        end = torch.full_like(start, n)
+        end[:-1] = start[1:]
         j0, j1 = start // L, (end - 1) // L
         x = j1 > j0
         self.fix = torch.stack([key_sorted[start[x]].long(), j0[x], j1[x], (start[x] != j0[x] * L).long()],
@@ -167,7 +168,10 @@ class MinibatchWindows:
 
 
 def _frame_csr(starts: torch.Tensor, n: int) -> torch.Tensor:
-    return torch.cat([starts, starts.new_tensor([n])]).to(torch.int32)
+    out = torch.empty(starts.numel() + 1, dtype=torch.int32, device=starts.device)
+    out[:-1] = starts
+    out[-1] = n  # a fill, not a host->device copy (no stream sync)
+    return out
 
 
 class WindowPlan:
@@ -220,13 +224,27 @@ class WindowPlan:
         dk, do = torch.sort(torch.cat([d for d, _ in wdst]), stable=True)
         self.dq_plan = SegmentPlan(dk, torch.cat([s for _, s in wdst])[do], item_len)
 
-    def epoch_minibatches(self, idxs: torch.Tensor, minibatch_size: int) -> list:
+    def update_minibatches(self, perms: list, minibatch_size: int) -> list:
+        """epoch_minibatches for every epoch's permutation at once: one stable sort and one host
+        read for the whole update (each host read drains the stream; per epoch that was ten
+        pipeline drains per update).  Returns one list of MinibatchWindows per epoch."""
+        B = int(perms[0].numel())
+        flat = self.epoch_minibatches(torch.cat(perms), minibatch_size, period=B)
+        nmb = (B + minibatch_size - 1) // minibatch_size
+        return [flat[e * nmb:(e + 1) * nmb] for e in range(len(perms))]
+
+    def epoch_minibatches(self, idxs: torch.Tensor, minibatch_size: int, period: int | None = None) -> list:
         """MinibatchWindows of every minibatch idxs[k*mb:(k+1)*mb] of one epoch's permutation,
         grouped by one stable sort and one host read for the whole epoch (a torch.unique per
-        minibatch would stall the host at every optimizer step).  Same groups as minibatch()."""
+        minibatch would stall the host at every optimizer step).  Same groups as minibatch().
+        period: idxs holds several epochs' permutations of that length back to back, each cut
+        into minibatches on its own (update_minibatches)."""
         dev, B, F = idxs.device, int(idxs.numel()), self.num_frames
-        nmb = (B + minibatch_size - 1) // minibatch_size
-        mb_of = torch.arange(B, device=dev) // minibatch_size
+        P = B if period is None else int(period)
+        per = (P + minibatch_size - 1) // minibatch_size
+        nmb = (B // P) * per
+        pos = torch.arange(B, device=dev)
+        mb_of = (pos // P) * per + (pos % P) // minibatch_size
         sk, perm = torch.sort(mb_of * F + self.frame_groups.uid[idxs], stable=True)
         new = torch.ones(B, dtype=torch.bool, device=dev)
         new[1:] = sk[1:] != sk[:-1]
@@ -237,7 +255,8 @@ class WindowPlan:
         counts = torch.bincount(uniq // F, minlength=nmb).tolist()
         out, off = [], 0
         for m, c in enumerate(counts):
-            lo, hi = m * minibatch_size, min(B, (m + 1) * minibatch_size)
+            e, k = divmod(m, per)
+            lo, hi = e * P + k * minibatch_size, e * P + min(P, (k + 1) * minibatch_size)
             g = uniq[off:off + c] % F
             slot = torch.full((F,), -1, dtype=torch.int32, device=dev)
             slot[g] = torch.arange(c, dtype=torch.int32, device=dev)

@@ -178,3 +178,13 @@ def test_epoch_minibatches_match_per_minibatch_grouping():
             frame_of = torch.repeat_interleave(torch.arange(f.numel() - 1), f[1:] - f[:-1])
             assert torch.equal(m.inv[o], frame_of)
             assert bool((o[1:] > o[:-1])[frame_of[1:] == frame_of[:-1]].all())
+    # every epoch at once (one host read per update) == epoch by epoch
+    perms = [torch.randperm(1000, generator=torch.Generator().manual_seed(s)) for s in (2, 3, 4)]
+    for mbs in (128, 300):
+        allm = plan.update_minibatches(perms, mbs)
+        for e, p in enumerate(perms):
+            ref = plan.epoch_minibatches(p, mbs)
+            assert len(allm[e]) == len(ref)
+            for m, r in zip(allm[e], ref):
+                for a in ("groups", "inv", "slot", "order", "offs"):
+                    assert torch.equal(getattr(m, a), getattr(r, a)), a
