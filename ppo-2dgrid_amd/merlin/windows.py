@@ -170,7 +170,7 @@ class MinibatchWindows:
 def _frame_csr(starts: torch.Tensor, n: int) -> torch.Tensor:
     out = torch.empty(starts.numel() + 1, dtype=torch.int32, device=starts.device)
     out[:-1] = starts
-    out[-1] = n  # a fill, not a host->device copy (no stream sync)
+    out[-1:].fill_(n)  # a fill kernel (indexed assignment of a Python int copies it host->device: a sync)
     return out
 
 
