@@ -185,7 +185,9 @@ class WindowPlan:
         rep = codes.index_select(0, frame_groups.rep)  # one code row per distinct frame
         F = int(rep.shape[0])
         cls = unpack_classes(rep)
-        uniq, inv = torch.unique(window_keys(cls).reshape(-1), return_inverse=True)
+        # (keys < 5**9, kid / band / window ids < 2**31: the sorts below run on int32 keys, half the
+        # radix passes of int64)
+        uniq, inv = torch.unique(window_keys(cls).reshape(-1).to(torch.int32), return_inverse=True)
         nw = int(uniq.numel())
         self.num_frames, self.num_windows = F, nw
         self.wid = inv.view(F, 25).to(torch.int32).contiguous()
@@ -200,7 +202,7 @@ class WindowPlan:
         pk, kid = torch.unique(patch_keys(cls).reshape(-1), return_inverse=True)
         self.num_patches = int(pk.numel())
         self.kid = kid.view(F, 9).to(torch.int32).contiguous()
-        ks, ko = torch.sort(kid, stable=True)
+        ks, ko = torch.sort(kid.to(torch.int32), stable=True)
         self.patch_plan = SegmentPlan(ks, ko, item_len)
         # band lists: entry (patch k, ky) -> S row band_off[ky] + (k's band ky); source R row k
         K = self.num_patches
@@ -215,13 +217,13 @@ class WindowPlan:
             # window at column kx (numbered by searching the sorted window keys)
             bd = digits5(ub, 15).view(-1, 3, 5)
             for kx in range(3):
-                w = torch.searchsorted(uniq, base5(bd[:, :, kx:kx + 3].reshape(-1, 9)))
+                w = torch.searchsorted(uniq, base5(bd[:, :, kx:kx + 3].reshape(-1, 9)).to(torch.int32))
                 wdst.append((w * 9 + ky * 3 + kx, off + torch.arange(ub.numel(), dtype=torch.int64, device=dev)))
             off += int(ub.numel())
         self.num_bands = off
-        bk, bo = torch.sort(torch.cat(bdst), stable=True)
+        bk, bo = torch.sort(torch.cat(bdst).to(torch.int32), stable=True)
         self.band_plan = SegmentPlan(bk, torch.cat(bsrc)[bo], item_len)
-        dk, do = torch.sort(torch.cat([d for d, _ in wdst]), stable=True)
+        dk, do = torch.sort(torch.cat([d for d, _ in wdst]).to(torch.int32), stable=True)
         self.dq_plan = SegmentPlan(dk, torch.cat([s for _, s in wdst])[do], item_len)
 
     def update_minibatches(self, perms: list, minibatch_size: int) -> list:
@@ -245,7 +247,10 @@ class WindowPlan:
         nmb = (B // P) * per
         pos = torch.arange(B, device=dev)
         mb_of = (pos // P) * per + (pos % P) // minibatch_size
-        sk, perm = torch.sort(mb_of * F + self.frame_groups.uid[idxs], stable=True)
+        key = mb_of * F + self.frame_groups.uid[idxs]
+        if nmb * F < 2 ** 31:  # int32 radix sort: half the passes
+            key = key.to(torch.int32)
+        sk, perm = torch.sort(key, stable=True)
         new = torch.ones(B, dtype=torch.bool, device=dev)
         new[1:] = sk[1:] != sk[:-1]
         inv = torch.empty(B, dtype=torch.int64, device=dev)

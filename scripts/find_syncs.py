@@ -37,6 +37,24 @@ def main():
     agent.update(lv)
     torch.cuda.set_sync_debug_mode("default")
     print(f"{sum(sites.values())} synchronising calls in one rollout + update", flush=True)
+    import time
+
+    from merlin.dedup import FrameGroups
+    from merlin.windows import WindowPlan
+    codes = agent.buf.flat_codes
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fg = FrameGroups(codes)
+        t1 = time.perf_counter()
+        plan = WindowPlan(codes, fg)
+        t2 = time.perf_counter()
+        perms = [torch.randperm(codes.shape[0], device=dev) for _ in range(10)]
+        plan.update_minibatches(perms, codes.shape[0] // 8)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        print(f"FrameGroups {1e3 * (t1 - t0):.1f} ms, WindowPlan {1e3 * (t2 - t1):.1f} ms, "
+              f"update_minibatches {1e3 * (t3 - t2):.1f} ms (wall, per update)", flush=True)
     for k, c in sites.most_common(40):
         print(f"{c:5d}  {k}", flush=True)
 
