@@ -256,7 +256,7 @@ class WindowPlan:
         inv = torch.empty(B, dtype=torch.int64, device=dev)
         inv[perm] = torch.cumsum(new, 0) - 1
         starts = torch.nonzero(new).squeeze(1)  # first sorted position of each (minibatch, frame)
-        uniq = sk[starts]
+        uniq = sk[starts].long()
         counts = torch.bincount(uniq // F, minlength=nmb).tolist()
         out, off = [], 0
         for m, c in enumerate(counts):

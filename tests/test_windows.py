@@ -170,6 +170,7 @@ def test_epoch_minibatches_match_per_minibatch_grouping():
         for k, m in enumerate(got):
             ref = plan.minibatch(idxs[k * mbs:(k + 1) * mbs])
             assert torch.equal(m.groups, ref.groups) and torch.equal(m.inv, ref.inv)
+            assert m.groups.dtype == torch.int64 and m.inv.dtype == torch.int64 and m.slot.dtype == torch.int32
             assert torch.equal(m.slot, ref.slot)
             assert torch.equal(m.order, ref.order) and torch.equal(m.offs, ref.offs)
             # CSR: frame u's samples are order[offs[u]:offs[u+1]], ascending, all with inv == u
