@@ -162,9 +162,50 @@ class MinibatchWindows:
     and the samples of each frame as CSR: order int32 [n] (sample positions grouped by frame,
     ascending within a frame), offs int32 [U+1] (merlin_ppo_loss sums per frame in that order)."""
 
-    def __init__(self, groups: torch.Tensor, inv: torch.Tensor, slot: torch.Tensor, order=None, offs=None):
-        self.groups, self.inv, self.slot = groups, inv, slot
-        self.order, self.offs = order, offs
+    def __init__(self, groups: torch.Tensor, inv: torch.Tensor, slot, order=None, offs=None, lazy=None):
+        self.groups = groups
+        self._inv, self._slot, self._order, self._offs = inv, slot, order, offs
+        # lazy = (F, inv_sorted, perm, starts, lo, hi, off): the tensors are derived on first use,
+        # when the minibatch's step runs (update_minibatches makes all 80 of an update right after
+        # its host read: derived there, their ~400 small launches would be host work with an idle GPU)
+        self._lazy = lazy
+
+    def _derive(self):
+        F, inv, perm, starts, lo, hi, off = self._lazy
+        g, dev = self.groups, self.groups.device
+        c = g.numel()
+        s = torch.full((F,), -1, dtype=torch.int32, device=dev)
+        s[g] = torch.arange(c, dtype=torch.int32, device=dev)
+        self._slot = s
+        self._inv = inv[lo:hi] - off
+        # sorted positions lo..hi hold exactly this minibatch's samples (mb_of is the major key)
+        self._order = (perm[lo:hi] - lo).to(torch.int32)
+        self._offs = _frame_csr(starts[off:off + c] - lo, hi - lo)
+        self._lazy = None
+
+    @property
+    def slot(self) -> torch.Tensor:
+        if self._lazy is not None:
+            self._derive()
+        return self._slot
+
+    @property
+    def inv(self) -> torch.Tensor:
+        if self._lazy is not None:
+            self._derive()
+        return self._inv
+
+    @property
+    def order(self):
+        if self._lazy is not None:
+            self._derive()
+        return self._order
+
+    @property
+    def offs(self):
+        if self._lazy is not None:
+            self._derive()
+        return self._offs
 
 
 def _frame_csr(starts: torch.Tensor, n: int) -> torch.Tensor:
@@ -259,15 +300,11 @@ class WindowPlan:
         uniq = sk[starts].long()
         counts = torch.bincount(uniq // F, minlength=nmb).tolist()
         out, off = [], 0
+        gall = uniq % F  # frame ids; each minibatch's groups are a view of it
         for m, c in enumerate(counts):
             e, k = divmod(m, per)
             lo, hi = e * P + k * minibatch_size, e * P + min(P, (k + 1) * minibatch_size)
-            g = uniq[off:off + c] % F
-            slot = torch.full((F,), -1, dtype=torch.int32, device=dev)
-            slot[g] = torch.arange(c, dtype=torch.int32, device=dev)
-            # sorted positions lo..hi hold exactly this minibatch's samples (mb_of is the major key)
-            order = (perm[lo:hi] - lo).to(torch.int32)
-            out.append(MinibatchWindows(g, inv[lo:hi] - off, slot, order, _frame_csr(starts[off:off + c] - lo, hi - lo)))
+            out.append(MinibatchWindows(gall[off:off + c], None, None, lazy=(F, inv, perm, starts, lo, hi, off)))
             off += c
         return out
 
