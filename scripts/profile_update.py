@@ -54,6 +54,13 @@ def main():
             rows.append((ka.self_device_time_total / steps, ka.count / steps, ka.key, str(ka.input_shapes)[:110]))
     for t, c, k, sh in sorted(rows, reverse=True)[:40]:
         print(f"{t:8.1f} us {c:5.1f}x {k:28s} {sh}", flush=True)
+    print("-- small ops by shape --", flush=True)
+    small = [r for r in rows if r[2] in ("aten::copy_", "aten::cat", "aten::add", "aten::fill_", "aten::mul",
+                                         "aten::_index_put_impl_", "aten::zero_", "aten::where", "aten::add_",
+                                         "aten::mul_", "aten::sub", "aten::threshold_backward", "aten::relu",
+                                         "aten::clone", "aten::index", "aten::gt", "aten::sum")]
+    for t, c, k, sh in sorted(small, reverse=True)[:40]:
+        print(f"{t:8.1f} us {c:5.1f}x {k:28s} {sh}", flush=True)
     print("-- by op --", flush=True)
     byop = [(ka.self_device_time_total / steps, ka.count / steps, ka.key) for ka in p.key_averages()
             if ka.self_device_time_total > 0]
