@@ -283,7 +283,8 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
     }
 }
 
-// fix rows (dst, j0, j1, slot0): out[t][dst] = carry[t][j0][slot0] + sum_{j0 < j <= j1} carry[t][j][0]
+// fix rows (dst, j0, j1, slot0): out[t][dst] = carry[t][j0][slot0] + sum_{j0 < j <= j1} carry[t][j][0];
+// rows with dst < 0 hold nothing (merlin/windows.py SegmentPlan: one row per item)
 __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carry, int64_t nitems,
                                                  const int4 *__restrict__ fix, int64_t nfix, int T,
                                                  float2 *__restrict__ out, int64_t out_rows, int acc_out) {
@@ -291,6 +292,7 @@ __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carr
     for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nfix; f += (int64_t)gridDim.x * 4) {
         if (t >= T) continue;
         const int4 x = fix[f];
+        if (x.x < 0) continue;
         const float2 *ct = carry + (size_t)t * nitems * 64 + c2;
         float2 acc = ct[(size_t)x.y * 64 + x.w * 32];
 #pragma unroll 8

@@ -480,7 +480,6 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
         assert mask.shape == (T, src_rows) and mask.is_contiguous()
     elif mask is not None:
         assert mask.shape == src.shape and mask.dtype == torch.float32 and mask.is_contiguous()
-    assert plan.max_key < out_rows
     if slot is not None:
         assert slot.dtype == torch.int32
     if out is None:

@@ -127,9 +127,10 @@ def window_rows(keys: torch.Tensor) -> torch.Tensor:
 class SegmentPlan:
     """A destination-sorted entry list for merlin_segment_sum: out[key[e]] = sum of src[row(e)]
     over the entries e of that key, in list order.  The list is cut into items of item_len
-    entries (one wave each); `fix` rows (dst, first item, last item, carry slot of the first
-    item) name the destinations whose entries span items: their items' partial sums are added
-    in item order."""
+    entries (one wave each); `fix` holds one row per item, (dst, first item, last item, carry slot
+    of the first item) for the destination that starts in that item and continues past it, or
+    dst = -1: its partial sums are added in item order.  Built without a host read (a stream
+    drain each): every size here is known from the list length."""
 
     def __init__(self, key_sorted: torch.Tensor, idx_sorted: torch.Tensor, item_len: int | None = None):
         dev = key_sorted.device
@@ -141,19 +142,20 @@ class SegmentPlan:
         self.idx = idx_sorted.to(torch.int32).contiguous()
         if n == 0:
             self.fix = torch.zeros((0, 4), dtype=torch.int32, device=dev)
-            self.max_key, self.num_segments = -1, 0
             return
+        pos = torch.arange(n, dtype=torch.int64, device=dev)
         new = torch.ones(n, dtype=torch.bool, device=dev)
-        new[1:] = key_sorted[1:] != key_sorted[:-1]
-        start = torch.nonzero(new).squeeze(1)
-        end = torch.full_like(start, n)
-        end[:-1] = start[1:]
-        j0, j1 = start // L, (end - 1) // L
-        x = j1 > j0
-        self.fix = torch.stack([key_sorted[start[x]].long(), j0[x], j1[x], (start[x] != j0[x] * L).long()],
-                               1).to(torch.int32).contiguous()
-        self.max_key = int(key_sorted[-1])
-        self.num_segments = int(start.numel())
+        new[1:] = self.key[1:] != self.key[:-1]
+        seg_start = torch.where(new, pos, torch.zeros_like(pos)).cummax(0).values
+        is_last = torch.ones(n, dtype=torch.bool, device=dev)
+        is_last[:-1] = new[1:]
+        seg_end = torch.where(is_last, pos + 1, torch.full_like(pos, n)).flip(0).cummin(0).values.flip(0)
+        j = torch.arange(self.nitems, dtype=torch.int64, device=dev)
+        p = torch.clamp((j + 1) * L, max=n) - 1  # each item's last entry
+        s, e = seg_start[p], seg_end[p]
+        live = (e > (j + 1) * L) & (s >= j * L)  # starts in this item, continues past it
+        dst = torch.where(live, self.key[p].long(), torch.full_like(j, -1))
+        self.fix = torch.stack([dst, j, (e - 1) // L, (s != j * L).long()], 1).to(torch.int32).contiguous()
 
 
 class MinibatchWindows:

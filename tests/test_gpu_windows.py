@@ -149,7 +149,8 @@ def test_segment_sum_masked_no_fill(device, L):
     # keys whose entries all fall outside the slot map: untouched, unless they span items (the
     # fix-up writes their zero carry)
     spans = torch.zeros(nkeys, dtype=torch.bool, device=device)
-    spans[plan.fix[:, 0].long()] = True
+    f = plan.fix[:, 0].long()
+    spans[f[f >= 0]] = True
     assert torch.isnan(out[:, ~live & ~spans]).all()
     assert (out[:, ~live & spans] == 0).all()
     err = (out[:, live].double() - ref[:, live]).abs()

@@ -65,6 +65,8 @@ def emulate_segment_sum(plan, src, out_rows, slot=None, sub=1, mask=None, fill=T
             else:
                 out[:, k] = a
     for d, j0, j1, s0 in plan.fix.tolist():
+        if d < 0:
+            continue
         a = carry[:, j0, s0].clone()
         for j in range(j0 + 1, j1 + 1):
             a += carry[:, j, 0]
