@@ -370,6 +370,9 @@ class CNNActorCritic(nn.Module):
         # "lut2": conv1+conv2 as table lookups, conv3/fc as hipBLASLt GEMMs (default)
         # "gemm": conv1 lookups, conv2/conv3/fc as GEMMs | "lut_nchw": conv1 lookups + MIOpen convs
         self.codes_impl = "lut2"
+        # fc1 of the update (heads_windows): "x6" = fp32 products on the bf16 matrix cores in exact
+        # three-plane form (csrc/merlin_gemm.hip); "hipblaslt" = torch's fp32 GEMMs
+        self.fc1_impl = "x6"
 
     # -- tile-code path (GPU envs) --------------------------------------------------
     def _atlas_on(self, device):
@@ -541,8 +544,10 @@ class CNNActorCritic(nn.Module):
         the rollout, fc1 and the heads once per distinct frame.  head_bias=False leaves the heads'
         biases out (merlin.ppo's fused loss adds them and returns their gradients)."""
         from .gemm_tuning import padded_rows
-        from .windows import tower_conv3
+        from .windows import tower_conv3, window_tower_head_x6
 
+        if self.fc1_impl == "x6":
+            return window_tower_head_x6(self, plan, mb, head_bias)
         n = int(mb.groups.numel())
         npad = padded_rows(n)  # fc1's rows on a tuned GEMM shape (merlin/gemm_tuning.py); zero rows past n
         logits, value = self._tower_head(tower_conv3(self, plan, mb, npad).view(2, npad, 576), npad, head_bias)

@@ -407,22 +407,66 @@ class _WindowConv3(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dY3):
         (bits,) = ctx.saved_tensors
-        plan, mb = ctx.plan, ctx.mb
-        T = bits.shape[0]
-        # pass 1: per-patch sums of the ReLU-masked dY3 rows of this minibatch's frames (rows of
-        # patches absent from the minibatch are left unwritten and skipped below)
-        R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
-                            name="k_seg_sum_R", mask=bits, fill=False)
-        live = plan.kid.index_select(0, mb.groups).reshape(-1)
-        kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32, device=bits.device)
-        kmap[live] = live
-        # pass 2: band sums over the live patches; pass 3: dQ[w][tap] from the bands
-        S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=kmap, sub=1, name="k_seg_sum_S")
-        nw = ctx.nw_q  # Q's rows (the windows, padded)
-        dQ = nat.segment_sum(S, plan.dq_plan, nw * 9, name="k_seg_sum_dQ")
-        dQ = dQ.view(T, nw, 9, 64)
-        db3 = _colsum(dQ[:, :, 0])
-        return dQ.view(T, nw, 576), db3, None, None, None
+        dQ, db3 = _conv3_backward(ctx.plan, ctx.mb, bits, dY3, ctx.nw_q)
+        return dQ, db3, None, None, None
+
+
+def _conv3_backward(plan, mb, bits, dY3, nw):
+    """(dQ [T, nw, 576], db3 [T, 64]) from dY3 [T, U*9, 64] (conv3's output gradient) and the ReLU bit
+    words of the forward: the patch -> band -> window segmented sums of the module docstring."""
+    T = bits.shape[0]
+    # pass 1: per-patch sums of the ReLU-masked dY3 rows of this minibatch's frames (rows of
+    # patches absent from the minibatch are left unwritten and skipped below)
+    R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
+                        name="k_seg_sum_R", mask=bits, fill=False)
+    live = plan.kid.index_select(0, mb.groups).reshape(-1)
+    kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32, device=bits.device)
+    kmap[live] = live
+    # pass 2: band sums over the live patches; pass 3: dQ[w][tap] from the bands
+    S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=kmap, sub=1, name="k_seg_sum_S")
+    dQ = nat.segment_sum(S, plan.dq_plan, nw * 9, name="k_seg_sum_dQ")
+    dQ = dQ.view(T, nw, 9, 64)
+    db3 = _colsum(dQ[:, :, 0])
+    return dQ.view(T, nw, 576), db3
+
+
+class _WindowTowerHeadX6(torch.autograd.Function):
+    """conv3 -> fc1 -> ReLU -> heads of both towers for the minibatch's distinct frames, with fc1's
+    three GEMMs on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip):
+      forward   a3 = relu(conv3) from Q (k_window_conv3, written straight into x6 planes, plus the
+                ReLU bit words), h = relu(a3 W4p^T + b4) (merlin_x6_gemm_nt, bias + ReLU epilogue),
+                logits = h0 Wa^T (+ ba), value = h1 wc (+ bc)   (src/actor_critic.py:13-14, 31-41)
+      backward  the heads' backward through fc1's ReLU (k_head_bwd, dz written in x6 planes), da3 =
+                dz W4p (x6 NT against W4p^T), dW4p = dz^T a3 (x6 TN, split-K), then conv3's backward
+                through the patch / band / window sums (_conv3_backward).
+    fp32 products throughout; no fp32 copy of a3 or dz exists."""
+
+    @staticmethod
+    def forward(ctx, Q, b3, W4p, b4, Wa, ba, Wc, bc, plan, mb):
+        a3p, bits = nat.window_conv3_x6(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous())
+        W4pp = nat.x6_split(W4p.detach())
+        h = nat.x6_gemm_nt(a3p, W4pp, bias=b4.detach(), cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
+        logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
+        value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)
+        ctx.save_for_backward(a3p, bits, W4p, h, Wa, Wc)
+        ctx.head_bias = (ba is not None, bc is not None)
+        ctx.plan, ctx.mb, ctx.nw_q = plan, mb, Q.shape[1]
+        return logits, value
+
+    @staticmethod
+    def backward(ctx, dlogits, dvalue):
+        a3p, bits, W4p, h, Wa, Wc = ctx.saved_tensors
+        n = h.shape[1]
+        dlogits = h.new_zeros(n, Wa.shape[0]) if dlogits is None else dlogits.contiguous()
+        dvalue = h.new_zeros(n) if dvalue is None else dvalue.contiguous()
+        dzp, db4, dWa, dWc = nat.head_bwd_x6(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
+        W4tp = nat.x6_split(W4p.detach().transpose(1, 2).contiguous())
+        da3 = nat.x6_gemm_nt(dzp, W4tp, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+        dW4p = nat.x6_gemm_tn(dzp, a3p, name="gemm_wgrad")
+        dQ, db3 = _conv3_backward(ctx.plan, ctx.mb, bits, da3.view(2, n * 9, 64), ctx.nw_q)
+        dba = dlogits.sum(0) if ctx.head_bias[0] else None
+        dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
+        return dQ, db3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc, None, None
 
 
 def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = None) -> torch.Tensor:
@@ -437,3 +481,21 @@ def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = N
     W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
     Q = _TunedBmm.apply(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
     return _WindowConv3.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), plan, mb, rows)
+
+
+def window_tower_head_x6(ac, plan: WindowPlan, mb: MinibatchWindows, head_bias: bool = True):
+    """(logits [U, act_dim], value [U]) of the minibatch's distinct frames: conv2 / conv3 through
+    the windows, fc1 on the bf16 matrix cores in exact three-plane form (_WindowTowerHeadX6)."""
+    from .gemm_tuning import padded_windows
+
+    ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
+    Z2w = _WindowConv2.apply(ac.conv2_tables(), plan, padded_windows(plan.num_windows))
+    a2w = _BiasRelu.apply(Z2w, torch.stack([ea[2].bias, ec[2].bias]))
+    W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
+    Q = _TunedBmm.apply(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
+    fa, fc = ac.actor[0], ac.critic[0]
+    W4 = torch.stack([fa.weight, fc.weight])  # [2, hidden, 576] in (co, p3) order
+    W4p = W4.view(2, W4.shape[1], 64, 9).transpose(2, 3).reshape(2, W4.shape[1], 576)
+    ba, bc = (ac.actor[2].bias, ac.critic[2].bias) if head_bias else (None, None)
+    return _WindowTowerHeadX6.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), W4p, torch.stack([fa.bias, fc.bias]),
+                                    ac.actor[2].weight, ba, ac.critic[2].weight, bc, plan, mb)
