@@ -110,7 +110,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restric
     static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
     // two LDS stages: step kt+1 is written into the other stage while step kt is multiplied, one
     // barrier per step; the registers hold step kt+2 in flight (issued a whole step before use)
-    constexpr int STAGE = 3 * (BM + BN) * 4;
+    // plane p of the A / B image at p * PSA / 3 * PSA + p * PSB chunks: the 12-chunk pad per plane
+    // (plus the chunk order of the staging loads, planes major within a row) makes every 16-lane
+    // group of the staging writes, and of the fragment reads, hit 16 distinct bank slots
+    constexpr int PSA = BM * 4 + 12, PSB = BN * 4 + 12;
+    constexpr int STAGE = 3 * (PSA + PSB);
     __shared__ u32x4 lds[2 * STAGE];
 
     const int t = blockIdx.y;
@@ -129,19 +133,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restric
 #pragma unroll
     for (int i = 0; i < CA; i++) {
         const int q = tid + i * NT;
-        const int row = q / CPR, rem = q - (q / CPR) * CPR, g = rem / 3, p = rem - (rem / 3) * 3;
+        const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
         const int64_t grow = std::min<int64_t>(m0 + std::min(row, BM - 1), M - 1);
-        ga[i] = A + grow * rowA + rem;
-        la[i] = (p * BM + row) * 4 + (g ^ ((row >> 2) & 3));
+        ga[i] = A + grow * rowA + g * 3 + p;
+        la[i] = p * PSA + row * 4 + (g ^ ((row >> 2) & 3));
     }
     const u32x4 *gb[CB];
     int lb[CB];
 #pragma unroll
     for (int i = 0; i < CB; i++) {
         const int q = tid + i * NT;
-        const int row = q / CPR, rem = q - (q / CPR) * CPR, g = rem / 3, p = rem - (rem / 3) * 3;
-        gb[i] = B + (int64_t)(n0 + std::min(row, BN - 1)) * rowA + rem;
-        lb[i] = 3 * BM * 4 + (p * BN + row) * 4 + (g ^ ((row >> 2) & 3));
+        const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
+        gb[i] = B + (int64_t)(n0 + std::min(row, BN - 1)) * rowA + g * 3 + p;
+        lb[i] = 3 * PSA + p * PSB + row * 4 + (g ^ ((row >> 2) & 3));
     }
     u32x4 ra[CA], rb[CB];
     auto load = [&](int kt) {
@@ -177,18 +181,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restric
         const int buf = kt & 1;
         if (kt + 1 < nk) store(buf ^ 1);
         if (kt + 2 < nk) load(kt + 2);
-        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * BM * 4;
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * PSA;
         if constexpr (FM <= FN) {  // A fragments resident, B streamed
             u32x4 af[FM][3];
 #pragma unroll
             for (int i = 0; i < FM; i++)
 #pragma unroll
-                for (int p = 0; p < 3; p++) af[i][p] = sAl[(p * BM + wm * WTM + i * 16 + fr) * 4 + fc];
+                for (int p = 0; p < 3; p++) af[i][p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
 #pragma unroll
             for (int j = 0; j < FN; j++) {
                 u32x4 bf[3];
 #pragma unroll
-                for (int p = 0; p < 3; p++) bf[p] = sBl[(p * BN + wn * WTN + j * 16 + fr) * 4 + fc];
+                for (int p = 0; p < 3; p++) bf[p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
 #pragma unroll
                 for (int i = 0; i < FM; i++) acc[i][j] = mma6(af[i], bf, acc[i][j]);
             }
@@ -197,12 +201,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restric
 #pragma unroll
             for (int j = 0; j < FN; j++)
 #pragma unroll
-                for (int p = 0; p < 3; p++) bf[j][p] = sBl[(p * BN + wn * WTN + j * 16 + fr) * 4 + fc];
+                for (int p = 0; p < 3; p++) bf[j][p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
 #pragma unroll
             for (int i = 0; i < FM; i++) {
                 u32x4 af[3];
 #pragma unroll
-                for (int p = 0; p < 3; p++) af[p] = sAl[(p * BM + wm * WTM + i * 16 + fr) * 4 + fc];
+                for (int p = 0; p < 3; p++) af[p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
 #pragma unroll
                 for (int j = 0; j < FN; j++) acc[i][j] = mma6(af, bf[j], acc[i][j]);
             }
@@ -226,6 +230,159 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restric
                 }
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The same product as a persistent kernel: one block per CU walks its tiles (tile j*G + base, tiles
+// numbered (t, tm, tn) with tn fastest; base puts G/8 consecutive tiles on each XCD per round, so
+// the BN-column tiles of one A panel run together on one L2) as one flat stream of k steps: the
+// loads of the next tile's first steps are in flight while the current tile finishes, and the
+// epilogue's stores overlap the next tile's multiplies.  G % 8 == 0.
+template <int BM, int BN, int WGM, int WGN, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_x6_ntp(const u32x4 *__restrict__ A, const u32x4 *__restrict__ B,
+                                                           int64_t M, int N, int K, int64_t sA, int64_t sB,
+                                                           const float *__restrict__ bias, float *__restrict__ C,
+                                                           int64_t sC, int tiles_m, int tiles_n, int T) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int FM = WTM / 16, FN = WTN / 16;
+    constexpr int CA = (BM * CPR + NT - 1) / NT, CB = (BN * CPR + NT - 1) / NT;
+    static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+    constexpr int PSA = BM * 4 + 12, PSB = BN * 4 + 12;
+    constexpr int STAGE = 3 * (PSA + PSB);
+    __shared__ u32x4 lds[2 * STAGE];
+
+    const int G = gridDim.x, b = blockIdx.x;
+    const int base = (b & 7) * (G >> 3) + (b >> 3);
+    const int per_t = tiles_m * tiles_n, total = T * per_t;
+    const int nk = K / BK;
+    const int ntl = base < total ? (total - base + G - 1) / G : 0;
+    const int steps = ntl * nk;
+    if (steps == 0) return;
+    const int64_t rowA = (int64_t)(K / 8) * 3;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    int rA[CA], oA[CA], la[CA];
+#pragma unroll
+    for (int i = 0; i < CA; i++) {
+        const int q = tid + i * NT;
+        const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
+        rA[i] = std::min(row, BM - 1);
+        oA[i] = g * 3 + p;
+        la[i] = p * PSA + row * 4 + (g ^ ((row >> 2) & 3));
+    }
+    int oB[CB], lb[CB];
+#pragma unroll
+    for (int i = 0; i < CB; i++) {
+        const int q = tid + i * NT;
+        const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
+        oB[i] = std::min(row, BN - 1) * (int)rowA + g * 3 + p;
+        lb[i] = 3 * PSA + p * PSB + row * 4 + (g ^ ((row >> 2) & 3));
+    }
+    auto tile_of = [&](int j, int &t, int &tm, int &tn) {
+        const int id = j * G + base;
+        t = id / per_t;
+        const int r = id - t * per_t;
+        tm = r / tiles_n;
+        tn = r - tm * tiles_n;
+    };
+    u32x4 ra[CA], rb[CB];
+    auto load = [&](int s) {
+        const int j = s / nk, kt = s - j * nk;
+        int t, tm, tn;
+        tile_of(j, t, tm, tn);
+        const u32x4 *Ab = A + t * sA + kt * CPR;
+        const u32x4 *Bb = B + t * sB + (int64_t)tn * BN * rowA + kt * CPR;
+        const int64_t m0 = (int64_t)tm * BM;
+#pragma unroll
+        for (int i = 0; i < CA; i++) ra[i] = Ab[std::min<int64_t>(m0 + rA[i], M - 1) * rowA + oA[i]];
+#pragma unroll
+        for (int i = 0; i < CB; i++) rb[i] = Bb[oB[i]];
+    };
+    auto store = [&](int buf) {
+        u32x4 *st = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < CA; i++)
+            if ((BM * CPR) % NT == 0 || i + 1 < CA || tid + i * NT < BM * CPR) st[la[i]] = ra[i];
+#pragma unroll
+        for (int i = 0; i < CB; i++)
+            if ((BN * CPR) % NT == 0 || i + 1 < CB || tid + i * NT < BN * CPR) st[lb[i]] = rb[i];
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    const int fr = lane & 15, fc = (lane >> 4) ^ ((lane & 15) >> 2);
+    load(0);
+    store(0);
+    if (steps > 1) load(1);
+    __syncthreads();
+    int kt = 0, jt = 0;
+    for (int s = 0; s < steps; s++) {
+        const int buf = s & 1;
+        if (s + 1 < steps) store(buf ^ 1);
+        if (s + 2 < steps) load(s + 2);
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * PSA;
+        if constexpr (FM <= FN) {
+            u32x4 af[FM][3];
+#pragma unroll
+            for (int i = 0; i < FM; i++)
+#pragma unroll
+                for (int p = 0; p < 3; p++) af[i][p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                u32x4 bf[3];
+#pragma unroll
+                for (int p = 0; p < 3; p++) bf[p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
+#pragma unroll
+                for (int i = 0; i < FM; i++) acc[i][j] = mma6(af[i], bf, acc[i][j]);
+            }
+        } else {
+            u32x4 bf[FN][3];
+#pragma unroll
+            for (int j = 0; j < FN; j++)
+#pragma unroll
+                for (int p = 0; p < 3; p++) bf[j][p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                u32x4 af[3];
+#pragma unroll
+                for (int p = 0; p < 3; p++) af[p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
+#pragma unroll
+                for (int j = 0; j < FN; j++) acc[i][j] = mma6(af, bf[j], acc[i][j]);
+            }
+        }
+        if (++kt == nk) {  // tile done: epilogue, fresh accumulators
+            int t, tm, tn;
+            tile_of(jt, t, tm, tn);
+            float *Ct = C + t * sC;
+            const int64_t m0 = (int64_t)tm * BM;
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                const int col = tn * BN + wn * WTN + j * 16 + fr;
+                const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
+#pragma unroll
+                for (int i = 0; i < FM; i++) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int64_t row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + r;
+                        if (row < M) {
+                            const float v = acc[i][j][r];
+                            Ct[row * N + col] = EPI == 1 ? relu_nan(v + bv) : v;
+                        }
+                    }
+                    acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                }
+            }
+            kt = 0;
+            jt++;
+        }
+        __syncthreads();
     }
 }
 
@@ -272,7 +429,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const u32x4 *__restric
     constexpr int CA = (QA + NT - 1) / NT, CB = (QB + NT - 1) / NT;
     static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
     // two LDS stages, one barrier per step (as k_x6_nt)
-    constexpr int STAGE = 3 * BK * (RCA + RCB);
+    // plane images of BK * RC chunks, padded to keep the staging writes conflict-free (rows of 16k + 8
+    // chunks), planes major in the staging order
+    constexpr int PSA = BK * RCA + (RCA % 16 ? 8 : 0), PSB = BK * RCB + (RCB % 16 ? 8 : 0);
+    constexpr int STAGE = 3 * (PSA + PSB);
     __shared__ u32x4 lds[2 * STAGE];
 
     const int t = blockIdx.z, s = blockIdx.y;
@@ -291,20 +451,20 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const u32x4 *__restric
     for (int i = 0; i < CA; i++) {
         const int q = tid + i * NT;
         const int k = std::min(q, QA - 1) / (RCA * 3), rem = std::min(q, QA - 1) - k * (RCA * 3);
-        const int g = rem / 3, p = rem - (rem / 3) * 3;
+        const int p = rem / RCA, g = rem - (rem / RCA) * RCA;
         ka[i] = k;
-        oa[i] = rem;
-        la[i] = (p * BK + k) * RCA + (g ^ tr_swz<RCA>(k));
+        oa[i] = g * 3 + p;
+        la[i] = p * PSA + k * RCA + (g ^ tr_swz<RCA>(k));
     }
     int kb[CB], ob[CB], lb[CB];
 #pragma unroll
     for (int i = 0; i < CB; i++) {
         const int q = tid + i * NT;
         const int k = std::min(q, QB - 1) / (RCB * 3), rem = std::min(q, QB - 1) - k * (RCB * 3);
-        const int g = rem / 3, p = rem - (rem / 3) * 3;
+        const int p = rem / RCB, g = rem - (rem / RCB) * RCB;
         kb[i] = k;
-        ob[i] = rem;
-        lb[i] = 3 * BK * RCA + (p * BK + k) * RCB + (g ^ tr_swz<RCB>(k));
+        ob[i] = g * 3 + p;
+        lb[i] = 3 * PSA + p * PSB + k * RCB + (g ^ tr_swz<RCB>(k));
     }
     const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
     u32x4 ra[CA], rb[CB];
@@ -348,18 +508,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const u32x4 *__restric
     for (int64_t kk = k0; kk < k1; kk += BK, buf ^= 1) {
         if (kk + BK < k1) store(buf ^ 1);
         if (kk + 2 * BK < k1) load(kk + 2 * BK);
-        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * BK * RCA;
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * PSA;
         if constexpr (FM <= FN) {
             bf16x8 af[FM][3];
 #pragma unroll
             for (int i = 0; i < FM; i++)
 #pragma unroll
-                for (int p = 0; p < 3; p++) af[i][p] = tr_frag<RCA>(sAl + p * BK * RCA, wm * WTM + i * 16, lane);
+                for (int p = 0; p < 3; p++) af[i][p] = tr_frag<RCA>(sAl + p * PSA, wm * WTM + i * 16, lane);
 #pragma unroll
             for (int j = 0; j < FN; j++) {
                 bf16x8 bf[3];
 #pragma unroll
-                for (int p = 0; p < 3; p++) bf[p] = tr_frag<RCB>(sBl + p * BK * RCB, wn * WTN + j * 16, lane);
+                for (int p = 0; p < 3; p++) bf[p] = tr_frag<RCB>(sBl + p * PSB, wn * WTN + j * 16, lane);
 #pragma unroll
                 for (int i = 0; i < FM; i++) acc[i][j] = mma6(af[i], bf, acc[i][j]);
             }
@@ -368,12 +528,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const u32x4 *__restric
 #pragma unroll
             for (int j = 0; j < FN; j++)
 #pragma unroll
-                for (int p = 0; p < 3; p++) bf[j][p] = tr_frag<RCB>(sBl + p * BK * RCB, wn * WTN + j * 16, lane);
+                for (int p = 0; p < 3; p++) bf[j][p] = tr_frag<RCB>(sBl + p * PSB, wn * WTN + j * 16, lane);
 #pragma unroll
             for (int i = 0; i < FM; i++) {
                 bf16x8 af[3];
 #pragma unroll
-                for (int p = 0; p < 3; p++) af[p] = tr_frag<RCA>(sAl + p * BK * RCA, wm * WTM + i * 16, lane);
+                for (int p = 0; p < 3; p++) af[p] = tr_frag<RCA>(sAl + p * PSA, wm * WTM + i * 16, lane);
 #pragma unroll
                 for (int j = 0; j < FN; j++) acc[i][j] = mma6(af, bf[j], acc[i][j]);
             }
@@ -426,6 +586,37 @@ hipError_t nt_launch(const u32x4 *A, const u32x4 *B, int64_t M, int N, int K, in
     else
         hipLaunchKernelGGL((k_x6_nt<BM, BN, WGM, WGN, 0>), grid, dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB,
                            nullptr, C, sC, tiles_n);
+    return hipGetLastError();
+}
+
+int num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            n = v;
+        else
+            n = 256;
+    }
+    return n;
+}
+
+template <int BM, int BN, int WGM, int WGN>
+hipError_t ntp_launch(const u32x4 *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
+                      const float *bias, float *C, int64_t sC, hipStream_t s) {
+    if (N % BN) return hipErrorInvalidValue;
+    const int64_t tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = N / BN;
+    const int64_t total = tiles_m * tiles_n * T;
+    if (total > INT32_MAX / 2) return hipErrorInvalidValue;
+    const int G = (int)std::min<int64_t>((total + 7) / 8 * 8, num_cus() / 8 * 8);
+    if (bias)
+        hipLaunchKernelGGL((k_x6_ntp<BM, BN, WGM, WGN, 1>), dim3(G), dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB,
+                           bias, C, sC, (int)tiles_m, tiles_n, T);
+    else
+        hipLaunchKernelGGL((k_x6_ntp<BM, BN, WGM, WGN, 0>), dim3(G), dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB,
+                           nullptr, C, sC, (int)tiles_m, tiles_n, T);
     return hipGetLastError();
 }
 
@@ -486,6 +677,10 @@ hipError_t launch_x6_gemm_nt(const void *A, const void *B, int64_t M, int N, int
         case 3: return nt_launch<128, 192, 2, 4>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         case 4: return nt_launch<128, 96, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         case 5: return nt_launch<256, 64, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 6: return ntp_launch<256, 128, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 7: return ntp_launch<128, 192, 2, 4>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 8: return ntp_launch<256, 64, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 9: return ntp_launch<128, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -143,16 +143,13 @@ class SegmentPlan:
         if n == 0:
             self.fix = torch.zeros((0, 4), dtype=torch.int32, device=dev)
             return
-        pos = torch.arange(n, dtype=torch.int64, device=dev)
-        new = torch.ones(n, dtype=torch.bool, device=dev)
-        new[1:] = self.key[1:] != self.key[:-1]
-        seg_start = torch.where(new, pos, torch.zeros_like(pos)).cummax(0).values
-        is_last = torch.ones(n, dtype=torch.bool, device=dev)
-        is_last[:-1] = new[1:]
-        seg_end = torch.where(is_last, pos + 1, torch.full_like(pos, n)).flip(0).cummin(0).values.flip(0)
         j = torch.arange(self.nitems, dtype=torch.int64, device=dev)
         p = torch.clamp((j + 1) * L, max=n) - 1  # each item's last entry
-        s, e = seg_start[p], seg_end[p]
+        # [s, e) = the run of p's key in the sorted list: two binary searches per item (a cummax /
+        # cummin scan over all n entries took ~1.3 ms each at the bench size)
+        kp = self.key[p].contiguous()
+        s = torch.searchsorted(self.key, kp, side="left")
+        e = torch.searchsorted(self.key, kp, side="right")
         live = (e > (j + 1) * L) & (s >= j * L)  # starts in this item, continues past it
         dst = torch.where(live, self.key[p].long(), torch.full_like(j, -1))
         self.fix = torch.stack([dst, j, (e - 1) // L, (s != j * L).long()], 1).to(torch.int32).contiguous()
