@@ -371,37 +371,27 @@ int merlin_tower_head_bwd(const float *h_dev, const float *dlogits_dev, const fl
                           float *dw_critic_dev, void *stream);
 
 /* fc1 (src/actor_critic.py:31-41, Linear(576, 512) of both towers) on the bf16 matrix cores in fp32
- * (csrc/merlin_gemm.hip): an fp32 matrix X[R][C] (C % 8 == 0) is held as "x6 planes", bf16
- * [R][C/8][3][8]: per group of 8 values three 16-byte chunks x0, x1, x2 with x = x0 + x1 + x2
- * exactly (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)), and a product is the six
- * plane products with i + j <= 2 accumulated in fp32 (the terms left out are below one fp32
- * rounding).  Replaces the three fp32 GEMMs of CNNActorCritic's fc1 in PPO.update (forward
- * src/actor_critic.py:40, backward through autograd at src/ppo.py:153-155).
+ * (csrc/merlin_gemm.hip): every fp32 operand value x is used as three bf16 planes x0 + x1 + x2 == x
+ * (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)), and a product as the six plane products
+ * with i + j <= 2 (the terms left out are below one fp32 rounding), summed per 32-deep k step and
+ * added to the fp32 running sum once.  Replaces the three fp32 GEMMs of CNNActorCritic's fc1 in
+ * PPO.update (forward src/actor_critic.py:40, backward through autograd at src/ppo.py:153-155).
+ * The weights are passed as "x6 planes", bf16 [R][C/8][3][8] (per group of 8 values three 16-byte
+ * chunks, planes 0, 1, 2; merlin_x6_split); the activations as plain fp32, split while staged.
  * split / join: n fp32 values (n % 8 == 0) <-> their planes (6 bytes per value).
- * gemm_nt:  C[t][m][n] = sum_k A[t][m][k] B[t][n][k] (A planes [M][K/8][3][8], B planes [N][K/8][3][8],
- *           K % 32 == 0, tower strides in values), + bias[t][n] and ReLU when bias != NULL;
- *           cfg selects the tile (0: 128x128, 1: 128x64, 2: 256x128, 3: 128x192, 4: 128x96, 5: 256x64;
- *           N must be a multiple of the tile width).
- * gemm_tn:  out[t][m][n] = sum_k A[t][k][m] B[t][k][n] (A planes [Kd][M/8][3][8], B [Kd][N/8][3][8]),
- *           the k range cut into <= splits slabs (slab float[merlin_x6_tn_slab_floats(...)]) summed in
- *           slab order; cfg 0: 128x64, 1: 128x192, 2: 128x192 (4x2 waves), 3: 64x192. */
+ * gemm_nt:  C[t][m][n] = sum_k A[t][m][k] B[t][n][k], A fp32 [M][K], B planes [N][K] (K % 32 == 0;
+ *           tower strides in values), + bias[t][n] and ReLU when bias != NULL; cfg selects the tile
+ *           (0: 256x128, 1: 128x192, 2: 128x128, 3: 256x64; N a multiple of the tile width).
+ * gemm_tn:  out[t][m][n] = sum_k A[t][k][m] B[t][k][n], A fp32 [Kd][M], B fp32 [Kd][N] (M, N multiples
+ *           of the tile: cfg 0 / 2: 128x192, 1: 128x64), the k range cut into <= splits slabs
+ *           (slab float[merlin_x6_tn_slab_floats(...)]) summed in slab order. */
 int merlin_x6_split(const float *x_dev, int64_t n, void *planes_dev, void *stream);
-/* The producers of fc1's update operands write them straight in x6 planes (no fp32 copy):
- * merlin_tower_window_conv3_bits with planes_dev bf16-planes[towers][n][576 * 3] instead of Y3, and
- * merlin_tower_head_bwd with dz_planes_dev [2][n][hidden * 3] instead of dz (hidden % 8 == 0). */
-int merlin_tower_window_conv3_x6(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
-                                 const int64_t *groups_dev, int64_t n, const float *b3_dev, int32_t towers,
-                                 void *planes_dev, uint64_t *relu_bits_dev, void *stream);
-int merlin_tower_head_bwd_x6(const float *h_dev, const float *dlogits_dev, const float *dvalue_dev,
-                             const float *w_actor_dev, const float *w_critic_dev, int64_t n, int32_t hidden,
-                             int32_t act_dim, void *dz_planes_dev, float *dbias_dev, float *dw_actor_dev,
-                             float *dw_critic_dev, void *stream);
 int merlin_x6_join(const void *planes_dev, int64_t n, float *x_dev, void *stream);
-int merlin_x6_gemm_nt(const void *A_dev, const void *B_dev, int64_t M, int32_t N, int32_t K, int32_t towers,
+int merlin_x6_gemm_nt(const float *A_dev, const void *B_dev, int64_t M, int32_t N, int32_t K, int32_t towers,
                       int64_t a_stride, int64_t b_stride, const float *bias_dev, float *C_dev, int64_t c_stride,
                       int32_t cfg, void *stream);
 int64_t merlin_x6_tn_slab_floats(int32_t M, int32_t N, int32_t towers, int32_t splits);
-int merlin_x6_gemm_tn(const void *A_dev, const void *B_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
+int merlin_x6_gemm_tn(const float *A_dev, const float *B_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
                       int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev, float *out_dev, int32_t cfg,
                       void *stream);
 

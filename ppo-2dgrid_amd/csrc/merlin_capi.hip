@@ -614,7 +614,7 @@ int merlin_tower_window_conv3(const float *Q, int64_t nw, const int32_t *wid, co
                               const float *b3, int32_t towers, float *Y3, void *stream) {
     if ((!Q || !wid || !b3 || !Y3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, nullptr, nullptr, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, nullptr, (hipStream_t)stream));
     return MERLIN_OK;
 }
 
@@ -622,16 +622,7 @@ int merlin_tower_window_conv3_bits(const float *Q, int64_t nw, const int32_t *wi
                                    const float *b3, int32_t towers, float *Y3, uint64_t *relu_bits, void *stream) {
     if ((!Q || !wid || !b3 || !Y3 || !relu_bits) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, nullptr, (hipStream_t)stream));
-    return MERLIN_OK;
-}
-
-int merlin_tower_window_conv3_x6(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                                 const float *b3, int32_t towers, void *planes, uint64_t *relu_bits, void *stream) {
-    if ((!Q || !wid || !b3 || !planes || !relu_bits) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
-    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, nullptr, relu_bits, planes,
-                                        (hipStream_t)stream));
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, (hipStream_t)stream));
     return MERLIN_OK;
 }
 
@@ -739,25 +730,8 @@ int merlin_tower_head_bwd(const float *h, const float *dlogits, const float *dva
     DeviceWs *ws = nullptr;
     int rc = device_ws(&ws);
     if (rc) return rc;
-    HIP_TRY(merlin::launch_head_bwd(h, dlogits, dvalue, w_actor, w_critic, n, hidden, act_dim, dz, nullptr, dbias,
-                                    dw_actor, dw_critic, ws->epi_work, (hipStream_t)stream));
-    return MERLIN_OK;
-}
-
-int merlin_tower_head_bwd_x6(const float *h, const float *dlogits, const float *dvalue, const float *w_actor,
-                             const float *w_critic, int64_t n, int32_t hidden, int32_t act_dim, void *dz_planes,
-                             float *dbias, float *dw_actor, float *dw_critic, void *stream) {
-    if (!dbias || !dw_actor || !dw_critic ||
-        ((!h || !dlogits || !dvalue || !w_actor || !w_critic || !dz_planes) && n > 0))
-        return fail(MERLIN_E_INVALID, "null argument");
-    if (act_dim < 1 || act_dim > merlin::epilogue_max_act()) return fail(MERLIN_E_UNSUPPORTED, "act_dim must be 1..8");
-    if (!merlin::epilogue_cols_ok(hidden) || hidden % 8)
-        return fail(MERLIN_E_UNSUPPORTED, "hidden must be a multiple of 8 dividing 1024");
-    DeviceWs *ws = nullptr;
-    int rc = device_ws(&ws);
-    if (rc) return rc;
-    HIP_TRY(merlin::launch_head_bwd(h, dlogits, dvalue, w_actor, w_critic, n, hidden, act_dim, nullptr, dz_planes,
-                                    dbias, dw_actor, dw_critic, ws->epi_work, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_head_bwd(h, dlogits, dvalue, w_actor, w_critic, n, hidden, act_dim, dz, dbias, dw_actor,
+                                    dw_critic, ws->epi_work, (hipStream_t)stream));
     return MERLIN_OK;
 }
 
@@ -775,13 +749,13 @@ int merlin_x6_join(const void *planes, int64_t n, float *x, void *stream) {
     return MERLIN_OK;
 }
 
-int merlin_x6_gemm_nt(const void *A, const void *B, int64_t M, int32_t N, int32_t K, int32_t towers, int64_t a_stride,
+int merlin_x6_gemm_nt(const float *A, const void *B, int64_t M, int32_t N, int32_t K, int32_t towers, int64_t a_stride,
                       int64_t b_stride, const float *bias, float *C, int64_t c_stride, int32_t cfg, void *stream) {
     if (M < 0 || N <= 0 || K <= 0) return fail(MERLIN_E_INVALID, "bad shape");
     if (M > 0 && (!A || !B || !C)) return fail(MERLIN_E_INVALID, "null argument");
     if (K % 32) return fail(MERLIN_E_UNSUPPORTED, "K must be a multiple of 32");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    if (a_stride % 8 || b_stride % 8) return fail(MERLIN_E_INVALID, "tower strides must be multiples of 8");
+    if (a_stride % 4 || b_stride % 8) return fail(MERLIN_E_INVALID, "tower strides: A multiple of 4, B of 8");
     const hipError_t e = merlin::launch_x6_gemm_nt(A, B, M, N, K, towers, a_stride, b_stride, bias, C, c_stride, cfg,
                                                    (hipStream_t)stream);
     if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "N not a multiple of the tile width / bad cfg");
@@ -793,13 +767,13 @@ int64_t merlin_x6_tn_slab_floats(int32_t M, int32_t N, int32_t towers, int32_t s
     return (int64_t)std::max(1, splits) * towers * M * N;
 }
 
-int merlin_x6_gemm_tn(const void *A, const void *B, int64_t Kd, int32_t M, int32_t N, int32_t towers, int64_t a_stride,
+int merlin_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int32_t M, int32_t N, int32_t towers, int64_t a_stride,
                       int64_t b_stride, int32_t splits, float *slab, float *out, int32_t cfg, void *stream) {
     if (Kd < 0 || M <= 0 || N <= 0) return fail(MERLIN_E_INVALID, "bad shape");
     if (!out || (Kd > 0 && (!A || !B || !slab))) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (splits < 1 || splits > merlin::x6_tn_max_splits()) return fail(MERLIN_E_INVALID, "splits out of range");
-    if (M % 8 || N % 8 || a_stride % 8 || b_stride % 8) return fail(MERLIN_E_INVALID, "M, N, strides: multiples of 8");
+    if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return fail(MERLIN_E_INVALID, "M, N: multiples of 8");
     const hipError_t e = merlin::launch_x6_gemm_tn(A, B, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, cfg,
                                                    (hipStream_t)stream);
     if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "M / N not multiples of the tile / bad cfg");

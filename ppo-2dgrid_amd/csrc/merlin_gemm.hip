@@ -14,20 +14,21 @@
 // at 16/6 of the f32 MFMA rate (tests/test_gpu_gemm.py measures the error against float64 beside
 // hipBLASLt's fp32 GEMM on the same operands).
 //
-// Plane layout ("x6 planes") of a logical fp32 matrix X[R][C], C % 8 == 0: bf16 [R][C/8][3][8],
-// i.e. per row and per group of 8 columns three 16-B chunks (planes 0, 1, 2).  The producers
-// write it directly (k_window_conv3: fc1's input rows; k_head_bwd: fc1's output gradient), so no
-// fp32 copy of either operand exists on the update path.
+// The activations (fc1's input rows a3 and output gradient dz, the big operands) are read as fp32
+// and split in registers while they are staged into LDS (4 bytes per value from HBM / L2 instead of
+// the planes' 6); the weights, small and re-read by every tile, are split once per call into
+// "x6 planes" (merlin_x6.h: bf16 [R][C/8][3][8]).  LDS holds every operand as three plane images.
 //
-//   k_x6_nt  C[t][m][n] = epi(sum_k A[t][m][k] B[t][n][k]) (both operands K-contiguous: forward
-//            with B = W4, input gradient with B = W4^T); block tile BM x BN, K steps of 32, the
-//            next step's chunks prefetched into registers while the current one is multiplied
-//            from LDS; LDS rows of 64 B with the 16-B chunk index XORed by (row >> 2) & 3 so each
-//            16-lane ds_read_b128 group hits 16 distinct bank slots.
-//   k_x6_tn  slab[s][t][m][n] = sum_{k in split s} A[t][k][m] B[t][k][n] (weight gradient: both
-//            operands row-major over the long reduction dimension k = the minibatch's frames);
-//            LDS images [k][m] read with ds_read_b64_tr_b16 (the hardware transposed read) so the
-//            MFMA fragments come out k-contiguous; k_x6_fold sums the slabs in split order.
+//   k_x6_nt  C[t][m][n] = epi(sum_k A[t][m][k] B[t][n][k]), A fp32 [M][K], B planes [N][K]
+//            (forward with B = W4, input gradient with B = W4^T); block tile BM x BN, k steps of
+//            32, two LDS stages (one barrier per step), the step after next in flight in
+//            registers; plane images with rows of 64 B, the 16-B chunk index XORed by
+//            (row >> 2) & 3, so the ds_read_b128 fragment reads and the staging writes are free of
+//            bank conflicts.
+//   k_x6_tn  slab[s][t][m][n] = sum_{k in split s} A[t][k][m] B[t][k][n], A and B fp32 row-major
+//            over the long reduction dimension k = the minibatch's frames (weight gradient dz^T
+//            a3); plane images [k][m] read with ds_read_b64_tr_b16 (the hardware transposed read)
+//            so the MFMA fragments come out k-contiguous; k_x6_fold sums the slabs in split order.
 #include <algorithm>
 
 #include "merlin_internal.h"
@@ -95,25 +96,33 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// 8 fp32 values -> their three planes as 16-B fragments chunks
+__device__ __forceinline__ void split8(const float4 a, const float4 b, u32x4 &p0, u32x4 &p1, u32x4 &p2) {
+    uint2 x[3], y[3];
+    x6_split4(a, x);
+    x6_split4(b, y);
+    p0 = u32x4{x[0].x, x[0].y, y[0].x, y[0].y};
+    p1 = u32x4{x[1].x, x[1].y, y[1].x, y[1].y};
+    p2 = u32x4{x[2].x, x[2].y, y[2].x, y[2].y};
+}
+
 // ---------------------------------------------------------------------------------------------
-// NT: C[t][m][n] = epi(sum_k A[t][m][k] B[t][n][k]); A, B in x6 planes (K % 32 == 0, N % BN == 0);
-// EPI 1: relu(. + bias[t][n]).  grid (tiles_m * tiles_n, T).
+// NT: C[t][m][n] = epi(sum_k A[t][m][k] B[t][n][k]); A fp32 [M][K], B x6 planes [N][K/8][3][8]
+// (K % 32 == 0, N % BN == 0); EPI 1: relu(. + bias[t][n]).  grid (tiles_m * tiles_n, T).
 template <int BM, int BN, int WGM, int WGN, int EPI>
-__global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restrict__ A, const u32x4 *__restrict__ B,
+__global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const float4 *__restrict__ A, const u32x4 *__restrict__ B,
                                                           int64_t M, int N, int K, int64_t sA, int64_t sB,
                                                           const float *__restrict__ bias, float *__restrict__ C,
                                                           int64_t sC, int tiles_n) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int FM = WTM / 16, FN = WTN / 16;
-    constexpr int CA = (BM * CPR + NT - 1) / NT, CB = (BN * CPR + NT - 1) / NT;
+    constexpr int UA = (BM * 4 + NT - 1) / NT;        // A units (row, group of 8 values) per thread
+    constexpr int CB = (BN * CPR + NT - 1) / NT;      // B 16-B plane chunks per thread
     static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
-    // two LDS stages: step kt+1 is written into the other stage while step kt is multiplied, one
-    // barrier per step; the registers hold step kt+2 in flight (issued a whole step before use)
-    // plane p of the A / B image at p * PSA / 3 * PSA + p * PSB chunks: the 12-chunk pad per plane
-    // (plus the chunk order of the staging loads, planes major within a row) makes every 16-lane
-    // group of the staging writes, and of the fragment reads, hit 16 distinct bank slots
-    constexpr int PSA = BM * 4 + 12, PSB = BN * 4 + 12;
+    // plane p of the A image at p * PSA chunks, of the B image at 3 * PSA + p * PSB; the B pad and
+    // chunk order (planes major within a row) keep its staging writes conflict-free as well
+    constexpr int PSA = BM * 4, PSB = BN * 4 + 12;
     constexpr int STAGE = 3 * (PSA + PSB);
     __shared__ u32x4 lds[2 * STAGE];
 
@@ -122,21 +131,21 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restric
     const int tm = L / tiles_n, tn = L - tm * tiles_n;
     const int64_t m0 = (int64_t)tm * BM;
     const int n0 = tn * BN;
-    const int64_t rowA = (int64_t)(K / 8) * 3;  // chunks per row
+    const int64_t rowA = K / 4;                 // float4 per A row
+    const int64_t rowB = (int64_t)(K / 8) * 3;  // chunks per B row
     A += t * sA;
     B += t * sB;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w / WGN, wn = w - (w / WGN) * WGN;
 
-    const u32x4 *ga[CA];
-    int la[CA];
+    const float4 *ga[UA];
+    int la[UA];
 #pragma unroll
-    for (int i = 0; i < CA; i++) {
+    for (int i = 0; i < UA; i++) {
         const int q = tid + i * NT;
-        const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
-        const int64_t grow = std::min<int64_t>(m0 + std::min(row, BM - 1), M - 1);
-        ga[i] = A + grow * rowA + g * 3 + p;
-        la[i] = p * PSA + row * 4 + (g ^ ((row >> 2) & 3));
+        const int row = std::min(q >> 2, BM - 1), g = q & 3;
+        ga[i] = A + std::min<int64_t>(m0 + row, M - 1) * rowA + g * 2;
+        la[i] = row * 4 + (g ^ ((row >> 2) & 3));
     }
     const u32x4 *gb[CB];
     int lb[CB];
@@ -144,21 +153,31 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restric
     for (int i = 0; i < CB; i++) {
         const int q = tid + i * NT;
         const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
-        gb[i] = B + (int64_t)(n0 + std::min(row, BN - 1)) * rowA + g * 3 + p;
+        gb[i] = B + (int64_t)(n0 + std::min(row, BN - 1)) * rowB + g * 3 + p;
         lb[i] = 3 * PSA + p * PSB + row * 4 + (g ^ ((row >> 2) & 3));
     }
-    u32x4 ra[CA], rb[CB];
+    float4 ra[UA][2];
+    u32x4 rb[CB];
     auto load = [&](int kt) {
 #pragma unroll
-        for (int i = 0; i < CA; i++) ra[i] = ga[i][(int64_t)kt * CPR];
+        for (int i = 0; i < UA; i++) {
+            ra[i][0] = ga[i][(int64_t)kt * 8];
+            ra[i][1] = ga[i][(int64_t)kt * 8 + 1];
+        }
 #pragma unroll
         for (int i = 0; i < CB; i++) rb[i] = gb[i][(int64_t)kt * CPR];
     };
     auto store = [&](int buf) {
         u32x4 *st = lds + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < CA; i++)
-            if ((BM * CPR) % NT == 0 || i + 1 < CA || tid + i * NT < BM * CPR) st[la[i]] = ra[i];
+        for (int i = 0; i < UA; i++)
+            if ((BM * 4) % NT == 0 || i + 1 < UA || tid + i * NT < BM * 4) {
+                u32x4 p0, p1, p2;
+                split8(ra[i][0], ra[i][1], p0, p1, p2);
+                st[la[i]] = p0;
+                st[PSA + la[i]] = p1;
+                st[2 * PSA + la[i]] = p2;
+            }
 #pragma unroll
         for (int i = 0; i < CB; i++)
             if ((BN * CPR) % NT == 0 || i + 1 < CB || tid + i * NT < BN * CPR) st[lb[i]] = rb[i];
@@ -234,165 +253,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const u32x4 *__restric
 }
 
 // ---------------------------------------------------------------------------------------------
-// The same product as a persistent kernel: one block per CU walks its tiles (tile j*G + base, tiles
-// numbered (t, tm, tn) with tn fastest; base puts G/8 consecutive tiles on each XCD per round, so
-// the BN-column tiles of one A panel run together on one L2) as one flat stream of k steps: the
-// loads of the next tile's first steps are in flight while the current tile finishes, and the
-// epilogue's stores overlap the next tile's multiplies.  G % 8 == 0.
-template <int BM, int BN, int WGM, int WGN, int EPI>
-__global__ __launch_bounds__(64 * WGM * WGN) void k_x6_ntp(const u32x4 *__restrict__ A, const u32x4 *__restrict__ B,
-                                                           int64_t M, int N, int K, int64_t sA, int64_t sB,
-                                                           const float *__restrict__ bias, float *__restrict__ C,
-                                                           int64_t sC, int tiles_m, int tiles_n, int T) {
-    constexpr int NT = 64 * WGM * WGN;
-    constexpr int WTM = BM / WGM, WTN = BN / WGN;
-    constexpr int FM = WTM / 16, FN = WTN / 16;
-    constexpr int CA = (BM * CPR + NT - 1) / NT, CB = (BN * CPR + NT - 1) / NT;
-    static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
-    constexpr int PSA = BM * 4 + 12, PSB = BN * 4 + 12;
-    constexpr int STAGE = 3 * (PSA + PSB);
-    __shared__ u32x4 lds[2 * STAGE];
-
-    const int G = gridDim.x, b = blockIdx.x;
-    const int base = (b & 7) * (G >> 3) + (b >> 3);
-    const int per_t = tiles_m * tiles_n, total = T * per_t;
-    const int nk = K / BK;
-    const int ntl = base < total ? (total - base + G - 1) / G : 0;
-    const int steps = ntl * nk;
-    if (steps == 0) return;
-    const int64_t rowA = (int64_t)(K / 8) * 3;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
-
-    int rA[CA], oA[CA], la[CA];
-#pragma unroll
-    for (int i = 0; i < CA; i++) {
-        const int q = tid + i * NT;
-        const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
-        rA[i] = std::min(row, BM - 1);
-        oA[i] = g * 3 + p;
-        la[i] = p * PSA + row * 4 + (g ^ ((row >> 2) & 3));
-    }
-    int oB[CB], lb[CB];
-#pragma unroll
-    for (int i = 0; i < CB; i++) {
-        const int q = tid + i * NT;
-        const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
-        oB[i] = std::min(row, BN - 1) * (int)rowA + g * 3 + p;
-        lb[i] = 3 * PSA + p * PSB + row * 4 + (g ^ ((row >> 2) & 3));
-    }
-    auto tile_of = [&](int j, int &t, int &tm, int &tn) {
-        const int id = j * G + base;
-        t = id / per_t;
-        const int r = id - t * per_t;
-        tm = r / tiles_n;
-        tn = r - tm * tiles_n;
-    };
-    u32x4 ra[CA], rb[CB];
-    auto load = [&](int s) {
-        const int j = s / nk, kt = s - j * nk;
-        int t, tm, tn;
-        tile_of(j, t, tm, tn);
-        const u32x4 *Ab = A + t * sA + kt * CPR;
-        const u32x4 *Bb = B + t * sB + (int64_t)tn * BN * rowA + kt * CPR;
-        const int64_t m0 = (int64_t)tm * BM;
-#pragma unroll
-        for (int i = 0; i < CA; i++) ra[i] = Ab[std::min<int64_t>(m0 + rA[i], M - 1) * rowA + oA[i]];
-#pragma unroll
-        for (int i = 0; i < CB; i++) rb[i] = Bb[oB[i]];
-    };
-    auto store = [&](int buf) {
-        u32x4 *st = lds + buf * STAGE;
-#pragma unroll
-        for (int i = 0; i < CA; i++)
-            if ((BM * CPR) % NT == 0 || i + 1 < CA || tid + i * NT < BM * CPR) st[la[i]] = ra[i];
-#pragma unroll
-        for (int i = 0; i < CB; i++)
-            if ((BN * CPR) % NT == 0 || i + 1 < CB || tid + i * NT < BN * CPR) st[lb[i]] = rb[i];
-    };
-
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; i++)
-#pragma unroll
-        for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-
-    const int fr = lane & 15, fc = (lane >> 4) ^ ((lane & 15) >> 2);
-    load(0);
-    store(0);
-    if (steps > 1) load(1);
-    __syncthreads();
-    int kt = 0, jt = 0;
-    for (int s = 0; s < steps; s++) {
-        const int buf = s & 1;
-        if (s + 1 < steps) store(buf ^ 1);
-        if (s + 2 < steps) load(s + 2);
-        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * PSA;
-        if constexpr (FM <= FN) {
-            u32x4 af[FM][3];
-#pragma unroll
-            for (int i = 0; i < FM; i++)
-#pragma unroll
-                for (int p = 0; p < 3; p++) af[i][p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
-#pragma unroll
-            for (int j = 0; j < FN; j++) {
-                u32x4 bf[3];
-#pragma unroll
-                for (int p = 0; p < 3; p++) bf[p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
-#pragma unroll
-                for (int i = 0; i < FM; i++) acc[i][j] = mma6(af[i], bf, acc[i][j]);
-            }
-        } else {
-            u32x4 bf[FN][3];
-#pragma unroll
-            for (int j = 0; j < FN; j++)
-#pragma unroll
-                for (int p = 0; p < 3; p++) bf[j][p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
-#pragma unroll
-            for (int i = 0; i < FM; i++) {
-                u32x4 af[3];
-#pragma unroll
-                for (int p = 0; p < 3; p++) af[p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
-#pragma unroll
-                for (int j = 0; j < FN; j++) acc[i][j] = mma6(af, bf[j], acc[i][j]);
-            }
-        }
-        if (++kt == nk) {  // tile done: epilogue, fresh accumulators
-            int t, tm, tn;
-            tile_of(jt, t, tm, tn);
-            float *Ct = C + t * sC;
-            const int64_t m0 = (int64_t)tm * BM;
-#pragma unroll
-            for (int j = 0; j < FN; j++) {
-                const int col = tn * BN + wn * WTN + j * 16 + fr;
-                const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
-#pragma unroll
-                for (int i = 0; i < FM; i++) {
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const int64_t row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + r;
-                        if (row < M) {
-                            const float v = acc[i][j][r];
-                            Ct[row * N + col] = EPI == 1 ? relu_nan(v + bv) : v;
-                        }
-                    }
-                    acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-                }
-            }
-            kt = 0;
-            jt++;
-        }
-        __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// TN: slab[s][t][m][n] = sum_{k in [s*kc, min(Kd, (s+1)*kc))} A[t][k][m] B[t][k][n]; A = x6 planes
-// [Kd][M/8][3][8], B = [Kd][N/8][3][8]; M % BM == 0, N % BN == 0, kc % 32 == 0.
-// grid (tiles_m * tiles_n, splits, T).
-// LDS image of one plane: [32 k rows][BM / 8 chunks], chunk index XOR sw(row) so that a 32-lane
-// half of a transposed read (rows r..r+3 and r+8..r+11, two adjacent chunks each) hits 16
-// distinct 16-B bank slots (rows of 16k chunks or of 16k + 8 chunks).
+// TN: slab[s][t][m][n] = sum_{k in [s*kc, min(Kd, (s+1)*kc))} A[t][k][m] B[t][k][n]; A fp32 [Kd][M],
+// B fp32 [Kd][N]; M % BM == 0, N % BN == 0, kc % 32 == 0.  grid (tiles_m * tiles_n, splits, T).
+// Plane image: [32 k rows][BM / 8 chunks], chunk index XOR tr_swz(row) so that a 32-lane half of
+// a transposed read (rows r..r+3 and r+8..r+11, two adjacent chunks each) hits 16 distinct 16-B
+// bank slots (rows of 16k chunks or of 16k + 8 chunks).
 template <int RC>
 __device__ __forceinline__ int tr_swz(int row) {
     static_assert(RC % 8 == 0, "row chunks");
@@ -418,20 +283,17 @@ __device__ __forceinline__ bf16x8 tr_frag(const u32x4 *img, int col0, int lane) 
 }
 
 template <int BM, int BN, int WGM, int WGN>
-__global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const u32x4 *__restrict__ A, const u32x4 *__restrict__ B,
+__global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restrict__ A, const float4 *__restrict__ B,
                                                           int64_t Kd, int M, int N, int64_t sA, int64_t sB, int64_t kc,
                                                           int tiles_n, float *__restrict__ slab) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int FM = WTM / 16, FN = WTN / 16;
-    constexpr int RCA = BM / 8, RCB = BN / 8;                 // chunks per LDS row (one plane)
-    constexpr int QA = BK * RCA * 3, QB = BK * RCB * 3;       // chunks per k step
-    constexpr int CA = (QA + NT - 1) / NT, CB = (QB + NT - 1) / NT;
+    constexpr int RCA = BM / 8, RCB = BN / 8;            // chunks (groups of 8 values) per image row
+    constexpr int QA = BK * RCA, QB = BK * RCB;          // units per k step
+    constexpr int UA = (QA + NT - 1) / NT, UB = (QB + NT - 1) / NT;
     static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
-    // two LDS stages, one barrier per step (as k_x6_nt)
-    // plane images of BK * RC chunks, padded to keep the staging writes conflict-free (rows of 16k + 8
-    // chunks), planes major in the staging order
-    constexpr int PSA = BK * RCA + (RCA % 16 ? 8 : 0), PSB = BK * RCB + (RCB % 16 ? 8 : 0);
+    constexpr int PSA = BK * RCA, PSB = BK * RCB;
     constexpr int STAGE = 3 * (PSA + PSB);
     __shared__ u32x4 lds[2 * STAGE];
 
@@ -440,56 +302,70 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const u32x4 *__restric
     const int tm = L / tiles_n, tn = L - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int64_t k0 = (int64_t)s * kc, k1 = std::min<int64_t>(Kd, k0 + kc);
-    const int64_t rowA = (int64_t)(M / 8) * 3, rowB = (int64_t)(N / 8) * 3;
-    A += t * sA + (m0 / 8) * 3;
-    B += t * sB + (n0 / 8) * 3;
+    const int64_t rowA = M / 4, rowB = N / 4;  // float4 per row
+    A += t * sA + m0 / 4;
+    B += t * sB + n0 / 4;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w / WGN, wn = w - (w / WGN) * WGN;
 
-    int ka[CA], oa[CA], la[CA];
+    int ka[UA], oa[UA], la[UA];
 #pragma unroll
-    for (int i = 0; i < CA; i++) {
-        const int q = tid + i * NT;
-        const int k = std::min(q, QA - 1) / (RCA * 3), rem = std::min(q, QA - 1) - k * (RCA * 3);
-        const int p = rem / RCA, g = rem - (rem / RCA) * RCA;
+    for (int i = 0; i < UA; i++) {
+        const int q = std::min(tid + i * NT, QA - 1);
+        const int k = q / RCA, g = q - (q / RCA) * RCA;
         ka[i] = k;
-        oa[i] = g * 3 + p;
-        la[i] = p * PSA + k * RCA + (g ^ tr_swz<RCA>(k));
+        oa[i] = g * 2;
+        la[i] = k * RCA + (g ^ tr_swz<RCA>(k));
     }
-    int kb[CB], ob[CB], lb[CB];
+    int kb[UB], ob[UB], lb[UB];
 #pragma unroll
-    for (int i = 0; i < CB; i++) {
-        const int q = tid + i * NT;
-        const int k = std::min(q, QB - 1) / (RCB * 3), rem = std::min(q, QB - 1) - k * (RCB * 3);
-        const int p = rem / RCB, g = rem - (rem / RCB) * RCB;
+    for (int i = 0; i < UB; i++) {
+        const int q = std::min(tid + i * NT, QB - 1);
+        const int k = q / RCB, g = q - (q / RCB) * RCB;
         kb[i] = k;
-        ob[i] = g * 3 + p;
-        lb[i] = 3 * PSA + p * PSB + k * RCB + (g ^ tr_swz<RCB>(k));
+        ob[i] = g * 2;
+        lb[i] = 3 * PSA + k * RCB + (g ^ tr_swz<RCB>(k));
     }
-    const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
-    u32x4 ra[CA], rb[CB];
+    const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float4 ra[UA][2], rb[UB][2];
     auto load = [&](int64_t kk) {
 #pragma unroll
-        for (int i = 0; i < CA; i++) {
+        for (int i = 0; i < UA; i++) {
             const int64_t k = kk + ka[i];
-            const u32x4 v = A[std::min(k, k1 - 1) * rowA + oa[i]];
-            ra[i] = k < k1 ? v : zero;
+            const float4 *src = A + std::min(k, k1 - 1) * rowA + oa[i];
+            const float4 x = src[0], y = src[1];
+            ra[i][0] = k < k1 ? x : zero;
+            ra[i][1] = k < k1 ? y : zero;
         }
 #pragma unroll
-        for (int i = 0; i < CB; i++) {
+        for (int i = 0; i < UB; i++) {
             const int64_t k = kk + kb[i];
-            const u32x4 v = B[std::min(k, k1 - 1) * rowB + ob[i]];
-            rb[i] = k < k1 ? v : zero;
+            const float4 *src = B + std::min(k, k1 - 1) * rowB + ob[i];
+            const float4 x = src[0], y = src[1];
+            rb[i][0] = k < k1 ? x : zero;
+            rb[i][1] = k < k1 ? y : zero;
         }
     };
     auto store = [&](int buf) {
         u32x4 *st = lds + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < CA; i++)
-            if (QA % NT == 0 || i + 1 < CA || tid + i * NT < QA) st[la[i]] = ra[i];
+        for (int i = 0; i < UA; i++)
+            if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
+                u32x4 p0, p1, p2;
+                split8(ra[i][0], ra[i][1], p0, p1, p2);
+                st[la[i]] = p0;
+                st[PSA + la[i]] = p1;
+                st[2 * PSA + la[i]] = p2;
+            }
 #pragma unroll
-        for (int i = 0; i < CB; i++)
-            if (QB % NT == 0 || i + 1 < CB || tid + i * NT < QB) st[lb[i]] = rb[i];
+        for (int i = 0; i < UB; i++)
+            if (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB) {
+                u32x4 p0, p1, p2;
+                split8(rb[i][0], rb[i][1], p0, p1, p2);
+                st[lb[i]] = p0;
+                st[PSB + lb[i]] = p1;
+                st[2 * PSB + lb[i]] = p2;
+            }
     };
 
     f32x4 acc[FM][FN];
@@ -570,10 +446,8 @@ __global__ __launch_bounds__(256) void k_x6_fold(const float4 *__restrict__ slab
     }
 }
 
-// NT tile configurations (cfg): 0 = 128 x 128, 4 waves (forward, N = 512); 1 = 128 x 64, 4 waves
-// (input gradient, N = 576); 2 = 256 x 128, 8 waves; 3 = 128 x 192, 8 waves; 4 = 128 x 96, 4 waves
 template <int BM, int BN, int WGM, int WGN>
-hipError_t nt_launch(const u32x4 *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
+hipError_t nt_launch(const float4 *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
                      const float *bias, float *C, int64_t sC, hipStream_t s) {
     if (N % BN) return hipErrorInvalidValue;
     const int64_t tiles_m = (M + BM - 1) / BM;
@@ -589,39 +463,8 @@ hipError_t nt_launch(const u32x4 *A, const u32x4 *B, int64_t M, int N, int K, in
     return hipGetLastError();
 }
 
-int num_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-            n = v;
-        else
-            n = 256;
-    }
-    return n;
-}
-
 template <int BM, int BN, int WGM, int WGN>
-hipError_t ntp_launch(const u32x4 *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
-                      const float *bias, float *C, int64_t sC, hipStream_t s) {
-    if (N % BN) return hipErrorInvalidValue;
-    const int64_t tiles_m = (M + BM - 1) / BM;
-    const int tiles_n = N / BN;
-    const int64_t total = tiles_m * tiles_n * T;
-    if (total > INT32_MAX / 2) return hipErrorInvalidValue;
-    const int G = (int)std::min<int64_t>((total + 7) / 8 * 8, num_cus() / 8 * 8);
-    if (bias)
-        hipLaunchKernelGGL((k_x6_ntp<BM, BN, WGM, WGN, 1>), dim3(G), dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB,
-                           bias, C, sC, (int)tiles_m, tiles_n, T);
-    else
-        hipLaunchKernelGGL((k_x6_ntp<BM, BN, WGM, WGN, 0>), dim3(G), dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB,
-                           nullptr, C, sC, (int)tiles_m, tiles_n, T);
-    return hipGetLastError();
-}
-
-template <int BM, int BN, int WGM, int WGN>
-hipError_t tn_launch(const u32x4 *A, const u32x4 *B, int64_t Kd, int M, int N, int T, int64_t sA, int64_t sB,
+hipError_t tn_launch(const float4 *A, const float4 *B, int64_t Kd, int M, int N, int T, int64_t sA, int64_t sB,
                      int splits, float *slab, float *out, hipStream_t s) {
     if (M % BM || N % BN) return hipErrorInvalidValue;
     const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
@@ -662,43 +505,37 @@ hipError_t launch_x6_join(const void *planes, int64_t n, float *x, hipStream_t s
     return hipGetLastError();
 }
 
-hipError_t launch_x6_gemm_nt(const void *A, const void *B, int64_t M, int N, int K, int T, int64_t a_stride,
+hipError_t launch_x6_gemm_nt(const float *A, const void *B, int64_t M, int N, int K, int T, int64_t a_stride,
                              int64_t b_stride, const float *bias, float *C, int64_t c_stride, int cfg, hipStream_t s) {
     if (M <= 0) return hipSuccess;
     if (K % BK || N <= 0) return hipErrorInvalidValue;
-    // strides are in elements; chunks of 8 bf16 x 3 planes = 8 logical elements per 3 chunks
-    if (a_stride % 8 || b_stride % 8) return hipErrorInvalidValue;
-    const u32x4 *a = static_cast<const u32x4 *>(A), *b = static_cast<const u32x4 *>(B);
-    const int64_t sA = a_stride / 8 * 3, sB = b_stride / 8 * 3;
+    // strides in values; B's planes: 3 chunks per 8 values
+    if (a_stride % 4 || b_stride % 8) return hipErrorInvalidValue;
+    const float4 *a = reinterpret_cast<const float4 *>(A);
+    const u32x4 *b = static_cast<const u32x4 *>(B);
+    const int64_t sA = a_stride / 4, sB = b_stride / 8 * 3;
     switch (cfg) {
-        case 0: return nt_launch<128, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 1: return nt_launch<128, 64, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 2: return nt_launch<256, 128, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 3: return nt_launch<128, 192, 2, 4>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 4: return nt_launch<128, 96, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 5: return nt_launch<256, 64, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 6: return ntp_launch<256, 128, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 7: return ntp_launch<128, 192, 2, 4>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 8: return ntp_launch<256, 64, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
-        case 9: return ntp_launch<128, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 0: return nt_launch<256, 128, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 1: return nt_launch<128, 192, 2, 4>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 2: return nt_launch<128, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 3: return nt_launch<256, 64, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 int x6_tn_max_splits() { return 64; }
 
-hipError_t launch_x6_gemm_tn(const void *A, const void *B, int64_t Kd, int M, int N, int T, int64_t a_stride,
+hipError_t launch_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int M, int N, int T, int64_t a_stride,
                              int64_t b_stride, int splits, float *slab, float *out, int cfg, hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    if (M % 8 || N % 8 || a_stride % 8 || b_stride % 8) return hipErrorInvalidValue;
+    if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
     if (Kd <= 0) return hipMemsetAsync(out, 0, sizeof(float) * (size_t)T * M * N, s);
-    const u32x4 *a = static_cast<const u32x4 *>(A), *b = static_cast<const u32x4 *>(B);
-    const int64_t sA = a_stride / 8 * 3, sB = b_stride / 8 * 3;
+    const float4 *a = reinterpret_cast<const float4 *>(A), *b = reinterpret_cast<const float4 *>(B);
+    const int64_t sA = a_stride / 4, sB = b_stride / 4;
     switch (cfg) {
-        case 0: return tn_launch<128, 64, 2, 2>(a, b, Kd, M, N, T, sA, sB, splits, slab, out, s);
-        case 1: return tn_launch<128, 192, 2, 4>(a, b, Kd, M, N, T, sA, sB, splits, slab, out, s);
+        case 0: return tn_launch<128, 192, 2, 4>(a, b, Kd, M, N, T, sA, sB, splits, slab, out, s);
+        case 1: return tn_launch<128, 64, 2, 2>(a, b, Kd, M, N, T, sA, sB, splits, slab, out, s);
         case 2: return tn_launch<128, 192, 4, 2>(a, b, Kd, M, N, T, sA, sB, splits, slab, out, s);
-        case 3: return tn_launch<64, 192, 2, 2>(a, b, Kd, M, N, T, sA, sB, splits, slab, out, s);
         default: return hipErrorInvalidValue;
     }
 }

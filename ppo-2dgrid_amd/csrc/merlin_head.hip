@@ -13,7 +13,6 @@
 #include <algorithm>
 
 #include "merlin_internal.h"
-#include "merlin_x6.h"
 
 namespace merlin {
 namespace {
@@ -123,7 +122,7 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
                                                    const float *__restrict__ dvalue, const float4 *__restrict__ wa,
                                                    const float4 *__restrict__ wc, int64_t n, int H4, int A,
                                                    int64_t per, float4 *__restrict__ dz,
-                                                   uint2 *__restrict__ dzp, float4 *__restrict__ partials) {
+                                                   float4 *__restrict__ partials) {
     __shared__ float4 red[EBLK];
     const int t = blockIdx.y, R = EBLK / H4;
     const int c = threadIdx.x % H4, r0 = threadIdx.x / H4;
@@ -166,8 +165,7 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
             accw[0].w += d * hv.w;
         }
         const float4 o = f4_mask(hv, g);
-        if (dz) dz[e] = o;
-        if (dzp) x6_store4(dzp, (int64_t)e, o);  // the same [2][n][H] matrix in x6 planes (merlin_gemm.hip)
+        dz[e] = o;
         f4_add(acc, o);
     }
     float4 *dst = partials + ((size_t)t * gridDim.x + blockIdx.x) * (size_t)(1 + A) * H4;
@@ -247,8 +245,8 @@ hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, in
 }
 
 hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
-                           const float *wc, int64_t n, int H, int A, float *dz, void *dz_planes, float *db4, float *dwa,
-                           float *dwc, float *work, hipStream_t s) {
+                           const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
+                           float *work, hipStream_t s) {
     if (n <= 0) {
         hipError_t e = hipMemsetAsync(db4, 0, sizeof(float) * 2 * H, s);
         if (e == hipSuccess) e = hipMemsetAsync(dwa, 0, sizeof(float) * A * H, s);
@@ -258,8 +256,7 @@ hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dv
     const int64_t per = (n + nblk - 1) / nblk;
     hipLaunchKernelGGL(k_head_bwd, dim3(nblk, 2), dim3(EBLK), 0, s, reinterpret_cast<const float4 *>(h), dlogits,
                        dvalue, reinterpret_cast<const float4 *>(wa), reinterpret_cast<const float4 *>(wc), n, H / 4,
-                       A, per, reinterpret_cast<float4 *>(dz), reinterpret_cast<uint2 *>(dz_planes),
-                       reinterpret_cast<float4 *>(work));
+                       A, per, reinterpret_cast<float4 *>(dz), reinterpret_cast<float4 *>(work));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int total = (1 + A) * H + 2 * H;

@@ -105,7 +105,7 @@ hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *d
 
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                               const float *b3, int T, float *Y3, uint64_t *bits, void *planes, hipStream_t s);
+                               const float *b3, int T, float *Y3, uint64_t *bits, hipStream_t s);
 hipError_t launch_act_heads(const float *z, const float *b4, int64_t n, int H, const float *wa, const float *ba,
                             const float *wc, const float *bc, int A, int det, uint64_t seed, const int64_t *epoch,
                             int64_t step, int64_t env_offset, int64_t *action, float *logp, float *value,
@@ -134,15 +134,15 @@ hipError_t launch_bias_relu(float *Z, const float *b, int64_t rows, int cols, in
 hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, int64_t rows, int cols, int T,
                                   float *dbias, float *work, hipStream_t s);
 hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
-                           const float *wc, int64_t n, int H, int A, float *dz, void *dz_planes, float *db4, float *dwa,
-                           float *dwc, float *work, hipStream_t s);
+                           const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
+                           float *work, hipStream_t s);
 
 // fc1 on the bf16 matrix cores in exact three-plane form (merlin_gemm.hip, merlin_x6.h)
 hipError_t launch_x6_split(const float *x, int64_t n, void *planes, hipStream_t s);
 hipError_t launch_x6_join(const void *planes, int64_t n, float *x, hipStream_t s);
-hipError_t launch_x6_gemm_nt(const void *A, const void *B, int64_t M, int N, int K, int T, int64_t a_stride,
+hipError_t launch_x6_gemm_nt(const float *A, const void *B, int64_t M, int N, int K, int T, int64_t a_stride,
                              int64_t b_stride, const float *bias, float *C, int64_t c_stride, int cfg, hipStream_t s);
-hipError_t launch_x6_gemm_tn(const void *A, const void *B, int64_t Kd, int M, int N, int T, int64_t a_stride,
+hipError_t launch_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int M, int N, int T, int64_t a_stride,
                              int64_t b_stride, int splits, float *slab, float *out, int cfg, hipStream_t s);
 int x6_tn_max_splits();
 

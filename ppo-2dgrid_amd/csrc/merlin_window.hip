@@ -20,7 +20,6 @@
 #include <algorithm>
 
 #include "merlin_internal.h"
-#include "merlin_x6.h"
 
 namespace merlin {
 namespace {
@@ -62,8 +61,7 @@ __global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ 
 }
 
 // Y3[t][u*9 + p3][c4] = relu(b3[t][c4] + sum_tap Q[t][wid[g*25 + p2(p3, tap)]][tap][c4]); 16
-// consecutive lanes read one 256-B row of Q per tap.  Y3 (or NULL) as fp32 and/or planes (or NULL)
-// as fc1's x6 planes (the same [T][n][576] matrix, merlin_gemm.hip).  bits (optional): bit ch of bits[t][u*9 + p3]
+// consecutive lanes read one 256-B row of Q per tap.  bits (optional): bit ch of bits[t][u*9 + p3]
 // = (Y3 channel ch > 0), the row's ReLU mask for the backward (16 lanes OR their nibbles together
 // with xor shuffles inside the row's 16-lane group; rows are 16-lane aligned, so the groups are
 // whole and converged).
@@ -71,8 +69,7 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
                                                       const int32_t *__restrict__ wid,
                                                       const int64_t *__restrict__ groups, int64_t n,
                                                       const float4 *__restrict__ b3, int T,
-                                                      float4 *__restrict__ Y3, uint64_t *__restrict__ bits,
-                                                      uint2 *__restrict__ planes) {
+                                                      float4 *__restrict__ Y3, uint64_t *__restrict__ bits) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
         const int c = (int)(e & 15);
@@ -94,8 +91,7 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
         const float4 b = b3[t * 16 + c];
         const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
                                      relu_nan(acc.w + b.w));
-        if (Y3) Y3[e] = y;
-        if (planes) x6_store4(planes, e, y);  // fc1's input rows [T][n][576] in x6 planes (merlin_x6.h)
+        Y3[e] = y;
         if (bits) {
             uint64_t v = (uint64_t)((y.x > 0.0f ? 1u : 0u) | (y.y > 0.0f ? 2u : 0u) | (y.z > 0.0f ? 4u : 0u) |
                                     (y.w > 0.0f ? 8u : 0u))
@@ -327,13 +323,12 @@ hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, 
 }
 
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                               const float *b3, int T, float *Y3, uint64_t *bits, void *planes, hipStream_t s) {
+                               const float *b3, int T, float *Y3, uint64_t *bits, hipStream_t s) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
     hipLaunchKernelGGL(k_window_conv3, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4 *>(Q), nw, wid,
-                       groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), bits,
-                       reinterpret_cast<uint2 *>(planes));
+                       groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), bits);
     return hipGetLastError();
 }
 

@@ -106,8 +106,6 @@ def lib():
     L.merlin_ppo_loss.argtypes = [vp, vp, vp, vp, i64, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp, C.c_double,
                                   C.c_double, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]
     L.merlin_x6_split.argtypes = [vp, i64, vp, vp]
-    L.merlin_tower_window_conv3_x6.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp]
-    L.merlin_tower_head_bwd_x6.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
     L.merlin_x6_join.argtypes = [vp, i64, vp, vp]
     L.merlin_x6_gemm_nt.argtypes = [vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, i32, vp]
     L.merlin_x6_tn_slab_floats.argtypes = [i32, i32, i32, i32]
@@ -150,7 +148,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
-    "merlin_x6_split", "merlin_x6_join", "merlin_tower_window_conv3_x6", "merlin_tower_head_bwd_x6", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
+    "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
 )
 
 
@@ -626,10 +624,10 @@ def act_heads(z, b4, w_actor, b_actor, w_critic, b_critic, deterministic=False, 
 
 
 # -- fc1 on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip) ------------------
-# An fp32 matrix [..., R, C] (C % 8 == 0) is held as int16 planes [..., R, 3 * C] (bf16 bits; per
-# group of 8 values three 16-B chunks, x = x0 + x1 + x2 exactly, include/merlin_hip.h).
-X6_NT_CFG = {"fwd": 2, "dgrad": 3}  # tile configurations of merlin_x6_gemm_nt (N = 512 / 576), scripts/probe_x6.py
-X6_TN_CFG = 1
+# Weights as int16 planes [..., R, 3 * C] (bf16 bits; per group of 8 values three 16-B chunks,
+# x = x0 + x1 + x2 exactly, include/merlin_hip.h); activations as fp32, split while staged.
+X6_NT_CFG = {"fwd": 0, "dgrad": 1}  # tile configurations of merlin_x6_gemm_nt (N = 512 / 576), scripts/probe_x6.py
+X6_TN_CFG = 0
 X6_TN_SPLITS = 32
 
 
@@ -654,12 +652,12 @@ def x6_join(planes: torch.Tensor) -> torch.Tensor:
 
 def x6_gemm_nt(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = None, cfg: int = 0,
                out: torch.Tensor | None = None, name: str = "x6_gemm_nt") -> torch.Tensor:
-    """C f32[T, M, N] = A @ B^T per tower (+ bias[t] and ReLU when bias is given) from planes A
-    int16[T, M, 3K], B int16[T, N, 3K]."""
-    T, M, K3 = (int(v) for v in A.shape)
+    """C f32[T, M, N] = A @ B^T per tower (+ bias[t] and ReLU when bias is given), A f32[T, M, K],
+    B planes int16[T, N, 3K] (x6_split of an f32 [T, N, K])."""
+    T, M, K = (int(v) for v in A.shape)
     N = int(B.shape[1])
-    K = K3 // 3
-    assert A.dtype == B.dtype == torch.int16 and B.shape == (T, N, K3) and A.is_contiguous() and B.is_contiguous()
+    assert A.dtype == torch.float32 and B.dtype == torch.int16 and B.shape == (T, N, 3 * K)
+    assert A.is_contiguous() and B.is_contiguous()
     if bias is not None:
         assert bias.shape == (T, N) and bias.dtype == torch.float32
         bias = bias.detach().contiguous()
@@ -674,12 +672,12 @@ def x6_gemm_nt(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = Non
 
 def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int = X6_TN_SPLITS, cfg: int = X6_TN_CFG,
                name: str = "x6_gemm_tn") -> torch.Tensor:
-    """out f32[T, M, N] = A^T @ B per tower from planes A int16[T, Kd, 3M], B int16[T, Kd, 3N] (the
-    long k range split into `splits` slabs summed in order)."""
-    T, Kd, M3 = (int(v) for v in A.shape)
-    N3 = int(B.shape[2])
-    M, N = M3 // 3, N3 // 3
-    assert A.dtype == B.dtype == torch.int16 and B.shape[:2] == (T, Kd) and A.is_contiguous() and B.is_contiguous()
+    """out f32[T, M, N] = A^T @ B per tower, A f32[T, Kd, M], B f32[T, Kd, N] (the long k range split
+    into `splits` slabs summed in order)."""
+    T, Kd, M = (int(v) for v in A.shape)
+    N = int(B.shape[2])
+    assert A.dtype == B.dtype == torch.float32 and B.shape[:2] == (T, Kd)
+    assert A.is_contiguous() and B.is_contiguous()
     out = torch.empty((T, M, N), dtype=torch.float32, device=A.device)
     slab = torch.empty(int(lib().merlin_x6_tn_slab_floats(M, N, T, int(splits))), dtype=torch.float32,
                        device=A.device)
@@ -687,35 +685,3 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int = X6_TN_SPLITS, cfg
         check(lib().merlin_x6_gemm_tn(ptr(A), ptr(B), Kd, M, N, T, Kd * M, Kd * N, int(splits), ptr(slab), ptr(out),
                                       int(cfg), stream_of(A)), "merlin_x6_gemm_tn")
     return out
-
-
-def window_conv3_x6(Q, wid, groups, b3):
-    """window_conv3(bits=True) writing fc1's input straight in x6 planes: (planes int16[T, n, 3 * 576],
-    bits int64[T, n*9])."""
-    T, nw = int(Q.shape[0]), int(Q.shape[1])
-    n = int(groups.numel())
-    assert Q.shape[2] == 576 and Q.dtype == torch.float32 and b3.shape == (T, 64)
-    assert wid.dtype == torch.int32 and wid.shape[1] == 25 and groups.dtype == torch.int64
-    planes = torch.empty((T, n, 3 * 576), dtype=torch.int16, device=Q.device)
-    mask = torch.empty((T, n * 9), dtype=torch.int64, device=Q.device)
-    # algorithmic bytes: planes (6 B per value) + bit words written, ids read, Q once
-    with KernelTimer.span("k_window_conv3", T * n * 9 * (64 * 6 + 8) + n * 108 + T * nw * 576 * 4):
-        check(lib().merlin_tower_window_conv3_x6(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(planes),
-                                                 ptr(mask), stream_of(Q)), "merlin_tower_window_conv3_x6")
-    return planes, mask
-
-
-def head_bwd_x6(h, dlogits, dvalue, w_actor, w_critic):
-    """head_bwd writing dz in x6 planes: (dz_planes int16[2, n, 3H], dbias, dw_actor, dw_critic)."""
-    _, n, H = (int(x) for x in h.shape)
-    A = int(w_actor.shape[0])
-    assert h.shape[0] == 2 and dlogits.shape == (n, A) and dvalue.numel() == n and w_critic.numel() == H
-    dzp = torch.empty((2, n, 3 * H), dtype=torch.int16, device=h.device)
-    db = torch.empty((2, H), dtype=torch.float32, device=h.device)
-    dwa = torch.empty((A, H), dtype=torch.float32, device=h.device)
-    dwc = torch.empty((H,), dtype=torch.float32, device=h.device)
-    with KernelTimer.span("k_head_bwd", h.numel() * (4 + 6) + n * (A + 1) * 4):
-        check(lib().merlin_tower_head_bwd_x6(ptr(h), ptr(dlogits), ptr(dvalue), ptr(w_actor), ptr(w_critic), n, H, A,
-                                             ptr(dzp), ptr(db), ptr(dwa), ptr(dwc), stream_of(h)),
-              "merlin_tower_head_bwd_x6")
-    return dzp, db, dwa, dwc

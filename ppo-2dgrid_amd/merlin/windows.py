@@ -430,41 +430,42 @@ def _conv3_backward(plan, mb, bits, dY3, nw):
 class _WindowTowerHeadX6(torch.autograd.Function):
     """conv3 -> fc1 -> ReLU -> heads of both towers for the minibatch's distinct frames, with fc1's
     three GEMMs on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip):
-      forward   a3 = relu(conv3) from Q (k_window_conv3, written straight into x6 planes, plus the
-                ReLU bit words), h = relu(a3 W4p^T + b4) (merlin_x6_gemm_nt, bias + ReLU epilogue),
-                logits = h0 Wa^T (+ ba), value = h1 wc (+ bc)   (src/actor_critic.py:13-14, 31-41)
-      backward  the heads' backward through fc1's ReLU (k_head_bwd, dz written in x6 planes), da3 =
-                dz W4p (x6 NT against W4p^T), dW4p = dz^T a3 (x6 TN, split-K), then conv3's backward
-                through the patch / band / window sums (_conv3_backward).
-    fp32 products throughout; no fp32 copy of a3 or dz exists."""
+      forward   a3 = relu(conv3) from Q (k_window_conv3, with the ReLU bit words), h = relu(a3 W4p^T +
+                b4) (merlin_x6_gemm_nt, bias + ReLU epilogue), logits = h0 Wa^T (+ ba), value = h1 wc
+                (+ bc)   (src/actor_critic.py:13-14, 31-41)
+      backward  the heads' backward through fc1's ReLU (k_head_bwd), da3 = dz W4p (x6 NT against the
+                planes of W4p^T), dW4p = dz^T a3 (x6 TN, split-K), then conv3's backward through the
+                patch / band / window sums (_conv3_backward).
+    fp32 products throughout (the activations are split into planes inside the GEMMs)."""
 
     @staticmethod
     def forward(ctx, Q, b3, W4p, b4, Wa, ba, Wc, bc, plan, mb):
-        a3p, bits = nat.window_conv3_x6(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous())
-        W4pp = nat.x6_split(W4p.detach())
-        h = nat.x6_gemm_nt(a3p, W4pp, bias=b4.detach(), cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
+        Y3, bits = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous(), bits=True)
+        n = int(mb.groups.numel())
+        a3 = Y3.view(2, n, 576)
+        h = nat.x6_gemm_nt(a3, nat.x6_split(W4p.detach()), bias=b4.detach(), cfg=nat.X6_NT_CFG["fwd"],
+                           name="gemm_fc1_fwd")
         logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
         value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)
-        ctx.save_for_backward(a3p, bits, W4p, h, Wa, Wc)
+        ctx.save_for_backward(a3, bits, W4p, h, Wa, Wc)
         ctx.head_bias = (ba is not None, bc is not None)
         ctx.plan, ctx.mb, ctx.nw_q = plan, mb, Q.shape[1]
         return logits, value
 
     @staticmethod
     def backward(ctx, dlogits, dvalue):
-        a3p, bits, W4p, h, Wa, Wc = ctx.saved_tensors
+        a3, bits, W4p, h, Wa, Wc = ctx.saved_tensors
         n = h.shape[1]
         dlogits = h.new_zeros(n, Wa.shape[0]) if dlogits is None else dlogits.contiguous()
         dvalue = h.new_zeros(n) if dvalue is None else dvalue.contiguous()
-        dzp, db4, dWa, dWc = nat.head_bwd_x6(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
+        dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
         W4tp = nat.x6_split(W4p.detach().transpose(1, 2).contiguous())
-        da3 = nat.x6_gemm_nt(dzp, W4tp, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
-        dW4p = nat.x6_gemm_tn(dzp, a3p, name="gemm_wgrad")
+        da3 = nat.x6_gemm_nt(dz, W4tp, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+        dW4p = nat.x6_gemm_tn(dz, a3, name="gemm_wgrad")
         dQ, db3 = _conv3_backward(ctx.plan, ctx.mb, bits, da3.view(2, n * 9, 64), ctx.nw_q)
         dba = dlogits.sum(0) if ctx.head_bias[0] else None
         dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
         return dQ, db3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc, None, None
-
 
 def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = None) -> torch.Tensor:
     """relu(conv3(relu(conv2(relu(conv1(frame)))))) of both towers of CNNActorCritic `ac` for the

@@ -39,12 +39,12 @@ def main():
     back = nat.x6_join(P).view(-1)
     print("split exact:", bool(torch.equal(back, x)), "mismatches", int((back != x).sum()))
 
-    for name, (N, K, cfgs) in {"fwd": (512, 576, [2, 6, 8, 9]), "dgrad": (576, 512, [3, 7, 8])}.items():
+    for name, (N, K, cfgs) in {"fwd": (512, 576, [0, 2, 3]), "dgrad": (576, 512, [1, 3])}.items():
         # fc1-like operands: A >= 0 sparse-ish activations, B weights
         A = torch.relu(torch.randn(2, M, K, device=dev, generator=g))
         B = torch.randn(2, N, K, device=dev, generator=g) / K ** 0.5
         bias = torch.randn(2, N, device=dev, generator=g) * 0.1
-        Ap, Bp = nat.x6_split(A), nat.x6_split(B)
+        Ap, Bp = A, nat.x6_split(B)
         rows = slice(0, min(M, 20000))
         C64 = torch.bmm(A[:, rows].double(), B.double().transpose(1, 2))
         den = torch.bmm(A[:, rows].abs().double(), B.abs().double().transpose(1, 2))
@@ -72,7 +72,7 @@ def main():
     Mj, Nc = 512, 576
     dz = torch.randn(2, M, Mj, device=dev, generator=g) * (torch.rand(2, M, Mj, device=dev, generator=g) > 0.5)
     a3 = torch.relu(torch.randn(2, M, Nc, device=dev, generator=g))
-    dzp, a3p = nat.x6_split(dz), nat.x6_split(a3)
+    dzp, a3p = dz, a3
     W64 = torch.bmm(dz.double().transpose(1, 2), a3.double())
     den = torch.bmm(dz.abs().double().transpose(1, 2), a3.abs().double())
     Wref = torch.bmm(dz.transpose(1, 2), a3)
@@ -80,8 +80,8 @@ def main():
     t_ref = timeit(lambda: torch.bmm(dz.transpose(1, 2), a3))
     print(f"[wgrad] Kd={M}: torch fp32 bmm {t_ref:.1f} us ({flops / t_ref / 1e6:.1f} TF), "
           f"max err/sum|ab| {rel_err(Wref, W64, den):.3e}")
-    for cfg in (1, 2):
-        for splits in (16, 32, 40, 48, 64):
+    for cfg in (0, 1, 2):
+        for splits in (32, 48, 64):
             try:
                 W = nat.x6_gemm_tn(dzp, a3p, splits=splits, cfg=cfg)
             except nat.MerlinNativeError as ex:

@@ -28,7 +28,7 @@ def main():
         W64 = torch.bmm(A.double().transpose(1, 2), B.double())
         Wt = torch.bmm(A.transpose(1, 2), B)
         Wsk = sum(torch.bmm(A[:, i:i + 3500].transpose(1, 2), B[:, i:i + 3500]) for i in range(0, Kd, 3500))
-        Ap, Bp = nat.x6_split(A), nat.x6_split(B)
+        Ap, Bp = A.contiguous(), B.contiguous()
         print(f"[wgrad, {name}] |W|/sum|ab| = {float(W64.norm() / torch.bmm(A.abs().double().transpose(1, 2), B.abs().double()).norm()):.2e}")
         print(f"  torch fp32 bmm   rel err {rel(Wt, W64):.3e}")
         print(f"  torch split-K    rel err {rel(Wsk, W64):.3e}")
@@ -36,10 +36,10 @@ def main():
             W = nat.x6_gemm_tn(Ap, Bp, splits=splits)
             print(f"  x6 tn splits {splits:2d} rel err {rel(W, W64):.3e}")
         # the same product through the NT kernel (transposed operands materialised)
-        At = nat.x6_split(A.transpose(1, 2).contiguous()[:, :, :Kd // 32 * 32])
-        Bt = nat.x6_split(B.transpose(1, 2).contiguous()[:, :, :Kd // 32 * 32])
+        At = A.transpose(1, 2)[:, :, :Kd // 32 * 32].contiguous()
+        Bt = nat.x6_split(B.transpose(1, 2)[:, :, :Kd // 32 * 32].contiguous())
         W64t = torch.bmm(A[:, :Kd // 32 * 32].double().transpose(1, 2), B[:, :Kd // 32 * 32].double())
-        print(f"  x6 nt (K={Kd // 32 * 32})   rel err {rel(nat.x6_gemm_nt(At, Bt, cfg=3), W64t):.3e}")
+        print(f"  x6 nt (K={Kd // 32 * 32})   rel err {rel(nat.x6_gemm_nt(At, Bt, cfg=1), W64t):.3e}")
 
 
 if __name__ == "__main__":

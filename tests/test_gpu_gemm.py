@@ -3,9 +3,10 @@
 The plane split must be lossless (x0 + x1 + x2 == x bit for bit); each GEMM is compared with a
 float64 product of the same fp32 operands, and its error must be no larger than that of torch's
 own fp32 GEMM (hipBLASLt) on the same operands, measured as max |C - C64| / sum_k |a_k b_k|
-(tolerance written below: 2x hipBLASLt's error, floor 1e-6).  Shapes: the update's fc1 (K = 576 / 512,
-N = 512 / 576) at row counts that are not tile multiples, both towers with their own operands;
-the producers' plane outputs (k_window_conv3, k_head_bwd) against splitting their fp32 outputs."""
+(tolerance written below: 2x hipBLASLt's error, floor 1e-6); on a cancellation-heavy weight
+gradient (the update's: the result ~1e-2 of sum |a b|) the error relative to the result's norm must
+not exceed hipBLASLt's own split-K product's.  Shapes: the update's fc1 (K = 576 / 512, N = 512 /
+576) at row counts that are not tile multiples, both towers with their own operands."""
 import pytest
 import torch
 
@@ -36,7 +37,7 @@ def test_split_is_exact(device):
     assert torch.equal(p0.view(torch.bfloat16), x.to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("N,K,cfg", [(512, 576, 2), (576, 512, 3), (512, 576, 0), (576, 512, 1), (576, 512, 5)])
+@pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 3)])
 @pytest.mark.parametrize("M", [1, 777, 20011])
 def test_gemm_nt_vs_float64(device, M, N, K, cfg):
     from merlin import _native as nat
@@ -48,15 +49,15 @@ def test_gemm_nt_vs_float64(device, M, N, K, cfg):
     C64 = torch.bmm(A.double(), B.double().transpose(1, 2))
     den = torch.bmm(A.abs().double(), B.abs().double().transpose(1, 2))
     tol = max(2 * _err(torch.bmm(A, B.transpose(1, 2)), C64, den), TOL_FLOOR)
-    Ap, Bp = nat.x6_split(A), nat.x6_split(B)
-    C = nat.x6_gemm_nt(Ap, Bp, cfg=cfg)
+    Bp = nat.x6_split(B)
+    C = nat.x6_gemm_nt(A, Bp, cfg=cfg)
     assert _err(C, C64, den) <= tol
-    Cb = nat.x6_gemm_nt(Ap, Bp, bias=bias, cfg=cfg)
+    Cb = nat.x6_gemm_nt(A, Bp, bias=bias, cfg=cfg)
     assert torch.equal(Cb, torch.relu(C + bias.unsqueeze(1)))
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2])
-@pytest.mark.parametrize("Kd,splits", [(1, 1), (4093, 7), (40000, 32)])
+@pytest.mark.parametrize("Kd,splits", [(1, 1), (4093, 7), (40000, 32), (40000, 64)])
 def test_gemm_tn_vs_float64(device, Kd, splits, cfg):
     from merlin import _native as nat
 
@@ -67,35 +68,25 @@ def test_gemm_tn_vs_float64(device, Kd, splits, cfg):
     W64 = torch.bmm(dz.double().transpose(1, 2), a3.double())
     den = torch.bmm(dz.abs().double().transpose(1, 2), a3.abs().double())
     tol = max(2 * _err(torch.bmm(dz.transpose(1, 2), a3), W64, den), TOL_FLOOR)
-    W = nat.x6_gemm_tn(nat.x6_split(dz), nat.x6_split(a3), splits=splits, cfg=cfg)
+    W = nat.x6_gemm_tn(dz, a3, splits=splits, cfg=cfg)
     assert _err(W, W64, den) <= tol
     # fixed-order slab fold: bitwise reproducible
-    assert torch.equal(W, nat.x6_gemm_tn(nat.x6_split(dz), nat.x6_split(a3), splits=splits, cfg=cfg))
+    assert torch.equal(W, nat.x6_gemm_tn(dz, a3, splits=splits, cfg=cfg))
 
 
-def test_producers_write_planes(device):
-    """k_window_conv3 / k_head_bwd plane outputs == splitting their fp32 outputs."""
+def test_gemm_tn_cancellation(device):
+    """The update's weight gradient: ~1e5 rows whose terms nearly cancel (|W| ~ 1e-2 sum |a b|)."""
     from merlin import _native as nat
 
-    from test_gpu_windows import _plan
-
-    codes, plan = _plan(device)
-    mb = plan.minibatch(torch.randperm(codes.shape[0], device=device)[:1500])
-    torch.manual_seed(3)
-    Q = torch.randn(2, plan.num_windows, 576, device=device)
-    b3 = torch.randn(2, 64, device=device)
-    Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True)
-    P, bits6 = nat.window_conv3_x6(Q, plan.wid, mb.groups, b3)
-    n = int(mb.groups.numel())
-    assert torch.equal(bits6, bits)
-    assert torch.equal(P, nat.x6_split(Y3.view(2, n, 576)))
-    h = torch.relu(torch.randn(2, 999, 512, device=device))
-    dl, dv = torch.randn(999, 3, device=device), torch.randn(999, device=device)
-    wa, wc = torch.randn(3, 512, device=device), torch.randn(1, 512, device=device)
-    dz, db, dwa, dwc = nat.head_bwd(h, dl, dv, wa, wc)
-    dzp, db6, dwa6, dwc6 = nat.head_bwd_x6(h, dl, dv, wa, wc)
-    assert torch.equal(dzp, nat.x6_split(dz))
-    assert torch.equal(db6, db) and torch.equal(dwa6, dwa) and torch.equal(dwc6, dwc)
+    g = torch.Generator(device=device).manual_seed(5)
+    Kd = 60000
+    a3 = torch.relu(torch.randn(2, Kd, 576, device=device, generator=g))
+    sgn = torch.where(torch.rand(2, Kd, 1, device=device, generator=g) < 0.5005, 1.0, -1.0)
+    dz = sgn * torch.rand(2, Kd, 512, device=device, generator=g)
+    W64 = torch.bmm(dz.double().transpose(1, 2), a3.double())
+    rel = lambda W: float((W.double() - W64).norm() / W64.norm())  # noqa: E731
+    ref = rel(sum(torch.bmm(dz[:, i:i + 2000].transpose(1, 2), a3[:, i:i + 2000]) for i in range(0, Kd, 2000)))
+    assert rel(nat.x6_gemm_tn(dz, a3)) <= ref
 
 
 def test_window_update_x6_matches_hipblaslt(device):
