@@ -54,6 +54,11 @@ FC_FWD_MACS = 2 * 294_912 + 512 * 3 + 512
 WINDOW_FWD_MACS = 2 * 64 * 576  # per window per minibatch
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (vector == f32 MFMA rate)
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense BF16 MFMA (MI355X_MICROARCH.md; no sparsity)
+# fc1's three GEMMs run on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip):
+# six bf16 MFMA products per fp32 product, so their executed MFMA work is 6x the fp32 FLOP count
+X6_GEMMS = ("gemm_fc1_fwd", "gemm_fc1_dgrad", "gemm_wgrad")
+X6_PRODUCTS = 6
 
 
 def parse():
@@ -247,7 +252,9 @@ def cpu_baseline():
 # fc1 GEMMs are hipBLASLt kernels, matched by name prefix (largest grid = the update's, not the
 # rollout's); their PMC key is the full Tensile kernel name.
 PMC_ALIAS = {"k_seg_sum_dQ": "k_seg_sum"}
-PMC_PREFIX = {"gemm_fc1_fwd": "Cijk_Alik_Bljk_S_B_Bias_HA_S_SAV_UserArgs_MT128x128x64"}
+PMC_PREFIX = {"gemm_fc1_fwd": "void merlin::(anonymous namespace)::k_x6_nt<256, 128, 4, 2, 1>",
+              "gemm_fc1_dgrad": "void merlin::(anonymous namespace)::k_x6_nt<128, 192, 2, 4, 0>",
+              "gemm_wgrad": "void merlin::(anonymous namespace)::k_x6_tn<128, 192, 2, 4>"}
 PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 
 
@@ -304,8 +311,16 @@ def kernel_table(records):
     return out
 
 
-def roofline_of(name, k):
+def roofline_of(name, k, x6=False):
     traffic = pmc_traffic(name)
+    if "tflops" in k and x6 and name in X6_GEMMS:  # fc1 on the bf16 matrix cores: executed bf16 MFMA work
+        ex = k["tflops"] * X6_PRODUCTS
+        return {"kernel": name, "bound": "mfma", "achieved": round(ex, 2), "peak": BF16_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ex / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                "flops_per_launch": k["flops_per_launch"] * X6_PRODUCTS, "avg_launch_us": k["avg_us"],
+                "launches": k["launches"], "mfma": "bf16 16x16x32, 6 plane products per fp32 product",
+                "fp32_equivalent_tflops": k["tflops"],
+                "fp32_equivalent_frac_of_f32_peak": round(k["tflops"] / FP32_PEAK_TFLOPS, 4)}
     if "tflops" in k:  # a hipBLASLt GEMM: f32 MFMA bound
         return {"kernel": name, "bound": "mfma", "achieved": k["tflops"], "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(k["tflops"] / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
@@ -422,6 +437,7 @@ def main():
             dist.barrier()
         return
     dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
+    x6 = getattr(agent.ac, "fc1_impl", None) == "x6"
     handwritten = max((k for k in kernels if k.startswith("k_")), key=lambda k: kernels[k]["total_ms"])
     ref_flop_per_step = 2 * FWD_MACS + args.epochs * 2 * (FWD_MACS + BWD_MACS)
     frac = agent.last_distinct_frac if agent.last_distinct_frac is not None else 1.0
@@ -442,6 +458,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
+        # fp32 arithmetic throughout; fc1's GEMMs compute their fp32 products from exact three-way bf16
+        # splits of the fp32 operands on the matrix cores (error vs float64 below hipBLASLt's fp32 GEMM,
+        # tests/test_gpu_gemm.py)
         "dtype": "fp32",
         "data": "synthetic: procedurally generated mediumhard maps (numpy-PCG64-exact, seeds 777+i), "
                 "random-init CNNActorCritic (torch seed 777), timed after the warm-up iterations",
@@ -458,12 +477,13 @@ def main():
                                        if agent.last_distinct_frac is not None else None),
         # dominant kernel of the timed loop by total HIP-event time (hand-written kernels and the
         # fc1 hipBLASLt GEMMs, which are timed the same way)
-        "roofline": roofline_of(dominant, kernels[dominant]),
+        "roofline": roofline_of(dominant, kernels[dominant], x6),
         # dominant hand-written kernel
         "roofline_handwritten": dict(roofline_of(handwritten, kernels[handwritten]),
                                      **gather_note(handwritten, kernels[handwritten])),
-        # every hipBLASLt GEMM family timed in the loop against the f32 MFMA peak
-        "roofline_gemm": {k: roofline_of(k, v) for k, v in kernels.items() if "tflops" in v},
+        # every GEMM family timed in the loop: fc1's (x6) against the bf16 MFMA peak with the executed
+        # plane products, hipBLASLt's against the f32 MFMA peak
+        "roofline_gemm": {k: roofline_of(k, v, x6) for k, v in kernels.items() if "tflops" in v},
         # the env-step kernel inside the timed loop (absent when the rollout replays as a graph:
         # no per-kernel events inside it); the HBM-scale measurement is tiers.env_only_2M_envs
         "roofline_env_step": roofline_of("k_env_step", kernels["k_env_step"]) if "k_env_step" in kernels else None,

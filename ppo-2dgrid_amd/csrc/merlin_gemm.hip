@@ -72,19 +72,22 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8 a, const bf16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// acc + the six plane products with i + j <= 2 of one k step.  The step's products are summed on
-// their own (smallest first, into a fresh accumulator) and the step's total is added to acc with one
-// rounding: the five small products never round at the running sum's scale, so the error is that of
-// a blocked fp32 sum (the matrix cores' own bf16 x bf16 products are exact).
-template <typename F>
+// acc + the six plane products with i + j <= 2 of one k step.  CHUNK: the step's products are
+// summed on their own (smallest first, into a fresh accumulator) and the step's total is added to
+// acc with one rounding, so the five small products never round at the running sum's scale -- the
+// error of a blocked fp32 sum (the matrix cores' own bf16 x bf16 products are exact); the weight
+// gradient's long, cancelling sums need it.  Without CHUNK the six products accumulate straight into
+// acc (smallest first): six roundings per 32-deep step at the running sum's scale, still fewer than
+// an fp32 fma chain's 32, and no vector adds beside the matrix cores.
+template <bool CHUNK, typename F>
 __device__ __forceinline__ f32x4 mma6(const F a[3], const F b[3], f32x4 acc) {
-    f32x4 c = mfma(a[2], b[0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+    f32x4 c = mfma(a[2], b[0], CHUNK ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : acc);
     c = mfma(a[1], b[1], c);
     c = mfma(a[0], b[2], c);
     c = mfma(a[1], b[0], c);
     c = mfma(a[0], b[1], c);
     c = mfma(a[0], b[0], c);
-    return acc + c;
+    return CHUNK ? acc + c : c;
 }
 
 __device__ __forceinline__ float relu_nan(float v) { return v != v ? v : fmaxf(v, 0.0f); }
@@ -109,7 +112,7 @@ __device__ __forceinline__ void split8(const float4 a, const float4 b, u32x4 &p0
 // ---------------------------------------------------------------------------------------------
 // NT: C[t][m][n] = epi(sum_k A[t][m][k] B[t][n][k]); A fp32 [M][K], B x6 planes [N][K/8][3][8]
 // (K % 32 == 0, N % BN == 0); EPI 1: relu(. + bias[t][n]).  grid (tiles_m * tiles_n, T).
-template <int BM, int BN, int WGM, int WGN, int EPI>
+template <int BM, int BN, int WGM, int WGN, int EPI, bool CHUNK>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const float4 *__restrict__ A, const u32x4 *__restrict__ B,
                                                           int64_t M, int N, int K, int64_t sA, int64_t sB,
                                                           const float *__restrict__ bias, float *__restrict__ C,
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const float4 *__restri
 #pragma unroll
                 for (int p = 0; p < 3; p++) bf[p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
 #pragma unroll
-                for (int i = 0; i < FM; i++) acc[i][j] = mma6(af[i], bf, acc[i][j]);
+                for (int i = 0; i < FM; i++) acc[i][j] = mma6<CHUNK>(af[i], bf, acc[i][j]);
             }
         } else {
             u32x4 bf[FN][3];
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const float4 *__restri
 #pragma unroll
                 for (int p = 0; p < 3; p++) af[p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
 #pragma unroll
-                for (int j = 0; j < FN; j++) acc[i][j] = mma6(af, bf[j], acc[i][j]);
+                for (int j = 0; j < FN; j++) acc[i][j] = mma6<CHUNK>(af, bf[j], acc[i][j]);
             }
         }
         __syncthreads();
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restri
 #pragma unroll
                 for (int p = 0; p < 3; p++) bf[p] = tr_frag<RCB>(sBl + p * PSB, wn * WTN + j * 16, lane);
 #pragma unroll
-                for (int i = 0; i < FM; i++) acc[i][j] = mma6(af[i], bf, acc[i][j]);
+                for (int i = 0; i < FM; i++) acc[i][j] = mma6<true>(af[i], bf, acc[i][j]);
             }
         } else {
             bf16x8 bf[FN][3];
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restri
 #pragma unroll
                 for (int p = 0; p < 3; p++) af[p] = tr_frag<RCA>(sAl + p * PSA, wm * WTM + i * 16, lane);
 #pragma unroll
-                for (int j = 0; j < FN; j++) acc[i][j] = mma6(af, bf[j], acc[i][j]);
+                for (int j = 0; j < FN; j++) acc[i][j] = mma6<true>(af, bf[j], acc[i][j]);
             }
         }
         __syncthreads();
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(256) void k_x6_fold(const float4 *__restrict__ slab
     }
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, bool CHUNK = true>
 hipError_t nt_launch(const float4 *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
                      const float *bias, float *C, int64_t sC, hipStream_t s) {
     if (N % BN) return hipErrorInvalidValue;
@@ -455,10 +458,10 @@ hipError_t nt_launch(const float4 *A, const u32x4 *B, int64_t M, int N, int K, i
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(tiles_m * tiles_n), T);
     if (bias)
-        hipLaunchKernelGGL((k_x6_nt<BM, BN, WGM, WGN, 1>), grid, dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB, bias,
+        hipLaunchKernelGGL((k_x6_nt<BM, BN, WGM, WGN, 1, CHUNK>), grid, dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB, bias,
                            C, sC, tiles_n);
     else
-        hipLaunchKernelGGL((k_x6_nt<BM, BN, WGM, WGN, 0>), grid, dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB,
+        hipLaunchKernelGGL((k_x6_nt<BM, BN, WGM, WGN, 0, CHUNK>), grid, dim3(64 * WGM * WGN), 0, s, A, B, M, N, K, sA, sB,
                            nullptr, C, sC, tiles_n);
     return hipGetLastError();
 }
@@ -519,6 +522,9 @@ hipError_t launch_x6_gemm_nt(const float *A, const void *B, int64_t M, int N, in
         case 1: return nt_launch<128, 192, 2, 4>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         case 2: return nt_launch<128, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         case 3: return nt_launch<256, 64, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        // unchunked accumulation (all six products straight into the running sum): ~2-6 % faster,
+        // error of the order of an fp32 fma chain (scripts/probe_x6.py); not used
+        case 4: return nt_launch<256, 128, 4, 2, false>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         default: return hipErrorInvalidValue;
     }
 }
