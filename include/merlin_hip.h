@@ -365,6 +365,11 @@ int merlin_tower_bias_relu(float *z_dev, const float *bias_dev, int64_t rows, in
                            void *stream);
 int merlin_tower_relu_bwd(const float *y_dev, const float *dy_dev, float *dz_dev, int64_t rows, int32_t cols,
                           int32_t towers, float *dbias_dev, void *stream);
+/* colsum: out float[towers][cols] = sum over r < rows of x[t * tower_stride + r * row_stride + c]
+ * (fixed order; strides in floats, multiples of 4): the conv3 bias gradient from the per-window tap-0
+ * rows of dQ (merlin/windows.py). */
+int merlin_tower_colsum(const float *x_dev, int64_t rows, int32_t cols, int64_t row_stride, int64_t tower_stride,
+                        int32_t towers, float *out_dev, void *stream);
 int merlin_tower_head_bwd(const float *h_dev, const float *dlogits_dev, const float *dvalue_dev,
                           const float *w_actor_dev, const float *w_critic_dev, int64_t n, int32_t hidden,
                           int32_t act_dim, float *dz_dev, float *dbias_dev, float *dw_actor_dev,

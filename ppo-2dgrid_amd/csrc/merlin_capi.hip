@@ -720,6 +720,20 @@ int merlin_tower_relu_bwd(const float *y, const float *dy, float *dz, int64_t ro
     return MERLIN_OK;
 }
 
+int merlin_tower_colsum(const float *x, int64_t rows, int32_t cols, int64_t row_stride, int64_t tower_stride,
+                        int32_t towers, float *out, void *stream) {
+    if (!out || (!x && rows > 0)) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (!merlin::epilogue_cols_ok(cols)) return fail(MERLIN_E_UNSUPPORTED, "cols must be 4 x a divisor of 256");
+    if (row_stride < cols || row_stride % 4 || tower_stride % 4) return fail(MERLIN_E_INVALID, "bad strides");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_colsum(x, rows, cols, row_stride, tower_stride, towers, out, ws->epi_work,
+                                  (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
 int merlin_tower_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *w_actor,
                           const float *w_critic, int64_t n, int32_t hidden, int32_t act_dim, float *dz, float *dbias,
                           float *dw_actor, float *dw_critic, void *stream) {

@@ -77,6 +77,26 @@ __global__ __launch_bounds__(EBLK) void k_relu_bwd_colsum(const float4 *__restri
     }
 }
 
+// partials[t][b][c4] = sum over the block's rows r of X[t][r * stride4 + c] (column sums of strided rows)
+__global__ __launch_bounds__(EBLK) void k_colsum(const float4 *__restrict__ X, int64_t rows, int c4, int64_t stride4,
+                                                 int64_t tstride4, int64_t per, float4 *__restrict__ partials) {
+    __shared__ float4 red[EBLK];
+    const int t = blockIdx.y, R = EBLK / c4;
+    const int c = threadIdx.x % c4, r0 = threadIdx.x / c4;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = std::min<int64_t>(rows, lo + per);
+    const float4 *Xt = X + (size_t)t * tstride4 + c;
+    float4 acc = f4_zero();
+#pragma unroll 4
+    for (int64_t r = lo + r0; r < hi; r += R) f4_add(acc, Xt[(size_t)r * stride4]);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < c4) {
+        float4 s = red[threadIdx.x];
+        for (int k = 1; k < R; k++) f4_add(s, red[threadIdx.x + k * c4]);
+        partials[((size_t)t * gridDim.x + blockIdx.x) * c4 + threadIdx.x] = s;
+    }
+}
+
 // Fold of per-block partials: output k (< total) is the sum over blocks b of
 // partials[(t * nblk + b) * S + off] with (t, off) = locate(k).  A block takes 32 outputs; its
 // 8 slices of 32 threads each sum every 8th block (8 loads in flight), then slice 0 adds the
@@ -241,6 +261,20 @@ hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, in
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fold_cols, dim3((T * cols + FOLD_COLS - 1) / FOLD_COLS), dim3(FOLD_COLS * FOLD_SLICES), 0, s,
                        work, nblk, cols, T, dbias);
+    return hipGetLastError();
+}
+
+hipError_t launch_colsum(const float *X, int64_t rows, int cols, int64_t row_stride, int64_t tower_stride, int T,
+                         float *out, float *work, hipStream_t s) {
+    if (rows <= 0) return hipMemsetAsync(out, 0, sizeof(float) * T * cols, s);
+    const int nblk = blocks_for(rows);
+    const int64_t per = (rows + nblk - 1) / nblk;
+    hipLaunchKernelGGL(k_colsum, dim3(nblk, T), dim3(EBLK), 0, s, reinterpret_cast<const float4 *>(X), rows, cols / 4,
+                       row_stride / 4, tower_stride / 4, per, reinterpret_cast<float4 *>(work));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_fold_cols, dim3((T * cols + FOLD_COLS - 1) / FOLD_COLS), dim3(FOLD_COLS * FOLD_SLICES), 0, s,
+                       work, nblk, cols, T, out);
     return hipGetLastError();
 }
 

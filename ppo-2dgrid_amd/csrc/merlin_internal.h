@@ -133,6 +133,8 @@ int epilogue_max_act();
 hipError_t launch_bias_relu(float *Z, const float *b, int64_t rows, int cols, int T, hipStream_t s);
 hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, int64_t rows, int cols, int T,
                                   float *dbias, float *work, hipStream_t s);
+hipError_t launch_colsum(const float *X, int64_t rows, int cols, int64_t row_stride, int64_t tower_stride, int T,
+                         float *out, float *work, hipStream_t s);
 hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
                            const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
                            float *work, hipStream_t s);

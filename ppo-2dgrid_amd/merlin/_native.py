@@ -98,6 +98,7 @@ def lib():
                                             vp]
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
+    L.merlin_tower_colsum.argtypes = [vp, i64, i32, i64, i64, i32, vp, vp]
     L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
     L.merlin_act_heads.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp,
                                    vp]
@@ -147,6 +148,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
+    "merlin_tower_colsum",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
 )
@@ -528,6 +530,18 @@ def relu_bwd(y, dy, out=None):
         check(lib().merlin_tower_relu_bwd(ptr(y), ptr(dy), ptr(dz), rows, cols, T, ptr(db), stream_of(y)),
               "merlin_tower_relu_bwd")
     return dz, db
+
+
+def colsum(x):
+    """x f32[T, rows, cols] (rows may be strided, columns contiguous) -> f32[T, cols] column sums (fixed
+    order)."""
+    T, rows, cols = (int(v) for v in x.shape)
+    assert x.dtype == torch.float32 and x.stride(2) == 1 and x.is_cuda
+    out = torch.empty((T, cols), dtype=torch.float32, device=x.device)
+    with KernelTimer.span("k_colsum", T * rows * cols * 4):
+        check(lib().merlin_tower_colsum(C.c_void_p(x.data_ptr()), rows, cols, int(x.stride(1)), int(x.stride(0)), T,
+                                        ptr(out), stream_of(x)), "merlin_tower_colsum")
+    return out
 
 
 def head_bwd(h, dlogits, dvalue, w_actor, w_critic):

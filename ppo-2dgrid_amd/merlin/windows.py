@@ -343,14 +343,14 @@ class _WindowConv2(torch.autograd.Function):
 
 
 def _colsum(x):
-    """x [T, n, C] (rows may be strided) -> [T, C] column sums as a ones-row GEMM: torch's reduce
-    over dim 1 of these [2, ~6.5k, 64] shapes takes ~50 us, the GEMM a few."""
-    ones = x.new_ones((x.shape[0], 1, x.shape[1]))
-    return torch.bmm(ones, x).squeeze(1)
+    """x [T, n, C] (rows may be strided) -> [T, C] column sums (merlin_tower_colsum: one pass, fixed
+    order; torch's dim-1 reduce over these [2, ~6.5k, 64] shapes took ~50 us, a ones-row GEMM ~32)."""
+    return nat.colsum(x)
 
 
 class _BiasRelu(torch.autograd.Function):
-    """relu(Z + b[:, None]) for Z [T, n, C], b [T, C]; backward's bias gradient by _colsum."""
+    """relu(Z + b[:, None]) for Z [T, n, C], b [T, C]; backward: the ReLU mask and the bias gradient in
+    one HIP pass (merlin_tower_relu_bwd)."""
 
     @staticmethod
     def forward(ctx, Z, b):
@@ -361,8 +361,7 @@ class _BiasRelu(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dA):
         (A,) = ctx.saved_tensors
-        dZ = torch.where(A > 0, dA, torch.zeros((), dtype=dA.dtype, device=dA.device))
-        return dZ, _colsum(dZ)
+        return nat.relu_bwd(A, dA.contiguous())
 
 
 class _TunedBmm(torch.autograd.Function):

@@ -45,3 +45,17 @@ def test_head_bwd_matches_autograd(device, n, A):
     torch.testing.assert_close(dWa, Wa.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(dWc.view(1, H), Wc.grad, rtol=1e-4, atol=1e-3)
     assert torch.equal(dWa, nat.head_bwd(h.detach(), gl, gv, Wa.detach(), Wc.detach())[2])
+
+
+@pytest.mark.parametrize("rows", [0, 1, 777, 6634])
+def test_colsum_strided_rows(device, rows):
+    """merlin_tower_colsum over strided rows (the conv3 bias gradient reads tap 0 of dQ [T, nw, 9, 64])
+    against a float64 sum; fixed order: bitwise reproducible."""
+    from merlin import _native as nat
+
+    torch.manual_seed(rows)
+    dQ = torch.randn(2, rows, 9, 64, device=device)
+    x = dQ[:, :, 0]
+    out = nat.colsum(x)
+    torch.testing.assert_close(out.double(), x.double().sum(1), rtol=1e-5, atol=1e-5)
+    assert torch.equal(out, nat.colsum(x))
