@@ -251,29 +251,30 @@ def cpu_baseline():
 # PMC summary keeps its largest-grid launches, which are the dQ ones (2048 blocks vs ~90).  The
 # fc1 GEMMs are hipBLASLt kernels, matched by name prefix (largest grid = the update's, not the
 # rollout's); their PMC key is the full Tensile kernel name.
-PMC_ALIAS = {"k_seg_sum_dQ": "k_seg_sum"}
-PMC_PREFIX = {"gemm_fc1_fwd": "void merlin::(anonymous namespace)::k_x6_nt<256, 128, 4, 2, 1>",
-              "gemm_fc1_dgrad": "void merlin::(anonymous namespace)::k_x6_nt<128, 192, 2, 4, 0>",
-              "gemm_wgrad": "void merlin::(anonymous namespace)::k_x6_tn<128, 192, 2, 4>"}
+PMC_ALIAS = {"k_seg_sum_dQ": "k_seg_sum",
+             # fc1's x6 GEMMs (untruncated rocprofv3 names keep the template arguments); the weight
+             # gradient's span covers the split-K kernel and its slab fold
+             "gemm_fc1_fwd": ("k_x6_nt<256, 128, 4, 2, 1, true>",),
+             "gemm_fc1_dgrad": ("k_x6_nt<128, 192, 2, 4, 0, true>",),
+             "gemm_wgrad": ("k_x6_tn<128, 192, 2, 4>", "k_x6_fold")}
 PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 
 
 def pmc_traffic(kernel: str):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 --pmc passes of the same bench
-    command (profiles/*_pmc.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE)."""
-    kernel = PMC_ALIAS.get(kernel, kernel)
+    command (profiles/*_pmc.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE);
+    a span made of several kernels (PMC_ALIAS tuple) adds theirs."""
+    names = PMC_ALIAS.get(kernel, kernel)
+    names = names if isinstance(names, tuple) else (names,)
     files = [PMC_FILE] if PMC_FILE else sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True)
     for f in files:
         try:
             dd = json.load(open(f))
         except Exception:
             continue
-        d = dd.get(kernel)
-        if d is None and kernel in PMC_PREFIX:
-            cands = [v for k, v in dd.items() if k.startswith(PMC_PREFIX[kernel])]
-            d = max(cands, key=lambda v: v.get("grid", 0)) if cands else None
-        if d and d.get("hbm_bytes_per_launch"):
-            return d["hbm_bytes_per_launch"]
+        got = [dd.get(n, {}).get("hbm_bytes_per_launch") for n in names]
+        if all(got):
+            return int(sum(got))
     return None
 
 

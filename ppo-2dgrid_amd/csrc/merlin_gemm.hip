@@ -288,7 +288,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const u32x4 *img, int col0, int lane) 
 template <int BM, int BN, int WGM, int WGN>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restrict__ A, const float4 *__restrict__ B,
                                                           int64_t Kd, int M, int N, int64_t sA, int64_t sB, int64_t kc,
-                                                          int tiles_n, float *__restrict__ slab) {
+                                                          int tiles_n, int tiles, int S, float *__restrict__ slab) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int FM = WTM / 16, FN = WTN / 16;
@@ -300,8 +300,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restri
     constexpr int STAGE = 3 * (PSA + PSB);
     __shared__ u32x4 lds[2 * STAGE];
 
-    const int t = blockIdx.z, s = blockIdx.y;
-    const int L = xcd_tile(blockIdx.x, gridDim.x);
+    // 1-D grid over (tower, split, tile), tile fastest, XCD-contiguous (xcd_tile): the tiles of one
+    // split read the same k rows of both operands, so they run together on one L2
+    const int P = xcd_tile(blockIdx.x, gridDim.x);
+    const int t = P / (S * tiles), s = (P / tiles) % S, L = P % tiles;
     const int tm = L / tiles_n, tn = L - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int64_t k0 = (int64_t)s * kc, k1 = std::min<int64_t>(Kd, k0 + kc);
@@ -420,7 +422,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restri
         __syncthreads();
     }
 
-    float *St = slab + ((int64_t)s * gridDim.z + t) * (int64_t)M * N;
+    float *St = slab + ((int64_t)s * (gridDim.x / (S * tiles)) + t) * (int64_t)M * N;
     const int fr = lane & 15;
 #pragma unroll
     for (int i = 0; i < FM; i++)
@@ -475,8 +477,8 @@ hipError_t tn_launch(const float4 *A, const float4 *B, int64_t Kd, int M, int N,
     int64_t kc = (Kd + S - 1) / S;
     kc = (kc + BK - 1) / BK * BK;
     S = (int)std::max<int64_t>(1, (Kd + kc - 1) / kc);
-    hipLaunchKernelGGL((k_x6_tn<BM, BN, WGM, WGN>), dim3(tiles, S, T), dim3(64 * WGM * WGN), 0, s, A, B, Kd, M, N, sA,
-                       sB, kc, tiles_n, slab);
+    hipLaunchKernelGGL((k_x6_tn<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s, A, B, Kd, M, N,
+                       sA, sB, kc, tiles_n, tiles, S, slab);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int64_t total4 = (int64_t)T * M * N / 4;

@@ -9,7 +9,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$R/gpurun_out/p
 tail -c 600 "$R/gpurun_out/prof_trace.log"
 if [ -n "$PMC" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "${PMC_RE:-k_}" -T -f csv \
+    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "${PMC_RE:-k_}" -f csv \
         -d "$R/gpurun_out/prof_pmc_$C" -o run -- python "$R/bench.py" $ARGS \
         > "$R/gpurun_out/prof_pmc_$C.log" 2>&1 || exit $?
     echo "pmc $C done"

@@ -7,6 +7,7 @@ its largest-grid launches, HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx
 FETCH_SIZE counts half of a wide coalesced read stream, MI355X_MICROARCH.md §HBM).
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -54,8 +55,13 @@ def pmc(tag):
 def collect(res, src, counter, rename):
     per = {}
     for r in csv.DictReader(open(src)):
-        name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").strip()
-        name = name.split("::")[-1]
+        raw = r["Kernel_Name"]
+        m = re.search(r"::(k_\w+(?:<[^>]*>)?)\(", raw)  # untruncated merlin kernel: keep template args
+        if m:
+            name = m.group(1)
+        else:
+            name = raw.split("(")[0].split("<")[0].replace("void ", "").strip()
+            name = name.split("::")[-1]
         name = rename.get(name, name)
         per.setdefault(name, []).append((int(r["Grid_Size"]), float(r["Counter_Value"])))
     for k, vals in per.items():
