@@ -426,6 +426,22 @@ def _conv3_backward(plan, mb, bits, dY3, nw):
     return dQ.view(T, nw, 576), db3
 
 
+# fc1's weight gradient on a side stream, overlapped with conv3's backward segmented sums (joined
+# before the Function returns: delivering it to the parameters only at the end of the backward pass,
+# so it also overlaps the window GEMMs / conv tables, measured slower: 2.56M against 2.74M env-steps/s)
+OVERLAP_WGRAD = True
+_SIDE = {}
+
+
+def _side_stream(device):
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    st = _SIDE.get(device)
+    if st is None:
+        st = _SIDE[device] = torch.cuda.Stream(device=device)
+    return st
+
+
 class _WindowTowerHeadX6(torch.autograd.Function):
     """conv3 -> fc1 -> ReLU -> heads of both towers for the minibatch's distinct frames, with fc1's
     three GEMMs on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip):
@@ -460,10 +476,25 @@ class _WindowTowerHeadX6(torch.autograd.Function):
         dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
         W4tp = nat.x6_split(W4p.detach().transpose(1, 2).contiguous())
         da3 = nat.x6_gemm_nt(dz, W4tp, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
-        dW4p = nat.x6_gemm_tn(dz, a3, name="gemm_wgrad")
+        side = _side_stream(dz.device) if OVERLAP_WGRAD else None
+        if side is None:
+            dW4p = nat.x6_gemm_tn(dz, a3, name="gemm_wgrad")
+        else:
+            # the weight gradient (matrix-core bound, one 120-KB-LDS block per CU) on a second stream,
+            # beside conv3's memory-bound patch / band / window sums on this one (no LDS: their waves
+            # fit next to the GEMM's on each CU); joined before the gradients are handed back
+            main = torch.cuda.current_stream(dz.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                dW4p = nat.x6_gemm_tn(dz, a3, name="gemm_wgrad")
+            dz.record_stream(side)
+            a3.record_stream(side)
+            dW4p.record_stream(main)
         dQ, db3 = _conv3_backward(ctx.plan, ctx.mb, bits, da3.view(2, n * 9, 64), ctx.nw_q)
         dba = dlogits.sum(0) if ctx.head_bias[0] else None
         dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
+        if side is not None:
+            torch.cuda.current_stream(dz.device).wait_stream(side)
         return dQ, db3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc, None, None
 
 def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = None) -> torch.Tensor:
