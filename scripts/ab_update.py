@@ -1,10 +1,12 @@
 """In-process A/B of update-path switches at the bench workload (4096 envs x 256 steps, 10 x 8
-minibatches): one agent, warmed up, then the settings alternate iteration by iteration (ABAB...),
-so device-to-device and clock differences between gpurun boxes do not enter the comparison.
+minibatches): one agent warmed up to the bench's state, one rollout, then the SAME update (same
+weights, optimizer state and minibatch permutations, restored before every run) timed under each
+setting in turn, repeatedly -- device-to-device and clock differences between gpurun boxes and the
+training state's drift do not enter the comparison.
 
-    python scripts/ab_update.py [iters_per_setting]
+    python scripts/ab_update.py [repeats] [warmup] [x6_overlap,no_overlap,hipblaslt]
 
-Prints ms per iteration (rollout + update) for each setting."""
+Prints ms per update for each setting."""
 import os
 import sys
 import time
@@ -18,13 +20,29 @@ from merlin.ppo import PPO
 
 
 def main():
-    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    import copy
+
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    warm = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     dev = torch.device("cuda", 0)
     env = MerlinVecEnv(4096, "mediumhard", seed=777, device=dev)
     torch.manual_seed(777)
     agent = PPO(env, batch_size=4096 * 256, minibatch_size=4096 * 256 // 8, ent_coef=0.05, device=dev)
-    for _ in range(3):
+    for _ in range(warm):
         agent.update(agent.collect_rollouts())
+    lv = agent.collect_rollouts()
+    perms = {}
+
+    def fixed_perm(n, epoch):
+        if epoch not in perms:
+            g = torch.Generator(device=dev)
+            g.manual_seed(1000 + epoch)
+            perms[epoch] = torch.randperm(n, device=dev, generator=g)
+        return perms[epoch]
+
+    agent.perm_fn = fixed_perm
+    sd = copy.deepcopy(agent.ac.state_dict())
+    opt = copy.deepcopy(agent.optimizer.state_dict())
 
     def setter(name):
         def s():
@@ -32,19 +50,22 @@ def main():
             agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6"
         return s
 
-    settings = {n: setter(n) for n in ("x6_overlap", "no_overlap", "hipblaslt")}
+    names = sys.argv[3].split(",") if len(sys.argv) > 3 else ["x6_overlap", "no_overlap", "hipblaslt"]
+    settings = {n: setter(n) for n in names}
     times = {n: [] for n in settings}
     for _ in range(iters):
         for n, s in settings.items():
             s()
+            agent.ac.load_state_dict(sd)
+            agent.optimizer.load_state_dict(opt)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            agent.update(agent.collect_rollouts())
+            agent.update(lv)
             torch.cuda.synchronize()
             times[n].append((time.perf_counter() - t0) * 1e3)
     for n, t in times.items():
         t = sorted(t)
-        print(f"{n:12s} median {t[len(t) // 2]:.1f} ms/iter  min {t[0]:.1f}  all {[round(x, 1) for x in times[n]]}")
+        print(f"{n:12s} median {t[len(t) // 2]:.1f} ms/update  min {t[0]:.1f}  all {[round(x, 1) for x in times[n]]}")
     print("distinct frames per sample", agent.last_distinct_frac)
 
 
