@@ -221,6 +221,38 @@ def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=1
                             "us_per_step": round(sec_reset / T * 1e6, 2), "resets": resets}}
 
 
+def x6_standalone(torch, U, device, reps=10):
+    """fc1's three x6 GEMMs timed alone (HIP events, no other stream active) at the update's shape
+    (U distinct frames per minibatch): in the timed loop the weight gradient shares the chip with
+    conv3's backward sums on the other stream, so its in-loop event time includes that sharing."""
+    from merlin import _native as nat
+
+    g = torch.Generator(device=device).manual_seed(0)
+    a3 = torch.relu(torch.randn(2, U, 576, device=device, generator=g))
+    dz = torch.randn(2, U, 512, device=device, generator=g)
+    Wp = nat.x6_split(torch.randn(2, 512, 576, device=device, generator=g) / 24)
+    Wtp = nat.x6_split(torch.randn(2, 576, 512, device=device, generator=g) / 24)
+    b = torch.zeros(2, 512, device=device)
+    runs = {"gemm_fc1_fwd": lambda: nat.x6_gemm_nt(a3, Wp, bias=b, cfg=nat.X6_NT_CFG["fwd"]),
+            "gemm_fc1_dgrad": lambda: nat.x6_gemm_nt(dz, Wtp, cfg=nat.X6_NT_CFG["dgrad"]),
+            "gemm_wgrad": lambda: nat.x6_gemm_tn(dz, a3)}
+    out = {}
+    for name, fn in runs.items():
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / reps * 1e3
+        ex = X6_PRODUCTS * 2 * 2 * U * 576 * 512 / (us * 1e-6) / 1e12
+        out[name] = {"avg_launch_us": round(us, 2), "achieved": round(ex, 2), "peak": BF16_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(ex / BF16_PEAK_TFLOPS, 4),
+                     "fp32_equivalent_tflops": round(ex / X6_PRODUCTS, 2)}
+    return {"rows": U, "kernels": out}
+
+
 def cpu_baseline():
     """The oracle's CPU port of the reference loop (oracle/ppo_cpu.py), N=1 env, batch 2048, 10 epochs x
     8 minibatches of 256, plus the per-iteration 3-episode deterministic eval of ppo/ppo_train.py:150
@@ -478,7 +510,10 @@ def main():
                                        if agent.last_distinct_frac is not None else None),
         # dominant kernel of the timed loop by total HIP-event time (hand-written kernels and the
         # fc1 hipBLASLt GEMMs, which are timed the same way)
-        "roofline": roofline_of(dominant, kernels[dominant], x6),
+        "roofline": dict(roofline_of(dominant, kernels[dominant], x6),
+                         **({"note": "in the loop the weight gradient runs on a side stream beside conv3's "
+                                     "backward segmented sums, so its event time includes that sharing; "
+                                     "alone: roofline_x6_standalone"} if dominant == "gemm_wgrad" and x6 else {})),
         # dominant hand-written kernel
         "roofline_handwritten": dict(roofline_of(handwritten, kernels[handwritten]),
                                      **gather_note(handwritten, kernels[handwritten])),
@@ -502,6 +537,10 @@ def main():
         "rollout_graph": agent._graph is not None,
         "kernels": kernels,
     }
+    if x6 and agent.last_distinct_frac is not None:
+        # the x6 GEMMs alone at the update's shape (distinct frames per minibatch)
+        U = int(round(agent.last_distinct_frac * (B // args.minibatches)))
+        out["roofline_x6_standalone"] = x6_standalone(torch, U, device)
     state["phase"] = "tiers"
     if not args.no_tiers:
         floors = floor_tier(agent)
