@@ -640,7 +640,7 @@ def act_heads(z, b4, w_actor, b_actor, w_critic, b_critic, deterministic=False, 
 # -- fc1 on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip) ------------------
 # Weights as int16 planes [..., R, 3 * C] (bf16 bits; per group of 8 values three 16-B chunks,
 # x = x0 + x1 + x2 exactly, include/merlin_hip.h); activations as fp32, split while staged.
-X6_NT_CFG = {"fwd": 0, "dgrad": 1}  # tile configurations of merlin_x6_gemm_nt (N = 512 / 576), scripts/probe_x6.py
+X6_NT_CFG = {"fwd": 0, "dgrad": 1, "rollout": 2}  # tile configurations of merlin_x6_gemm_nt (N = 512 / 576), scripts/probe_x6.py
 X6_TN_CFG = 0
 X6_TN_SPLITS = 32
 

@@ -493,12 +493,17 @@ class CNNActorCritic(nn.Module):
         Z2 = nat.window_lut(self._all_window_rows(T2.device), T2)  # [2, 5**9, 64]
         a2 = torch.relu_(Z2.add_(torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1)))
         W3r = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 2, 3, 4, 1).reshape(2, 64, 576)
-        return {
+        W4p = W4.view(2, H, 64, 9).transpose(2, 3).reshape(2, H, 576)
+        pack = {
             "Qall": torch.bmm(a2, W3r),  # [2, windows, (ky, kx, co)]
             "b3": torch.stack([ea[4].bias, ec[4].bias]).contiguous(),
-            "W4t": W4.view(2, H, 64, 9).transpose(2, 3).reshape(2, H, 576).transpose(1, 2).contiguous(),
             "b4": torch.stack([fa.bias, fc.bias]).contiguous(),
         }
+        if self.fc1_impl == "x6":  # fc1 of every step on the bf16 MFMA, fp32 products (merlin_gemm.hip)
+            pack["W4pp"] = nat.x6_split(W4p.contiguous())
+        else:
+            pack["W4t"] = W4p.transpose(1, 2).contiguous()
+        return pack
 
     @torch.no_grad()
     def act_codes_packed(self, codes, pack, deterministic=False, seed=0, epoch=None, step=0, out=None, env_offset=0):
@@ -512,8 +517,11 @@ class CNNActorCritic(nn.Module):
 
         n = codes.shape[0]
         a3 = nat.codes_conv3(codes, pack["Qall"], pack["b3"]).view(2, n, 576)
-        with tuned("rollout"):
-            z = torch.bmm(a3, pack["W4t"])
+        if "W4pp" in pack:
+            z = nat.x6_gemm_nt(a3, pack["W4pp"], cfg=nat.X6_NT_CFG["rollout"], name="gemm_rollout_fc1")
+        else:
+            with tuned("rollout"):
+                z = torch.bmm(a3, pack["W4t"])
         return nat.act_heads(z, pack["b4"], self.actor[2].weight, self.actor[2].bias, self.critic[2].weight,
                              self.critic[2].bias, deterministic, seed=seed, epoch=epoch, step=step, out=out,
                              env_offset=env_offset)
