@@ -454,7 +454,7 @@ class _WindowTowerHeadX6(torch.autograd.Function):
     fp32 products throughout (the activations are split into planes inside the GEMMs)."""
 
     @staticmethod
-    def forward(ctx, Q, b3, W4p, b4, Wa, ba, Wc, bc, plan, mb):
+    def forward(ctx, Q, b3, W4p, b4, Wa, ba, Wc, bc, plan, mb, fc1_weights=None):
         Y3, bits = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous(), bits=True)
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
@@ -465,6 +465,7 @@ class _WindowTowerHeadX6(torch.autograd.Function):
         ctx.save_for_backward(a3, bits, W4p, h, Wa, Wc)
         ctx.head_bias = (ba is not None, bc is not None)
         ctx.plan, ctx.mb, ctx.nw_q = plan, mb, Q.shape[1]
+        ctx.fc1_weights = fc1_weights  # (actor, critic) fc1 weights W4p was stacked from (deferred mode)
         return logits, value
 
     @staticmethod
@@ -493,9 +494,26 @@ class _WindowTowerHeadX6(torch.autograd.Function):
         dQ, db3 = _conv3_backward(ctx.plan, ctx.mb, bits, da3.view(2, n * 9, 64), ctx.nw_q)
         dba = dlogits.sum(0) if ctx.head_bias[0] else None
         dbc = dvalue.sum(0, keepdim=True) if ctx.head_bias[1] else None
-        if side is not None:
+        if side is not None and OVERLAP_WGRAD == "deferred" and ctx.fc1_weights is not None:
+            # deliver fc1's weight gradient only at the end of the backward pass (autograd-engine
+            # callback), so the side stream also runs beside the window GEMMs and the conv tables
+            weights, H = ctx.fc1_weights, dW4p.shape[1]
+            g = dW4p
+
+            def finish():
+                torch.cuda.current_stream(g.device).wait_stream(side)
+                dW4 = g.view(2, H, 9, 64).transpose(2, 3).reshape(2, H, 576)  # (p3, co) -> (co, p3)
+                for t, w in enumerate(weights):
+                    if w.grad is None:
+                        w.grad = dW4[t].contiguous()
+                    else:
+                        w.grad.add_(dW4[t])
+
+            torch.autograd.Variable._execution_engine.queue_callback(finish)
+            dW4p = None
+        elif side is not None:
             torch.cuda.current_stream(dz.device).wait_stream(side)
-        return dQ, db3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc, None, None
+        return dQ, db3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc, None, None, None
 
 def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = None) -> torch.Tensor:
     """relu(conv3(relu(conv2(relu(conv1(frame)))))) of both towers of CNNActorCritic `ac` for the
@@ -526,4 +544,5 @@ def window_tower_head_x6(ac, plan: WindowPlan, mb: MinibatchWindows, head_bias: 
     W4p = W4.view(2, W4.shape[1], 64, 9).transpose(2, 3).reshape(2, W4.shape[1], 576)
     ba, bc = (ac.actor[2].bias, ac.critic[2].bias) if head_bias else (None, None)
     return _WindowTowerHeadX6.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), W4p, torch.stack([fa.bias, fc.bias]),
-                                    ac.actor[2].weight, ba, ac.critic[2].weight, bc, plan, mb)
+                                    ac.actor[2].weight, ba, ac.critic[2].weight, bc, plan, mb,
+                                    (fa.weight, fc.weight))

@@ -46,7 +46,7 @@ def main():
 
     def setter(name):
         def s():
-            W.OVERLAP_WGRAD = name != "no_overlap"
+            W.OVERLAP_WGRAD = {"no_overlap": False, "deferred": "deferred"}.get(name, True)
             agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6"
         return s
 
