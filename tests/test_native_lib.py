@@ -93,3 +93,20 @@ def test_env_config_binding_matches_the_c_struct():
     block = doc[doc.index("class MerlinEnvConfig"):]
     block = block[:block.index("]")]
     assert re.findall(r'\("(\w+)"', block) == [f for f, _ in nat.EnvConfig._fields_]
+
+
+def test_x6_gemm_argument_checks():
+    """fc1's x6 GEMM entry points reject bad shapes on the host (no device work is queued)."""
+    from merlin import _native as nat
+
+    L = nat.lib()
+    # K not a multiple of 32
+    assert L.merlin_x6_gemm_nt(None, None, 0, 512, 33, 2, 0, 0, None, None, 0, 0, None) == 4
+    # null operands with rows to do
+    assert L.merlin_x6_gemm_nt(None, None, 10, 512, 576, 2, 0, 0, None, None, 0, 0, None) == 1
+    assert L.merlin_x6_gemm_tn(None, None, 10, 512, 576, 2, 0, 0, 32, None, None, 0, None) == 1
+    # planes need groups of 8 values
+    assert L.merlin_x6_split(None, 7, None, None) == 1
+    assert L.merlin_x6_tn_slab_floats(512, 576, 2, 32) == 32 * 2 * 512 * 576
+    # colsum: rows of 4 x a divisor of 256 floats only
+    assert L.merlin_tower_colsum(None, 0, 7, 7, 0, 1, None, None) == 1
