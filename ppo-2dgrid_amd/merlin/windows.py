@@ -426,10 +426,12 @@ def _conv3_backward(plan, mb, bits, dY3, nw):
     return dQ.view(T, nw, 576), db3
 
 
-# fc1's weight gradient on a side stream, overlapped with conv3's backward segmented sums (joined
-# before the Function returns: delivering it to the parameters only at the end of the backward pass,
-# so it also overlaps the window GEMMs / conv tables, measured slower: 2.56M against 2.74M env-steps/s)
-OVERLAP_WGRAD = True
+# fc1's weight gradient on a side stream, overlapped with conv3's backward segmented sums: True =
+# joined before the window Function returns; "deferred" = delivered to the fc1 weights only at the
+# end of the backward pass (autograd-engine callback), so it also overlaps the window GEMMs and the
+# conv tables.  scripts/ab_update.py, one update replayed per setting: 300.6 (off) / 297.0 (True) /
+# 293.4 (deferred) ms per update.
+OVERLAP_WGRAD = "deferred"
 _SIDE = {}
 
 
