@@ -400,6 +400,19 @@ int merlin_x6_gemm_tn(const float *A_dev, const float *B_dev, int64_t Kd, int32_
                       int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev, float *out_dev, int32_t cfg,
                       void *stream);
 
+/* Optimizer step of PPO.update (src/ppo.py:153-156: clip_grad_norm_(params, max_norm) then
+ * Adam.step(), replacing torch.nn.utils.clip_grad_norm_ + torch.optim.Adam(fused=True).step()) over
+ * n_tensors (1..32) float32 parameter tensors, csrc/merlin_optim.hip.  params / grads / exp_avg /
+ * exp_avg_sq / steps are host arrays of device pointers (steps: each tensor's Adam step counter,
+ * float32[1], advanced by one), numel[i] > 0.  The gradients are scaled in place by
+ * min(max_norm / (||g||_2 + 1e-6), 1) as clip_grad_norm_ does; norm_out (float32[1], NULL: not
+ * written) gets ||g||_2 before clipping.  Adam: torch's fused arithmetic (no weight decay, amsgrad
+ * or maximize).  workspace double[merlin_clip_adam_workspace(n_tensors, numel)]. */
+int64_t merlin_clip_adam_workspace(int32_t n_tensors, const int64_t *numel);
+int merlin_clip_adam(int32_t n_tensors, float *const *params, float *const *grads, float *const *exp_avg,
+                     float *const *exp_avg_sq, float *const *steps, const int64_t *numel, double lr, double beta1,
+                     double beta2, double eps, float max_norm, float *norm_out, double *workspace, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -795,4 +795,29 @@ int merlin_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int32_t M, int
     return MERLIN_OK;
 }
 
+int64_t merlin_clip_adam_workspace(int32_t n_tensors, const int64_t *numel) {
+    if (n_tensors < 0 || n_tensors > merlin::OPT_MAX_TENSORS || (n_tensors > 0 && !numel)) return -1;
+    return std::max<int64_t>(1, merlin::opt_blocks(n_tensors, numel));
+}
+
+int merlin_clip_adam(int32_t n_tensors, float *const *params, float *const *grads, float *const *exp_avg,
+                     float *const *exp_avg_sq, float *const *steps, const int64_t *numel, double lr, double beta1,
+                     double beta2, double eps, float max_norm, float *norm_out, double *workspace, void *stream) {
+    if (n_tensors < 1 || n_tensors > merlin::OPT_MAX_TENSORS)
+        return fail(MERLIN_E_INVALID, "n_tensors must be in [1, 32]");
+    if (!params || !grads || !exp_avg || !exp_avg_sq || !steps || !numel || !workspace)
+        return fail(MERLIN_E_INVALID, "null argument");
+    int64_t blocks = 0;
+    for (int i = 0; i < n_tensors; i++) {
+        if (numel[i] <= 0) return fail(MERLIN_E_INVALID, "every tensor needs numel > 0");
+        if (!params[i] || !grads[i] || !exp_avg[i] || !exp_avg_sq[i] || !steps[i])
+            return fail(MERLIN_E_INVALID, "null tensor pointer");
+    }
+    blocks = merlin::opt_blocks(n_tensors, numel);
+    if (blocks > INT32_MAX / 2) return fail(MERLIN_E_INVALID, "too many elements");
+    HIP_TRY(merlin::launch_clip_adam(n_tensors, params, grads, exp_avg, exp_avg_sq, steps, numel, lr, beta1, beta2, eps,
+                                     max_norm, norm_out, workspace, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
 }  // extern "C"

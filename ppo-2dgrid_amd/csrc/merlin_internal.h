@@ -148,4 +148,11 @@ hipError_t launch_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int M, 
                              int64_t b_stride, int splits, float *slab, float *out, int cfg, hipStream_t s);
 int x6_tn_max_splits();
 
+// clip_grad_norm_ + Adam step over a parameter list (merlin_optim.hip)
+constexpr int OPT_MAX_TENSORS = 32;
+int64_t opt_blocks(int n, const int64_t *numel);
+hipError_t launch_clip_adam(int n, float *const *params, float *const *grads, float *const *exp_avg,
+                            float *const *exp_avg_sq, float *const *steps, const int64_t *numel, double lr, double beta1,
+                            double beta2, double eps, float max_norm, float *norm_out, double *partial, hipStream_t s);
+
 }  // namespace merlin

@@ -104,6 +104,10 @@ def lib():
                                    vp]
     L.merlin_ppo_loss_workspace.argtypes = [i64]
     L.merlin_ppo_loss_workspace.restype = i64
+    L.merlin_clip_adam_workspace.argtypes = [i32, vp]
+    L.merlin_clip_adam_workspace.restype = i64
+    L.merlin_clip_adam.argtypes = [i32, vp, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double, C.c_double, C.c_float,
+                                   vp, vp, vp]
     L.merlin_ppo_loss.argtypes = [vp, vp, vp, vp, i64, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp, C.c_double,
                                   C.c_double, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]
     L.merlin_x6_split.argtypes = [vp, i64, vp, vp]
@@ -151,6 +155,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_colsum",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
+    "merlin_clip_adam_workspace", "merlin_clip_adam",
 )
 
 
@@ -699,3 +704,31 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int = X6_TN_SPLITS, cfg
         check(lib().merlin_x6_gemm_tn(ptr(A), ptr(B), Kd, M, N, T, Kd * M, Kd * N, int(splits), ptr(slab), ptr(out),
                                       int(cfg), stream_of(A)), "merlin_x6_gemm_tn")
     return out
+
+
+def clip_adam(params, grads, exp_avgs, exp_avg_sqs, steps, lr, beta1, beta2, eps, max_norm, norm_out=None,
+              workspace=None):
+    """clip_grad_norm_(params, max_norm) + torch's fused Adam step (src/ppo.py:153-156) in two
+    launches (merlin_clip_adam): the gradients are clipped in place, (param, exp_avg, exp_avg_sq)
+    updated, each float32[1] step counter advanced.  Returns the pre-clip global norm (norm_out)."""
+    n = len(params)
+    if not (len(grads) == len(exp_avgs) == len(exp_avg_sqs) == len(steps) == n):
+        raise ValueError("clip_adam: parameter / state lists differ in length")
+    for group in (params, grads, exp_avgs, exp_avg_sqs, steps):
+        for t in group:
+            if t.dtype != torch.float32:
+                raise MerlinNativeError("clip_adam: float32 tensors only")
+    for p, g, m, v in zip(params, grads, exp_avgs, exp_avg_sqs):
+        if not (p.numel() == g.numel() == m.numel() == v.numel()):
+            raise ValueError("clip_adam: a parameter and its gradient / state differ in size")
+    numel = (C.c_int64 * n)(*[int(p.numel()) for p in params])
+    arr = lambda ts: (C.c_void_p * n)(*[ptr(t).value for t in ts])  # noqa: E731
+    dev = params[0].device
+    if workspace is None:
+        workspace = torch.empty(int(lib().merlin_clip_adam_workspace(n, numel)), dtype=torch.float64, device=dev)
+    if norm_out is None:
+        norm_out = torch.empty((), dtype=torch.float32, device=dev)
+    check(lib().merlin_clip_adam(n, arr(params), arr(grads), arr(exp_avgs), arr(exp_avg_sqs), arr(steps), numel,
+                                 float(lr), float(beta1), float(beta2), float(eps), float(max_norm), ptr(norm_out),
+                                 ptr(workspace), stream_of(params[0])), "merlin_clip_adam")
+    return norm_out

@@ -142,6 +142,12 @@ class PPO:
         self.optimizer = optim.Adam(self.ac.parameters(), lr=lr, fused=True)
         self.dp.attach(self.ac)
         self._params = [p for p in self.ac.parameters() if p.requires_grad]
+        # clip_grad_norm_(0.5) + Adam.step() as two HIP launches on the device (merlin/optim.py)
+        self._clip_adam = None
+        if self.device.type == "cuda":
+            from .optim import ClipAdam
+
+            self._clip_adam = ClipAdam(self.optimizer, 0.5)
 
     # ------------------------------------------------------------------ helpers
     def _obs_to_tensor(self, state):
@@ -361,8 +367,11 @@ class PPO:
                 self.dp.zero_grad(self.optimizer)
                 loss.backward()
                 self.dp.allreduce_grads()
-                grad_norm = torch.nn.utils.clip_grad_norm_(self._params, 0.5)
-                self.optimizer.step()
+                if self._clip_adam is not None:
+                    grad_norm = self._clip_adam.step()
+                else:
+                    grad_norm = torch.nn.utils.clip_grad_norm_(self._params, 0.5)
+                    self.optimizer.step()
                 totals[5:].add_(grad_norm.detach())
                 nb += 1
         t = totals.cpu().tolist()
