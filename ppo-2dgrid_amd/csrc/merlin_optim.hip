@@ -17,7 +17,7 @@ namespace merlin {
 namespace {
 
 constexpr int OPT_BLK = 256;
-constexpr int OPT_PER_THREAD = 16;
+constexpr int OPT_PER_THREAD = 4;  // ~730 blocks for the 745k parameters: fills the chip
 constexpr int OPT_CHUNK = OPT_BLK * OPT_PER_THREAD;
 
 struct OptList {
@@ -93,19 +93,33 @@ __global__ __launch_bounds__(OPT_BLK) void k_opt_adam(OptList L, const double *p
     const float bc1 = (float)(1.0 - pow(beta1, stepc));
     const float bc2_sqrt = (float)sqrt(1.0 - pow(beta2, stepc));
     const float step_size = (float)(lr / (double)bc1);
-    float *p = L.p[i], *g = L.g[i], *m = L.m[i], *v = L.v[i];
-#pragma unroll 4
+    float *__restrict__ p = L.p[i];
+    float *__restrict__ g = L.g[i];
+    float *__restrict__ m = L.m[i];
+    float *__restrict__ v = L.v[i];
+    float rg[OPT_PER_THREAD], rm[OPT_PER_THREAD], rv[OPT_PER_THREAD], rp[OPT_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < OPT_PER_THREAD; k++) {  // all loads in flight before the arithmetic
+        const int64_t e = base + k * OPT_BLK + threadIdx.x;
+        if (e < n) {
+            rg[k] = g[e];
+            rm[k] = m[e];
+            rv[k] = v[e];
+            rp[k] = p[e];
+        }
+    }
+#pragma unroll
     for (int k = 0; k < OPT_PER_THREAD; k++) {
         const int64_t e = base + k * OPT_BLK + threadIdx.x;
         if (e < n) {
-            const float gr = g[e] * coef;
+            const float gr = rg[k] * coef;
+            const float ma = (float)(beta1 * (double)rm[k] + (1.0 - beta1) * (double)gr);
+            const float va = (float)(beta2 * (double)rv[k] + (1.0 - beta2) * (double)gr * (double)gr);
+            const float denom = (float)((double)(sqrtf(va) / bc2_sqrt) + eps);
             g[e] = gr;
-            const float ma = (float)(beta1 * (double)m[e] + (1.0 - beta1) * (double)gr);
-            const float va = (float)(beta2 * (double)v[e] + (1.0 - beta2) * (double)gr * (double)gr);
             m[e] = ma;
             v[e] = va;
-            const float denom = (float)((double)(sqrtf(va) / bc2_sqrt) + eps);
-            p[e] = p[e] - step_size * ma / denom;
+            p[e] = rp[k] - step_size * ma / denom;
         }
     }
 }

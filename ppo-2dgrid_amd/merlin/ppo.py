@@ -30,6 +30,8 @@ instead of six .item() syncs per minibatch (ppo.py:158-163).
 """
 from __future__ import annotations
 
+import time
+
 import warnings
 
 import numpy as np
@@ -323,6 +325,7 @@ class PPO:
                 plan = WindowPlan(codes, groups)
                 self.last_num_windows = plan.num_windows
         distinct = 0
+        t_host = time.perf_counter()
         perms = [self._perm(B, epoch) for epoch in range(self.update_epochs)]  # drawn in epoch order
         # one host read per update for every minibatch's distinct-frame groups (merlin/windows.py)
         all_mbws = plan.update_minibatches(perms, self.minibatch_size) if plan is not None else None
@@ -374,6 +377,7 @@ class PPO:
                     self.optimizer.step()
                 totals[5:].add_(grad_norm.detach())
                 nb += 1
+        self.last_host_loop_ms = (time.perf_counter() - t_host) * 1e3  # host time to queue the update
         t = totals.cpu().tolist()
         if groups is not None:
             self.last_distinct_frac = float(distinct) / float(self.update_epochs * B)

@@ -44,10 +44,14 @@ def main():
     sd = copy.deepcopy(agent.ac.state_dict())
     opt = copy.deepcopy(agent.optimizer.state_dict())
 
+    clip_adam = agent._clip_adam
+    host = {}
+
     def setter(name):
         def s():
-            W.OVERLAP_WGRAD = {"no_overlap": False, "deferred": "deferred"}.get(name, True)
+            W.OVERLAP_WGRAD = {"no_overlap": False, "x6_overlap": True}.get(name, "deferred")
             agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6"
+            agent._clip_adam = None if name == "torch_opt" else clip_adam
         return s
 
     names = sys.argv[3].split(",") if len(sys.argv) > 3 else ["x6_overlap", "no_overlap", "hipblaslt"]
@@ -63,9 +67,12 @@ def main():
             agent.update(lv)
             torch.cuda.synchronize()
             times[n].append((time.perf_counter() - t0) * 1e3)
+            host.setdefault(n, []).append(agent.last_host_loop_ms)
     for n, t in times.items():
         t = sorted(t)
-        print(f"{n:12s} median {t[len(t) // 2]:.1f} ms/update  min {t[0]:.1f}  all {[round(x, 1) for x in times[n]]}")
+        h = sorted(host[n])
+        print(f"{n:12s} median {t[len(t) // 2]:.1f} ms/update  min {t[0]:.1f}  all {[round(x, 1) for x in times[n]]}"
+              f"  host queueing median {h[len(h) // 2]:.1f} ms")
     print("distinct frames per sample", agent.last_distinct_frac)
 
 

@@ -110,3 +110,24 @@ def test_x6_gemm_argument_checks():
     assert L.merlin_x6_tn_slab_floats(512, 576, 2, 32) == 32 * 2 * 512 * 576
     # colsum: rows of 4 x a divisor of 256 floats only
     assert L.merlin_tower_colsum(None, 0, 7, 7, 0, 1, None, None) == 1
+
+
+def test_clip_adam_argument_checks():
+    """merlin_clip_adam rejects bad tensor lists on the host (no device work is queued)."""
+    import ctypes as C
+
+    from merlin import _native as nat
+
+    L = nat.lib()
+    numel = (C.c_int64 * 3)(10, 4096, 5000)
+    assert L.merlin_clip_adam_workspace(3, numel) == 1 + 4 + 5  # 1024-element blocks per tensor
+    assert L.merlin_clip_adam_workspace(33, numel) == -1
+    assert L.merlin_clip_adam(0, None, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-8, 0.5, None, None, None) == 1
+    assert L.merlin_clip_adam(33, None, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-8, 0.5, None, None, None) == 1
+    nul = (C.c_void_p * 3)()
+    ws = (C.c_double * 4)()
+    # null tensor pointers
+    assert L.merlin_clip_adam(3, nul, nul, nul, nul, nul, numel, 1e-3, 0.9, 0.999, 1e-8, 0.5, None, ws, None) == 1
+    # an empty tensor
+    zero = (C.c_int64 * 3)(10, 0, 5)
+    assert L.merlin_clip_adam(3, nul, nul, nul, nul, nul, zero, 1e-3, 0.9, 0.999, 1e-8, 0.5, None, ws, None) == 1
