@@ -295,12 +295,28 @@ __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carr
         if (x.x < 0) continue;
         const float2 *ct = carry + (size_t)t * nitems * 64 + c2;
         float2 acc = ct[(size_t)x.y * 64 + x.w * 32];
-#pragma unroll 8
-        for (int j = x.y + 1; j <= x.z; j++) {
-            const float2 v = ct[(size_t)j * 64];
-            acc.x += v.x;
-            acc.y += v.y;
+        // a hot destination spans hundreds of items: four independent partial sums (items
+        // j0+1+4i+q go to partial q) keep 16 loads in flight instead of one dependent chain;
+        // the partials join in a fixed order, so the result stays bitwise reproducible
+        float2 a[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+        int j = x.y + 1;
+        for (; j + 15 <= x.z; j += 16) {
+            float2 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) v[u] = ct[(size_t)(j + u) * 64];
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                a[u & 3].x += v[u].x;
+                a[u & 3].y += v[u].y;
+            }
         }
+        for (int q = 0; j <= x.z; j++, q = (q + 1) & 3) {
+            const float2 v = ct[(size_t)j * 64];
+            a[q].x += v.x;
+            a[q].y += v.y;
+        }
+        acc.x += (a[0].x + a[1].x) + (a[2].x + a[3].x);
+        acc.y += (a[0].y + a[1].y) + (a[2].y + a[3].y);
         float2 *o = out + ((size_t)t * out_rows + x.x) * 32 + c2;
         if (acc_out) {
             const float2 p = *o;

@@ -68,9 +68,10 @@ def emulate_segment_sum(plan, src, out_rows, slot=None, sub=1, mask=None, fill=T
         if d < 0:
             continue
         a = carry[:, j0, s0].clone()
-        for j in range(j0 + 1, j1 + 1):
-            a += carry[:, j, 0]
-        out[:, d] = a
+        part = [torch.zeros_like(a) for _ in range(4)]  # k_seg_fix: item j0+1+i goes to partial i % 4
+        for i, j in enumerate(range(j0 + 1, j1 + 1)):
+            part[i % 4] += carry[:, j, 0]
+        out[:, d] = a + ((part[0] + part[1]) + (part[2] + part[3]))
     return out
 
 
