@@ -71,16 +71,20 @@ def test_fullsize_window_update_matches_lookup_path(device):
         agent.optimizer.load_state_dict(opt0)
         agent.windows = windows
         first = []
-        orig_step = agent.optimizer.step
+        # the first step's clipped gradient: merlin_clip_adam (merlin/optim.py) clips the
+        # gradients in place, as clip_grad_norm_ does, so they are read right after its step
+        ca = agent._clip_adam
+        orig_step = ca.step
 
-        def step(*a, **k):
+        def step():
+            r = orig_step()
             if not first:
                 first.append([p.grad.detach().clone() for p in agent._params])
-            return orig_step(*a, **k)
+            return r
 
-        agent.optimizer.step = step
+        ca.step = step
         stats = agent.update(lv)
-        agent.optimizer.step = orig_step
+        ca.step = orig_step
         results.append((stats, first[0], [p.detach().clone() for p in agent.ac.parameters()],
                         agent.last_num_windows if windows else None, agent.last_distinct_frac))
     (s1, g1, p1, nw, frac), (s2, g2, p2, _, _) = results
