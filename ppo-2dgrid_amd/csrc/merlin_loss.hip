@@ -169,11 +169,34 @@ __global__ __launch_bounds__(256) void k_ppo_loss_fix(const int32_t *__restrict_
     const float *c = carry + ((size_t)j0 * 2 + 1) * (MAXA + 1);
 #pragma unroll
     for (int j = 0; j <= MAXA; j++) acc[j] = c[j];
-    for (int64_t it = j0 + 1; it <= j1; it++) {
+    // a hot frame (thousands of samples) spans many items: two independent partial sums over
+    // alternate items keep twice the loads in flight; fixed join order (bitwise reproducible)
+    float acc2[MAXA + 1];
+#pragma unroll
+    for (int j = 0; j <= MAXA; j++) acc2[j] = 0.0f;
+    int64_t it = j0 + 1;
+    for (; it + 1 <= j1; it += 2) {
+        const float *c0 = carry + ((size_t)it * 2) * (MAXA + 1);
+        const float *c1 = carry + ((size_t)(it + 1) * 2) * (MAXA + 1);
+        float v0[MAXA + 1], v1[MAXA + 1];
+#pragma unroll
+        for (int j = 0; j <= MAXA; j++) {
+            v0[j] = c0[j];
+            v1[j] = c1[j];
+        }
+#pragma unroll
+        for (int j = 0; j <= MAXA; j++) {
+            acc[j] += v0[j];
+            acc2[j] += v1[j];
+        }
+    }
+    if (it <= j1) {
         c = carry + ((size_t)it * 2) * (MAXA + 1);
 #pragma unroll
         for (int j = 0; j <= MAXA; j++) acc[j] += c[j];
     }
+#pragma unroll
+    for (int j = 0; j <= MAXA; j++) acc[j] += acc2[j];
 #pragma unroll
     for (int j = 0; j < MAXA; j++)
         if (j < A) dlogits[u * A + j] = acc[j];

@@ -310,10 +310,15 @@ __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carr
                 a[u & 3].y += v[u].y;
             }
         }
-        for (int q = 0; j <= x.z; j++, q = (q + 1) & 3) {
-            const float2 v = ct[(size_t)j * 64];
-            a[q].x += v.x;
-            a[q].y += v.y;
+        for (; j <= x.z; j += 4) {  // static partial indices (a dynamic a[q] would live in scratch)
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (j + u <= x.z) {
+                    const float2 v = ct[(size_t)(j + u) * 64];
+                    a[u].x += v.x;
+                    a[u].y += v.y;
+                }
+            }
         }
         acc.x += (a[0].x + a[1].x) + (a[2].x + a[3].x);
         acc.y += (a[0].y + a[1].y) + (a[2].y + a[3].y);
