@@ -79,7 +79,9 @@ __global__ __launch_bounds__(OPT_BLK) void k_opt_adam(OptList L, const double *p
     if (threadIdx.x == 0) {
         const float norm = (float)sqrt(tot);
         float c = max_norm / (norm + 1e-6f);
-        coef_s = c < 1.0f ? c : 1.0f;
+        // torch.clamp(max=1) keeps a NaN coefficient (non-finite norm): every gradient and
+        // parameter then turns NaN, as with clip_grad_norm_, instead of a partly hidden step
+        coef_s = (c != c) ? c : (c < 1.0f ? c : 1.0f);
         if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
     }
     __syncthreads();

@@ -477,12 +477,22 @@ class CNNActorCritic(nn.Module):
             self._all_rows = window_rows(torch.arange(nat.ALL_WINDOWS, dtype=torch.int64, device=device)).contiguous()
         return self._all_rows
 
-    def rollout_pack(self):
+    # below this many frames per rollout the acting path looks conv2 up per frame instead of building
+    # the all-windows table (Qall: 9 GB and ~288 GFLOP per rollout, whatever the rollout's size)
+    ALL_WINDOWS_MIN_FRAMES = 1 << 18
+
+    def rollout_pack(self, frames: int | None = None):
         """The weights of the acting path in the layouts its kernels and GEMMs read, built once
-        per rollout (the weights do not change while acting): conv2 (from the conv1+conv2 tables)
-        and conv3's per-tap products for EVERY possible 3x3 tile window, Qall [2, 5**9, 576] (9 GB:
-        conv2 + ReLU of all 1,953,125 windows and one [5**9, 64] x [64, 576] GEMM per tower, a few
-        ms per rollout), fc1 with columns permuted to (p3, co) as [2, 576, H], biases stacked."""
+        per rollout (the weights do not change while acting).
+
+        Large rollouts (frames >= ALL_WINDOWS_MIN_FRAMES, or frames not given): conv2 (from the
+        conv1+conv2 tables) and conv3's per-tap products for EVERY possible 3x3 tile window, Qall
+        [2, 5**9, 576] (9 GB + 1 GB of conv2 rows while it is built: conv2 + ReLU of all 1,953,125
+        windows and one [5**9, 64] x [64, 576] GEMM per tower, a few ms per rollout); each step then
+        sums 81 table rows per frame.  Small rollouts, or when the device has less than ~12 GB free:
+        the conv2 table T2 (2,720 rows) and conv3's weights, and each step looks conv2 up per frame
+        position and runs conv3 as a GEMM over the im2col rows (merlin_tower_conv2_lut_fwd +
+        conv3_im2col_fwd, a few MB).  Both: fc1 with columns permuted to (p3, co), biases stacked."""
         from . import _native as nat
 
         ea, ec = self.actor_extractor.network, self.critic_extractor.network
@@ -490,20 +500,35 @@ class CNNActorCritic(nn.Module):
         W4 = torch.stack([fa.weight, fc.weight])
         H = W4.shape[1]
         T2 = self.conv2_tables().contiguous()
-        Z2 = nat.window_lut(self._all_window_rows(T2.device), T2)  # [2, 5**9, 64]
-        a2 = torch.relu_(Z2.add_(torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1)))
         W3r = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 2, 3, 4, 1).reshape(2, 64, 576)
         W4p = W4.view(2, H, 64, 9).transpose(2, 3).reshape(2, H, 576)
         pack = {
-            "Qall": torch.bmm(a2, W3r),  # [2, windows, (ky, kx, co)]
             "b3": torch.stack([ea[4].bias, ec[4].bias]).contiguous(),
             "b4": torch.stack([fa.bias, fc.bias]).contiguous(),
         }
+        if self._use_all_windows(frames, T2.device):
+            Z2 = nat.window_lut(self._all_window_rows(T2.device), T2)  # [2, 5**9, 64]
+            a2 = torch.relu_(Z2.add_(torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1)))
+            pack["Qall"] = torch.bmm(a2, W3r)  # [2, windows, (ky, kx, co)]
+        else:
+            pack["T2"] = T2
+            pack["b2"] = torch.stack([ea[2].bias, ec[2].bias]).contiguous()
+            # im2col rows of A3 are (ky, kx, ci): conv3 weights as [2, 576, 64] in that order
+            pack["W3t"] = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64).contiguous()
         if self.fc1_impl == "x6":  # fc1 of every step on the bf16 MFMA, fp32 products (merlin_gemm.hip)
             pack["W4pp"] = nat.x6_split(W4p.contiguous())
         else:
             pack["W4t"] = W4p.transpose(1, 2).contiguous()
         return pack
+
+    def _use_all_windows(self, frames, device) -> bool:
+        if frames is not None and frames < self.ALL_WINDOWS_MIN_FRAMES:
+            return False
+        try:
+            free, _ = torch.cuda.mem_get_info(device)
+        except Exception:
+            return True
+        return free >= (12 << 30)
 
     @torch.no_grad()
     def act_codes_packed(self, codes, pack, deterministic=False, seed=0, epoch=None, step=0, out=None, env_offset=0):
@@ -516,7 +541,11 @@ class CNNActorCritic(nn.Module):
         from .gemm_tuning import tuned
 
         n = codes.shape[0]
-        a3 = nat.codes_conv3(codes, pack["Qall"], pack["b3"]).view(2, n, 576)
+        if "Qall" in pack:
+            a3 = nat.codes_conv3(codes, pack["Qall"], pack["b3"]).view(2, n, 576)
+        else:  # per-frame conv2 lookups + conv3 GEMM (small rollouts, rollout_pack)
+            A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
+            a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
         if "W4pp" in pack:
             z = nat.x6_gemm_nt(a3, pack["W4pp"], cfg=nat.X6_NT_CFG["rollout"], name="gemm_rollout_fc1")
         else:

@@ -123,6 +123,13 @@ class MerlinVecEnv:
                                                 self.num_envs, self._stream), "merlin_env_seed")
         self._seeded_once = True
 
+    def set_base_seed(self, seed: int) -> None:
+        """Seed the next reset() that is given no seed with base `seed` (env i: seed + env_offset + i),
+        as the constructor's `seed` does: for callers holding an env from a factory that, like the
+        reference's create_env, ignores its seed argument (ppo_train.py's single env)."""
+        self._seed_pending = int(seed)
+        self._seeded_once = False
+
     def seed_each(self, seeds) -> None:
         """Seed env i with seeds[i] (e.g. FOMAML task seeds)."""
         seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64))

@@ -20,7 +20,9 @@ GEMMs it was made for (`with tuned(which):`); there a shape found in the file ru
 solution, any other runs PyTorch's default, and every other GEMM of the process takes PyTorch's
 usual path.  Nothing is timed or written at run time.  The file's validator lines (PyTorch /
 HIP / hipBLASLt / rocBLAS versions, gfx950) make TunableOp reject it on any other stack.
-MERLIN_GEMM_TUNING=0 switches it off; MERLIN_UNTUNED=rollout,dgrad,window switches groups off."""
+MERLIN_GEMM_TUNING=0 switches it off; MERLIN_UNTUNED=rollout,dgrad,window switches groups off.
+The file is loaded lazily, by the first GEMM that asks for it (`tuned()` / `padded_*`): the default
+training path (x6 fc1, all-windows acting table) never does, so TunableOp stays off there."""
 from __future__ import annotations
 
 import contextlib
@@ -60,6 +62,8 @@ def enable(path: str = TUNED_FILE) -> bool:
 @contextlib.contextmanager
 def tuned(which: str = ""):
     """TunableOp dispatch (recorded solutions, no tuning) for the GEMMs inside the block."""
+    if not _state["tried"] and torch.cuda.is_available():
+        enable()
     if (not _state["on"] or (which and which in os.environ.get("MERLIN_UNTUNED", "").split(","))
             or os.environ.get("MERLIN_PAD_ONLY")):  # (testing: the padding without the tuned dispatch)
         yield
@@ -81,6 +85,8 @@ def padded_windows(n: int) -> int:
     """The tuned window-GEMM row count to pad n windows to (n when none lies within WINDOW_BUCKET)."""
     if "window" in os.environ.get("MERLIN_UNTUNED", "").split(","):
         return n
+    if not _state["tried"] and torch.cuda.is_available():
+        enable()
     for r in _state["windows"]:
         if n <= r < n + WINDOW_BUCKET:
             return r
@@ -91,6 +97,8 @@ def padded_rows(n: int) -> int:
     """The tuned fc1 row count to pad n frames to (n itself when none lies within ROW_BUCKET)."""
     if "dgrad" in os.environ.get("MERLIN_UNTUNED", "").split(","):
         return n
+    if not _state["tried"] and torch.cuda.is_available():
+        enable()
     for r in _state["rows"]:  # (row counts of the dgrad entries: nn_576_<rows>_512)
         if n <= r < n + ROW_BUCKET:
             return r

@@ -44,6 +44,7 @@ from .distributed import DataParallel
 from .envs import MerlinEnv, MerlinVecEnv
 from .metrics.ppo_metrics import aggregate_ppo_update_metrics
 from .rollout_buffer import CodeRolloutBuffer, RolloutBuffer
+from .windows import deferred_fc1_wgrad
 
 INV255 = 1.0 / 255.0
 
@@ -122,10 +123,6 @@ class PPO:
             # look-ahead map refills on a side stream after every step, overlapping the next act
             # (MerlinVecEnv.refill; the env's own every-16-steps refill is switched off)
             self._refill_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
-            if self.device.type == "cuda":
-                from . import gemm_tuning
-
-                gemm_tuning.enable()  # pre-tuned fc1 GEMM solutions on gfx950 (merlin/gemm_tuning.py)
             if self._refill_stream is not None:
                 self.vec.set_refill_interval(0)
         else:
@@ -188,7 +185,7 @@ class PPO:
         env.reset(out=buf.codes[0])
         with torch.no_grad():
             self._act_epoch.add_(1)
-            pack = self.ac.rollout_pack() if self.conv1_from_codes else None
+            pack = self.ac.rollout_pack(frames=(T + 1) * buf.N) if self.conv1_from_codes else None
             for t in range(T):
                 self._act(buf.codes[t], pack, t, out=(buf.actions[t], buf.logprobs[t], buf.values[t]))
                 if side is not None and t > 0:
@@ -339,7 +336,8 @@ class PPO:
                     # and adds the statistics to totals[:5] on the device
                     mbw = mbws[k]
                     distinct += int(mbw.groups.numel())
-                    logits, values = self.ac.heads_windows(plan, mbw, head_bias=False)
+                    with deferred_fc1_wgrad():  # this loop reads p.grad after loss.backward() only
+                        logits, values = self.ac.heads_windows(plan, mbw, head_bias=False)
                     loss = _PPOLoss.apply(logits, values, self.ac.actor[2].bias, self.ac.critic[2].bias, mbw, mb_idx,
                                           actions, logp_old, adv, returns, self.clip_eps, self.vf_coef,
                                           self.ent_coef, totals)

@@ -40,6 +40,9 @@ frames are its distinct observations (merlin/dedup.py); fc1 and the heads run on
 """
 from __future__ import annotations
 
+import contextlib
+import threading
+
 import torch
 
 from . import _native as nat
@@ -433,6 +436,25 @@ def _conv3_backward(plan, mb, bits, dY3, nw):
 # 293.4 (deferred) ms per update.
 OVERLAP_WGRAD = "deferred"
 _SIDE = {}
+# The deferred delivery writes .grad of the fc1 weights itself, around autograd: it is only right for a
+# caller that runs loss.backward() and reads p.grad (PPO._sgd).  Everyone else (torch.autograd.grad,
+# backward(inputs=...), grad hooks) gets the joined side-stream mode, which returns dW4p through
+# autograd.  PPO._sgd opts in with `with deferred_fc1_wgrad():` around its forward.
+_DEFER = threading.local()
+
+
+@contextlib.contextmanager
+def deferred_fc1_wgrad(enabled: bool = True):
+    prev = getattr(_DEFER, "on", False)
+    _DEFER.on = bool(enabled)
+    try:
+        yield
+    finally:
+        _DEFER.on = prev
+
+
+def _defer_active() -> bool:
+    return OVERLAP_WGRAD == "deferred" and getattr(_DEFER, "on", False)
 
 
 def _side_stream(device):
@@ -533,18 +555,20 @@ def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = N
 
 def window_tower_head_x6(ac, plan: WindowPlan, mb: MinibatchWindows, head_bias: bool = True):
     """(logits [U, act_dim], value [U]) of the minibatch's distinct frames: conv2 / conv3 through
-    the windows, fc1 on the bf16 matrix cores in exact three-plane form (_WindowTowerHeadX6)."""
-    from .gemm_tuning import padded_windows
-
+    the windows, fc1 on the bf16 matrix cores in exact three-plane form (_WindowTowerHeadX6).  The
+    window GEMMs take PyTorch's default hipBLASLt path (no TunableOp: merlin/gemm_tuning.py)."""
     ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
-    Z2w = _WindowConv2.apply(ac.conv2_tables(), plan, padded_windows(plan.num_windows))
+    Z2w = _WindowConv2.apply(ac.conv2_tables(), plan, plan.num_windows)
     a2w = _BiasRelu.apply(Z2w, torch.stack([ea[2].bias, ec[2].bias]))
     W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
-    Q = _TunedBmm.apply(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
+    Q = torch.bmm(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
     fa, fc = ac.actor[0], ac.critic[0]
     W4 = torch.stack([fa.weight, fc.weight])  # [2, hidden, 576] in (co, p3) order
     W4p = W4.view(2, W4.shape[1], 64, 9).transpose(2, 3).reshape(2, W4.shape[1], 576)
     ba, bc = (ac.actor[2].bias, ac.critic[2].bias) if head_bias else (None, None)
+    # deferred fc1 weight gradient only for a caller that opted in (deferred_fc1_wgrad) and only when
+    # both weights take plain .grad accumulation
+    defer = _defer_active() and fa.weight.requires_grad and fc.weight.requires_grad and torch.is_grad_enabled()
     return _WindowTowerHeadX6.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), W4p, torch.stack([fa.bias, fc.bias]),
                                     ac.actor[2].weight, ba, ac.critic[2].weight, bc, plan, mb,
-                                    (fa.weight, fc.weight))
+                                    (fa.weight, fc.weight) if defer else None)

@@ -147,6 +147,7 @@ def train_minigrid(args):
     else:
         # rank r's single env is global env r: seed + r, and its action draws are keyed by r
         env = sc.create_env(args.difficulty, seed=args.seed, device=device, env_offset=rank, **size_kw, **flags)
+        env.vec.set_base_seed(args.seed)  # create_env ignores its seed, like the reference's
     agent = PPO(env, lr=args.lr, gamma=args.gamma, lam=args.lam, clip_eps=args.clip_eps,
                 update_epochs=args.update_epochs, batch_size=batch, minibatch_size=args.minibatch_size,
                 vf_coef=args.vf_coef, ent_coef=args.ent_coef, device=device, dp=dp)

@@ -84,3 +84,26 @@ def test_batched_eval_matches_serial_single_env(device):
             done = te or tr
         assert n == steps[ep]
         assert abs(total - rewards[ep]) < 1e-6
+
+
+def test_cli_single_env_seed_reproducible(tmp_path, monkeypatch, device):
+    """--seed reproduces a single-env (num_envs 1) run: the env is reset with seed + rank once
+    (create_env ignores its seed, like the reference's, so ppo_train sets it), and two runs with
+    the same seed give the same maps, episodes and weights; another seed gives other maps."""
+    mod = _load_cli()
+    monkeypatch.chdir(tmp_path)
+
+    def run(seed, ts):
+        args = mod.parse_args(["--device", "cuda", "--difficulty", "mediumhard", "--seed", str(seed), "--num_envs",
+                               "1", "--batch_size", "128", "--minibatch_size", "64", "--update_epochs", "1",
+                               "--total_steps", "256", "--eval_episodes", "1", "--group_timestamp", ts])
+        agent = mod.train_minigrid(args)
+        return (agent.buf.codes.cpu().clone(), agent.vec.get_state()["rng"],
+                {k: v.cpu().clone() for k, v in agent.ac.state_dict().items()})
+
+    c1, r1, s1 = run(777, "A")
+    c2, r2, s2 = run(777, "B")
+    c3, r3, _ = run(778, "C")
+    assert torch.equal(c1, c2) and (r1 == r2).all()
+    assert all(torch.equal(s1[k], s2[k]) for k in s1)
+    assert not (r1 == r3).all()

@@ -70,3 +70,34 @@ def test_clip_adam_rejects_mismatched_state(device):
     p = torch.zeros(10, device=device)
     with pytest.raises(ValueError):
         nat.clip_adam([p], [p[:5]], [p], [p], [torch.zeros((), device=device)], 1e-3, 0.9, 0.999, 1e-8, 0.5)
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf")])
+def test_clip_adam_nonfinite_gradient_matches_torch(device, bad):
+    """A non-finite gradient element: torch's clip_grad_norm_ keeps the NaN / zero coefficient
+    (clamp(max=1) propagates NaN), so the kernel must poison the same elements torch does."""
+    from merlin.optim import ClipAdam
+
+    shapes = _shapes()
+    mine = _make(shapes, device, True, 3)
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in mine]
+    opt_m = torch.optim.Adam(mine, lr=2.5e-4, fused=True)
+    opt_r = torch.optim.Adam(ref, lr=2.5e-4, fused=True)
+    ca = ClipAdam(opt_m, 0.5)
+    gen = torch.Generator().manual_seed(2)
+    grads = [(torch.randn(s, generator=gen) * 1e-3).to(device) for s in shapes]
+    grads[3].view(-1)[7] = bad
+    for p, q, gr in zip(mine, ref, grads):
+        p.grad = gr.clone()
+        q.grad = gr.clone()
+    n_m = ca.step()
+    n_r = torch.nn.utils.clip_grad_norm_(ref, 0.5)
+    opt_r.step()
+    torch.cuda.synchronize()
+    assert (torch.isnan(n_m) == torch.isnan(n_r)).all() and (torch.isinf(n_m) == torch.isinf(n_r)).all()
+    for p, q in zip(mine, ref):
+        # same non-finite pattern everywhere; finite values equal up to Adam rounding
+        assert torch.equal(torch.isfinite(p.grad), torch.isfinite(q.grad))
+        assert torch.equal(torch.isfinite(p.detach()), torch.isfinite(q.detach()))
+        fin = torch.isfinite(q.detach())
+        torch.testing.assert_close(p.detach()[fin], q.detach()[fin], rtol=2e-6, atol=2.5e-4 * 1e-5)

@@ -9,7 +9,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_packed_act_matches_act_codes(device):
+@pytest.mark.parametrize("frames", [None, 1000])
+def test_packed_act_matches_act_codes(device, frames):
+    """Both acting layouts of rollout_pack: the all-windows table (large rollouts) and the per-frame
+    conv2 lookups + conv3 GEMM (small rollouts, no 9-GB table)."""
     from merlin.actor_critic import CNNActorCritic
     from test_gpu_conv2lut import _codes
 
@@ -18,7 +21,9 @@ def test_packed_act_matches_act_codes(device):
     ac = CNNActorCritic((56, 56, 3), 3).to(device)
     with torch.no_grad():
         a1, lp1, v1 = ac.act_codes(codes, deterministic=True)
-        a2, lp2, v2 = ac.act_codes_packed(codes, ac.rollout_pack(), deterministic=True)
+        pack = ac.rollout_pack(frames=frames)
+        assert ("Qall" in pack) == (frames is None)
+        a2, lp2, v2 = ac.act_codes_packed(codes, pack, deterministic=True)
     same = a1 == a2
     assert same.float().mean() > 0.99
     torch.testing.assert_close(lp1[same], lp2[same], rtol=1e-5, atol=1e-5)

@@ -228,3 +228,40 @@ def test_window_update_matches_lookup_path(device):
     for d in ds:
         assert d.max().item() <= 2 * 3e-4 * 8
     assert (torch.cat(ds) > 5e-5).float().mean().item() < 0.05
+
+
+def test_evaluate_windows_autograd_grad_fc1(device):
+    """torch.autograd.grad through evaluate_windows for the fc1 weights: the x6 path hands fc1's weight
+    gradient back through autograd (the deferred .grad delivery is only for PPO._sgd, which opts in
+    with deferred_fc1_wgrad), leaves .grad untouched, and equals what loss.backward() accumulates,
+    with and without the opt-in."""
+    from merlin.actor_critic import CNNActorCritic
+    from merlin.windows import deferred_fc1_wgrad
+
+    codes, plan = _plan(device)
+    mb = plan.minibatch(torch.randperm(codes.shape[0], device=device)[:2048])
+    acts = torch.randint(0, 3, (2048,), device=device)
+    torch.manual_seed(12)
+    ac = CNNActorCritic((56, 56, 3), 3).to(device)
+    w = [ac.actor[0].weight, ac.critic[0].weight]
+    ga = torch.autograd.grad(_loss(*ac.evaluate_windows(plan, mb, acts)), w)
+    torch.cuda.synchronize()
+    assert all(p.grad is None for p in ac.parameters())
+    _loss(*ac.evaluate_windows(plan, mb, acts)).backward()
+    gb = [p.grad.clone() for p in w]
+    ac.zero_grad(set_to_none=True)
+    with deferred_fc1_wgrad():
+        _loss(*ac.evaluate_windows(plan, mb, acts)).backward()
+    torch.cuda.synchronize()
+    gc = [p.grad.clone() for p in w]
+    for a, b, c in zip(ga, gb, gc):
+        assert torch.equal(a, b) and torch.equal(b, c)
+    # requires_grad=False on fc1: no gradient anywhere near it, other parameters still get theirs
+    ac.zero_grad(set_to_none=True)
+    for p in w:
+        p.requires_grad_(False)
+    with deferred_fc1_wgrad():
+        _loss(*ac.evaluate_windows(plan, mb, acts)).backward()
+    torch.cuda.synchronize()
+    assert all(p.grad is None for p in w)
+    assert ac.actor_extractor.network[0].weight.grad is not None
