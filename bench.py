@@ -363,26 +363,77 @@ def roofline_of(name, k, x6=False):
             "bytes_per_launch": k["bytes_per_launch"], "avg_launch_us": k["avg_us"], "launches": k["launches"]}
 
 
-def floor_tier(agent, iters=1):
-    """The update without exploiting repeated observations (no distinct-frame grouping, no
-    receptive-field windows: every minibatch sample through the per-position lookup path), on the
-    agent's current state, after the timed region: env-steps/s of rollout + update."""
+def _median_iter_rate(agent, warmup, iters):
+    """env-steps/s of rollout + update: `warmup` untimed iterations, then the median of `iters` iterations
+    each timed on its own (host clock around a synchronised iteration)."""
     import torch
 
+    for _ in range(warmup):
+        agent.update(agent.collect_rollouts())
+    times = []
+    for _ in range(iters):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        agent.update(agent.collect_rollouts())
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    return agent.batch_size / float(np.median(times)), times
+
+
+def floor_tier(agent, warmup=1, iters=3):
+    """The update without exploiting repeated observations, on the agent's current state, after the timed
+    region: env-steps/s of rollout + update, median of `iters` iterations after `warmup` untimed ones per
+    setting (the first iteration of a setting pays its one-time costs: MIOpen / hipBLASLt heuristics for
+    new shapes, allocator growth).
+      no_windows           distinct frames per minibatch (merlin/dedup.py), conv1+conv2 by per-position
+                           table lookups and conv3 as an im2col GEMM per distinct frame
+      no_dedup_no_windows  the same on every minibatch sample (no grouping at all)
+    Without the windows the grouping's gain is only the distinct fraction of the sample count (0.89 at
+    the bench state) while it adds a sort + gather per minibatch, so the two floors are close."""
     saved = (agent.dedup, agent.windows)
     out = {}
     try:
         for name, (dedup, windows) in (("no_windows", (True, False)), ("no_dedup_no_windows", (False, False))):
             agent.dedup, agent.windows = dedup, windows
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(iters):
-                agent.update(agent.collect_rollouts())
-            torch.cuda.synchronize()
-            out[name] = round(iters * agent.batch_size / (time.perf_counter() - t0), 1)
+            rate, times = _median_iter_rate(agent, warmup, iters)
+            out[name] = round(rate, 1)
+            out[name + "_iter_ms"] = [round(t * 1e3, 1) for t in times]
     finally:
         agent.dedup, agent.windows = saved
     return out
+
+
+def hard22_tier(device, N, T, epochs, minibatches, warmup=2, iters=3):
+    """BASELINE cfg 4: the same full loop on hard 22x22 grids (src/custom_envs/hard_env.py:11-97: mid
+    wall with 2-5 gaps, 6-12 extra walls, goal in the right half), 4096 envs x 256 steps, a fresh agent
+    (torch seed 777, env seeds 777+i); median of `iters` iterations after `warmup`."""
+    import torch
+
+    from merlin import MerlinVecEnv
+    from merlin.ppo import PPO
+
+    env = MerlinVecEnv(N, difficulty="hard", size=22, seed=777, device=device)
+    torch.manual_seed(777)
+    agent = PPO(env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=epochs, batch_size=N * T,
+                minibatch_size=N * T // minibatches, vf_coef=0.5, ent_coef=0.05, device=device)
+    rate, times = _median_iter_rate(agent, warmup, iters)
+    out = {"value": round(rate, 1), "unit": "env-steps/s", "iter_ms": [round(t * 1e3, 1) for t in times],
+           "config": f"hard 22x22, {N} envs x k_steps {T}, {epochs} epochs x {minibatches} minibatches",
+           "state": f"iterations {warmup + 1}..{warmup + iters} from random init",
+           "distinct_frames_per_sample": round(agent.last_distinct_frac, 4),
+           "windows_per_update": agent.last_num_windows}
+    env.close()
+    del agent
+    torch.cuda.empty_cache()
+    return out
+
+
+def rollout_ms_of(ph):
+    return sum(a.elapsed_time(b) for a, b, _ in ph) / len(ph)
+
+
+def update_ms_of(ph):
+    return sum(b.elapsed_time(c) for _, b, c in ph) / len(ph)
 
 
 def heartbeat(state):
@@ -461,9 +512,26 @@ def main():
         elapsed = float(t.item())
 
     kernels = kernel_table(nat.KernelTimer.stop())
-    rollout_ms = sum(a.elapsed_time(b) for a, b, _ in ph) / len(ph)
-    update_ms = sum(b.elapsed_time(c) for _, b, c in ph) / len(ph)
+    rollout_ms, update_ms = rollout_ms_of(ph), update_ms_of(ph)
     value = args.steps * B * world / elapsed
+    rank_spread = None
+    if dp.enabled:
+        # per-rank work of the timed iterations: the gradient all-reduce of every optimizer step makes
+        # all ranks wait for the slowest, so the imbalance shows as each rank's own GPU-kernel time (HIP
+        # event spans of the timed kernels) and its distinct frames per sample (the update's work
+        # scales with them), not in the phase times, which the all-reduce equalises
+        busy = sum(k["total_ms"] for k in kernels.values()) / args.steps
+        mine = torch.tensor([rollout_ms_of(ph), update_ms_of(ph), busy,
+                             agent.last_distinct_frac if agent.last_distinct_frac is not None else 1.0],
+                            dtype=torch.float64, device=device)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        a = torch.stack(allv).cpu().numpy()
+        rank_spread = {"rollout_ms": [round(float(x), 2) for x in a[:, 0]],
+                       "update_ms": [round(float(x), 2) for x in a[:, 1]],
+                       "kernel_ms_per_iter": [round(float(x), 2) for x in a[:, 2]],
+                       "distinct_frames_per_sample": [round(float(x), 4) for x in a[:, 3]],
+                       "kernel_ms_max_over_min": round(float(a[:, 2].max() / max(a[:, 2].min(), 1e-9)), 4)}
 
     if rank != 0:
         if dp.enabled:
@@ -537,6 +605,8 @@ def main():
         "rollout_graph": agent._graph is not None,
         "kernels": kernels,
     }
+    if rank_spread is not None:
+        out["ranks"] = rank_spread
     if x6 and agent.last_distinct_frac is not None:
         # the x6 GEMMs alone at the update's shape (distinct frames per minibatch)
         U = int(round(agent.last_distinct_frac * (B // args.minibatches)))
@@ -550,9 +620,10 @@ def main():
                         "rollout_only": round(B / (rollout_ms / 1e3), 1),
                         "env_only_2M_envs": env_large_tier(torch, MerlinVecEnv, args.difficulty, args.size, device),
                         "full_loop_per_gpu": round(value / world, 1),
-                        # the same loop, one iteration each right after the timed region, with the
-                        # observation reuse switched off: the data-independent floor
+                        # the same loop right after the timed region with the observation reuse switched
+                        # off (median of 3 after a warm-up iteration per setting): the data-independent floor
                         "full_loop_floor": floors,
+                        "hard_22": hard22_tier(device, N, T, args.epochs, args.minibatches),
                         "fomaml": fomaml_tier(device, args.difficulty)}
     state["phase"] = "cpu_baseline"
     if world == 1 and not args.no_cpu_baseline:

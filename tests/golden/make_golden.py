@@ -19,6 +19,8 @@ Sources, per fixture:
                   torch.manual_seed: param checksums + act/evaluate outputs.
   update_ref.npz  one REFERENCE PPO.update (src/ppo.py:122-168) on a small
                   replay batch, with the randperm draws recorded for replay.
+  update_rollout_ref.npz  the same on a real single-env rollout of the C oracle's env (repeated
+                  observations, episode ends), the fixture the benched update path is pinned to.
   fomaml_ref.npz  the REFERENCE FOMAML.compute_loss (src/fomaml.py:110-156) and the
                   per-task inner SGD step + query-gradient accumulation of
                   meta_train_step (:158-212) on recorded support / query batches of
@@ -283,6 +285,58 @@ def gen_update():
     )
 
 
+def gen_update_rollout():
+    """update_rollout_ref.npz: one REFERENCE PPO.update (src/ppo.py:122-168) on a real single-env
+    rollout (the C oracle's mediumhard env, seed 777, uniformly random actions, max_steps 48 so that
+    episodes end and auto-reset): its observations repeat (turns in place, revisited cells), so the
+    distinct-frame grouping and the receptive-field windows of the benched update path are exercised
+    on the reference's own numbers.  Values / log-probs from the reference's initial weights."""
+    import torch
+
+    PPO, _, _ = _import_reference()
+    atlas = build_atlas()
+    B, MB, EPOCHS = 1024, 256, 3
+    rs = np.random.RandomState(31)
+    actions = rs.randint(0, 3, size=(B, 1)).astype(np.int64)
+    codes, rew, term, trunc, _ = O.batch_rollout(np.array([777], dtype=np.uint64), actions, max_steps=48)
+    codes = codes[:B, 0]
+    imgs = O.render(codes, atlas)
+    rewards = rew[:, 0].astype(np.float32)
+    dones = np.maximum(term, trunc)[:, 0].astype(np.float32)
+    actions = actions[:, 0]
+
+    class _StubEnv:
+        action_space = types.SimpleNamespace(n=3)
+
+        def reset(self, seed=None):
+            return imgs[0].copy(), {}
+
+    torch.manual_seed(0)
+    agent = PPO(_StubEnv(), lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=EPOCHS,
+                batch_size=B, minibatch_size=MB, vf_coef=0.5, ent_coef=0.05, device="cpu")
+    keys, sums0 = _param_checksums(agent.ac)
+    with torch.no_grad():
+        lp, _, v = agent.ac.evaluate(torch.from_numpy(imgs.astype(np.float32)), torch.from_numpy(actions))
+    for t in range(B):
+        agent.buffer.add(torch.from_numpy(imgs[t].astype(np.float32)), torch.tensor(actions[t]), lp[t], v[t],
+                         torch.tensor(rewards[t]), torch.tensor(dones[t]))
+    last_value = float(v[-1].item())
+    torch.manual_seed(4321)
+    perms = np.stack([torch.randperm(B).numpy() for _ in range(EPOCHS)])
+    torch.manual_seed(4321)
+    stats = agent.update(last_value)
+    keys1, sums1 = _param_checksums(agent.ac)
+    assert (keys1 == keys).all()
+    np.savez_compressed(
+        os.path.join(HERE, "update_rollout_ref.npz"),
+        cfg=np.array([B, MB, EPOCHS], dtype=np.int64), codes=codes, actions=actions,
+        logp=lp.numpy(), values=v.numpy(), rewards=rewards, dones=dones,
+        last_value=np.float32(last_value), perms=perms, keys=keys, sums0=sums0, sums1=sums1,
+        stat_names=np.array(sorted(stats)), stat_vals=np.array([stats[k] for k in sorted(stats)]),
+        hparams=np.array([3e-4, 0.99, 0.95, 0.2, 0.5, 0.05]),
+    )
+
+
 def gen_fomaml():
     import copy
 
@@ -371,5 +425,6 @@ if __name__ == "__main__":
     gen_gae()
     gen_cnn()
     gen_update()
+    gen_update_rollout()
     gen_fomaml()
     print("golden fixtures written to", HERE)
