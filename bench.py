@@ -279,13 +279,14 @@ def cpu_baseline():
                       "ppo/ppo_train.py:150"}
 
 
-# bench names -> rocprofv3 kernel names: the dQ and dT2 segmented sums are one kernel; the
-# PMC summary keeps its largest-grid launches, which are the dQ ones (2048 blocks vs ~90).  The
-# fc1 GEMMs are hipBLASLt kernels, matched by name prefix (largest grid = the update's, not the
-# rollout's); their PMC key is the full Tensile kernel name.
-PMC_ALIAS = {"k_seg_sum_dQ": "k_seg_sum",
-             # fc1's x6 GEMMs (untruncated rocprofv3 names keep the template arguments); the weight
-             # gradient's span covers the split-K kernel and its slab fold
+# bench names -> rocprofv3 kernel names (untruncated: template arguments kept).  A span made of several
+# kernels adds their bytes; the first name of a tuple must be present, the rest (e.g. a segmented sum's
+# fix-up pass, absent when no destination crosses an item) count when they are.
+PMC_ALIAS = {"k_seg_sum_R": ("k_seg_sum<2, 1>", "k_seg_fix<1>"),
+             "k_seg_sum_S": ("k_seg_sum<0, 2>", "k_seg_fix<2>"),
+             "k_seg_sum_dQ": ("k_seg_sum<0, 3>", "k_seg_fix<3>"),
+             "k_seg_sum_dT2": ("k_seg_sum<0, 4>", "k_seg_fix<4>"),
+             # fc1's x6 GEMMs; the weight gradient's span covers the split-K kernel and its slab fold
              "gemm_fc1_fwd": ("k_x6_nt<256, 128, 4, 2, 1, true>",),
              "gemm_fc1_dgrad": ("k_x6_nt<128, 192, 2, 4, 0, true>",),
              "gemm_wgrad": ("k_x6_tn<128, 192, 2, 4>", "k_x6_fold")}
@@ -305,8 +306,8 @@ def pmc_traffic(kernel: str):
         except Exception:
             continue
         got = [dd.get(n, {}).get("hbm_bytes_per_launch") for n in names]
-        if all(got):
-            return int(sum(got))
+        if got[0]:
+            return int(sum(g for g in got if g))
     return None
 
 

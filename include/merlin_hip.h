@@ -301,6 +301,10 @@ int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *id
 #define MERLIN_SEG_ACCUMULATE 1
 #define MERLIN_SEG_NO_FILL 2
 #define MERLIN_SEG_MASK_BITS 4
+/* bits 8..10: which pass of conv3's backward this is (1 R, 2 S, 3 dQ, 4 dT2; 0 generic) -- it only
+ * names the kernel instantiation, so profiles tell the passes apart; the sums are the same */
+#define MERLIN_SEG_ROLE_SHIFT 8
+#define MERLIN_SEG_ROLE_MASK (7 << MERLIN_SEG_ROLE_SHIFT)
 int merlin_segment_sum_masked(const float *src_dev, const void *mask_dev, int64_t src_rows,
                               const int32_t *idx_dev, const int32_t *key_dev, int64_t nnz,
                               const int32_t *slot_dev, int32_t sub, int64_t item_len,

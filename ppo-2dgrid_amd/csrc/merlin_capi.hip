@@ -645,11 +645,12 @@ int merlin_segment_sum_masked(const float *src, const void *mask, int64_t src_ro
     if (n_fix > 0 && !fix) return fail(MERLIN_E_INVALID, "null fix-up list");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (item_len <= 0 || sub <= 0) return fail(MERLIN_E_INVALID, "item_len and sub must be > 0");
-    if (flags & ~(MERLIN_SEG_ACCUMULATE | MERLIN_SEG_NO_FILL | MERLIN_SEG_MASK_BITS))
+    if (flags & ~(MERLIN_SEG_ACCUMULATE | MERLIN_SEG_NO_FILL | MERLIN_SEG_MASK_BITS | MERLIN_SEG_ROLE_MASK))
         return fail(MERLIN_E_INVALID, "unknown flags");
     HIP_TRY(merlin::launch_seg_sum(src, mask, (flags & MERLIN_SEG_MASK_BITS) ? 1 : 0, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
                                    out_rows, carry, (flags & MERLIN_SEG_ACCUMULATE) ? 1 : 0,
-                                   (flags & MERLIN_SEG_NO_FILL) ? 0 : 1, (hipStream_t)stream));
+                                   (flags & MERLIN_SEG_NO_FILL) ? 0 : 1,
+                                   (flags & MERLIN_SEG_ROLE_MASK) >> MERLIN_SEG_ROLE_SHIFT, (hipStream_t)stream));
     return MERLIN_OK;
 }
 

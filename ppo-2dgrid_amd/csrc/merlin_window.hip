@@ -162,8 +162,10 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
 // threshold_backward(src, mask) rows, never materialised.  MASK 2: the same mask as one 64-bit
 // word per row (bit ch = mask channel ch > 0, as k_window_conv3 writes it): 8 B per row instead
 // of 256.
+// ROLE only names the instantiation (rocprofv3 tells the passes of conv3's backward apart by it):
+// 0 generic, 1 R (patch sums), 2 S (band sums), 3 dQ (window sums), 4 dT2 (table rows)
 constexpr int SEG_WAVES = 4, SEG_UNROLL = 8;
-template <int MASK>
+template <int MASK, int ROLE>
 __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__restrict__ src,
                                                            const void *__restrict__ mask, int64_t src_rows,
                                                            const int32_t *__restrict__ idx,
@@ -285,6 +287,7 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
 
 // fix rows (dst, j0, j1, slot0): out[t][dst] = carry[t][j0][slot0] + sum_{j0 < j <= j1} carry[t][j][0];
 // rows with dst < 0 hold nothing (merlin/windows.py SegmentPlan: one row per item)
+template <int ROLE>
 __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carry, int64_t nitems,
                                                  const int4 *__restrict__ fix, int64_t nfix, int T,
                                                  float2 *__restrict__ out, int64_t out_rows, int acc_out) {
@@ -363,35 +366,55 @@ hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, 
     return hipGetLastError();
 }
 
-hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
-                          const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
-                          int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,
-                          hipStream_t s) {
-    hipError_t e = (acc_out || !fill) ? hipSuccess
-                                      : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
-    if (e != hipSuccess || nnz <= 0) return e;
+namespace {
+template <int ROLE>
+hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
+                      const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
+                      int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, hipStream_t s) {
     const int64_t nitems = (nnz + L - 1) / L;
     const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
     if (mask && mask_bits)
-        hipLaunchKernelGGL(k_seg_sum<2>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
+        hipLaunchKernelGGL((k_seg_sum<2, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
                            reinterpret_cast<const float4 *>(src), mask, src_rows, idx, key, nnz, slot, S, L, nitems,
                            T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out);
     else if (mask)
-        hipLaunchKernelGGL(k_seg_sum<1>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
+        hipLaunchKernelGGL((k_seg_sum<1, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
                            reinterpret_cast<const float4 *>(src), mask, src_rows, idx, key, nnz, slot, S, L, nitems,
                            T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out);
     else
-        hipLaunchKernelGGL(k_seg_sum<0>, dim3(grid), dim3(64 * SEG_WAVES), 0, s,
+        hipLaunchKernelGGL((k_seg_sum<0, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
                            reinterpret_cast<const float4 *>(src), nullptr, src_rows, idx, key, nnz, slot, S, L,
                            nitems, T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry),
                            acc_out);
-    e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess || nfix <= 0) return e;
     const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);
-    hipLaunchKernelGGL(k_seg_fix, dim3(gfix), dim3(256), 0, s, reinterpret_cast<const float2 *>(carry), nitems,
+    hipLaunchKernelGGL(k_seg_fix<ROLE>, dim3(gfix), dim3(256), 0, s, reinterpret_cast<const float2 *>(carry), nitems,
                        reinterpret_cast<const int4 *>(fix), nfix, T, reinterpret_cast<float2 *>(out), out_rows,
                        acc_out);
     return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
+                          const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
+                          int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,
+                          int role, hipStream_t s) {
+    hipError_t e = (acc_out || !fill) ? hipSuccess
+                                      : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
+    if (e != hipSuccess || nnz <= 0) return e;
+    switch (role) {
+        case 1: return seg_launch<1>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
+                                     out_rows, carry, acc_out, s);
+        case 2: return seg_launch<2>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
+                                     out_rows, carry, acc_out, s);
+        case 3: return seg_launch<3>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
+                                     out_rows, carry, acc_out, s);
+        case 4: return seg_launch<4>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
+                                     out_rows, carry, acc_out, s);
+        default: return seg_launch<0>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
+                                      out_rows, carry, acc_out, s);
+    }
 }
 
 }  // namespace merlin

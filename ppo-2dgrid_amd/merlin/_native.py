@@ -476,6 +476,9 @@ def codes_conv3(codes, Qall, b3):
 
 
 SEG_ACCUMULATE, SEG_NO_FILL, SEG_MASK_BITS = 1, 2, 4  # include/merlin_hip.h
+SEG_ROLE_SHIFT = 8
+# the conv3-backward passes get their own kernel instantiations (names in rocprofv3 profiles)
+SEG_ROLES = {"k_seg_sum_R": 1, "k_seg_sum_S": 2, "k_seg_sum_dQ": 3, "k_seg_sum_dT2": 4}
 
 
 def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum", out=None,
@@ -507,6 +510,7 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
     mrow = 0 if mask is None else (8 if mask_bits else 256)
     nb = plan.nnz * (8 + (4 if slot is not None else 0)) + T * (src_rows * (256 + mrow) + out_rows * 256)
     flags = (SEG_ACCUMULATE if accumulate else 0) | (0 if fill else SEG_NO_FILL) | (SEG_MASK_BITS if mask_bits else 0)
+    flags |= SEG_ROLES.get(name, 0) << SEG_ROLE_SHIFT
     with KernelTimer.span(name, nb):
         check(lib().merlin_segment_sum_masked(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz,
                                               ptr(slot), int(sub), plan.item_len, ptr(plan.fix),

@@ -13,7 +13,7 @@ import sys
 
 
 def short(name):
-    m = re.search(r"(k_\w+)", name)
+    m = re.search(r"(k_\w+(?:<[^>]*>)?)", name)
     if m:
         return m.group(1)
     return name.split("(")[0].split("<")[0][-60:]
@@ -24,7 +24,7 @@ def main(src, out, anchor="k_ppo_loss"):
     for r in csv.DictReader(open(src)):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Queue_Id", "")))
     rows.sort()
-    marks = [i for i, r in enumerate(rows) if short(r[2]) == anchor]
+    marks = [i for i, r in enumerate(rows) if short(r[2]).split("<")[0] == anchor]
     if len(marks) < 3:
         raise SystemExit(f"fewer than 3 {anchor} launches")
     a, b = marks[-3], marks[-2]

@@ -18,22 +18,50 @@ OUT = os.path.join(REPO, "gpurun_out")
 DEST = os.path.join(REPO, "profiles")
 
 
+def kname(raw):
+    """Kernel name for the tables: merlin kernels keep their template arguments (the x6 GEMM roles and
+    the segmented-sum passes are template instantiations), others are cut to the function name."""
+    m = re.search(r"::(k_\w+(?:<[^>]*>)?)\(", raw) or re.search(r"^(k_\w+(?:<[^>]*>)?)", raw)
+    if m:
+        return m.group(1)
+    name = raw.split("(")[0].split("<")[0].replace("void ", "").strip()
+    return name.split("::")[-1][:90]
+
+
 def stats(tag):
-    src = os.path.join(OUT, "prof_trace", "run_kernel_stats.csv")
+    """Per-kernel table from the per-dispatch kernel trace (untruncated names), plus the ordered
+    launches of one optimizer step (scripts/kernel_sequence.py)."""
+    src = os.path.join(OUT, "prof_trace", "run_kernel_trace.csv")
     if not os.path.exists(src):
         return
-    rows = list(csv.DictReader(open(src)))
-    rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
-    tot = sum(float(r["TotalDurationNs"]) for r in rows)
-    lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py` (1 warmup + timed iterations)", "",
+    agg = {}
+    for r in csv.DictReader(open(src)):
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        a = agg.setdefault(kname(r["Kernel_Name"]), [0, 0])
+        a[0] += 1
+        a[1] += d
+    rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    tot = sum(v[1] for v in agg.values())
+    lines = [f"# {tag}: rocprofv3 --kernel-trace of `bench.py` (per-dispatch durations, untruncated names)", "",
              f"total kernel time {tot / 1e6:.1f} ms", "",
              "| kernel | calls | total ms | % | avg us |", "|---|---|---|---|---|"]
-    for r in rows[:40]:
-        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
-                     f"{float(r['Percentage']):.2f} | {float(r['AverageNs']) / 1e3:.2f} |")
+    os.makedirs(DEST, exist_ok=True)
+    with open(os.path.join(DEST, f"{tag}_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "total_ns", "avg_ns"])
+        for k, (c, ns) in rows:
+            w.writerow([k, c, ns, ns // c])
+    for k, (c, ns) in rows[:60]:
+        lines.append(f"| `{k}` | {c} | {ns / 1e6:.2f} | {100 * ns / tot:.2f} | {ns / c / 1e3:.2f} |")
     os.makedirs(DEST, exist_ok=True)
     open(os.path.join(DEST, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
-    shutil.copy(src, os.path.join(DEST, f"{tag}_kernel_stats.csv"))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import kernel_sequence
+
+    try:
+        kernel_sequence.main(src, os.path.join(DEST, f"{tag}_step_sequence.md"))
+    except SystemExit as e:
+        print("no step sequence:", e)
 
 
 def pmc(tag):
@@ -55,13 +83,7 @@ def pmc(tag):
 def collect(res, src, counter, rename):
     per = {}
     for r in csv.DictReader(open(src)):
-        raw = r["Kernel_Name"]
-        m = re.search(r"::(k_\w+(?:<[^>]*>)?)\(", raw)  # untruncated merlin kernel: keep template args
-        if m:
-            name = m.group(1)
-        else:
-            name = raw.split("(")[0].split("<")[0].replace("void ", "").strip()
-            name = name.split("::")[-1]
+        name = kname(r["Kernel_Name"])
         name = rename.get(name, name)
         per.setdefault(name, []).append((int(r["Grid_Size"]), float(r["Counter_Value"])))
     for k, vals in per.items():

@@ -254,8 +254,11 @@ def test_evaluate_windows_autograd_grad_fc1(device):
         _loss(*ac.evaluate_windows(plan, mb, acts)).backward()
     torch.cuda.synchronize()
     gc = [p.grad.clone() for p in w]
+    # (evaluate_windows' index_select backward is an atomic index_add over the samples of a frame, so
+    # the three runs agree to fp32 summation order, not bit for bit)
     for a, b, c in zip(ga, gb, gc):
-        assert torch.equal(a, b) and torch.equal(b, c)
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-9)
+        torch.testing.assert_close(c, b, rtol=1e-4, atol=1e-9)
     # requires_grad=False on fc1: no gradient anywhere near it, other parameters still get theirs
     ac.zero_grad(set_to_none=True)
     for p in w:
