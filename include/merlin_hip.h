@@ -252,6 +252,19 @@ int merlin_tower_conv2_lut_fwd(const uint32_t *codes_dev, const int64_t *index_d
 int merlin_tower_conv2_lut_bwd(const uint32_t *codes_dev, int64_t n, const float *dZ2c_dev,
                                const uint32_t *absmax_dev, int32_t towers, float *dtables_dev,
                                void *stream);
+/* Grouped form (one weight set per group of frames: FOMAML's per-task policies, src/fomaml.py:158-212).
+ * towers = 2 * groups; frames codes[g * group_frames + i] (i < group_frames) belong to group g and are
+ * evaluated by towers 2g (actor) and 2g+1 (critic) only, with their own tables:
+ * lut_fwd_grouped: Z2[2g + c][i*25 + p2][co] for the n = groups * group_frames frames;
+ * lut_bwd_grouped: dtables[2g + c] from dZ2c[2g + c] (chunk-major, group_frames frames per tower, as
+ *   merlin_tower_conv3_col2im_bwd_chunked writes it for n = group_frames, towers = 2 * groups);
+ *   slabs_dev: caller-owned scratch of merlin_tower_conv2_lut_slab_bytes(towers, group_frames) bytes. */
+int merlin_tower_conv2_lut_fwd_grouped(const uint32_t *codes_dev, int64_t n, int64_t group_frames,
+                                       const float *tables_dev, int32_t towers, float *Z2_dev, void *stream);
+int64_t merlin_tower_conv2_lut_slab_bytes(int32_t towers, int64_t group_frames);
+int merlin_tower_conv2_lut_bwd_grouped(const uint32_t *codes_dev, int64_t group_frames, const float *dZ2c_dev,
+                                       const uint32_t *absmax_dev, int32_t towers, float *dtables_dev,
+                                       void *slabs_dev, void *stream);
 
 /* Receptive-field windows (csrc/merlin_window.hip; the plan is built by merlin/windows.py).
  * window_lut:   Z2w[t][w][co] = sum over the 16 taps of tables[t][rows[w][tap]][co]

@@ -575,7 +575,7 @@ int merlin_tower_conv3_col2im_bwd(const float *dA3, const float *Z2, const float
 int merlin_tower_conv3_col2im_bwd_chunked(const float *dA3, const float *Z2, const float *b2, int64_t n,
                                           int32_t towers, float *dZ2c, uint32_t *absmax, void *stream) {
     if (!absmax || ((!dA3 || !Z2 || !b2 || !dZ2c) && n > 0)) return fail(MERLIN_E_INVALID, "null argument");
-    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (towers < 1) return fail(MERLIN_E_INVALID, "towers must be >= 1");
     HIP_TRY(merlin::launch_col2im3_bwd(dA3, Z2, b2, n, towers, 1, dZ2c, absmax, (hipStream_t)stream));
     return MERLIN_OK;
 }
@@ -599,6 +599,30 @@ int merlin_tower_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ
     if (rc) return rc;
     HIP_TRY(merlin::launch_conv2_lut_bwd(codes, n, dZ2c, absmax, towers, dtables, ws->lut2_slabs,
                                          (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_conv2_lut_fwd_grouped(const uint32_t *codes, int64_t n, int64_t group_frames, const float *tables,
+                                       int32_t towers, float *Z2, void *stream) {
+    if ((!codes || !tables || !Z2) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 2 || towers % 2 || group_frames <= 0) return fail(MERLIN_E_INVALID, "bad grouping");
+    if (n != (int64_t)(towers / 2) * group_frames) return fail(MERLIN_E_INVALID, "n != groups * group_frames");
+    HIP_TRY(merlin::launch_conv2_lut_fwd(codes, nullptr, n, tables, towers, Z2, (hipStream_t)stream, group_frames));
+    return MERLIN_OK;
+}
+
+int64_t merlin_tower_conv2_lut_slab_bytes(int32_t towers, int64_t group_frames) {
+    return (int64_t)merlin::conv2_lut_slab_bytes(towers, merlin::conv2_lut_fblocks(group_frames));
+}
+
+int merlin_tower_conv2_lut_bwd_grouped(const uint32_t *codes, int64_t group_frames, const float *dZ2c,
+                                       const uint32_t *absmax, int32_t towers, float *dtables, void *slabs,
+                                       void *stream) {
+    if (!dtables || ((!codes || !dZ2c || !absmax || !slabs) && group_frames > 0))
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 2 || towers % 2) return fail(MERLIN_E_INVALID, "bad grouping");
+    HIP_TRY(merlin::launch_conv2_lut_bwd(codes, group_frames, dZ2c, absmax, towers, dtables, slabs,
+                                         (hipStream_t)stream, group_frames));
     return MERLIN_OK;
 }
 

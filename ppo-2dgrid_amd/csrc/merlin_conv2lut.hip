@@ -86,10 +86,13 @@ __device__ __forceinline__ void stage_classes(const uint32_t *__restrict__ codes
 
 // ---------------------------------------------------------------------------
 constexpr int FWD_WAVES = 4, FWD_G = 4;  // frames per wave group
+// gstride > 0 (grouped): frame s belongs to group g = s / gstride and is evaluated only by that group's
+// two towers 2g, 2g+1 (their own tables: one weight set per group, e.g. FOMAML's per-task policies);
+// Z2 is then [towers][gstride*25][16 float4] with the frame at its index within the group.
 __global__ __launch_bounds__(64 * FWD_WAVES) void k_conv2_lut_fwd(const uint32_t *__restrict__ codes,
                                                                  const int64_t *__restrict__ index, int64_t n,
                                                                  const float4 *__restrict__ tab, int towers,
-                                                                 float4 *__restrict__ Z2) {
+                                                                 float4 *__restrict__ Z2, int64_t gstride) {
     __shared__ uint8_t cls_all[FWD_WAVES][FWD_G * 49 + 4];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint8_t *cls = cls_all[wv];
@@ -98,10 +101,18 @@ __global__ __launch_bounds__(64 * FWD_WAVES) void k_conv2_lut_fwd(const uint32_t
         const int64_t s0 = g * FWD_G;
         const int nf = (int)std::min<int64_t>(FWD_G, n - s0);
         stage_classes(codes, index, s0, nf, lane, cls);
-        const int tasks = towers * nf * P2 * 16;
+        const int tasks = (gstride > 0 ? 2 : towers) * nf * P2 * 16;
         for (int tid = lane; tid < tasks; tid += 64) {
             const int q = tid & 15, r = tid >> 4;
-            const int p = r % P2, tf = r / P2, f = tf % nf, t = tf / nf;
+            const int p = r % P2, tf = r / P2, f = tf % nf;
+            int t = tf / nf;
+            int64_t orow = s0 + f, rows_per_t = n;  // output row of the frame within its tower's block
+            if (gstride > 0) {
+                const int64_t gi = (s0 + f) / gstride;
+                t += 2 * (int)gi;
+                orow = s0 + f - gi * gstride;
+                rows_per_t = gstride;
+            }
             int w[9], rows[16];
             window(cls + f * 49, p, w);
             tap_rows(w, rows);
@@ -117,7 +128,7 @@ __global__ __launch_bounds__(64 * FWD_WAVES) void k_conv2_lut_fwd(const uint32_t
                 acc.z += v[k].z;
                 acc.w += v[k].w;
             }
-            Z2[((size_t)t * n + s0 + f) * (P2 * 16) + p * 16 + q] = acc;
+            Z2[((size_t)t * rows_per_t + orow) * (P2 * 16) + p * 16 + q] = acc;
         }
         __builtin_amdgcn_wave_barrier();  // this group's classes consumed before restaging
     }
@@ -163,10 +174,12 @@ __device__ __forceinline__ long long to_fixed(float g, int K) {
 // codes here are the minibatch's own rows (the caller gathers them once), so a wave's group
 // of frames is one contiguous 128-B read; the next group's dZ2 slice and code words are
 // loaded into registers while the current group is accumulated.
+// grouped (gstride > 0): n = frames per tower, and tower t's frames are codes rows (t / 2) * gstride + [0, n)
 __global__ __launch_bounds__(64 * HIST_WAVES) void k_conv2_lut_hist(const uint32_t *__restrict__ codes, int64_t n,
                                                                    const float *__restrict__ dZ2c,
                                                                    const uint32_t *__restrict__ absmax, int fblocks,
-                                                                   unsigned long long *__restrict__ slabs) {
+                                                                   unsigned long long *__restrict__ slabs,
+                                                                   int64_t gstride) {
     __shared__ unsigned long long tab[HSLICE];
     __shared__ uint32_t words_all[HIST_WAVES][HIST_G * MERLIN_OBS_WORDS];
     // per frame, per parity type and 2x2-tile window origin (r, c) in 0..5: the type's table
@@ -176,6 +189,7 @@ __global__ __launch_bounds__(64 * HIST_WAVES) void k_conv2_lut_hist(const uint32
     __shared__ __align__(16) long long q_all[HIST_WAVES][HIST_G * P2 * HCH];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tc = blockIdx.x / fblocks, fb = blockIdx.x - tc * fblocks;  // tc = tower*16 + chunk
+    if (gstride > 0) codes += (size_t)(tc / NHCHUNK / 2) * gstride * MERLIN_OBS_WORDS;
     uint32_t *words = words_all[wv];
     uint16_t *rb = rb_all[wv];
     long long *qs = q_all[wv];
@@ -278,12 +292,12 @@ size_t conv2_lut_slab_bytes(int towers, int fblocks) {
 }
 
 hipError_t launch_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
-                                int towers, float *Z2, hipStream_t s) {
+                                int towers, float *Z2, hipStream_t s, int64_t gstride) {
     if (n <= 0) return hipSuccess;
     const int64_t groups = (n + FWD_G - 1) / FWD_G;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((groups + FWD_WAVES - 1) / FWD_WAVES, 256 * 8));
     hipLaunchKernelGGL(k_conv2_lut_fwd, dim3(grid), dim3(64 * FWD_WAVES), 0, s, codes, index, n,
-                       reinterpret_cast<const float4 *>(tables), towers, reinterpret_cast<float4 *>(Z2));
+                       reinterpret_cast<const float4 *>(tables), towers, reinterpret_cast<float4 *>(Z2), gstride);
     return hipGetLastError();
 }
 
@@ -293,12 +307,12 @@ int conv2_lut_fblocks(int64_t n) {
 }
 
 hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
-                                int towers, float *dT, void *slabs, hipStream_t s) {
+                                int towers, float *dT, void *slabs, hipStream_t s, int64_t gstride) {
     if (n <= 0) return hipMemsetAsync(dT, 0, sizeof(float) * towers * NROW * C2, s);
     const int fblocks = conv2_lut_fblocks(n);
     auto *sl = reinterpret_cast<unsigned long long *>(slabs);
     hipLaunchKernelGGL(k_conv2_lut_hist, dim3(towers * NHCHUNK * fblocks), dim3(64 * HIST_WAVES), 0, s, codes,
-                       n, dZ2c, absmax, fblocks, sl);
+                       n, dZ2c, absmax, fblocks, sl, gstride);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_conv2_lut_fold, dim3((towers * NROW * C2 + 255) / 256), dim3(256), 0, s, sl, absmax, n,

@@ -256,6 +256,191 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt(const float4 *__restri
 }
 
 // ---------------------------------------------------------------------------------------------
+// NT, interleaved: the same tiles, LDS images and numerics as k_x6_nt, but the staging of the next
+// k step (the A split + plane stores, the B chunk stores) and the global loads of the step after are
+// spread over the MFMA groups of the current step instead of running as one block before them: with
+// one barrier per k step every wave of a SIMD otherwise reaches its split at the same time and the
+// matrix pipe idles through it.  The loop body has no branches (the last steps stage/load clamped,
+// never-read data), so the scheduler sees one block per k step.  SCHED 1: sched_group_barrier pins an
+// MFMA / VALU / DS alternation; SCHED 2: additionally s_setprio 1 around the MFMA groups.
+template <int BM, int BN, int WGM, int WGN, int EPI, int SCHED>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt_il(const float4 *__restrict__ A, const u32x4 *__restrict__ B,
+                                                             int64_t M, int N, int K, int64_t sA, int64_t sB,
+                                                             const float *__restrict__ bias, float *__restrict__ C,
+                                                             int64_t sC, int tiles_n) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int FM = WTM / 16, FN = WTN / 16;
+    constexpr int UA = (BM * 4 + NT - 1) / NT;
+    constexpr int CB = (BN * CPR + NT - 1) / NT;
+    static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+    constexpr int PSA = BM * 4, PSB = BN * 4 + 12;
+    constexpr int STAGE = 3 * (PSA + PSB);
+    constexpr int NO = FM <= FN ? FN : FM;  // outer fragment loop: staging pieces go between its groups
+    static_assert(NO >= 2, "need two MFMA groups per k step");
+    __shared__ u32x4 lds[2 * STAGE];
+
+    const int t = blockIdx.y;
+    const int L = xcd_tile(blockIdx.x, gridDim.x);
+    const int tm = L / tiles_n, tn = L - tm * tiles_n;
+    const int64_t m0 = (int64_t)tm * BM;
+    const int n0 = tn * BN;
+    const int64_t rowA = K / 4;
+    const int64_t rowB = (int64_t)(K / 8) * 3;
+    A += t * sA;
+    B += t * sB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    const float4 *ga[UA];
+    int la[UA];
+#pragma unroll
+    for (int i = 0; i < UA; i++) {
+        const int q = tid + i * NT;
+        const int row = std::min(q >> 2, BM - 1), g = q & 3;
+        ga[i] = A + std::min<int64_t>(m0 + row, M - 1) * rowA + g * 2;
+        la[i] = row * 4 + (g ^ ((row >> 2) & 3));
+    }
+    const u32x4 *gb[CB];
+    int lb[CB];
+#pragma unroll
+    for (int i = 0; i < CB; i++) {
+        const int q = tid + i * NT;
+        const int row = q / CPR, rem = q - (q / CPR) * CPR, p = rem >> 2, g = rem & 3;
+        gb[i] = B + (int64_t)(n0 + std::min(row, BN - 1)) * rowB + g * 3 + p;
+        lb[i] = 3 * PSA + p * PSB + row * 4 + (g ^ ((row >> 2) & 3));
+    }
+    float4 ra[UA][2];
+    u32x4 rb[CB];
+    const int nk = K / BK;
+    auto load = [&](int kt) {
+        kt = std::min(kt, nk - 1);  // past the end: reload the last step (never stored to a read stage)
+#pragma unroll
+        for (int i = 0; i < UA; i++) {
+            ra[i][0] = ga[i][(int64_t)kt * 8];
+            ra[i][1] = ga[i][(int64_t)kt * 8 + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < CB; i++) rb[i] = gb[i][(int64_t)kt * CPR];
+    };
+    auto store_a = [&](u32x4 *st, int i) {
+        if ((BM * 4) % NT == 0 || i + 1 < UA || tid + i * NT < BM * 4) {
+            u32x4 p0, p1, p2;
+            split8(ra[i][0], ra[i][1], p0, p1, p2);
+            st[la[i]] = p0;
+            st[PSA + la[i]] = p1;
+            st[2 * PSA + la[i]] = p2;
+        }
+    };
+    auto store_b = [&](u32x4 *st, int i) {
+        if ((BN * CPR) % NT == 0 || i + 1 < CB || tid + i * NT < BN * CPR) st[lb[i]] = rb[i];
+    };
+    // staging piece o (0 .. NO-2) of the next step: A units and groups of 3 B chunks, round robin
+    constexpr int PIECES = UA + (CB + 2) / 3;
+    auto stage = [&](u32x4 *st, int o) {
+#pragma unroll
+        for (int i = 0; i < UA; i++)
+            if (i % (NO - 1) == o) store_a(st, i);
+#pragma unroll
+        for (int i = 0; i < CB; i++)
+            if ((UA + i / 3) % (NO - 1) == o) store_b(st, i);
+    };
+    (void)PIECES;
+    auto pin = [&]() {
+        if constexpr (SCHED >= 1) {
+            // per MFMA: one MFMA then two VALU; a DS write or read every few
+#pragma unroll
+            for (int q = 0; q < (FM <= FN ? FM : FN) * 6; q++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                if (q % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                if (q % 8 == 7) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+        }
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    const int fr = lane & 15, fc = (lane >> 4) ^ ((lane & 15) >> 2);
+    load(0);
+#pragma unroll
+    for (int i = 0; i < UA; i++) store_a(lds, i);
+#pragma unroll
+    for (int i = 0; i < CB; i++) store_b(lds, i);
+    load(1);
+    __syncthreads();
+    if constexpr (SCHED >= 2) __builtin_amdgcn_s_setprio(1);
+    for (int kt = 0; kt < nk; kt++) {
+        const int buf = kt & 1;
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * PSA;
+        u32x4 *st = lds + (buf ^ 1) * STAGE;
+        if constexpr (FM <= FN) {
+            u32x4 af[FM][3];
+#pragma unroll
+            for (int i = 0; i < FM; i++)
+#pragma unroll
+                for (int p = 0; p < 3; p++) af[i][p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                u32x4 bf[3];
+#pragma unroll
+                for (int p = 0; p < 3; p++) bf[p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
+#pragma unroll
+                for (int i = 0; i < FM; i++) acc[i][j] = mma6<true>(af[i], bf, acc[i][j]);
+                if (j < NO - 1)
+                    stage(st, j);
+                else
+                    load(kt + 2);
+                pin();
+            }
+        } else {
+            u32x4 bf[FN][3];
+#pragma unroll
+            for (int j = 0; j < FN; j++)
+#pragma unroll
+                for (int p = 0; p < 3; p++) bf[j][p] = sBl[p * PSB + (wn * WTN + j * 16 + fr) * 4 + fc];
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                u32x4 af[3];
+#pragma unroll
+                for (int p = 0; p < 3; p++) af[p] = sAl[p * PSA + (wm * WTM + i * 16 + fr) * 4 + fc];
+#pragma unroll
+                for (int j = 0; j < FN; j++) acc[i][j] = mma6<true>(af, bf[j], acc[i][j]);
+                if (i < NO - 1)
+                    stage(st, i);
+                else
+                    load(kt + 2);
+                pin();
+            }
+        }
+        __syncthreads();
+    }
+    if constexpr (SCHED >= 2) __builtin_amdgcn_s_setprio(0);
+
+    float *Ct = C + t * sC;
+#pragma unroll
+    for (int j = 0; j < FN; j++) {
+        const int col = n0 + wn * WTN + j * 16 + fr;
+        const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < FM; i++) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int64_t row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + r;
+                if (row < M) {
+                    const float v = acc[i][j][r];
+                    Ct[row * N + col] = EPI == 1 ? relu_nan(v + bv) : v;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // TN: slab[s][t][m][n] = sum_{k in [s*kc, min(Kd, (s+1)*kc))} A[t][k][m] B[t][k][n]; A fp32 [Kd][M],
 // B fp32 [Kd][N]; M % BM == 0, N % BN == 0, kc % 32 == 0.  grid (tiles_m * tiles_n, splits, T).
 // Plane image: [32 k rows][BM / 8 chunks], chunk index XOR tr_swz(row) so that a 32-lane half of
@@ -468,6 +653,23 @@ hipError_t nt_launch(const float4 *A, const u32x4 *B, int64_t M, int N, int K, i
     return hipGetLastError();
 }
 
+template <int BM, int BN, int WGM, int WGN, int SCHED>
+hipError_t nt_il_launch(const float4 *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
+                        const float *bias, float *C, int64_t sC, hipStream_t s) {
+    if (N % BN) return hipErrorInvalidValue;
+    const int64_t tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = N / BN;
+    if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(tiles_m * tiles_n), T);
+    if (bias)
+        hipLaunchKernelGGL((k_x6_nt_il<BM, BN, WGM, WGN, 1, SCHED>), grid, dim3(64 * WGM * WGN), 0, s, A, B, M, N, K,
+                           sA, sB, bias, C, sC, tiles_n);
+    else
+        hipLaunchKernelGGL((k_x6_nt_il<BM, BN, WGM, WGN, 0, SCHED>), grid, dim3(64 * WGM * WGN), 0, s, A, B, M, N, K,
+                           sA, sB, nullptr, C, sC, tiles_n);
+    return hipGetLastError();
+}
+
 template <int BM, int BN, int WGM, int WGN>
 hipError_t tn_launch(const float4 *A, const float4 *B, int64_t Kd, int M, int N, int T, int64_t sA, int64_t sB,
                      int splits, float *slab, float *out, hipStream_t s) {
@@ -516,6 +718,8 @@ hipError_t launch_x6_gemm_nt(const float *A, const void *B, int64_t M, int N, in
     if (K % BK || N <= 0) return hipErrorInvalidValue;
     // strides in values; B's planes: 3 chunks per 8 values
     if (a_stride % 4 || b_stride % 8) return hipErrorInvalidValue;
+    if (cfg >= 20)  // the 32x32x16 MFMA kernels (merlin_gemm2.hip)
+        return launch_x6_gemm_nt32(A, B, M, N, K, T, a_stride, b_stride, bias, C, c_stride, cfg, s);
     const float4 *a = reinterpret_cast<const float4 *>(A);
     const u32x4 *b = static_cast<const u32x4 *>(B);
     const int64_t sA = a_stride / 4, sB = b_stride / 8 * 3;
@@ -527,6 +731,16 @@ hipError_t launch_x6_gemm_nt(const float *A, const void *B, int64_t M, int N, in
         // unchunked accumulation (all six products straight into the running sum): ~2-6 % faster,
         // error of the order of an fp32 fma chain (scripts/probe_x6.py); not used
         case 4: return nt_launch<256, 128, 4, 2, false>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        // interleaved staging (k_x6_nt_il): fwd / dgrad tiles, SCHED 0 / 1 / 2
+        case 10: return nt_il_launch<256, 128, 4, 2, 0>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 11: return nt_il_launch<256, 128, 4, 2, 1>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 12: return nt_il_launch<256, 128, 4, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 13: return nt_il_launch<128, 192, 2, 4, 0>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 14: return nt_il_launch<128, 192, 2, 4, 1>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 15: return nt_il_launch<128, 192, 2, 4, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        // one wave per SIMD: 256 x 128 over 4 waves (128 x 64 each)
+        case 16: return nt_il_launch<256, 128, 2, 2, 0>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 17: return nt_il_launch<256, 128, 2, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         default: return hipErrorInvalidValue;
     }
 }

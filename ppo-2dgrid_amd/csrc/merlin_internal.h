@@ -99,9 +99,9 @@ int conv2_lut_rows();
 int conv2_lut_fblocks(int64_t n);
 size_t conv2_lut_slab_bytes(int towers, int fblocks);
 hipError_t launch_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int64_t n, const float *tables,
-                                int towers, float *Z2, hipStream_t s);
+                                int towers, float *Z2, hipStream_t s, int64_t gstride = 0);
 hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
-                                int towers, float *dT, void *slabs, hipStream_t s);
+                                int towers, float *dT, void *slabs, hipStream_t s, int64_t gstride = 0);
 
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
@@ -119,6 +119,8 @@ hipError_t launch_ppo_loss(const float *logits, const float *value, const float 
                            double *workspace, hipStream_t s);
 hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, const float *b3, int T, float *Y3,
                               hipStream_t s);
+hipError_t launch_x6_gemm_nt32(const float *A, const void *B, int64_t M, int N, int K, int T, int64_t a_stride,
+                               int64_t b_stride, const float *bias, float *C, int64_t c_stride, int cfg, hipStream_t s);
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill, int role,

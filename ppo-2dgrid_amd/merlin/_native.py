@@ -88,6 +88,10 @@ def lib():
     L.merlin_tower_conv2_lut_rows.restype = C.c_int
     L.merlin_tower_conv2_lut_fwd.argtypes = [vp, vp, i64, vp, i32, vp, vp]
     L.merlin_tower_conv2_lut_bwd.argtypes = [vp, i64, vp, vp, i32, vp, vp]
+    L.merlin_tower_conv2_lut_fwd_grouped.argtypes = [vp, i64, i64, vp, i32, vp, vp]
+    L.merlin_tower_conv2_lut_slab_bytes.argtypes = [i32, i64]
+    L.merlin_tower_conv2_lut_slab_bytes.restype = i64
+    L.merlin_tower_conv2_lut_bwd_grouped.argtypes = [vp, i64, vp, vp, i32, vp, vp, vp]
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp]
@@ -149,7 +153,8 @@ EXPORTED_SYMBOLS = (
     "merlin_conv1_lut_fwd", "merlin_conv1_lut_bwd", "merlin_tower_conv2_im2col_fwd",
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
-    "merlin_tower_conv2_lut_bwd", "merlin_tower_window_lut", "merlin_tower_window_conv3",
+    "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
+    "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_tower_colsum",
@@ -394,6 +399,42 @@ def conv2_lut_fwd(codes, index, tables):
         check(lib().merlin_tower_conv2_lut_fwd(ptr(codes), ptr(index), n, ptr(tables), T, ptr(out),
                                                stream_of(codes)), "merlin_tower_conv2_lut_fwd")
     return out
+
+
+def conv2_lut_fwd_grouped(codes, tables, group_frames: int):
+    """Grouped conv2_lut_fwd: codes int32 [G * group_frames, 8] (group g's frames contiguous), tables
+    f32 [2G, 2720, 64] (towers 2g / 2g+1 = group g's actor / critic) -> Z2 f32 [2G, group_frames*25, 64]."""
+    T = int(tables.shape[0])
+    n = int(codes.shape[0])
+    assert T % 2 == 0 and n == (T // 2) * group_frames, (T, n, group_frames)
+    assert tables.shape == (T, LUT2_ROWS, 64) and tables.dtype == torch.float32 and tables.is_contiguous()
+    assert codes.dtype == torch.int32 and codes.shape[-1] == OBS_WORDS and codes.is_contiguous()
+    out = torch.empty((T, group_frames * 25, 64), dtype=torch.float32, device=codes.device)
+    with KernelTimer.span("k_conv2_lut_fwd", n * (2 * 25 * 64 * 4 + 32)):
+        check(lib().merlin_tower_conv2_lut_fwd_grouped(ptr(codes), n, int(group_frames), ptr(tables), T, ptr(out),
+                                                       stream_of(codes)), "merlin_tower_conv2_lut_fwd_grouped")
+    return out
+
+
+_SLABS = {}
+
+
+def conv2_lut_bwd_grouped(codes, dZ2c, absmax):
+    """Grouped conv2_lut_bwd: dtables f32 [2G, 2720, 64] from chunk-major dZ2c f32 [2G, 16, F*25, 4]
+    (F = frames per group) of frames codes [G * F, 8] (group g's rows contiguous)."""
+    T = int(dZ2c.shape[0])
+    F = int(dZ2c.shape[2]) // 25
+    assert codes.dtype == torch.int32 and codes.shape == ((T // 2) * F, OBS_WORDS) and codes.is_contiguous()
+    nbytes = int(lib().merlin_tower_conv2_lut_slab_bytes(T, F))
+    key = dZ2c.device
+    slabs = _SLABS.get(key)
+    if slabs is None or slabs.numel() < nbytes:
+        slabs = _SLABS[key] = torch.empty(nbytes, dtype=torch.uint8, device=dZ2c.device)
+    dt = torch.empty((T, LUT2_ROWS, 64), dtype=torch.float32, device=dZ2c.device)
+    with KernelTimer.span("k_conv2_lut_hist", F * (T * 25 * 64 * 4 + 16 * T * 32)):
+        check(lib().merlin_tower_conv2_lut_bwd_grouped(ptr(codes), F, ptr(dZ2c), ptr(absmax), T, ptr(dt), ptr(slabs),
+                                                       stream_of(dZ2c)), "merlin_tower_conv2_lut_bwd_grouped")
+    return dt
 
 
 def conv2_lut_bwd(codes, dZ2c, absmax=None):
@@ -649,7 +690,9 @@ def act_heads(z, b4, w_actor, b_actor, w_critic, b_critic, deterministic=False, 
 # -- fc1 on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip) ------------------
 # Weights as int16 planes [..., R, 3 * C] (bf16 bits; per group of 8 values three 16-B chunks,
 # x = x0 + x1 + x2 exactly, include/merlin_hip.h); activations as fp32, split while staged.
-X6_NT_CFG = {"fwd": 0, "dgrad": 1, "rollout": 2}  # tile configurations of merlin_x6_gemm_nt (N = 512 / 576), scripts/probe_x6.py
+# fwd / dgrad on the 32x32x16 MFMA with split hi / lo accumulators (csrc/merlin_gemm2.hip: 806 / 790 us
+# against 857 / 843 for the 16x16x32 kernels at the update's shape, scripts/probe_x6_il.py)
+X6_NT_CFG = {"fwd": 20, "dgrad": 22, "rollout": 2}  # tile configurations of merlin_x6_gemm_nt (N = 512 / 576)
 X6_TN_CFG = 0
 X6_TN_SPLITS = 32
 

@@ -195,20 +195,20 @@ def bias_relu_bmm(X, W, b):
     return out
 
 
-def _splitk_bmm_tn(X, dY, chunks):
+def _splitk_bmm_tn(X, dY, chunks, min_chunk=1024, name="gemm_wgrad"):
     """X^T @ dY for X [T, M, K], dY [T, M, N] with the long M reduction split into `chunks`
     batched GEMMs plus a sum: hipBLASLt runs the plain tall-skinny product at about half the
     FP32 rate on these shapes (scripts/probe_gemm2.py), the split form at ~105-125 TFLOP/s."""
     T, M, K = X.shape
     N = dY.shape[2]
     c = M // chunks
-    if chunks <= 1 or c < 1024:
-        with _gemm_span("gemm_wgrad", T, K, N, M):
+    if chunks <= 1 or c < min_chunk:
+        with _gemm_span(name, T, K, N, M):
             return torch.bmm(X.transpose(1, 2), dY)
     # per tower the first c*chunks rows are a view [chunks, c, K] (merging the tower and chunk
     # dims would copy both operands whenever M % chunks != 0: 2 x 0.1 ms per call at the bench size)
     part = X.new_empty((T, chunks, K, N))
-    with _gemm_span("gemm_wgrad", T, K, N, c * chunks):
+    with _gemm_span(name, T, K, N, c * chunks):
         for t in range(T):
             torch.bmm(X[t, : c * chunks].view(chunks, c, K).transpose(1, 2), dY[t, : c * chunks].view(chunks, c, N),
                       out=part[t])
@@ -334,23 +334,25 @@ class _Conv2Tables(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, P, b1, W2, G, part):
+        T = P.shape[0]  # 2 towers (or 2 per group: merlin/grouped_policy.py)
         HT = torch.matmul(G, P.transpose(1, 2))
         HT = torch.relu_(HT.add_(b1.unsqueeze(1)))
-        Wall = W2.reshape(2, 64, 32, 2, 2, 2, 2).permute(0, 2, 4, 6, 3, 5, 1).reshape(2, 32, 1024)
-        X = torch.bmm(HT, Wall).view(2, -1, 4, 256)
+        Wall = W2.reshape(T, 64, 32, 2, 2, 2, 2).permute(0, 2, 4, 6, 3, 5, 1).reshape(T, 32, 1024)
+        X = torch.bmm(HT, Wall).view(T, -1, 4, 256)
         ar = torch.arange(part.numel(), device=part.device)
         ctx.save_for_backward(HT, Wall, G, part, ar)
-        return X[:, ar, part].reshape(2, -1, 64)
+        return X[:, ar, part].reshape(T, -1, 64)
 
     @staticmethod
     def backward(ctx, dT2):
         HT, Wall, G, part, ar = ctx.saved_tensors
         V = part.numel()
-        dX = dT2.new_zeros((2, V, 4, 256))
-        dX[:, ar, part] = dT2.reshape(2, V, 256)
-        dX = dX.view(2, V, 1024)
+        T = HT.shape[0]
+        dX = dT2.new_zeros((T, V, 4, 256))
+        dX[:, ar, part] = dT2.reshape(T, V, 256)
+        dX = dX.view(T, V, 1024)
         dWall = torch.bmm(HT.transpose(1, 2), dX)
-        dW2 = dWall.view(2, 32, 2, 2, 2, 2, 64).permute(0, 6, 1, 4, 2, 5, 3).reshape(2, 64, 32, 4, 4)
+        dW2 = dWall.view(T, 32, 2, 2, 2, 2, 64).permute(0, 6, 1, 4, 2, 5, 3).reshape(T, 64, 32, 4, 4)
         dH = torch.bmm(dX, Wall.transpose(1, 2)).mul_(HT > 0)
         return torch.matmul(dH.transpose(1, 2), G), dH.sum(1), dW2, None, None
 

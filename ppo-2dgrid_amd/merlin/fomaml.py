@@ -12,10 +12,13 @@ Reference semantics kept (src/fomaml.py:9-223):
     gradient (:187-202); meta gradient / n_tasks, clip_grad_norm_(0.5), Adam(lr_outer)
     (:207-212); returns (avg query loss, avg query episode reward, avg query episode
     length, the last task's query stats) (:214-223).
-MI355X batching: the support rollouts of all tasks run with the meta weights in one vector
-env (fast == meta before the inner step); the per-task fast policies are stacked tensors
-(merlin.batched_policy), so the inner step, the query rollouts and the query gradients of
-all tasks are single batched launches; GAE is the HIP kernel ([k][tasks] layout).
+MI355X batching: every task's policy is a set of stacked tensors [G, *shape] (merlin.batched_policy
+.stack_params) run on the tile-code path with one tower pair per task (merlin.grouped_policy: per-task
+conv2 tables, grouped table lookups, batched GEMMs), so both rollouts, the inner step and the query
+gradients of all tasks are single batched launches; GAE is the HIP kernel ([k][tasks] layout).  Each
+rollout (reset + k x (act -> env step) + bootstrap value) is recorded once as a HIP graph and replayed
+with the weights refreshed in place; the draws are the Gumbel-max form of Categorical(logits).sample()
+on torch's generator (every replay draws afresh).
 """
 from __future__ import annotations
 
@@ -25,11 +28,9 @@ import torch.optim as optim
 
 from . import _native as nat
 from . import batched_policy as bp
+from . import grouped_policy as gp
 from .actor_critic import CNNActorCritic
 from .envs import MerlinVecEnv
-
-INV255 = 1.0 / 255.0
-
 
 class FOMAML:
     def __init__(self, scenario_creator, lr_inner=0.01, lr_outer=3e-4, device="cuda", difficulty="medium"):
@@ -45,6 +46,9 @@ class FOMAML:
         self.gamma, self.lam = 0.995, 0.95
         self.vf_coef, self.ent_coef, self.clip_eps = 0.5, 0.05, 0.2
         self._env = None
+        self._task_seeds = None
+        self._rollouts = {}  # per rollout kind: storage, weight pack and its captured HIP graph
+        self.rollout_graph = True
 
     # ------------------------------------------------------------------ envs
     def _task_env(self, task_seeds) -> MerlinVecEnv:
@@ -53,45 +57,76 @@ class FOMAML:
             if self._env is not None:
                 self._env.close()
             self._env = MerlinVecEnv(G, device=self.device, reseed_each_reset=True, **self.env_kwargs)
-        self._env.seed_each(np.asarray(task_seeds, dtype=np.uint64))
+        self._task_seeds = np.asarray(task_seeds, dtype=np.uint64)
+        self._env.seed_each(self._task_seeds)
         return self._env
 
     # ------------------------------------------------------------ rollouts
-    @torch.no_grad()
-    def collect_trajectory(self, env: MerlinVecEnv, params, steps: int):
-        """k steps of every task in parallel (collect_trajectory, src/fomaml.py:54-108).
-        params: stacked per-task weights (bp.stack_params) or None for the meta policy."""
-        G = env.num_envs
+    def _rollout_state(self, key, G, steps, params):
+        st = self._rollouts.get(key)
+        if st is not None and st["G"] == G and st["steps"] == steps:
+            return st
         dev = self.device
-        codes = torch.empty((steps + 1, G, 8), dtype=torch.int32, device=dev)
-        act = torch.empty((steps, G), dtype=torch.int64, device=dev)
-        logp = torch.empty((steps, G), dtype=torch.float32, device=dev)
-        val = torch.empty((steps, G), dtype=torch.float32, device=dev)
-        rew = torch.empty((steps, G), dtype=torch.float32, device=dev)
-        done = torch.empty((steps, G), dtype=torch.float32, device=dev)
-        epr = torch.empty((steps, G), dtype=torch.float64, device=dev)
-        epl = torch.empty((steps, G), dtype=torch.int32, device=dev)
-        env.reset(out=codes[0])  # = env.reset(seed=task_seed)
-        frames = torch.empty((G, 3, 56, 56), dtype=torch.float32, device=dev)
+        st = {"G": G, "steps": steps, "graph": None,
+              "codes": torch.zeros((steps + 1, G, 8), dtype=torch.int32, device=dev),
+              "act": torch.zeros((steps, G), dtype=torch.int64, device=dev),
+              "logp": torch.zeros((steps, G), dtype=torch.float32, device=dev),
+              "val": torch.zeros((steps, G), dtype=torch.float32, device=dev),
+              "rew": torch.zeros((steps, G), dtype=torch.float32, device=dev),
+              "done": torch.zeros((steps, G), dtype=torch.float32, device=dev),
+              "epr": torch.zeros((steps, G), dtype=torch.float64, device=dev),
+              "epl": torch.zeros((steps, G), dtype=torch.int32, device=dev),
+              "last": torch.zeros(G, dtype=torch.float32, device=dev),
+              "pack": gp.pack(params)}
+        self._rollouts[key] = st
+        return st
+
+    def _rollout_body(self, env, st):
+        steps = st["steps"]
+        pk = st["pack"]
+        env.reset(out=st["codes"][0])  # = env.reset(seed=task_seed) for every task
         for t in range(steps):
-            if params is None:
-                a, lp, v = self.meta_policy.act_codes(codes[t])
-            else:
-                nat.expand_obs(codes[t], out=frames, scale=INV255)
-                a, lp, v = bp.act(params, frames.unsqueeze(1))
-                a, lp, v = a[:, 0], lp[:, 0], v[:, 0]
-            act[t], logp[t], val[t] = a, lp, v
-            env.step_into(act[t], codes[t + 1], rew[t], None, None, done[t], epr[t], epl[t])
+            gp.act_packed(pk, st["codes"][t], out=(st["act"][t], st["logp"][t], st["val"][t]))
+            env.step_into(st["act"][t], st["codes"][t + 1], st["rew"][t], None, None, st["done"][t], st["epr"][t],
+                          st["epl"][t])
+        _, _, last = gp.act_packed(pk, st["codes"][steps])
+        st["last"].copy_(last)
+
+    @torch.no_grad()
+    def collect_trajectory(self, env: MerlinVecEnv, params, steps: int, key: str = "rollout"):
+        """k steps of every task in parallel (collect_trajectory, src/fomaml.py:54-108), each task acting
+        with its own weights params[name] [G, *shape] (None: the meta policy for every task).  The first
+        call per key records the rollout as a HIP graph; later calls refresh the weights in place and
+        replay it."""
+        G = env.num_envs
         if params is None:
-            _, _, last = self.meta_policy.act_codes(codes[steps])
+            params = {n: p.detach().unsqueeze(0).expand(G, *p.shape) for n, p in self.meta_policy.named_parameters()}
+        st = self._rollout_state(key, G, steps, params)
+        if st["graph"] is None:
+            gp.pack_into(st["pack"], params)
+            self._rollout_body(env, st)
+            if self.rollout_graph:
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                try:
+                    with torch.cuda.graph(g):
+                        self._rollout_body(env, st)
+                    st["graph"] = g
+                except Exception:  # keep launching eagerly
+                    self.rollout_graph = False
+                    torch.cuda.synchronize(self.device)
+                # the capture recorded the launches without running them: the rollout returned is a
+                # replay (every rollout starts with the reset to the task seeds)
+                if st["graph"] is not None:
+                    st["graph"].replay()
         else:
-            nat.expand_obs(codes[steps], out=frames, scale=INV255)
-            _, _, last = bp.act(params, frames.unsqueeze(1))
-            last = last[:, 0]
+            gp.pack_into(st["pack"], params)
+            st["graph"].replay()
         env.errors()
-        d = done > 0
-        return {"codes": codes, "act": act, "logp": logp, "val": val, "rew": rew, "done": done, "last_val": last,
-                "ep_rews": epr[d].cpu().tolist(), "ep_lens": epl[d].cpu().tolist()}
+        d = st["done"] > 0
+        return {"codes": st["codes"], "act": st["act"], "logp": st["logp"], "val": st["val"], "rew": st["rew"],
+                "done": st["done"], "last_val": st["last"], "ep_rews": st["epr"][d].cpu().tolist(),
+                "ep_lens": st["epl"][d].cpu().tolist()}
 
     # ---------------------------------------------------------------- loss
     def compute_loss(self, batch, params):
@@ -101,9 +136,8 @@ class FOMAML:
                          batch["last_val"].float().contiguous(), self.gamma, self.lam)
         adv_n = (adv - adv.mean(dim=0, keepdim=True)) / (adv.std(dim=0, keepdim=True) + 1e-8)  # per task
         ret = (batch["val"] + adv_n).detach()
-        frames = nat.expand_obs(batch["codes"][:k].reshape(k * G, 8), scale=INV255)
-        frames = frames.view(k, G, 3, 56, 56).transpose(0, 1)  # [G, k, ...]
-        new_logp, ent, new_val = bp.evaluate(params, frames, batch["act"].t())
+        codes = batch["codes"][:k].transpose(0, 1).reshape(G * k, 8).contiguous()  # task-major
+        new_logp, ent, new_val = gp.evaluate(params, codes, k, batch["act"].t())
         old_logp = batch["logp"].t()
         a_t, r_t = adv_n.t(), ret.t()
         ratio = torch.exp(new_logp - old_logp)
@@ -138,7 +172,7 @@ class FOMAML:
         self.meta_optimizer.zero_grad()
         names = [n for n, _ in self.meta_policy.named_parameters()]
         # inner loop: all fast policies start as the meta policy -> batched support rollout
-        support = self.collect_trajectory(env, None, k_support)
+        support = self.collect_trajectory(env, None, k_support, key="support")
         fast = bp.stack_params(self.meta_policy, G)
         loss_s, _ = self.compute_loss(support, fast)
         grads = dict(zip(names, torch.autograd.grad(loss_s, [fast[n] for n in names])))
@@ -146,7 +180,7 @@ class FOMAML:
         with torch.no_grad():
             adapted = {n: (fast[n] - self.lr_inner * grads[n]).detach().requires_grad_(True) for n in names}
         # outer loop: query rollouts with each task's adapted policy
-        query = self.collect_trajectory(env, adapted, k_query)
+        query = self.collect_trajectory(env, adapted, k_query, key="query")
         loss_q, qstats = self.compute_loss(query, adapted)
         qgrads = torch.autograd.grad(loss_q, [adapted[n] for n in names])
         for (n, p), g in zip(self.meta_policy.named_parameters(), qgrads):

@@ -391,6 +391,30 @@ class _TunedBmm(torch.autograd.Function):
         return dA, dB
 
 
+class _WindowGemm(torch.autograd.Function):
+    """Q = a2w @ W3r over both towers (a2w [T, windows, 64], W3r [T, 64, 576]); backward da2w = dQ W3r^T
+    and dW3r = a2w^T dQ, the latter split over 256-window chunks: its output is only 64 x 576 per tower,
+    so hipBLASLt's plain form runs ~36 workgroups over the ~6.6k-deep reduction (280 us per minibatch in
+    profiles/r03a_step_sequence.md, on the critical path); the split form fills the chip."""
+
+    @staticmethod
+    def forward(ctx, a2w, W3r):
+        ctx.save_for_backward(a2w, W3r)
+        return torch.bmm(a2w, W3r)
+
+    @staticmethod
+    def backward(ctx, dQ):
+        from .actor_critic import _splitk_bmm_tn
+
+        a2w, W3r = ctx.saved_tensors
+        dQ = dQ.contiguous()
+        da2w = torch.bmm(dQ, W3r.transpose(1, 2)) if ctx.needs_input_grad[0] else None
+        chunks = max(1, a2w.shape[1] // 256)
+        dW3r = _splitk_bmm_tn(a2w, dQ, chunks, min_chunk=128, name="gemm_window_wgrad") if ctx.needs_input_grad[1] \
+            else None
+        return da2w, dW3r
+
+
 class _WindowConv3(torch.autograd.Function):
     """Y3 [2, U*9, 64] = relu(conv3) rows (u, p3) of the minibatch's distinct frames, from Q."""
 
@@ -561,7 +585,7 @@ def window_tower_head_x6(ac, plan: WindowPlan, mb: MinibatchWindows, head_bias: 
     Z2w = _WindowConv2.apply(ac.conv2_tables(), plan, plan.num_windows)
     a2w = _BiasRelu.apply(Z2w, torch.stack([ea[2].bias, ec[2].bias]))
     W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
-    Q = torch.bmm(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
+    Q = _WindowGemm.apply(a2w, W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576))  # [2, windows, (ky, kx, co)]
     fa, fc = ac.actor[0], ac.critic[0]
     W4 = torch.stack([fa.weight, fc.weight])  # [2, hidden, 576] in (co, p3) order
     W4p = W4.view(2, W4.shape[1], 64, 9).transpose(2, 3).reshape(2, W4.shape[1], 576)

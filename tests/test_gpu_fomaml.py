@@ -66,8 +66,8 @@ def test_meta_step_matches_serial_reference(device):
     recorded = []
     orig = fm.collect_trajectory
 
-    def rec(env, params, steps):
-        b = orig(env, params, steps)
+    def rec(env, params, steps, **kw):
+        b = orig(env, params, steps, **kw)
         recorded.append(b)
         return b
 

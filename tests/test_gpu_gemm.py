@@ -37,7 +37,8 @@ def test_split_is_exact(device):
     assert torch.equal(p0.view(torch.bfloat16), x.to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 3)])
+@pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 3), (512, 576, 20),
+                                     (576, 512, 22), (512, 576, 21), (576, 512, 23)])
 @pytest.mark.parametrize("M", [1, 777, 20011])
 def test_gemm_nt_vs_float64(device, M, N, K, cfg):
     from merlin import _native as nat
