@@ -752,6 +752,16 @@ hipError_t launch_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int M, 
     if (M <= 0 || N <= 0) return hipSuccess;
     if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
     if (Kd <= 0) return hipMemsetAsync(out, 0, sizeof(float) * (size_t)T * M * N, s);
+    if (cfg >= 20) {  // the 32x32x16 MFMA kernels (merlin_gemm2.hip), then the same fold
+        int S = 1;
+        hipError_t e = launch_x6_gemm_tn32(A, B, Kd, M, N, T, a_stride, b_stride, splits, slab, cfg, s, &S);
+        if (e != hipSuccess) return e;
+        const int64_t total4 = (int64_t)T * M * N / 4;
+        const int grid = (int)std::min<int64_t>((total4 + 255) / 256, 256 * 8);
+        hipLaunchKernelGGL(k_x6_fold, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4 *>(slab), S, total4,
+                           reinterpret_cast<float4 *>(out));
+        return hipGetLastError();
+    }
     const float4 *a = reinterpret_cast<const float4 *>(A), *b = reinterpret_cast<const float4 *>(B);
     const int64_t sA = a_stride / 4, sB = b_stride / 4;
     switch (cfg) {

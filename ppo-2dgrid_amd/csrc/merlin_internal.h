@@ -121,6 +121,8 @@ hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, 
                               hipStream_t s);
 hipError_t launch_x6_gemm_nt32(const float *A, const void *B, int64_t M, int N, int K, int T, int64_t a_stride,
                                int64_t b_stride, const float *bias, float *C, int64_t c_stride, int cfg, hipStream_t s);
+hipError_t launch_x6_gemm_tn32(const float *A, const float *B, int64_t Kd, int M, int N, int T, int64_t a_stride,
+                               int64_t b_stride, int splits, float *slab, int cfg, hipStream_t s, int *S_out);
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill, int role,

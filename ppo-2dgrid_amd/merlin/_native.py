@@ -570,41 +570,47 @@ def bias_relu_(z, bias):
     return z
 
 
-def relu_bwd(y, dy, out=None):
+def relu_bwd(y, dy, out=None, out_bias=None):
     """(dz, dbias): dz = [y > 0] * dy (out may be dy itself), dbias f32[T, cols] = column sums of dz."""
     T, rows, cols = (int(x) for x in y.shape)
     assert dy.shape == y.shape and y.dtype == dy.dtype == torch.float32
     dz = torch.empty_like(dy) if out is None else out
-    db = torch.empty((T, cols), dtype=torch.float32, device=y.device)
+    db = torch.empty((T, cols), dtype=torch.float32, device=y.device) if out_bias is None else out_bias
+    assert db.shape == (T, cols) and db.is_contiguous()
     with KernelTimer.span("k_relu_bwd_colsum", 3 * y.numel() * 4):
         check(lib().merlin_tower_relu_bwd(ptr(y), ptr(dy), ptr(dz), rows, cols, T, ptr(db), stream_of(y)),
               "merlin_tower_relu_bwd")
     return dz, db
 
 
-def colsum(x):
+def colsum(x, out=None):
     """x f32[T, rows, cols] (rows may be strided, columns contiguous) -> f32[T, cols] column sums (fixed
     order)."""
     T, rows, cols = (int(v) for v in x.shape)
     assert x.dtype == torch.float32 and x.stride(2) == 1 and x.is_cuda
-    out = torch.empty((T, cols), dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty((T, cols), dtype=torch.float32, device=x.device)
+    assert out.shape == (T, cols) and out.is_contiguous()
     with KernelTimer.span("k_colsum", T * rows * cols * 4):
         check(lib().merlin_tower_colsum(C.c_void_p(x.data_ptr()), rows, cols, int(x.stride(1)), int(x.stride(0)), T,
                                         ptr(out), stream_of(x)), "merlin_tower_colsum")
     return out
 
 
-def head_bwd(h, dlogits, dvalue, w_actor, w_critic):
+def head_bwd(h, dlogits, dvalue, w_actor, w_critic, out_bias=None, out_w_actor=None, out_w_critic=None):
     """Heads backward through fc1's ReLU: h f32[2, n, H] = relu(fc1) of both towers, dlogits
     f32[n, A], dvalue f32[n], w_actor f32[A, H], w_critic f32[1, H] or [H] ->
-    (dz f32[2, n, H], dbias f32[2, H], dw_actor f32[A, H], dw_critic f32[H])."""
+    (dz f32[2, n, H], dbias f32[2, H], dw_actor f32[A, H], dw_critic f32[H]); the out_* tensors, when
+    given, receive the bias / head-weight gradients (e.g. views of a flat gradient buffer)."""
     _, n, H = (int(x) for x in h.shape)
     A = int(w_actor.shape[0])
     assert h.shape[0] == 2 and dlogits.shape == (n, A) and dvalue.numel() == n and w_critic.numel() == H
     dz = torch.empty_like(h)
-    db = torch.empty((2, H), dtype=torch.float32, device=h.device)
-    dwa = torch.empty((A, H), dtype=torch.float32, device=h.device)
-    dwc = torch.empty((H,), dtype=torch.float32, device=h.device)
+    db = torch.empty((2, H), dtype=torch.float32, device=h.device) if out_bias is None else out_bias
+    dwa = torch.empty((A, H), dtype=torch.float32, device=h.device) if out_w_actor is None else out_w_actor
+    dwc = torch.empty((H,), dtype=torch.float32, device=h.device) if out_w_critic is None else out_w_critic
+    assert db.shape == (2, H) and dwa.shape == (A, H) and dwc.numel() == H
+    assert db.is_contiguous() and dwa.is_contiguous() and dwc.is_contiguous()
     with KernelTimer.span("k_head_bwd", 2 * h.numel() * 4 + n * (A + 1) * 4):
         check(lib().merlin_tower_head_bwd(ptr(h), ptr(dlogits), ptr(dvalue), ptr(w_actor), ptr(w_critic), n, H, A,
                                           ptr(dz), ptr(db), ptr(dwa), ptr(dwc), stream_of(h)), "merlin_tower_head_bwd")
@@ -613,7 +619,7 @@ def head_bwd(h, dlogits, dvalue, w_actor, w_critic):
 
 # -- PPO loss (csrc/merlin_loss.hip) -------------------------------------------------------------
 def ppo_loss(logits, value, offs, order, frame_of, sample_index, actions, logp_old, adv, ret, clip_eps, vf_coef,
-             ent_coef, stats=None, bias_actor=None, bias_critic=None):
+             ent_coef, stats=None, bias_actor=None, bias_critic=None, out_bias_actor=None, out_bias_critic=None):
     """(loss f32[], dlogits f32[U, A], dvalue f32[U], dbias_actor f32[A] | None, dbias_critic f32[1] |
     None): the PPO minibatch loss of src/ppo.py:136-150 over the samples of U distinct frames (CSR
     offs int32[U+1] / order int32[n], frame_of int64[n] = the frame of sample i; sample i reads
@@ -638,11 +644,13 @@ def ppo_loss(logits, value, offs, order, frame_of, sample_index, actions, logp_o
     if bias_actor is not None:
         assert bias_actor.shape == (A,) and bias_actor.dtype == torch.float32
         bias_actor = bias_actor.detach().contiguous()
-        dba = torch.empty((A,), dtype=torch.float32, device=dev)
+        dba = torch.empty((A,), dtype=torch.float32, device=dev) if out_bias_actor is None else out_bias_actor
+        assert dba.shape == (A,) and dba.is_contiguous()
     if bias_critic is not None:
         assert bias_critic.numel() == 1 and bias_critic.dtype == torch.float32
         bias_critic = bias_critic.detach().contiguous()
-        dbc = torch.empty((1,), dtype=torch.float32, device=dev)
+        dbc = torch.empty((1,), dtype=torch.float32, device=dev) if out_bias_critic is None else out_bias_critic
+        assert dbc.numel() == 1 and dbc.is_contiguous()
     ws = torch.empty(max(int(lib().merlin_ppo_loss_workspace(n)), 1), dtype=torch.float64, device=dev)
     with KernelTimer.span("k_ppo_loss", U * (4 * A + 4) * 2 + n * (4 + 8 + 8 + 12)):
         check(lib().merlin_ppo_loss(ptr(logits.contiguous()), ptr(value.contiguous()), ptr(bias_actor),
@@ -721,8 +729,13 @@ def x6_gemm_nt(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = Non
     """C f32[T, M, N] = A @ B^T per tower (+ bias[t] and ReLU when bias is given), A f32[T, M, K],
     B planes int16[T, N, 3K] (x6_split of an f32 [T, N, K])."""
     T, M, K = (int(v) for v in A.shape)
+    if A.dtype == torch.int16:  # A as planes too (x6_split of an f32 [T, M, K]): the cfg >= 30 kernels
+        assert cfg >= 30 and K % 24 == 0, "planes A needs an x6 planes-A configuration (cfg >= 30)"
+        K //= 3
+    else:
+        assert A.dtype == torch.float32 and cfg < 30
     N = int(B.shape[1])
-    assert A.dtype == torch.float32 and B.dtype == torch.int16 and B.shape == (T, N, 3 * K)
+    assert B.dtype == torch.int16 and B.shape == (T, N, 3 * K)
     assert A.is_contiguous() and B.is_contiguous()
     if bias is not None:
         assert bias.shape == (T, N) and bias.dtype == torch.float32
@@ -737,14 +750,22 @@ def x6_gemm_nt(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = Non
 
 
 def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int = X6_TN_SPLITS, cfg: int = X6_TN_CFG,
-               name: str = "x6_gemm_tn") -> torch.Tensor:
+               name: str = "x6_gemm_tn", out: torch.Tensor | None = None) -> torch.Tensor:
     """out f32[T, M, N] = A^T @ B per tower, A f32[T, Kd, M], B f32[T, Kd, N] (the long k range split
     into `splits` slabs summed in order)."""
     T, Kd, M = (int(v) for v in A.shape)
     N = int(B.shape[2])
-    assert A.dtype == B.dtype == torch.float32 and B.shape[:2] == (T, Kd)
+    if A.dtype == torch.int16:  # both operands as planes (x6_split of f32 [T, Kd, M] / [T, Kd, N]): cfg >= 30
+        assert B.dtype == torch.int16 and cfg >= 30 and M % 24 == 0 and N % 24 == 0
+        M //= 3
+        N //= 3
+    else:
+        assert A.dtype == B.dtype == torch.float32 and cfg < 30
+    assert B.shape[:2] == (T, Kd)
     assert A.is_contiguous() and B.is_contiguous()
-    out = torch.empty((T, M, N), dtype=torch.float32, device=A.device)
+    if out is None:
+        out = torch.empty((T, M, N), dtype=torch.float32, device=A.device)
+    assert out.shape == (T, M, N) and out.dtype == torch.float32 and out.is_contiguous()
     slab = torch.empty(int(lib().merlin_x6_tn_slab_floats(M, N, T, int(splits))), dtype=torch.float32,
                        device=A.device)
     with KernelTimer.span(name, 0, 2 * T * M * N * Kd):

@@ -195,7 +195,7 @@ def bias_relu_bmm(X, W, b):
     return out
 
 
-def _splitk_bmm_tn(X, dY, chunks, min_chunk=1024, name="gemm_wgrad"):
+def _splitk_bmm_tn(X, dY, chunks, min_chunk=1024, name="gemm_wgrad", out=None):
     """X^T @ dY for X [T, M, K], dY [T, M, N] with the long M reduction split into `chunks`
     batched GEMMs plus a sum: hipBLASLt runs the plain tall-skinny product at about half the
     FP32 rate on these shapes (scripts/probe_gemm2.py), the split form at ~105-125 TFLOP/s."""
@@ -204,7 +204,7 @@ def _splitk_bmm_tn(X, dY, chunks, min_chunk=1024, name="gemm_wgrad"):
     c = M // chunks
     if chunks <= 1 or c < min_chunk:
         with _gemm_span(name, T, K, N, M):
-            return torch.bmm(X.transpose(1, 2), dY)
+            return torch.bmm(X.transpose(1, 2), dY) if out is None else torch.bmm(X.transpose(1, 2), dY, out=out)
     # per tower the first c*chunks rows are a view [chunks, c, K] (merging the tower and chunk
     # dims would copy both operands whenever M % chunks != 0: 2 x 0.1 ms per call at the bench size)
     part = X.new_empty((T, chunks, K, N))
@@ -212,10 +212,10 @@ def _splitk_bmm_tn(X, dY, chunks, min_chunk=1024, name="gemm_wgrad"):
         for t in range(T):
             torch.bmm(X[t, : c * chunks].view(chunks, c, K).transpose(1, 2), dY[t, : c * chunks].view(chunks, c, N),
                       out=part[t])
-    head = part.sum(1)
     if c * chunks < M:
-        head = head + torch.bmm(X[:, c * chunks:].transpose(1, 2), dY[:, c * chunks:])
-    return head
+        tail = torch.bmm(X[:, c * chunks:].transpose(1, 2), dY[:, c * chunks:])
+        return part.sum(1) + tail if out is None else torch.add(part.sum(1), tail, out=out)
+    return part.sum(1) if out is None else torch.sum(part, 1, out=out)
 
 
 class _BiasReluBmm(torch.autograd.Function):

@@ -96,6 +96,10 @@ class PPO:
         # after one eager rollout, replay the vectorised rollout as one captured HIP graph
         self.rollout_graph = rollout_graph
         self._graph = None
+        # PPO._sgd on the window + x6 path: the minibatch step with its launches written out (merlin/fast_step.py;
+        # False = the same kernels through the autograd engine)
+        self.fast_step = True
+        self._wstep = None
         # acting draws: counter-based (merlin_act_heads), keyed by this seed (torch.manual_seed's,
         # read without consuming the RNG), the rollout counter below (bumped inside the captured
         # graph: every replay draws afresh), the step and the GLOBAL env index (env_offset + i):
@@ -322,10 +326,19 @@ class PPO:
                 plan = WindowPlan(codes, groups)
                 self.last_num_windows = plan.num_windows
         distinct = 0
+        host_mb = []
         t_host = time.perf_counter()
         perms = [self._perm(B, epoch) for epoch in range(self.update_epochs)]  # drawn in epoch order
+        # the window + x6 path's step with its launches written out (merlin/fast_step.py)
+        fast = plan is not None and self.fast_step and getattr(self.ac, "fc1_impl", None) == "x6"
+        if fast:
+            if self._wstep is None or not self._wstep.valid():
+                from .fast_step import WindowStep
+
+                self._wstep = WindowStep(self)
+            self._wstep.bind_grads()
         # one host read per update for every minibatch's distinct-frame groups (merlin/windows.py)
-        all_mbws = plan.update_minibatches(perms, self.minibatch_size) if plan is not None else None
+        all_mbws = plan.update_minibatches(perms, self.minibatch_size, bulk=fast) if plan is not None else None
         for epoch in range(self.update_epochs):
             idxs = perms[epoch]
             mbws = all_mbws[epoch] if all_mbws is not None else None
@@ -336,11 +349,14 @@ class PPO:
                     # and adds the statistics to totals[:5] on the device
                     mbw = mbws[k]
                     distinct += int(mbw.groups.numel())
-                    with deferred_fc1_wgrad():  # this loop reads p.grad after loss.backward() only
-                        logits, values = self.ac.heads_windows(plan, mbw, head_bias=False)
-                    loss = _PPOLoss.apply(logits, values, self.ac.actor[2].bias, self.ac.critic[2].bias, mbw, mb_idx,
-                                          actions, logp_old, adv, returns, self.clip_eps, self.vf_coef,
-                                          self.ent_coef, totals)
+                    if fast:  # forward + backward; every gradient left in its .grad view
+                        self._wstep.step(plan, mbw, mb_idx, actions, logp_old, adv, returns, totals)
+                    else:
+                        with deferred_fc1_wgrad():  # this loop reads p.grad after loss.backward() only
+                            logits, values = self.ac.heads_windows(plan, mbw, head_bias=False)
+                        loss = _PPOLoss.apply(logits, values, self.ac.actor[2].bias, self.ac.critic[2].bias, mbw,
+                                              mb_idx, actions, logp_old, adv, returns, self.clip_eps, self.vf_coef,
+                                              self.ent_coef, totals)
                 else:
                     lp_old, a_mb, ret_mb = logp_old[mb_idx], adv[mb_idx], returns[mb_idx]
                     if use_codes:
@@ -365,8 +381,9 @@ class PPO:
                         clipfrac = (torch.abs(ratio - 1.0) > self.clip_eps).float().mean()
                         totals[:5] += torch.stack([pi_loss.detach(), v_loss.detach(), ent.detach(), approx_kl,
                                                    clipfrac]).double()
-                self.dp.zero_grad(self.optimizer)
-                loss.backward()
+                if not fast:
+                    self.dp.zero_grad(self.optimizer)
+                    loss.backward()
                 self.dp.allreduce_grads()
                 if self._clip_adam is not None:
                     grad_norm = self._clip_adam.step()
@@ -375,7 +392,10 @@ class PPO:
                     self.optimizer.step()
                 totals[5:].add_(grad_norm.detach())
                 nb += 1
+                host_mb.append(time.perf_counter())
         self.last_host_loop_ms = (time.perf_counter() - t_host) * 1e3  # host time to queue the update
+        # host time to queue each minibatch's optimizer step (the first one includes the update's planning)
+        self.last_host_mb_ms = [(b - a) * 1e3 for a, b in zip([t_host] + host_mb[:-1], host_mb)]
         t = totals.cpu().tolist()
         if groups is not None:
             self.last_distinct_frac = float(distinct) / float(self.update_epochs * B)

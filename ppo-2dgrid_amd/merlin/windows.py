@@ -269,16 +269,54 @@ class WindowPlan:
         dk, do = torch.sort(torch.cat([d for d, _ in wdst]).to(torch.int32), stable=True)
         self.dq_plan = SegmentPlan(dk, torch.cat([s for _, s in wdst])[do], item_len)
 
-    def update_minibatches(self, perms: list, minibatch_size: int) -> list:
+    def update_minibatches(self, perms: list, minibatch_size: int, bulk: bool = False) -> list:
         """epoch_minibatches for every epoch's permutation at once: one stable sort and one host
         read for the whole update (each host read drains the stream; per epoch that was ten
         pipeline drains per update).  Returns one list of MinibatchWindows per epoch."""
         B = int(perms[0].numel())
-        flat = self.epoch_minibatches(torch.cat(perms), minibatch_size, period=B)
+        flat = self.epoch_minibatches(torch.cat(perms), minibatch_size, period=B, bulk=bulk)
         nmb = (B + minibatch_size - 1) // minibatch_size
         return [flat[e * nmb:(e + 1) * nmb] for e in range(len(perms))]
 
-    def epoch_minibatches(self, idxs: torch.Tensor, minibatch_size: int, period: int | None = None) -> list:
+    def _bulk_minibatches(self, uniq, inv, perm, starts, mb_of, counts, P, per, minibatch_size) -> list:
+        """Every minibatch's MinibatchWindows tensors for the whole update in a few launches (merlin/fast_step.py:
+        the minibatch step then issues none of its own): each minibatch's slot / inv / order / offs and its live
+        patch map kmap are views of update-wide arrays (slot [nmb, F] and kmap [nmb, K] int32)."""
+        dev, F, K = uniq.device, self.num_frames, self.num_patches
+        nmb, G = len(counts), int(uniq.numel())
+        goff_h = [0]
+        for c in counts:
+            goff_h.append(goff_h[-1] + c)
+        lo_h = [(m // per) * P + (m % per) * minibatch_size for m in range(nmb)]
+        hi_h = [(m // per) * P + min(P, (m % per + 1) * minibatch_size) for m in range(nmb)]
+        goff = torch.tensor(goff_h, dtype=torch.int64).to(dev, non_blocking=True)
+        lo = torch.tensor(lo_h, dtype=torch.int64).to(dev, non_blocking=True)
+        span = torch.tensor([h - l for h, l in zip(hi_h, lo_h)], dtype=torch.int32).to(dev, non_blocking=True)
+        mbg = uniq // F  # minibatch of each (minibatch, frame) group
+        gall = uniq - mbg * F
+        j = torch.arange(G, device=dev) - goff[mbg]  # position of the group in its minibatch
+        slot = torch.full((nmb, F), -1, dtype=torch.int32, device=dev)
+        slot.view(-1)[mbg * F + gall] = j.to(torch.int32)
+        inv_local = inv - goff[mb_of]
+        # sorted positions lo..hi hold exactly minibatch m's samples: order = position - lo of its minibatch
+        order = ((perm % P) % minibatch_size).to(torch.int32)
+        offs = torch.empty(G + nmb, dtype=torch.int32, device=dev)
+        offs[torch.arange(G, device=dev) + mbg] = (starts - lo[mbg]).to(torch.int32)
+        offs[goff[1:] + torch.arange(nmb, device=dev)] = span
+        live = self.kid.index_select(0, gall)  # [G, 9] patch ids
+        kmap = torch.full((nmb, K), -1, dtype=torch.int32, device=dev)
+        kmap.view(-1)[(mbg.unsqueeze(1) * K + live).reshape(-1)] = live.reshape(-1)
+        out = []
+        for m, c in enumerate(counts):
+            g0 = goff_h[m]
+            mw = MinibatchWindows(gall[g0:g0 + c], inv_local[lo_h[m]:hi_h[m]], slot[m], order[lo_h[m]:hi_h[m]],
+                                  offs[g0 + m:g0 + m + c + 1])
+            mw.kmap = kmap[m]
+            out.append(mw)
+        return out
+
+    def epoch_minibatches(self, idxs: torch.Tensor, minibatch_size: int, period: int | None = None,
+                          bulk: bool = False) -> list:
         """MinibatchWindows of every minibatch idxs[k*mb:(k+1)*mb] of one epoch's permutation,
         grouped by one stable sort and one host read for the whole epoch (a torch.unique per
         minibatch would stall the host at every optimizer step).  Same groups as minibatch().
@@ -301,6 +339,8 @@ class WindowPlan:
         starts = torch.nonzero(new).squeeze(1)  # first sorted position of each (minibatch, frame)
         uniq = sk[starts].long()
         counts = torch.bincount(uniq // F, minlength=nmb).tolist()
+        if bulk:
+            return self._bulk_minibatches(uniq, inv, perm, starts, mb_of, counts, P, per, minibatch_size)
         out, off = [], 0
         gall = uniq % F  # frame ids; each minibatch's groups are a view of it
         for m, c in enumerate(counts):

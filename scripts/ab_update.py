@@ -52,6 +52,7 @@ def main():
             W.OVERLAP_WGRAD = {"no_overlap": False, "x6_overlap": True}.get(name, "deferred")
             agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6"
             agent._clip_adam = None if name == "torch_opt" else clip_adam
+            agent.fast_step = name == "fast"  # merlin/fast_step.py vs the autograd engine
         return s
 
     names = sys.argv[3].split(",") if len(sys.argv) > 3 else ["x6_overlap", "no_overlap", "hipblaslt"]

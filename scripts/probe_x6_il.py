@@ -27,7 +27,7 @@ def main():
     cfgs = [int(c) for c in os.environ.get("CFGS", "").split(",") if c] or None
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
-    shapes = {"fwd": (512, 576, True, [0, 20, 21, 24, 25, 10]), "dgrad": (576, 512, False, [1, 22, 23, 13])}
+    shapes = {"fwd": (512, 576, True, [0, 20, 21, 24, 25, 10, 30]), "dgrad": (576, 512, False, [1, 22, 23, 13, 32])}
     if os.environ.get("PROF"):
         shapes = {"fwd": (512, 576, True, [0, 20]), "dgrad": (576, 512, False, [1, 22])}
     for name, (N, K, use_bias, cl) in shapes.items():
@@ -36,6 +36,8 @@ def main():
             torch.randn(2, U, K, device=dev, generator=g) * (torch.rand(2, U, K, device=dev, generator=g) > 0.5)
         Bp = nat.x6_split(torch.randn(2, N, K, device=dev, generator=g) / K ** 0.5)
         bias = torch.randn(2, N, device=dev, generator=g) * 0.1 if use_bias else None
+        Ap = nat.x6_split(A)  # A as planes for the cfg >= 30 kernels
+        AA = lambda c, X=None: (nat.x6_split(X) if X is not None else Ap) if c >= 30 else (A if X is None else X)  # noqa: E731
         ref = nat.x6_gemm_nt(A, Bp, bias=bias, cfg=cl[0])
         # error vs float64 on the first rows, relative to sum |a b| (no bias: the raw product)
         Bf = nat.x6_join(Bp).view(2, N, K)
@@ -47,8 +49,8 @@ def main():
         ok = {}
         for c in cl:
             try:
-                out = nat.x6_gemm_nt(A, Bp, bias=bias, cfg=c)
-                raw = nat.x6_gemm_nt(A[:, rows].contiguous(), Bp, cfg=c)
+                out = nat.x6_gemm_nt(AA(c), Bp, bias=bias, cfg=c)
+                raw = nat.x6_gemm_nt(AA(c, A[:, rows].contiguous()), Bp, cfg=c)
                 err = float(((raw.double() - C64).abs() / den).max())
                 ok[c] = (bool(torch.equal(out, ref)), err)
             except nat.MerlinNativeError as ex:
@@ -56,7 +58,7 @@ def main():
         times = {c: [] for c in ok}
         for _ in range(rounds):
             for c in ok:
-                times[c].append(ev_time(lambda: nat.x6_gemm_nt(A, Bp, bias=bias, cfg=c)))
+                times[c].append(ev_time(lambda: nat.x6_gemm_nt(AA(c), Bp, bias=bias, cfg=c)))
         ex = 6 * 2 * 2 * U * N * K
         for c in ok:
             med = statistics.median(times[c])

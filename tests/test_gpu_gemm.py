@@ -57,7 +57,7 @@ def test_gemm_nt_vs_float64(device, M, N, K, cfg):
     assert torch.equal(Cb, torch.relu(C + bias.unsqueeze(1)))
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 20, 21])
 @pytest.mark.parametrize("Kd,splits", [(1, 1), (4093, 7), (40000, 32), (40000, 64)])
 def test_gemm_tn_vs_float64(device, Kd, splits, cfg):
     from merlin import _native as nat
@@ -75,7 +75,8 @@ def test_gemm_tn_vs_float64(device, Kd, splits, cfg):
     assert torch.equal(W, nat.x6_gemm_tn(dz, a3, splits=splits, cfg=cfg))
 
 
-def test_gemm_tn_cancellation(device):
+@pytest.mark.parametrize("cfg", [0, 20, 21])
+def test_gemm_tn_cancellation(device, cfg):
     """The update's weight gradient: ~1e5 rows whose terms nearly cancel (|W| ~ 1e-2 sum |a b|)."""
     from merlin import _native as nat
 
@@ -87,7 +88,7 @@ def test_gemm_tn_cancellation(device):
     W64 = torch.bmm(dz.double().transpose(1, 2), a3.double())
     rel = lambda W: float((W.double() - W64).norm() / W64.norm())  # noqa: E731
     ref = rel(sum(torch.bmm(dz[:, i:i + 2000].transpose(1, 2), a3[:, i:i + 2000]) for i in range(0, Kd, 2000)))
-    assert rel(nat.x6_gemm_tn(dz, a3)) <= ref
+    assert rel(nat.x6_gemm_tn(dz, a3, cfg=cfg)) <= ref
 
 
 def test_window_update_x6_matches_hipblaslt(device):
