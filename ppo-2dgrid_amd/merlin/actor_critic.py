@@ -388,21 +388,29 @@ class CNNActorCritic(nn.Module):
     def conv1_tables(self):
         """P[t][co][slot][bin] (t: actor, critic; slot = 2*dy + dx; bin = 4*class + 2*qy + qx)."""
         c1a, c1c = self.actor_extractor.network[0], self.critic_extractor.network[0]
-        W = torch.stack([c1a.weight, c1c.weight]).view(2, 32, 3, 2, 4, 2, 4)  # t o c dy ky dx kx
-        A = self._atlas_on(c1a.weight.device).view(5, 3, 2, 4, 2, 4)  # cls c qy ky qx kx
+        return self.conv1_tables_from(torch.stack([c1a.weight, c1c.weight])), torch.stack([c1a.bias, c1c.bias])
+
+    def conv1_tables_from(self, W1):
+        """conv1_tables of the stacked conv1 weights W1 [2, 32, 3, 8, 8]."""
+        W = W1.view(2, 32, 3, 2, 4, 2, 4)  # t o c dy ky dx kx
+        A = self._atlas_on(W1.device).view(5, 3, 2, 4, 2, 4)  # cls c qy ky qx kx
         P = torch.einsum("tocakbl,zcekfl->toabzef", W, A)
-        return P.reshape(2, 32, 4, 20), torch.stack([c1a.bias, c1c.bias])
+        return P.reshape(2, 32, 4, 20)
 
     def conv2_tables(self):
         """T2[t][row][co] (t: actor, critic; 2720 rows, csrc/merlin_conv2lut.hip layout):
         W2[:, :, ky, kx] applied to relu(conv1) of each tile combination (_Conv2Tables: autograd
         maps dT2 to the conv1 and conv2 weight gradients)."""
-        P, b1 = self.conv1_tables()
+        ea, ec = self.actor_extractor.network, self.critic_extractor.network
+        return self.conv2_tables_from(torch.stack([ea[0].weight, ec[0].weight]), torch.stack([ea[0].bias, ec[0].bias]),
+                                      torch.stack([ea[2].weight, ec[2].weight]))
+
+    def conv2_tables_from(self, W1, b1, W2):
+        """conv2_tables of the stacked weights W1 [2, 32, 3, 8, 8], b1 [2, 32], W2 [2, 64, 32, 4, 4]."""
+        P = self.conv1_tables_from(W1)
         if self._lut2_gather is None or self._lut2_gather[0].device != P.device or self._lut2_gather[0].dtype != P.dtype:
             G, part = _lut2_gather_matrix()
             self._lut2_gather = (G.to(device=P.device, dtype=P.dtype), part.to(P.device))
-        ea, ec = self.actor_extractor.network, self.critic_extractor.network
-        W2 = torch.stack([ea[2].weight, ec[2].weight])  # [2, co 64, ci 32, ky 4, kx 4]
         return _Conv2Tables.apply(P.reshape(2, 32, 80), b1, W2, *self._lut2_gather)
 
     def _conv2_tables_autograd(self):

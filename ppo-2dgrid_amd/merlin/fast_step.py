@@ -28,39 +28,83 @@ from . import _native as nat
 from .actor_critic import _splitk_bmm_tn
 
 
+def flatten_parameters(module: torch.nn.Module) -> torch.Tensor:
+    """Re-home every parameter of `module` into one contiguous buffer (parameter order), each parameter a view of
+    it: the weight stage gathers all its derived weights with one indexed read, and the optimizer / all-reduce see
+    one block.  Values are unchanged; call before anything captures parameter addresses (the rollout graph)."""
+    params = list(module.parameters())
+    flat = torch.empty(sum(p.numel() for p in params), dtype=params[0].dtype, device=params[0].device)
+    off = 0
+    with torch.no_grad():
+        for p in params:
+            n = p.numel()
+            v = flat[off:off + n].view_as(p)
+            v.copy_(p.data)
+            p.data = v
+            off += n
+    return flat
+
+
 class WeightStage:
     """Parameter-only forward / backward of the minibatch step as two captured HIP graphs.
 
-    forward() -> (T2 [2, 2720, 64], b2 [2, 64], W3r [2, 64, 576], b3 [2, 64], W4p [2, H, 576], b4 [2, H]) and
-    self.planes = (x6 planes of W4p, of W4p^T); backward() maps the gradients left in self.grads (same shapes
-    as forward()'s outputs) to the gradients of the 16 tower / fc1 parameters, written into `grad_views`."""
+    The derived weights are one indexed read of the flat parameter buffer, laid out as D = [W1 [2, 32, 3, 8, 8],
+    b1 [2, 32], W2 [2, 64, 32, 4, 4], b2 [2, 64], W3r [2, 64, 576], b3 [2, 64], b4 [2, H], W4p [2, H, 576],
+    W4p^T [2, 576, H]] (the towers stacked, conv3's and fc1's weights in the (ky, kx, co) / (p3, co) orders the
+    window kernels read); then T2 from (W1, b1, W2) (CNNActorCritic.conv2_tables_from) and fc1's x6 planes of W4p
+    and W4p^T in one split.  forward() -> (T2, b2, W3r, b3, W4p, b4); self.planes = (planes of W4p, of W4p^T).
+    The backward graph maps dT2 (self.gT2) through the table adjoints to dW1 / db1 / dW2, puts them beside the
+    gradients the step wrote into self.grads (db2, dW3r, db3, dW4p, db4: views of the derived-gradient buffer),
+    and scatters the whole buffer onto the stage parameters' slots of the flat gradient (one launch)."""
 
-    def __init__(self, ac, grad_views: dict):
+    def __init__(self, ac, flat_params: torch.Tensor, flat_grad: torch.Tensor):
         self.ac = ac
-        ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
-        fa, fc = ac.actor[0], ac.critic[0]
-        self.params = [ea[0].weight, ea[0].bias, ec[0].weight, ec[0].bias, ea[2].weight, ea[2].bias, ec[2].weight,
-                       ec[2].bias, ea[4].weight, ea[4].bias, ec[4].weight, ec[4].bias, fa.weight, fa.bias, fc.weight,
-                       fc.bias]
-        self.views = [grad_views[p] for p in self.params]
-        self.ptrs = [p.data_ptr() for p in self.params]
-        self._capture()
-
-    def _fwd(self):
-        ac = self.ac
+        self.flat_params, self.flat_grad = flat_params, flat_grad
+        self.ptr = flat_params.data_ptr()
         ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
         fa, fc = ac.actor[0], ac.critic[0]
         H = fa.weight.shape[0]
-        T2 = ac.conv2_tables()
-        b2 = torch.stack([ea[2].bias, ec[2].bias])
-        W3 = torch.stack([ea[4].weight, ec[4].weight])  # [2, co, ci, ky, kx]
-        W3r = W3.permute(0, 2, 3, 4, 1).reshape(2, 64, 576)  # [2, ci, (ky, kx, co)]
-        b3 = torch.stack([ea[4].bias, ec[4].bias])
-        W4 = torch.stack([fa.weight, fc.weight])  # [2, H, 576] in (co, p3) order
-        W4p = W4.view(2, H, 64, 9).transpose(2, 3).reshape(2, H, 576)  # (p3, co): a3's column order
-        b4 = torch.stack([fa.bias, fc.bias])
-        planes = (nat.x6_split(W4p.detach()), nat.x6_split(W4p.detach().transpose(1, 2).contiguous()))
-        return (T2, b2, W3r, b3, W4p, b4), planes
+        # the flat parameter offsets, as index tensors shaped like the parameters
+        idx, off = {}, 0
+        for p in ac.parameters():
+            n = p.numel()
+            idx[p] = torch.arange(off, off + n, dtype=torch.int64).view(p.shape)
+            off += n
+        st = lambda a, b: torch.stack([idx[a], idx[b]])  # noqa: E731
+        W4 = st(fa.weight, fc.weight)  # [2, H, 576] in (co, p3) order
+        W4p = W4.view(2, H, 64, 9).transpose(2, 3).reshape(2, H, 576)
+        segs = [("W1", st(ea[0].weight, ec[0].weight)), ("b1", st(ea[0].bias, ec[0].bias)),
+                ("W2", st(ea[2].weight, ec[2].weight)), ("b2", st(ea[2].bias, ec[2].bias)),
+                ("W3r", st(ea[4].weight, ec[4].weight).permute(0, 2, 3, 4, 1).reshape(2, 64, 576)),
+                ("b3", st(ea[4].bias, ec[4].bias)), ("b4", st(fa.bias, fc.bias)), ("W4p", W4p),
+                ("W4pT", W4p.transpose(1, 2).contiguous())]
+        self.shapes, self.offs, o = {}, {}, 0
+        for name, t in segs:
+            self.shapes[name], self.offs[name] = tuple(t.shape), o
+            o += t.numel()
+        dev = flat_params.device
+        self.fwd_map = torch.cat([t.reshape(-1) for _, t in segs]).to(dev)
+        self.n_grad = self.offs["W4pT"]  # every stage-parameter element once in D[:n_grad]
+        assert int(self.fwd_map[:self.n_grad].unique().numel()) == self.n_grad
+        self._capture()
+
+    def seg(self, buf, name):
+        o = self.offs[name]
+        shape = self.shapes[name]
+        n = 1
+        for d in shape:
+            n *= d
+        return buf[o:o + n].view(shape)
+
+    def _fwd(self):
+        D = self.flat_params.index_select(0, self.fwd_map)  # every derived weight in one launch
+        W1, b1, W2 = (self.seg(D, k).requires_grad_() for k in ("W1", "b1", "W2"))
+        T2 = self.ac.conv2_tables_from(W1, b1, W2)
+        o = self.offs["W4p"]
+        planes = nat.x6_split(D[o:].view(-1, 8)).view(-1)  # W4p and W4p^T back to back
+        H = self.shapes["W4p"][1]
+        n4 = 2 * H * 576 * 3
+        return D, (W1, b1, W2), T2, (planes[:n4].view(2, H, 3 * 576), planes[n4:].view(2, 576, 3 * H))
 
     def _capture(self):
         main = torch.cuda.current_stream()
@@ -68,27 +112,32 @@ class WeightStage:
         side.wait_stream(main)
         with torch.cuda.stream(side), torch.enable_grad():
             for _ in range(2):  # lazy initialisation (GEMM handles, cached gather matrices) outside the captures
-                outs, _ = self._fwd()
-                torch.autograd.grad(outs, self.params, grad_outputs=[torch.ones_like(o) for o in outs])
+                _, leaves, T2, _ = self._fwd()
+                torch.autograd.grad(T2, leaves, grad_outputs=torch.ones_like(T2))
         main.wait_stream(side)
         torch.cuda.synchronize()
         self.pool = torch.cuda.graph_pool_handle()
         self.gfwd, self.gbwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        DG = torch.zeros(self.fwd_map.numel(), dtype=torch.float32, device=self.flat_params.device)
+        self.gT2 = torch.zeros((2, nat.LUT2_ROWS, 64), dtype=torch.float32, device=DG.device)
         with torch.enable_grad():
             with torch.cuda.graph(self.gfwd, pool=self.pool):
-                outs, planes = self._fwd()
-            self.grads = tuple(torch.zeros_like(o) for o in outs)
+                D, leaves, T2, planes = self._fwd()
             with torch.cuda.graph(self.gbwd, pool=self.pool):
-                gs = torch.autograd.grad(outs, self.params, grad_outputs=self.grads, retain_graph=True)
-                for g, v in zip(gs, self.views):
-                    v.copy_(g)
-        self._keep = (outs, gs)  # the saved tensors the backward graph reads stay allocated
-        self.outs = tuple(o.detach() for o in outs)
+                gs = torch.autograd.grad(T2, leaves, grad_outputs=self.gT2, retain_graph=True)
+                for g, k in zip(gs, ("W1", "b1", "W2")):
+                    self.seg(DG, k).copy_(g)
+                self.flat_grad.index_copy_(0, self.fwd_map[:self.n_grad], DG[:self.n_grad])
+        self._keep = (D, leaves, T2, gs)  # the saved tensors the backward graph reads stay allocated
+        self.outs = (T2.detach(),) + tuple(self.seg(D, k) for k in ("b2", "W3r", "b3", "W4p", "b4"))
         self.planes = planes
+        # the gradients the step writes for the backward graph: dT2, then views of DG
+        self.grads = (self.gT2,) + tuple(self.seg(DG, k) for k in ("b2", "W3r", "b3", "W4p", "b4"))
+        self.DG = DG
         torch.cuda.synchronize()
 
     def valid(self) -> bool:
-        return all(p.data_ptr() == q for p, q in zip(self.params, self.ptrs))
+        return self.flat_params.data_ptr() == self.ptr
 
     def forward(self):
         self.gfwd.replay()
@@ -104,24 +153,37 @@ class WindowStep:
     def __init__(self, agent):
         self.agent = agent
         ac = agent.ac
-        self.params = [p for p in ac.parameters() if p.requires_grad]
+        self.params = list(ac.parameters())
+        flat_params = agent._flat_params
+        off = 0
+        for p in self.params:  # the parameters are views of agent._flat_params in parameter order
+            assert p.data_ptr() == flat_params.data_ptr() + 4 * off, "parameters moved off the flat buffer"
+            off += p.numel()
         dp = agent.dp
         if dp.enabled:
             flat = dp._flat_grad  # the gradient RCCL all-reduces; every p.grad is a view of it
         else:
-            flat = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=agent.device)
+            flat = torch.zeros(off, dtype=torch.float32, device=agent.device)
+        assert flat.numel() == off
         views, off = {}, 0
         for p in self.params:
             n = p.numel()
             views[p] = flat[off:off + n].view_as(p)
             off += n
         self.flat, self.views = flat, views
-        self.stage = WeightStage(ac, views)
+        self.stage = WeightStage(ac, flat_params, flat)
         self.head = (ac.actor[2].weight, ac.actor[2].bias, ac.critic[2].weight, ac.critic[2].bias)
         self._side = None
 
     def valid(self) -> bool:
-        return self.stage.valid() and all(p.requires_grad for p in self.params)
+        if not (self.stage.valid() and all(p.requires_grad for p in self.params)):
+            return False
+        off, base = 0, self.stage.flat_params.data_ptr()
+        for p in self.params:
+            if p.data_ptr() != base + 4 * off:
+                return False
+            off += p.numel()
+        return True
 
     def bind_grads(self):
         """Every parameter's .grad is its view of the flat buffer (each step overwrites all of them)."""

@@ -141,6 +141,11 @@ class PPO:
                 self.obs_shape = sample_obs.shape
                 self.ac = CNNActorCritic(self.obs_shape, act_dim).to(self.device)
             self.buffer = RolloutBuffer(batch_size, self.obs_shape, self.device, is_discrete=True)
+        # every parameter a view of one flat buffer (merlin/fast_step.py: the weight stage reads it with one
+        # indexed gather; done before anything captures parameter addresses)
+        from .fast_step import flatten_parameters
+
+        self._flat_params = flatten_parameters(self.ac)
         # torch's fused Adam: one multi-tensor kernel per step instead of the foreach chain (~9)
         self.optimizer = optim.Adam(self.ac.parameters(), lr=lr, fused=True)
         self.dp.attach(self.ac)

@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch
 
 from merlin import MerlinVecEnv
+from merlin import _native as nat
 from merlin import windows as W
 from merlin.ppo import PPO
 
@@ -52,7 +53,7 @@ def main():
             W.OVERLAP_WGRAD = {"no_overlap": False, "x6_overlap": True}.get(name, "deferred")
             agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6"
             agent._clip_adam = None if name == "torch_opt" else clip_adam
-            agent.fast_step = name == "fast"  # merlin/fast_step.py vs the autograd engine
+            agent.fast_step = name.startswith("fast")  # merlin/fast_step.py vs the autograd engine
         return s
 
     names = sys.argv[3].split(",") if len(sys.argv) > 3 else ["x6_overlap", "no_overlap", "hipblaslt"]
@@ -64,9 +65,12 @@ def main():
             agent.ac.load_state_dict(sd)
             agent.optimizer.load_state_dict(opt)
             torch.cuda.synchronize()
+            if n.endswith("_timers"):  # bench.py's per-kernel HIP events switched on
+                nat.KernelTimer.start()
             t0 = time.perf_counter()
             agent.update(lv)
             torch.cuda.synchronize()
+            nat.KernelTimer.stop()
             times[n].append((time.perf_counter() - t0) * 1e3)
             host.setdefault(n, []).append(agent.last_host_loop_ms)
     for n, t in times.items():
