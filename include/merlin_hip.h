@@ -417,6 +417,21 @@ int merlin_x6_gemm_tn(const float *A_dev, const float *B_dev, int64_t Kd, int32_
                       int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev, float *out_dev, int32_t cfg,
                       void *stream);
 
+/* The conv1 / conv2 tables of both towers and their adjoint (the parameter-only part of PPO.update's
+ * minibatch step, merlin/fast_step.py WeightStage; replaces CNNActorCritic.conv2_tables and its autograd
+ * backward, src/actor_critic.py:9-14 conv1 / conv2), csrc/merlin_stage.hip.  Per tower t < towers (1..2):
+ * W1 f32[t][32][3][8][8], b1 f32[t][32], W2 f32[t][64][32][4][4] (the conv weights, towers stacked), atlas
+ * f32[5][3][8][8] (the tile atlas / 255), idx int16[680][4] (the conv1-table entries of each tile
+ * combination, CNNActorCritic._lut2_h1_index order).  Forward: HT f32[t][680][32] (relu(conv1) of every
+ * combination, kept for the backward), T2 f32[t][2720][64].  Backward from dT2 f32[t][2720][64]: dH
+ * f32[t][680][32] (scratch), dW1 / db1 / dW2 in the layouts of W1 / b1 / W2; koff int16[81] / kv int16[2720]
+ * = the combinations v of each table entry k (CSR, (v, e) order).  Fixed-order sums (bitwise reproducible). */
+int merlin_stage_tables_fwd(const float *W1_dev, const float *b1_dev, const float *W2_dev, const float *atlas_dev,
+                            const int16_t *idx_dev, int32_t towers, float *HT_dev, float *T2_dev, void *stream);
+int merlin_stage_tables_bwd(const float *W2_dev, const float *HT_dev, const float *dT2_dev, const float *atlas_dev,
+                            const int16_t *koff_dev, const int16_t *kv_dev, int32_t towers, float *dH_dev,
+                            float *dW1_dev, float *db1_dev, float *dW2_dev, void *stream);
+
 /* Optimizer step of PPO.update (src/ppo.py:153-156: clip_grad_norm_(params, max_norm) then
  * Adam.step(), replacing torch.nn.utils.clip_grad_norm_ + torch.optim.Adam(fused=True).step()) over
  * n_tensors (1..32) float32 parameter tensors, csrc/merlin_optim.hip.  params / grads / exp_avg /

@@ -781,6 +781,24 @@ int merlin_x6_split(const float *x, int64_t n, void *planes, void *stream) {
     return MERLIN_OK;
 }
 
+int merlin_stage_tables_fwd(const float *W1, const float *b1, const float *W2, const float *atlas, const int16_t *idx,
+                            int32_t towers, float *HT, float *T2, void *stream) {
+    if (!W1 || !b1 || !W2 || !atlas || !idx || !HT || !T2) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_stage_fwd(W1, b1, W2, atlas, idx, towers, HT, T2, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_stage_tables_bwd(const float *W2, const float *HT, const float *dT2, const float *atlas,
+                            const int16_t *koff, const int16_t *kv, int32_t towers, float *dH, float *dW1, float *db1,
+                            float *dW2, void *stream) {
+    if (!W2 || !HT || !dT2 || !atlas || !koff || !kv || !dH || !dW1 || !db1 || !dW2)
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_stage_bwd(W2, HT, dT2, atlas, koff, kv, towers, dH, dW1, db1, dW2, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
 int merlin_x6_join(const void *planes, int64_t n, float *x, void *stream) {
     if ((!x || !planes) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (n < 0 || n % 8) return fail(MERLIN_E_INVALID, "n must be a non-negative multiple of 8");

@@ -242,8 +242,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_nt32(const void *__restri
 // 4 (r & 3)) and RC = 24 (row stride 24 = 8 mod 16 separates odd rows; XOR by 4 ((r >> 1) & 1)).
 template <int RC>
 __device__ __forceinline__ int tr32_swz(int row) {
-    static_assert(RC == 16 || RC == 24, "row chunks");
-    return RC == 16 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
+    static_assert(RC % 16 == 0 || RC == 24, "row chunks");
+    return RC % 16 == 0 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
 }
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -449,6 +449,170 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn32(const void *__restri
             }
 }
 
+// TN with 16-deep k steps and a bigger block tile: 256 x 192 (both of fc1's weight-gradient dimensions in 2 x 3
+// tiles) over 8 waves of 64 x 96.  Per MFMA it stages, splits and reads from LDS 35-65 % less than the 128 x 192 /
+// 32-deep form (the split and the staging are per element of the tile's edges, the MFMAs per element of its
+// area); two 43-KB LDS stages.  The accumulators are chunked per k step (the step's six plane products of a
+// 32 x 32 tile in a fresh register set, added to the running sum once): 96 + 16 registers instead of the
+// 192 of split hi / lo sums.
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn32k16(const float4 *__restrict__ A,
+                                                               const float4 *__restrict__ B, int64_t Kd, int M, int N,
+                                                               int64_t sA, int64_t sB, int64_t kc, int tiles_n,
+                                                               int tiles, int S, float *__restrict__ slab) {
+    constexpr int K16 = 16;
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int RCA = BM / 8, RCB = BN / 8;
+    constexpr int QA = K16 * RCA, QB = K16 * RCB;
+    constexpr int UA = (QA + NT - 1) / NT, UB = (QB + NT - 1) / NT;
+    static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile of 32 x 32 MFMA tiles");
+    constexpr int PSA = K16 * RCA, PSB = K16 * RCB;
+    constexpr int STAGE = 3 * (PSA + PSB);
+    __shared__ u32x4 lds[2 * STAGE];
+
+    const int P = xcd_tile(blockIdx.x, gridDim.x);
+    const int t = P / (S * tiles), s = (P / tiles) % S, L = P % tiles;
+    const int tm = L / tiles_n, tn = L - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int64_t k0 = (int64_t)s * kc, k1 = std::min<int64_t>(Kd, k0 + kc);
+    const int64_t rowA = M / 4, rowB = N / 4;
+    A += t * sA + m0 / 4;
+    B += t * sB + n0 / 4;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    int ka[UA], oa[UA], la[UA];
+#pragma unroll
+    for (int i = 0; i < UA; i++) {
+        const int q = std::min(tid + i * NT, QA - 1);
+        const int k = q / RCA, g = q - (q / RCA) * RCA;
+        ka[i] = k;
+        oa[i] = g * 2;
+        la[i] = k * RCA + (g ^ tr32_swz<RCA>(k));
+    }
+    int kb[UB], ob[UB], lb[UB];
+#pragma unroll
+    for (int i = 0; i < UB; i++) {
+        const int q = std::min(tid + i * NT, QB - 1);
+        const int k = q / RCB, g = q - (q / RCB) * RCB;
+        kb[i] = k;
+        ob[i] = g * 2;
+        lb[i] = 3 * PSA + k * RCB + (g ^ tr32_swz<RCB>(k));
+    }
+    const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float4 ra[UA][2], rb[UB][2];
+    auto load = [&](int64_t kk) {
+#pragma unroll
+        for (int i = 0; i < UA; i++) {
+            const int64_t k = kk + ka[i];
+            const float4 *src = A + std::min(k, k1 - 1) * rowA + oa[i];
+            const float4 x = src[0], y = src[1];
+            ra[i][0] = k < k1 ? x : zero;
+            ra[i][1] = k < k1 ? y : zero;
+        }
+#pragma unroll
+        for (int i = 0; i < UB; i++) {
+            const int64_t k = kk + kb[i];
+            const float4 *src = B + std::min(k, k1 - 1) * rowB + ob[i];
+            const float4 x = src[0], y = src[1];
+            rb[i][0] = k < k1 ? x : zero;
+            rb[i][1] = k < k1 ? y : zero;
+        }
+    };
+    auto store = [&](int buf) {
+        u32x4 *st = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < UA; i++)
+            if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
+                u32x4 p0, p1, p2;
+                split8(ra[i][0], ra[i][1], p0, p1, p2);
+                st[la[i]] = p0;
+                st[PSA + la[i]] = p1;
+                st[2 * PSA + la[i]] = p2;
+            }
+#pragma unroll
+        for (int i = 0; i < UB; i++)
+            if (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB) {
+                u32x4 p0, p1, p2;
+                split8(rb[i][0], rb[i][1], p0, p1, p2);
+                st[lb[i]] = p0;
+                st[PSB + lb[i]] = p1;
+                st[2 * PSB + lb[i]] = p2;
+            }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) acc[i][j] = f32x16{};
+
+    if (k0 < k1) {
+        load(k0);
+        store(0);
+        if (k0 + K16 < k1) load(k0 + K16);
+        __syncthreads();
+    }
+    int buf = 0;
+    for (int64_t kk = k0; kk < k1; kk += K16, buf ^= 1) {
+        if (kk + K16 < k1) store(buf ^ 1);
+        if (kk + 2 * K16 < k1) load(kk + 2 * K16);
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * PSA;
+        u32x4 af[TM][3];
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int p = 0; p < 3; p++) af[i][p] = tr32_frag<RCA>(sAl + p * PSA, wm * WTM + i * 32, 0, lane);
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            u32x4 bf[3];
+#pragma unroll
+            for (int p = 0; p < 3; p++) bf[p] = tr32_frag<RCB>(sBl + p * PSB, wn * WTN + j * 32, 0, lane);
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                f32x16 c = mfma32(af[i][2], bf[0], f32x16{});
+                c = mfma32(af[i][1], bf[1], c);
+                c = mfma32(af[i][0], bf[2], c);
+                c = mfma32(af[i][1], bf[0], c);
+                c = mfma32(af[i][0], bf[1], c);
+                c = mfma32(af[i][0], bf[0], c);
+                acc[i][j] += c;
+            }
+        }
+        __syncthreads();
+    }
+
+    float *St = slab + ((int64_t)s * (gridDim.x / (S * tiles)) + t) * (int64_t)M * N;
+    const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                St[(int64_t)row * N + n0 + wn * WTN + j * 32 + fr] = acc[i][j][r];
+            }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+hipError_t tn32k16_launch(const void *A, const void *B, int64_t Kd, int M, int N, int T, int64_t sA, int64_t sB,
+                          int splits, float *slab, hipStream_t s, int *S_out) {
+    if (M % BM || N % BN) return hipErrorInvalidValue;
+    const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
+    int S = std::max(1, splits);
+    int64_t kc = (Kd + S - 1) / S;
+    kc = (kc + 15) / 16 * 16;
+    S = (int)std::max<int64_t>(1, (Kd + kc - 1) / kc);
+    *S_out = S;
+    hipLaunchKernelGGL((k_x6_tn32k16<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
+                       static_cast<const float4 *>(A), static_cast<const float4 *>(B), Kd, M, N, sA, sB, kc, tiles_n,
+                       tiles, S, slab);
+    return hipGetLastError();
+}
+
 template <int BM, int BN, int WGM, int WGN, int ACC, int APL = 0>
 hipError_t nt32_launch(const void *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
                        const float *bias, float *C, int64_t sC, hipStream_t s) {
@@ -500,6 +664,9 @@ hipError_t launch_x6_gemm_tn32(const float *A, const float *B, int64_t Kd, int M
         // 128 x 192 blocks: 8 waves of 32 x 96, or 4 waves (one per SIMD) of 64 x 96
         case 20: return tn32_launch<128, 192, 4, 2>(a, b, Kd, M, N, T, sA, sB, splits, slab, s, S_out);
         case 21: return tn32_launch<128, 192, 2, 2>(a, b, Kd, M, N, T, sA, sB, splits, slab, s, S_out);
+        // 256 x 192 blocks, 16-deep k steps, 8 waves of 64 x 96 (k_x6_tn32k16)
+        case 24: return tn32k16_launch<256, 192, 4, 2>(a, b, Kd, M, N, T, sA, sB, splits, slab, s, S_out);
+        case 25: return tn32k16_launch<256, 192, 8, 1>(a, b, Kd, M, N, T, sA, sB, splits, slab, s, S_out);
         default: return hipErrorInvalidValue;
     }
 }

@@ -123,6 +123,11 @@ hipError_t launch_x6_gemm_nt32(const float *A, const void *B, int64_t M, int N, 
                                int64_t b_stride, const float *bias, float *C, int64_t c_stride, int cfg, hipStream_t s);
 hipError_t launch_x6_gemm_tn32(const float *A, const float *B, int64_t Kd, int M, int N, int T, int64_t a_stride,
                                int64_t b_stride, int splits, float *slab, int cfg, hipStream_t s, int *S_out);
+hipError_t launch_stage_fwd(const float *W1, const float *b1, const float *W2, const float *atlas, const int16_t *idx,
+                            int T, float *HT, float *T2, hipStream_t s);
+hipError_t launch_stage_bwd(const float *W2, const float *HT, const float *dT2, const float *atlas,
+                            const int16_t *koff, const int16_t *kv, int T, float *dH, float *dW1, float *db1,
+                            float *dW2, hipStream_t s);
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill, int role,

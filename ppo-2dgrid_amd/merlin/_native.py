@@ -120,6 +120,8 @@ def lib():
     L.merlin_x6_tn_slab_floats.argtypes = [i32, i32, i32, i32]
     L.merlin_x6_tn_slab_floats.restype = i64
     L.merlin_x6_gemm_tn.argtypes = [vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
+    L.merlin_stage_tables_fwd.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp]
+    L.merlin_stage_tables_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     check_env_config_layout(L)
     _lib = L
     return L
@@ -772,6 +774,38 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int = X6_TN_SPLITS, cfg
         check(lib().merlin_x6_gemm_tn(ptr(A), ptr(B), Kd, M, N, T, Kd * M, Kd * N, int(splits), ptr(slab), ptr(out),
                                       int(cfg), stream_of(A)), "merlin_x6_gemm_tn")
     return out
+
+
+# -- the conv1 / conv2 tables and their adjoint (csrc/merlin_stage.hip) -----------------------------
+def stage_tables_fwd(W1, b1, W2, atlas, idx, HT=None, T2=None):
+    """(HT f32[T, 680, 32], T2 f32[T, 2720, 64]) of the stacked conv weights W1 f32[T, 32, 3, 8, 8], b1 f32[T, 32],
+    W2 f32[T, 64, 32, 4, 4] (atlas f32[5, 3, 8, 8] / 255, idx int16[680, 4]: CNNActorCritic.stage_consts)."""
+    T = int(W1.shape[0])
+    assert W1.shape == (T, 32, 3, 8, 8) and b1.shape == (T, 32) and W2.shape == (T, 64, 32, 4, 4)
+    assert all(x.dtype == torch.float32 and x.is_contiguous() for x in (W1, b1, W2, atlas))
+    assert idx.dtype == torch.int16 and idx.shape == (680, 4) and atlas.shape == (5, 3, 8, 8)
+    HT = torch.empty((T, 680, 32), dtype=torch.float32, device=W1.device) if HT is None else HT
+    T2 = torch.empty((T, LUT2_ROWS, 64), dtype=torch.float32, device=W1.device) if T2 is None else T2
+    check(lib().merlin_stage_tables_fwd(ptr(W1), ptr(b1), ptr(W2), ptr(atlas), ptr(idx), T, ptr(HT), ptr(T2),
+                                        stream_of(W1)), "merlin_stage_tables_fwd")
+    return HT, T2
+
+
+def stage_tables_bwd(W2, HT, dT2, atlas, koff, kv, dW1=None, db1=None, dW2=None, dH=None):
+    """(dW1, db1, dW2) of stage_tables_fwd from dT2 f32[T, 2720, 64] (koff int16[81] / kv int16[2720]: the
+    combinations of each conv1-table entry, CNNActorCritic.stage_consts)."""
+    T = int(W2.shape[0])
+    dev = W2.device
+    assert dT2.shape == (T, LUT2_ROWS, 64) and HT.shape == (T, 680, 32) and dT2.is_contiguous()
+    assert koff.dtype == kv.dtype == torch.int16 and koff.numel() == 81 and kv.numel() == 2720
+    dW1 = torch.empty((T, 32, 3, 8, 8), dtype=torch.float32, device=dev) if dW1 is None else dW1
+    db1 = torch.empty((T, 32), dtype=torch.float32, device=dev) if db1 is None else db1
+    dW2 = torch.empty((T, 64, 32, 4, 4), dtype=torch.float32, device=dev) if dW2 is None else dW2
+    dH = torch.empty((T, 680, 32), dtype=torch.float32, device=dev) if dH is None else dH
+    assert all(x.is_contiguous() for x in (dW1, db1, dW2, dH))
+    check(lib().merlin_stage_tables_bwd(ptr(W2), ptr(HT), ptr(dT2), ptr(atlas), ptr(koff), ptr(kv), T, ptr(dH),
+                                        ptr(dW1), ptr(db1), ptr(dW2), stream_of(W2)), "merlin_stage_tables_bwd")
+    return dW1, db1, dW2
 
 
 def clip_adam(params, grads, exp_avgs, exp_avg_sqs, steps, lr, beta1, beta2, eps, max_norm, norm_out=None,

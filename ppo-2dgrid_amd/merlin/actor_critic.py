@@ -405,6 +405,21 @@ class CNNActorCritic(nn.Module):
         return self.conv2_tables_from(torch.stack([ea[0].weight, ec[0].weight]), torch.stack([ea[0].bias, ec[0].bias]),
                                       torch.stack([ea[2].weight, ec[2].weight]))
 
+    def stage_consts(self, device):
+        """(atlas f32[5, 3, 8, 8] / 255, idx int16[680, 4], koff int16[81], kv int16[2720]) for the HIP table
+        kernels (merlin_stage_tables_fwd / _bwd): each combination's four conv1-table entries, in table order,
+        and per entry k the combinations reading it (CSR, (v, e) order)."""
+        if getattr(self, "_stage_consts", None) is None or self._stage_consts[0].device != device:
+            idx = torch.cat([i for _, i in _LUT2_H1])  # [680, 4] int64
+            flat = idx.reshape(-1)
+            order = torch.sort(flat, stable=True).indices  # (v, e) positions grouped by entry, (v, e) order
+            kv = (order // 4).to(torch.int16)
+            koff = torch.zeros(81, dtype=torch.int64)
+            koff[1:] = torch.cumsum(torch.bincount(flat, minlength=80), 0)
+            self._stage_consts = (self._atlas_on(device).contiguous(), idx.to(torch.int16).to(device),
+                                  koff.to(torch.int16).to(device), kv.to(device))
+        return self._stage_consts
+
     def conv2_tables_from(self, W1, b1, W2):
         """conv2_tables of the stacked weights W1 [2, 32, 3, 8, 8], b1 [2, 32], W2 [2, 64, 32, 4, 4]."""
         P = self.conv1_tables_from(W1)

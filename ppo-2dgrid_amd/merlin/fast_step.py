@@ -57,8 +57,11 @@ class WeightStage:
     gradients the step wrote into self.grads (db2, dW3r, db3, dW4p, db4: views of the derived-gradient buffer),
     and scatters the whole buffer onto the stage parameters' slots of the flat gradient (one launch)."""
 
-    def __init__(self, ac, flat_params: torch.Tensor, flat_grad: torch.Tensor):
+    def __init__(self, ac, flat_params: torch.Tensor, flat_grad: torch.Tensor, impl: str = "hip"):
         self.ac = ac
+        # "hip": T2 and its adjoint by csrc/merlin_stage.hip (2 launches each way); "torch": the same tables by
+        # CNNActorCritic.conv2_tables_from and autograd (the autograd path's exact arithmetic)
+        self.impl = impl
         self.flat_params, self.flat_grad = flat_params, flat_grad
         self.ptr = flat_params.data_ptr()
         ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
@@ -98,35 +101,50 @@ class WeightStage:
 
     def _fwd(self):
         D = self.flat_params.index_select(0, self.fwd_map)  # every derived weight in one launch
-        W1, b1, W2 = (self.seg(D, k).requires_grad_() for k in ("W1", "b1", "W2"))
-        T2 = self.ac.conv2_tables_from(W1, b1, W2)
+        if self.impl == "hip":
+            W1, b1, W2 = (self.seg(D, k) for k in ("W1", "b1", "W2"))
+            HT, T2 = nat.stage_tables_fwd(W1, b1, W2, *self.ac.stage_consts(D.device)[:2])
+            leaves = (W2, HT)
+        else:
+            leaves = W1, b1, W2 = tuple(self.seg(D, k).requires_grad_() for k in ("W1", "b1", "W2"))
+            T2 = self.ac.conv2_tables_from(W1, b1, W2)
         o = self.offs["W4p"]
         planes = nat.x6_split(D[o:].view(-1, 8)).view(-1)  # W4p and W4p^T back to back
         H = self.shapes["W4p"][1]
         n4 = 2 * H * 576 * 3
-        return D, (W1, b1, W2), T2, (planes[:n4].view(2, H, 3 * 576), planes[n4:].view(2, 576, 3 * H))
+        return D, leaves, T2, (planes[:n4].view(2, H, 3 * 576), planes[n4:].view(2, 576, 3 * H))
 
     def _capture(self):
         main = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(main)
+        hip = self.impl == "hip"
         with torch.cuda.stream(side), torch.enable_grad():
             for _ in range(2):  # lazy initialisation (GEMM handles, cached gather matrices) outside the captures
                 _, leaves, T2, _ = self._fwd()
-                torch.autograd.grad(T2, leaves, grad_outputs=torch.ones_like(T2))
+                if not hip:
+                    torch.autograd.grad(T2, leaves, grad_outputs=torch.ones_like(T2))
         main.wait_stream(side)
         torch.cuda.synchronize()
         self.pool = torch.cuda.graph_pool_handle()
         self.gfwd, self.gbwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         DG = torch.zeros(self.fwd_map.numel(), dtype=torch.float32, device=self.flat_params.device)
         self.gT2 = torch.zeros((2, nat.LUT2_ROWS, 64), dtype=torch.float32, device=DG.device)
+        self._dH = torch.empty((2, 680, 32), dtype=torch.float32, device=DG.device)  # scratch of the HIP adjoint
         with torch.enable_grad():
             with torch.cuda.graph(self.gfwd, pool=self.pool):
                 D, leaves, T2, planes = self._fwd()
             with torch.cuda.graph(self.gbwd, pool=self.pool):
-                gs = torch.autograd.grad(T2, leaves, grad_outputs=self.gT2, retain_graph=True)
-                for g, k in zip(gs, ("W1", "b1", "W2")):
-                    self.seg(DG, k).copy_(g)
+                if hip:
+                    gs = None
+                    W2, HT = leaves
+                    atlas, _, koff, kv = self.ac.stage_consts(DG.device)
+                    nat.stage_tables_bwd(W2, HT, self.gT2, atlas, koff, kv, dW1=self.seg(DG, "W1"),
+                                         db1=self.seg(DG, "b1"), dW2=self.seg(DG, "W2"), dH=self._dH)
+                else:
+                    gs = torch.autograd.grad(T2, leaves, grad_outputs=self.gT2, retain_graph=True)
+                    for g, k in zip(gs, ("W1", "b1", "W2")):
+                        self.seg(DG, k).copy_(g)
                 self.flat_grad.index_copy_(0, self.fwd_map[:self.n_grad], DG[:self.n_grad])
         self._keep = (D, leaves, T2, gs)  # the saved tensors the backward graph reads stay allocated
         self.outs = (T2.detach(),) + tuple(self.seg(D, k) for k in ("b2", "W3r", "b3", "W4p", "b4"))
@@ -171,7 +189,7 @@ class WindowStep:
             views[p] = flat[off:off + n].view_as(p)
             off += n
         self.flat, self.views = flat, views
-        self.stage = WeightStage(ac, flat_params, flat)
+        self.stage = WeightStage(ac, flat_params, flat, impl=getattr(agent, "stage_impl", "hip"))
         self.head = (ac.actor[2].weight, ac.actor[2].bias, ac.critic[2].weight, ac.critic[2].bias)
         self._side = None
 

@@ -99,6 +99,7 @@ class PPO:
         # PPO._sgd on the window + x6 path: the minibatch step with its launches written out (merlin/fast_step.py;
         # False = the same kernels through the autograd engine)
         self.fast_step = True
+        self.stage_impl = "hip"  # the fast step's conv tables: csrc/merlin_stage.hip, or "torch" (autograd's arithmetic)
         self._wstep = None
         # acting draws: counter-based (merlin_act_heads), keyed by this seed (torch.manual_seed's,
         # read without consuming the RNG), the rollout counter below (bumped inside the captured

@@ -107,3 +107,27 @@ def test_cli_single_env_seed_reproducible(tmp_path, monkeypatch, device):
     assert torch.equal(c1, c2) and (r1 == r2).all()
     assert all(torch.equal(s1[k], s2[k]) for k in s1)
     assert not (r1 == r3).all()
+
+
+def test_fomaml_cli_smoke(tmp_path, monkeypatch, device):
+    """fomaml_train.py (drop-in for the reference's fomaml/fomaml_train.py:37-178) end to end at a tiny budget:
+    two meta-iterations of 4 tasks, checkpoints in the reference's layout, loadable with the model's keys."""
+    import importlib.util
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ppo-2dgrid_amd",
+                        "fomaml_train.py")
+    spec = importlib.util.spec_from_file_location("fomaml_train", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    monkeypatch.chdir(tmp_path)
+    args = mod.parse_args(["--device", "cuda", "--difficulty", "mediumhard", "--seed", "7", "--iterations", "2",
+                           "--tasks_per_batch", "4", "--k_steps", "32", "--save_every", "2"])
+    fomaml = mod.train_fomaml(args)
+    runs = os.listdir(tmp_path / "checkpoints")
+    assert len(runs) == 1 and runs[0].startswith("MERLIN-MediumHard-v0_16x16_mediumhard_FOMAML_")
+    d = tmp_path / "checkpoints" / runs[0] / "seed_7"
+    names = sorted(os.listdir(d))
+    assert names == ["fomaml_best.pth", "fomaml_final.pth", "fomaml_iter_2.pth"]
+    sd = torch.load(d / "fomaml_final.pth", weights_only=True)
+    assert set(sd) == set(fomaml.meta_policy.state_dict())
+    assert all(torch.isfinite(v).all() for v in sd.values())

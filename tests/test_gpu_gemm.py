@@ -57,7 +57,7 @@ def test_gemm_nt_vs_float64(device, M, N, K, cfg):
     assert torch.equal(Cb, torch.relu(C + bias.unsqueeze(1)))
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 20, 21])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 20, 21, 24, 25])
 @pytest.mark.parametrize("Kd,splits", [(1, 1), (4093, 7), (40000, 32), (40000, 64)])
 def test_gemm_tn_vs_float64(device, Kd, splits, cfg):
     from merlin import _native as nat
@@ -75,7 +75,7 @@ def test_gemm_tn_vs_float64(device, Kd, splits, cfg):
     assert torch.equal(W, nat.x6_gemm_tn(dz, a3, splits=splits, cfg=cfg))
 
 
-@pytest.mark.parametrize("cfg", [0, 20, 21])
+@pytest.mark.parametrize("cfg", [0, 20, 21, 24, 25])
 def test_gemm_tn_cancellation(device, cfg):
     """The update's weight gradient: ~1e5 rows whose terms nearly cancel (|W| ~ 1e-2 sum |a b|)."""
     from merlin import _native as nat
