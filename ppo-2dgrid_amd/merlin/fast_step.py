@@ -165,6 +165,11 @@ class WeightStage:
         self.gbwd.replay()
 
 
+# fc1's weight gradient on the side stream from right after the heads' backward (True: beside the input gradient
+# too) or from after the input gradient (False: beside conv3's segmented sums only)
+WGRAD_EARLY = False
+
+
 class WindowStep:
     """One optimizer step of PPO._sgd on the window + x6 path (see the module docstring)."""
 
@@ -240,12 +245,17 @@ class WindowStep:
         # ---- backward (_WindowTowerHeadX6.backward, _WindowGemm / _BiasRelu / _WindowConv2 backward)
         dz, _, _, _ = nat.head_bwd(h, dlogits, dvalue, Wa, Wc, out_bias=g[5], out_w_actor=self.views[Wa],
                                    out_w_critic=self.views[Wc])
-        da3 = nat.x6_gemm_nt(dz, P4t, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
         main = torch.cuda.current_stream()
         side = self.side_stream(dz.device)
-        side.wait_stream(main)  # fc1's weight gradient beside conv3's segmented sums
-        with torch.cuda.stream(side):
-            nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
+        if WGRAD_EARLY:  # fc1's weight gradient beside the input gradient and conv3's segmented sums
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
+        da3 = nat.x6_gemm_nt(dz, P4t, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+        if not WGRAD_EARLY:  # fc1's weight gradient beside conv3's segmented sums
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
         dz.record_stream(side)
         a3.record_stream(side)
         dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]))

@@ -54,6 +54,9 @@ def main():
             agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6"
             agent._clip_adam = None if name == "torch_opt" else clip_adam
             agent.fast_step = name.startswith("fast")  # merlin/fast_step.py vs the autograd engine
+            from merlin import fast_step as FS
+
+            FS.WGRAD_EARLY = "wgrad_early" in name
             if agent.stage_impl != ("torch" if "torch_stage" in name else "hip"):
                 agent.stage_impl = "torch" if "torch_stage" in name else "hip"
                 agent._wstep = None  # recapture the weight stage with the other table implementation

@@ -63,7 +63,7 @@ def test_fast_step_hip_tables_close_and_reproducible(device):
         d = (p1 - p0).detach().abs()
         assert float(d.max()) <= 2 * 1e-3 * 8, k
         if k.startswith("critic"):
-            assert int((d <= 1e-6 + 1e-4 * p0.detach().abs()).sum()) >= 0.999 * p0.numel(), k
+            assert int((d <= 1e-6 + 1e-4 * p0.detach().abs()).sum()) >= 0.99 * p0.numel(), k
 
 
 def test_stage_tables_match_torch(device):
