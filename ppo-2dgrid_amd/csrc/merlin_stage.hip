@@ -10,125 +10,170 @@
 //   T2[t][4 v + j][co]  = sum_o HT[t][v][o] * W2[t][co][o][2 a + yp][2 b + xp]   (j = 2 a + b, (yp, xp) = v's
 //                         parity type; csrc/merlin_conv2lut.hip's table layout)
 // Backward from dT2: dH = [HT > 0] * (dT2 . W2), dW2 = sum over the type's combinations of HT x dT2, db1 = sum_v dH,
-// dP[o][k] = sum over the (v, e) with idx[v][e] = k of dH[v][o], dW1 = dP contracted with the atlas.  Every sum
-// runs in a fixed order: the same bits every call.
+// dP[o][k] = sum over the (v, e) with idx[v][e] = k of dH[v][o], dW1 = dP contracted with the atlas.
+//
+// The combinations of one parity type (ee 5, eo 25, oe 25, oo 625) all read the same 4 of W2's 16 taps, so the
+// forward and dH kernels work on chunks of up to 8 combinations of one type with that type's W2 slice ([64][4][32],
+// 32 KB) in LDS; dW2 is one block per (tower, type, tap) summing over the type's combinations in chunks staged
+// through LDS.  Every sum runs in a fixed order: the same bits every call.
 #include "merlin_internal.h"
 
 namespace merlin {
 namespace {
 
 constexpr int C1 = 32, C2 = 64, NV = 680, NROW = 4 * NV;  // conv1 / conv2 channels, combinations, T2 rows
-constexpr int VB = 8;                                    // combinations per block of the forward / dH kernels
-// combinations of parity types ee, eo, oe, oo: v in [off[p], off[p + 1])
-__device__ __forceinline__ int part_of(int v) { return v < 5 ? 0 : v < 30 ? 1 : v < 55 ? 2 : 3; }
-__device__ __forceinline__ int part_off(int p) { return p == 0 ? 0 : p == 1 ? 5 : p == 2 ? 30 : 55; }
+constexpr int VB = 8;                                    // combinations per chunk
+constexpr int NCH = 1 + 4 + 4 + 79;                      // chunks of 8 per type: ceil(5/8) + 2 ceil(25/8) + ceil(625/8)
 
-// P[o][k] (k = slot * 20 + bin) of one tower into LDS: 2,560 values, 48 products each
-__device__ void conv1_tables(const float *__restrict__ W1, const float *__restrict__ atlas, float *__restrict__ P) {
-    for (int q = threadIdx.x; q < C1 * 80; q += blockDim.x) {
+__device__ __forceinline__ int part_off(int p) { return p == 0 ? 0 : p == 1 ? 5 : p == 2 ? 30 : p == 3 ? 55 : NV; }
+
+// chunk -> (type, first combination, count)
+__device__ __forceinline__ void chunk_of(int c, int &p, int &v0, int &nv) {
+    const int first[5] = {0, 1, 5, 9, NCH};
+    p = c < first[1] ? 0 : c < first[2] ? 1 : c < first[3] ? 2 : 3;
+    v0 = part_off(p) + (c - first[p]) * VB;
+    nv = min(VB, part_off(p + 1) - v0);
+}
+
+// W2[t] slice of type p into LDS as [co][j][o] (o fastest: conflict-free reads across o)
+__device__ void load_w2_slice(const float *__restrict__ W2, int p, float *__restrict__ Ws) {
+    const int yp = p >> 1, xp = p & 1;
+    for (int q = threadIdx.x; q < C2 * 4 * C1; q += blockDim.x) {
+        const int co = q / (4 * C1), r = q - co * 4 * C1, j = r / C1, o = r - j * C1;
+        Ws[q] = W2[((size_t)co * C1 + o) * 16 + (2 * (j >> 1) + yp) * 4 + 2 * (j & 1) + xp];
+    }
+}
+
+// grid (NCH, T): HT rows of one chunk and their T2 rows; HT saved for the backward
+__global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1, const float *__restrict__ b1,
+                                                   const float *__restrict__ W2, const float *__restrict__ atlas,
+                                                   const int16_t *__restrict__ idx, float *__restrict__ HT,
+                                                   float *__restrict__ T2) {
+    __shared__ float Wl[C1 * 3 * 64], Al[5 * 3 * 64], P[C1 * 80], H[VB][C1], Ws[C2 * 4 * C1];
+    const int t = blockIdx.y;
+    int p, v0, nv;
+    chunk_of(blockIdx.x, p, v0, nv);
+    W1 += (size_t)t * C1 * 3 * 64;
+    for (int q = threadIdx.x; q < C1 * 3 * 64; q += 256) Wl[q] = W1[q];
+    for (int q = threadIdx.x; q < 5 * 3 * 64; q += 256) Al[q] = atlas[q];
+    load_w2_slice(W2 + (size_t)t * C2 * C1 * 16, p, Ws);
+    __syncthreads();
+    for (int q = threadIdx.x; q < C1 * 80; q += 256) {  // P[o][k], 48 products each
         const int o = q / 80, k = q - o * 80;
         const int slot = k / 20, bin = k - slot * 20;
         const int dy = slot >> 1, dx = slot & 1, z = bin >> 2, qy = (bin >> 1) & 1, qx = bin & 1;
         float acc = 0.0f;
         for (int c = 0; c < 3; c++)
+#pragma unroll
             for (int kk = 0; kk < 4; kk++)
+#pragma unroll
                 for (int l = 0; l < 4; l++)
-                    acc += W1[((o * 3 + c) * 8 + 4 * dy + kk) * 8 + 4 * dx + l] *
-                           atlas[((z * 3 + c) * 8 + 4 * qy + kk) * 8 + 4 * qx + l];
+                    acc += Wl[(o * 3 + c) * 64 + (4 * dy + kk) * 8 + 4 * dx + l] *
+                           Al[(z * 3 + c) * 64 + (4 * qy + kk) * 8 + 4 * qx + l];
         P[q] = acc;
     }
-}
-
-// grid (NV / VB, T): HT rows v0 .. v0 + VB and their T2 rows; HT saved for the backward
-__global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1, const float *__restrict__ b1,
-                                                   const float *__restrict__ W2, const float *__restrict__ atlas,
-                                                   const int16_t *__restrict__ idx, float *__restrict__ HT,
-                                                   float *__restrict__ T2) {
-    __shared__ float P[C1 * 80];
-    __shared__ float H[VB][C1];
-    const int t = blockIdx.y, v0 = blockIdx.x * VB;
-    W1 += (size_t)t * C1 * 3 * 64;
-    b1 += t * C1;
-    W2 += (size_t)t * C2 * C1 * 16;
-    conv1_tables(W1, atlas, P);
     __syncthreads();
     {
         const int vl = threadIdx.x / C1, o = threadIdx.x - vl * C1;  // VB * C1 == 256
-        const int v = v0 + vl;
-        float s = b1[o];
-        for (int e = 0; e < 4; e++) s += P[o * 80 + idx[v * 4 + e]];
-        s = s != s ? s : fmaxf(s, 0.0f);
-        H[vl][o] = s;
-        HT[((size_t)t * NV + v) * C1 + o] = s;
+        if (vl < nv) {
+            const int v = v0 + vl;
+            float s = b1[t * C1 + o];
+            for (int e = 0; e < 4; e++) s += P[o * 80 + idx[v * 4 + e]];
+            s = s != s ? s : fmaxf(s, 0.0f);
+            H[vl][o] = s;
+            HT[((size_t)t * NV + v) * C1 + o] = s;
+        }
     }
     __syncthreads();
-    // T2 rows 4 v + j, v in the block: VB * 4 * 64 = 2048 outputs, 8 per thread
-    for (int q = threadIdx.x; q < VB * 4 * C2; q += 256) {
+    for (int q = threadIdx.x; q < nv * 4 * C2; q += 256) {  // T2 rows 4 v + j
         const int vl = q / (4 * C2), r = q - vl * 4 * C2, j = r / C2, co = r - j * C2;
-        const int v = v0 + vl, p = part_of(v), yp = p >> 1, xp = p & 1, a = j >> 1, b = j & 1;
-        const float *w = W2 + (size_t)co * C1 * 16 + (2 * a + yp) * 4 + 2 * b + xp;
+        const float *w = Ws + (co * 4 + j) * C1;
         float acc = 0.0f;
-        for (int o = 0; o < C1; o++) acc += H[vl][o] * w[o * 16];
-        T2[((size_t)t * NROW + 4 * v + j) * C2 + co] = acc;
+#pragma unroll 8
+        for (int o = 0; o < C1; o++) acc += H[vl][o] * w[o];
+        T2[((size_t)t * NROW + 4 * (v0 + vl) + j) * C2 + co] = acc;
     }
 }
 
-// grid (NV / VB, T): dH[t][v][o] = [HT > 0] * sum_{j, co} dT2[4 v + j][co] * W2[co][o][tap(v, j)]
+// grid (NCH, T): dH[t][v][o] = [HT > 0] * sum_{j, co} dT2[4 v + j][co] * W2[co][o][tap(type, j)]
 __global__ __launch_bounds__(256) void k_stage_bwd_h(const float *__restrict__ W2, const float *__restrict__ HT,
                                                      const float *__restrict__ dT2, float *__restrict__ dH) {
-    __shared__ float G[VB][4 * C2];
-    const int t = blockIdx.y, v0 = blockIdx.x * VB;
-    W2 += (size_t)t * C2 * C1 * 16;
-    for (int q = threadIdx.x; q < VB * 4 * C2; q += 256)
+    __shared__ float G[VB][4 * C2], Ws[C2 * 4 * C1];
+    const int t = blockIdx.y;
+    int p, v0, nv;
+    chunk_of(blockIdx.x, p, v0, nv);
+    load_w2_slice(W2 + (size_t)t * C2 * C1 * 16, p, Ws);
+    for (int q = threadIdx.x; q < nv * 4 * C2; q += 256)
         G[q / (4 * C2)][q % (4 * C2)] = dT2[((size_t)t * NROW + 4 * v0) * C2 + q];
     __syncthreads();
     const int vl = threadIdx.x / C1, o = threadIdx.x - vl * C1;
-    const int v = v0 + vl, p = part_of(v), yp = p >> 1, xp = p & 1;
+    if (vl >= nv) return;
     float acc = 0.0f;
-    for (int j = 0; j < 4; j++) {
-        const int tap = (2 * (j >> 1) + yp) * 4 + 2 * (j & 1) + xp;
-        for (int co = 0; co < C2; co++) acc += G[vl][j * C2 + co] * W2[((size_t)co * C1 + o) * 16 + tap];
-    }
-    const size_t hi = ((size_t)t * NV + v) * C1 + o;
+    for (int j = 0; j < 4; j++)
+#pragma unroll 8
+        for (int co = 0; co < C2; co++) acc += G[vl][j * C2 + co] * Ws[(co * 4 + j) * C1 + o];
+    const size_t hi = ((size_t)t * NV + v0 + vl) * C1 + o;
     dH[hi] = HT[hi] > 0.0f ? acc : 0.0f;
 }
 
-// blocks [0, T * 128): dW2, 256 outputs each (t, co, o, tap): sum over the combinations of the tap's parity type
-// of HT[v][o] * dT2[4 v + j][co];  blocks [T * 128, T * 128 + T * C1): tower t, conv1 channel o: db1[o] =
-// sum_v dH[v][o], dP[o][k] for the 80 k (combinations in v order, through the CSR kinv), then dW1[o][c][ky][kx]
+constexpr int VS = 32;  // combinations per LDS stage of the dW2 blocks
+
+// blocks [0, T * 16): (tower, type, j): dW2[co][o][tap] = sum over the type's combinations of HT[v][o] *
+// dT2[4 v + j][co], 8 outputs per thread, combinations staged VS at a time;  blocks [T * 16, T * 16 + T * C1):
+// tower t, conv1 channel o: db1[o] = sum_v dH[v][o] (256 strided partial sums, then a fixed tree), dP[o][k] for
+// the 80 k (combinations in (v, e) order through the CSR kinv), then dW1[o][c][ky][kx]
 __global__ __launch_bounds__(256) void k_stage_bwd_w(const float *__restrict__ HT, const float *__restrict__ dT2,
                                                      const float *__restrict__ dH, const float *__restrict__ atlas,
                                                      const int16_t *__restrict__ koff, const int16_t *__restrict__ kv,
                                                      int T, float *__restrict__ dW1, float *__restrict__ db1,
                                                      float *__restrict__ dW2) {
-    const int nb2 = T * (C2 * C1 * 16 / 256);
-    if ((int)blockIdx.x < nb2) {
-        const int q = blockIdx.x * 256 + threadIdx.x;  // (t, co, o, tap) in dW2's layout
-        const int t = q / (C2 * C1 * 16), r = q - t * (C2 * C1 * 16);
-        const int co = r / (C1 * 16), o = (r / 16) % C1, tap = r % 16, ky = tap >> 2, kx = tap & 3;
-        const int p = 2 * (ky & 1) + (kx & 1), j = 2 * (ky >> 1) + (kx >> 1);
-        const int va = part_off(p), vb = p == 3 ? NV : part_off(p + 1);
-        const float *h = HT + (size_t)t * NV * C1 + o;
-        const float *g = dT2 + (size_t)t * NROW * C2 + j * C2 + co;
-        float acc = 0.0f;
-        for (int v = va; v < vb; v++) acc += h[(size_t)v * C1] * g[(size_t)v * 4 * C2];
-        dW2[q] = acc;
+    __shared__ float Hs[VS][C1], Gs[VS][C2], red[256], dP[80];
+    if ((int)blockIdx.x < T * 16) {
+        const int t = blockIdx.x / 16, p = (blockIdx.x / 4) & 3, j = blockIdx.x & 3;
+        const int tap = (2 * (j >> 1) + (p >> 1)) * 4 + 2 * (j & 1) + (p & 1);
+        const int va = part_off(p), vb = part_off(p + 1);
+        const int o = threadIdx.x & (C1 - 1), cq = threadIdx.x >> 5;  // outputs (co = cq + 8 i, o)
+        float acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) acc[i] = 0.0f;
+        for (int vs = va; vs < vb; vs += VS) {
+            const int n = min(VS, vb - vs);
+            __syncthreads();
+            for (int q = threadIdx.x; q < n * C1; q += 256) Hs[q / C1][q % C1] = HT[((size_t)t * NV + vs) * C1 + q];
+            for (int q = threadIdx.x; q < n * C2; q += 256) {
+                const int vl = q / C2, co = q - vl * C2;
+                Gs[vl][co] = dT2[((size_t)t * NROW + 4 * (vs + vl) + j) * C2 + co];
+            }
+            __syncthreads();
+            for (int vl = 0; vl < n; vl++) {
+                const float h = Hs[vl][o];
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] += h * Gs[vl][cq + 8 * i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) dW2[(((size_t)t * C2 + cq + 8 * i) * C1 + o) * 16 + tap] = acc[i];
         return;
     }
-    __shared__ float dP[80];
-    const int b = blockIdx.x - nb2, t = b / C1, o = b - t * C1;
+    const int b = blockIdx.x - T * 16, t = b / C1, o = b - t * C1;
     const float *d = dH + (size_t)t * NV * C1 + o;
+    {  // db1: thread i sums combinations i, i + 256, ... in order, then a fixed tree
+        float s = 0.0f;
+        for (int v = threadIdx.x; v < NV; v += 256) s += d[(size_t)v * C1];
+        red[threadIdx.x] = s;
+    }
     if (threadIdx.x < 80) {  // dP[o][k]: the (v, e) entries with idx[v][e] = k, in (v, e) order
         const int k = threadIdx.x;
         float acc = 0.0f;
         for (int i = koff[k]; i < koff[k + 1]; i++) acc += d[(size_t)kv[i] * C1];
         dP[k] = acc;
-    } else if (threadIdx.x == 128) {
-        float acc = 0.0f;
-        for (int v = 0; v < NV; v++) acc += d[(size_t)v * C1];
-        db1[t * C1 + o] = acc;
     }
     __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) db1[t * C1 + o] = red[0];
     for (int q = threadIdx.x; q < 3 * 64; q += 256) {  // dW1[t][o][c][ky][kx]
         const int c = q >> 6, ky = (q >> 3) & 7, kx = q & 7;
         const int dy = ky >> 2, kk = ky & 3, dx = kx >> 2, l = kx & 3, slot = 2 * dy + dx;
@@ -145,18 +190,18 @@ __global__ __launch_bounds__(256) void k_stage_bwd_w(const float *__restrict__ H
 
 hipError_t launch_stage_fwd(const float *W1, const float *b1, const float *W2, const float *atlas, const int16_t *idx,
                             int T, float *HT, float *T2, hipStream_t s) {
-    hipLaunchKernelGGL(k_stage_fwd, dim3(NV / VB, T), dim3(256), 0, s, W1, b1, W2, atlas, idx, HT, T2);
+    hipLaunchKernelGGL(k_stage_fwd, dim3(NCH, T), dim3(256), 0, s, W1, b1, W2, atlas, idx, HT, T2);
     return hipGetLastError();
 }
 
 hipError_t launch_stage_bwd(const float *W2, const float *HT, const float *dT2, const float *atlas,
                             const int16_t *koff, const int16_t *kv, int T, float *dH, float *dW1, float *db1,
                             float *dW2, hipStream_t s) {
-    hipLaunchKernelGGL(k_stage_bwd_h, dim3(NV / VB, T), dim3(256), 0, s, W2, HT, dT2, dH);
+    hipLaunchKernelGGL(k_stage_bwd_h, dim3(NCH, T), dim3(256), 0, s, W2, HT, dT2, dH);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_stage_bwd_w, dim3(T * (C2 * C1 * 16 / 256) + T * C1), dim3(256), 0, s, HT, dT2, dH, atlas,
-                       koff, kv, T, dW1, db1, dW2);
+    hipLaunchKernelGGL(k_stage_bwd_w, dim3(T * 16 + T * C1), dim3(256), 0, s, HT, dT2, dH, atlas, koff, kv, T, dW1,
+                       db1, dW2);
     return hipGetLastError();
 }
 
