@@ -345,6 +345,10 @@ def kernel_table(records):
     return out
 
 
+# the MFMA each x6 GEMM runs on (merlin._native.X6_NT_CFG / X6_TN_CFG: cfg >= 20 are the 32x32x16 kernels)
+X6_MFMA = {"gemm_fc1_fwd": "bf16 32x32x16", "gemm_fc1_dgrad": "bf16 32x32x16", "gemm_wgrad": "bf16 16x16x32"}
+
+
 def roofline_of(name, k, x6=False):
     traffic = pmc_traffic(name)
     if "tflops" in k and x6 and name in X6_GEMMS:  # fc1 on the bf16 matrix cores: executed bf16 MFMA work
@@ -352,7 +356,7 @@ def roofline_of(name, k, x6=False):
         return {"kernel": name, "bound": "mfma", "achieved": round(ex, 2), "peak": BF16_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ex / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                 "flops_per_launch": k["flops_per_launch"] * X6_PRODUCTS, "avg_launch_us": k["avg_us"],
-                "launches": k["launches"], "mfma": "bf16 16x16x32, 6 plane products per fp32 product",
+                "launches": k["launches"], "mfma": X6_MFMA.get(name, "bf16") + ", 6 plane products per fp32 product",
                 "fp32_equivalent_tflops": k["tflops"],
                 "fp32_equivalent_frac_of_f32_peak": round(k["tflops"] / FP32_PEAK_TFLOPS, 4)}
     if "tflops" in k:  # a hipBLASLt GEMM: f32 MFMA bound
