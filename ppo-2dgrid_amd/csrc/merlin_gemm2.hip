@@ -613,6 +613,169 @@ hipError_t tn32k16_launch(const void *A, const void *B, int64_t Kd, int M, int N
     return hipGetLastError();
 }
 
+// NT with 16-deep k steps, four waves and two blocks per CU.  The 8-wave kernels above hold a whole CU (one block:
+// 122-147 KB of LDS), and one barrier per k step keeps both waves of each SIMD in the same phase, so the matrix
+// pipe idles while they split, stage and wait for fragments together.  Here a block is one wave per SIMD with a
+// 61-74 KB two-stage LDS ring, two blocks share a CU, and the two waves of a SIMD come from different blocks:
+// one's staging runs beside the other's MFMAs.  Per MFMA the split, the staging and the fragment reads are
+// smaller too (wave tiles of 128 x 64 / 64 x 96).  Accumulators chunked per k step (the step's six plane
+// products of a 32 x 32 tile in a fresh set, added to the running sum once).  LDS plane images: rows of two
+// 16-B chunks, chunk index XOR (row >> 3) & 1 (the ds_read_b128 fragment reads of each lane group hit 16
+// distinct 16-B bank slots).
+template <int BM, int BN, int WGM, int WGN, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN, 2) void k_x6_nt32b(const float4 *__restrict__ A, const u32x4 *__restrict__ B,
+                                                                int64_t M, int N, int K, int64_t sA, int64_t sB,
+                                                                const float *__restrict__ bias, float *__restrict__ C,
+                                                                int64_t sC, int tiles_n) {
+    constexpr int K16 = 16;
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int QA = BM * 2;           // A units (row, group of 8 values) per k step
+    constexpr int QB = BN * 6;           // B 16-B chunks (row, group, plane) per k step
+    constexpr int UA = (QA + NT - 1) / NT, CB = (QB + NT - 1) / NT;
+    static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile of 32 x 32 MFMA tiles");
+    constexpr int PSA = BM * 2, PSB = BN * 2;  // chunks per plane image
+    constexpr int STAGE = 3 * (PSA + PSB);
+    __shared__ u32x4 lds[2 * STAGE];
+
+    const int t = blockIdx.y;
+    const int L = xcd_tile(blockIdx.x, gridDim.x);
+    const int tm = L / tiles_n, tn = L - tm * tiles_n;
+    const int64_t m0 = (int64_t)tm * BM;
+    const int n0 = tn * BN;
+    const int64_t rowA = K / 4;                 // float4s per A row
+    const int64_t rowB = (int64_t)(K / 8) * 3;  // chunks per B row
+    A += t * sA;
+    B += t * sB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    int oa[UA], la[UA];  // A: float4 offset of the unit's first value at k step 0; LDS chunk of plane 0
+#pragma unroll
+    for (int i = 0; i < UA; i++) {
+        const int q = std::min(tid + i * NT, QA - 1);
+        const int row = q >> 1, g = q & 1;
+        oa[i] = (int)(std::min<int64_t>(m0 + row, M - 1) * rowA) + g * 2;
+        la[i] = row * 2 + (g ^ ((row >> 3) & 1));
+    }
+    int ob[CB], lb[CB];
+#pragma unroll
+    for (int i = 0; i < CB; i++) {
+        const int q = std::min(tid + i * NT, QB - 1);
+        const int row = q / 6, rem = q - row * 6, g = rem / 3, p = rem - g * 3;
+        ob[i] = (int)((int64_t)(n0 + row) * rowB) + g * 3 + p;
+        lb[i] = 3 * PSA + p * PSB + row * 2 + (g ^ ((row >> 3) & 1));
+    }
+    float4 ra[UA][2];
+    u32x4 rb[CB];
+    auto load = [&](int kt) {
+#pragma unroll
+        for (int i = 0; i < UA; i++) {
+            ra[i][0] = A[(int64_t)oa[i] + kt * 4];
+            ra[i][1] = A[(int64_t)oa[i] + kt * 4 + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < CB; i++) rb[i] = B[ob[i] + kt * 6];
+    };
+    auto store = [&](int buf) {
+        u32x4 *st = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < UA; i++)
+            if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
+                u32x4 p0, p1, p2;
+                split8(ra[i][0], ra[i][1], p0, p1, p2);
+                st[la[i]] = p0;
+                st[PSA + la[i]] = p1;
+                st[2 * PSA + la[i]] = p2;
+            }
+#pragma unroll
+        for (int i = 0; i < CB; i++)
+            if (QB % NT == 0 || i + 1 < CB || tid + i * NT < QB) st[lb[i]] = rb[i];
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) acc[i][j] = f32x16{};
+
+    // fragment reads: row (tile base + lane & 31), chunk (lane >> 5) XOR (row >> 3) & 1
+    const int fr = lane & 31, fh = lane >> 5;
+    const int nk = K / K16;
+    load(0);
+    store(0);
+    if (nk > 1) load(1);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) store(buf ^ 1);
+        if (kt + 2 < nk) load(kt + 2);
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * PSA;
+        u32x4 bf[TN][3];
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int row = wn * WTN + j * 32 + fr;
+#pragma unroll
+            for (int p = 0; p < 3; p++) bf[j][p] = sBl[p * PSB + row * 2 + (fh ^ ((row >> 3) & 1))];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            const int row = wm * WTM + i * 32 + fr;
+            u32x4 af[3];
+#pragma unroll
+            for (int p = 0; p < 3; p++) af[p] = sAl[p * PSA + row * 2 + (fh ^ ((row >> 3) & 1))];
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                f32x16 c = mfma32(af[2], bf[j][0], f32x16{});
+                c = mfma32(af[1], bf[j][1], c);
+                c = mfma32(af[0], bf[j][2], c);
+                c = mfma32(af[1], bf[j][0], c);
+                c = mfma32(af[0], bf[j][1], c);
+                c = mfma32(af[0], bf[j][0], c);
+                acc[i][j] += c;
+            }
+        }
+        __syncthreads();
+    }
+
+    float *Ct = C + t * sC;
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+        const int col = n0 + wn * WTN + j * 32 + fr;
+        const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (row < M) {
+                    const float v = acc[i][j][r];
+                    Ct[row * N + col] = EPI == 1 ? relu_nan(v + bv) : v;
+                }
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+hipError_t nt32b_launch(const float *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
+                        const float *bias, float *C, int64_t sC, hipStream_t s) {
+    if (N % BN || K % 16) return hipErrorInvalidValue;
+    if ((M + BM) * (int64_t)(K / 4) > INT32_MAX) return hipErrorInvalidValue;  // 32-bit A offsets
+    const int64_t tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = N / BN;
+    const dim3 grid((unsigned)(tiles_m * tiles_n), T);
+    const float4 *a = reinterpret_cast<const float4 *>(A);
+    if (bias)
+        hipLaunchKernelGGL((k_x6_nt32b<BM, BN, WGM, WGN, 1>), grid, dim3(64 * WGM * WGN), 0, s, a, B, M, N, K, sA, sB, bias,
+                           C, sC, tiles_n);
+    else
+        hipLaunchKernelGGL((k_x6_nt32b<BM, BN, WGM, WGN, 0>), grid, dim3(64 * WGM * WGN), 0, s, a, B, M, N, K, sA, sB,
+                           nullptr, C, sC, tiles_n);
+    return hipGetLastError();
+}
+
 template <int BM, int BN, int WGM, int WGN, int ACC, int APL = 0>
 hipError_t nt32_launch(const void *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
                        const float *bias, float *C, int64_t sC, hipStream_t s) {
@@ -688,6 +851,10 @@ hipError_t launch_x6_gemm_nt32(const float *A, const void *B, int64_t M, int N, 
     const float *a = A;
     const int64_t sA = a_stride / 4;
     switch (cfg) {
+        // k_x6_nt32b: 16-deep k steps, 4 waves, two blocks per CU (forward 256 x 128, input gradient 128 x 192)
+        case 26: return nt32b_launch<256, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 27: return nt32b_launch<128, 192, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        case 28: return nt32b_launch<128, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         // forward shape (N = 512): 256 x 128 blocks, 8 waves of 64 x 64
         case 20: return nt32_launch<256, 128, 4, 2, 1>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         case 21: return nt32_launch<256, 128, 4, 2, 0>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);

@@ -57,6 +57,8 @@ def main():
             from merlin import fast_step as FS
 
             FS.WGRAD_EARLY = "wgrad_early" in name
+            nat.X6_NT_CFG["fwd"] = 28 if "fwd28" in name else 20
+            nat.X6_NT_CFG["dgrad"] = 27 if "dgrad27" in name else 22
             if agent.stage_impl != ("torch" if "torch_stage" in name else "hip"):
                 agent.stage_impl = "torch" if "torch_stage" in name else "hip"
                 agent._wstep = None  # recapture the weight stage with the other table implementation

@@ -27,7 +27,7 @@ def main():
     cfgs = [int(c) for c in os.environ.get("CFGS", "").split(",") if c] or None
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
-    shapes = {"fwd": (512, 576, True, [0, 20, 21, 24, 25, 10, 30]), "dgrad": (576, 512, False, [1, 22, 23, 13, 32])}
+    shapes = {"fwd": (512, 576, True, [0, 20, 21, 24, 25, 10, 30, 26, 28]), "dgrad": (576, 512, False, [1, 22, 23, 13, 32, 27])}
     if os.environ.get("PROF"):
         shapes = {"fwd": (512, 576, True, [0, 20]), "dgrad": (576, 512, False, [1, 22])}
     for name, (N, K, use_bias, cl) in shapes.items():
@@ -35,6 +35,9 @@ def main():
         A = torch.relu(torch.randn(2, U, K, device=dev, generator=g)) if use_bias else \
             torch.randn(2, U, K, device=dev, generator=g) * (torch.rand(2, U, K, device=dev, generator=g) > 0.5)
         Bp = nat.x6_split(torch.randn(2, N, K, device=dev, generator=g) / K ** 0.5)
+        if os.environ.get("ZEROS"):  # operand data toggling no bits: the matrix cores' power draw drops
+            A.zero_()
+            Bp.zero_()
         bias = torch.randn(2, N, device=dev, generator=g) * 0.1 if use_bias else None
         Ap = nat.x6_split(A)  # A as planes for the cfg >= 30 kernels
         AA = lambda c, X=None: (nat.x6_split(X) if X is not None else Ap) if c >= 30 else (A if X is None else X)  # noqa: E731
