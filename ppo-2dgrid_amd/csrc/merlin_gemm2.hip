@@ -855,6 +855,8 @@ hipError_t launch_x6_gemm_nt32(const float *A, const void *B, int64_t M, int N, 
         case 26: return nt32b_launch<256, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         case 27: return nt32b_launch<128, 192, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         case 28: return nt32b_launch<128, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
+        // small row counts (the rollout's fc1: 4,096 rows): 64 x 128 tiles, twice the blocks
+        case 29: return nt32b_launch<64, 128, 2, 2>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         // forward shape (N = 512): 256 x 128 blocks, 8 waves of 64 x 64
         case 20: return nt32_launch<256, 128, 4, 2, 1>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
         case 21: return nt32_launch<256, 128, 4, 2, 0>(a, b, M, N, K, T, sA, sB, bias, C, c_stride, s);
