@@ -518,31 +518,52 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restri
     }
     const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float4 ra[UA][2], rb[UB][2];
+    // each unit's row pointer at k0; a step whose rows are all below k1 (every step but a split's last) reads
+    // pointer + a wave-uniform row offset, no per-lane 64-bit clamp arithmetic (whose temporaries made the
+    // compiler park the loaded values in other registers: a wait right behind every load)
+    const float4 *pa[UA], *pb[UB];
+#pragma unroll
+    for (int i = 0; i < UA; i++) pa[i] = A + (k0 + ka[i]) * rowA + oa[i];
+#pragma unroll
+    for (int i = 0; i < UB; i++) pb[i] = B + (k0 + kb[i]) * rowB + ob[i];
     auto load = [&](int64_t kk) {
+        if (kk + BK <= k1) {
+            const int64_t da = (kk - k0) * rowA, db = (kk - k0) * rowB;
+#pragma unroll
+            for (int i = 0; i < UA; i++) {
+                ra[i][0] = pa[i][da];
+                ra[i][1] = pa[i][da + 1];
+            }
+#pragma unroll
+            for (int i = 0; i < UB; i++) {
+                rb[i][0] = pb[i][db];
+                rb[i][1] = pb[i][db + 1];
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < UA; i++) {
             const int64_t k = kk + ka[i];
             const float4 *src = A + std::min(k, k1 - 1) * rowA + oa[i];
-            const float4 x = src[0], y = src[1];
-            ra[i][0] = k < k1 ? x : zero;
-            ra[i][1] = k < k1 ? y : zero;
+            ra[i][0] = src[0];  // rows past k1 re-read row k1 - 1 and are zeroed when staged: a select
+            ra[i][1] = src[1];  // here would make the wave wait for the loads right after issuing them
         }
 #pragma unroll
         for (int i = 0; i < UB; i++) {
             const int64_t k = kk + kb[i];
             const float4 *src = B + std::min(k, k1 - 1) * rowB + ob[i];
-            const float4 x = src[0], y = src[1];
-            rb[i][0] = k < k1 ? x : zero;
-            rb[i][1] = k < k1 ? y : zero;
+            rb[i][0] = src[0];
+            rb[i][1] = src[1];
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int64_t kk) {  // the registers hold the rows of step kk; rows past k1 stage as zero
         u32x4 *st = lds + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < UA; i++)
             if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
+                const bool in = kk + ka[i] < k1;
                 u32x4 p0, p1, p2;
-                split8(ra[i][0], ra[i][1], p0, p1, p2);
+                split8(in ? ra[i][0] : zero, in ? ra[i][1] : zero, p0, p1, p2);
                 st[la[i]] = p0;
                 st[PSA + la[i]] = p1;
                 st[2 * PSA + la[i]] = p2;
@@ -550,8 +571,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restri
 #pragma unroll
         for (int i = 0; i < UB; i++)
             if (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB) {
+                const bool in = kk + kb[i] < k1;
                 u32x4 p0, p1, p2;
-                split8(rb[i][0], rb[i][1], p0, p1, p2);
+                split8(in ? rb[i][0] : zero, in ? rb[i][1] : zero, p0, p1, p2);
                 st[lb[i]] = p0;
                 st[PSB + lb[i]] = p1;
                 st[2 * PSB + lb[i]] = p2;
@@ -566,13 +588,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_x6_tn(const float4 *__restri
 
     if (k0 < k1) {
         load(k0);
-        store(0);
+        store(0, k0);
         if (k0 + BK < k1) load(k0 + BK);
         __syncthreads();
     }
     int buf = 0;
     for (int64_t kk = k0; kk < k1; kk += BK, buf ^= 1) {
-        if (kk + BK < k1) store(buf ^ 1);
+        if (kk + BK < k1) store(buf ^ 1, kk + BK);
         if (kk + 2 * BK < k1) load(kk + 2 * BK);
         const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 3 * PSA;
         if constexpr (FM <= FN) {

@@ -214,21 +214,22 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
         // the item's entries in chunks of 64 (one per lane), software-pipelined: while chunk c's rows are summed,
         // chunk c+1's slot lookups and chunk c+2's (idx, key) are in flight (a chunk's three dependent reads --
         // entry, slot, row -- used to run back to back).  Reads are clamped into the item, never branched around.
+        // (the lane's validity is kept apart from the loaded key and applied where the key is used: a select
+        // right behind a load makes the wave wait for it there)
         auto fetch = [&](int64_t b, int &v, int &k) {
             const int64_t e = std::min<int64_t>(b + lane, e1 - 1);
             v = idx[e];
-            const int kk = key[e];
-            k = b + lane < e1 ? kk : -1;
+            k = key[e];
         };
-        int v0, kc0, v1 = 0, kc1 = -1;
+        int v0, kc0, v1 = 0, kc1 = 0;
         fetch(e0, v0, kc0);
         int sl0 = slot ? slot[v0 / S] : 0;
         if (e0 + 64 < e1) fetch(e0 + 64, v1, kc1);
         for (int64_t base = e0; base < e1; base += 64) {
-            const int k = kc0;
+            const int k = base + lane < e1 ? kc0 : -1;
             const int row = k < 0 ? -1 : !slot ? v0 : sl0 >= 0 ? sl0 * S + (v0 - (v0 / S) * S) : -1;
             const int sl1 = slot ? slot[v1 / S] : 0;
-            int v2 = 0, kc2 = -1;
+            int v2 = 0, kc2 = 0;
             if (base + 128 < e1) fetch(base + 128, v2, kc2);
             v0 = v1;
             kc0 = kc1;

@@ -751,10 +751,12 @@ def x6_gemm_nt(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = Non
     return out
 
 
-def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int = X6_TN_SPLITS, cfg: int = X6_TN_CFG,
+def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg: int | None = None,
                name: str = "x6_gemm_tn", out: torch.Tensor | None = None) -> torch.Tensor:
     """out f32[T, M, N] = A^T @ B per tower, A f32[T, Kd, M], B f32[T, Kd, N] (the long k range split
     into `splits` slabs summed in order)."""
+    splits = X6_TN_SPLITS if splits is None else splits  # module settings read at call time
+    cfg = X6_TN_CFG if cfg is None else cfg
     T, Kd, M = (int(v) for v in A.shape)
     N = int(B.shape[2])
     if A.dtype == torch.int16:  # both operands as planes (x6_split of f32 [T, Kd, M] / [T, Kd, N]): cfg >= 30
