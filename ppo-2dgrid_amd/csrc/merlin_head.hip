@@ -138,6 +138,8 @@ __global__ __launch_bounds__(FOLD_COLS * FOLD_SLICES) void k_fold_cols(const flo
 //   tower 1: dz[1][k] = [h1 > 0] * (dvalue[k] * wc),               dwc    += dvalue[k] * h1[k]
 //   db4[t] += dz[t][k]
 // partials[t][b][(1 + A) * H4] (float4): tower 0 = (db4_0, dWa rows 0..A-1), tower 1 = (db4_1, dwc).
+// NA: the register arrays' size (A <= NA; the bench's A = 3 instance keeps 4 waves per SIMD resident)
+template <int NA>
 __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h, const float *__restrict__ dlogits,
                                                    const float *__restrict__ dvalue, const float4 *__restrict__ wa,
                                                    const float4 *__restrict__ wc, int64_t n, int H4, int A,
@@ -147,50 +149,55 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
     const int t = blockIdx.y, R = EBLK / H4;
     const int c = threadIdx.x % H4, r0 = threadIdx.x / H4;
     const int nw = t == 0 ? A : 1;
-    float4 w[MAXA], accw[MAXA];
+    float4 w[NA], accw[NA];
 #pragma unroll
-    for (int j = 0; j < MAXA; j++) {
+    for (int j = 0; j < NA; j++) {
         w[j] = j < nw ? (t == 0 ? wa[j * H4 + c] : wc[c]) : f4_zero();
         accw[j] = f4_zero();
     }
     float4 acc = f4_zero();
     const int64_t lo = (int64_t)blockIdx.x * per, hi = std::min<int64_t>(n, lo + per);
     const size_t base = (size_t)t * n * H4;
-#pragma unroll 2
-    for (int64_t r = lo + r0; r < hi; r += R) {
-        const size_t e = base + (size_t)r * H4 + c;
-        const float4 hv = h[e];
-        float4 g = f4_zero();
-        if (t == 0) {
+    // HEAD_ROWS rows per thread per round, all their loads issued before any is used (rows past the
+    // block's range read its last row and are dropped): 64 B of h in flight per thread instead of 32 --
+    // the pass is HBM-bound (h in, dz out) and 16 waves per CU kept too little in flight
+    constexpr int HEAD_ROWS = 4;
+    for (int64_t r = lo + r0; r < hi; r += HEAD_ROWS * R) {
+        float4 hv[HEAD_ROWS];
+        float d[HEAD_ROWS][NA];
 #pragma unroll
-            for (int j = 0; j < MAXA; j++) {
-                if (j < A) {
-                    const float d = dlogits[r * A + j];
-                    g.x += d * w[j].x;
-                    g.y += d * w[j].y;
-                    g.z += d * w[j].z;
-                    g.w += d * w[j].w;
-                    accw[j].x += d * hv.x;
-                    accw[j].y += d * hv.y;
-                    accw[j].z += d * hv.z;
-                    accw[j].w += d * hv.w;
+        for (int k = 0; k < HEAD_ROWS; k++) {
+            const int64_t rk = std::min<int64_t>(r + k * R, hi - 1);
+            hv[k] = h[base + (size_t)rk * H4 + c];
+#pragma unroll
+            for (int j = 0; j < NA; j++)
+                d[k][j] = j < nw ? (t == 0 ? dlogits[rk * A + j] : dvalue[rk]) : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < HEAD_ROWS; k++) {
+            if (r + k * R >= hi) break;
+            float4 g = f4_zero();
+#pragma unroll
+            for (int j = 0; j < NA; j++) {
+                if (j < nw) {
+                    g.x += d[k][j] * w[j].x;
+                    g.y += d[k][j] * w[j].y;
+                    g.z += d[k][j] * w[j].z;
+                    g.w += d[k][j] * w[j].w;
+                    accw[j].x += d[k][j] * hv[k].x;
+                    accw[j].y += d[k][j] * hv[k].y;
+                    accw[j].z += d[k][j] * hv[k].z;
+                    accw[j].w += d[k][j] * hv[k].w;
                 }
             }
-        } else {
-            const float d = dvalue[r];
-            g = make_float4(d * w[0].x, d * w[0].y, d * w[0].z, d * w[0].w);
-            accw[0].x += d * hv.x;
-            accw[0].y += d * hv.y;
-            accw[0].z += d * hv.z;
-            accw[0].w += d * hv.w;
+            const float4 o = f4_mask(hv[k], g);
+            dz[base + (size_t)(r + k * R) * H4 + c] = o;
+            f4_add(acc, o);
         }
-        const float4 o = f4_mask(hv, g);
-        dz[e] = o;
-        f4_add(acc, o);
     }
     float4 *dst = partials + ((size_t)t * gridDim.x + blockIdx.x) * (size_t)(1 + A) * H4;
 #pragma unroll
-    for (int q = 0; q < 1 + MAXA; q++) {
+    for (int q = 0; q < 1 + NA; q++) {
         if (q <= nw) {  // block-uniform
             __syncthreads();
             red[threadIdx.x] = q == 0 ? acc : accw[q > 0 ? q - 1 : 0];
@@ -288,9 +295,10 @@ hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dv
     }
     const int nblk = blocks_for(n);
     const int64_t per = (n + nblk - 1) / nblk;
-    hipLaunchKernelGGL(k_head_bwd, dim3(nblk, 2), dim3(EBLK), 0, s, reinterpret_cast<const float4 *>(h), dlogits,
-                       dvalue, reinterpret_cast<const float4 *>(wa), reinterpret_cast<const float4 *>(wc), n, H / 4,
-                       A, per, reinterpret_cast<float4 *>(dz), reinterpret_cast<float4 *>(work));
+    hipLaunchKernelGGL(A <= 3 ? k_head_bwd<3> : k_head_bwd<MAXA>, dim3(nblk, 2), dim3(EBLK), 0, s,
+                       reinterpret_cast<const float4 *>(h), dlogits, dvalue, reinterpret_cast<const float4 *>(wa),
+                       reinterpret_cast<const float4 *>(wc), n, H / 4, A, per, reinterpret_cast<float4 *>(dz),
+                       reinterpret_cast<float4 *>(work));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int total = (1 + A) * H + 2 * H;

@@ -701,8 +701,9 @@ def act_heads(z, b4, w_actor, b_actor, w_critic, b_critic, deterministic=False, 
 # Weights as int16 planes [..., R, 3 * C] (bf16 bits; per group of 8 values three 16-B chunks,
 # x = x0 + x1 + x2 exactly, include/merlin_hip.h); activations as fp32, split while staged.
 # fwd / dgrad on the 32x32x16 MFMA with split hi / lo accumulators (csrc/merlin_gemm2.hip: 806 / 790 us
-# against 857 / 843 for the 16x16x32 kernels at the update's shape, scripts/probe_x6_il.py)
-X6_NT_CFG = {"fwd": 20, "dgrad": 22, "rollout": 2}  # tile configurations of merlin_x6_gemm_nt (N = 512 / 576)
+# against 857 / 843 for the 16x16x32 kernels at the update's shape, scripts/probe_x6_il.py); the rollout's
+# 4096-row fc1 on 128 x 128 tiles of the same kernel (37.2 us against 41.3 for cfg 2, scripts/probe_rollout_fc1.py)
+X6_NT_CFG = {"fwd": 20, "dgrad": 22, "rollout": 25}  # tile configurations of merlin_x6_gemm_nt (N = 512 / 576)
 X6_TN_CFG = 0
 X6_TN_SPLITS = 32
 

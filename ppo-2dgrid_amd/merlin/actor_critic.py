@@ -393,7 +393,7 @@ class CNNActorCritic(nn.Module):
     def conv1_tables_from(self, W1):
         """conv1_tables of the stacked conv1 weights W1 [2, 32, 3, 8, 8]."""
         W = W1.view(2, 32, 3, 2, 4, 2, 4)  # t o c dy ky dx kx
-        A = self._atlas_on(W1.device).view(5, 3, 2, 4, 2, 4)  # cls c qy ky qx kx
+        A = self._atlas_on(W1.device).to(W1.dtype).view(5, 3, 2, 4, 2, 4)  # cls c qy ky qx kx
         P = torch.einsum("tocakbl,zcekfl->toabzef", W, A)
         return P.reshape(2, 32, 4, 20)
 

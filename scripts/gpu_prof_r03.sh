@@ -17,5 +17,6 @@ if [ -n "$PMC" ]; then
   done
 fi
 cd "$R" && python scripts/prof_summary.py "${TAG:-r03}" gpurun_out/summary || exit $?
+python scripts/busy_union.py gpurun_out/prof_trace/run_kernel_trace.csv > gpurun_out/summary/${TAG:-r03}_busy_union.txt
 cp gpurun_out/prof_trace.log gpurun_out/summary/ 2>/dev/null
 rm -f gpurun_out/prof_*/run_kernel_trace.csv gpurun_out/prof_*/run_counter_collection.csv

@@ -27,7 +27,8 @@ def main():
     cfgs = [int(c) for c in os.environ.get("CFGS", "").split(",") if c] or None
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
-    shapes = {"fwd": (512, 576, True, [0, 20, 21, 24, 25, 10, 30, 26, 28]), "dgrad": (576, 512, False, [1, 22, 23, 13, 32, 27])}
+    shapes = {"fwd": (512, 576, True, [0, 20, 21, 24, 25, 2, 10, 30, 26, 28]),
+              "dgrad": (576, 512, False, [1, 22, 23, 13, 32, 27])}
     if os.environ.get("PROF"):
         shapes = {"fwd": (512, 576, True, [0, 20]), "dgrad": (576, 512, False, [1, 22])}
     for name, (N, K, use_bias, cl) in shapes.items():

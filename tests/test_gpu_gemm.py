@@ -39,7 +39,7 @@ def test_split_is_exact(device):
 
 @pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 3), (512, 576, 20),
                                      (576, 512, 22), (512, 576, 21), (576, 512, 23), (512, 576, 26),
-                                     (576, 512, 27), (512, 576, 28)])
+                                     (576, 512, 27), (512, 576, 28), (512, 576, 24), (512, 576, 25)])
 @pytest.mark.parametrize("M", [1, 777, 20011])
 def test_gemm_nt_vs_float64(device, M, N, K, cfg):
     from merlin import _native as nat
