@@ -287,8 +287,10 @@ PMC_ALIAS = {"k_seg_sum_R": ("k_seg_sum<2, 1>", "k_seg_fix<1>"),
              "k_seg_sum_dQ": ("k_seg_sum<0, 3>", "k_seg_fix<3>"),
              "k_seg_sum_dT2": ("k_seg_sum<0, 4>", "k_seg_fix<4>"),
              # fc1's x6 GEMMs; the weight gradient's span covers the split-K kernel and its slab fold
-             "gemm_fc1_fwd": ("k_x6_nt32<256, 128, 4, 2, 1, 1>",),
-             "gemm_fc1_dgrad": ("k_x6_nt32<128, 192, 4, 2, 0, 1>",),
+             "gemm_fc1_fwd": ("k_x6_nt32<256, 128, 4, 2, 1, 1, 0>",),
+             "gemm_fc1_dgrad": ("k_x6_nt32<128, 192, 4, 2, 0, 1, 0>",),
+             "gemm_rollout_fc1": ("k_x6_nt32<128, 128, 2, 2, 0, 1, 0>",),
+             "k_head_bwd": ("k_head_bwd<3>", "k_head_fold"),
              "gemm_wgrad": ("k_x6_tn<128, 192, 2, 4>", "k_x6_fold")}
 PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 

@@ -96,6 +96,9 @@ class PPO:
         # after one eager rollout, replay the vectorised rollout as one captured HIP graph
         self.rollout_graph = rollout_graph
         self._graph = None
+        # look-ahead map refill on the side stream after every 4th env step (_rollout_body; scripts/probe_rollout.py,
+        # one process: 33.5 / 32.5 / 32.0 ms per rollout refilling every 1 / 2 / 4 steps)
+        self.refill_every = 4
         # PPO._sgd on the window + x6 path: the minibatch step with its launches written out (merlin/fast_step.py;
         # False = the same kernels through the autograd engine)
         self.fast_step = True
@@ -187,27 +190,34 @@ class PPO:
     def _rollout_body(self):
         """ppo.py:64-105 for N envs: reset (ppo.py:65: every rollout starts from a fresh
         reset), T x (act -> env step writing into the [T][N] storage), bootstrap value.
-        After each step the used look-ahead map slots are refilled on a side stream, beside the
-        next act (which reads only the obs codes), and joined before the next step."""
+        After every `refill_every`-th step the used look-ahead map slots are refilled on a side stream,
+        beside the next act (which reads only the obs codes), and joined before the next step.  (A
+        refill's ~60 us of map generation is as long as the act beside it, so refilling after every step
+        put it on the step's critical path; an env whose slot is still empty when it resets again takes
+        the in-step fallback, which changes no result.)"""
         buf, env = self.buf, self.vec
         T = buf.T
         main, side = torch.cuda.current_stream(self.device), self._refill_stream
+        every = max(1, int(self.refill_every))
         env.reset(out=buf.codes[0])
         with torch.no_grad():
             self._act_epoch.add_(1)
             pack = self.ac.rollout_pack(frames=(T + 1) * buf.N) if self.conv1_from_codes else None
+            pending = False
             for t in range(T):
                 self._act(buf.codes[t], pack, t, out=(buf.actions[t], buf.logprobs[t], buf.values[t]))
-                if side is not None and t > 0:
+                if pending:
                     main.wait_stream(side)
+                    pending = False
                 env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
                               buf.ep_return[t], buf.ep_length[t])
-                if side is not None:
+                if side is not None and (t % every == every - 1 or t == T - 1):
                     side.wait_stream(main)
                     with torch.cuda.stream(side):
                         env.refill()
+                    pending = True
             _, _, last_value = self._act(buf.codes[T], pack, T)
-            if side is not None:
+            if pending:
                 main.wait_stream(side)
             buf.last_value.copy_(last_value)
 

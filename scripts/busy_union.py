@@ -31,3 +31,35 @@ for a, b in runs[-6:]:
     out.append(((t1 - t0) / 1e6, busy / 1e6, len(seg)))
 for w, bz, n in out:
     print(f"update: span {w:8.1f} ms, GPU busy (union) {bz:8.1f} ms, idle {w - bz:7.1f} ms ({(w - bz) / w * 100:.1f} %), {n} dispatches")
+
+
+# rollout phases: from the first k_env_step of a run to the last one, plus the per-kernel means and the mean step
+# period (k_env_step start to start), so the dispatch gaps of the captured rollout graph show
+def union(seg):
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _ in seg:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    return busy + (cur_e - cur_s if cur_e is not None else 0)
+
+
+bounds = [marks[0]] + [b for a, b in zip(marks, marks[1:]) if b - a > 200]
+ends = [a for a, b in zip(marks, marks[1:]) if b - a > 200] + [marks[-1]]
+for a, b in list(zip(bounds, ends))[-3:]:
+    seg = rows[a:b + 1]
+    t0, t1 = seg[0][0], max(e for _, e, _ in seg)
+    bz = union(seg)
+    steps = [s for s, _, k in seg if "k_env_step" in k]
+    per = (steps[-1] - steps[0]) / max(1, len(steps) - 1) / 1e3
+    print(f"rollout: span {(t1 - t0) / 1e6:8.2f} ms, GPU busy (union) {bz / 1e6:8.2f} ms, {len(steps)} env steps, "
+          f"step period {per:.1f} us, {len(seg)} dispatches")
+    agg = {}
+    for s, e, k in seg:
+        n, tot = agg.get(k[:60], (0, 0))
+        agg[k[:60]] = (n + 1, tot + e - s)
+    for k, (n, tot) in sorted(agg.items(), key=lambda x: -x[1][1])[:8]:
+        print(f"    {k:60s} {n:5d} x {tot / n / 1e3:7.1f} us")

@@ -1,0 +1,46 @@
+"""In-process A/B of rollout settings at the bench workload (4096 envs x 256 steps, captured rollout graph):
+one agent, each setting's graph captured once, then rollouts timed alternately.
+    python scripts/probe_rollout.py [rounds] [refill_every values, e.g. 1,2,4]"""
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-2dgrid_amd"))
+import torch
+
+from merlin import MerlinVecEnv
+from merlin.ppo import PPO
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    vals = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1,2").split(",")]
+    dev = torch.device("cuda", 0)
+    env = MerlinVecEnv(4096, "mediumhard", seed=777, device=dev)
+    torch.manual_seed(777)
+    agent = PPO(env, batch_size=4096 * 256, minibatch_size=4096 * 256 // 8, ent_coef=0.05, device=dev)
+    for _ in range(2):
+        agent.update(agent.collect_rollouts())
+    graphs = {}
+    for v in vals:
+        agent.refill_every = v
+        agent._graph = None
+        agent.collect_rollouts()  # eager + capture
+        graphs[v] = agent._graph
+    times = {v: [] for v in vals}
+    for _ in range(rounds):
+        for v in vals:
+            agent._graph = graphs[v]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            agent.collect_rollouts()
+            torch.cuda.synchronize()
+            times[v].append((time.perf_counter() - t0) * 1e3)
+    for v in vals:
+        print(f"refill_every {v}: median {statistics.median(times[v]):.2f} ms per rollout  all "
+              f"{[round(x, 2) for x in times[v]]}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
