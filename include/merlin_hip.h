@@ -323,6 +323,17 @@ int merlin_segment_sum_masked(const float *src_dev, const void *mask_dev, int64_
                               const int32_t *slot_dev, int32_t sub, int64_t item_len,
                               const int32_t *fix_dev, int64_t n_fix, int32_t towers, float *out_dev,
                               int64_t out_rows, float *carry_dev, int32_t flags, void *stream);
+/* merlin_segment_sum_masked that also marks the destinations it sums into: mark_dev int32[out_rows]
+ * (or NULL), mark[key(e)] = key(e) for every entry e not skipped; rows of other keys keep what the
+ * caller put there (-1).  The marks are a slot map (sub 1) for a following pass that reads these
+ * rows, so it skips the rows no entry was summed into (with MERLIN_SEG_NO_FILL they are never
+ * written: merlin/fast_step.py's band sums of conv3's backward). */
+int merlin_segment_sum_marked(const float *src_dev, const void *mask_dev, int64_t src_rows,
+                              const int32_t *idx_dev, const int32_t *key_dev, int64_t nnz,
+                              const int32_t *slot_dev, int32_t sub, int64_t item_len,
+                              const int32_t *fix_dev, int64_t n_fix, int32_t towers, float *out_dev,
+                              int64_t out_rows, float *carry_dev, int32_t flags, int32_t *mark_dev,
+                              void *stream);
 
 /* Acting tail (src/actor_critic.py:48-55 act, src/ppo.py:69-71): z float[2][n][hidden] = fc1's
  * pre-activation of the actor / critic tower, b4 float[2][hidden]; h = relu(z + b4); logits =

@@ -162,6 +162,8 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
 // threshold_backward(src, mask) rows, never materialised.  MASK 2: the same mask as one 64-bit
 // word per row (bit ch = mask channel ch > 0, as k_window_conv3 writes it): 8 B per row instead
 // of 256.
+// mark (optional): mark[key] = key for every entry not skipped -- the destinations this launch sums into, as a
+// slot map for a following pass over them (the caller presets -1).
 // ROLE only names the instantiation (rocprofv3 tells the passes of conv3's backward apart by it):
 // 0 generic, 1 R (patch sums), 2 S (band sums), 3 dQ (window sums), 4 dT2 (table rows)
 constexpr int SEG_WAVES = 4, SEG_UNROLL = 8;
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
                                                            const int32_t *__restrict__ slot, int S, int64_t L,
                                                            int64_t nitems, int T, float4 *__restrict__ out,
                                                            int64_t out_rows, float4 *__restrict__ carry,
-                                                           int acc_out) {
+                                                           int acc_out, int32_t *__restrict__ mark) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int t = lane >> 5, q = (lane >> 4) & 1, c = lane & 15;
     const bool live = t < T;
@@ -228,6 +230,7 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
         for (int64_t base = e0; base < e1; base += 64) {
             const int k = base + lane < e1 ? kc0 : -1;
             const int row = k < 0 ? -1 : !slot ? v0 : sl0 >= 0 ? sl0 * S + (v0 - (v0 / S) * S) : -1;
+            if (mark && row >= 0) mark[k] = k;  // destinations that receive a sum (same-value stores)
             const int sl1 = slot ? slot[v1 / S] : 0;
             int v2 = 0, kc2 = 0;
             if (base + 128 < e1) fetch(base + 128, v2, kc2);
@@ -427,22 +430,23 @@ namespace {
 template <int ROLE>
 hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                       const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
-                      int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, hipStream_t s) {
+                      int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int32_t *mark,
+                      hipStream_t s) {
     const int64_t nitems = (nnz + L - 1) / L;
     const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
     if (mask && mask_bits)
         hipLaunchKernelGGL((k_seg_sum<2, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
                            reinterpret_cast<const float4 *>(src), mask, src_rows, idx, key, nnz, slot, S, L, nitems,
-                           T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out);
+                           T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out, mark);
     else if (mask)
         hipLaunchKernelGGL((k_seg_sum<1, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
                            reinterpret_cast<const float4 *>(src), mask, src_rows, idx, key, nnz, slot, S, L, nitems,
-                           T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out);
+                           T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out, mark);
     else
         hipLaunchKernelGGL((k_seg_sum<0, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
                            reinterpret_cast<const float4 *>(src), nullptr, src_rows, idx, key, nnz, slot, S, L,
                            nitems, T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry),
-                           acc_out);
+                           acc_out, mark);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || nfix <= 0) return e;
     const int gfix = (int)std::min<int64_t>((nfix + FIX_ROWS - 1) / FIX_ROWS, 256 * 8);
@@ -456,21 +460,21 @@ hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,
-                          int role, hipStream_t s) {
+                          int role, int32_t *mark, hipStream_t s) {
     hipError_t e = (acc_out || !fill) ? hipSuccess
                                       : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
     if (e != hipSuccess || nnz <= 0) return e;
     switch (role) {
         case 1: return seg_launch<1>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                     out_rows, carry, acc_out, s);
+                                     out_rows, carry, acc_out, mark, s);
         case 2: return seg_launch<2>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                     out_rows, carry, acc_out, s);
+                                     out_rows, carry, acc_out, mark, s);
         case 3: return seg_launch<3>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                     out_rows, carry, acc_out, s);
+                                     out_rows, carry, acc_out, mark, s);
         case 4: return seg_launch<4>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                     out_rows, carry, acc_out, s);
+                                     out_rows, carry, acc_out, mark, s);
         default: return seg_launch<0>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                      out_rows, carry, acc_out, s);
+                                      out_rows, carry, acc_out, mark, s);
     }
 }
 

@@ -100,6 +100,8 @@ def lib():
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
     L.merlin_segment_sum_masked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                             vp]
+    L.merlin_segment_sum_marked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
+                                            vp, vp]
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_colsum.argtypes = [vp, i64, i32, i64, i64, i32, vp, vp]
@@ -158,7 +160,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
     "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
-    "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
+    "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_tower_colsum",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
@@ -525,14 +527,16 @@ SEG_ROLES = {"k_seg_sum_R": 1, "k_seg_sum_S": 2, "k_seg_sum_dQ": 3, "k_seg_sum_d
 
 
 def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum", out=None,
-                accumulate: bool = False, carry=None, mask=None, fill: bool = True):
+                accumulate: bool = False, carry=None, mask=None, fill: bool = True, mark=None):
     """out f32[T, out_rows, 64]: out[t][key] = the sum, in entry order, of src[t][row(e)] over
     the plan's entries e with that key (merlin.windows.SegmentPlan); row(e) = idx[e], or
     slot[idx[e] // sub] * sub + idx[e] % sub with entries whose slot is -1 skipped.  With
     accumulate the sums are added to `out` (a list split over source blocks, in call order).
     mask (same shape as src): sum ReLU-backward rows, src where mask > 0 else 0; or the same mask as
     int64 [T, src_rows] bit words (window_conv3(bits=True)).  fill=False leaves the rows of keys
-    without a live entry unwritten (merlin_segment_sum_masked)."""
+    without a live entry unwritten (merlin_segment_sum_masked).  mark (int32 [out_rows], preset to -1):
+    mark[key] = key for every key that received a live entry (merlin_segment_sum_marked), the slot map of
+    a following pass over these rows."""
     T, src_rows = int(src.shape[0]), int(src.shape[1])
     assert src.shape[2] == 64 and src.dtype == torch.float32 and src.is_contiguous()
     mask_bits = mask is not None and mask.dtype == torch.int64
@@ -554,11 +558,13 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
     nb = plan.nnz * (8 + (4 if slot is not None else 0)) + T * (src_rows * (256 + mrow) + out_rows * 256)
     flags = (SEG_ACCUMULATE if accumulate else 0) | (0 if fill else SEG_NO_FILL) | (SEG_MASK_BITS if mask_bits else 0)
     flags |= SEG_ROLES.get(name, 0) << SEG_ROLE_SHIFT
+    if mark is not None:
+        assert mark.dtype == torch.int32 and mark.shape == (out_rows,) and mark.is_contiguous()
     with KernelTimer.span(name, nb):
-        check(lib().merlin_segment_sum_masked(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz,
+        check(lib().merlin_segment_sum_marked(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz,
                                               ptr(slot), int(sub), plan.item_len, ptr(plan.fix),
                                               int(plan.fix.shape[0]), T, ptr(out), int(out_rows), ptr(carry), flags,
-                                              stream_of(src)), "merlin_segment_sum_masked")
+                                              ptr(mark), stream_of(src)), "merlin_segment_sum_marked")
     return out
 
 

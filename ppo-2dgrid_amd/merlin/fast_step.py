@@ -275,5 +275,12 @@ def _conv3_backward_bulk(plan, mb, bits, dY3, nw):
     the update-wide array (mb.kmap, WindowPlan.update_minibatches(bulk=True))."""
     R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
                         name="k_seg_sum_R", mask=bits, fill=False)
-    S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=mb.kmap, sub=1, name="k_seg_sum_S")
-    return nat.segment_sum(S, plan.dq_plan, nw * 9, name="k_seg_sum_dQ")
+    # band sums over the live patches, marking the bands that got one (merlin_segment_sum_marked); dQ reads only
+    # those: the dead bands' rows are never zeroed (a 128-MB fill per step) nor read
+    bslot = getattr(plan, "_bslot", None)
+    if bslot is None:
+        bslot = plan._bslot = torch.empty(plan.num_bands, dtype=torch.int32, device=dY3.device)
+    bslot.fill_(-1)
+    S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=mb.kmap, sub=1, name="k_seg_sum_S", fill=False,
+                        mark=bslot)
+    return nat.segment_sum(S, plan.dq_plan, nw * 9, slot=bslot, sub=1, name="k_seg_sum_dQ")

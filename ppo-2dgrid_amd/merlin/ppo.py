@@ -96,9 +96,11 @@ class PPO:
         # after one eager rollout, replay the vectorised rollout as one captured HIP graph
         self.rollout_graph = rollout_graph
         self._graph = None
-        # look-ahead map refill on the side stream after every 4th env step (_rollout_body; scripts/probe_rollout.py,
-        # one process: 33.5 / 32.5 / 32.0 ms per rollout refilling every 1 / 2 / 4 steps)
-        self.refill_every = 4
+        # look-ahead map refill on the side stream after every `refill_every`-th env step (_rollout_body).  Every
+        # step: at the bench state (iterations 6-25) refilling every 4th step left so many slots empty at a second
+        # reset that the in-step fallback grew from 4.6 to 23 us per step (rollout 35.3 vs ~31 ms,
+        # profiles/r03i_busy_union.txt), though at random init it measured 32.0 vs 33.5 ms (scripts/probe_rollout.py)
+        self.refill_every = 1
         # PPO._sgd on the window + x6 path: the minibatch step with its launches written out (merlin/fast_step.py;
         # False = the same kernels through the autograd engine)
         self.fast_step = True

@@ -485,9 +485,12 @@ def _conv3_backward(plan, mb, bits, dY3, nw):
     live = plan.kid.index_select(0, mb.groups).reshape(-1)
     kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32, device=bits.device)
     kmap[live] = live
-    # pass 2: band sums over the live patches; pass 3: dQ[w][tap] from the bands
-    S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=kmap, sub=1, name="k_seg_sum_S")
-    dQ = nat.segment_sum(S, plan.dq_plan, nw * 9, name="k_seg_sum_dQ")
+    # pass 2: band sums over the live patches, marking the bands that got one; pass 3: dQ[w][tap] from the
+    # marked bands (the others hold no sum and are neither zeroed nor read)
+    bslot = torch.full((plan.num_bands,), -1, dtype=torch.int32, device=bits.device)
+    S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=kmap, sub=1, name="k_seg_sum_S", fill=False,
+                        mark=bslot)
+    dQ = nat.segment_sum(S, plan.dq_plan, nw * 9, slot=bslot, sub=1, name="k_seg_sum_dQ")
     dQ = dQ.view(T, nw, 9, 64)
     db3 = _colsum(dQ[:, :, 0])
     return dQ.view(T, nw, 576), db3

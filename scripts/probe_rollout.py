@@ -20,7 +20,7 @@ def main():
     env = MerlinVecEnv(4096, "mediumhard", seed=777, device=dev)
     torch.manual_seed(777)
     agent = PPO(env, batch_size=4096 * 256, minibatch_size=4096 * 256 // 8, ent_coef=0.05, device=dev)
-    for _ in range(2):
+    for _ in range(int(os.environ.get("WARM", "6"))):  # the bench's state: episode lengths change with training
         agent.update(agent.collect_rollouts())
     graphs = {}
     for v in vals:

@@ -105,6 +105,20 @@ def test_segment_sum_matches_index_add(device, n, nkeys, L, use_slot):
     err = (out.double() - ref).abs()
     assert (err <= 1e-5 * mag + 1e-6).all(), (err / (mag + 1e-6)).max().item()
     assert torch.equal(out, nat.segment_sum(src, plan, nkeys, slot=slot, sub=S))  # fixed order
+    # marks: exactly the keys with a live entry; without fill their rows are the same sums, the others untouched
+    mark = torch.full((nkeys,), -1, dtype=torch.int32, device=device)
+    got = torch.full_like(out, 7.0)
+    nat.segment_sum(src, plan, nkeys, slot=slot, sub=S, out=got, fill=False, mark=mark)
+    has = torch.zeros(nkeys, dtype=torch.bool, device=device)
+    has[kk] = True
+    ar = torch.arange(nkeys, dtype=torch.int32, device=device)
+    assert torch.equal(mark, torch.where(has, ar, torch.full_like(ar, -1)))
+    assert torch.equal(got[:, has], out[:, has])
+    # keys crossing items get their (zero) fix-up row written even when dead; every other dead key is untouched
+    crossing = torch.zeros(nkeys, dtype=torch.bool, device=device)
+    fx = plan.fix[plan.fix[:, 0] >= 0, 0].long()
+    crossing[fx] = True
+    assert (got[:, ~has & ~crossing] == 7.0).all()
     # accumulate: a second list added onto the first's sums, exactly the fp32 sum of the two
     keys2 = torch.randint(0, nkeys, (n,), device=device, generator=g)
     o2 = torch.sort(keys2, stable=True).indices
