@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--minibatches", type=int, default=8)
     ap.add_argument("--difficulty", default="mediumhard")
     ap.add_argument("--size", type=int, default=16)
+    ap.add_argument("--timer-every", type=int, default=4,
+                    help="HIP-event timing of every k-th launch of each kernel in the timed region (kernels table, "
+                         "rooflines); the event records cost the loop ~2-3 %% when every launch is timed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tiers", action="store_true")
     ap.add_argument("--env-tier-only", action="store_true",
@@ -325,9 +328,10 @@ def gather_note(name, k):
                              "guide_l2_gather_tbs": [16.8, 18.8], "frac_of_18_8": round(tbs / 18.8, 3)}}
 
 
-def kernel_table(records):
+def kernel_table(records, every: int = 1):
     """{name: launches, total ms, avg us, algorithmic bytes (GB/s) or flops (TFLOP/s) per launch}
-    from HIP events."""
+    from HIP events; with every > 1 only each every-th launch was timed (`launches_timed`), and launches /
+    total_ms are scaled up to the whole region."""
     agg = {}
     for name, e0, e1, nbytes, flops in records:
         ms = e0.elapsed_time(e1)
@@ -338,7 +342,9 @@ def kernel_table(records):
         a[3] += flops
     out = {}
     for name, (cnt, ms, nb, fl) in agg.items():
-        d = {"launches": cnt, "total_ms": round(ms, 3), "avg_us": round(ms / cnt * 1e3, 2)}
+        d = {"launches": cnt * every, "total_ms": round(ms * every, 3), "avg_us": round(ms / cnt * 1e3, 2)}
+        if every > 1:
+            d["launches_timed"] = cnt
         if fl:
             d.update(flops_per_launch=fl // cnt, tflops=round(fl / (ms / 1e3) / 1e12, 2))
         else:
@@ -498,7 +504,7 @@ def main():
         dist.barrier()
 
     state["phase"] = "timed"
-    nat.KernelTimer.start()
+    nat.KernelTimer.start(every=args.timer_every)
     ph = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -518,7 +524,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kernels = kernel_table(nat.KernelTimer.stop())
+    kernels = kernel_table(nat.KernelTimer.stop(), args.timer_every)
     rollout_ms, update_ms = rollout_ms_of(ph), update_ms_of(ph)
     value = args.steps * B * world / elapsed
     rank_spread = None

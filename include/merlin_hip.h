@@ -402,6 +402,13 @@ int merlin_tower_head_bwd(const float *h_dev, const float *dlogits_dev, const fl
                           const float *w_actor_dev, const float *w_critic_dev, int64_t n, int32_t hidden,
                           int32_t act_dim, float *dz_dev, float *dbias_dev, float *dw_actor_dev,
                           float *dw_critic_dev, void *stream);
+/* heads_fwd: the two heads (actor_critic.py:41-46, Linear(512, act_dim) / Linear(512, 1)) on h
+ * float[2][n][hidden] = relu(fc1) of the actor / critic tower: logits float[n][act_dim] = h0 w_actor^T
+ * (+ b_actor), value float[n] = h1 . w_critic (+ b_critic); biases may be NULL (not added).  hidden 512,
+ * act_dim <= 8; one fixed summation order (every call the same bits). */
+int merlin_tower_heads_fwd(const float *h_dev, int64_t n, int32_t hidden, const float *w_actor_dev,
+                           int32_t act_dim, const float *w_critic_dev, const float *b_actor_dev,
+                           const float *b_critic_dev, float *logits_dev, float *value_dev, void *stream);
 
 /* fc1 (src/actor_critic.py:31-41, Linear(576, 512) of both towers) on the bf16 matrix cores in fp32
  * (csrc/merlin_gemm.hip): every fp32 operand value x is used as three bf16 planes x0 + x1 + x2 == x

@@ -783,6 +783,18 @@ int merlin_tower_head_bwd(const float *h, const float *dlogits, const float *dva
     return MERLIN_OK;
 }
 
+int merlin_tower_heads_fwd(const float *h, int64_t n, int32_t hidden, const float *w_actor, int32_t act_dim,
+                           const float *w_critic, const float *b_actor, const float *b_critic, float *logits,
+                           float *value, void *stream) {
+    if ((!h || !w_actor || !w_critic || !logits || !value) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (n < 0) return fail(MERLIN_E_INVALID, "n must be >= 0");
+    if (act_dim < 1 || act_dim > merlin::epilogue_max_act()) return fail(MERLIN_E_UNSUPPORTED, "act_dim must be 1..8");
+    if (hidden != 512) return fail(MERLIN_E_UNSUPPORTED, "hidden must be 512");
+    HIP_TRY(merlin::launch_heads_fwd(h, n, hidden, w_actor, act_dim, w_critic, b_actor, b_critic, logits, value,
+                                     (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
 int merlin_x6_split(const float *x, int64_t n, void *planes, void *stream) {
     if ((!x || !planes) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (n < 0 || n % 8) return fail(MERLIN_E_INVALID, "n must be a non-negative multiple of 8");

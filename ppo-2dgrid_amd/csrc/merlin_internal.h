@@ -128,6 +128,8 @@ hipError_t launch_stage_fwd(const float *W1, const float *b1, const float *W2, c
 hipError_t launch_stage_bwd(const float *W2, const float *HT, const float *dT2, const float *atlas,
                             const int16_t *koff, const int16_t *kv, int T, float *dH, float *dW1, float *db1,
                             float *dW2, hipStream_t s);
+hipError_t launch_heads_fwd(const float *h, int64_t n, int H, const float *wa, int A, const float *wc, const float *ba,
+                            const float *bc, float *logits, float *value, hipStream_t s);
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill, int role,

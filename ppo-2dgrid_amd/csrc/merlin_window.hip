@@ -301,96 +301,51 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
 }
 
 // fix rows (dst, j0, j1, slot0): out[t][dst] = carry[t][j0][slot0] + sum_{j0 < j <= j1} carry[t][j][0];
-// rows with dst < 0 hold nothing (merlin/windows.py SegmentPlan: one row per item).
-// A hot destination spans hundreds of items, and as one wave's chain of dependent 16-load rounds its row was
-// the tail of the whole launch (45-65 us against ~10 us of carry reads, profiles/r03e_kernel_stats.md).  A
-// block takes FIX_ROWS consecutive rows: each wave finishes its rows of up to FIX_SHORT items alone and defers
-// the longer ones to a list in LDS; then the block's FIX_WAVES waves take the deferred rows one by one, wave w
-// the 16-item groups w, w + FIX_WAVES, ... (four partials each), the waves' sums joined in LDS in wave order.
-// Every order is fixed by the row's length, so the result stays bitwise reproducible.
-constexpr int FIX_WAVES = 4, FIX_SHORT = 64, FIX_ROWS = 4 * FIX_WAVES;
-
-// sum of carry rows j0 < j <= j1 in the groups of 16 that start at j (stride `step`), item j0+1+i into partial
-// i % 4, partials joined as (0 + 1) + (2 + 3)
-__device__ __forceinline__ float2 fix_span(const float2 *ct, int j, int j1, int step) {
-    float2 a[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-    for (; j + 15 <= j1; j += step) {
-        float2 v[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) v[u] = ct[(size_t)(j + u) * 64];
-#pragma unroll
-        for (int u = 0; u < 16; u++) {
-            a[u & 3].x += v[u].x;
-            a[u & 3].y += v[u].y;
-        }
-    }
-    for (; j <= j1; j += 4) {  // the remainder (< 16 items), static partial indices (no scratch)
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            if (j + u <= j1) {
-                const float2 v = ct[(size_t)(j + u) * 64];
-                a[u].x += v.x;
-                a[u].y += v.y;
-            }
-        }
-    }
-    return make_float2((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y));
-}
-
-__device__ __forceinline__ void fix_write(const float2 *ct, const int4 x, float2 s, int t, int T, int c2,
-                                          float2 *__restrict__ out, int64_t out_rows, int acc_out) {
-    if (t >= T) return;
-    float2 acc = ct[(size_t)x.y * 64 + x.w * 32];
-    acc.x += s.x;
-    acc.y += s.y;
-    float2 *o = out + ((size_t)t * out_rows + x.x) * 32 + c2;
-    if (acc_out) {
-        const float2 p = *o;
-        *o = make_float2(p.x + acc.x, p.y + acc.y);
-    } else {
-        *o = acc;
-    }
-}
-
+// rows with dst < 0 hold nothing (merlin/windows.py SegmentPlan: one row per item)
 template <int ROLE>
-__global__ __launch_bounds__(64 * FIX_WAVES) void k_seg_fix(const float2 *__restrict__ carry, int64_t nitems,
-                                                            const int4 *__restrict__ fix, int64_t nfix, int T,
-                                                            float2 *__restrict__ out, int64_t out_rows,
-                                                            int acc_out) {
-    __shared__ float2 part[FIX_WAVES][64];
-    __shared__ int longs[FIX_ROWS];
-    __shared__ int nlong;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, t = lane >> 5, c2 = lane & 31;
-    const float2 *ct = carry + (size_t)(t < T ? t : 0) * nitems * 64 + c2;
-    for (int64_t base = (int64_t)blockIdx.x * FIX_ROWS; base < nfix; base += (int64_t)gridDim.x * FIX_ROWS) {
-        if (threadIdx.x == 0) nlong = 0;
-        __syncthreads();
-        for (int r = w; r < FIX_ROWS; r += FIX_WAVES) {  // wave-uniform rows
-            if (base + r >= nfix) break;
-            const int4 x = fix[base + r];
-            if (x.x < 0) continue;
-            if (x.z - x.y > FIX_SHORT) {
-                if (lane == 0) longs[atomicAdd(&nlong, 1)] = r;  // list order is free: rows are independent
-                continue;
-            }
-            fix_write(ct, x, fix_span(ct, x.y + 1, x.z, 16), t, T, c2, out, out_rows, acc_out);
-        }
-        __syncthreads();
-        const int nl = nlong;
-        for (int q = 0; q < nl; q++) {
-            const int4 x = fix[base + longs[q]];
-            part[w][lane] = fix_span(ct, x.y + 1 + 16 * w, x.z, 16 * FIX_WAVES);
-            __syncthreads();
-            if (w == 0) {
-                float2 s = part[0][lane];
+__global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carry, int64_t nitems,
+                                                 const int4 *__restrict__ fix, int64_t nfix, int T,
+                                                 float2 *__restrict__ out, int64_t out_rows, int acc_out) {
+    const int lane = threadIdx.x & 63, t = lane >> 5, c2 = lane & 31;
+    for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nfix; f += (int64_t)gridDim.x * 4) {
+        if (t >= T) continue;
+        const int4 x = fix[f];
+        if (x.x < 0) continue;
+        const float2 *ct = carry + (size_t)t * nitems * 64 + c2;
+        float2 acc = ct[(size_t)x.y * 64 + x.w * 32];
+        // a hot destination spans hundreds of items: four independent partial sums (items
+        // j0+1+4i+q go to partial q) keep 16 loads in flight instead of one dependent chain;
+        // the partials join in a fixed order, so the result stays bitwise reproducible
+        float2 a[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+        int j = x.y + 1;
+        for (; j + 15 <= x.z; j += 16) {
+            float2 v[16];
 #pragma unroll
-                for (int k = 1; k < FIX_WAVES; k++) {
-                    s.x += part[k][lane].x;
-                    s.y += part[k][lane].y;
-                }
-                fix_write(ct, x, s, t, T, c2, out, out_rows, acc_out);
+            for (int u = 0; u < 16; u++) v[u] = ct[(size_t)(j + u) * 64];
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                a[u & 3].x += v[u].x;
+                a[u & 3].y += v[u].y;
             }
-            __syncthreads();  // part[] (and, after the last row, nlong / longs[]) are rewritten next
+        }
+        for (; j <= x.z; j += 4) {  // static partial indices (a dynamic a[q] would live in scratch)
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (j + u <= x.z) {
+                    const float2 v = ct[(size_t)(j + u) * 64];
+                    a[u].x += v.x;
+                    a[u].y += v.y;
+                }
+            }
+        }
+        acc.x += (a[0].x + a[1].x) + (a[2].x + a[3].x);
+        acc.y += (a[0].y + a[1].y) + (a[2].y + a[3].y);
+        float2 *o = out + ((size_t)t * out_rows + x.x) * 32 + c2;
+        if (acc_out) {
+            const float2 p = *o;
+            *o = make_float2(p.x + acc.x, p.y + acc.y);
+        } else {
+            *o = acc;
         }
     }
 }
@@ -449,8 +404,8 @@ hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t
                            acc_out, mark);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || nfix <= 0) return e;
-    const int gfix = (int)std::min<int64_t>((nfix + FIX_ROWS - 1) / FIX_ROWS, 256 * 8);
-    hipLaunchKernelGGL(k_seg_fix<ROLE>, dim3(gfix), dim3(64 * FIX_WAVES), 0, s, reinterpret_cast<const float2 *>(carry), nitems,
+    const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);
+    hipLaunchKernelGGL(k_seg_fix<ROLE>, dim3(gfix), dim3(256), 0, s, reinterpret_cast<const float2 *>(carry), nitems,
                        reinterpret_cast<const int4 *>(fix), nfix, T, reinterpret_cast<float2 *>(out), out_rows,
                        acc_out);
     return hipGetLastError();

@@ -100,6 +100,7 @@ def lib():
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
     L.merlin_segment_sum_masked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                             vp]
+    L.merlin_tower_heads_fwd.argtypes = [vp, i64, i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.merlin_segment_sum_marked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                             vp, vp]
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
@@ -160,7 +161,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
     "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
-    "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
+    "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_tower_colsum",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
@@ -174,10 +175,14 @@ class KernelTimer:
     hipBLASLt GEMMs of the towers are timed the same way (flops only)."""
 
     records: list | None = None
+    every = 1
+    counts: dict = {}
 
     @classmethod
-    def start(cls):
-        cls.records = []
+    def start(cls, every: int = 1):
+        """every: time only each every-th launch of each kernel name (the event records are not free: two
+        marker packets per timed launch)."""
+        cls.records, cls.every, cls.counts = [], max(1, int(every)), {}
 
     @classmethod
     def stop(cls):
@@ -188,6 +193,10 @@ class KernelTimer:
     def span(cls, name: str, nbytes: int, flops: int = 0):
         # no events inside a HIP-graph capture (the captured rollout, merlin/ppo.py)
         if cls.records is None or torch.cuda.is_current_stream_capturing():
+            return _NULL_SPAN
+        c = cls.counts.get(name, 0)
+        cls.counts[name] = c + 1
+        if c % cls.every:
             return _NULL_SPAN
         return _Span(name, nbytes, flops)
 
@@ -603,6 +612,24 @@ def colsum(x, out=None):
         check(lib().merlin_tower_colsum(C.c_void_p(x.data_ptr()), rows, cols, int(x.stride(1)), int(x.stride(0)), T,
                                         ptr(out), stream_of(x)), "merlin_tower_colsum")
     return out
+
+
+def heads_fwd(h: torch.Tensor, w_actor: torch.Tensor, w_critic: torch.Tensor, b_actor=None, b_critic=None,
+              name: str = "k_heads_fwd"):
+    """(logits f32[n, act_dim], value f32[n]) = h[0] w_actor^T (+ b_actor), h[1] w_critic^T (+ b_critic) for h
+    f32[2, n, 512] (merlin_tower_heads_fwd: both heads in one pass over h)."""
+    assert h.dim() == 3 and h.shape[0] == 2 and h.shape[2] == 512 and h.dtype == torch.float32 and h.is_contiguous()
+    n, A = int(h.shape[1]), int(w_actor.shape[0])
+    wa, wc = w_actor.detach().contiguous(), w_critic.detach().reshape(-1).contiguous()
+    assert wa.shape == (A, 512) and wc.numel() == 512
+    ba = None if b_actor is None else b_actor.detach().contiguous()
+    bc = None if b_critic is None else b_critic.detach().reshape(-1).contiguous()
+    logits = torch.empty((n, A), dtype=torch.float32, device=h.device)
+    value = torch.empty(n, dtype=torch.float32, device=h.device)
+    with KernelTimer.span(name, h.numel() * 4 + n * (A + 1) * 4):
+        check(lib().merlin_tower_heads_fwd(ptr(h), n, 512, ptr(wa), A, ptr(wc), ptr(ba), ptr(bc), ptr(logits),
+                                           ptr(value), stream_of(h)), "merlin_tower_heads_fwd")
+    return logits, value
 
 
 def head_bwd(h, dlogits, dvalue, w_actor, w_critic, out_bias=None, out_w_actor=None, out_w_critic=None):

@@ -235,8 +235,7 @@ class WindowStep:
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
         h = nat.x6_gemm_nt(a3, P4, bias=b4, cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
-        logits = torch.mm(h[0], Wa.t())
-        value = torch.mm(h[1], Wc.t()).squeeze(-1)
+        logits, value = nat.heads_fwd(h, Wa, Wc)  # both heads in one pass over h (the loss adds their biases)
         # ---- loss and its gradient per frame (merlin.ppo._PPOLoss); the head-bias gradients land in .grad
         _, dlogits, dvalue, _, _ = nat.ppo_loss(
             logits, value, mb.offs, mb.order, mb.inv, mb_idx, actions, logp_old, adv, ret, ag.clip_eps, ag.vf_coef,

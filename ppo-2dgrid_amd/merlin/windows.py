@@ -551,8 +551,7 @@ class _WindowTowerHeadX6(torch.autograd.Function):
         a3 = Y3.view(2, n, 576)
         h = nat.x6_gemm_nt(a3, nat.x6_split(W4p.detach()), bias=b4.detach(), cfg=nat.X6_NT_CFG["fwd"],
                            name="gemm_fc1_fwd")
-        logits = torch.mm(h[0], Wa.t()) if ba is None else torch.addmm(ba, h[0], Wa.t())
-        value = (torch.mm(h[1], Wc.t()) if bc is None else torch.addmm(bc, h[1], Wc.t())).squeeze(-1)
+        logits, value = nat.heads_fwd(h, Wa, Wc, ba, bc)  # both heads in one pass over h
         ctx.save_for_backward(a3, bits, W4p, h, Wa, Wc)
         ctx.head_bias = (ba is not None, bc is not None)
         ctx.plan, ctx.mb, ctx.nw_q = plan, mb, Q.shape[1]

@@ -75,8 +75,8 @@ def main():
             agent.ac.load_state_dict(sd)
             agent.optimizer.load_state_dict(opt)
             torch.cuda.synchronize()
-            if n.endswith("_timers"):  # bench.py's per-kernel HIP events switched on
-                nat.KernelTimer.start()
+            if "_timers" in n:  # bench.py's per-kernel HIP events switched on (_timers4: every 4th launch)
+                nat.KernelTimer.start(every=4 if n.endswith("_timers4") else 1)
             t0 = time.perf_counter()
             agent.update(lv)
             torch.cuda.synchronize()

@@ -59,3 +59,26 @@ def test_colsum_strided_rows(device, rows):
     out = nat.colsum(x)
     torch.testing.assert_close(out.double(), x.double().sum(1), rtol=1e-5, atol=1e-5)
     assert torch.equal(out, nat.colsum(x))
+
+
+@pytest.mark.parametrize("n,A,bias", [(1, 3, False), (333, 3, True), (70001, 3, False), (100, 8, True), (513, 1, True)])
+def test_heads_fwd_matches_float64(device, n, A, bias):
+    """merlin_tower_heads_fwd (both heads in one pass over h) against float64 F.linear: within float32
+    summation error of the 512-term dot products, and the same bits on every call."""
+    from merlin import _native as nat
+
+    torch.manual_seed(n + A)
+    h = torch.relu(torch.randn(2, n, 512, device=device))
+    wa = torch.randn(A, 512, device=device) / 512 ** 0.5
+    wc = torch.randn(1, 512, device=device) / 512 ** 0.5
+    ba = torch.randn(A, device=device) if bias else None
+    bc = torch.randn(1, device=device) if bias else None
+    logits, value = nat.heads_fwd(h, wa, wc, ba, bc)
+    rl = F.linear(h[0].double(), wa.double(), None if ba is None else ba.double())
+    rv = F.linear(h[1].double(), wc.double(), None if bc is None else bc.double()).squeeze(-1)
+    mag_l = F.linear(h[0].double().abs(), wa.double().abs()) + (0 if ba is None else ba.double().abs())
+    mag_v = F.linear(h[1].double().abs(), wc.double().abs()).squeeze(-1) + (0 if bc is None else bc.double().abs())
+    assert ((logits.double() - rl).abs() <= 1e-6 * mag_l + 1e-7).all()
+    assert ((value.double() - rv).abs() <= 1e-6 * mag_v + 1e-7).all()
+    l2, v2 = nat.heads_fwd(h, wa, wc, ba, bc)
+    assert torch.equal(logits, l2) and torch.equal(value, v2)

@@ -68,17 +68,10 @@ def emulate_segment_sum(plan, src, out_rows, slot=None, sub=1, mask=None, fill=T
         if d < 0:
             continue
         a = carry[:, j0, s0].clone()
-        # k_seg_fix: rows of more than FIX_SHORT = 64 items go to FIX_WAVES = 4 waves by 16-item groups (group g to
-        # wave g % 4), each wave's item j0+1+i to its partial i % 4; the wave sums join in wave order
-        waves = 4 if j1 - j0 > 64 else 1
-        part = [[torch.zeros_like(a) for _ in range(4)] for _ in range(waves)]
+        part = [torch.zeros_like(a) for _ in range(4)]  # k_seg_fix: item j0+1+i goes to partial i % 4
         for i, j in enumerate(range(j0 + 1, j1 + 1)):
-            part[(i // 16) % waves][i % 4] += carry[:, j, 0]
-        s = None
-        for p in part:
-            w = (p[0] + p[1]) + (p[2] + p[3])
-            s = w if s is None else s + w
-        out[:, d] = a + s
+            part[i % 4] += carry[:, j, 0]
+        out[:, d] = a + ((part[0] + part[1]) + (part[2] + part[3]))
     return out
 
 
