@@ -6,4 +6,4 @@ rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] ||
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/smoke.log
 [ -n "$NO_PROF" ] && exit 0
-TAG=${TAG:-r03f} PMC=1 bash scripts/gpu_prof_r03.sh || exit $?
+TAG=${TAG:-r03j} PMC=1 bash scripts/gpu_prof_r03.sh || exit $?
