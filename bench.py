@@ -294,6 +294,7 @@ PMC_ALIAS = {"k_seg_sum_R": ("k_seg_sum<2, 1>", "k_seg_fix<1>"),
              "gemm_fc1_dgrad": ("k_x6_nt32<128, 192, 4, 2, 0, 1, 0>",),
              "gemm_rollout_fc1": ("k_x6_nt32<128, 128, 2, 2, 0, 1, 0>",),
              "k_head_bwd": ("k_head_bwd<3>", "k_head_fold"),
+             "k_heads_fwd": ("k_heads_fwd<3>",),
              "gemm_wgrad": ("k_x6_tn<128, 192, 2, 4>", "k_x6_fold")}
 PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 
