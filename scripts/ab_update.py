@@ -59,7 +59,7 @@ def main():
             FS.WGRAD_EARLY = "wgrad_early" in name
             nat.X6_NT_CFG["fwd"] = 28 if "fwd28" in name else 20
             nat.X6_NT_CFG["dgrad"] = 27 if "dgrad27" in name else 22
-            nat.X6_TN_CFG = 20 if "tn20" in name else 24 if "tn24" in name else 0
+            nat.X6_TN_CFG = next((int(t[2:]) for t in name.split("_") if t[:2] == "tn" and t[2:].isdigit()), 0)
             nat.X6_TN_SPLITS = 64 if "tn24" in name else next(
                 (int(t[1:]) for t in name.split("_") if t[:1] == "s" and t[1:].isdigit()), 32)  # e.g. fast_s64
             if agent.stage_impl != ("torch" if "torch_stage" in name else "hip"):
