@@ -329,10 +329,11 @@ def gather_note(name, k):
                              "guide_l2_gather_tbs": [16.8, 18.8], "frac_of_18_8": round(tbs / 18.8, 3)}}
 
 
-def kernel_table(records, every: int = 1):
+def kernel_table(records, counts=None):
     """{name: launches, total ms, avg us, algorithmic bytes (GB/s) or flops (TFLOP/s) per launch}
-    from HIP events; with every > 1 only each every-th launch was timed (`launches_timed`), and launches /
-    total_ms are scaled up to the whole region."""
+    from HIP events; `counts` = every launch of each name in the region (KernelTimer.counts): when only
+    each every-th launch was timed (`launches_timed` < launches), total_ms = the timed average x the true
+    launch count."""
     agg = {}
     for name, e0, e1, nbytes, flops in records:
         ms = e0.elapsed_time(e1)
@@ -343,8 +344,9 @@ def kernel_table(records, every: int = 1):
         a[3] += flops
     out = {}
     for name, (cnt, ms, nb, fl) in agg.items():
-        d = {"launches": cnt * every, "total_ms": round(ms * every, 3), "avg_us": round(ms / cnt * 1e3, 2)}
-        if every > 1:
+        n = int(counts.get(name, cnt)) if counts else cnt
+        d = {"launches": n, "total_ms": round(ms / cnt * n, 3), "avg_us": round(ms / cnt * 1e3, 2)}
+        if n != cnt:
             d["launches_timed"] = cnt
         if fl:
             d.update(flops_per_launch=fl // cnt, tflops=round(fl / (ms / 1e3) / 1e12, 2))
@@ -483,10 +485,16 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank (LOCAL_RANK); MERLIN_BENCH_DEVICE pins every rank to one device and
+    # MERLIN_DIST_BACKEND=gloo replaces RCCL, so a world-2 run can rehearse the multi-rank path on
+    # one GPU (tests/test_gpu_bench_dp.py: RCCL needs one GPU per rank)
+    local = int(os.environ.get("MERLIN_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    dp = DataParallel.init_from_env("nccl" if world > 1 else None, device)
+    backend = os.environ.get("MERLIN_DIST_BACKEND", "nccl") if world > 1 else None
+    dp = DataParallel.init_from_env(backend, device)
+    # small host-side exchanges (timing, per-rank spread) on the backend's own device kind
+    coll_dev = device if (backend or "nccl") == "nccl" else torch.device("cpu")
 
     N, T = args.num_envs, args.k_steps
     B = N * T
@@ -521,11 +529,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dp.enabled:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kernels = kernel_table(nat.KernelTimer.stop(), args.timer_every)
+    kernels = kernel_table(nat.KernelTimer.stop(), dict(nat.KernelTimer.counts))
     rollout_ms, update_ms = rollout_ms_of(ph), update_ms_of(ph)
     value = args.steps * B * world / elapsed
     rank_spread = None
@@ -537,7 +545,7 @@ def main():
         busy = sum(k["total_ms"] for k in kernels.values()) / args.steps
         mine = torch.tensor([rollout_ms_of(ph), update_ms_of(ph), busy,
                              agent.last_distinct_frac if agent.last_distinct_frac is not None else 1.0],
-                            dtype=torch.float64, device=device)
+                            dtype=torch.float64, device=coll_dev)
         allv = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allv, mine)
         a = torch.stack(allv).cpu().numpy()
@@ -546,11 +554,12 @@ def main():
                        "kernel_ms_per_iter": [round(float(x), 2) for x in a[:, 2]],
                        "distinct_frames_per_sample": [round(float(x), 4) for x in a[:, 3]],
                        "kernel_ms_max_over_min": round(float(a[:, 2].max() / max(a[:, 2].min(), 1e-9)), 4)}
-
-    if rank != 0:
-        if dp.enabled:
-            dist.barrier()
-        return
+        # the last collective of the run: everything below is rank 0 alone and collective-free (the tiers,
+        # which build agents whose updates all-reduce, run only at world 1; the N=1 line carries them)
+        dist.barrier()
+        if rank != 0:
+            dist.destroy_process_group()
+            return
     dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
     x6 = getattr(agent.ac, "fc1_impl", None) == "x6"
     handwritten = max((k for k in kernels if k.startswith("k_")), key=lambda k: kernels[k]["total_ms"])
@@ -617,6 +626,8 @@ def main():
         # conv2/conv3 evaluated once per distinct receptive-field window (merlin/windows.py)
         "windows_per_update": agent.last_num_windows,
         "rollout_graph": agent._graph is not None,
+        # the acting layout the rollout ran (CNNActorCritic.rollout_pack)
+        "rollout_acting": ("all-windows conv3 table" if agent.rollout_all_windows else "per-frame conv2 lookups"),
         "kernels": kernels,
     }
     if rank_spread is not None:
@@ -626,7 +637,9 @@ def main():
         U = int(round(agent.last_distinct_frac * (B // args.minibatches)))
         out["roofline_x6_standalone"] = x6_standalone(torch, U, device)
     state["phase"] = "tiers"
-    if not args.no_tiers:
+    if world > 1:
+        out["tiers"] = "run at n_gpus=1 only (their agents' updates would all-reduce on the world group)"
+    elif not args.no_tiers:
         floors = floor_tier(agent)
         fused, single = env_only_tier(torch, MerlinVecEnv, N, T, args.difficulty, args.size, device)
         out["tiers"] = {"env_only_fused_T_steps_per_launch": round(fused, 1),
@@ -644,7 +657,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline()
     print(json.dumps(out), flush=True)
     if dp.enabled:
-        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -813,6 +813,9 @@ template <int BM, int BN, int WGM, int WGN, int ACC, int APL = 0>
 hipError_t nt32_launch(const void *A, const u32x4 *B, int64_t M, int N, int K, int T, int64_t sA, int64_t sB,
                        const float *bias, float *C, int64_t sC, hipStream_t s) {
     if (N % BN) return hipErrorInvalidValue;
+    // planes-A form: the kernel keeps A chunk offsets (and B's, N * K * 3 / 8) in 32 bits
+    if (APL && (M + BM) * ((int64_t)(K / 8) * 3) > INT32_MAX) return hipErrorInvalidValue;
+    if ((int64_t)N * (K / 8) * 3 > INT32_MAX) return hipErrorInvalidValue;
     const int64_t tiles_m = (M + BM - 1) / BM;
     const int tiles_n = N / BN;
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;

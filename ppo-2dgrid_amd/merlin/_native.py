@@ -7,7 +7,9 @@ call is ordered on torch's current stream of the tensor's device.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import gc
 import os
 
 import torch  # loads the HIP runtime that libmerlin_hip.so links against (same soname)
@@ -167,6 +169,56 @@ EXPORTED_SYMBOLS = (
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
     "merlin_clip_adam_workspace", "merlin_clip_adam",
 )
+
+
+_CAPTURE_DEPTH = 0
+_DEFERRED: list = []
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """Wrap every HIP-graph capture (the rollout graph, FOMAML's rollout graphs, the fast step's weight stage).
+    Python's cyclic GC can run in the middle of a capture, triggered by any allocation, and finalise garbage
+    from earlier agents: a MerlinVecEnv's merlin_env_destroy (hipFree) or an old torch.cuda.CUDAGraph destroyed
+    mid-capture invalidates it or aborts the process (gpurun_out/t_w.log, round 3).  So: collect first, keep
+    the collector off until the capture ends, and have native handles released while a capture is open
+    (merlin.envs.MerlinVecEnv.close) queue their release until it has ended."""
+    global _CAPTURE_DEPTH
+    gc.collect()
+    was_enabled = gc.isenabled()
+    gc.disable()
+    _CAPTURE_DEPTH += 1
+    try:
+        yield
+    finally:
+        _CAPTURE_DEPTH -= 1
+        if _CAPTURE_DEPTH == 0:
+            if was_enabled:
+                gc.enable()
+            run_deferred()
+
+
+def capturing() -> bool:
+    """A capture is open in this process (capture_guard) or on the current stream."""
+    if _CAPTURE_DEPTH > 0:
+        return True
+    try:
+        return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    except Exception:
+        return False
+
+
+def defer_release(fn) -> None:
+    """Run `fn` (a native release: hipFree underneath) now, or after the open capture ends."""
+    if capturing():
+        _DEFERRED.append(fn)
+    else:
+        fn()
+
+
+def run_deferred() -> None:
+    while _DEFERRED:
+        _DEFERRED.pop(0)()
 
 
 class KernelTimer:

@@ -506,7 +506,7 @@ class CNNActorCritic(nn.Module):
     # the all-windows table (Qall: 9 GB and ~288 GFLOP per rollout, whatever the rollout's size)
     ALL_WINDOWS_MIN_FRAMES = 1 << 18
 
-    def rollout_pack(self, frames: int | None = None):
+    def rollout_pack(self, frames: int | None = None, all_windows: bool | None = None):
         """The weights of the acting path in the layouts its kernels and GEMMs read, built once
         per rollout (the weights do not change while acting).
 
@@ -517,7 +517,9 @@ class CNNActorCritic(nn.Module):
         sums 81 table rows per frame.  Small rollouts, or when the device has less than ~12 GB free:
         the conv2 table T2 (2,720 rows) and conv3's weights, and each step looks conv2 up per frame
         position and runs conv3 as a GEMM over the im2col rows (merlin_tower_conv2_lut_fwd +
-        conv3_im2col_fwd, a few MB).  Both: fc1 with columns permuted to (p3, co), biases stacked."""
+        conv3_im2col_fwd, a few MB).  Both: fc1 with columns permuted to (p3, co), biases stacked.
+        all_windows: the layout decided by the caller (PPO decides once, before its rollout is captured: the
+        free-memory reading changes between the eager rollout and the capture); None = decide here."""
         from . import _native as nat
 
         ea, ec = self.actor_extractor.network, self.critic_extractor.network
@@ -531,7 +533,9 @@ class CNNActorCritic(nn.Module):
             "b3": torch.stack([ea[4].bias, ec[4].bias]).contiguous(),
             "b4": torch.stack([fa.bias, fc.bias]).contiguous(),
         }
-        if self._use_all_windows(frames, T2.device):
+        if all_windows is None:
+            all_windows = self._use_all_windows(frames, T2.device)
+        if all_windows:
             Z2 = nat.window_lut(self._all_window_rows(T2.device), T2)  # [2, 5**9, 64]
             a2 = torch.relu_(Z2.add_(torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1)))
             pack["Qall"] = torch.bmm(a2, W3r)  # [2, windows, (ky, kx, co)]

@@ -40,8 +40,10 @@ class DataParallel:
         return DataParallel()
 
     def attach(self, module: torch.nn.Module) -> None:
-        """Broadcast rank 0's parameters and back every .grad by one flat buffer."""
-        params = [p for p in module.parameters() if p.requires_grad]
+        """Broadcast rank 0's parameters and back every .grad by one flat buffer.  The buffer spans every
+        parameter in parameter order (frozen ones too, so it lines up with the flat parameter buffer of
+        merlin/fast_step.py whatever is frozen later); only parameters that require grad get a .grad view."""
+        params = list(module.parameters())
         self._params = params
         if not self.enabled:
             return
@@ -61,7 +63,7 @@ class DataParallel:
         off = 0
         for p in self._params:
             n = p.numel()
-            p.grad = self._flat_grad[off:off + n].view_as(p)
+            p.grad = self._flat_grad[off:off + n].view_as(p) if p.requires_grad else None
             off += n
 
     def zero_grad(self, optimizer) -> None:

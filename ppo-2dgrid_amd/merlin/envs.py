@@ -101,9 +101,14 @@ class MerlinVecEnv:
         self._epl = torch.zeros(n, dtype=torch.int32, device=self.device)
 
     def close(self):
-        if getattr(self, "_h", None):
-            self._lib.merlin_env_destroy(self._h)
+        """Release the env's device state (merlin_env_destroy: hipFree).  While a HIP-graph capture is open
+        (e.g. this env dropped by a GC pass inside another agent's capture) the release waits for it to end:
+        a hipFree inside a capture invalidates it (merlin._native.capture_guard)."""
+        h = getattr(self, "_h", None)
+        if h:
             self._h = None
+            lib_ = self._lib
+            nat.defer_release(lambda: lib_.merlin_env_destroy(h))
 
     def __del__(self):  # pragma: no cover
         try:

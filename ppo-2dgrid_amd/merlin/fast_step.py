@@ -22,6 +22,8 @@ Same arithmetic as the autograd path (tests/test_gpu_fast_step.py compares a who
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import _native as nat
@@ -131,7 +133,7 @@ class WeightStage:
         DG = torch.zeros(self.fwd_map.numel(), dtype=torch.float32, device=self.flat_params.device)
         self.gT2 = torch.zeros((2, nat.LUT2_ROWS, 64), dtype=torch.float32, device=DG.device)
         self._dH = torch.empty((2, 680, 32), dtype=torch.float32, device=DG.device)  # scratch of the HIP adjoint
-        with torch.enable_grad():
+        with torch.enable_grad(), nat.capture_guard():  # no GC finalisers inside the captures
             with torch.cuda.graph(self.gfwd, pool=self.pool):
                 D, leaves, T2, planes = self._fwd()
             with torch.cuda.graph(self.gbwd, pool=self.pool):
@@ -174,7 +176,9 @@ class WindowStep:
     """One optimizer step of PPO._sgd on the window + x6 path (see the module docstring)."""
 
     def __init__(self, agent):
-        self.agent = agent
+        # weak: the agent holds this step (agent._wstep); a strong back-reference made every agent a reference
+        # cycle that only the cyclic GC frees -- possibly in the middle of another agent's graph capture
+        self._agent = weakref.ref(agent)
         ac = agent.ac
         self.params = list(ac.parameters())
         flat_params = agent._flat_params
@@ -223,7 +227,7 @@ class WindowStep:
     def step(self, plan, mb, mb_idx, actions, logp_old, adv, ret, totals):
         """Forward, loss (statistics added to `totals`), backward of one minibatch: every parameter's gradient
         is left in its .grad view (the optimizer step follows in PPO._sgd)."""
-        ag = self.agent
+        ag = self._agent()
         Wa, ba, Wc, bc = self.head
         g = self.stage.grads  # (dT2, db2, dW3r, db3, dW4p, db4)
         # ---- forward (merlin/windows.py window_tower_head_x6)

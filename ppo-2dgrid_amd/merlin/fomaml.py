@@ -109,7 +109,7 @@ class FOMAML:
                 torch.cuda.synchronize(self.device)
                 g = torch.cuda.CUDAGraph()
                 try:
-                    with torch.cuda.graph(g):
+                    with nat.capture_guard(), torch.cuda.graph(g):  # no GC finalisers inside the capture
                         self._rollout_body(env, st)
                     st["graph"] = g
                 except Exception:  # keep launching eagerly

@@ -96,6 +96,9 @@ class PPO:
         # after one eager rollout, replay the vectorised rollout as one captured HIP graph
         self.rollout_graph = rollout_graph
         self._graph = None
+        # the acting layout (CNNActorCritic.rollout_pack): the all-windows conv3 table, or per-frame conv2 lookups;
+        # decided at the first rollout and kept (None = not decided yet)
+        self.rollout_all_windows = None
         # look-ahead map refill on the side stream after every `refill_every`-th env step (_rollout_body).  Every
         # step: at the bench state (iterations 6-25) refilling every 4th step left so many slots empty at a second
         # reset that the in-step fallback grew from 4.6 to 23 us per step (rollout 35.3 vs ~31 ms,
@@ -175,9 +178,31 @@ class PPO:
         return torch.randperm(n, device=self.device)
 
     # ----------------------------------------------------------------- rollouts
+    def _params_on_flat(self) -> bool:
+        """Every parameter still a view of self._flat_params at its offset (parameter order)."""
+        off, base = 0, self._flat_params.data_ptr()
+        for p in self.ac.parameters():
+            if p.data_ptr() != base + p.element_size() * off:
+                return False
+            off += p.numel()
+        return off == self._flat_params.numel()
+
+    def _rehome_parameters(self) -> None:
+        """A parameter was rebound (`p.data = ...`, load_state_dict(assign=True)): put every parameter back on one
+        flat buffer (values kept; the Parameter objects, hence the optimizer state, stay the same) and drop what
+        captured the old addresses (the rollout graph, the fast step's weight stage)."""
+        from .fast_step import flatten_parameters
+
+        torch.cuda.synchronize(self.device)
+        self._graph = None
+        self._wstep = None
+        self._flat_params = flatten_parameters(self.ac)
+
     def collect_rollouts(self):
         if self.vec is None:
             return self._collect_rollouts_single()
+        if self._graph is not None and not self._params_on_flat():
+            self._rehome_parameters()  # the graph would read the old parameter storage: re-capture
         if self._graph is not None:
             self._graph.replay()
         else:
@@ -204,7 +229,10 @@ class PPO:
         env.reset(out=buf.codes[0])
         with torch.no_grad():
             self._act_epoch.add_(1)
-            pack = self.ac.rollout_pack(frames=(T + 1) * buf.N) if self.conv1_from_codes else None
+            if self.conv1_from_codes and self.rollout_all_windows is None:  # decided once, before any capture
+                self.rollout_all_windows = self.ac._use_all_windows((T + 1) * buf.N, self.device)
+            pack = (self.ac.rollout_pack(frames=(T + 1) * buf.N, all_windows=self.rollout_all_windows)
+                    if self.conv1_from_codes else None)
             pending = False
             for t in range(T):
                 self._act(buf.codes[t], pack, t, out=(buf.actions[t], buf.logprobs[t], buf.values[t]))
@@ -233,7 +261,7 @@ class PPO:
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g):
+            with nat.capture_guard(), torch.cuda.graph(g):  # no GC finalisers inside the capture
                 self._rollout_body()
         except Exception as e:  # an op this stack cannot capture: keep launching eagerly
             warnings.warn(f"rollout graph capture failed, rollouts stay eager: {e}")
@@ -349,10 +377,19 @@ class PPO:
         perms = [self._perm(B, epoch) for epoch in range(self.update_epochs)]  # drawn in epoch order
         # the window + x6 path's step with its launches written out (merlin/fast_step.py)
         fast = plan is not None and self.fast_step and getattr(self.ac, "fc1_impl", None) == "x6"
+        if fast and not all(p.requires_grad for p in self.ac.parameters()):
+            # the fast step writes a gradient for every parameter (and the optimizer steps every parameter that
+            # has one): with a frozen parameter the update takes the autograd path, which leaves it untouched
+            fast = False
+            for p in self.ac.parameters():
+                if not p.requires_grad:
+                    p.grad = None
         if fast:
             if self._wstep is None or not self._wstep.valid():
                 from .fast_step import WindowStep
 
+                if not self._params_on_flat():
+                    self._rehome_parameters()
                 self._wstep = WindowStep(self)
             self._wstep.bind_grads()
         # one host read per update for every minibatch's distinct-frame groups (merlin/windows.py)

@@ -1,0 +1,43 @@
+"""GPU: bench.py's multi-rank path end to end (BASELINE cfg 3's launch form), rehearsed on ONE
+GPU: `python -m torch.distributed.run --nproc-per-node 2 bench.py --gpus 2 ...` with gloo in place of RCCL
+(MERLIN_DIST_BACKEND) and both ranks pinned to device 0 (MERLIN_BENCH_DEVICE), as a fresh child process.
+The run must end by itself (no rank left waiting on a collective its partner never issues), print exactly
+one JSON line from rank 0 with n_gpus 2 and the per-rank spread, and report the whole-job rate."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_on_one_gpu_ends_with_one_line():
+    env = dict(os.environ, MERLIN_DIST_BACKEND="gloo", MERLIN_BENCH_DEVICE="0", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--num-envs", "256", "--k-steps", "16", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-4000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 2 * 256 * 16
+    assert out["value"] > 0 and out["scaling"] == "weak"
+    ranks = out["ranks"]
+    for k in ("rollout_ms", "update_ms", "kernel_ms_per_iter", "distinct_frames_per_sample"):
+        assert len(ranks[k]) == 2, (k, ranks)
+    # whole-job rate: both ranks' env-steps over the max-over-ranks time
+    assert abs(out["value"] - 2 * 2 * 256 * 16 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 0.01
