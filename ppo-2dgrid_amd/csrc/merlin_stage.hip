@@ -15,7 +15,9 @@
 // The combinations of one parity type (ee 5, eo 25, oe 25, oo 625) all read the same 4 of W2's 16 taps, so the
 // forward and dH kernels work on chunks of up to 8 combinations of one type with that type's W2 slice ([64][4][32],
 // 32 KB) in LDS; dW2 is one block per (tower, type, tap) summing over the type's combinations in chunks staged
-// through LDS.  Every sum runs in a fixed order: the same bits every call.
+// through LDS.  Every sum runs in a fixed order (the same bits every call) and accumulates in f64, rounded once to
+// f32 (dH, HT, T2 and the gradients): more accurate than the fp32 blocked sums of the torch formulation
+// (tests/test_gpu_stage_precision.py), for ~11 M multiply-adds per table, where the f64 rate costs nothing visible.
 #include "merlin_internal.h"
 
 namespace merlin {
@@ -49,7 +51,8 @@ __global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1,
                                                    const float *__restrict__ W2, const float *__restrict__ atlas,
                                                    const int16_t *__restrict__ idx, float *__restrict__ HT,
                                                    float *__restrict__ T2) {
-    __shared__ float Wl[C1 * 3 * 64], Al[5 * 3 * 64], P[C1 * 80], H[VB][C1], Ws[C2 * 4 * C1];
+    __shared__ float Wl[C1 * 3 * 64], Al[5 * 3 * 64], H[VB][C1], Ws[C2 * 4 * C1];
+    __shared__ double P[C1 * 80];
     const int t = blockIdx.y;
     int p, v0, nv;
     chunk_of(blockIdx.x, p, v0, nv);
@@ -62,14 +65,14 @@ __global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1,
         const int o = q / 80, k = q - o * 80;
         const int slot = k / 20, bin = k - slot * 20;
         const int dy = slot >> 1, dx = slot & 1, z = bin >> 2, qy = (bin >> 1) & 1, qx = bin & 1;
-        float acc = 0.0f;
+        double acc = 0.0;
         for (int c = 0; c < 3; c++)
 #pragma unroll
             for (int kk = 0; kk < 4; kk++)
 #pragma unroll
                 for (int l = 0; l < 4; l++)
-                    acc += Wl[(o * 3 + c) * 64 + (4 * dy + kk) * 8 + 4 * dx + l] *
-                           Al[(z * 3 + c) * 64 + (4 * qy + kk) * 8 + 4 * qx + l];
+                    acc += (double)Wl[(o * 3 + c) * 64 + (4 * dy + kk) * 8 + 4 * dx + l] *
+                           (double)Al[(z * 3 + c) * 64 + (4 * qy + kk) * 8 + 4 * qx + l];
         P[q] = acc;
     }
     __syncthreads();
@@ -77,8 +80,9 @@ __global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1,
         const int vl = threadIdx.x / C1, o = threadIdx.x - vl * C1;  // VB * C1 == 256
         if (vl < nv) {
             const int v = v0 + vl;
-            float s = b1[t * C1 + o];
-            for (int e = 0; e < 4; e++) s += P[o * 80 + idx[v * 4 + e]];
+            double d = b1[t * C1 + o];
+            for (int e = 0; e < 4; e++) d += P[o * 80 + idx[v * 4 + e]];
+            float s = (float)d;
             s = s != s ? s : fmaxf(s, 0.0f);
             H[vl][o] = s;
             HT[((size_t)t * NV + v) * C1 + o] = s;
@@ -88,10 +92,10 @@ __global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1,
     for (int q = threadIdx.x; q < nv * 4 * C2; q += 256) {  // T2 rows 4 v + j
         const int vl = q / (4 * C2), r = q - vl * 4 * C2, j = r / C2, co = r - j * C2;
         const float *w = Ws + (co * 4 + j) * C1;
-        float acc = 0.0f;
+        double acc = 0.0;
 #pragma unroll 8
-        for (int o = 0; o < C1; o++) acc += H[vl][o] * w[o];
-        T2[((size_t)t * NROW + 4 * (v0 + vl) + j) * C2 + co] = acc;
+        for (int o = 0; o < C1; o++) acc += (double)H[vl][o] * (double)w[o];
+        T2[((size_t)t * NROW + 4 * (v0 + vl) + j) * C2 + co] = (float)acc;
     }
 }
 
@@ -108,12 +112,12 @@ __global__ __launch_bounds__(256) void k_stage_bwd_h(const float *__restrict__ W
     __syncthreads();
     const int vl = threadIdx.x / C1, o = threadIdx.x - vl * C1;
     if (vl >= nv) return;
-    float acc = 0.0f;
+    double acc = 0.0;
     for (int j = 0; j < 4; j++)
 #pragma unroll 8
-        for (int co = 0; co < C2; co++) acc += G[vl][j * C2 + co] * Ws[(co * 4 + j) * C1 + o];
+        for (int co = 0; co < C2; co++) acc += (double)G[vl][j * C2 + co] * (double)Ws[(co * 4 + j) * C1 + o];
     const size_t hi = ((size_t)t * NV + v0 + vl) * C1 + o;
-    dH[hi] = HT[hi] > 0.0f ? acc : 0.0f;
+    dH[hi] = HT[hi] > 0.0f ? (float)acc : 0.0f;
 }
 
 constexpr int VS = 32;  // combinations per LDS stage of the dW2 blocks
@@ -127,15 +131,16 @@ __global__ __launch_bounds__(256) void k_stage_bwd_w(const float *__restrict__ H
                                                      const int16_t *__restrict__ koff, const int16_t *__restrict__ kv,
                                                      int T, float *__restrict__ dW1, float *__restrict__ db1,
                                                      float *__restrict__ dW2) {
-    __shared__ float Hs[VS][C1], Gs[VS][C2], red[256], dP[80];
+    __shared__ float Hs[VS][C1], Gs[VS][C2];
+    __shared__ double red[256], dP[80];
     if ((int)blockIdx.x < T * 16) {
         const int t = blockIdx.x / 16, p = (blockIdx.x / 4) & 3, j = blockIdx.x & 3;
         const int tap = (2 * (j >> 1) + (p >> 1)) * 4 + 2 * (j & 1) + (p & 1);
         const int va = part_off(p), vb = part_off(p + 1);
         const int o = threadIdx.x & (C1 - 1), cq = threadIdx.x >> 5;  // outputs (co = cq + 8 i, o)
-        float acc[8];
+        double acc[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) acc[i] = 0.0f;
+        for (int i = 0; i < 8; i++) acc[i] = 0.0;
         for (int vs = va; vs < vb; vs += VS) {
             const int n = min(VS, vb - vs);
             __syncthreads();
@@ -146,25 +151,25 @@ __global__ __launch_bounds__(256) void k_stage_bwd_w(const float *__restrict__ H
             }
             __syncthreads();
             for (int vl = 0; vl < n; vl++) {
-                const float h = Hs[vl][o];
+                const double h = Hs[vl][o];
 #pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] += h * Gs[vl][cq + 8 * i];
+                for (int i = 0; i < 8; i++) acc[i] += h * (double)Gs[vl][cq + 8 * i];
             }
         }
 #pragma unroll
-        for (int i = 0; i < 8; i++) dW2[(((size_t)t * C2 + cq + 8 * i) * C1 + o) * 16 + tap] = acc[i];
+        for (int i = 0; i < 8; i++) dW2[(((size_t)t * C2 + cq + 8 * i) * C1 + o) * 16 + tap] = (float)acc[i];
         return;
     }
     const int b = blockIdx.x - T * 16, t = b / C1, o = b - t * C1;
     const float *d = dH + (size_t)t * NV * C1 + o;
     {  // db1: thread i sums combinations i, i + 256, ... in order, then a fixed tree
-        float s = 0.0f;
+        double s = 0.0;
         for (int v = threadIdx.x; v < NV; v += 256) s += d[(size_t)v * C1];
         red[threadIdx.x] = s;
     }
     if (threadIdx.x < 80) {  // dP[o][k]: the (v, e) entries with idx[v][e] = k, in (v, e) order
         const int k = threadIdx.x;
-        float acc = 0.0f;
+        double acc = 0.0;
         for (int i = koff[k]; i < koff[k + 1]; i++) acc += d[(size_t)kv[i] * C1];
         dP[k] = acc;
     }
@@ -173,16 +178,16 @@ __global__ __launch_bounds__(256) void k_stage_bwd_w(const float *__restrict__ H
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) db1[t * C1 + o] = red[0];
+    if (threadIdx.x == 0) db1[t * C1 + o] = (float)red[0];
     for (int q = threadIdx.x; q < 3 * 64; q += 256) {  // dW1[t][o][c][ky][kx]
         const int c = q >> 6, ky = (q >> 3) & 7, kx = q & 7;
         const int dy = ky >> 2, kk = ky & 3, dx = kx >> 2, l = kx & 3, slot = 2 * dy + dx;
-        float acc = 0.0f;
+        double acc = 0.0;
         for (int bin = 0; bin < 20; bin++) {
             const int z = bin >> 2, qy = (bin >> 1) & 1, qx = bin & 1;
-            acc += dP[slot * 20 + bin] * atlas[((z * 3 + c) * 8 + 4 * qy + kk) * 8 + 4 * qx + l];
+            acc += dP[slot * 20 + bin] * (double)atlas[((z * 3 + c) * 8 + 4 * qy + kk) * 8 + 4 * qx + l];
         }
-        dW1[(((size_t)t * C1 + o) * 3 + c) * 64 + ky * 8 + kx] = acc;
+        dW1[(((size_t)t * C1 + o) * 3 + c) * 64 + ky * 8 + kx] = (float)acc;
     }
 }
 

@@ -62,10 +62,8 @@ def test_fast_step_hip_tables_close_and_reproducible(device):
     for (k, p0), p1 in zip(a0.ac.named_parameters(), a1.ac.parameters()):
         d = (p1 - p0).detach().abs()
         assert float(d.max()) <= 2 * 1e-3 * 8, k
-        if k.startswith("critic"):  # 99 % of the elements, and at least all but one (Adam's per-element
-            # normalisation turns a float32-level difference in a near-zero gradient into a step of ~lr)
-            close = int((d <= 1e-6 + 1e-4 * p0.detach().abs()).sum())
-            assert close >= min(0.99 * p0.numel(), p0.numel() - 1), (k, close, p0.numel())
+        if k.startswith("critic"):
+            assert int((d <= 1e-6 + 1e-4 * p0.detach().abs()).sum()) >= 0.999 * p0.numel(), k
 
 
 def test_stage_tables_match_torch(device):

@@ -102,16 +102,17 @@ def test_fullsize_window_update_matches_lookup_path(device):
     table = [(name, rel(a, r), rel(b, r)) for (name, _), a, b, r in zip(agent.ac.named_parameters(), g1, g2, g64)]
     print("\n".join(f"{n:40s} windows {x:.2e} lookup {y:.2e}" for n, x, y in table))
     # The actor tower's level is fp32 rounding times the cancellation of the policy-gradient sum (advantages of
-    # mean 0 over a near-uniform policy), so it moves with any regrouping of the forward's fp32 sums: windows
-    # with the HIP conv tables (csrc/merlin_stage.hip, the default) 5.4e-4 on conv1's weight, with the torch
-    # tables 2.0e-4, lookup 3.2e-4 -- while the tables themselves sit at float32 level either way (T2 1.6e-7,
-    # dW1 3.8e-7 vs torch's 1.6e-7 / 2.7e-7 of float64, scripts/probe_stage_precision.py).  Hence the cap of
-    # 1e-3, with windows held to twice the lookup path's own distance from float64.
-    bad = [t for t in table if t[1] > 1e-3 or t[2] > 1e-3 or t[1] > 2 * t[2] + 2e-5]
+    # mean 0 over a near-uniform policy).  The HIP conv tables (csrc/merlin_stage.hip) accumulate in f64 and round
+    # once, no further from float64 than the torch formulation (tests/test_gpu_stage_precision.py); windows are
+    # held to twice the lookup path's own distance from float64.
+    bad = [t for t in table if t[1] > 5e-4 or t[2] > 5e-4 or t[1] > 2 * t[2] + 2e-5]
     assert not bad, bad
     assert nw is not None and nw > 1000 and 0.1 < frac <= 1.0, (nw, frac)
     for k in s1:
-        tol = 4.0 / (B // MB) if k == "clipfrac" else 1e-4 * max(1.0, abs(s2[k]))
+        # the pre-clip gradient norm is 1-Lipschitz in the gradient, so the gradient cap above bounds it: each path
+        # within 5e-4 of float64 (measured 1.3e-4 apart); the loss statistics to 1e-4
+        tol = (4.0 / (B // MB) if k == "clipfrac" else 5e-4 * abs(s2[k]) if k == "gradnorm"
+               else 1e-4 * max(1.0, abs(s2[k])))
         assert abs(s1[k] - s2[k]) <= tol, (k, s1[k], s2[k])
     ds = [(a - b).abs().flatten() for a, b in zip(p1, p2)]
     for d in ds:
