@@ -55,10 +55,11 @@ WINDOW_FWD_MACS = 2 * 64 * 576  # per window per minibatch
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (vector == f32 MFMA rate)
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense BF16 MFMA (MI355X_MICROARCH.md; no sparsity)
-# fc1's three GEMMs run on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip):
-# six bf16 MFMA products per fp32 product, so their executed MFMA work is 6x the fp32 FLOP count
+# fc1's three GEMMs run on the matrix cores in plane form: "h3" (default, csrc/merlin_h3.hip) three f16 MFMA
+# products per fp32 product, "x6" (csrc/merlin_gemm.hip) six bf16 products; their executed MFMA work is that
+# multiple of the fp32 FLOP count, priced against the dense 16-bit MFMA peak (f16 = bf16 rate)
 X6_GEMMS = ("gemm_fc1_fwd", "gemm_fc1_dgrad", "gemm_wgrad")
-X6_PRODUCTS = 6
+PLANE_PRODUCTS = {"h3": 3, "x6": 6}
 
 
 def parse():
@@ -224,21 +225,30 @@ def env_large_tier(torch, MerlinVecEnv, difficulty, size, device, n=1 << 21, T=1
                             "us_per_step": round(sec_reset / T * 1e6, 2), "resets": resets}}
 
 
-def x6_standalone(torch, U, device, reps=10):
-    """fc1's three x6 GEMMs timed alone (HIP events, no other stream active) at the update's shape
+def x6_standalone(torch, U, device, impl="h3", reps=10):
+    """fc1's three plane-form GEMMs timed alone (HIP events, no other stream active) at the update's shape
     (U distinct frames per minibatch): in the timed loop the weight gradient shares the chip with
     conv3's backward sums on the other stream, so its in-loop event time includes that sharing."""
     from merlin import _native as nat
 
     g = torch.Generator(device=device).manual_seed(0)
     a3 = torch.relu(torch.randn(2, U, 576, device=device, generator=g))
-    dz = torch.randn(2, U, 512, device=device, generator=g)
-    Wp = nat.x6_split(torch.randn(2, 512, 576, device=device, generator=g) / 24)
-    Wtp = nat.x6_split(torch.randn(2, 576, 512, device=device, generator=g) / 24)
+    dz = torch.randn(2, U, 512, device=device, generator=g) * 1e-6
+    W = torch.randn(2, 512, 576, device=device, generator=g) / 24
+    Wt = W.transpose(1, 2).contiguous()
     b = torch.zeros(2, 512, device=device)
-    runs = {"gemm_fc1_fwd": lambda: nat.x6_gemm_nt(a3, Wp, bias=b, cfg=nat.X6_NT_CFG["fwd"]),
-            "gemm_fc1_dgrad": lambda: nat.x6_gemm_nt(dz, Wtp, cfg=nat.X6_NT_CFG["dgrad"]),
-            "gemm_wgrad": lambda: nat.x6_gemm_tn(dz, a3)}
+    if impl == "h3":
+        am3, amz, amW = nat.h3_amax(a3), nat.h3_amax(dz), nat.h3_amax(W)
+        Wp, Wtp = nat.h3_split(W, amW), nat.h3_split(Wt, amW)
+        runs = {"gemm_fc1_fwd": lambda: nat.h3_gemm_nt(a3, am3, Wp, amW, bias=b, cfg=nat.H3_NT_CFG["fwd"]),
+                "gemm_fc1_dgrad": lambda: nat.h3_gemm_nt(dz, amz, Wtp, amW, cfg=nat.H3_NT_CFG["dgrad"]),
+                "gemm_wgrad": lambda: nat.h3_gemm_tn(dz, amz, a3, am3)}
+    else:
+        Wp, Wtp = nat.x6_split(W), nat.x6_split(Wt)
+        runs = {"gemm_fc1_fwd": lambda: nat.x6_gemm_nt(a3, Wp, bias=b, cfg=nat.X6_NT_CFG["fwd"]),
+                "gemm_fc1_dgrad": lambda: nat.x6_gemm_nt(dz, Wtp, cfg=nat.X6_NT_CFG["dgrad"]),
+                "gemm_wgrad": lambda: nat.x6_gemm_tn(dz, a3)}
+    P = PLANE_PRODUCTS[impl]
     out = {}
     for name, fn in runs.items():
         fn()
@@ -249,11 +259,11 @@ def x6_standalone(torch, U, device, reps=10):
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / reps * 1e3
-        ex = X6_PRODUCTS * 2 * 2 * U * 576 * 512 / (us * 1e-6) / 1e12
+        ex = P * 2 * 2 * U * 576 * 512 / (us * 1e-6) / 1e12
         out[name] = {"avg_launch_us": round(us, 2), "achieved": round(ex, 2), "peak": BF16_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(ex / BF16_PEAK_TFLOPS, 4),
-                     "fp32_equivalent_tflops": round(ex / X6_PRODUCTS, 2)}
-    return {"rows": U, "kernels": out}
+                     "fp32_equivalent_tflops": round(ex / P, 2)}
+    return {"rows": U, "impl": impl, "kernels": out}
 
 
 def cpu_baseline():
@@ -356,18 +366,20 @@ def kernel_table(records, counts=None):
     return out
 
 
-# the MFMA each x6 GEMM runs on (merlin._native.X6_NT_CFG / X6_TN_CFG: cfg >= 20 are the 32x32x16 kernels)
-X6_MFMA = {"gemm_fc1_fwd": "bf16 32x32x16", "gemm_fc1_dgrad": "bf16 32x32x16", "gemm_wgrad": "bf16 16x16x32"}
+# the MFMA each plane-form GEMM runs on (merlin._native.H3_* / X6_NT_CFG / X6_TN_CFG)
+PLANE_MFMA = {"h3": {k: "f16 32x32x16" for k in X6_GEMMS},
+              "x6": {"gemm_fc1_fwd": "bf16 32x32x16", "gemm_fc1_dgrad": "bf16 32x32x16", "gemm_wgrad": "bf16 16x16x32"}}
 
 
-def roofline_of(name, k, x6=False):
+def roofline_of(name, k, impl=None):
     traffic = pmc_traffic(name)
-    if "tflops" in k and x6 and name in X6_GEMMS:  # fc1 on the bf16 matrix cores: executed bf16 MFMA work
-        ex = k["tflops"] * X6_PRODUCTS
+    if "tflops" in k and impl in PLANE_PRODUCTS and name in X6_GEMMS:  # fc1 on the 16-bit matrix cores
+        P = PLANE_PRODUCTS[impl]
+        ex = k["tflops"] * P
         return {"kernel": name, "bound": "mfma", "achieved": round(ex, 2), "peak": BF16_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ex / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
-                "flops_per_launch": k["flops_per_launch"] * X6_PRODUCTS, "avg_launch_us": k["avg_us"],
-                "launches": k["launches"], "mfma": X6_MFMA.get(name, "bf16") + ", 6 plane products per fp32 product",
+                "flops_per_launch": k["flops_per_launch"] * P, "avg_launch_us": k["avg_us"],
+                "launches": k["launches"], "mfma": f"{PLANE_MFMA[impl][name]}, {P} plane products per fp32 product",
                 "fp32_equivalent_tflops": k["tflops"],
                 "fp32_equivalent_frac_of_f32_peak": round(k["tflops"] / FP32_PEAK_TFLOPS, 4)}
     if "tflops" in k:  # a hipBLASLt GEMM: f32 MFMA bound
@@ -561,7 +573,8 @@ def main():
             dist.destroy_process_group()
             return
     dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
-    x6 = getattr(agent.ac, "fc1_impl", None) == "x6"
+    fc1 = getattr(agent.ac, "fc1_impl", None)
+    x6 = fc1 in PLANE_PRODUCTS
     handwritten = max((k for k in kernels if k.startswith("k_")), key=lambda k: kernels[k]["total_ms"])
     ref_flop_per_step = 2 * FWD_MACS + args.epochs * 2 * (FWD_MACS + BWD_MACS)
     frac = agent.last_distinct_frac if agent.last_distinct_frac is not None else 1.0
@@ -601,7 +614,7 @@ def main():
                                        if agent.last_distinct_frac is not None else None),
         # dominant kernel of the timed loop by total HIP-event time (hand-written kernels and the
         # fc1 hipBLASLt GEMMs, which are timed the same way)
-        "roofline": dict(roofline_of(dominant, kernels[dominant], x6),
+        "roofline": dict(roofline_of(dominant, kernels[dominant], fc1),
                          **({"note": "in the loop the weight gradient runs on a side stream beside conv3's "
                                      "backward segmented sums, so its event time includes that sharing; "
                                      "alone: roofline_x6_standalone"} if dominant == "gemm_wgrad" and x6 else {})),
@@ -610,7 +623,9 @@ def main():
                                      **gather_note(handwritten, kernels[handwritten])),
         # every GEMM family timed in the loop: fc1's (x6) against the bf16 MFMA peak with the executed
         # plane products, hipBLASLt's against the f32 MFMA peak
-        "roofline_gemm": {k: roofline_of(k, v, x6) for k, v in kernels.items() if "tflops" in v},
+        "roofline_gemm": {k: roofline_of(k, v, fc1) for k, v in kernels.items() if "tflops" in v},
+        # fc1's GEMM form: h3 = f16 two-plane (3 products, error below hipBLASLt's fp32 GEMM), x6 = bf16 three-plane
+        "fc1_impl": fc1,
         # the env-step kernel inside the timed loop (absent when the rollout replays as a graph:
         # no per-kernel events inside it); the HBM-scale measurement is tiers.env_only_2M_envs
         "roofline_env_step": roofline_of("k_env_step", kernels["k_env_step"]) if "k_env_step" in kernels else None,
@@ -635,7 +650,7 @@ def main():
     if x6 and agent.last_distinct_frac is not None:
         # the x6 GEMMs alone at the update's shape (distinct frames per minibatch)
         U = int(round(agent.last_distinct_frac * (B // args.minibatches)))
-        out["roofline_x6_standalone"] = x6_standalone(torch, U, device)
+        out["roofline_x6_standalone"] = x6_standalone(torch, U, device, fc1)
     state["phase"] = "tiers"
     if world > 1:
         out["tiers"] = "run at n_gpus=1 only (their agents' updates would all-reduce on the world group)"

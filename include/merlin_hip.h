@@ -295,10 +295,13 @@ int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32
 int64_t merlin_tower_all_windows(void);
 int merlin_tower_codes_conv3(const uint32_t *codes_dev, int64_t n, const float *Qall_dev,
                              const float *b3_dev, int32_t towers, float *Y3_dev, void *stream);
-/* Same, also writing relu_bits_dev uint64[towers][n*9]: bit co of row (k*9 + p3) = Y3 > 0 there. */
+/* Same, also writing relu_bits_dev uint64[towers][n*9]: bit co of row (k*9 + p3) = Y3 > 0 there; amax_dev
+ * (or NULL): atomicMax of max |Y3| per tower as float bits into amax_dev[t] (zeroed by the caller), the operand
+ * scale of fc1's f16 two-plane GEMMs (merlin_h3_gemm_*). */
 int merlin_tower_window_conv3_bits(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
                                    const int64_t *groups_dev, int64_t n, const float *b3_dev,
-                                   int32_t towers, float *Y3_dev, uint64_t *relu_bits_dev, void *stream);
+                                   int32_t towers, float *Y3_dev, uint64_t *relu_bits_dev, uint32_t *amax_dev,
+                                   void *stream);
 int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *idx_dev,
                        const int32_t *key_dev, int64_t nnz, const int32_t *slot_dev, int32_t sub,
                        int64_t item_len, const int32_t *fix_dev, int64_t n_fix, int32_t towers,
@@ -388,7 +391,8 @@ int merlin_ppo_loss(const float *logits_dev, const float *value_dev, const float
  *            w_actor float[act_dim][hidden], w_critic float[hidden] ->
  *            dz[0][k] = [h0 > 0] * (dlogits[k] . w_actor), dz[1][k] = [h1 > 0] * dvalue[k] * w_critic,
  *            dbias float[2][hidden] = sum_k dz[t][k], dw_actor = dlogits^T h0, dw_critic = dvalue^T h1
- *            (fixed-order sums; act_dim <= 8). */
+ *            (fixed-order sums; act_dim <= 8); amax_dev (or NULL): atomicMax of max |dz| per tower as float
+ *            bits into amax_dev[0..1] (zeroed by the caller; merlin_h3_gemm_*'s operand scale). */
 int merlin_tower_bias_relu(float *z_dev, const float *bias_dev, int64_t rows, int32_t cols, int32_t towers,
                            void *stream);
 int merlin_tower_relu_bwd(const float *y_dev, const float *dy_dev, float *dz_dev, int64_t rows, int32_t cols,
@@ -401,7 +405,7 @@ int merlin_tower_colsum(const float *x_dev, int64_t rows, int32_t cols, int64_t 
 int merlin_tower_head_bwd(const float *h_dev, const float *dlogits_dev, const float *dvalue_dev,
                           const float *w_actor_dev, const float *w_critic_dev, int64_t n, int32_t hidden,
                           int32_t act_dim, float *dz_dev, float *dbias_dev, float *dw_actor_dev,
-                          float *dw_critic_dev, void *stream);
+                          float *dw_critic_dev, uint32_t *amax_dev, void *stream);
 /* heads_fwd: the two heads (actor_critic.py:41-46, Linear(512, act_dim) / Linear(512, 1)) on h
  * float[2][n][hidden] = relu(fc1) of the actor / critic tower: logits float[n][act_dim] = h0 w_actor^T
  * (+ b_actor), value float[n] = h1 . w_critic (+ b_critic); biases may be NULL (not added).  hidden 512,
@@ -434,6 +438,31 @@ int64_t merlin_x6_tn_slab_floats(int32_t M, int32_t N, int32_t towers, int32_t s
 int merlin_x6_gemm_tn(const float *A_dev, const float *B_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
                       int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev, float *out_dev, int32_t cfg,
                       void *stream);
+
+/* fc1 (src/actor_critic.py:31-41) on the f16 matrix cores in fp32-class two-plane form (csrc/merlin_h3.hip, the
+ * default of PPO.update's fc1 GEMMs): every operand x is scaled by a per-tower power of two 2^e (from its max |x|:
+ * max |x| 2^e in [2^14, 2^15)) and used as two f16 planes h = f16(x'), l = f16((x' - h) 2^11); a product as the three
+ * plane products h h, h l, l h (fp32 accumulation, the lo sum scaled by 2^-11 once), the result scaled back by
+ * 2^-(eA + eB).  Error per output below the fp32 GEMM's (hipBLASLt) on the same operands (tests/test_gpu_h3.py).
+ * Replaces the same three fp32 GEMMs as merlin_x6_* (forward src/actor_critic.py:40, backward src/ppo.py:153-155).
+ * amax:  amax_dev[t] = float bits of max |x| over tower t's n values (x + t * stride; n, stride % 4 == 0).
+ * split: weight planes f16 [t][n/8][2][8] (per group of 8 values a hi and a lo 16-byte chunk), scaled by the
+ *        exponent of amax_dev[t]; 4 bytes per value.
+ * gemm_nt: C[t][m][n] = sum_k A[t][m][k] B[t][n][k], A fp32 [M][K] with its amax, B planes [N][K] (K % 32 == 0;
+ *          tower strides in values), + bias[t][n] and ReLU when bias != NULL; cfg: 0 256x128, 1 128x192,
+ *          2 128x128, 3 128x256 (N a multiple of the tile width).
+ * gemm_tn: out[t][m][n] = sum_k A[t][k][m] B[t][k][n], both fp32 with their amax (cfg 0 / 1: 128x192 tiles, M % 128,
+ *          N % 192), the k range cut into <= splits slabs (slab float[merlin_x6_tn_slab_floats(...)]) summed in slab
+ *          order. */
+int merlin_h3_amax(const float *x_dev, int64_t n, int32_t towers, int64_t stride, uint32_t *amax_dev, void *stream);
+int merlin_h3_split(const float *x_dev, int64_t n, int32_t towers, const uint32_t *amax_dev, void *planes_dev,
+                    void *stream);
+int merlin_h3_gemm_nt(const float *A_dev, const uint32_t *amax_a_dev, const void *B_dev, const uint32_t *amax_b_dev,
+                      int64_t M, int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride,
+                      const float *bias_dev, float *C_dev, int64_t c_stride, int32_t cfg, void *stream);
+int merlin_h3_gemm_tn(const float *A_dev, const uint32_t *amax_a_dev, const float *B_dev, const uint32_t *amax_b_dev,
+                      int64_t Kd, int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride,
+                      int32_t splits, float *slab_dev, float *out_dev, int32_t cfg, void *stream);
 
 /* The conv1 / conv2 tables of both towers and their adjoint (the parameter-only part of PPO.update's
  * minibatch step, merlin/fast_step.py WeightStage; replaces CNNActorCritic.conv2_tables and its autograd

@@ -638,15 +638,16 @@ int merlin_tower_window_conv3(const float *Q, int64_t nw, const int32_t *wid, co
                               const float *b3, int32_t towers, float *Y3, void *stream) {
     if ((!Q || !wid || !b3 || !Y3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, nullptr, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, nullptr, nullptr, (hipStream_t)stream));
     return MERLIN_OK;
 }
 
 int merlin_tower_window_conv3_bits(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                                   const float *b3, int32_t towers, float *Y3, uint64_t *relu_bits, void *stream) {
+                                   const float *b3, int32_t towers, float *Y3, uint64_t *relu_bits, uint32_t *amax,
+                                   void *stream) {
     if ((!Q || !wid || !b3 || !Y3 || !relu_bits) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, amax, (hipStream_t)stream));
     return MERLIN_OK;
 }
 
@@ -770,7 +771,7 @@ int merlin_tower_colsum(const float *x, int64_t rows, int32_t cols, int64_t row_
 
 int merlin_tower_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *w_actor,
                           const float *w_critic, int64_t n, int32_t hidden, int32_t act_dim, float *dz, float *dbias,
-                          float *dw_actor, float *dw_critic, void *stream) {
+                          float *dw_actor, float *dw_critic, uint32_t *amax, void *stream) {
     if (!dbias || !dw_actor || !dw_critic || ((!h || !dlogits || !dvalue || !w_actor || !w_critic || !dz) && n > 0))
         return fail(MERLIN_E_INVALID, "null argument");
     if (act_dim < 1 || act_dim > merlin::epilogue_max_act()) return fail(MERLIN_E_UNSUPPORTED, "act_dim must be 1..8");
@@ -779,7 +780,7 @@ int merlin_tower_head_bwd(const float *h, const float *dlogits, const float *dva
     int rc = device_ws(&ws);
     if (rc) return rc;
     HIP_TRY(merlin::launch_head_bwd(h, dlogits, dvalue, w_actor, w_critic, n, hidden, act_dim, dz, dbias, dw_actor,
-                                    dw_critic, ws->epi_work, (hipStream_t)stream));
+                                    dw_critic, ws->epi_work, amax, (hipStream_t)stream));
     return MERLIN_OK;
 }
 
@@ -854,6 +855,52 @@ int merlin_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int32_t M, int
     if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return fail(MERLIN_E_INVALID, "M, N: multiples of 8");
     const hipError_t e = merlin::launch_x6_gemm_tn(A, B, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, cfg,
                                                    (hipStream_t)stream);
+    if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "M / N not multiples of the tile / bad cfg");
+    HIP_TRY(e);
+    return MERLIN_OK;
+}
+
+int merlin_h3_amax(const float *x, int64_t n, int32_t towers, int64_t stride, uint32_t *amax, void *stream) {
+    if (!amax || (n > 0 && !x)) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (n < 0 || n % 4 || stride % 4 || (towers > 1 && stride < n)) return fail(MERLIN_E_INVALID, "n, stride: multiples of 4");
+    HIP_TRY(merlin::launch_h3_amax(x, n, towers, stride, amax, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_h3_split(const float *x, int64_t n, int32_t towers, const uint32_t *amax, void *planes, void *stream) {
+    if ((!x || !planes || !amax) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (n < 0 || n % 8) return fail(MERLIN_E_INVALID, "n must be a non-negative multiple of 8");
+    HIP_TRY(merlin::launch_h3_split(x, n, towers, amax, planes, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
+                      int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride, const float *bias,
+                      float *C, int64_t c_stride, int32_t cfg, void *stream) {
+    if (M < 0 || N <= 0 || K <= 0) return fail(MERLIN_E_INVALID, "bad shape");
+    if (M > 0 && (!A || !B || !C || !amax_a || !amax_b)) return fail(MERLIN_E_INVALID, "null argument");
+    if (K % 32) return fail(MERLIN_E_UNSUPPORTED, "K must be a multiple of 32");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (a_stride % 4 || b_stride % 8) return fail(MERLIN_E_INVALID, "tower strides: A multiple of 4, B of 8");
+    const hipError_t e = merlin::launch_h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, bias, C,
+                                                   c_stride, cfg, (hipStream_t)stream);
+    if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "N not a multiple of the tile width / bad cfg");
+    HIP_TRY(e);
+    return MERLIN_OK;
+}
+
+int merlin_h3_gemm_tn(const float *A, const uint32_t *amax_a, const float *B, const uint32_t *amax_b, int64_t Kd,
+                      int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride, int32_t splits,
+                      float *slab, float *out, int32_t cfg, void *stream) {
+    if (Kd < 0 || M <= 0 || N <= 0) return fail(MERLIN_E_INVALID, "bad shape");
+    if (!out || (Kd > 0 && (!A || !B || !slab || !amax_a || !amax_b))) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (splits < 1 || splits > merlin::x6_tn_max_splits()) return fail(MERLIN_E_INVALID, "splits out of range");
+    if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return fail(MERLIN_E_INVALID, "M, N: multiples of 8");
+    const hipError_t e = merlin::launch_h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits,
+                                                   slab, out, cfg, (hipStream_t)stream);
     if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "M / N not multiples of the tile / bad cfg");
     HIP_TRY(e);
     return MERLIN_OK;

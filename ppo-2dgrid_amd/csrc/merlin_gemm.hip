@@ -769,6 +769,15 @@ hipError_t launch_x6_gemm_nt(const float *A, const void *B, int64_t M, int N, in
 
 int x6_tn_max_splits() { return 64; }
 
+hipError_t launch_x6_fold(const float *slab, int S, int64_t total, float *out, hipStream_t s) {
+    if (total % 4) return hipErrorInvalidValue;
+    const int64_t total4 = total / 4;
+    const int grid = (int)std::min<int64_t>((total4 + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(k_x6_fold, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4 *>(slab), S, total4,
+                       reinterpret_cast<float4 *>(out));
+    return hipGetLastError();
+}
+
 hipError_t launch_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int M, int N, int T, int64_t a_stride,
                              int64_t b_stride, int splits, float *slab, float *out, int cfg, hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;

@@ -1,0 +1,567 @@
+// merlin_h3.hip -- fc1's fp32 GEMMs on the f16 matrix cores in two-plane form ("h3": three f16 products per fp32
+// product; src/actor_critic.py:31-41, the Linear(576, 512) of both towers in PPO.update, src/ppo.py:136-155).
+//
+// Every fp32 operand x of a GEMM is used as x' = x * 2^e (e: one power of two per tensor and tower, from its max
+// |x|, so that max |x'| lies in [2^14, 2^15): inside the f16 range with room to round) and two f16 planes
+//     h = f16(x'),   l = f16((x' - h) * 2^11)          (round to nearest even)
+// x' - h is exact in fp32 and |x' - h| <= 2^-11 |h|, so l lies inside the f16 range too and carries the next 11
+// bits: |x' - (h + l 2^-11)| <= 2^-23 |x'| for every |x'| >= 2^-12 (values within 2^26 of the tensor's max; below
+// that the error is 2^-36 absolute, i.e. 2^-50 of the max).  A product a b is then
+//     a' b' = h_a h_b + 2^-11 (h_a l_b + l_a h_b) + 2^-22 l_a l_b
+// and the GEMM sums the first three on the f16 MFMA (v_mfma_f32_32x32x16_f16: every f16 x f16 product is exact in
+// the fp32 accumulator) into two accumulators -- hi = sum h_a h_b, lo = sum (h_a l_b + l_a h_b) -- combined once in
+// the epilogue, C = (hi + 2^-11 lo) * 2^-(e_A + e_B) (exact power-of-two scalings).  Per product the error is
+// <= ~2^-21 |a b| (the dropped 2^-22 l_a l_b and the planes' rounding), of random sign; per output it stays below
+// the error of the fp32 GEMM on the f32 MFMA (hipBLASLt) on the same operands (tests/test_gpu_h3.py holds it to
+// that against float64).  That is Ootomo & Yokota's fp16 split (IJHPCA 2022) with a per-tensor exponent.
+//
+// Half the matrix-core work of the exact three-plane bf16 form (merlin_gemm.hip, six products) for an error still
+// below the fp32 GEMM's; 4 B of LDS per staged value (two f16 planes) instead of 6.
+//
+// Scales: merlin_h3_amax writes max |x| per tower as float bits (uint32, atomicMax of non-negative floats); the
+// GEMMs read it and derive e in-kernel, so no host round trip.
+#include <algorithm>
+
+#include "merlin_internal.h"
+
+namespace merlin {
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((address_space(3))) char lds_char;
+
+constexpr int BK = 32;           // k per step
+constexpr float LO_SCALE = 2048.0f;
+constexpr float LO_INV = 1.0f / 2048.0f;
+
+__device__ __forceinline__ f32x16 mfma16(const u32x4 a, const u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                   0);
+}
+
+__device__ __forceinline__ float relu_nan(float v) { return v != v ? v : fmaxf(v, 0.0f); }
+
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// the scale exponent e of a tensor whose max |x| has float bits `amax`: max |x| 2^e in [2^14, 2^15)
+__device__ __forceinline__ int h3_exp(uint32_t amax) {
+    if (amax == 0u) return 0;
+    const int e = (int)((amax >> 23) & 0xffu) - 127;  // floor(log2) for a normal max (inf / nan: e = 128)
+    return std::min(std::max(14 - e, -120), 120);
+}
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+
+// an operand scale written by another kernel's atomics: read with a vector load at agent scope (L2-coherent), not
+// through the scalar data cache a wave-uniform load would take
+__device__ __forceinline__ uint32_t load_amax(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// planes of two scaled values: hi word (h of a, h of b), lo word (l of a, l of b)
+__device__ __forceinline__ void h3_pair(float a, float b, uint32_t &hi, uint32_t &lo) {
+    const f16x2 h = f16x2{(_Float16)a, (_Float16)b};
+    const float ra = (a - (float)h.x) * LO_SCALE, rb = (b - (float)h.y) * LO_SCALE;
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, f16x2{(_Float16)ra, (_Float16)rb});
+}
+
+// 8 consecutive values (two float4) scaled by sc -> hi chunk p0, lo chunk p1
+__device__ __forceinline__ void h3_split8(const float4 a, const float4 b, float sc, u32x4 &p0, u32x4 &p1) {
+    uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
+    h3_pair(a.x * sc, a.y * sc, h0, l0);
+    h3_pair(a.z * sc, a.w * sc, h1, l1);
+    h3_pair(b.x * sc, b.y * sc, h2, l2);
+    h3_pair(b.z * sc, b.w * sc, h3, l3);
+    p0 = u32x4{h0, h1, h2, h3};
+    p1 = u32x4{l0, l1, l2, l3};
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// amax[t] = max over the tower's rows x cols of |x| (float bits; the caller zeroes amax)
+__global__ __launch_bounds__(256) void k_h3_amax(const float4 *__restrict__ x, int64_t n4, int64_t s4,
+                                                 uint32_t *__restrict__ amax) {
+    const int t = blockIdx.y;
+    x += t * s4;
+    uint32_t m = 0u;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
+        const float4 v = x[e];
+        m = std::max(m, std::max(std::max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
+                                 std::max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+    }
+    for (int o = 32; o > 0; o >>= 1) m = std::max(m, (uint32_t)__shfl_xor((int)m, o));
+    __shared__ uint32_t red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = std::max(std::max(red[0], red[1]), std::max(red[2], red[3]));
+        if (m) atomicMax(amax + t, m);
+    }
+}
+
+__global__ void k_h3_zero(uint32_t *__restrict__ amax, int T) {
+    if ((int)threadIdx.x < T) amax[threadIdx.x] = 0u;
+}
+
+// planes of a row-major [T][R][C] fp32 tensor: [T][R][C/8][2][8] f16 (per group of 8 values a hi chunk and a lo
+// chunk), each tower scaled by its own 2^e
+__global__ __launch_bounds__(256) void k_h3_split(const float4 *__restrict__ x, int64_t g8, const uint32_t *amax,
+                                                  u32x4 *__restrict__ planes) {
+    const int t = blockIdx.y;
+    const float sc = pow2f(h3_exp(load_amax(amax + t)));
+    x += t * g8 * 2;
+    planes += t * g8 * 2;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < g8; e += (int64_t)gridDim.x * 256) {
+        u32x4 p0, p1;
+        h3_split8(x[2 * e], x[2 * e + 1], sc, p0, p1);
+        planes[2 * e] = p0;
+        planes[2 * e + 1] = p1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// NT: C[t][m][n] = epi(sum_k A[t][m][k] B[t][n][k]); A fp32 [M][K] (split while staged), B h3 planes [N][K/8][2][8]
+// (K % 32 == 0, N % BN == 0); EPI 1: relu(. + bias[t][n]).  grid (tiles_m * tiles_n, T).
+// Block BM x BN, waves WGM x WGN, each wave (BM/WGM) x (BN/WGN) in 32 x 32 MFMA tiles.  LDS plane images: 64-B rows
+// (a k step's 4 chunks of 8 values), chunk g stored at g XOR (row >> 2) & 3 -- a 32x32x16 fragment read (lane l:
+// row l & 31, chunk 2 kh + (l >> 5)) hits 16 distinct 16-B bank slots per ds_read_b128 lane group; B's images padded
+// by 12 chunks so a lane group's 8 staging writes (4 chunks of each plane) land on 8 distinct slots.  Two LDS
+// stages, one barrier per k step, the step after next in registers.
+template <int BM, int BN, int WGM, int WGN, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restrict__ A, const u32x4 *__restrict__ B,
+                                                          const uint32_t *__restrict__ amaxA,
+                                                          const uint32_t *__restrict__ amaxB, int64_t M, int N, int K,
+                                                          int64_t sA, int64_t sB, const float *__restrict__ bias,
+                                                          float *__restrict__ C, int64_t sC, int tiles_n) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int QA = BM * 4, QB = BN * 8;  // A units (row, group of 8 values), B chunks (row, group, plane)
+    constexpr int UA = (QA + NT - 1) / NT, CB = (QB + NT - 1) / NT;
+    static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile of 32 x 32 MFMA tiles");
+    constexpr int PSA = BM * 4, PSB = BN * 4 + 12;
+    constexpr int STAGE = 2 * (PSA + PSB);
+    __shared__ u32x4 lds[2 * STAGE];
+
+    const int t = blockIdx.y;
+    const int L = xcd_tile(blockIdx.x, gridDim.x);
+    const int tm = L / tiles_n, tn = L - tm * tiles_n;
+    const int64_t m0 = (int64_t)tm * BM;
+    const int n0 = tn * BN;
+    const int eA = h3_exp(load_amax(amaxA + t)), eB = h3_exp(load_amax(amaxB + t));
+    const float scA = pow2f(eA);
+    const int64_t rowB = (int64_t)(K / 8) * 2;  // chunks per B row
+    B += t * sB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    const float4 *ga[UA];
+    int la[UA];
+#pragma unroll
+    for (int i = 0; i < UA; i++) {
+        const int q = tid + i * NT;
+        const int row = std::min(q >> 2, BM - 1), g = q & 3;
+        ga[i] = reinterpret_cast<const float4 *>(A + t * sA + std::min<int64_t>(m0 + row, M - 1) * K) + g * 2;
+        la[i] = row * 4 + (g ^ ((row >> 2) & 3));
+    }
+    int gb[CB], lb[CB];
+#pragma unroll
+    for (int i = 0; i < CB; i++) {
+        const int q = tid + i * NT;
+        const int row = std::min(q >> 3, BN - 1), g = (q >> 1) & 3, p = q & 1;
+        gb[i] = (int)((int64_t)(n0 + row) * rowB + g * 2 + p);
+        lb[i] = 2 * PSA + p * PSB + row * 4 + (g ^ ((row >> 2) & 3));
+    }
+    float4 ra[UA][2];
+    u32x4 rb[CB];
+    auto load = [&](int kt) {
+#pragma unroll
+        for (int i = 0; i < UA; i++) {
+            ra[i][0] = ga[i][(int64_t)kt * 8];
+            ra[i][1] = ga[i][(int64_t)kt * 8 + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < CB; i++) rb[i] = B[gb[i] + kt * 8];
+    };
+    auto store = [&](int buf) {
+        u32x4 *st = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < UA; i++)
+            if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
+                u32x4 p0, p1;
+                h3_split8(ra[i][0], ra[i][1], scA, p0, p1);
+                st[la[i]] = p0;
+                st[PSA + la[i]] = p1;
+            }
+#pragma unroll
+        for (int i = 0; i < CB; i++)
+            if (QB % NT == 0 || i + 1 < CB || tid + i * NT < QB) st[lb[i]] = rb[i];
+    };
+
+    f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = f32x16{};
+            lo[i][j] = f32x16{};
+        }
+
+    const int fr = lane & 31, fh = lane >> 5, fs = (fr >> 2) & 3;
+    const int nk = K / BK;
+    load(0);
+    store(0);
+    if (nk > 1) load(1);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) store(buf ^ 1);
+        if (kt + 2 < nk) load(kt + 2);
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 2 * PSA;
+        u32x4 bf[TN][2][2];
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++)
+                    bf[j][kh][p] = sBl[p * PSB + (wn * WTN + j * 32 + fr) * 4 + ((2 * kh + fh) ^ fs)];
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            u32x4 af[2][2];
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++) af[kh][p] = sAl[p * PSA + (wm * WTM + i * 32 + fr) * 4 + ((2 * kh + fh) ^ fs)];
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                f32x16 l = lo[i][j], h = hi[i][j];
+#pragma unroll
+                for (int kh = 0; kh < 2; kh++) {
+                    l = mfma16(af[kh][1], bf[j][kh][0], l);
+                    l = mfma16(af[kh][0], bf[j][kh][1], l);
+                    h = mfma16(af[kh][0], bf[j][kh][0], h);
+                }
+                lo[i][j] = l;
+                hi[i][j] = h;
+            }
+        }
+        __syncthreads();
+    }
+
+    const float inv = pow2f(-eA), invB = pow2f(-eB);
+    float *Ct = C + t * sC;
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+        const int col = n0 + wn * WTN + j * 32 + fr;
+        const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (row < M) {
+                    const float v = (hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB;
+                    Ct[row * N + col] = EPI == 1 ? relu_nan(v + bv) : v;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// TN: slab[s][t][m][n] = sum_{k in split s} A[t][k][m] B[t][k][n], A fp32 [Kd][M], B fp32 [Kd][N] (the weight
+// gradient dz^T a3: both operands row-major over the minibatch's frames), both split while staged into plane
+// images [32 k rows][RC chunks of 8 columns]; fragments k-contiguous through ds_read_b64_tr_b16 (a 32x32x16
+// fragment, lane l: column l & 31, k = 8 (l >> 5) + j, is two transposed reads: 16-lane group g takes columns
+// 16 (g & 1) .. + 15 and k rows 8 (g >> 1) + 4 h2 .. + 3).  Chunk c of row r sits at r RC + (c ^ swz(r)): the 16
+// chunks a 32-lane half reads (4 rows x 4 adjacent chunks) land on 16 distinct 16-B bank slots for RC = 16 (XOR
+// 4 (r & 3)) and RC = 24 (XOR 4 ((r >> 1) & 1)).  Slabs are written already unscaled (x 2^-(eA + eB), exact).
+template <int RC>
+__device__ __forceinline__ int tr_swz(int row) {
+    static_assert(RC % 16 == 0 || RC == 24, "row chunks");
+    return RC % 16 == 0 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
+}
+
+template <int RC>
+__device__ __forceinline__ u32x4 tr_frag(const u32x4 *img, int col0, int kh, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int chunk = ((col0 + 16 * (g & 1)) >> 3) + (p >> 1);
+    bf16x4 v[2];  // 16-bit lanes moved as bits (the planes are f16)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; h2++) {
+        const int row = 16 * kh + 8 * (g >> 1) + 4 * h2 + q;
+        const int off = (row * RC + (chunk ^ tr_swz<RC>(row))) * 16 + (p & 1) * 8;
+        v[h2] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4 *)((lds_char *)img + off));
+    }
+    return __builtin_bit_cast(u32x4, bf16x8{v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]});
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restrict__ A, const float4 *__restrict__ B,
+                                                          const uint32_t *__restrict__ amaxA,
+                                                          const uint32_t *__restrict__ amaxB, int64_t Kd, int M, int N,
+                                                          int64_t sA, int64_t sB, int64_t kc, int tiles_n, int tiles,
+                                                          int S, float *__restrict__ slab) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int RCA = BM / 8, RCB = BN / 8;
+    constexpr int QA = BK * RCA, QB = BK * RCB;  // units (k row, group of 8 columns) per k step
+    constexpr int UA = (QA + NT - 1) / NT, UB = (QB + NT - 1) / NT;
+    static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile of 32 x 32 MFMA tiles");
+    constexpr int PSA = BK * RCA, PSB = BK * RCB;
+    constexpr int STAGE = 2 * (PSA + PSB);
+    __shared__ u32x4 lds[2 * STAGE];
+
+    // 1-D grid over (tower, split, tile), tile fastest, XCD-contiguous: the tiles of one split read the same k rows
+    const int P = xcd_tile(blockIdx.x, gridDim.x);
+    const int t = P / (S * tiles), s = (P / tiles) % S, Lt = P % tiles;
+    const int tm = Lt / tiles_n, tn = Lt - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int64_t k0 = (int64_t)s * kc, k1 = std::min<int64_t>(Kd, k0 + kc);
+    const int eA = h3_exp(load_amax(amaxA + t)), eB = h3_exp(load_amax(amaxB + t));
+    const float scA = pow2f(eA), scB = pow2f(eB);
+    const int64_t rowA = M / 4, rowB = N / 4;
+    A += t * sA + m0 / 4;
+    B += t * sB + n0 / 4;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    int ka[UA], la[UA], kb[UB], lb[UB];
+    const float4 *pa[UA], *pb[UB];
+#pragma unroll
+    for (int i = 0; i < UA; i++) {
+        const int q = std::min(tid + i * NT, QA - 1);
+        const int k = q / RCA, g = q - (q / RCA) * RCA;
+        ka[i] = k;
+        la[i] = k * RCA + (g ^ tr_swz<RCA>(k));
+        pa[i] = A + (k0 + k) * rowA + g * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < UB; i++) {
+        const int q = std::min(tid + i * NT, QB - 1);
+        const int k = q / RCB, g = q - (q / RCB) * RCB;
+        kb[i] = k;
+        lb[i] = 2 * PSA + k * RCB + (g ^ tr_swz<RCB>(k));
+        pb[i] = B + (k0 + k) * rowB + g * 2;
+    }
+    const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float4 ra[UA][2], rb[UB][2];
+    auto load = [&](int64_t kk) {
+        if (kk + BK <= k1) {  // full step: row pointers + a wave-uniform offset
+            const int64_t da = (kk - k0) * rowA, db = (kk - k0) * rowB;
+#pragma unroll
+            for (int i = 0; i < UA; i++) {
+                ra[i][0] = pa[i][da];
+                ra[i][1] = pa[i][da + 1];
+            }
+#pragma unroll
+            for (int i = 0; i < UB; i++) {
+                rb[i][0] = pb[i][db];
+                rb[i][1] = pb[i][db + 1];
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < UA; i++) {  // a split's last step: rows past k1 re-read row k1 - 1, zeroed when staged
+            const float4 *src = pa[i] + (std::min(kk + ka[i], k1 - 1) - k0 - ka[i]) * rowA;
+            ra[i][0] = src[0];
+            ra[i][1] = src[1];
+        }
+#pragma unroll
+        for (int i = 0; i < UB; i++) {
+            const float4 *src = pb[i] + (std::min(kk + kb[i], k1 - 1) - k0 - kb[i]) * rowB;
+            rb[i][0] = src[0];
+            rb[i][1] = src[1];
+        }
+    };
+    auto store = [&](int buf, int64_t kk) {
+        u32x4 *st = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < UA; i++)
+            if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
+                const bool in = kk + ka[i] < k1;
+                u32x4 p0, p1;
+                h3_split8(in ? ra[i][0] : zero, in ? ra[i][1] : zero, scA, p0, p1);
+                st[la[i]] = p0;
+                st[PSA + la[i]] = p1;
+            }
+#pragma unroll
+        for (int i = 0; i < UB; i++)
+            if (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB) {
+                const bool in = kk + kb[i] < k1;
+                u32x4 p0, p1;
+                h3_split8(in ? rb[i][0] : zero, in ? rb[i][1] : zero, scB, p0, p1);
+                st[lb[i]] = p0;
+                st[PSB + lb[i]] = p1;
+            }
+    };
+
+    f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = f32x16{};
+            lo[i][j] = f32x16{};
+        }
+
+    if (k0 < k1) {
+        load(k0);
+        store(0, k0);
+        if (k0 + BK < k1) load(k0 + BK);
+        __syncthreads();
+    }
+    int buf = 0;
+    for (int64_t kk = k0; kk < k1; kk += BK, buf ^= 1) {
+        if (kk + BK < k1) store(buf ^ 1, kk + BK);
+        if (kk + 2 * BK < k1) load(kk + 2 * BK);
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 2 * PSA;
+        u32x4 af[TM][2][2];
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++) af[i][kh][p] = tr_frag<RCA>(sAl + p * PSA, wm * WTM + i * 32, kh, lane);
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            u32x4 bf[2][2];
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++) bf[kh][p] = tr_frag<RCB>(sBl + p * PSB, wn * WTN + j * 32, kh, lane);
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                f32x16 l = lo[i][j], h = hi[i][j];
+#pragma unroll
+                for (int kh = 0; kh < 2; kh++) {
+                    l = mfma16(af[i][kh][1], bf[kh][0], l);
+                    l = mfma16(af[i][kh][0], bf[kh][1], l);
+                    h = mfma16(af[i][kh][0], bf[kh][0], h);
+                }
+                lo[i][j] = l;
+                hi[i][j] = h;
+            }
+        }
+        __syncthreads();
+    }
+
+    const float inv = pow2f(-eA), invB = pow2f(-eB);
+    float *St = slab + ((int64_t)s * (gridDim.x / (S * tiles)) + t) * (int64_t)M * N;
+    const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                St[(int64_t)row * N + n0 + wn * WTN + j * 32 + fr] =
+                    (hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB;
+            }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
+                     int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
+    if (N % BN) return hipErrorInvalidValue;
+    if ((int64_t)N * (K / 8) * 2 > INT32_MAX) return hipErrorInvalidValue;  // 32-bit B chunk offsets
+    const int64_t tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = N / BN;
+    if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(tiles_m * tiles_n), T);
+    if (bias)
+        hipLaunchKernelGGL((k_h3_nt<BM, BN, WGM, WGN, 1>), grid, dim3(64 * WGM * WGN), 0, s, A, B, amaxA, amaxB, M, N,
+                           K, sA, sB, bias, C, sC, tiles_n);
+    else
+        hipLaunchKernelGGL((k_h3_nt<BM, BN, WGM, WGN, 0>), grid, dim3(64 * WGM * WGN), 0, s, A, B, amaxA, amaxB, M, N,
+                           K, sA, sB, nullptr, C, sC, tiles_n);
+    return hipGetLastError();
+}
+
+template <int BM, int BN, int WGM, int WGN>
+hipError_t tn_launch(const float *A, const float *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t Kd, int M,
+                     int N, int T, int64_t sA, int64_t sB, int splits, float *slab, int *S_out, hipStream_t s) {
+    if (M % BM || N % BN) return hipErrorInvalidValue;
+    const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
+    int S = std::max(1, splits);
+    int64_t kc = (Kd + S - 1) / S;
+    kc = (kc + BK - 1) / BK * BK;
+    S = (int)std::max<int64_t>(1, (Kd + kc - 1) / kc);
+    *S_out = S;
+    hipLaunchKernelGGL((k_h3_tn<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
+                       reinterpret_cast<const float4 *>(A), reinterpret_cast<const float4 *>(B), amaxA, amaxB, Kd, M,
+                       N, sA / 4, sB / 4, kc, tiles_n, tiles, S, slab);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_h3_amax(const float *x, int64_t n, int T, int64_t stride, uint32_t *amax, hipStream_t s) {
+    // zeroed by a kernel, not hipMemsetAsync: this runs inside the fast step's captured forward graph, and a
+    // captured memset node replays with a wrong fill value on ROCm 7 (scripts/probe_graph_then.py: 0x80808080)
+    hipLaunchKernelGGL(k_h3_zero, dim3(1), dim3(64), 0, s, amax, T);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || n <= 0) return e;
+    if (n % 4 || stride % 4) return hipErrorInvalidValue;
+    const int64_t n4 = n / 4;
+    const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_h3_amax, dim3(grid, T), dim3(256), 0, s, reinterpret_cast<const float4 *>(x), n4, stride / 4,
+                       amax);
+    return hipGetLastError();
+}
+
+hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *amax, void *planes, hipStream_t s) {
+    if (n % 8) return hipErrorInvalidValue;
+    if (n <= 0) return hipSuccess;
+    const int64_t g8 = n / 8;
+    const int grid = (int)std::min<int64_t>((g8 + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_h3_split, dim3(grid, T), dim3(256), 0, s, reinterpret_cast<const float4 *>(x), g8, amax,
+                       static_cast<u32x4 *>(planes));
+    return hipGetLastError();
+}
+
+hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
+                             int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
+                             int64_t c_stride, int cfg, hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    if (K % BK || N <= 0 || a_stride % 4 || b_stride % 8) return hipErrorInvalidValue;
+    const u32x4 *b = static_cast<const u32x4 *>(B);
+    const int64_t sB = b_stride / 8 * 2;  // chunks
+    switch (cfg) {
+        case 0: return nt_launch<256, 128, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        case 1: return nt_launch<128, 192, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        case 2: return nt_launch<128, 128, 2, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        case 3: return nt_launch<128, 256, 2, 4>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_h3_gemm_tn(const float *A, const uint32_t *amaxA, const float *B, const uint32_t *amaxB, int64_t Kd,
+                             int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits, float *slab,
+                             float *out, int cfg, hipStream_t s) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
+    if (Kd <= 0) return hipMemsetAsync(out, 0, sizeof(float) * (size_t)T * M * N, s);
+    int S = 1;
+    hipError_t e;
+    switch (cfg) {
+        case 0: e = tn_launch<128, 192, 4, 2>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s); break;
+        case 1: e = tn_launch<128, 192, 2, 2>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    if (e != hipSuccess) return e;
+    return launch_x6_fold(slab, S, (int64_t)T * M * N, out, s);
+}
+
+}  // namespace merlin

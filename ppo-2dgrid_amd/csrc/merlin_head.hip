@@ -144,7 +144,7 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
                                                    const float *__restrict__ dvalue, const float4 *__restrict__ wa,
                                                    const float4 *__restrict__ wc, int64_t n, int H4, int A,
                                                    int64_t per, float4 *__restrict__ dz,
-                                                   float4 *__restrict__ partials) {
+                                                   float4 *__restrict__ partials, uint32_t *__restrict__ amax) {
     __shared__ float4 red[EBLK];
     const int t = blockIdx.y, R = EBLK / H4;
     const int c = threadIdx.x % H4, r0 = threadIdx.x / H4;
@@ -156,6 +156,7 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
         accw[j] = f4_zero();
     }
     float4 acc = f4_zero();
+    uint32_t mz = 0u;  // max |dz| of the block as float bits (merlin_h3.hip's operand scale)
     const int64_t lo = (int64_t)blockIdx.x * per, hi = std::min<int64_t>(n, lo + per);
     const size_t base = (size_t)t * n * H4;
     // HEAD_ROWS rows per thread per round, all their loads issued before any is used (rows past the
@@ -193,7 +194,13 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
             const float4 o = f4_mask(hv[k], g);
             dz[base + (size_t)(r + k * R) * H4 + c] = o;
             f4_add(acc, o);
+            mz = std::max(mz, std::max(std::max(__float_as_uint(o.x) & 0x7fffffffu, __float_as_uint(o.y) & 0x7fffffffu),
+                                       std::max(__float_as_uint(o.z) & 0x7fffffffu, __float_as_uint(o.w) & 0x7fffffffu)));
         }
+    }
+    if (amax) {  // block-uniform
+        const uint32_t mx[2] = {t == 0 ? mz : 0u, t == 1 ? mz : 0u};
+        block_amax2(mx, 2, amax);
     }
     float4 *dst = partials + ((size_t)t * gridDim.x + blockIdx.x) * (size_t)(1 + A) * H4;
 #pragma unroll
@@ -348,7 +355,7 @@ hipError_t launch_colsum(const float *X, int64_t rows, int cols, int64_t row_str
 
 hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
                            const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
-                           float *work, hipStream_t s) {
+                           float *work, uint32_t *amax, hipStream_t s) {
     if (n <= 0) {
         hipError_t e = hipMemsetAsync(db4, 0, sizeof(float) * 2 * H, s);
         if (e == hipSuccess) e = hipMemsetAsync(dwa, 0, sizeof(float) * A * H, s);
@@ -359,7 +366,7 @@ hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dv
     hipLaunchKernelGGL(A <= 3 ? k_head_bwd<3> : k_head_bwd<MAXA>, dim3(nblk, 2), dim3(EBLK), 0, s,
                        reinterpret_cast<const float4 *>(h), dlogits, dvalue, reinterpret_cast<const float4 *>(wa),
                        reinterpret_cast<const float4 *>(wc), n, H / 4, A, per, reinterpret_cast<float4 *>(dz),
-                       reinterpret_cast<float4 *>(work));
+                       reinterpret_cast<float4 *>(work), amax);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int total = (1 + A) * H + 2 * H;

@@ -105,7 +105,7 @@ hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *d
 
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                               const float *b3, int T, float *Y3, uint64_t *bits, hipStream_t s);
+                               const float *b3, int T, float *Y3, uint64_t *bits, uint32_t *amax, hipStream_t s);
 hipError_t launch_act_heads(const float *z, const float *b4, int64_t n, int H, const float *wa, const float *ba,
                             const float *wc, const float *bc, int A, int det, uint64_t seed, const int64_t *epoch,
                             int64_t step, int64_t env_offset, int64_t *action, float *logp, float *value,
@@ -148,7 +148,28 @@ hipError_t launch_colsum(const float *X, int64_t rows, int cols, int64_t row_str
                          float *out, float *work, hipStream_t s);
 hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
                            const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
-                           float *work, hipStream_t s);
+                           float *work, uint32_t *amax, hipStream_t s);
+
+// atomicMax of each tower's block maximum (float bits of non-negative values) into amax[t], t < T <= 2; every
+// thread of the 256-thread block calls it
+__device__ __forceinline__ void block_amax2(const uint32_t mx[2], int T, uint32_t *amax) {
+    __shared__ uint32_t red[2][4];
+    uint32_t m0 = mx[0], m1 = mx[1];
+    for (int o = 32; o > 0; o >>= 1) {
+        m0 = max(m0, (uint32_t)__shfl_xor((int)m0, o));
+        m1 = max(m1, (uint32_t)__shfl_xor((int)m1, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = m0;
+        red[1][threadIdx.x >> 6] = m1;
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)T) {
+        const uint32_t *r = red[threadIdx.x];
+        const uint32_t m = max(max(r[0], r[1]), max(r[2], r[3]));
+        if (m) atomicMax(amax + threadIdx.x, m);
+    }
+}
 
 // fc1 on the bf16 matrix cores in exact three-plane form (merlin_gemm.hip, merlin_x6.h)
 hipError_t launch_x6_split(const float *x, int64_t n, void *planes, hipStream_t s);
@@ -158,6 +179,17 @@ hipError_t launch_x6_gemm_nt(const float *A, const void *B, int64_t M, int N, in
 hipError_t launch_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int M, int N, int T, int64_t a_stride,
                              int64_t b_stride, int splits, float *slab, float *out, int cfg, hipStream_t s);
 int x6_tn_max_splits();
+// out[e] = sum over s < S of slab[s][e], in slab order (total % 4 == 0)
+hipError_t launch_x6_fold(const float *slab, int S, int64_t total, float *out, hipStream_t s);
+// fc1 on the f16 matrix cores in two-plane form (merlin_h3.hip)
+hipError_t launch_h3_amax(const float *x, int64_t n, int T, int64_t stride, uint32_t *amax, hipStream_t s);
+hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *amax, void *planes, hipStream_t s);
+hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
+                             int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
+                             int64_t c_stride, int cfg, hipStream_t s);
+hipError_t launch_h3_gemm_tn(const float *A, const uint32_t *amaxA, const float *B, const uint32_t *amaxB, int64_t Kd,
+                             int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits, float *slab,
+                             float *out, int cfg, hipStream_t s);
 
 // clip_grad_norm_ + Adam step over a parameter list (merlin_optim.hip)
 constexpr int OPT_MAX_TENSORS = 32;

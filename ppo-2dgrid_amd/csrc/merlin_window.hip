@@ -69,8 +69,10 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
                                                       const int32_t *__restrict__ wid,
                                                       const int64_t *__restrict__ groups, int64_t n,
                                                       const float4 *__restrict__ b3, int T,
-                                                      float4 *__restrict__ Y3, uint64_t *__restrict__ bits) {
+                                                      float4 *__restrict__ Y3, uint64_t *__restrict__ bits,
+                                                      uint32_t *__restrict__ amax) {
     const int64_t total = (int64_t)T * n * 9 * 16;
+    uint32_t mx[2] = {0u, 0u};  // max |Y3| per tower as float bits (merlin_h3.hip's operand scale)
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
         const int c = (int)(e & 15);
         const int64_t r = e >> 4, tu = r / 9;
@@ -92,6 +94,12 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
         const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
                                      relu_nan(acc.w + b.w));
         Y3[e] = y;
+        if (amax) {
+            const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
+                                        std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
+            if (t == 0) mx[0] = std::max(mx[0], m);
+            else mx[1] = std::max(mx[1], m);
+        }
         if (bits) {
             uint64_t v = (uint64_t)((y.x > 0.0f ? 1u : 0u) | (y.y > 0.0f ? 2u : 0u) | (y.z > 0.0f ? 4u : 0u) |
                                     (y.w > 0.0f ? 8u : 0u))
@@ -101,6 +109,7 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
             if (c == 0) bits[r] = v;
         }
     }
+    if (amax) block_amax2(mx, T, amax);
 }
 
 // The acting path's conv3 from a table over EVERY possible 3x3 tile window (5^9 = 1,953,125 rows, built
@@ -362,12 +371,13 @@ hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, 
 }
 
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                               const float *b3, int T, float *Y3, uint64_t *bits, hipStream_t s) {
+                               const float *b3, int T, float *Y3, uint64_t *bits, uint32_t *amax, hipStream_t s) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
     hipLaunchKernelGGL(k_window_conv3, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4 *>(Q), nw, wid,
-                       groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), bits);
+                       groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), bits,
+                       amax);
     return hipGetLastError();
 }
 

@@ -96,7 +96,7 @@ def lib():
     L.merlin_tower_conv2_lut_bwd_grouped.argtypes = [vp, i64, vp, vp, i32, vp, vp, vp]
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
-    L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp]
+    L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp]
     L.merlin_tower_all_windows.restype = i64
     L.merlin_tower_codes_conv3.argtypes = [vp, i64, vp, vp, i32, vp, vp]
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
@@ -108,7 +108,7 @@ def lib():
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_colsum.argtypes = [vp, i64, i32, i64, i64, i32, vp, vp]
-    L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]
+    L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]
     L.merlin_act_heads.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp,
                                    vp]
     L.merlin_ppo_loss_workspace.argtypes = [i64]
@@ -125,6 +125,10 @@ def lib():
     L.merlin_x6_tn_slab_floats.argtypes = [i32, i32, i32, i32]
     L.merlin_x6_tn_slab_floats.restype = i64
     L.merlin_x6_gemm_tn.argtypes = [vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
+    L.merlin_h3_amax.argtypes = [vp, i64, i32, i64, vp, vp]
+    L.merlin_h3_split.argtypes = [vp, i64, i32, vp, vp, vp]
+    L.merlin_h3_gemm_nt.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, i32, vp]
+    L.merlin_h3_gemm_tn.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
     L.merlin_stage_tables_fwd.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_stage_tables_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     check_env_config_layout(L)
@@ -168,6 +172,7 @@ EXPORTED_SYMBOLS = (
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
     "merlin_clip_adam_workspace", "merlin_clip_adam",
+    "merlin_h3_amax", "merlin_h3_split", "merlin_h3_gemm_nt", "merlin_h3_gemm_tn",
 )
 
 
@@ -535,11 +540,12 @@ def window_lut(rows, tables):
     return out
 
 
-def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None):
+def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None, amax=None):
     """Y3 f32[T, n*9, 64] = relu(conv3) rows (k, p3) of frames groups[k] from
     Q f32[T, nw, 576], the per-window, per-tap conv3 partial sums (merlin/windows.py).
     bits: also return the rows' ReLU masks, int64[T, n*9] (bit co = Y3 > 0).  rows >= n: the
-    outputs hold `rows` frames, those past n zero (Y3) / unwritten (bits)."""
+    outputs hold `rows` frames, those past n zero (Y3) / unwritten (bits).  amax (with bits): int32[T],
+    zeroed by the caller, receives max |Y3| per tower as float bits (h3_amax's format)."""
     T, nw = int(Q.shape[0]), int(Q.shape[1])
     n = int(groups.numel())
     R = n if rows is None else int(rows)
@@ -554,7 +560,8 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
         mask = torch.empty((T, R * 9), dtype=torch.int64, device=Q.device)
         with KernelTimer.span("k_window_conv3", T * n * 9 * 264 + n * 108 + T * nw * 576 * 4):
             check(lib().merlin_tower_window_conv3_bits(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
-                                                       ptr(mask), stream_of(Q)), "merlin_tower_window_conv3_bits")
+                                                       ptr(mask), ptr(amax), stream_of(Q)),
+                  "merlin_tower_window_conv3_bits")
         return out, mask
     with KernelTimer.span("k_window_conv3", T * n * 9 * 256 + n * 108 + T * nw * 576 * 4):
         check(lib().merlin_tower_window_conv3(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
@@ -684,11 +691,12 @@ def heads_fwd(h: torch.Tensor, w_actor: torch.Tensor, w_critic: torch.Tensor, b_
     return logits, value
 
 
-def head_bwd(h, dlogits, dvalue, w_actor, w_critic, out_bias=None, out_w_actor=None, out_w_critic=None):
+def head_bwd(h, dlogits, dvalue, w_actor, w_critic, out_bias=None, out_w_actor=None, out_w_critic=None, amax=None):
     """Heads backward through fc1's ReLU: h f32[2, n, H] = relu(fc1) of both towers, dlogits
     f32[n, A], dvalue f32[n], w_actor f32[A, H], w_critic f32[1, H] or [H] ->
     (dz f32[2, n, H], dbias f32[2, H], dw_actor f32[A, H], dw_critic f32[H]); the out_* tensors, when
-    given, receive the bias / head-weight gradients (e.g. views of a flat gradient buffer)."""
+    given, receive the bias / head-weight gradients (e.g. views of a flat gradient buffer).  amax int32[2], zeroed by
+    the caller, receives max |dz| per tower as float bits (h3_amax's format)."""
     _, n, H = (int(x) for x in h.shape)
     A = int(w_actor.shape[0])
     assert h.shape[0] == 2 and dlogits.shape == (n, A) and dvalue.numel() == n and w_critic.numel() == H
@@ -700,7 +708,8 @@ def head_bwd(h, dlogits, dvalue, w_actor, w_critic, out_bias=None, out_w_actor=N
     assert db.is_contiguous() and dwa.is_contiguous() and dwc.is_contiguous()
     with KernelTimer.span("k_head_bwd", 2 * h.numel() * 4 + n * (A + 1) * 4):
         check(lib().merlin_tower_head_bwd(ptr(h), ptr(dlogits), ptr(dvalue), ptr(w_actor), ptr(w_critic), n, H, A,
-                                          ptr(dz), ptr(db), ptr(dwa), ptr(dwc), stream_of(h)), "merlin_tower_head_bwd")
+                                          ptr(dz), ptr(db), ptr(dwa), ptr(dwc), ptr(amax), stream_of(h)),
+              "merlin_tower_head_bwd")
     return dz, db, dwa, dwc
 
 
@@ -861,6 +870,80 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
     with KernelTimer.span(name, 0, 2 * T * M * N * Kd):
         check(lib().merlin_x6_gemm_tn(ptr(A), ptr(B), Kd, M, N, T, Kd * M, Kd * N, int(splits), ptr(slab), ptr(out),
                                       int(cfg), stream_of(A)), "merlin_x6_gemm_tn")
+    return out
+
+
+# -- fc1 on the f16 matrix cores in two-plane form (csrc/merlin_h3.hip) ----------------------------------------
+H3_NT_CFG = {"fwd": 0, "dgrad": 1, "rollout": 2}  # tile configurations of merlin_h3_gemm_nt (N = 512 / 576)
+H3_TN_CFG = 0
+H3_TN_SPLITS = 32
+
+
+def h3_amax(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """int32[T] (uint32 float bits) of max |x| per tower, x f32[T, ...] contiguous (numel per tower % 4 == 0)."""
+    assert x.dtype == torch.float32 and x.is_contiguous()
+    T = int(x.shape[0])
+    n = x.numel() // max(T, 1)
+    if out is None:
+        out = torch.empty(T, dtype=torch.int32, device=x.device)
+    assert out.dtype == torch.int32 and out.numel() >= T and out.is_contiguous()
+    with KernelTimer.span("k_h3_amax", 4 * T * n):
+        check(lib().merlin_h3_amax(ptr(x), n, T, n, ptr(out), stream_of(x)), "merlin_h3_amax")
+    return out
+
+
+def h3_split(x: torch.Tensor, amax: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 [T, ..., C] -> f16 planes as int16 [T, ..., 2C] ([..., C/8, 2, 8]: hi and lo chunk per 8 values),
+    tower t scaled by the exponent of amax[t] (h3_amax)."""
+    assert x.dtype == torch.float32 and x.shape[-1] % 8 == 0 and amax.dtype == torch.int32
+    x = x.contiguous()
+    T = int(x.shape[0])
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (2 * x.shape[-1],), dtype=torch.int16, device=x.device)
+    check(lib().merlin_h3_split(ptr(x), x.numel() // T, T, ptr(amax), ptr(out), stream_of(x)), "merlin_h3_split")
+    return out
+
+
+def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,
+               bias: torch.Tensor | None = None, cfg: int = 0, out: torch.Tensor | None = None,
+               name: str = "h3_gemm_nt") -> torch.Tensor:
+    """C f32[T, M, N] = A @ B^T per tower (+ bias[t] and ReLU when bias is given), A f32[T, M, K] with its h3_amax,
+    B planes int16[T, N, 2K] (h3_split of an f32 [T, N, K] with amaxB)."""
+    T, M, K = (int(v) for v in A.shape)
+    N = int(B.shape[1])
+    assert A.dtype == torch.float32 and B.dtype == torch.int16 and B.shape == (T, N, 2 * K)
+    assert A.is_contiguous() and B.is_contiguous() and amaxA.dtype == amaxB.dtype == torch.int32
+    if out is None:
+        out = torch.empty((T, M, N), dtype=torch.float32, device=A.device)
+    assert out.shape == (T, M, N) and out.is_contiguous()
+    if bias is not None:
+        assert bias.shape == (T, N) and bias.is_contiguous()
+    with KernelTimer.span(name, 0, 2 * T * M * N * K):
+        check(lib().merlin_h3_gemm_nt(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, T, M * K, N * K,
+                                      ptr(bias) if bias is not None else None, ptr(out), M * N, int(cfg),
+                                      stream_of(A)), "merlin_h3_gemm_nt")
+    return out
+
+
+def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,
+               splits: int | None = None, cfg: int | None = None, name: str = "h3_gemm_tn",
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """out f32[T, M, N] = A^T @ B per tower, A f32[T, Kd, M], B f32[T, Kd, N] with their h3_amax (the long k range
+    split into `splits` slabs summed in order)."""
+    splits = H3_TN_SPLITS if splits is None else splits
+    cfg = H3_TN_CFG if cfg is None else cfg
+    T, Kd, M = (int(v) for v in A.shape)
+    N = int(B.shape[2])
+    assert A.dtype == B.dtype == torch.float32 and B.shape[:2] == (T, Kd)
+    assert A.is_contiguous() and B.is_contiguous() and amaxA.dtype == amaxB.dtype == torch.int32
+    if out is None:
+        out = torch.empty((T, M, N), dtype=torch.float32, device=A.device)
+    assert out.shape == (T, M, N) and out.dtype == torch.float32 and out.is_contiguous()
+    slab = torch.empty(int(lib().merlin_x6_tn_slab_floats(M, N, T, int(splits))), dtype=torch.float32,
+                       device=A.device)
+    with KernelTimer.span(name, 0, 2 * T * M * N * Kd):
+        check(lib().merlin_h3_gemm_tn(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), Kd, M, N, T, Kd * M, Kd * N,
+                                      int(splits), ptr(slab), ptr(out), int(cfg), stream_of(A)), "merlin_h3_gemm_tn")
     return out
 
 

@@ -372,9 +372,11 @@ class CNNActorCritic(nn.Module):
         # "lut2": conv1+conv2 as table lookups, conv3/fc as hipBLASLt GEMMs (default)
         # "gemm": conv1 lookups, conv2/conv3/fc as GEMMs | "lut_nchw": conv1 lookups + MIOpen convs
         self.codes_impl = "lut2"
-        # fc1 of the update (heads_windows): "x6" = fp32 products on the bf16 matrix cores in exact
-        # three-plane form (csrc/merlin_gemm.hip); "hipblaslt" = torch's fp32 GEMMs
-        self.fc1_impl = "x6"
+        # fc1 of the update (heads_windows): "h3" = fp32-class products on the f16 matrix cores in two-plane
+        # form, three products each, error below hipBLASLt's fp32 GEMM (csrc/merlin_h3.hip); "x6" = exact fp32
+        # products on the bf16 matrix cores in three-plane form, six products (csrc/merlin_gemm.hip);
+        # "hipblaslt" = torch's fp32 GEMMs
+        self.fc1_impl = "h3"
 
     # -- tile-code path (GPU envs) --------------------------------------------------
     def _atlas_on(self, device):
@@ -544,7 +546,7 @@ class CNNActorCritic(nn.Module):
             pack["b2"] = torch.stack([ea[2].bias, ec[2].bias]).contiguous()
             # im2col rows of A3 are (ky, kx, ci): conv3 weights as [2, 576, 64] in that order
             pack["W3t"] = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64).contiguous()
-        if self.fc1_impl == "x6":  # fc1 of every step on the bf16 MFMA, fp32 products (merlin_gemm.hip)
+        if self.fc1_impl in ("x6", "h3"):  # fc1 of every step on the bf16 MFMA, exact fp32 products (merlin_gemm2.hip)
             pack["W4pp"] = nat.x6_split(W4p.contiguous())
         else:
             pack["W4t"] = W4p.transpose(1, 2).contiguous()
@@ -612,7 +614,7 @@ class CNNActorCritic(nn.Module):
         from .gemm_tuning import padded_rows
         from .windows import tower_conv3, window_tower_head_x6
 
-        if self.fc1_impl == "x6":
+        if self.fc1_impl in ("x6", "h3"):
             return window_tower_head_x6(self, plan, mb, head_bias)
         n = int(mb.groups.numel())
         npad = padded_rows(n)  # fc1's rows on a tuned GEMM shape (merlin/gemm_tuning.py); zero rows past n

@@ -1,4 +1,4 @@
-"""PPO.update's minibatch step on the window + x6 path with the launch sequence written out
+"""PPO.update's minibatch step on the window path (fc1 on the h3 or x6 GEMMs) with the launch sequence written out
 (src/ppo.py:136-156: forward, loss, backward, clip_grad_norm_(0.5), Adam).
 
 The autograd engine walked ~95 kernels per optimizer step, ~60 of them small torch ops, and the host
@@ -7,8 +7,8 @@ waiting for the host (scripts/busy_union.py on a rocprofv3 kernel trace: 67-75 m
 Here the step is the same kernels with the same operands in the same order, issued directly:
 
   * WeightStage -- everything that depends on the parameters alone (the conv1 / conv2 tables T2,
-    the stacked and permuted conv3 / fc1 weights, fc1's x6 planes for the forward and the input
-    gradient) is one captured HIP graph, and the backward of that subgraph (the table / stacking
+    the stacked and permuted conv3 / fc1 weights, fc1's weight planes (and their scale) for the forward and the
+    input gradient) is one captured HIP graph, and the backward of that subgraph (the table / stacking
     adjoints down to every parameter's gradient, written into a flat gradient buffer) a second one.
     Parameters keep their storage for the whole run (the optimizer updates them in place), so the
     graphs replay on live weights.
@@ -59,8 +59,12 @@ class WeightStage:
     gradients the step wrote into self.grads (db2, dW3r, db3, dW4p, db4: views of the derived-gradient buffer),
     and scatters the whole buffer onto the stage parameters' slots of the flat gradient (one launch)."""
 
-    def __init__(self, ac, flat_params: torch.Tensor, flat_grad: torch.Tensor, impl: str = "hip"):
+    def __init__(self, ac, flat_params: torch.Tensor, flat_grad: torch.Tensor, impl: str = "hip", fc1: str = "h3"):
         self.ac = ac
+        # fc1's GEMM form: "h3" (f16 two-plane; the weight planes' per-tower scale amaxW is computed by this graph,
+        # the activations' by the step's producer kernels, merlin.fast_step.WindowStep.step) or "x6" (bf16
+        # three-plane)
+        self.fc1 = fc1
         # "hip": T2 and its adjoint by csrc/merlin_stage.hip (2 launches each way); "torch": the same tables by
         # CNNActorCritic.conv2_tables_from and autograd (the autograd path's exact arithmetic)
         self.impl = impl
@@ -88,6 +92,7 @@ class WeightStage:
             self.shapes[name], self.offs[name] = tuple(t.shape), o
             o += t.numel()
         dev = flat_params.device
+        self.amaxW = torch.zeros(2, dtype=torch.int32, device=dev)
         self.fwd_map = torch.cat([t.reshape(-1) for _, t in segs]).to(dev)
         self.n_grad = self.offs["W4pT"]  # every stage-parameter element once in D[:n_grad]
         assert int(self.fwd_map[:self.n_grad].unique().numel()) == self.n_grad
@@ -111,8 +116,12 @@ class WeightStage:
             leaves = W1, b1, W2 = tuple(self.seg(D, k).requires_grad_() for k in ("W1", "b1", "W2"))
             T2 = self.ac.conv2_tables_from(W1, b1, W2)
         o = self.offs["W4p"]
-        planes = nat.x6_split(D[o:].view(-1, 8)).view(-1)  # W4p and W4p^T back to back
         H = self.shapes["W4p"][1]
+        if self.fc1 == "h3":
+            W4p, W4pT = self.seg(D, "W4p"), self.seg(D, "W4pT")
+            nat.h3_amax(W4p, out=self.amaxW)  # W4p^T holds the same values: one scale for both
+            return D, leaves, T2, (nat.h3_split(W4p, self.amaxW), nat.h3_split(W4pT, self.amaxW))
+        planes = nat.x6_split(D[o:].view(-1, 8)).view(-1)  # W4p and W4p^T back to back
         n4 = 2 * H * 576 * 3
         return D, leaves, T2, (planes[:n4].view(2, H, 3 * 576), planes[n4:].view(2, 576, 3 * H))
 
@@ -170,6 +179,7 @@ class WeightStage:
 # fc1's weight gradient on the side stream from right after the heads' backward (True: beside the input gradient
 # too) or from after the input gradient (False: beside conv3's segmented sums only)
 WGRAD_EARLY = False
+WGRAD_SIDE = True  # False: the weight gradient on the main stream (diagnostics)
 
 
 class WindowStep:
@@ -198,12 +208,17 @@ class WindowStep:
             views[p] = flat[off:off + n].view_as(p)
             off += n
         self.flat, self.views = flat, views
-        self.stage = WeightStage(ac, flat_params, flat, impl=getattr(agent, "stage_impl", "hip"))
+        self.fc1 = getattr(ac, "fc1_impl", "h3")
+        self.stage = WeightStage(ac, flat_params, flat, impl=getattr(agent, "stage_impl", "hip"), fc1=self.fc1)
         self.head = (ac.actor[2].weight, ac.actor[2].bias, ac.critic[2].weight, ac.critic[2].bias)
         self._side = None
+        self.amax_act = torch.zeros(4, dtype=torch.int32, device=agent.device)
 
     def valid(self) -> bool:
         if not (self.stage.valid() and all(p.requires_grad for p in self.params)):
+            return False
+        ag = self._agent()
+        if ag is None or getattr(ag.ac, "fc1_impl", "h3") != self.fc1:
             return False
         off, base = 0, self.stage.flat_params.data_ptr()
         for p in self.params:
@@ -231,14 +246,26 @@ class WindowStep:
         Wa, ba, Wc, bc = self.head
         g = self.stage.grads  # (dT2, db2, dW3r, db3, dW4p, db4)
         # ---- forward (merlin/windows.py window_tower_head_x6)
+        h3 = self.fc1 == "h3"
+        # this step's operand scales [max |a3| per tower, max |dz| per tower], filled by atomics in the producer
+        # kernels; zeroed here by a plain launch, not inside the captured forward graph: a zeroing captured as a
+        # memset node replays with a wrong fill value on ROCm 7 (0x80808080: an exponent that overflows every plane,
+        # NaN in the second update; scripts/probe_graph_then.py)
+        am = self.amax_act
+        if h3:
+            am.zero_()
         T2, b2, W3r, b3, _, b4 = self.stage.forward()
         P4, P4t = self.stage.planes
+        am3, amz, amW = am[0:2], am[2:4], self.stage.amaxW
         a2w = nat.bias_relu_(nat.window_lut(plan.rows, T2), b2)  # relu(conv2) of every window
         Q = torch.bmm(a2w, W3r)  # [2, windows, (ky, kx, co)]
-        Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True)
+        Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None)
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
-        h = nat.x6_gemm_nt(a3, P4, bias=b4, cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
+        if h3:
+            h = nat.h3_gemm_nt(a3, am3, P4, amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd")
+        else:
+            h = nat.x6_gemm_nt(a3, P4, bias=b4, cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
         logits, value = nat.heads_fwd(h, Wa, Wc)  # both heads in one pass over h (the loss adds their biases)
         # ---- loss and its gradient per frame (merlin.ppo._PPOLoss); the head-bias gradients land in .grad
         _, dlogits, dvalue, _, _ = nat.ppo_loss(
@@ -247,18 +274,30 @@ class WindowStep:
             out_bias_critic=self.views[bc])
         # ---- backward (_WindowTowerHeadX6.backward, _WindowGemm / _BiasRelu / _WindowConv2 backward)
         dz, _, _, _ = nat.head_bwd(h, dlogits, dvalue, Wa, Wc, out_bias=g[5], out_w_actor=self.views[Wa],
-                                   out_w_critic=self.views[Wc])
+                                   out_w_critic=self.views[Wc], amax=amz if h3 else None)
         main = torch.cuda.current_stream()
         side = self.side_stream(dz.device)
+
+        def wgrad():
+            if h3:
+                nat.h3_gemm_tn(dz, amz, a3, am3, name="gemm_wgrad", out=g[4])
+            else:
+                nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
+
         if WGRAD_EARLY:  # fc1's weight gradient beside the input gradient and conv3's segmented sums
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
-        da3 = nat.x6_gemm_nt(dz, P4t, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
-        if not WGRAD_EARLY:  # fc1's weight gradient beside conv3's segmented sums
+                wgrad()
+        if h3:
+            da3 = nat.h3_gemm_nt(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+        else:
+            da3 = nat.x6_gemm_nt(dz, P4t, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+        if not WGRAD_SIDE:
+            wgrad()
+        elif not WGRAD_EARLY:  # fc1's weight gradient beside conv3's segmented sums
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
+                wgrad()
         dz.record_stream(side)
         a3.record_stream(side)
         dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]))

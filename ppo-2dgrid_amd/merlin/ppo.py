@@ -376,7 +376,7 @@ class PPO:
         t_host = time.perf_counter()
         perms = [self._perm(B, epoch) for epoch in range(self.update_epochs)]  # drawn in epoch order
         # the window + x6 path's step with its launches written out (merlin/fast_step.py)
-        fast = plan is not None and self.fast_step and getattr(self.ac, "fc1_impl", None) == "x6"
+        fast = plan is not None and self.fast_step and getattr(self.ac, "fc1_impl", None) in ("x6", "h3")
         if fast and not all(p.requires_grad for p in self.ac.parameters()):
             # the fast step writes a gradient for every parameter (and the optimizer steps every parameter that
             # has one): with a frozen parameter the update takes the autograd path, which leaves it untouched

@@ -533,9 +533,40 @@ def _side_stream(device):
     return st
 
 
+class _Fc1:
+    """fc1's three GEMMs on the matrix cores: impl "h3" (two f16 planes per value, per-tower scales from max |x|,
+    csrc/merlin_h3.hip) or "x6" (three bf16 planes, csrc/merlin_gemm.hip / merlin_gemm2.hip)."""
+
+    def __init__(self, impl, W4p):
+        self.impl = impl
+        W = W4p.detach().contiguous()
+        Wt = W.transpose(1, 2).contiguous()
+        if impl == "h3":
+            self.amW = nat.h3_amax(W)  # W4p^T holds the same values: one scale for both
+            self.P, self.Pt = nat.h3_split(W, self.amW), nat.h3_split(Wt, self.amW)
+        else:
+            self.P, self.Pt = nat.x6_split(W), nat.x6_split(Wt)
+
+    def fwd(self, a3, b4, am3=None):
+        if self.impl == "h3":
+            return nat.h3_gemm_nt(a3, am3, self.P, self.amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd")
+        return nat.x6_gemm_nt(a3, self.P, bias=b4, cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
+
+    def dgrad(self, dz, amz=None):
+        if self.impl == "h3":
+            return nat.h3_gemm_nt(dz, amz, self.Pt, self.amW, cfg=nat.H3_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+        return nat.x6_gemm_nt(dz, self.Pt, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+
+    def wgrad(self, dz, a3, amz=None, am3=None, out=None):
+        if self.impl == "h3":
+            return nat.h3_gemm_tn(dz, amz, a3, am3, name="gemm_wgrad", out=out)
+        return nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=out)
+
+
 class _WindowTowerHeadX6(torch.autograd.Function):
     """conv3 -> fc1 -> ReLU -> heads of both towers for the minibatch's distinct frames, with fc1's
-    three GEMMs on the bf16 matrix cores in exact three-plane form (csrc/merlin_gemm.hip):
+    three GEMMs on the matrix cores (_Fc1: f16 two-plane form by default, csrc/merlin_h3.hip, or the exact
+    bf16 three-plane form, csrc/merlin_gemm.hip):
       forward   a3 = relu(conv3) from Q (k_window_conv3, with the ReLU bit words), h = relu(a3 W4p^T +
                 b4) (merlin_x6_gemm_nt, bias + ReLU epilogue), logits = h0 Wa^T (+ ba), value = h1 wc
                 (+ bc)   (src/actor_critic.py:13-14, 31-41)
@@ -545,14 +576,17 @@ class _WindowTowerHeadX6(torch.autograd.Function):
     fp32 products throughout (the activations are split into planes inside the GEMMs)."""
 
     @staticmethod
-    def forward(ctx, Q, b3, W4p, b4, Wa, ba, Wc, bc, plan, mb, fc1_weights=None):
-        Y3, bits = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous(), bits=True)
+    def forward(ctx, Q, b3, W4p, b4, Wa, ba, Wc, bc, plan, mb, fc1_weights=None, impl="x6"):
+        am = torch.zeros(4, dtype=torch.int32, device=Q.device) if impl == "h3" else None  # max |a3|, max |dz|
+        Y3, bits = nat.window_conv3(Q.detach().contiguous(), plan.wid, mb.groups, b3.detach().contiguous(), bits=True,
+                                    amax=am[0:2] if am is not None else None)
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
-        h = nat.x6_gemm_nt(a3, nat.x6_split(W4p.detach()), bias=b4.detach(), cfg=nat.X6_NT_CFG["fwd"],
-                           name="gemm_fc1_fwd")
+        fc1 = _Fc1(impl, W4p)
+        h = fc1.fwd(a3, b4.detach(), am[0:2] if am is not None else None)
         logits, value = nat.heads_fwd(h, Wa, Wc, ba, bc)  # both heads in one pass over h
         ctx.save_for_backward(a3, bits, W4p, h, Wa, Wc)
+        ctx.fc1, ctx.am = fc1, am
         ctx.head_bias = (ba is not None, bc is not None)
         ctx.plan, ctx.mb, ctx.nw_q = plan, mb, Q.shape[1]
         ctx.fc1_weights = fc1_weights  # (actor, critic) fc1 weights W4p was stacked from (deferred mode)
@@ -564,12 +598,14 @@ class _WindowTowerHeadX6(torch.autograd.Function):
         n = h.shape[1]
         dlogits = h.new_zeros(n, Wa.shape[0]) if dlogits is None else dlogits.contiguous()
         dvalue = h.new_zeros(n) if dvalue is None else dvalue.contiguous()
-        dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous())
-        W4tp = nat.x6_split(W4p.detach().transpose(1, 2).contiguous())
-        da3 = nat.x6_gemm_nt(dz, W4tp, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+        fc1, am = ctx.fc1, ctx.am
+        amz, am3 = (am[2:4], am[0:2]) if am is not None else (None, None)
+        dz, db4, dWa, dWc = nat.head_bwd(h, dlogits, dvalue, Wa.detach().contiguous(), Wc.detach().contiguous(),
+                                         amax=amz)
+        da3 = fc1.dgrad(dz, amz)
         side = _side_stream(dz.device) if OVERLAP_WGRAD else None
         if side is None:
-            dW4p = nat.x6_gemm_tn(dz, a3, name="gemm_wgrad")
+            dW4p = fc1.wgrad(dz, a3, amz, am3)
         else:
             # the weight gradient (matrix-core bound, one 120-KB-LDS block per CU) on a second stream,
             # beside conv3's memory-bound patch / band / window sums on this one (no LDS: their waves
@@ -577,9 +613,11 @@ class _WindowTowerHeadX6(torch.autograd.Function):
             main = torch.cuda.current_stream(dz.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                dW4p = nat.x6_gemm_tn(dz, a3, name="gemm_wgrad")
+                dW4p = fc1.wgrad(dz, a3, amz, am3)
             dz.record_stream(side)
             a3.record_stream(side)
+            if am is not None:
+                am.record_stream(side)
             dW4p.record_stream(main)
         dQ, db3 = _conv3_backward(ctx.plan, ctx.mb, bits, da3.view(2, n * 9, 64), ctx.nw_q)
         dba = dlogits.sum(0) if ctx.head_bias[0] else None
@@ -603,7 +641,7 @@ class _WindowTowerHeadX6(torch.autograd.Function):
             dW4p = None
         elif side is not None:
             torch.cuda.current_stream(dz.device).wait_stream(side)
-        return dQ, db3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc, None, None, None
+        return dQ, db3, dW4p, db4, dWa, dba, dWc.view_as(Wc), dbc, None, None, None, None
 
 def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = None) -> torch.Tensor:
     """relu(conv3(relu(conv2(relu(conv1(frame)))))) of both towers of CNNActorCritic `ac` for the
@@ -621,7 +659,7 @@ def tower_conv3(ac, plan: WindowPlan, mb: MinibatchWindows, rows: int | None = N
 
 def window_tower_head_x6(ac, plan: WindowPlan, mb: MinibatchWindows, head_bias: bool = True):
     """(logits [U, act_dim], value [U]) of the minibatch's distinct frames: conv2 / conv3 through
-    the windows, fc1 on the bf16 matrix cores in exact three-plane form (_WindowTowerHeadX6).  The
+    the windows, fc1 on the matrix cores (_WindowTowerHeadX6, ac.fc1_impl "h3" or "x6").  The
     window GEMMs take PyTorch's default hipBLASLt path (no TunableOp: merlin/gemm_tuning.py)."""
     ea, ec = ac.actor_extractor.network, ac.critic_extractor.network
     Z2w = _WindowConv2.apply(ac.conv2_tables(), plan, plan.num_windows)
@@ -637,4 +675,4 @@ def window_tower_head_x6(ac, plan: WindowPlan, mb: MinibatchWindows, head_bias: 
     defer = _defer_active() and fa.weight.requires_grad and fc.weight.requires_grad and torch.is_grad_enabled()
     return _WindowTowerHeadX6.apply(Q, torch.stack([ea[4].bias, ec[4].bias]), W4p, torch.stack([fa.bias, fc.bias]),
                                     ac.actor[2].weight, ba, ac.critic[2].weight, bc, plan, mb,
-                                    (fa.weight, fc.weight) if defer else None)
+                                    (fa.weight, fc.weight) if defer else None, ac.fc1_impl)

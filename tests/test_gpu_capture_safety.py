@@ -120,3 +120,27 @@ def test_frozen_parameter_stays_and_others_train(device):
     moved = [not torch.equal(a, p.detach()) for a, p in zip(others, [p for p in agent.ac.parameters()
                                                                       if p.requires_grad])]
     assert all(moved)
+
+
+def test_captured_scale_reduction_replays_correctly(device):
+    """merlin_h3_amax inside a captured HIP graph (the fast step's forward graph computes fc1's weight scale this
+    way) must give every replay's own max: its zeroing is a kernel, not a hipMemsetAsync -- a memset node captured on
+    ROCm 7 replayed with the fill value 0x80808080 (scripts/probe_graph_then.py), an operand scale of 2^120."""
+    from merlin import _native as nat
+
+    S = torch.zeros(2, 64, device=device)
+    am = torch.zeros(2, dtype=torch.int32, device=device)
+    nat.h3_amax(S, out=am)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        nat.h3_amax(S, out=am)
+    R = torch.zeros(20, 2, dtype=torch.int32, device=device)
+    for k in range(20):
+        S.fill_(float(k + 1))
+        S[1].mul_(-0.5)
+        g.replay()
+        R[k].copy_(am)
+    torch.cuda.synchronize()
+    want = torch.tensor([[k + 1.0, (k + 1.0) / 2] for k in range(20)], device=device)
+    assert torch.equal(R.view(torch.float32), want)

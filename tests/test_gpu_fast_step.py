@@ -12,7 +12,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(device, fast, iters=3, stage_impl="hip"):
+def _run(device, fast, iters=3, stage_impl="hip", first_grads=None):
     from merlin import MerlinVecEnv
     from merlin.ppo import PPO
 
@@ -22,6 +22,16 @@ def _run(device, fast, iters=3, stage_impl="hip"):
                 device=device)
     agent.fast_step = fast
     agent.stage_impl = stage_impl
+    if first_grads is not None:  # record the first optimizer step's (pre-clip) gradient of every parameter
+        ca = agent._clip_adam
+        orig = ca.step
+
+        def step():
+            if not first_grads:
+                first_grads.extend(p.grad.detach().clone() for p in agent.ac.parameters())
+            return orig()
+
+        ca.step = step
     stats = []
     for _ in range(iters):
         stats.append(agent.update(agent.collect_rollouts()))
@@ -47,23 +57,27 @@ def test_fast_step_matches_autograd_bitwise(device):
 
 
 def test_fast_step_hip_tables_close_and_reproducible(device):
-    a0, s0 = _run(device, False, iters=1)
-    a1, s1 = _run(device, True, iters=1)
+    g0, g1 = [], []
+    a0, s0 = _run(device, False, iters=1, first_grads=g0)
+    a1, s1 = _run(device, True, iters=1, first_grads=g1)
     a2, s2 = _run(device, True, iters=1)
     assert s1 == s2
     for p1, p2 in zip(a1.ac.parameters(), a2.ac.parameters()):
         assert torch.equal(p1, p2)
     for k in s0[0]:
         assert abs(s0[0][k] - s1[0][k]) <= 1e-4 * max(1.0, abs(s0[0][k])), k
-    # every parameter within the 8 Adam steps' size (lr each); the critic tower, whose loss is smooth, to float32
-    # level -- the actor's clipped surrogate turns float32-level differences in the logits into different clip
-    # decisions near the boundary, which Adam's per-element normalisation then carries to ~lr per step (the
-    # tables' own gradients are compared directly in test_stage_tables_match_torch)
+    # the first optimizer step's gradient of every parameter, HIP tables against the autograd path's torch tables:
+    # equal to fp32 level (1e-5 of each tensor's norm; the tables' own gradients: test_stage_tables_match_torch)
+    names = [k for k, _ in a0.ac.named_parameters()]
+    for k, x, y in zip(names, g0, g1):
+        rel = float((x - y).norm() / x.norm().clamp_min(1e-30))
+        assert rel <= 1e-5, (k, rel)
+    # after the update (8 Adam steps) every parameter within the steps' size (lr each): Adam's per-element
+    # normalisation turns an fp32-level difference in a gradient element that cancels to ~0 into a ~lr step of
+    # either sign, so the parameters are held to that bound and the gradients above to fp32 level
     for (k, p0), p1 in zip(a0.ac.named_parameters(), a1.ac.parameters()):
         d = (p1 - p0).detach().abs()
         assert float(d.max()) <= 2 * 1e-3 * 8, k
-        if k.startswith("critic"):
-            assert int((d <= 1e-6 + 1e-4 * p0.detach().abs()).sum()) >= 0.999 * p0.numel(), k
 
 
 def test_stage_tables_match_torch(device):

@@ -92,9 +92,11 @@ def test_gemm_tn_cancellation(device, cfg):
     assert rel(nat.x6_gemm_tn(dz, a3, cfg=cfg)) <= ref
 
 
-def test_window_update_x6_matches_hipblaslt(device):
-    """One window-path forward + backward with fc1 on the x6 GEMMs vs the same with torch's fp32
-    GEMMs: outputs and every parameter gradient agree to fp32 GEMM accuracy."""
+@pytest.mark.parametrize("impl", ["x6", "h3"])
+def test_window_update_x6_matches_hipblaslt(device, impl):
+    """One window-path forward + backward with fc1 on the plane-form GEMMs (x6: bf16 three-plane, h3: f16
+    two-plane, csrc/merlin_h3.hip) vs the same with torch's fp32 GEMMs: outputs and every parameter gradient agree
+    to fp32 GEMM accuracy."""
     from merlin import CNNActorCritic
 
     from test_gpu_windows import _plan
@@ -104,16 +106,16 @@ def test_window_update_x6_matches_hipblaslt(device):
     ac = CNNActorCritic((56, 56, 3), 3).to(device)
     mb = plan.minibatch(torch.randperm(codes.shape[0], device=device)[:3000])
     outs, grads = {}, {}
-    for impl in ("x6", "hipblaslt"):
-        ac.fc1_impl = impl
+    for which in (impl, "hipblaslt"):
+        ac.fc1_impl = which
         ac.zero_grad()
         logits, value = ac.heads_windows(plan, mb)
         (logits.square().sum() + value.sum()).backward()
-        outs[impl] = (logits.detach().clone(), value.detach().clone())
-        grads[impl] = {k: p.grad.detach().clone() for k, p in ac.named_parameters()}
-    for a, b in zip(outs["x6"], outs["hipblaslt"]):
+        outs[which] = (logits.detach().clone(), value.detach().clone())
+        grads[which] = {k: p.grad.detach().clone() for k, p in ac.named_parameters()}
+    for a, b in zip(outs[impl], outs["hipblaslt"]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
-    for k in grads["x6"]:
-        g1, g2 = grads["x6"][k], grads["hipblaslt"][k]
+    for k in grads[impl]:
+        g1, g2 = grads[impl][k], grads["hipblaslt"][k]
         scale = float(g2.abs().max()) + 1e-12
         assert float((g1 - g2).abs().max()) <= 2e-5 * scale, k

@@ -1,0 +1,107 @@
+"""GPU: fc1's fp32 GEMMs on the f16 matrix cores in two-plane form (csrc/merlin_h3.hip).
+
+Every operand is scaled by a per-tower power of two from its max |x| and used as two f16 planes; the planes must
+reconstruct x' = x 2^e to 2^-23 |x'| (values within 2^26 of the tower max).  Each GEMM is compared with a float64
+product of the same fp32 operands, and its error must be no larger than that of torch's own fp32 GEMM (hipBLASLt,
+the f32 MFMA) on the same operands: max |C - C64| / sum_k |a_k b_k| (floor: one product's bound, 2^-21), and on the
+update's
+cancellation-heavy weight gradient the error relative to the result's norm.  Operand magnitudes include the
+update's gradient scale (dz ~ 1e-7: only the per-tensor exponent keeps those inside the f16 range) and rows of
+very different scales.  Shapes: the update's fc1 (K = 576 / 512, N = 512 / 576), row counts that are not tile
+multiples, both towers with their own operands and scales."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# one product's own error bound: the two planes hold each scaled value to 2^-23, the dropped l_a l_b term is below
+# 2^-22 |a b| -- together under 2^-21 |a b| (a K = 1 "GEMM" is a single product, exact in fp32); from K ~ 100 on the
+# fp32 accumulation error of either GEMM is larger than this
+FLOOR = 2.0 ** -21
+
+
+def _err(C, C64, den):
+    return float(((C.double() - C64).abs() / den.clamp_min(1e-300)).max())
+
+
+def test_amax_and_split(device):
+    from merlin import _native as nat
+
+    g = torch.Generator(device=device).manual_seed(3)
+    x = torch.randn(2, 333, 576, device=device, generator=g)
+    x[0] *= 1e-7
+    x[1] *= 3e4
+    am = nat.h3_amax(x)
+    ref = x.abs().amax(dim=(1, 2))
+    assert torch.equal(am.view(torch.float32), ref)
+    P = nat.h3_split(x, am).view(torch.float16).view(2, 333, 72, 2, 8).float()
+    e = 14 - torch.floor(torch.log2(ref))  # max |x| 2^e in [2^14, 2^15)
+    xs = x * torch.exp2(e).view(2, 1, 1)
+    assert float(xs.abs().amax()) < 2 ** 15 and float(xs.abs().amax()) >= 2 ** 14
+    rec = (P[..., 0, :].double() + P[..., 1, :].double() / 2048).reshape(2, 333, 576)
+    rel = ((rec - xs.double()).abs() / xs.double().abs().clamp_min(2 ** -12)).max()
+    assert float(rel) <= 2 ** -23
+
+
+def _operands(device, M, N, K, seed, scale_a=1.0, ragged=False):
+    g = torch.Generator(device=device).manual_seed(seed)
+    A = torch.relu(torch.randn(2, M, K, device=device, generator=g)) * scale_a
+    if ragged:  # rows of very different magnitudes within one tensor
+        A = A * torch.exp2(torch.randint(-12, 4, (2, M, 1), device=device, generator=g).float())
+    B = torch.randn(2, N, K, device=device, generator=g) / K ** 0.5
+    return A, B
+
+
+@pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 2), (512, 576, 3)])
+@pytest.mark.parametrize("M,scale_a,ragged", [(1, 1.0, False), (777, 1.0, False), (20011, 1.0, False),
+                                              (20011, 1e-7, False), (9999, 1.0, True)])
+def test_gemm_nt_vs_float64(device, M, N, K, cfg, scale_a, ragged):
+    from merlin import _native as nat
+
+    if N % (192 if cfg == 1 else 256 if cfg == 3 else 128):
+        pytest.skip("N not a multiple of the tile width")
+    A, B = _operands(device, M, N, K, M + N + cfg, scale_a, ragged)
+    bias = torch.randn(2, N, device=device)
+    C64 = torch.bmm(A.double(), B.double().transpose(1, 2))
+    den = torch.bmm(A.abs().double(), B.abs().double().transpose(1, 2))
+    tol = max(_err(torch.bmm(A, B.transpose(1, 2)), C64, den), FLOOR)
+    amA, amB = nat.h3_amax(A), nat.h3_amax(B)
+    Bp = nat.h3_split(B, amB)
+    C = nat.h3_gemm_nt(A, amA, Bp, amB, cfg=cfg)
+    assert _err(C, C64, den) <= tol
+    Cb = nat.h3_gemm_nt(A, amA, Bp, amB, bias=bias, cfg=cfg)
+    assert torch.equal(Cb, torch.relu(C + bias.unsqueeze(1)))
+    assert torch.equal(C, nat.h3_gemm_nt(A, amA, Bp, amB, cfg=cfg))  # fixed order: the same bits every call
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("Kd,splits,scale", [(1, 1, 1.0), (4093, 7, 1.0), (40000, 32, 1.0), (40000, 32, 1e-7)])
+def test_gemm_tn_vs_float64(device, Kd, splits, scale, cfg):
+    from merlin import _native as nat
+
+    g = torch.Generator(device=device).manual_seed(Kd + cfg)
+    dz = torch.randn(2, Kd, 512, device=device, generator=g) * (torch.rand(2, Kd, 512, device=device,
+                                                                           generator=g) > 0.5) * scale
+    a3 = torch.relu(torch.randn(2, Kd, 576, device=device, generator=g))
+    W64 = torch.bmm(dz.double().transpose(1, 2), a3.double())
+    den = torch.bmm(dz.abs().double().transpose(1, 2), a3.abs().double())
+    tol = max(_err(torch.bmm(dz.transpose(1, 2), a3), W64, den), FLOOR)
+    W = nat.h3_gemm_tn(dz, nat.h3_amax(dz), a3, nat.h3_amax(a3), splits=splits, cfg=cfg)
+    assert _err(W, W64, den) <= tol
+    assert torch.equal(W, nat.h3_gemm_tn(dz, nat.h3_amax(dz), a3, nat.h3_amax(a3), splits=splits, cfg=cfg))
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+def test_gemm_tn_cancellation(device, cfg):
+    """The update's weight gradient: ~1e5 rows whose terms nearly cancel (|W| ~ 1e-2 sum |a b|)."""
+    from merlin import _native as nat
+
+    g = torch.Generator(device=device).manual_seed(5)
+    Kd = 60000
+    a3 = torch.relu(torch.randn(2, Kd, 576, device=device, generator=g))
+    sgn = torch.where(torch.rand(2, Kd, 1, device=device, generator=g) < 0.5005, 1.0, -1.0)
+    dz = sgn * torch.rand(2, Kd, 512, device=device, generator=g) * 1e-6
+    W64 = torch.bmm(dz.double().transpose(1, 2), a3.double())
+    rel = lambda W: float((W.double() - W64).norm() / W64.norm())  # noqa: E731
+    ref = rel(sum(torch.bmm(dz[:, i:i + 2000].transpose(1, 2), a3[:, i:i + 2000]) for i in range(0, Kd, 2000)))
+    assert rel(nat.h3_gemm_tn(dz, nat.h3_amax(dz), a3, nat.h3_amax(a3), cfg=cfg)) <= ref
