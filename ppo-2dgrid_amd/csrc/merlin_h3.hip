@@ -56,7 +56,7 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 __device__ __forceinline__ int h3_exp(uint32_t amax) {
     if (amax == 0u) return 0;
     const int e = (int)((amax >> 23) & 0xffu) - 127;  // floor(log2) for a normal max (inf / nan: e = 128)
-    return std::min(std::max(14 - e, -120), 120);
+    return std::min(std::max(14 - e, -120), 115);  // e + 11 stays a normal power of two
 }
 __device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
 
@@ -66,21 +66,28 @@ __device__ __forceinline__ uint32_t load_amax(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// planes of two scaled values: hi word (h of a, h of b), lo word (l of a, l of b)
-__device__ __forceinline__ void h3_pair(float a, float b, uint32_t &hi, uint32_t &lo) {
-    const f16x2 h = f16x2{(_Float16)a, (_Float16)b};
-    const float ra = (a - (float)h.x) * LO_SCALE, rb = (b - (float)h.y) * LO_SCALE;
-    hi = __builtin_bit_cast(uint32_t, h);
-    lo = __builtin_bit_cast(uint32_t, f16x2{(_Float16)ra, (_Float16)rb});
+// planes of two unscaled values a, b (sc = 2^e, sc2 = 2^(e + 11)): hi word (h of a, h of b) = f16(x'), lo word =
+// f16(2^11 x' - 2^11 h), each by one v_fma_mix{lo,hi}_f16 (the mixed fma rounds its exact result once to f16; in
+// the lo ones h is read as an f16 operand from its half of the hi word, so x' - h is never formed in f32): six
+// vector instructions per pair (the compiler's version of the same expressions took nine, computing h twice)
+__device__ __forceinline__ void h3_pair(float a, float b, float sc, float sc2, uint32_t &hi, uint32_t &lo) {
+    const float m2048 = -LO_SCALE, za = a * sc2, zb = b * sc2;
+    uint32_t h, l;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(a), "v"(sc));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(b), "v"(sc));
+    asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(h), "v"(m2048), "v"(za));
+    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(h), "v"(m2048), "v"(zb));
+    hi = h;
+    lo = l;
 }
 
-// 8 consecutive values (two float4) scaled by sc -> hi chunk p0, lo chunk p1
-__device__ __forceinline__ void h3_split8(const float4 a, const float4 b, float sc, u32x4 &p0, u32x4 &p1) {
+// 8 consecutive values (two float4) scaled by sc (sc2 = 2^11 sc) -> hi chunk p0, lo chunk p1
+__device__ __forceinline__ void h3_split8(const float4 a, const float4 b, float sc, float sc2, u32x4 &p0, u32x4 &p1) {
     uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
-    h3_pair(a.x * sc, a.y * sc, h0, l0);
-    h3_pair(a.z * sc, a.w * sc, h1, l1);
-    h3_pair(b.x * sc, b.y * sc, h2, l2);
-    h3_pair(b.z * sc, b.w * sc, h3, l3);
+    h3_pair(a.x, a.y, sc, sc2, h0, l0);
+    h3_pair(a.z, a.w, sc, sc2, h1, l1);
+    h3_pair(b.x, b.y, sc, sc2, h2, l2);
+    h3_pair(b.z, b.w, sc, sc2, h3, l3);
     p0 = u32x4{h0, h1, h2, h3};
     p1 = u32x4{l0, l1, l2, l3};
 }
@@ -116,14 +123,15 @@ __global__ void k_h3_zero(uint32_t *__restrict__ amax, int T) {
 __global__ __launch_bounds__(256) void k_h3_split(const float4 *__restrict__ x, int64_t g8, const uint32_t *amax,
                                                   u32x4 *__restrict__ planes) {
     const int t = blockIdx.y;
-    const float sc = pow2f(h3_exp(load_amax(amax + t)));
+    const int e = h3_exp(load_amax(amax + t));
+    const float sc = pow2f(e), sc2 = pow2f(e + 11);
     x += t * g8 * 2;
     planes += t * g8 * 2;
-    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < g8; e += (int64_t)gridDim.x * 256) {
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < g8; q += (int64_t)gridDim.x * 256) {
         u32x4 p0, p1;
-        h3_split8(x[2 * e], x[2 * e + 1], sc, p0, p1);
-        planes[2 * e] = p0;
-        planes[2 * e + 1] = p1;
+        h3_split8(x[2 * q], x[2 * q + 1], sc, sc2, p0, p1);
+        planes[2 * q] = p0;
+        planes[2 * q + 1] = p1;
     }
 }
 
@@ -157,7 +165,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
     const int64_t m0 = (int64_t)tm * BM;
     const int n0 = tn * BN;
     const int eA = h3_exp(load_amax(amaxA + t)), eB = h3_exp(load_amax(amaxB + t));
-    const float scA = pow2f(eA);
+    const float scA = pow2f(eA), scA2 = pow2f(eA + 11);
     const int64_t rowB = (int64_t)(K / 8) * 2;  // chunks per B row
     B += t * sB;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -197,7 +205,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
         for (int i = 0; i < UA; i++)
             if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
                 u32x4 p0, p1;
-                h3_split8(ra[i][0], ra[i][1], scA, p0, p1);
+                h3_split8(ra[i][0], ra[i][1], scA, scA2, p0, p1);
                 st[la[i]] = p0;
                 st[PSA + la[i]] = p1;
             }
@@ -277,6 +285,173 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
     }
 }
 
+// The same NT product with the k step's split and staging interleaved into its MFMAs.  In k_h3_nt every k step is
+// [split + stage the next step, VALU] -> [fragment reads -> MFMAs] -> barrier, and the two waves of a SIMD, held in
+// step by the barrier, run their VALU blocks side by side and then their MFMA blocks: the matrix pipe idles through
+// the first (PMC: MFMA busy 38 %, 3.3 VALU per MFMA).  Here the main loop has no conditional parts (the last two
+// steps are peeled), the body reads all its fragments first, and sched_group_barrier hints lay the next step's
+// split (VALU), its LDS stores and the global loads of the step after it between the MFMAs (guide T19).
+template <int BM, int BN, int WGM, int WGN, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restrict__ A, const u32x4 *__restrict__ B,
+                                                           const uint32_t *__restrict__ amaxA,
+                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N,
+                                                           int K, int64_t sA, int64_t sB,
+                                                           const float *__restrict__ bias, float *__restrict__ C,
+                                                           int64_t sC, int tiles_n) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int QA = BM * 4, QB = BN * 8;
+    constexpr int UA = (QA + NT - 1) / NT, CB = (QB + NT - 1) / NT;
+    static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile of 32 x 32 MFMA tiles");
+    static_assert(QA % NT == 0 && QB % NT == 0, "whole staging units per thread");
+    constexpr int PSA = BM * 4, PSB = BN * 4 + 12;
+    constexpr int STAGE = 2 * (PSA + PSB);
+    constexpr int NMFMA = TM * TN * 6;  // per k step and wave
+    __shared__ u32x4 lds[2 * STAGE];
+
+    const int t = blockIdx.y;
+    const int L = xcd_tile(blockIdx.x, gridDim.x);
+    const int tm = L / tiles_n, tn = L - tm * tiles_n;
+    const int64_t m0 = (int64_t)tm * BM;
+    const int n0 = tn * BN;
+    const int eA = h3_exp(load_amax(amaxA + t)), eB = h3_exp(load_amax(amaxB + t));
+    const float scA = pow2f(eA), scA2 = pow2f(eA + 11);
+    const int64_t rowB = (int64_t)(K / 8) * 2;
+    B += t * sB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    const float4 *ga[UA];
+    int la[UA];
+#pragma unroll
+    for (int i = 0; i < UA; i++) {
+        const int q = tid + i * NT;
+        const int row = q >> 2, g = q & 3;
+        ga[i] = reinterpret_cast<const float4 *>(A + t * sA + std::min<int64_t>(m0 + row, M - 1) * K) + g * 2;
+        la[i] = row * 4 + (g ^ ((row >> 2) & 3));
+    }
+    int gb[CB], lb[CB];
+#pragma unroll
+    for (int i = 0; i < CB; i++) {
+        const int q = tid + i * NT;
+        const int row = q >> 3, g = (q >> 1) & 3, p = q & 1;
+        gb[i] = (int)((int64_t)(n0 + row) * rowB + g * 2 + p);
+        lb[i] = 2 * PSA + p * PSB + row * 4 + (g ^ ((row >> 2) & 3));
+    }
+    float4 ra[UA][2];
+    u32x4 rb[CB];
+    auto load = [&](int kt) {
+#pragma unroll
+        for (int i = 0; i < UA; i++) {
+            ra[i][0] = ga[i][(int64_t)kt * 8];
+            ra[i][1] = ga[i][(int64_t)kt * 8 + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < CB; i++) rb[i] = B[gb[i] + kt * 8];
+    };
+    auto store = [&](int buf) {
+        u32x4 *st = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < UA; i++) {
+            u32x4 p0, p1;
+            h3_split8(ra[i][0], ra[i][1], scA, scA2, p0, p1);
+            st[la[i]] = p0;
+            st[PSA + la[i]] = p1;
+        }
+#pragma unroll
+        for (int i = 0; i < CB; i++) st[lb[i]] = rb[i];
+    };
+
+    f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = f32x16{};
+            lo[i][j] = f32x16{};
+        }
+    const int fr = lane & 31, fh = lane >> 5, fs = (fr >> 2) & 3;
+    auto compute = [&](int buf) {
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 2 * PSA;
+        u32x4 af[TM][2][2], bf[TN][2][2];
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++)
+                    bf[j][kh][p] = sBl[p * PSB + (wn * WTN + j * 32 + fr) * 4 + ((2 * kh + fh) ^ fs)];
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++)
+                    af[i][kh][p] = sAl[p * PSA + (wm * WTM + i * 32 + fr) * 4 + ((2 * kh + fh) ^ fs)];
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                f32x16 l = lo[i][j], h = hi[i][j];
+#pragma unroll
+                for (int kh = 0; kh < 2; kh++) {
+                    l = mfma16(af[i][kh][1], bf[j][kh][0], l);
+                    l = mfma16(af[i][kh][0], bf[j][kh][1], l);
+                    h = mfma16(af[i][kh][0], bf[j][kh][0], h);
+                }
+                lo[i][j] = l;
+                hi[i][j] = h;
+            }
+    };
+
+    const int nk = K / BK;  // >= 2 (K % 32 == 0, K >= 64: the launcher checks)
+    load(0);
+    store(0);
+    load(1);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 2 < nk; kt++) {
+        const int buf = kt & 1;
+        compute(buf);
+        store(buf ^ 1);
+        load(kt + 2);
+        // the fragment reads first, then each MFMA followed by a share of the split, the stores and the loads
+        __builtin_amdgcn_sched_group_barrier(0x100, TM * 4 + TN * 4, 0);
+#pragma unroll
+        for (int m = 0; m < NMFMA; m++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            if (m % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            if (m >= NMFMA / 2 && m % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __syncthreads();
+    }
+    compute(kt & 1);  // kt = nk - 2: stage the last step
+    store((kt & 1) ^ 1);
+    __syncthreads();
+    compute((kt + 1) & 1);
+
+    const float inv = pow2f(-eA), invB = pow2f(-eB);
+    float *Ct = C + t * sC;
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+        const int col = n0 + wn * WTN + j * 32 + fr;
+        const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (row < M) {
+                    const float v = (hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB;
+                    Ct[row * N + col] = EPI == 1 ? relu_nan(v + bv) : v;
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // TN: slab[s][t][m][n] = sum_{k in split s} A[t][k][m] B[t][k][n], A fp32 [Kd][M], B fp32 [Kd][N] (the weight
 // gradient dz^T a3: both operands row-major over the minibatch's frames), both split while staged into plane
@@ -329,7 +504,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
     const int m0 = tm * BM, n0 = tn * BN;
     const int64_t k0 = (int64_t)s * kc, k1 = std::min<int64_t>(Kd, k0 + kc);
     const int eA = h3_exp(load_amax(amaxA + t)), eB = h3_exp(load_amax(amaxB + t));
-    const float scA = pow2f(eA), scB = pow2f(eB);
+    const float scA = pow2f(eA), scB = pow2f(eB), scA2 = pow2f(eA + 11), scB2 = pow2f(eB + 11);
     const int64_t rowA = M / 4, rowB = N / 4;
     A += t * sA + m0 / 4;
     B += t * sB + n0 / 4;
@@ -391,7 +566,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
             if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
                 const bool in = kk + ka[i] < k1;
                 u32x4 p0, p1;
-                h3_split8(in ? ra[i][0] : zero, in ? ra[i][1] : zero, scA, p0, p1);
+                h3_split8(in ? ra[i][0] : zero, in ? ra[i][1] : zero, scA, scA2, p0, p1);
                 st[la[i]] = p0;
                 st[PSA + la[i]] = p1;
             }
@@ -400,7 +575,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
             if (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB) {
                 const bool in = kk + kb[i] < k1;
                 u32x4 p0, p1;
-                h3_split8(in ? rb[i][0] : zero, in ? rb[i][1] : zero, scB, p0, p1);
+                h3_split8(in ? rb[i][0] : zero, in ? rb[i][1] : zero, scB, scB2, p0, p1);
                 st[lb[i]] = p0;
                 st[PSB + lb[i]] = p1;
             }
@@ -490,6 +665,24 @@ hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, cons
 }
 
 template <int BM, int BN, int WGM, int WGN>
+hipError_t ntp_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
+                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
+    if (N % BN || K < 2 * BK) return hipErrorInvalidValue;
+    if ((int64_t)N * (K / 8) * 2 > INT32_MAX) return hipErrorInvalidValue;
+    const int64_t tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = N / BN;
+    if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(tiles_m * tiles_n), T);
+    if (bias)
+        hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 1>), grid, dim3(64 * WGM * WGN), 0, s, A, B, amaxA, amaxB, M, N,
+                           K, sA, sB, bias, C, sC, tiles_n);
+    else
+        hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 0>), grid, dim3(64 * WGM * WGN), 0, s, A, B, amaxA, amaxB, M, N,
+                           K, sA, sB, nullptr, C, sC, tiles_n);
+    return hipGetLastError();
+}
+
+template <int BM, int BN, int WGM, int WGN>
 hipError_t tn_launch(const float *A, const float *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t Kd, int M,
                      int N, int T, int64_t sA, int64_t sB, int splits, float *slab, int *S_out, hipStream_t s) {
     if (M % BM || N % BN) return hipErrorInvalidValue;
@@ -543,6 +736,11 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 1: return nt_launch<128, 192, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
         case 2: return nt_launch<128, 128, 2, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
         case 3: return nt_launch<128, 256, 2, 4>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        // k_h3_ntp: the k step's split / staging interleaved into the MFMAs
+        case 10: return ntp_launch<256, 128, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        case 11: return ntp_launch<128, 192, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        case 12: return ntp_launch<128, 128, 2, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        case 13: return ntp_launch<128, 256, 2, 4>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
         default: return hipErrorInvalidValue;
     }
 }

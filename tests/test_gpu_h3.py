@@ -38,6 +38,10 @@ def test_amax_and_split(device):
     e = 14 - torch.floor(torch.log2(ref))  # max |x| 2^e in [2^14, 2^15)
     xs = x * torch.exp2(e).view(2, 1, 1)
     assert float(xs.abs().amax()) < 2 ** 15 and float(xs.abs().amax()) >= 2 ** 14
+    # the planes exactly: h = f16(x'), l = f16(2^11 (x' - h)) (round to nearest even; x' - h is exact in fp32)
+    h = xs.view(2, 333, 72, 8).half()
+    l = ((xs.view(2, 333, 72, 8) - h.float()) * 2048).half()
+    assert torch.equal(P[..., 0, :].half(), h) and torch.equal(P[..., 1, :].half(), l)
     rec = (P[..., 0, :].double() + P[..., 1, :].double() / 2048).reshape(2, 333, 576)
     rel = ((rec - xs.double()).abs() / xs.double().abs().clamp_min(2 ** -12)).max()
     assert float(rel) <= 2 ** -23
@@ -52,13 +56,14 @@ def _operands(device, M, N, K, seed, scale_a=1.0, ragged=False):
     return A, B
 
 
-@pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 2), (512, 576, 3)])
+@pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 2), (512, 576, 3),
+                                     (512, 576, 10), (576, 512, 11), (512, 576, 12), (576, 512, 12), (512, 576, 13)])
 @pytest.mark.parametrize("M,scale_a,ragged", [(1, 1.0, False), (777, 1.0, False), (20011, 1.0, False),
                                               (20011, 1e-7, False), (9999, 1.0, True)])
 def test_gemm_nt_vs_float64(device, M, N, K, cfg, scale_a, ragged):
     from merlin import _native as nat
 
-    if N % (192 if cfg == 1 else 256 if cfg == 3 else 128):
+    if N % {1: 192, 11: 192, 3: 256, 13: 256}.get(cfg, 128):
         pytest.skip("N not a multiple of the tile width")
     A, B = _operands(device, M, N, K, M + N + cfg, scale_a, ragged)
     bias = torch.randn(2, N, device=device)
