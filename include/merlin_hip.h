@@ -159,6 +159,11 @@ int merlin_env_step(merlin_env *env, const int64_t *actions_dev, int32_t n_steps
  * either way. */
 int merlin_env_set_refill_interval(merlin_env *env, int32_t every);
 int merlin_env_refill(merlin_env *env, void *stream);
+/* The fully observable observation (FullyObsWrapper + ImgObsWrapper, src/scenario_creator/scenario_creator.py:45-50,
+ * observation.fully_observable in src/config/scenario.yaml) of every env's current state: out_dev uint8[N][size][size]
+ * [3], out[i][x][y] = minigrid Grid.encode's (object, color, state) of cell (x, y), the agent's cell (10, 0, dir).
+ * observation.flatten (FlattenObservation, :52-53) is the same bytes read as uint8[N][size*size*3]. */
+int merlin_env_full_obs(merlin_env *env, uint8_t *out_dev, void *stream);
 /* [sync] copy env state to host: walls uint32[N][size] (bit x of row y = wall at
  * (x,y)); agent int32[N][8] = (x, y, dir, step_count, goal_x, goal_y, stay, 0);
  * rng uint64[N][5] = (state_hi, state_lo, inc_hi, inc_lo, has32<<32|buf32).
@@ -450,19 +455,28 @@ int merlin_x6_gemm_tn(const float *A_dev, const float *B_dev, int64_t Kd, int32_
  *        exponent of amax_dev[t]; 4 bytes per value.
  * gemm_nt: C[t][m][n] = sum_k A[t][m][k] B[t][n][k], A fp32 [M][K] with its amax, B planes [N][K] (K % 32 == 0;
  *          tower strides in values), + bias[t][n] and ReLU when bias != NULL; cfg: 0 256x128, 1 128x192,
- *          2 128x128, 3 128x256 (N a multiple of the tile width).
+ *          2 128x128, 3 128x256 (N a multiple of the tile width), 10..13 the same tiles with the split interleaved
+ *          into the MFMAs (K >= 64).  a_planes_dev (nullable): receives A's planes as the kernel makes them
+ *          ([t][M][K/8][2][8] f16, A's byte layout and tower stride) for a later gemm_tn_planes.
  * gemm_tn: out[t][m][n] = sum_k A[t][k][m] B[t][k][n], both fp32 with their amax (cfg 0 / 1: 128x192 tiles, M % 128,
  *          N % 192), the k range cut into <= splits slabs (slab float[merlin_x6_tn_slab_floats(...)]) summed in slab
- *          order. */
+ *          order.
+ * gemm_tn_planes: the same product over operands already in plane form (the a_planes output of gemm_nt for the same
+ *          tensor and amax), strides in values. */
 int merlin_h3_amax(const float *x_dev, int64_t n, int32_t towers, int64_t stride, uint32_t *amax_dev, void *stream);
 int merlin_h3_split(const float *x_dev, int64_t n, int32_t towers, const uint32_t *amax_dev, void *planes_dev,
                     void *stream);
 int merlin_h3_gemm_nt(const float *A_dev, const uint32_t *amax_a_dev, const void *B_dev, const uint32_t *amax_b_dev,
                       int64_t M, int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride,
-                      const float *bias_dev, float *C_dev, int64_t c_stride, int32_t cfg, void *stream);
+                      const float *bias_dev, float *C_dev, int64_t c_stride, void *a_planes_dev, int32_t cfg,
+                      void *stream);
 int merlin_h3_gemm_tn(const float *A_dev, const uint32_t *amax_a_dev, const float *B_dev, const uint32_t *amax_b_dev,
                       int64_t Kd, int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride,
                       int32_t splits, float *slab_dev, float *out_dev, int32_t cfg, void *stream);
+int merlin_h3_gemm_tn_planes(const void *A_planes_dev, const uint32_t *amax_a_dev, const void *B_planes_dev,
+                             const uint32_t *amax_b_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
+                             int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev, float *out_dev,
+                             int32_t cfg, void *stream);
 
 /* The conv1 / conv2 tables of both towers and their adjoint (the parameter-only part of PPO.update's
  * minibatch step, merlin/fast_step.py WeightStage; replaces CNNActorCritic.conv2_tables and its autograd

@@ -300,3 +300,31 @@ class LiteralEnv:
                 c = self.grid.get(i, j)
                 out[j, i] = 1 if c == WALL else 2 if c == GOAL else 0
         return out
+
+    def full_obs(self):
+        """FullyObsWrapper.observation (minigrid 3.0.0 wrappers.py) after ImgObsWrapper: Grid.encode() of the whole
+        grid -- [i][j] = (OBJECT_TO_IDX, COLOR_TO_IDX, state) of cell (i, j), None as empty (1, 0, 0), Wall (2, grey
+        5, 0), Goal (8, green 1, 0) -- with the agent's cell overwritten by (agent 10, red 0, agent_dir)."""
+        out = np.zeros((self.width, self.height, 3), dtype=np.uint8)
+        for i in range(self.width):
+            for j in range(self.height):
+                c = self.grid.get(i, j)
+                out[i, j] = (2, 5, 0) if c == WALL else (8, 1, 0) if c == GOAL else (1, 0, 0)
+        ax, ay = self.agent_pos
+        out[ax, ay] = (10, 0, self.agent_dir)
+        return out
+
+
+def full_obs_from_state(walls, agent_pos, agent_dir, goal_pos, size):
+    """The same observation from the bit-row state MerlinVecEnv.get_state reports (walls[y] bit x = wall at
+    (x, y)): the checker of merlin_env_full_obs."""
+    out = np.zeros((size, size, 3), dtype=np.uint8)
+    out[...] = (1, 0, 0)
+    for y in range(size):
+        for x in range(size):
+            if (int(walls[y]) >> x) & 1:
+                out[x, y] = (2, 5, 0)
+    out[int(goal_pos[0]), int(goal_pos[1])] = (8, 1, 0)
+    out[int(agent_pos[0]), int(agent_pos[1])] = (10, 0, int(agent_dir))
+    return out
+

@@ -405,6 +405,12 @@ int merlin_env_refill(merlin_env *e, void *stream) {
     return MERLIN_OK;
 }
 
+int merlin_env_full_obs(merlin_env *e, uint8_t *out, void *stream) {
+    if (!e || !out) return fail(MERLIN_E_INVALID, "null argument");
+    HIP_TRY(merlin::launch_env_full_obs(e->dev, out, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
 int merlin_env_get_state(merlin_env *e, uint32_t *walls, int32_t *agent, uint64_t *rng, void *stream) {
     if (!e) return fail(MERLIN_E_INVALID, "null env");
     hipStream_t s = (hipStream_t)stream;
@@ -878,15 +884,30 @@ int merlin_h3_split(const float *x, int64_t n, int32_t towers, const uint32_t *a
 
 int merlin_h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
                       int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride, const float *bias,
-                      float *C, int64_t c_stride, int32_t cfg, void *stream) {
+                      float *C, int64_t c_stride, void *a_planes, int32_t cfg, void *stream) {
     if (M < 0 || N <= 0 || K <= 0) return fail(MERLIN_E_INVALID, "bad shape");
     if (M > 0 && (!A || !B || !C || !amax_a || !amax_b)) return fail(MERLIN_E_INVALID, "null argument");
     if (K % 32) return fail(MERLIN_E_UNSUPPORTED, "K must be a multiple of 32");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (a_stride % 4 || b_stride % 8) return fail(MERLIN_E_INVALID, "tower strides: A multiple of 4, B of 8");
     const hipError_t e = merlin::launch_h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, bias, C,
-                                                   c_stride, cfg, (hipStream_t)stream);
+                                                   c_stride, a_planes, cfg, (hipStream_t)stream);
     if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "N not a multiple of the tile width / bad cfg");
+    HIP_TRY(e);
+    return MERLIN_OK;
+}
+
+static int h3_gemm_tn(const void *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t Kd,
+                      int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride, int32_t splits,
+                      float *slab, float *out, bool planes, int32_t cfg, void *stream) {
+    if (Kd < 0 || M <= 0 || N <= 0) return fail(MERLIN_E_INVALID, "bad shape");
+    if (!out || (Kd > 0 && (!A || !B || !slab || !amax_a || !amax_b))) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (splits < 1 || splits > merlin::x6_tn_max_splits()) return fail(MERLIN_E_INVALID, "splits out of range");
+    if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return fail(MERLIN_E_INVALID, "M, N: multiples of 8");
+    const hipError_t e = merlin::launch_h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits,
+                                                   slab, out, planes, cfg, (hipStream_t)stream);
+    if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "M / N not multiples of the tile / bad cfg");
     HIP_TRY(e);
     return MERLIN_OK;
 }
@@ -894,16 +915,15 @@ int merlin_h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, con
 int merlin_h3_gemm_tn(const float *A, const uint32_t *amax_a, const float *B, const uint32_t *amax_b, int64_t Kd,
                       int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride, int32_t splits,
                       float *slab, float *out, int32_t cfg, void *stream) {
-    if (Kd < 0 || M <= 0 || N <= 0) return fail(MERLIN_E_INVALID, "bad shape");
-    if (!out || (Kd > 0 && (!A || !B || !slab || !amax_a || !amax_b))) return fail(MERLIN_E_INVALID, "null argument");
-    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    if (splits < 1 || splits > merlin::x6_tn_max_splits()) return fail(MERLIN_E_INVALID, "splits out of range");
-    if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return fail(MERLIN_E_INVALID, "M, N: multiples of 8");
-    const hipError_t e = merlin::launch_h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits,
-                                                   slab, out, cfg, (hipStream_t)stream);
-    if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "M / N not multiples of the tile / bad cfg");
-    HIP_TRY(e);
-    return MERLIN_OK;
+    return h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, false, cfg,
+                      stream);
+}
+
+int merlin_h3_gemm_tn_planes(const void *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t Kd,
+                             int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride, int32_t splits,
+                             float *slab, float *out, int32_t cfg, void *stream) {
+    return h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, true, cfg,
+                      stream);
 }
 
 int64_t merlin_clip_adam_workspace(int32_t n_tensors, const int64_t *numel) {

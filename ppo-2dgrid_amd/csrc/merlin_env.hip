@@ -839,6 +839,37 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
     if (err) atomicOr(E.err, err);
 }
 
+// The fully observable image (FullyObsWrapper + ImgObsWrapper, scenario_creator.py:45-50; minigrid 3.0.0
+// wrappers.py FullyObsWrapper.observation, core/grid.py Grid.encode): out[env][x][y] = (object, color, state) of
+// cell (x, y) -- empty (1, 0, 0), wall (2, grey 5, 0), goal (8, green 1, 0) -- and the agent's cell
+// (agent 10, red 0, direction).  One thread per cell; the rows of walls are read as the bit rows the step keeps.
+__global__ __launch_bounds__(256) void k_env_full_obs(EnvDev E, uint8_t *__restrict__ out) {
+    const int S = E.size, cells = S * S;
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= (int64_t)E.n * cells) return;
+    const int i = (int)(c / cells), xy = (int)(c - (int64_t)i * cells), x = xy / S, y = xy - x * S;
+    const uint4 a = E.agent[i];
+    const int ax = a.x & 0xff, ay = (a.x >> 8) & 0xff, dir = (a.x >> 16) & 3;
+    const int gx = a.z & 0xff, gy = (a.z >> 8) & 0xff;
+    uint8_t o = 1, col = 0, st = 0;
+    if ((E.walls[(size_t)i * E.sp + y] >> x) & 1u) {
+        o = 2;
+        col = 5;
+    } else if (x == gx && y == gy) {
+        o = 8;
+        col = 1;
+    }
+    if (x == ax && y == ay) {
+        o = 10;
+        col = 0;
+        st = (uint8_t)dir;
+    }
+    uint8_t *p = out + c * 3;
+    p[0] = o;
+    p[1] = col;
+    p[2] = st;
+}
+
 }  // namespace
 
 template <int SP>
@@ -883,6 +914,13 @@ static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t 
 hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s) {
     hipError_t e = E.sp == 16 ? launch_step_sp<16>(E, O, s) : launch_step_sp<32>(E, O, s);
     return (e != hipSuccess || !refill) ? e : launch_env_refill(E, false, s);
+}
+
+hipError_t launch_env_full_obs(const EnvDev &E, uint8_t *out, hipStream_t s) {
+    const int64_t total = (int64_t)E.n * E.size * E.size;
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_env_full_obs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, E, out);
+    return hipGetLastError();
 }
 
 }  // namespace merlin

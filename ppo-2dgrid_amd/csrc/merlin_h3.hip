@@ -148,7 +148,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
                                                           const uint32_t *__restrict__ amaxA,
                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N, int K,
                                                           int64_t sA, int64_t sB, const float *__restrict__ bias,
-                                                          float *__restrict__ C, int64_t sC, int tiles_n) {
+                                                          float *__restrict__ C, int64_t sC, int tiles_n,
+    u32x4 *__restrict__ Pout) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -173,12 +174,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
 
     const float4 *ga[UA];
     int la[UA];
+    u32x4 *pa[UA];  // plane output of this unit (the first column tile's blocks write A's planes; else null)
 #pragma unroll
     for (int i = 0; i < UA; i++) {
         const int q = tid + i * NT;
         const int row = std::min(q >> 2, BM - 1), g = q & 3;
         ga[i] = reinterpret_cast<const float4 *>(A + t * sA + std::min<int64_t>(m0 + row, M - 1) * K) + g * 2;
         la[i] = row * 4 + (g ^ ((row >> 2) & 3));
+        pa[i] = Pout && tn == 0 && m0 + row < M ? Pout + (t * sA + (m0 + row) * K) / 4 + g * 2 : nullptr;
     }
     int gb[CB], lb[CB];
 #pragma unroll
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
 #pragma unroll
         for (int i = 0; i < CB; i++) rb[i] = B[gb[i] + kt * 8];
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int kt) {
         u32x4 *st = lds + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < UA; i++)
@@ -208,6 +211,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
                 h3_split8(ra[i][0], ra[i][1], scA, scA2, p0, p1);
                 st[la[i]] = p0;
                 st[PSA + la[i]] = p1;
+                if (pa[i]) {
+                    pa[i][kt * 8] = p0;
+                    pa[i][kt * 8 + 1] = p1;
+                }
             }
 #pragma unroll
         for (int i = 0; i < CB; i++)
@@ -226,12 +233,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
     const int fr = lane & 31, fh = lane >> 5, fs = (fr >> 2) & 3;
     const int nk = K / BK;
     load(0);
-    store(0);
+    store(0, 0);
     if (nk > 1) load(1);
     __syncthreads();
     for (int kt = 0; kt < nk; kt++) {
         const int buf = kt & 1;
-        if (kt + 1 < nk) store(buf ^ 1);
+        if (kt + 1 < nk) store(buf ^ 1, kt + 1);
         if (kt + 2 < nk) load(kt + 2);
         const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 2 * PSA;
         u32x4 bf[TN][2][2];
@@ -297,7 +304,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
                                                            const uint32_t *__restrict__ amaxB, int64_t M, int N,
                                                            int K, int64_t sA, int64_t sB,
                                                            const float *__restrict__ bias, float *__restrict__ C,
-                                                           int64_t sC, int tiles_n) {
+                                                           int64_t sC, int tiles_n,
+    u32x4 *__restrict__ Pout) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -324,12 +332,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
 
     const float4 *ga[UA];
     int la[UA];
+    u32x4 *pa[UA];
 #pragma unroll
     for (int i = 0; i < UA; i++) {
         const int q = tid + i * NT;
         const int row = q >> 2, g = q & 3;
         ga[i] = reinterpret_cast<const float4 *>(A + t * sA + std::min<int64_t>(m0 + row, M - 1) * K) + g * 2;
         la[i] = row * 4 + (g ^ ((row >> 2) & 3));
+        pa[i] = Pout && tn == 0 && m0 + row < M ? Pout + (t * sA + (m0 + row) * K) / 4 + g * 2 : nullptr;
     }
     int gb[CB], lb[CB];
 #pragma unroll
@@ -350,7 +360,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
 #pragma unroll
         for (int i = 0; i < CB; i++) rb[i] = B[gb[i] + kt * 8];
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int kt) {
         u32x4 *st = lds + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < UA; i++) {
@@ -358,6 +368,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
             h3_split8(ra[i][0], ra[i][1], scA, scA2, p0, p1);
             st[la[i]] = p0;
             st[PSA + la[i]] = p1;
+            if (pa[i]) {
+                pa[i][kt * 8] = p0;
+                pa[i][kt * 8 + 1] = p1;
+            }
         }
 #pragma unroll
         for (int i = 0; i < CB; i++) st[lb[i]] = rb[i];
@@ -407,14 +421,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
 
     const int nk = K / BK;  // >= 2 (K % 32 == 0, K >= 64: the launcher checks)
     load(0);
-    store(0);
+    store(0, 0);
     load(1);
     __syncthreads();
     int kt = 0;
     for (; kt + 2 < nk; kt++) {
         const int buf = kt & 1;
         compute(buf);
-        store(buf ^ 1);
+        store(buf ^ 1, kt + 1);
         load(kt + 2);
         // the fragment reads first, then each MFMA followed by a share of the split, the stores and the loads
         __builtin_amdgcn_sched_group_barrier(0x100, TM * 4 + TN * 4, 0);
@@ -428,7 +442,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
         __syncthreads();
     }
     compute(kt & 1);  // kt = nk - 2: stage the last step
-    store((kt & 1) ^ 1);
+    store((kt & 1) ^ 1, kt + 1);
     __syncthreads();
     compute((kt + 1) & 1);
 
@@ -646,44 +660,178 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
             }
 }
 
+// TN over operands already in plane form ([T][Kd][cols/8][2][8] f16 -- the a_planes output of the NT kernels, so
+// the fast step's weight gradient reads the planes its forward and input-gradient GEMMs made): k_h3_tn without the
+// split, staging a copy of 16-B chunks.  Thread q of a k row takes plane q / RC, chunk q % RC: the 8 lanes of a
+// ds_write_b128 group write 8 chunks of one plane image (8 distinct bank slots).
 template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tnq(const u32x4 *__restrict__ A, const u32x4 *__restrict__ B,
+                                                           const uint32_t *__restrict__ amaxA,
+                                                           const uint32_t *__restrict__ amaxB, int64_t Kd, int M,
+                                                           int N, int64_t sA, int64_t sB, int64_t kc, int tiles_n,
+                                                           int tiles, int S, float *__restrict__ slab) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int RCA = BM / 8, RCB = BN / 8;
+    constexpr int QA = BK * RCA * 2, QB = BK * RCB * 2;  // chunks per k step
+    constexpr int UA = QA / NT, UB = QB / NT;
+    static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile of 32 x 32 MFMA tiles");
+    static_assert(QA % NT == 0 && QB % NT == 0 && RCA % 8 == 0 && RCB % 8 == 0, "whole staging chunks per thread");
+    constexpr int PSA = BK * RCA, PSB = BK * RCB;
+    constexpr int STAGE = 2 * (PSA + PSB);
+    __shared__ u32x4 lds[2 * STAGE];
+
+    const int P = xcd_tile(blockIdx.x, gridDim.x);
+    const int t = P / (S * tiles), s = (P / tiles) % S, Lt = P % tiles;
+    const int tm = Lt / tiles_n, tn = Lt - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int64_t k0 = (int64_t)s * kc, k1 = std::min<int64_t>(Kd, k0 + kc);
+    const int eA = h3_exp(load_amax(amaxA + t)), eB = h3_exp(load_amax(amaxB + t));
+    const int64_t rowA = M / 4, rowB = N / 4;  // chunks per k row
+    A += t * sA + m0 / 4;
+    B += t * sB + n0 / 4;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    int ka[UA], la[UA], kb[UB], lb[UB];
+    const u32x4 *pa[UA], *pb[UB];
+#pragma unroll
+    for (int i = 0; i < UA; i++) {
+        const int q = tid + i * NT;
+        const int k = q / (2 * RCA), c = q - k * (2 * RCA), p = c / RCA, g = c - p * RCA;
+        ka[i] = k;
+        la[i] = p * PSA + k * RCA + (g ^ tr_swz<RCA>(k));
+        pa[i] = A + (k0 + k) * rowA + g * 2 + p;
+    }
+#pragma unroll
+    for (int i = 0; i < UB; i++) {
+        const int q = tid + i * NT;
+        const int k = q / (2 * RCB), c = q - k * (2 * RCB), p = c / RCB, g = c - p * RCB;
+        kb[i] = k;
+        lb[i] = 2 * PSA + p * PSB + k * RCB + (g ^ tr_swz<RCB>(k));
+        pb[i] = B + (k0 + k) * rowB + g * 2 + p;
+    }
+    u32x4 ra[UA], rb[UB];
+    auto load = [&](int64_t kk) {
+        if (kk + BK <= k1) {
+            const int64_t da = (kk - k0) * rowA, db = (kk - k0) * rowB;
+#pragma unroll
+            for (int i = 0; i < UA; i++) ra[i] = pa[i][da];
+#pragma unroll
+            for (int i = 0; i < UB; i++) rb[i] = pb[i][db];
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < UA; i++) ra[i] = pa[i][(std::min(kk + ka[i], k1 - 1) - k0 - ka[i]) * rowA];
+#pragma unroll
+        for (int i = 0; i < UB; i++) rb[i] = pb[i][(std::min(kk + kb[i], k1 - 1) - k0 - kb[i]) * rowB];
+    };
+    auto store = [&](int buf, int64_t kk) {
+        u32x4 *st = lds + buf * STAGE;
+        const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < UA; i++) st[la[i]] = kk + ka[i] < k1 ? ra[i] : zero;
+#pragma unroll
+        for (int i = 0; i < UB; i++) st[lb[i]] = kk + kb[i] < k1 ? rb[i] : zero;
+    };
+
+    f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = f32x16{};
+            lo[i][j] = f32x16{};
+        }
+
+    if (k0 < k1) {
+        load(k0);
+        store(0, k0);
+        if (k0 + BK < k1) load(k0 + BK);
+        __syncthreads();
+    }
+    int buf = 0;
+    for (int64_t kk = k0; kk < k1; kk += BK, buf ^= 1) {
+        if (kk + BK < k1) store(buf ^ 1, kk + BK);
+        if (kk + 2 * BK < k1) load(kk + 2 * BK);
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 2 * PSA;
+        u32x4 af[TM][2][2];
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++) af[i][kh][p] = tr_frag<RCA>(sAl + p * PSA, wm * WTM + i * 32, kh, lane);
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            u32x4 bf[2][2];
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++) bf[kh][p] = tr_frag<RCB>(sBl + p * PSB, wn * WTN + j * 32, kh, lane);
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                f32x16 l = lo[i][j], h = hi[i][j];
+#pragma unroll
+                for (int kh = 0; kh < 2; kh++) {
+                    l = mfma16(af[i][kh][1], bf[kh][0], l);
+                    l = mfma16(af[i][kh][0], bf[kh][1], l);
+                    h = mfma16(af[i][kh][0], bf[kh][0], h);
+                }
+                lo[i][j] = l;
+                hi[i][j] = h;
+            }
+        }
+        __syncthreads();
+    }
+
+    const float inv = pow2f(-eA), invB = pow2f(-eB);
+    float *St = slab + ((int64_t)s * (gridDim.x / (S * tiles)) + t) * (int64_t)M * N;
+    const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                St[(int64_t)row * N + n0 + wn * WTN + j * 32 + fr] =
+                    (hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB;
+            }
+}
+
+template <int BM, int BN, int WGM, int WGN, bool PIPE>
 hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
-                     int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
-    if (N % BN) return hipErrorInvalidValue;
+                     int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
+                     hipStream_t s) {
+    if (N % BN || (PIPE && K < 2 * BK)) return hipErrorInvalidValue;
     if ((int64_t)N * (K / 8) * 2 > INT32_MAX) return hipErrorInvalidValue;  // 32-bit B chunk offsets
     const int64_t tiles_m = (M + BM - 1) / BM;
     const int tiles_n = N / BN;
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)(tiles_m * tiles_n), T);
-    if (bias)
-        hipLaunchKernelGGL((k_h3_nt<BM, BN, WGM, WGN, 1>), grid, dim3(64 * WGM * WGN), 0, s, A, B, amaxA, amaxB, M, N,
-                           K, sA, sB, bias, C, sC, tiles_n);
-    else
-        hipLaunchKernelGGL((k_h3_nt<BM, BN, WGM, WGN, 0>), grid, dim3(64 * WGM * WGN), 0, s, A, B, amaxA, amaxB, M, N,
-                           K, sA, sB, nullptr, C, sC, tiles_n);
+    const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
+    if (PIPE) {
+        if (bias)
+            hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 1>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
+                               bias, C, sC, tiles_n, Pout);
+        else
+            hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 0>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
+                               nullptr, C, sC, tiles_n, Pout);
+    } else {
+        if (bias)
+            hipLaunchKernelGGL((k_h3_nt<BM, BN, WGM, WGN, 1>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
+                               bias, C, sC, tiles_n, Pout);
+        else
+            hipLaunchKernelGGL((k_h3_nt<BM, BN, WGM, WGN, 0>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
+                               nullptr, C, sC, tiles_n, Pout);
+    }
     return hipGetLastError();
 }
 
-template <int BM, int BN, int WGM, int WGN>
-hipError_t ntp_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
-                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
-    if (N % BN || K < 2 * BK) return hipErrorInvalidValue;
-    if ((int64_t)N * (K / 8) * 2 > INT32_MAX) return hipErrorInvalidValue;
-    const int64_t tiles_m = (M + BM - 1) / BM;
-    const int tiles_n = N / BN;
-    if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)(tiles_m * tiles_n), T);
-    if (bias)
-        hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 1>), grid, dim3(64 * WGM * WGN), 0, s, A, B, amaxA, amaxB, M, N,
-                           K, sA, sB, bias, C, sC, tiles_n);
-    else
-        hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 0>), grid, dim3(64 * WGM * WGN), 0, s, A, B, amaxA, amaxB, M, N,
-                           K, sA, sB, nullptr, C, sC, tiles_n);
-    return hipGetLastError();
-}
-
-template <int BM, int BN, int WGM, int WGN>
-hipError_t tn_launch(const float *A, const float *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t Kd, int M,
+// Q: the operands are plane images (k_h3_tnq), strides in values as for fp32 operands (4 B per value either way)
+template <int BM, int BN, int WGM, int WGN, bool Q>
+hipError_t tn_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t Kd, int M,
                      int N, int T, int64_t sA, int64_t sB, int splits, float *slab, int *S_out, hipStream_t s) {
     if (M % BM || N % BN) return hipErrorInvalidValue;
     const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
@@ -692,10 +840,20 @@ hipError_t tn_launch(const float *A, const float *B, const uint32_t *amaxA, cons
     kc = (kc + BK - 1) / BK * BK;
     S = (int)std::max<int64_t>(1, (Kd + kc - 1) / kc);
     *S_out = S;
-    hipLaunchKernelGGL((k_h3_tn<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
-                       reinterpret_cast<const float4 *>(A), reinterpret_cast<const float4 *>(B), amaxA, amaxB, Kd, M,
-                       N, sA / 4, sB / 4, kc, tiles_n, tiles, S, slab);
+    if (Q)
+        hipLaunchKernelGGL((k_h3_tnq<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
+                           static_cast<const u32x4 *>(A), static_cast<const u32x4 *>(B), amaxA, amaxB, Kd, M, N,
+                           sA / 4, sB / 4, kc, tiles_n, tiles, S, slab);
+    else
+        hipLaunchKernelGGL((k_h3_tn<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
+                           static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
+                           sA / 4, sB / 4, kc, tiles_n, tiles, S, slab);
     return hipGetLastError();
+}
+
+__global__ void k_h3_fill0(float4 *__restrict__ out, int64_t n4) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256)
+        out[e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
 }  // namespace
@@ -726,40 +884,53 @@ hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *ama
 
 hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
-                             int64_t c_stride, int cfg, hipStream_t s) {
+                             int64_t c_stride, void *a_planes, int cfg, hipStream_t s) {
     if (M <= 0) return hipSuccess;
     if (K % BK || N <= 0 || a_stride % 4 || b_stride % 8) return hipErrorInvalidValue;
     const u32x4 *b = static_cast<const u32x4 *>(B);
+    u32x4 *P = static_cast<u32x4 *>(a_planes);
     const int64_t sB = b_stride / 8 * 2;  // chunks
+#define H3_NT(BM, BN, WM, WN, PIPE) \
+    nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s)
     switch (cfg) {
-        case 0: return nt_launch<256, 128, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
-        case 1: return nt_launch<128, 192, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
-        case 2: return nt_launch<128, 128, 2, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
-        case 3: return nt_launch<128, 256, 2, 4>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        case 0: return H3_NT(256, 128, 4, 2, false);
+        case 1: return H3_NT(128, 192, 4, 2, false);
+        case 2: return H3_NT(128, 128, 2, 2, false);
+        case 3: return H3_NT(128, 256, 2, 4, false);
         // k_h3_ntp: the k step's split / staging interleaved into the MFMAs
-        case 10: return ntp_launch<256, 128, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
-        case 11: return ntp_launch<128, 192, 4, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
-        case 12: return ntp_launch<128, 128, 2, 2>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
-        case 13: return ntp_launch<128, 256, 2, 4>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, s);
+        case 10: return H3_NT(256, 128, 4, 2, true);
+        case 11: return H3_NT(128, 192, 4, 2, true);
+        case 12: return H3_NT(128, 128, 2, 2, true);
+        case 13: return H3_NT(128, 256, 2, 4, true);
         default: return hipErrorInvalidValue;
     }
+#undef H3_NT
 }
 
-hipError_t launch_h3_gemm_tn(const float *A, const uint32_t *amaxA, const float *B, const uint32_t *amaxB, int64_t Kd,
+hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t Kd,
                              int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits, float *slab,
-                             float *out, int cfg, hipStream_t s) {
+                             float *out, bool planes, int cfg, hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;
     if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
-    if (Kd <= 0) return hipMemsetAsync(out, 0, sizeof(float) * (size_t)T * M * N, s);
+    const int64_t total = (int64_t)T * M * N;
+    if (Kd <= 0) {  // a kernel, not a memset (capture-safe, see launch_h3_amax)
+        hipLaunchKernelGGL(k_h3_fill0, dim3((unsigned)std::min<int64_t>((total / 4 + 255) / 256, 2048)), dim3(256),
+                           0, s, reinterpret_cast<float4 *>(out), total / 4);
+        return hipGetLastError();
+    }
     int S = 1;
     hipError_t e;
+#define H3_TN(BM, BN, WM, WN)                                                                                     \
+    (planes ? tn_launch<BM, BN, WM, WN, true>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s) \
+            : tn_launch<BM, BN, WM, WN, false>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s))
     switch (cfg) {
-        case 0: e = tn_launch<128, 192, 4, 2>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s); break;
-        case 1: e = tn_launch<128, 192, 2, 2>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s); break;
+        case 0: e = H3_TN(128, 192, 4, 2); break;
+        case 1: e = H3_TN(128, 192, 2, 2); break;
         default: return hipErrorInvalidValue;
     }
+#undef H3_TN
     if (e != hipSuccess) return e;
-    return launch_x6_fold(slab, S, (int64_t)T * M * N, out, s);
+    return launch_x6_fold(slab, S, total, out, s);
 }
 
 }  // namespace merlin

@@ -69,6 +69,7 @@ struct StepOut {
 
 hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s);
 hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s);
+hipError_t launch_env_full_obs(const EnvDev &E, uint8_t *out, hipStream_t s);
 hipError_t launch_env_refill(const EnvDev &E, bool full, hipStream_t s);
 hipError_t upload_atlas(const uint8_t *atlas_host);
 hipError_t launch_obs_expand_f32(const uint32_t *codes, const int64_t *index, int64_t n, float *out,
@@ -184,12 +185,15 @@ hipError_t launch_x6_fold(const float *slab, int S, int64_t total, float *out, h
 // fc1 on the f16 matrix cores in two-plane form (merlin_h3.hip)
 hipError_t launch_h3_amax(const float *x, int64_t n, int T, int64_t stride, uint32_t *amax, hipStream_t s);
 hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *amax, void *planes, hipStream_t s);
+// a_planes (nullable): receives A's planes ([T][M][K/8][2][8] f16, A's byte layout), written by the first column
+// tile's blocks
 hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
-                             int64_t c_stride, int cfg, hipStream_t s);
-hipError_t launch_h3_gemm_tn(const float *A, const uint32_t *amaxA, const float *B, const uint32_t *amaxB, int64_t Kd,
+                             int64_t c_stride, void *a_planes, int cfg, hipStream_t s);
+// planes: A and B are plane images (an NT's a_planes) instead of fp32 tensors
+hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t Kd,
                              int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits, float *slab,
-                             float *out, int cfg, hipStream_t s);
+                             float *out, bool planes, int cfg, hipStream_t s);
 
 // clip_grad_norm_ + Adam step over a parameter list (merlin_optim.hip)
 constexpr int OPT_MAX_TENSORS = 32;

@@ -75,6 +75,7 @@ def lib():
     L.merlin_env_set_refill_interval.argtypes = [vp, i32]
     L.merlin_env_refill.argtypes = [vp, vp]
     L.merlin_env_get_state.argtypes = [vp, vp, vp, vp, vp]
+    L.merlin_env_full_obs.argtypes = [vp, vp, vp]
     L.merlin_env_errors.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), vp]
     L.merlin_obs_expand_f32.argtypes = [vp, vp, i64, vp, C.c_float, i32, vp]
     L.merlin_obs_expand_u8.argtypes = [vp, vp, i64, vp, vp]
@@ -127,8 +128,9 @@ def lib():
     L.merlin_x6_gemm_tn.argtypes = [vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
     L.merlin_h3_amax.argtypes = [vp, i64, i32, i64, vp, vp]
     L.merlin_h3_split.argtypes = [vp, i64, i32, vp, vp, vp]
-    L.merlin_h3_gemm_nt.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, i32, vp]
+    L.merlin_h3_gemm_nt.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, vp, i32, vp]
     L.merlin_h3_gemm_tn.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
+    L.merlin_h3_gemm_tn_planes.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
     L.merlin_stage_tables_fwd.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_stage_tables_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     check_env_config_layout(L)
@@ -159,7 +161,7 @@ EXPORTED_SYMBOLS = (
     "merlin_version", "merlin_last_error", "merlin_tile_atlas", "merlin_env_config_layout", "merlin_env_create",
     "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step",
     "merlin_env_set_refill_interval", "merlin_env_refill",
-    "merlin_env_get_state", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
+    "merlin_env_get_state", "merlin_env_full_obs", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
     "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
     "merlin_conv1_lut_fwd", "merlin_conv1_lut_bwd", "merlin_tower_conv2_im2col_fwd",
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
@@ -173,6 +175,7 @@ EXPORTED_SYMBOLS = (
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
     "merlin_clip_adam_workspace", "merlin_clip_adam",
     "merlin_h3_amax", "merlin_h3_split", "merlin_h3_gemm_nt", "merlin_h3_gemm_tn",
+    "merlin_h3_gemm_tn_planes",
 )
 
 
@@ -906,9 +909,10 @@ def h3_split(x: torch.Tensor, amax: torch.Tensor, out: torch.Tensor | None = Non
 
 def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,
                bias: torch.Tensor | None = None, cfg: int = 0, out: torch.Tensor | None = None,
-               name: str = "h3_gemm_nt") -> torch.Tensor:
+               name: str = "h3_gemm_nt", planes_out: torch.Tensor | None = None) -> torch.Tensor:
     """C f32[T, M, N] = A @ B^T per tower (+ bias[t] and ReLU when bias is given), A f32[T, M, K] with its h3_amax,
-    B planes int16[T, N, 2K] (h3_split of an f32 [T, N, K] with amaxB)."""
+    B planes int16[T, N, 2K] (h3_split of an f32 [T, N, K] with amaxB).  planes_out int16[T, M, 2K], if given,
+    receives A's planes (h3_split(A, amaxA), made by the kernel while it stages A) for a later h3_gemm_tn."""
     T, M, K = (int(v) for v in A.shape)
     N = int(B.shape[1])
     assert A.dtype == torch.float32 and B.dtype == torch.int16 and B.shape == (T, N, 2 * K)
@@ -918,9 +922,12 @@ def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
     assert out.shape == (T, M, N) and out.is_contiguous()
     if bias is not None:
         assert bias.shape == (T, N) and bias.is_contiguous()
+    if planes_out is not None:
+        assert planes_out.dtype == torch.int16 and planes_out.shape == (T, M, 2 * K) and planes_out.is_contiguous()
     with KernelTimer.span(name, 0, 2 * T * M * N * K):
         check(lib().merlin_h3_gemm_nt(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, T, M * K, N * K,
-                                      ptr(bias) if bias is not None else None, ptr(out), M * N, int(cfg),
+                                      ptr(bias) if bias is not None else None, ptr(out), M * N,
+                                      ptr(planes_out) if planes_out is not None else None, int(cfg),
                                       stream_of(A)), "merlin_h3_gemm_nt")
     return out
 
@@ -929,21 +936,29 @@ def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
                splits: int | None = None, cfg: int | None = None, name: str = "h3_gemm_tn",
                out: torch.Tensor | None = None) -> torch.Tensor:
     """out f32[T, M, N] = A^T @ B per tower, A f32[T, Kd, M], B f32[T, Kd, N] with their h3_amax (the long k range
-    split into `splits` slabs summed in order)."""
+    split into `splits` slabs summed in order).  A and B may instead both be planes, int16[T, Kd, 2M] / [T, Kd, 2N]
+    (h3_gemm_nt's planes_out of the same tensors and scales): the same product without splitting them again."""
     splits = H3_TN_SPLITS if splits is None else splits
     cfg = H3_TN_CFG if cfg is None else cfg
+    planes = A.dtype == torch.int16
     T, Kd, M = (int(v) for v in A.shape)
     N = int(B.shape[2])
-    assert A.dtype == B.dtype == torch.float32 and B.shape[:2] == (T, Kd)
+    if planes:
+        assert B.dtype == torch.int16 and M % 2 == 0 and N % 2 == 0
+        M, N = M // 2, N // 2
+    else:
+        assert A.dtype == B.dtype == torch.float32
+    assert B.shape[:2] == (T, Kd)
     assert A.is_contiguous() and B.is_contiguous() and amaxA.dtype == amaxB.dtype == torch.int32
     if out is None:
         out = torch.empty((T, M, N), dtype=torch.float32, device=A.device)
     assert out.shape == (T, M, N) and out.dtype == torch.float32 and out.is_contiguous()
     slab = torch.empty(int(lib().merlin_x6_tn_slab_floats(M, N, T, int(splits))), dtype=torch.float32,
                        device=A.device)
+    fn = lib().merlin_h3_gemm_tn_planes if planes else lib().merlin_h3_gemm_tn
     with KernelTimer.span(name, 0, 2 * T * M * N * Kd):
-        check(lib().merlin_h3_gemm_tn(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), Kd, M, N, T, Kd * M, Kd * N,
-                                      int(splits), ptr(slab), ptr(out), int(cfg), stream_of(A)), "merlin_h3_gemm_tn")
+        check(fn(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), Kd, M, N, T, Kd * M, Kd * N, int(splits), ptr(slab),
+                 ptr(out), int(cfg), stream_of(A)), "merlin_h3_gemm_tn")
     return out
 
 

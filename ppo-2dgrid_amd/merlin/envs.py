@@ -212,6 +212,19 @@ class MerlinVecEnv:
         codes = self.obs if codes is None else codes
         return nat.expand_obs_u8(codes.reshape(-1, nat.OBS_WORDS))
 
+    def render_full(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        """uint8[N, size, size, 3]: the fully observable observation of every env's current state
+        (observation.fully_observable: FullyObsWrapper + ImgObsWrapper, src/scenario_creator/scenario_creator.py:45-50),
+        out[i, x, y] = (object, color, state) of cell (x, y) as minigrid's Grid.encode, the agent's cell (10, 0, dir)
+        (merlin_env_full_obs)."""
+        S = self.size
+        if out is None:
+            out = torch.empty((self.num_envs, S, S, 3), dtype=torch.uint8, device=self.device)
+        assert out.dtype == torch.uint8 and out.is_contiguous() and out.numel() == self.num_envs * S * S * 3
+        with torch.cuda.device(self.device):
+            nat.check(self._lib.merlin_env_full_obs(self._h, nat.ptr(out), self._stream), "merlin_env_full_obs")
+        return out
+
     # -- introspection (host syncs; tests / tooling) --------------------------
     def get_state(self) -> dict:
         n, S = self.num_envs, self.size
@@ -255,10 +268,18 @@ class MerlinEnv:
     reference on a GPU device (src/ppo.py:59,76); use ``MerlinVecEnv`` for speed.
     """
 
-    def __init__(self, difficulty: str = "mediumhard", size: int = 16, device="cuda", **kw):
+    def __init__(self, difficulty: str = "mediumhard", size: int = 16, device="cuda", fully_observable: bool = False,
+                 flatten: bool = False, **kw):
         self.vec = MerlinVecEnv(1, difficulty=difficulty, size=size, device=device, **kw)
         self.action_space = self.vec.action_space
-        self.observation_space = self.vec.single_observation_space
+        # the reference's observation options (src/config/scenario.yaml observation.*,
+        # src/scenario_creator/scenario_creator.py:45-53): the RGB partial view (default) or the encoded full grid,
+        # either flattened to a vector by FlattenObservation
+        self.fully_observable, self.flatten = bool(fully_observable), bool(flatten)
+        shape = (self.vec.size, self.vec.size, 3) if self.fully_observable else (56, 56, 3)
+        if self.flatten:
+            shape = (int(np.prod(shape)),)
+        self.observation_space = Box(0, 255, shape, np.uint8)
         self.max_steps = self.vec.max_steps
         self._done = True
 
@@ -271,7 +292,9 @@ class MerlinEnv:
         return tuple(int(v) for v in self.vec.get_state()["agent_pos"][0])
 
     def _frame(self) -> np.ndarray:
-        return self.vec.render_rgb()[0].cpu().numpy()
+        img = self.vec.render_full() if self.fully_observable else self.vec.render_rgb()
+        img = img[0].cpu().numpy()
+        return img.reshape(-1) if self.flatten else img
 
     def reset(self, seed: int | None = None, options=None):
         if seed is not None:

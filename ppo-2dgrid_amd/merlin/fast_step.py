@@ -180,6 +180,9 @@ class WeightStage:
 # too) or from after the input gradient (False: beside conv3's segmented sums only)
 WGRAD_EARLY = False
 WGRAD_SIDE = True  # False: the weight gradient on the main stream (diagnostics)
+# h3: the weight gradient over the planes the NT GEMMs left (False: it splits a3, dz itself).  Off: the planes cost the
+# forward 60-100 us of writes (a3: 2 x U x 576 x 4 B) for 50 us saved in the weight gradient (scripts/probe_h3.py)
+WGRAD_PLANES = False
 
 
 class WindowStep:
@@ -262,8 +265,14 @@ class WindowStep:
         Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None)
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
+        pa3 = pdz = None
         if h3:
-            h = nat.h3_gemm_nt(a3, am3, P4, amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd")
+            # the forward and input-gradient GEMMs leave their fp32 operand's planes (a3's, dz's) for the weight
+            # gradient, which then stages copies instead of splitting both operands again
+            if WGRAD_PLANES:
+                pa3 = torch.empty((2, n, 1152), dtype=torch.int16, device=a3.device)
+            h = nat.h3_gemm_nt(a3, am3, P4, amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd",
+                               planes_out=pa3)
         else:
             h = nat.x6_gemm_nt(a3, P4, bias=b4, cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
         logits, value = nat.heads_fwd(h, Wa, Wc)  # both heads in one pass over h (the loss adds their biases)
@@ -279,7 +288,9 @@ class WindowStep:
         side = self.side_stream(dz.device)
 
         def wgrad():
-            if h3:
+            if h3 and pdz is not None:
+                nat.h3_gemm_tn(pdz, amz, pa3, am3, name="gemm_wgrad", out=g[4])
+            elif h3:
                 nat.h3_gemm_tn(dz, amz, a3, am3, name="gemm_wgrad", out=g[4])
             else:
                 nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
@@ -289,7 +300,10 @@ class WindowStep:
             with torch.cuda.stream(side):
                 wgrad()
         if h3:
-            da3 = nat.h3_gemm_nt(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
+            if pa3 is not None and not WGRAD_EARLY:
+                pdz = torch.empty((2, n, 1024), dtype=torch.int16, device=dz.device)
+            da3 = nat.h3_gemm_nt(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad"], name="gemm_fc1_dgrad",
+                                 planes_out=pdz)
         else:
             da3 = nat.x6_gemm_nt(dz, P4t, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
         if not WGRAD_SIDE:
@@ -298,8 +312,9 @@ class WindowStep:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 wgrad()
-        dz.record_stream(side)
-        a3.record_stream(side)
+        for x in (dz, a3, pdz, pa3):
+            if x is not None:
+                x.record_stream(side)
         dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]))
         nat.colsum(dQ.view(2, -1, 9, 64)[:, :, 0], out=g[3])  # db3: every (u, p3) has one window at tap 0
         dQ = dQ.view(2, -1, 576)

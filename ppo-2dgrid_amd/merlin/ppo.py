@@ -120,6 +120,10 @@ class PPO:
         self.episode_lengths: list[int] = []
 
         self.vec = env.vec if isinstance(env, MerlinEnv) else env if isinstance(env, MerlinVecEnv) else None
+        if isinstance(env, MerlinEnv) and (env.fully_observable or env.flatten):
+            # the observation options (scenario.yaml observation.*): the reference's generic env loop, an MLP on a
+            # flattened observation (src/ppo.py:38-45) or the CNN on the (size, size, 3) grid encoding
+            self.vec = None
         act_dim = env.action_space.n
         if self.vec is not None:
             N = self.vec.num_envs

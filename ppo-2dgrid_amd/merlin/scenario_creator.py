@@ -52,18 +52,27 @@ class ScenarioCreator:
         cfg = self.config["difficulties"].get(difficulty)
         if not cfg:
             raise ValueError(f"Unknown difficulty: {difficulty}")
-        if self.obs_cfg.get("fully_observable", False) or self.obs_cfg.get("flatten", False):
-            raise NotImplementedError("only the RGB partial-observation mode is implemented on the GPU path")
         kw = {**self.global_cfg, **cfg.get("params", {})}
         kw.pop("render_mode", None)
         gen = _ENV_IDS.get(cfg["env_id"], difficulty)
         return {"difficulty": gen, "size": int(kw.pop("size", 16)), **kw}
 
     def create_env(self, difficulty: str = "easy", seed=None, device="cuda", **flags):
-        return MerlinEnv(device=device, **self._env_kwargs(difficulty), **flags)
+        """The single env of scenario_creator.py:35-57 with the configured observation wrappers (observation.
+        fully_observable: the encoded full grid instead of the RGB partial view; observation.flatten: as a vector)."""
+        obs = {"fully_observable": bool(self.obs_cfg.get("fully_observable", False)),
+               "flatten": bool(self.obs_cfg.get("flatten", False))}
+        return MerlinEnv(device=device, **self._env_kwargs(difficulty), **obs, **flags)
 
     def create_vec_env(self, difficulty: str, num_envs: int, seed=None, device="cuda", env_offset: int = 0,
                        **flags) -> MerlinVecEnv:
+        """N envs for the batched trainer.  Their step produces the RGB partial view's tile codes (the only
+        observation the reference's CNNActorCritic can train on: the full grid is 16 x 16, smaller than its conv
+        stack's receptive field, and a flattened vector has no (h, w, c) shape); the full grid of any state is
+        MerlinVecEnv.render_full."""
+        if self.obs_cfg.get("fully_observable", False) or self.obs_cfg.get("flatten", False):
+            raise ValueError("CNNActorCritic trains on the (56, 56, 3) RGB partial view (src/actor_critic.py:22-28); "
+                             "observation.fully_observable / flatten give observations it cannot take")
         return MerlinVecEnv(num_envs, seed=seed, device=device, env_offset=env_offset,
                             **self._env_kwargs(difficulty), **flags)
 

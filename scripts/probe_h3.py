@@ -39,6 +39,7 @@ def main():
     am3 = nat.h3_amax(a3)
     amz = nat.h3_amax(dz)
     flop = 2 * 2 * U * 576 * 512
+    pa3, pdz = nat.h3_split(a3, am3), nat.h3_split(dz, amz)
     runs = {
         "x6 fwd": (lambda: nat.x6_gemm_nt(a3, Wp, bias=b, cfg=nat.X6_NT_CFG["fwd"]), 6),
         "h3 fwd": (lambda: nat.h3_gemm_nt(a3, am3, Hp, amW, bias=b, cfg=cf), 3),
@@ -46,6 +47,8 @@ def main():
         "h3 dgrad": (lambda: nat.h3_gemm_nt(dz, amz, Htp, amWt, cfg=cd), 3),
         "x6 wgrad": (lambda: nat.x6_gemm_tn(dz, a3), 6),
         "h3 wgrad": (lambda: nat.h3_gemm_tn(dz, amz, a3, am3, cfg=ct), 3),
+        "h3 wgrad pl": (lambda: nat.h3_gemm_tn(pdz, amz, pa3, am3, cfg=ct), 3),
+        "h3 fwd +pl": (lambda: nat.h3_gemm_nt(a3, am3, Hp, amW, bias=b, cfg=cf, planes_out=pa3), 3),
         "h3 amax a3": (lambda: nat.h3_amax(a3, out=am3), 0),
     }
     res = {k: [] for k in runs}

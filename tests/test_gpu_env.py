@@ -263,3 +263,62 @@ def test_single_env_gym_api(device, golden):
     assert env.action_space.n == 3
     with pytest.raises(IndexError):
         env.step(3)
+
+
+@pytest.mark.parametrize("diff,size", [("mediumhard", 16), ("hard", 22), ("hardest", 16)])
+def test_full_observation_vs_state(device, diff, size):
+    """merlin_env_full_obs (observation.fully_observable: FullyObsWrapper + ImgObsWrapper) equals the bit-row
+    restatement of minigrid's Grid.encode (oracle/minigrid_literal.full_obs_from_state) on the state the env reports,
+    after resets and random steps with auto-reset."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    from minigrid_literal import full_obs_from_state
+
+    env = make_env(300, diff, size, 11, device)
+    env.reset()
+    g = torch.Generator(device=device).manual_seed(4)
+    for k in range(12):
+        if k:
+            env.step(torch.randint(0, 3, (300,), device=device, generator=g))
+        full = env.render_full().cpu().numpy()
+        st = env.get_state()
+        assert full.shape == (300, size, size, 3)
+        for i in range(0, 300, 7):
+            want = full_obs_from_state(st["walls"][i], st["agent_pos"][i], st["agent_dir"][i], st["goal_pos"][i], size)
+            assert np.array_equal(full[i], want), (k, i)
+
+
+def test_single_env_observation_modes(device, tmp_path):
+    """The single env's observation options (scenario_creator.py:45-53): the full grid encoding, flattened or not,
+    and the flattened RGB view; PPO takes a flattened observation down the reference's MLP path (src/ppo.py:38-41)."""
+    from merlin import MerlinEnv
+    from merlin.actor_critic import MLPActorCritic
+    from merlin.ppo import PPO
+    from merlin.scenario_creator import ScenarioCreator
+
+    full = MerlinEnv("easy", device=device, fully_observable=True)
+    obs, _ = full.reset(seed=5)
+    assert obs.shape == (16, 16, 3) and obs.dtype == np.uint8 and full.observation_space.shape == (16, 16, 3)
+    ax, ay = full.agent_pos
+    assert obs[ax, ay, 0] == 10
+    flat = MerlinEnv("easy", device=device, fully_observable=True, flatten=True)
+    fobs, _ = flat.reset(seed=5)
+    assert fobs.shape == (768,) and np.array_equal(fobs, obs.reshape(-1))
+    o2, *_ = flat.step(2)
+    o1, *_ = full.step(2)
+    assert np.array_equal(o2, o1.reshape(-1))
+    rgb = MerlinEnv("easy", device=device, flatten=True)
+    robs, _ = rgb.reset(seed=5)
+    assert robs.shape == (56 * 56 * 3,)
+    p = tmp_path / "s.yaml"
+    p.write_text("observation:\n  fully_observable: true\n  flatten: true\n"
+                 "difficulties:\n  easy:\n    env_id: MERLIN-Easy-v0\n    params:\n      size: 16\n")
+    env = ScenarioCreator(str(p)).create_env("easy")
+    assert env.observation_space.shape == (768,)
+    torch.manual_seed(0)
+    agent = PPO(env, batch_size=64, minibatch_size=32, update_epochs=1, device=device)
+    assert isinstance(agent.ac, MLPActorCritic) and agent.obs_shape == (768,)
+    stats = agent.update(agent.collect_rollouts())
+    assert all(np.isfinite(v) for v in stats.values())

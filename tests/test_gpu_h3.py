@@ -77,6 +77,9 @@ def test_gemm_nt_vs_float64(device, M, N, K, cfg, scale_a, ragged):
     Cb = nat.h3_gemm_nt(A, amA, Bp, amB, bias=bias, cfg=cfg)
     assert torch.equal(Cb, torch.relu(C + bias.unsqueeze(1)))
     assert torch.equal(C, nat.h3_gemm_nt(A, amA, Bp, amB, cfg=cfg))  # fixed order: the same bits every call
+    P = torch.full((2, M, 2 * K), 0x5555, dtype=torch.int16, device=device)
+    Cp = nat.h3_gemm_nt(A, amA, Bp, amB, cfg=cfg, planes_out=P)  # A's planes as a by-product: h3_split's exactly
+    assert torch.equal(Cp, C) and torch.equal(P, nat.h3_split(A, amA))
 
 
 @pytest.mark.parametrize("cfg", [0, 1])
@@ -91,9 +94,13 @@ def test_gemm_tn_vs_float64(device, Kd, splits, scale, cfg):
     W64 = torch.bmm(dz.double().transpose(1, 2), a3.double())
     den = torch.bmm(dz.abs().double().transpose(1, 2), a3.abs().double())
     tol = max(_err(torch.bmm(dz.transpose(1, 2), a3), W64, den), FLOOR)
-    W = nat.h3_gemm_tn(dz, nat.h3_amax(dz), a3, nat.h3_amax(a3), splits=splits, cfg=cfg)
+    amz, am3 = nat.h3_amax(dz), nat.h3_amax(a3)
+    W = nat.h3_gemm_tn(dz, amz, a3, am3, splits=splits, cfg=cfg)
     assert _err(W, W64, den) <= tol
-    assert torch.equal(W, nat.h3_gemm_tn(dz, nat.h3_amax(dz), a3, nat.h3_amax(a3), splits=splits, cfg=cfg))
+    assert torch.equal(W, nat.h3_gemm_tn(dz, amz, a3, am3, splits=splits, cfg=cfg))
+    # over the operands' planes (what the fast step's NT GEMMs leave): the same images, the same bits
+    Wq = nat.h3_gemm_tn(nat.h3_split(dz, amz), amz, nat.h3_split(a3, am3), am3, splits=splits, cfg=cfg)
+    assert torch.equal(Wq, W)
 
 
 @pytest.mark.parametrize("cfg", [0, 1])

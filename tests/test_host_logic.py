@@ -1,6 +1,8 @@
 """CPU: host-side logic mirrored from the reference (no GPU calls)."""
 import os
+import sys
 
+import numpy as np
 import pytest
 
 
@@ -28,13 +30,41 @@ def test_scenario_config_surface():
         ScenarioCreator("/nonexistent.yaml")
 
 
-def test_scenario_rejects_unsupported_observation_modes(tmp_path):
+def test_scenario_observation_modes(tmp_path):
+    """observation.fully_observable / flatten reach the single env (scenario_creator.py:45-53); the batched trainer's
+    vec env refuses them (CNNActorCritic cannot take those observations, src/actor_critic.py:22-28)."""
     from merlin.scenario_creator import ScenarioCreator
 
     p = tmp_path / "s.yaml"
     p.write_text("observation:\n  fully_observable: true\ndifficulties:\n  easy:\n    env_id: MERLIN-Easy-v0\n")
-    with pytest.raises(NotImplementedError):
-        ScenarioCreator(str(p))._env_kwargs("easy")
+    sc = ScenarioCreator(str(p))
+    assert sc._env_kwargs("easy")["difficulty"] == "easy"
+    with pytest.raises(ValueError):
+        sc.create_vec_env("easy", 4)
+
+
+def test_full_observation_restatements_agree():
+    """The object-level FullyObsWrapper restatement and the bit-row one (merlin_env_full_obs's checker) agree over
+    reset and random steps of every difficulty."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    from minigrid_literal import LiteralEnv, full_obs_from_state
+
+    rng = np.random.default_rng(0)
+    for diff in ("easy", "medium", "mediumhard", "hard", "hardest"):
+        env = LiteralEnv(16, diff)
+        env.reset(seed=int(rng.integers(1 << 30)))
+        for _ in range(20):
+            cells = env.cells()
+            walls = [sum(1 << x for x in range(16) if cells[y, x] == 1) for y in range(16)]
+            goal = [(x, y) for y in range(16) for x in range(16) if cells[y, x] == 2][0]
+            full = env.full_obs()
+            assert full.shape == (16, 16, 3)
+            assert np.array_equal(full, full_obs_from_state(walls, env.agent_pos, env.agent_dir, goal, 16))
+            assert tuple(full[env.agent_pos[0], env.agent_pos[1]]) == (10, 0, env.agent_dir)
+            assert (full[0, :, 0] == 2).all() and (full[:, 15, 0] == 2).all()  # the outer walls
+            _, _, term, trunc = env.step(int(rng.integers(3)))
+            if term or trunc:
+                break
 
 
 def test_cli_flags_match_reference_defaults():
