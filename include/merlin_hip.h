@@ -342,6 +342,18 @@ int merlin_segment_sum_marked(const float *src_dev, const void *mask_dev, int64_
                               const int32_t *fix_dev, int64_t n_fix, int32_t towers, float *out_dev,
                               int64_t out_rows, float *carry_dev, int32_t flags, int32_t *mark_dev,
                               void *stream);
+/* merlin_segment_sum_marked with the destinations that span items finished inside the launch (no second fix-up
+ * launch): head_fix_dev int32[n_items] = the fix row (the item) at which item i's first destination started when it
+ * continues into item i, else -1; counters_dev int32[n_fix] zero before the first call (the launch leaves them zero).
+ * Requires one fix row per item (n_fix = ceil(nnz / item_len), as merlin/windows.py SegmentPlan builds it).  The
+ * item that completes a row adds the row's partial sums in the fix-up pass's order: the same bits as
+ * merlin_segment_sum_marked.  Both NULL: that function. */
+int merlin_segment_sum_fused(const float *src_dev, const void *mask_dev, int64_t src_rows,
+                             const int32_t *idx_dev, const int32_t *key_dev, int64_t nnz,
+                             const int32_t *slot_dev, int32_t sub, int64_t item_len,
+                             const int32_t *fix_dev, int64_t n_fix, int32_t towers, float *out_dev,
+                             int64_t out_rows, float *carry_dev, int32_t flags, int32_t *mark_dev,
+                             const int32_t *head_fix_dev, int32_t *counters_dev, void *stream);
 
 /* Acting tail (src/actor_critic.py:48-55 act, src/ppo.py:69-71): z float[2][n][hidden] = fc1's
  * pre-activation of the actor / critic tower, b4 float[2][hidden]; h = relu(z + b4); logits =

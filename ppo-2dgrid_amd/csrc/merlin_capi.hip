@@ -667,23 +667,35 @@ int merlin_tower_codes_conv3(const uint32_t *codes, int64_t n, const float *Qall
     return MERLIN_OK;
 }
 
-int merlin_segment_sum_marked(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,
-                              const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub, int64_t item_len,
-                              const int32_t *fix, int64_t n_fix, int32_t towers, float *out, int64_t out_rows,
-                              float *carry, int32_t flags, int32_t *mark, void *stream) {
+int merlin_segment_sum_fused(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,
+                             const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub, int64_t item_len,
+                             const int32_t *fix, int64_t n_fix, int32_t towers, float *out, int64_t out_rows,
+                             float *carry, int32_t flags, int32_t *mark, const int32_t *head_fix, int32_t *counters,
+                             void *stream) {
     if (!out && out_rows > 0) return fail(MERLIN_E_INVALID, "null output");
     if (nnz > 0 && (!src || !idx || !key || !carry)) return fail(MERLIN_E_INVALID, "null argument");
     if (n_fix > 0 && !fix) return fail(MERLIN_E_INVALID, "null fix-up list");
+    if ((head_fix == nullptr) != (counters == nullptr)) return fail(MERLIN_E_INVALID, "head_fix and counters go together");
+    if (counters && nnz > 0 && n_fix != (nnz + item_len - 1) / item_len)
+        return fail(MERLIN_E_INVALID, "in-launch fix-ups need one fix row per item");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (item_len <= 0 || sub <= 0) return fail(MERLIN_E_INVALID, "item_len and sub must be > 0");
     if (flags & ~(MERLIN_SEG_ACCUMULATE | MERLIN_SEG_NO_FILL | MERLIN_SEG_MASK_BITS | MERLIN_SEG_ROLE_MASK))
         return fail(MERLIN_E_INVALID, "unknown flags");
-    HIP_TRY(merlin::launch_seg_sum(src, mask, (flags & MERLIN_SEG_MASK_BITS) ? 1 : 0, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
-                                   out_rows, carry, (flags & MERLIN_SEG_ACCUMULATE) ? 1 : 0,
-                                   (flags & MERLIN_SEG_NO_FILL) ? 0 : 1,
-                                   (flags & MERLIN_SEG_ROLE_MASK) >> MERLIN_SEG_ROLE_SHIFT, mark,
+    HIP_TRY(merlin::launch_seg_sum(src, mask, (flags & MERLIN_SEG_MASK_BITS) ? 1 : 0, src_rows, idx, key, nnz, slot,
+                                   sub, item_len, fix, n_fix, towers, out, out_rows, carry,
+                                   (flags & MERLIN_SEG_ACCUMULATE) ? 1 : 0, (flags & MERLIN_SEG_NO_FILL) ? 0 : 1,
+                                   (flags & MERLIN_SEG_ROLE_MASK) >> MERLIN_SEG_ROLE_SHIFT, mark, head_fix, counters,
                                    (hipStream_t)stream));
     return MERLIN_OK;
+}
+
+int merlin_segment_sum_marked(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,
+                              const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub, int64_t item_len,
+                              const int32_t *fix, int64_t n_fix, int32_t towers, float *out, int64_t out_rows,
+                              float *carry, int32_t flags, int32_t *mark, void *stream) {
+    return merlin_segment_sum_fused(src, mask, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
+                                    out_rows, carry, flags, mark, nullptr, nullptr, stream);
 }
 
 int merlin_segment_sum_masked(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,

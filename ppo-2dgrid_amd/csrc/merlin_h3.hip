@@ -467,6 +467,223 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
 }
 
 // ---------------------------------------------------------------------------------------------------------------
+// The NT product with both operands staged by LDS-DMA (global_load_lds_dwordx4) three k steps deep: k_h3_nt's one
+// step of register prefetch left every k step waiting on the global loads issued one step before (PMC: a third of
+// the wave cycles in s_waitcnt, LDS waits 4 %, MFMA busy 38 %).  Here a k step's A (fp32, 128 B per row) and B
+// (planes, 128 B per row) go straight into LDS two steps ahead, with no staging registers and no ds_write pass;
+// each wave splits its own A fragments after reading them (the A values a wave reads are split by the WGN waves of
+// its row band).  LDS images: rows of 8 16-B chunks, chunk c of row r at c ^ ((r >> 1) & 7) -- a DMA writes 1 KB
+// lane-linear, so the permutation is applied to the global source address; a fragment read (16 lanes of a
+// ds_read_b128 group, 16 different rows, one chunk) then hits 16 distinct 16-B bank slots.  Raw s_barrier with
+// counted vmcnt: the DMA of step kt + 2 stays in flight across the barrier that publishes step kt + 1.
+__device__ __forceinline__ int g_swz(int r) { return (r >> 1) & 7; }
+
+template <int BM, int BN, int WGM, int WGN, int EPI, bool KP>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restrict__ A, const u32x4 *__restrict__ B,
+                                                           const uint32_t *__restrict__ amaxA,
+                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N,
+                                                           int K, int64_t sA, int64_t sB,
+                                                           const float *__restrict__ bias, float *__restrict__ C,
+                                                           int64_t sC, int tiles_n) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int GA = BM * 8 / NT, GB = BN * 8 / NT;  // DMA instructions per thread and k step
+    constexpr int G = GA + GB;
+    constexpr int STG = (BM + BN) * 8;  // chunks per stage
+    static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile of 32 x 32 MFMA tiles");
+    static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "whole DMA instructions per thread");
+    __shared__ u32x4 lds[3 * STG];
+
+    const int t = blockIdx.y;
+    const int L = xcd_tile(blockIdx.x, gridDim.x);
+    const int tm = L / tiles_n, tn = L - tm * tiles_n;
+    const int64_t m0 = (int64_t)tm * BM;
+    const int n0 = tn * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+    const int64_t rowB = (int64_t)(K / 8) * 2;  // chunks per B row
+
+    // DMA sources: the chunk lane q of instruction i lands on is LDS chunk i NT + q (row q >> 3 of the image)
+    const float *srcA[GA];
+    const u32x4 *srcB[GB];
+#pragma unroll
+    for (int i = 0; i < GA; i++) {
+        const int q = i * NT + tid, r = q >> 3, c = (q & 7) ^ g_swz(r);
+        srcA[i] = A + t * sA + std::min<int64_t>(m0 + r, M - 1) * K + c * 4;
+    }
+#pragma unroll
+    for (int i = 0; i < GB; i++) {
+        const int q = i * NT + tid, r = q >> 3, c = (q & 7) ^ g_swz(r);
+        srcB[i] = B + t * sB + (int64_t)(n0 + r) * rowB + c;
+    }
+    // the scales first: an ordinary load consumed after a DMA is issued makes the compiler wait for the DMA too
+    const int eA = h3_exp(load_amax(amaxA + t)), eB = h3_exp(load_amax(amaxB + t));
+    const float scA = pow2f(eA), scA2 = pow2f(eA + 11);
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef __attribute__((address_space(1))) void gbl_void;
+    auto issue = [&](int kt, int st) {
+        u32x4 *base = lds + st * STG + w * 64;
+#pragma unroll
+        for (int i = 0; i < GA; i++)
+            __builtin_amdgcn_global_load_lds((gbl_void *)(srcA[i] + kt * 32), (lds_void *)(base + i * NT), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < GB; i++)
+            __builtin_amdgcn_global_load_lds((gbl_void *)(srcB[i] + kt * 8), (lds_void *)(base + BM * 8 + i * NT),
+                                             16, 0, 0);
+    };
+
+    f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = f32x16{};
+            lo[i][j] = f32x16{};
+        }
+    const int fr = lane & 31, fh = lane >> 5;
+
+    const int nk = K / BK;
+    issue(0, 0);
+    if (nk > 1) {
+        issue(1, 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    // a 16-deep half step's fragments: A as fp32 (two chunks per 32-row tile, split after the read), B as planes
+    struct Frag {
+        u32x4 a[TM][2], b[TN][2];
+    };
+    auto read = [&](int st, int kh, Frag &f) {
+        const u32x4 *sAl = lds + st * STG, *sBl = sAl + BM * 8;
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int r = wn * WTN + j * 32 + fr, g = 2 * kh + fh;
+#pragma unroll
+            for (int p = 0; p < 2; p++) f.b[j][p] = sBl[r * 8 + ((2 * g + p) ^ g_swz(r))];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            const int r = wm * WTM + i * 32 + fr, c = 4 * kh + 2 * fh;
+            f.a[i][0] = sAl[r * 8 + (c ^ g_swz(r))];
+            f.a[i][1] = sAl[r * 8 + ((c + 1) ^ g_swz(r))];
+        }
+    };
+    // A's fragments split into planes (in place: a[i][0] = hi plane, a[i][1] = lo plane), then the MFMAs
+    auto split = [&](Frag &f) {
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            u32x4 ah, al;
+            h3_split8(__builtin_bit_cast(float4, f.a[i][0]), __builtin_bit_cast(float4, f.a[i][1]), scA, scA2, ah, al);
+            f.a[i][0] = ah;
+            f.a[i][1] = al;
+        }
+    };
+    auto mfmas = [&](const Frag &f) {
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                lo[i][j] = mfma16(f.a[i][1], f.b[j][0], lo[i][j]);
+                lo[i][j] = mfma16(f.a[i][0], f.b[j][1], lo[i][j]);
+                hi[i][j] = mfma16(f.a[i][0], f.b[j][0], hi[i][j]);
+            }
+    };
+    auto mma = [&](Frag &f) {
+        split(f);
+        mfmas(f);
+    };
+    int st = 0;
+    if constexpr (KP) {
+        // each half step's MFMAs run while the next half step's fragments are read: split kh 0, [read kh 1 | MFMA
+        // kh 0], barrier (publishes step kt + 1), split kh 1, [read kh 0 of step kt + 1 | MFMA kh 1].  The split
+        // goes before the reads so its wait covers only its own fragments; the last two steps are peeled, so the
+        // loop has no conditional part (a join makes the compiler wait for every read in flight); scheduling
+        // barriers keep the reads ahead of the MFMAs they are to run under and the barrier behind them.
+        auto next = [](int s) { return s == 2 ? 0 : s + 1; };
+        Frag f0, f1;
+        read(0, 0, f0);
+        int kt = 0;
+        for (; kt + 2 < nk; kt++) {
+            const int sn = next(st);
+            issue(kt + 2, next(sn));  // the stage read in step kt - 1
+            split(f0);
+            read(st, 1, f1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas(f0);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+            __builtin_amdgcn_s_barrier();
+            split(f1);
+            read(sn, 0, f0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas(f1);
+            __builtin_amdgcn_sched_barrier(0);
+            st = sn;
+        }
+        if (kt + 1 < nk) {  // step nk - 2: no DMA left to issue
+            const int sn = next(st);
+            split(f0);
+            read(st, 1, f1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas(f0);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            split(f1);
+            read(sn, 0, f0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfmas(f1);
+            st = sn;
+        }
+        split(f0);  // step nk - 1
+        read(st, 1, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(f0);
+        mma(f1);
+    } else {
+        for (int kt = 0; kt < nk; kt++) {
+            if (kt + 2 < nk) issue(kt + 2, st == 0 ? 2 : st - 1);  // the stage read in step kt - 1
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++) {
+                Frag f;
+                read(st, kh, f);
+                mma(f);
+            }
+            // publish step kt + 1 (this wave's DMA of it done; step kt + 2's may stay in flight), and every wave is
+            // past its reads of stage st before step kt + 3's DMA overwrites it
+            if (kt + 2 < nk)
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            st = st == 2 ? 0 : st + 1;
+        }
+    }
+
+    const float inv = pow2f(-eA), invB = pow2f(-eB);
+    float *Ct = C + t * sC;
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+        const int col = n0 + wn * WTN + j * 32 + fr;
+        const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (row < M) {
+                    const float v = (hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB;
+                    Ct[row * N + col] = EPI == 1 ? relu_nan(v + bv) : v;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
 // TN: slab[s][t][m][n] = sum_{k in split s} A[t][k][m] B[t][k][n], A fp32 [Kd][M], B fp32 [Kd][N] (the weight
 // gradient dz^T a3: both operands row-major over the minibatch's frames), both split while staged into plane
 // images [32 k rows][RC chunks of 8 columns]; fragments k-contiguous through ds_read_b64_tr_b16 (a 32x32x16
@@ -829,6 +1046,25 @@ hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, cons
     return hipGetLastError();
 }
 
+template <int BM, int BN, int WGM, int WGN, bool KP>
+hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
+                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
+                      hipStream_t s) {
+    if (N % BN || Pout) return hipErrorInvalidValue;  // no plane output from the DMA-staged kernel
+    if ((int64_t)N * (K / 8) * 2 > INT32_MAX) return hipErrorInvalidValue;
+    const int64_t tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = N / BN;
+    if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
+    if (bias)
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
+                           bias, C, sC, tiles_n);
+    else
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
+                           nullptr, C, sC, tiles_n);
+    return hipGetLastError();
+}
+
 // Q: the operands are plane images (k_h3_tnq), strides in values as for fp32 operands (4 B per value either way)
 template <int BM, int BN, int WGM, int WGN, bool Q>
 hipError_t tn_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t Kd, int M,
@@ -902,9 +1138,18 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 11: return H3_NT(128, 192, 4, 2, true);
         case 12: return H3_NT(128, 128, 2, 2, true);
         case 13: return H3_NT(128, 256, 2, 4, true);
+#undef H3_NT
+        // k_h3_ntg: both operands staged by LDS-DMA, three k steps deep
+#define H3_NTG(BM, BN, WM, WN, KP) \
+    ntg_launch<BM, BN, WM, WN, KP>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s)
+        case 20: return H3_NTG(256, 128, 4, 2, false);
+        case 21: return H3_NTG(128, 192, 4, 2, false);
+        // the same with each half step's fragment reads under the previous half step's MFMAs
+        case 30: return H3_NTG(256, 128, 4, 2, true);
+        case 31: return H3_NTG(128, 192, 4, 2, true);
+#undef H3_NTG
         default: return hipErrorInvalidValue;
     }
-#undef H3_NT
 }
 
 hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t Kd,

@@ -176,6 +176,64 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
 // ROLE only names the instantiation (rocprofv3 tells the passes of conv3's backward apart by it):
 // 0 generic, 1 R (patch sums), 2 S (band sums), 3 dQ (window sums), 4 dT2 (table rows)
 constexpr int SEG_WAVES = 4, SEG_UNROLL = 8;
+
+// A carry word: 8 bytes (a float2 of a row), read at agent scope (sc1, past this CU's L1) when the carries were
+// published inside the same launch by other workgroups, plainly otherwise.
+template <bool SC1>
+__device__ __forceinline__ float2 carry_load(const float2 *p) {
+    if constexpr (SC1) {
+        const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        return __builtin_bit_cast(float2, v);
+    } else {
+        return *p;
+    }
+}
+
+// one fix row (dst, j0, j1, slot0) by one wave, lane = (tower t, float2 column c2):
+// out[t][dst] (+)= carry[t][j0][slot0] + sum_{j0 < j <= j1} carry[t][j][0], in that order
+template <bool SC1>
+__device__ __forceinline__ void seg_fix_row(const float2 *__restrict__ carry, int64_t nitems, int4 x, int T,
+                                            float2 *__restrict__ out, int64_t out_rows, int acc_out, int lane) {
+    const int t = lane >> 5, c2 = lane & 31;
+    if (t >= T) return;
+    const float2 *ct = carry + (size_t)t * nitems * 64 + c2;
+    float2 acc = carry_load<SC1>(ct + (size_t)x.y * 64 + x.w * 32);
+    // a hot destination spans hundreds of items: four independent partial sums (items
+    // j0+1+4i+q go to partial q) keep 16 loads in flight instead of one dependent chain;
+    // the partials join in a fixed order, so the result stays bitwise reproducible
+    float2 a[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+    int j = x.y + 1;
+    for (; j + 15 <= x.z; j += 16) {
+        float2 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = carry_load<SC1>(ct + (size_t)(j + u) * 64);
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            a[u & 3].x += v[u].x;
+            a[u & 3].y += v[u].y;
+        }
+    }
+    for (; j <= x.z; j += 4) {  // static partial indices (a dynamic a[q] would live in scratch)
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (j + u <= x.z) {
+                const float2 v = carry_load<SC1>(ct + (size_t)(j + u) * 64);
+                a[u].x += v.x;
+                a[u].y += v.y;
+            }
+        }
+    }
+    acc.x += (a[0].x + a[1].x) + (a[2].x + a[3].x);
+    acc.y += (a[0].y + a[1].y) + (a[2].y + a[3].y);
+    float2 *o = out + ((size_t)t * out_rows + x.x) * 32 + c2;
+    if (acc_out) {
+        const float2 p = *o;
+        *o = make_float2(p.x + acc.x, p.y + acc.y);
+    } else {
+        *o = acc;
+    }
+}
 template <int MASK, int ROLE>
 __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__restrict__ src,
                                                            const void *__restrict__ mask, int64_t src_rows,
@@ -184,7 +242,10 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
                                                            const int32_t *__restrict__ slot, int S, int64_t L,
                                                            int64_t nitems, int T, float4 *__restrict__ out,
                                                            int64_t out_rows, float4 *__restrict__ carry,
-                                                           int acc_out, int32_t *__restrict__ mark) {
+                                                           int acc_out, int32_t *__restrict__ mark,
+                                                           const int4 *__restrict__ fix,
+                                                           const int32_t *__restrict__ hfix,
+                                                           int32_t *__restrict__ cnt) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int t = lane >> 5, q = (lane >> 4) & 1, c = lane & 15;
     const bool live = t < T;
@@ -301,10 +362,46 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
             }
         }
         if (cur >= 0) flush();
+        if (!cnt) {
+            if (live && q == 0) {
+                float4 *cr = carry + ((size_t)t * nitems + it) * 32 + c;
+                cr[0] = head;
+                cr[16] = tail;
+            }
+            continue;
+        }
+        // in-launch fix-up (cnt != null): publish the carries write-through (8-byte agent-scope stores: sc1, no
+        // release fence), drain, then count this item in at the fix rows it takes part in -- the one its first
+        // destination started at (hfix, when that destination continues from an earlier item) and its own (when
+        // its last destination starts here and continues).  The item that completes a row's count sums the row's
+        // carries in k_seg_fix's order with agent-scope loads, so the result does not depend on which item is
+        // last, and resets the counter for the next launch.
         if (live && q == 0) {
-            float4 *cr = carry + ((size_t)t * nitems + it) * 32 + c;
-            cr[0] = head;
-            cr[16] = tail;
+            uint64_t *cr = reinterpret_cast<uint64_t *>(carry + ((size_t)t * nitems + it) * 32 + c);
+            __hip_atomic_store(cr, __builtin_bit_cast(uint64_t, make_float2(head.x, head.y)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cr + 1, __builtin_bit_cast(uint64_t, make_float2(head.z, head.w)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cr + 32, __builtin_bit_cast(uint64_t, make_float2(tail.x, tail.y)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cr + 33, __builtin_bit_cast(uint64_t, make_float2(tail.z, tail.w)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int f0 = hfix[it];
+        const int f1 = fix[it].x >= 0 ? (int)it : -1;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int f = k == 0 ? f0 : f1;  // wave-uniform
+            if (f < 0) continue;
+            const int4 x = fix[f];
+            int old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_add(cnt + f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            old = __shfl(old, 0);
+            if (old != x.z - x.y) continue;  // not the last of the row's j1 - j0 + 1 items
+            if (lane == 0) __hip_atomic_store(cnt + f, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            seg_fix_row<true>(reinterpret_cast<const float2 *>(carry), nitems, x, T, reinterpret_cast<float2 *>(out),
+                              out_rows, acc_out, lane);
         }
     }
 }
@@ -315,47 +412,11 @@ template <int ROLE>
 __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carry, int64_t nitems,
                                                  const int4 *__restrict__ fix, int64_t nfix, int T,
                                                  float2 *__restrict__ out, int64_t out_rows, int acc_out) {
-    const int lane = threadIdx.x & 63, t = lane >> 5, c2 = lane & 31;
+    const int lane = threadIdx.x & 63;
     for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nfix; f += (int64_t)gridDim.x * 4) {
-        if (t >= T) continue;
         const int4 x = fix[f];
         if (x.x < 0) continue;
-        const float2 *ct = carry + (size_t)t * nitems * 64 + c2;
-        float2 acc = ct[(size_t)x.y * 64 + x.w * 32];
-        // a hot destination spans hundreds of items: four independent partial sums (items
-        // j0+1+4i+q go to partial q) keep 16 loads in flight instead of one dependent chain;
-        // the partials join in a fixed order, so the result stays bitwise reproducible
-        float2 a[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-        int j = x.y + 1;
-        for (; j + 15 <= x.z; j += 16) {
-            float2 v[16];
-#pragma unroll
-            for (int u = 0; u < 16; u++) v[u] = ct[(size_t)(j + u) * 64];
-#pragma unroll
-            for (int u = 0; u < 16; u++) {
-                a[u & 3].x += v[u].x;
-                a[u & 3].y += v[u].y;
-            }
-        }
-        for (; j <= x.z; j += 4) {  // static partial indices (a dynamic a[q] would live in scratch)
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (j + u <= x.z) {
-                    const float2 v = ct[(size_t)(j + u) * 64];
-                    a[u].x += v.x;
-                    a[u].y += v.y;
-                }
-            }
-        }
-        acc.x += (a[0].x + a[1].x) + (a[2].x + a[3].x);
-        acc.y += (a[0].y + a[1].y) + (a[2].y + a[3].y);
-        float2 *o = out + ((size_t)t * out_rows + x.x) * 32 + c2;
-        if (acc_out) {
-            const float2 p = *o;
-            *o = make_float2(p.x + acc.x, p.y + acc.y);
-        } else {
-            *o = acc;
-        }
+        seg_fix_row<false>(carry, nitems, x, T, out, out_rows, acc_out, lane);
     }
 }
 
@@ -396,24 +457,25 @@ template <int ROLE>
 hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                       const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                       int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int32_t *mark,
-                      hipStream_t s) {
+                      const int32_t *hfix, int32_t *cnt, hipStream_t s) {
     const int64_t nitems = (nnz + L - 1) / L;
+    if (cnt && nfix != nitems) return hipErrorInvalidValue;  // in-launch fix-ups: one fix row per item
     const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
+    const int4 *fx = cnt ? reinterpret_cast<const int4 *>(fix) : nullptr;
+    const int32_t *hf = cnt ? hfix : nullptr;
+    const float4 *s4 = reinterpret_cast<const float4 *>(src);
+    float4 *o4 = reinterpret_cast<float4 *>(out), *c4 = reinterpret_cast<float4 *>(carry);
     if (mask && mask_bits)
-        hipLaunchKernelGGL((k_seg_sum<2, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
-                           reinterpret_cast<const float4 *>(src), mask, src_rows, idx, key, nnz, slot, S, L, nitems,
-                           T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out, mark);
+        hipLaunchKernelGGL((k_seg_sum<2, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, mask, src_rows, idx, key,
+                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt);
     else if (mask)
-        hipLaunchKernelGGL((k_seg_sum<1, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
-                           reinterpret_cast<const float4 *>(src), mask, src_rows, idx, key, nnz, slot, S, L, nitems,
-                           T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry), acc_out, mark);
+        hipLaunchKernelGGL((k_seg_sum<1, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, mask, src_rows, idx, key,
+                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt);
     else
-        hipLaunchKernelGGL((k_seg_sum<0, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s,
-                           reinterpret_cast<const float4 *>(src), nullptr, src_rows, idx, key, nnz, slot, S, L,
-                           nitems, T, reinterpret_cast<float4 *>(out), out_rows, reinterpret_cast<float4 *>(carry),
-                           acc_out, mark);
+        hipLaunchKernelGGL((k_seg_sum<0, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, nullptr, src_rows, idx,
+                           key, nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || nfix <= 0) return e;
+    if (e != hipSuccess || nfix <= 0 || cnt) return e;
     const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);
     hipLaunchKernelGGL(k_seg_fix<ROLE>, dim3(gfix), dim3(256), 0, s, reinterpret_cast<const float2 *>(carry), nitems,
                        reinterpret_cast<const int4 *>(fix), nfix, T, reinterpret_cast<float2 *>(out), out_rows,
@@ -425,22 +487,21 @@ hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,
-                          int role, int32_t *mark, hipStream_t s) {
+                          int role, int32_t *mark, const int32_t *hfix, int32_t *cnt, hipStream_t s) {
     hipError_t e = (acc_out || !fill) ? hipSuccess
                                       : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
     if (e != hipSuccess || nnz <= 0) return e;
+#define SEG_ROLE(R) \
+    seg_launch<R>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out, out_rows, carry, \
+                  acc_out, mark, hfix, cnt, s)
     switch (role) {
-        case 1: return seg_launch<1>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                     out_rows, carry, acc_out, mark, s);
-        case 2: return seg_launch<2>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                     out_rows, carry, acc_out, mark, s);
-        case 3: return seg_launch<3>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                     out_rows, carry, acc_out, mark, s);
-        case 4: return seg_launch<4>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                     out_rows, carry, acc_out, mark, s);
-        default: return seg_launch<0>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out,
-                                      out_rows, carry, acc_out, mark, s);
+        case 1: return SEG_ROLE(1);
+        case 2: return SEG_ROLE(2);
+        case 3: return SEG_ROLE(3);
+        case 4: return SEG_ROLE(4);
+        default: return SEG_ROLE(0);
     }
+#undef SEG_ROLE
 }
 
 }  // namespace merlin

@@ -106,6 +106,8 @@ def lib():
     L.merlin_tower_heads_fwd.argtypes = [vp, i64, i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.merlin_segment_sum_marked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                             vp, vp]
+    L.merlin_segment_sum_fused.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
+                                           vp, vp, vp, vp]
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_colsum.argtypes = [vp, i64, i32, i64, i64, i32, vp, vp]
@@ -169,7 +171,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
     "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
-    "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
+    "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_segment_sum_fused", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_tower_colsum",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
@@ -597,6 +599,11 @@ SEG_ROLE_SHIFT = 8
 SEG_ROLES = {"k_seg_sum_R": 1, "k_seg_sum_S": 2, "k_seg_sum_dQ": 3, "k_seg_sum_dT2": 4}
 
 
+# the destinations that span items finished inside the segmented-sum launch (merlin_segment_sum_fused: write-through
+# carries and an arrival counter per row), not by a second k_seg_fix launch; the same bits either way
+SEG_FUSED = True
+
+
 def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum", out=None,
                 accumulate: bool = False, carry=None, mask=None, fill: bool = True, mark=None):
     """out f32[T, out_rows, 64]: out[t][key] = the sum, in entry order, of src[t][row(e)] over
@@ -631,11 +638,14 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
     flags |= SEG_ROLES.get(name, 0) << SEG_ROLE_SHIFT
     if mark is not None:
         assert mark.dtype == torch.int32 and mark.shape == (out_rows,) and mark.is_contiguous()
+    fused = SEG_FUSED and getattr(plan, "counters", None) is not None
     with KernelTimer.span(name, nb):
-        check(lib().merlin_segment_sum_marked(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz,
-                                              ptr(slot), int(sub), plan.item_len, ptr(plan.fix),
-                                              int(plan.fix.shape[0]), T, ptr(out), int(out_rows), ptr(carry), flags,
-                                              ptr(mark), stream_of(src)), "merlin_segment_sum_marked")
+        check(lib().merlin_segment_sum_fused(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz,
+                                             ptr(slot), int(sub), plan.item_len, ptr(plan.fix),
+                                             int(plan.fix.shape[0]), T, ptr(out), int(out_rows), ptr(carry), flags,
+                                             ptr(mark), ptr(plan.head_fix) if fused else None,
+                                             ptr(plan.counters) if fused else None, stream_of(src)),
+              "merlin_segment_sum_fused")
     return out
 
 

@@ -145,6 +145,8 @@ class SegmentPlan:
         self.idx = idx_sorted.to(torch.int32).contiguous()
         if n == 0:
             self.fix = torch.zeros((0, 4), dtype=torch.int32, device=dev)
+            self.head_fix = torch.zeros(0, dtype=torch.int32, device=dev)
+            self.counters = torch.zeros(0, dtype=torch.int32, device=dev)
             return
         j = torch.arange(self.nitems, dtype=torch.int64, device=dev)
         p = torch.clamp((j + 1) * L, max=n) - 1  # each item's last entry
@@ -156,6 +158,13 @@ class SegmentPlan:
         live = (e > (j + 1) * L) & (s >= j * L)  # starts in this item, continues past it
         dst = torch.where(live, self.key[p].long(), torch.full_like(j, -1))
         self.fix = torch.stack([dst, j, (e - 1) // L, (s != j * L).long()], 1).to(torch.int32).contiguous()
+        # for the in-launch fix-ups (merlin_segment_sum_fused): the fix row (= item) at which each item's first
+        # destination started, when it continues into the item, else -1; and the rows' arrival counters (each
+        # launch leaves them zero)
+        kf = self.key[j * L].contiguous()
+        sf = torch.searchsorted(self.key, kf, side="left")
+        self.head_fix = torch.where(sf < j * L, sf // L, torch.full_like(j, -1)).to(torch.int32).contiguous()
+        self.counters = torch.zeros(self.nitems, dtype=torch.int32, device=dev)
 
 
 class MinibatchWindows:

@@ -10,7 +10,9 @@ import torch
 
 from merlin import _native as nat
 
-TILES = {0: (256, 128), 1: (128, 192), 2: (128, 128), 3: (128, 256), 10: (256, 128), 11: (128, 192), 12: (128, 128),
+TILES = {0: (256, 128), 1: (128, 192), 2: (128, 128), 3: (128, 256), 4: (256, 128), 6: (128, 192), 14: (256, 128), 10: (256, 128), 11: (128, 192), 12: (128, 128),
+         20: (256, 128), 21: (128, 192), 22: (256, 128), 23: (128, 256), 24: (128, 128), 25: (128, 192),
+         30: (256, 128), 31: (128, 192), 32: (256, 128), 33: (128, 256), 34: (128, 128), 35: (128, 192),
          13: (128, 256)}
 
 

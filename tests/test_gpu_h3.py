@@ -57,13 +57,14 @@ def _operands(device, M, N, K, seed, scale_a=1.0, ragged=False):
 
 
 @pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 2), (512, 576, 3),
-                                     (512, 576, 10), (576, 512, 11), (512, 576, 12), (576, 512, 12), (512, 576, 13)])
+                                     (512, 576, 10), (576, 512, 11), (512, 576, 12), (576, 512, 12), (512, 576, 13),
+                                     (512, 576, 20), (576, 512, 21), (512, 576, 30), (576, 512, 31)])
 @pytest.mark.parametrize("M,scale_a,ragged", [(1, 1.0, False), (777, 1.0, False), (20011, 1.0, False),
                                               (20011, 1e-7, False), (9999, 1.0, True)])
 def test_gemm_nt_vs_float64(device, M, N, K, cfg, scale_a, ragged):
     from merlin import _native as nat
 
-    if N % {1: 192, 11: 192, 3: 256, 13: 256}.get(cfg, 128):
+    if N % {1: 192, 11: 192, 21: 192, 31: 192, 3: 256, 13: 256}.get(cfg, 128):
         pytest.skip("N not a multiple of the tile width")
     A, B = _operands(device, M, N, K, M + N + cfg, scale_a, ragged)
     bias = torch.randn(2, N, device=device)
@@ -77,6 +78,10 @@ def test_gemm_nt_vs_float64(device, M, N, K, cfg, scale_a, ragged):
     Cb = nat.h3_gemm_nt(A, amA, Bp, amB, bias=bias, cfg=cfg)
     assert torch.equal(Cb, torch.relu(C + bias.unsqueeze(1)))
     assert torch.equal(C, nat.h3_gemm_nt(A, amA, Bp, amB, cfg=cfg))  # fixed order: the same bits every call
+    # every tile shape and staging path sums each output's products in the same order: the same bits
+    assert torch.equal(C, nat.h3_gemm_nt(A, amA, Bp, amB, cfg=1 if N % 128 else 2))
+    if cfg >= 20:
+        return  # the DMA-staged kernel has no plane output
     P = torch.full((2, M, 2 * K), 0x5555, dtype=torch.int16, device=device)
     Cp = nat.h3_gemm_nt(A, amA, Bp, amB, cfg=cfg, planes_out=P)  # A's planes as a by-product: h3_split's exactly
     assert torch.equal(Cp, C) and torch.equal(P, nat.h3_split(A, amA))

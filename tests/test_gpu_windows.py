@@ -128,6 +128,37 @@ def test_segment_sum_matches_index_add(device, n, nkeys, L, use_slot):
     assert torch.equal(both, out + out2)
 
 
+@pytest.mark.parametrize("n,nkeys,L", [(300000, 50, 64), (200000, 3000, 16), (5000, 4000, 1024)])
+def test_segment_sum_in_launch_fixups_equal_fix_pass(device, n, nkeys, L, monkeypatch):
+    """merlin_segment_sum_fused: destinations spanning items (some over thousands of them) are finished inside the
+    launch by the item that completes their count -- the same bits as the separate k_seg_fix pass, on every call
+    (the counters come back to zero), with accumulate and a slot map too."""
+    from merlin import _native as nat
+    from merlin.windows import SegmentPlan
+
+    g = torch.Generator(device=device)
+    g.manual_seed(n + L)
+    keys = (torch.rand(n, device=device, generator=g) ** 4 * nkeys).long()
+    F_, S = 3000, 9
+    idx = torch.randint(0, F_ * S, (n,), device=device, generator=g)
+    o = torch.sort(keys, stable=True).indices
+    plan = SegmentPlan(keys[o], idx[o], item_len=L)
+    assert int((plan.fix[:, 2] - plan.fix[:, 1]).max()) >= 1  # rows spanning items
+    slot = torch.full((F_,), -1, dtype=torch.int32, device=device)
+    slot[torch.randperm(F_, device=device, generator=g)[:2000]] = torch.arange(2000, dtype=torch.int32, device=device)
+    src = torch.randn(2, 2000 * S, 64, device=device, generator=g)
+    base = torch.randn(2, nkeys, 64, device=device, generator=g)
+    monkeypatch.setattr(nat, "SEG_FUSED", False)
+    want = nat.segment_sum(src, plan, nkeys, slot=slot, sub=S)
+    want_acc = nat.segment_sum(src, plan, nkeys, slot=slot, sub=S, out=base.clone(), accumulate=True)
+    monkeypatch.setattr(nat, "SEG_FUSED", True)
+    for _ in range(3):
+        assert torch.equal(nat.segment_sum(src, plan, nkeys, slot=slot, sub=S), want)
+        assert torch.equal(nat.segment_sum(src, plan, nkeys, slot=slot, sub=S, out=base.clone(), accumulate=True),
+                           want_acc)
+        assert int(plan.counters.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("L", [16, 1024])
 def test_segment_sum_masked_no_fill(device, L):
     """merlin_segment_sum_masked: the ReLU mask of a second tensor fused into the gathers, and
