@@ -299,13 +299,24 @@ PMC_ALIAS = {"k_seg_sum_R": ("k_seg_sum<2, 1>", "k_seg_fix<1>"),
              "k_seg_sum_S": ("k_seg_sum<0, 2>", "k_seg_fix<2>"),
              "k_seg_sum_dQ": ("k_seg_sum<0, 3>", "k_seg_fix<3>"),
              "k_seg_sum_dT2": ("k_seg_sum<0, 4>", "k_seg_fix<4>"),
-             # fc1's x6 GEMMs; the weight gradient's span covers the split-K kernel and its slab fold
-             "gemm_fc1_fwd": ("k_x6_nt32<256, 128, 4, 2, 1, 1, 0>",),
-             "gemm_fc1_dgrad": ("k_x6_nt32<128, 192, 4, 2, 0, 1, 0>",),
+             # the rollout's fc1 (x6); the update's fc1 GEMMs follow H3_NT_CFG (h3_gemm_names); the weight
+             # gradient's span covers the split-K kernel and its slab fold
              "gemm_rollout_fc1": ("k_x6_nt32<128, 128, 2, 2, 0, 1, 0>",),
              "k_head_bwd": ("k_head_bwd<3>", "k_head_fold"),
              "k_heads_fwd": ("k_heads_fwd<3>",),
-             "gemm_wgrad": ("k_x6_tn<128, 192, 2, 4>", "k_x6_fold")}
+             "k_window_lut": ("k_window_lut<0>",),
+             "k_window_lut_all": ("k_window_lut<1>",),
+             "gemm_wgrad": ("k_h3_tn<128, 192, 4, 2>", "k_x6_fold")}
+# rocprofv3 names of merlin_h3_gemm_nt's configurations (csrc/merlin_h3.hip launch_h3_gemm_nt)
+H3_NT_NAMES = {0: "k_h3_nt<256, 128, 4, 2, {}>", 1: "k_h3_nt<128, 192, 4, 2, {}>", 2: "k_h3_nt<128, 128, 2, 2, {}>",
+               3: "k_h3_nt<128, 256, 2, 4, {}>", 10: "k_h3_ntp<256, 128, 4, 2, {}>", 11: "k_h3_ntp<128, 192, 4, 2, {}>",
+               12: "k_h3_ntp<128, 128, 2, 2, {}>", 13: "k_h3_ntp<128, 256, 2, 4, {}>"}
+
+
+def h3_gemm_names(nat):
+    """PMC_ALIAS entries of the update's fc1 forward (bias + ReLU epilogue) and input gradient."""
+    return {"gemm_fc1_fwd": (H3_NT_NAMES.get(nat.H3_NT_CFG["fwd"], "?").format(1),),
+            "gemm_fc1_dgrad": (H3_NT_NAMES.get(nat.H3_NT_CFG["dgrad"], "?").format(0),)}
 PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 
 
@@ -313,7 +324,9 @@ def pmc_traffic(kernel: str):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 --pmc passes of the same bench
     command (profiles/*_pmc.json: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE);
     a span made of several kernels (PMC_ALIAS tuple) adds theirs."""
-    names = PMC_ALIAS.get(kernel, kernel)
+    from merlin import _native as nat
+
+    names = {**PMC_ALIAS, **h3_gemm_names(nat)}.get(kernel, kernel)
     names = names if isinstance(names, tuple) else (names,)
     files = [PMC_FILE] if PMC_FILE else sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True)
     for f in files:

@@ -39,7 +39,10 @@ __device__ __forceinline__ float4 f4_mask(const float4 y, const float4 g) {
                        y.w > 0.0f ? g.w : 0.0f);
 }
 
-// Z2w[t][w][c4] = sum_{k<16} T2[t][rows[w][k]][c4], taps in k_conv2_lut_fwd's order
+// Z2w[t][w][c4] = sum_{k<16} T2[t][rows[w][k]][c4], taps in k_conv2_lut_fwd's order.  ALL only names the
+// instantiation: 1 for the rollout's table over every possible window (5^9 rows, once per rollout), 0 for an
+// update's windows (every minibatch) -- so a profile tells the two apart
+template <int ALL>
 __global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ rows, int64_t nw,
                                                     const float4 *__restrict__ tab, int T,
                                                     float4 *__restrict__ Z2w) {
@@ -426,8 +429,12 @@ hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, 
     const int64_t total = (int64_t)T * nw * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
-    hipLaunchKernelGGL(k_window_lut, dim3(grid), dim3(256), 0, s, rows, nw, reinterpret_cast<const float4 *>(tab), T,
-                       reinterpret_cast<float4 *>(Z2w));
+    if (nw == 1953125)  // 5^9: merlin_tower_all_windows()
+        hipLaunchKernelGGL(k_window_lut<1>, dim3(grid), dim3(256), 0, s, rows, nw, reinterpret_cast<const float4 *>(tab),
+                           T, reinterpret_cast<float4 *>(Z2w));
+    else
+        hipLaunchKernelGGL(k_window_lut<0>, dim3(grid), dim3(256), 0, s, rows, nw, reinterpret_cast<const float4 *>(tab),
+                           T, reinterpret_cast<float4 *>(Z2w));
     return hipGetLastError();
 }
 

@@ -539,7 +539,8 @@ def window_lut(rows, tables):
     assert rows.dtype == torch.int32 and rows.shape == (nw, 16)
     out = torch.empty((T, nw, 64), dtype=torch.float32, device=tables.device)
     # algorithmic bytes: row indices + Z2w written (table rows are L2-resident gathers)
-    with KernelTimer.span("k_window_lut", nw * (64 + T * 256)):
+    # the rollout's all-windows table (5^9 rows) is its own kernel instantiation and span (k_window_lut<1>)
+    with KernelTimer.span("k_window_lut_all" if nw == 5 ** 9 else "k_window_lut", nw * (64 + T * 256)):
         check(lib().merlin_tower_window_lut(ptr(rows), nw, ptr(tables), T, ptr(out), stream_of(tables)),
               "merlin_tower_window_lut")
     return out
@@ -887,7 +888,9 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
 
 
 # -- fc1 on the f16 matrix cores in two-plane form (csrc/merlin_h3.hip) ----------------------------------------
-H3_NT_CFG = {"fwd": 0, "dgrad": 1, "rollout": 2}  # tile configurations of merlin_h3_gemm_nt (N = 512 / 576)
+# tile configurations of merlin_h3_gemm_nt (N = 512 / 576): the split interleaved into the MFMAs (k_h3_ntp), forward
+# 128 x 256 and input gradient 128 x 192 tiles (scripts/ab_update.py, same update replayed: 204.5 vs 209.0 ms for cfg 0 / 1)
+H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 2}
 H3_TN_CFG = 0
 H3_TN_SPLITS = 32
 

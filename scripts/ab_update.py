@@ -4,7 +4,7 @@ weights, optimizer state and minibatch permutations, restored before every run) 
 setting in turn, repeatedly -- device-to-device and clock differences between gpurun boxes and the
 training state's drift do not enter the comparison.
 
-    python scripts/ab_update.py [repeats] [warmup] [x6_overlap,no_overlap,hipblaslt]
+    python scripts/ab_update.py [repeats] [warmup] [fast,fast_segfix,fast_x6,fast_h3f10_h3d11,...]
 
 Prints ms per update for each setting."""
 import os
@@ -51,7 +51,10 @@ def main():
     def setter(name):
         def s():
             W.OVERLAP_WGRAD = {"no_overlap": False, "x6_overlap": True}.get(name, "deferred")
-            agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6"
+            agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6" if "x6" in name else "h3"
+            nat.SEG_FUSED = "segfix" not in name  # the segmented sums' fix-ups in a second launch (k_seg_fix)
+            nat.H3_NT_CFG["fwd"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3f"), 0)
+            nat.H3_NT_CFG["dgrad"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3d"), 1)
             agent._clip_adam = None if name == "torch_opt" else clip_adam
             agent.fast_step = name.startswith("fast")  # merlin/fast_step.py vs the autograd engine
             from merlin import fast_step as FS
