@@ -300,6 +300,11 @@ int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32
 int64_t merlin_tower_all_windows(void);
 int merlin_tower_codes_conv3(const uint32_t *codes_dev, int64_t n, const float *Qall_dev,
                              const float *b3_dev, int32_t towers, float *Y3_dev, void *stream);
+/* Same, with amax_dev (or NULL): atomicMax of max |Y3| per tower as float bits into amax_dev[t] (zeroed by the
+ * caller), the operand scale of the acting path's fc1 on merlin_h3_gemm_nt. */
+int merlin_tower_codes_conv3_amax(const uint32_t *codes_dev, int64_t n, const float *Qall_dev,
+                                  const float *b3_dev, int32_t towers, float *Y3_dev, uint32_t *amax_dev,
+                                  void *stream);
 /* Same, also writing relu_bits_dev uint64[towers][n*9]: bit co of row (k*9 + p3) = Y3 > 0 there; amax_dev
  * (or NULL): atomicMax of max |Y3| per tower as float bits into amax_dev[t] (zeroed by the caller), the operand
  * scale of fc1's f16 two-plane GEMMs (merlin_h3_gemm_*). */

@@ -659,12 +659,17 @@ int merlin_tower_window_conv3_bits(const float *Q, int64_t nw, const int32_t *wi
 
 int64_t merlin_tower_all_windows(void) { return 1953125; }
 
-int merlin_tower_codes_conv3(const uint32_t *codes, int64_t n, const float *Qall, const float *b3, int32_t towers,
-                             float *Y3, void *stream) {
+int merlin_tower_codes_conv3_amax(const uint32_t *codes, int64_t n, const float *Qall, const float *b3,
+                                  int32_t towers, float *Y3, uint32_t *amax, void *stream) {
     if ((!codes || !Qall || !b3 || !Y3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_codes_conv3(codes, n, Qall, b3, towers, Y3, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_codes_conv3(codes, n, Qall, b3, towers, Y3, amax, (hipStream_t)stream));
     return MERLIN_OK;
+}
+
+int merlin_tower_codes_conv3(const uint32_t *codes, int64_t n, const float *Qall, const float *b3, int32_t towers,
+                             float *Y3, void *stream) {
+    return merlin_tower_codes_conv3_amax(codes, n, Qall, b3, towers, Y3, nullptr, stream);
 }
 
 int merlin_segment_sum_fused(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,

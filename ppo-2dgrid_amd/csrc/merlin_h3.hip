@@ -304,8 +304,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
                                                            const uint32_t *__restrict__ amaxB, int64_t M, int N,
                                                            int K, int64_t sA, int64_t sB,
                                                            const float *__restrict__ bias, float *__restrict__ C,
-                                                           int64_t sC, int tiles_n,
-    u32x4 *__restrict__ Pout) {
+                                                           int64_t sC, int tiles_n, u32x4 *__restrict__ Pout) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -877,6 +876,199 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
             }
 }
 
+// The TN product with the k step's split and staging interleaved into its MFMAs, as k_h3_ntp does for NT: the
+// steps whose loads are whole (all but a split's last one or two) run in a loop with no conditional part, each
+// reading its fragments first, then sched_group_barrier hints lay the next step's split (VALU), its LDS stores and
+// the global loads of the step after it between the MFMAs; the remaining steps run as in k_h3_tn.  Same
+// instructions per output as k_h3_tn, the same order of products and sums: the same bits.
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tnp(const float4 *__restrict__ A, const float4 *__restrict__ B,
+                                                           const uint32_t *__restrict__ amaxA,
+                                                           const uint32_t *__restrict__ amaxB, int64_t Kd, int M,
+                                                           int N, int64_t sA, int64_t sB, int64_t kc, int tiles_n,
+                                                           int tiles, int S, float *__restrict__ slab) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int RCA = BM / 8, RCB = BN / 8;
+    constexpr int QA = BK * RCA, QB = BK * RCB;
+    constexpr int UA = (QA + NT - 1) / NT, UB = (QB + NT - 1) / NT;
+    static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile of 32 x 32 MFMA tiles");
+    constexpr int PSA = BK * RCA, PSB = BK * RCB;
+    constexpr int STAGE = 2 * (PSA + PSB);
+    constexpr int NMFMA = TM * TN * 6;
+    __shared__ u32x4 lds[2 * STAGE];
+
+    const int P = xcd_tile(blockIdx.x, gridDim.x);
+    const int t = P / (S * tiles), s = (P / tiles) % S, Lt = P % tiles;
+    const int tm = Lt / tiles_n, tn = Lt - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int64_t k0 = (int64_t)s * kc, k1 = std::min<int64_t>(Kd, k0 + kc);
+    const int eA = h3_exp(load_amax(amaxA + t)), eB = h3_exp(load_amax(amaxB + t));
+    const float scA = pow2f(eA), scB = pow2f(eB), scA2 = pow2f(eA + 11), scB2 = pow2f(eB + 11);
+    const int64_t rowA = M / 4, rowB = N / 4;
+    A += t * sA + m0 / 4;
+    B += t * sB + n0 / 4;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+
+    int ka[UA], la[UA], kb[UB], lb[UB];
+    const float4 *pa[UA], *pb[UB];
+#pragma unroll
+    for (int i = 0; i < UA; i++) {
+        const int q = std::min(tid + i * NT, QA - 1);
+        const int k = q / RCA, g = q - (q / RCA) * RCA;
+        ka[i] = k;
+        la[i] = k * RCA + (g ^ tr_swz<RCA>(k));
+        pa[i] = A + (k0 + k) * rowA + g * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < UB; i++) {
+        const int q = std::min(tid + i * NT, QB - 1);
+        const int k = q / RCB, g = q - (q / RCB) * RCB;
+        kb[i] = k;
+        lb[i] = 2 * PSA + k * RCB + (g ^ tr_swz<RCB>(k));
+        pb[i] = B + (k0 + k) * rowB + g * 2;
+    }
+    const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float4 ra[UA][2], rb[UB][2];
+    auto load_full = [&](int64_t kk) {
+        const int64_t da = (kk - k0) * rowA, db = (kk - k0) * rowB;
+#pragma unroll
+        for (int i = 0; i < UA; i++) {
+            ra[i][0] = pa[i][da];
+            ra[i][1] = pa[i][da + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < UB; i++) {
+            rb[i][0] = pb[i][db];
+            rb[i][1] = pb[i][db + 1];
+        }
+    };
+    auto load = [&](int64_t kk) {
+        if (kk + BK <= k1) {
+            load_full(kk);
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < UA; i++) {
+            const float4 *src = pa[i] + (std::min(kk + ka[i], k1 - 1) - k0 - ka[i]) * rowA;
+            ra[i][0] = src[0];
+            ra[i][1] = src[1];
+        }
+#pragma unroll
+        for (int i = 0; i < UB; i++) {
+            const float4 *src = pb[i] + (std::min(kk + kb[i], k1 - 1) - k0 - kb[i]) * rowB;
+            rb[i][0] = src[0];
+            rb[i][1] = src[1];
+        }
+    };
+    auto store = [&](int buf, int64_t kk) {
+        u32x4 *st = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < UA; i++)
+            if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
+                const bool in = kk + ka[i] < k1;
+                u32x4 p0, p1;
+                h3_split8(in ? ra[i][0] : zero, in ? ra[i][1] : zero, scA, scA2, p0, p1);
+                st[la[i]] = p0;
+                st[PSA + la[i]] = p1;
+            }
+#pragma unroll
+        for (int i = 0; i < UB; i++)
+            if (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB) {
+                const bool in = kk + kb[i] < k1;
+                u32x4 p0, p1;
+                h3_split8(in ? rb[i][0] : zero, in ? rb[i][1] : zero, scB, scB2, p0, p1);
+                st[lb[i]] = p0;
+                st[PSB + lb[i]] = p1;
+            }
+    };
+
+    f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = f32x16{};
+            lo[i][j] = f32x16{};
+        }
+    auto compute = [&](int buf) {
+        const u32x4 *sAl = lds + buf * STAGE, *sBl = sAl + 2 * PSA;
+        u32x4 af[TM][2][2], bf[TN][2][2];
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++) af[i][kh][p] = tr_frag<RCA>(sAl + p * PSA, wm * WTM + i * 32, kh, lane);
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+                for (int p = 0; p < 2; p++) bf[j][kh][p] = tr_frag<RCB>(sBl + p * PSB, wn * WTN + j * 32, kh, lane);
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                f32x16 l = lo[i][j], h = hi[i][j];
+#pragma unroll
+                for (int kh = 0; kh < 2; kh++) {
+                    l = mfma16(af[i][kh][1], bf[j][kh][0], l);
+                    l = mfma16(af[i][kh][0], bf[j][kh][1], l);
+                    h = mfma16(af[i][kh][0], bf[j][kh][0], h);
+                }
+                lo[i][j] = l;
+                hi[i][j] = h;
+            }
+    };
+
+    const int64_t nsteps = k0 < k1 ? (k1 - k0 + BK - 1) / BK : 0, nfull = k0 < k1 ? (k1 - k0) / BK : 0;
+    if (nsteps > 0) {
+        load(k0);
+        store(0, k0);
+        if (nsteps > 1) load(k0 + BK);
+        __syncthreads();
+    }
+    int buf = 0;
+    int64_t st = 0, kk = k0;
+    for (; st + 2 < nfull; st++, kk += BK, buf ^= 1) {  // the load of step st + 2 is whole
+        compute(buf);
+        store(buf ^ 1, kk + BK);
+        load_full(kk + 2 * BK);
+        __builtin_amdgcn_sched_group_barrier(0x100, (TM + TN) * 8, 0);
+#pragma unroll
+        for (int m = 0; m < NMFMA; m++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            if (m % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            if (m >= NMFMA / 2 && m % 2 == 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __syncthreads();
+    }
+    for (; st < nsteps; st++, kk += BK, buf ^= 1) {
+        if (st + 1 < nsteps) store(buf ^ 1, kk + BK);
+        if (st + 2 < nsteps) load(kk + 2 * BK);
+        compute(buf);
+        __syncthreads();
+    }
+
+    const float inv = pow2f(-eA), invB = pow2f(-eB);
+    float *Sl = slab + ((int64_t)s * (gridDim.x / (S * tiles)) + t) * (int64_t)M * N;
+    const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                Sl[(int64_t)row * N + n0 + wn * WTN + j * 32 + fr] =
+                    (hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB;
+            }
+}
+
 // TN over operands already in plane form ([T][Kd][cols/8][2][8] f16 -- the a_planes output of the NT kernels, so
 // the fast step's weight gradient reads the planes its forward and input-gradient GEMMs made): k_h3_tn without the
 // split, staging a copy of 16-B chunks.  Thread q of a k row takes plane q / RC, chunk q % RC: the 8 lanes of a
@@ -1066,7 +1258,7 @@ hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, con
 }
 
 // Q: the operands are plane images (k_h3_tnq), strides in values as for fp32 operands (4 B per value either way)
-template <int BM, int BN, int WGM, int WGN, bool Q>
+template <int BM, int BN, int WGM, int WGN, int Q>
 hipError_t tn_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t Kd, int M,
                      int N, int T, int64_t sA, int64_t sB, int splits, float *slab, int *S_out, hipStream_t s) {
     if (M % BM || N % BN) return hipErrorInvalidValue;
@@ -1076,9 +1268,13 @@ hipError_t tn_launch(const void *A, const void *B, const uint32_t *amaxA, const 
     kc = (kc + BK - 1) / BK * BK;
     S = (int)std::max<int64_t>(1, (Kd + kc - 1) / kc);
     *S_out = S;
-    if (Q)
+    if (Q == 1)
         hipLaunchKernelGGL((k_h3_tnq<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
                            static_cast<const u32x4 *>(A), static_cast<const u32x4 *>(B), amaxA, amaxB, Kd, M, N,
+                           sA / 4, sB / 4, kc, tiles_n, tiles, S, slab);
+    else if (Q == 2)
+        hipLaunchKernelGGL((k_h3_tnp<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
+                           static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
                            sA / 4, sB / 4, kc, tiles_n, tiles, S, slab);
     else
         hipLaunchKernelGGL((k_h3_tn<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
@@ -1165,12 +1361,15 @@ hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B
     }
     int S = 1;
     hipError_t e;
-#define H3_TN(BM, BN, WM, WN)                                                                                     \
-    (planes ? tn_launch<BM, BN, WM, WN, true>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s) \
-            : tn_launch<BM, BN, WM, WN, false>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s))
+#define H3_TN(BM, BN, WM, WN, PIPE)                                                                              \
+    (planes ? tn_launch<BM, BN, WM, WN, 1>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s)  \
+            : tn_launch<BM, BN, WM, WN, PIPE>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s))
     switch (cfg) {
-        case 0: e = H3_TN(128, 192, 4, 2); break;
-        case 1: e = H3_TN(128, 192, 2, 2); break;
+        case 0: e = H3_TN(128, 192, 4, 2, 0); break;
+        case 1: e = H3_TN(128, 192, 2, 2, 0); break;
+        // k_h3_tnp: the split / staging interleaved into the MFMAs
+        case 10: e = H3_TN(128, 192, 4, 2, 2); break;
+        case 11: e = H3_TN(128, 192, 2, 2, 2); break;
         default: return hipErrorInvalidValue;
     }
 #undef H3_TN

@@ -123,8 +123,9 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
 constexpr int64_t ALL_WINDOWS = 1953125;
 __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict__ codes, int64_t n,
                                                      const float4 *__restrict__ Q, const float4 *__restrict__ b3,
-                                                     int T, float4 *__restrict__ Y3) {
+                                                     int T, float4 *__restrict__ Y3, uint32_t *__restrict__ amax) {
     const int64_t total = (int64_t)T * n * 9 * 16;
+    uint32_t mx[2] = {0u, 0u};  // max |Y3| per tower as float bits (fc1's h3 operand scale), when amax != null
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
         const int c = (int)(e & 15);
         const int64_t r = e >> 4, tu = r / 9;
@@ -154,9 +155,17 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
 #pragma unroll
         for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
         const float4 b = b3[t * 16 + c];
-        Y3[e] = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
-                            relu_nan(acc.w + b.w));
+        const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
+                                     relu_nan(acc.w + b.w));
+        Y3[e] = y;
+        if (amax) {
+            const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
+                                        std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
+            if (t == 0) mx[0] = std::max(mx[0], m);
+            else mx[1] = std::max(mx[1], m);
+        }
     }
+    if (amax) block_amax2(mx, T, amax);
 }
 
 // One wave per item of L entries; lane = (tower t, entry parity q, float4 column c): one wave
@@ -450,12 +459,12 @@ hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, c
 }
 
 hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, const float *b3, int T, float *Y3,
-                              hipStream_t s) {
+                              uint32_t *amax, hipStream_t s) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
     hipLaunchKernelGGL(k_codes_conv3, dim3(grid), dim3(256), 0, s, codes, n, reinterpret_cast<const float4 *>(Q),
-                       reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3));
+                       reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), amax);
     return hipGetLastError();
 }
 

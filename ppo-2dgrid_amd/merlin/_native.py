@@ -100,6 +100,7 @@ def lib():
     L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp]
     L.merlin_tower_all_windows.restype = i64
     L.merlin_tower_codes_conv3.argtypes = [vp, i64, vp, vp, i32, vp, vp]
+    L.merlin_tower_codes_conv3_amax.argtypes = [vp, i64, vp, vp, i32, vp, vp, vp]
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
     L.merlin_segment_sum_masked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                             vp]
@@ -171,6 +172,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
     "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
+    "merlin_tower_codes_conv3_amax",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_segment_sum_fused", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_tower_colsum",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
@@ -578,19 +580,22 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
 ALL_WINDOWS = 5 ** 9  # merlin_tower_all_windows()
 
 
-def codes_conv3(codes, Qall, b3):
+def codes_conv3(codes, Qall, b3, amax=None):
     """Y3 f32[T, n*9, 64]: relu(conv3) rows (k, p3) of frames codes[k] (int32 [n, 8]) from Qall
     f32[T, 5**9, 576], the per-window, per-tap conv3 partial sums of every possible window
-    (merlin_tower_codes_conv3)."""
+    (merlin_tower_codes_conv3).  amax (int32 [T], zeroed by the caller): receives max |Y3| per tower as float
+    bits (h3_amax's format)."""
     T, n = int(Qall.shape[0]), int(codes.shape[0])
     assert Qall.shape == (T, ALL_WINDOWS, 576) and Qall.dtype == torch.float32 and Qall.is_contiguous()
     assert codes.dtype == torch.int32 and codes.shape[1] == 8 and codes.is_contiguous() and b3.shape == (T, 64)
+    if amax is not None:
+        assert amax.dtype == torch.int32 and amax.numel() >= T
     out = torch.empty((T, n * 9, 64), dtype=torch.float32, device=Qall.device)
     # algorithmic bytes: codes read + Y3 written (the 81 Qall rows per frame and tower come from the
     # few thousand windows a rollout holds: cache-resident gathers, rocprofv3 PMC ~38 MB per launch)
     with KernelTimer.span("k_codes_conv3", n * 32 + T * n * 9 * 256):
-        check(lib().merlin_tower_codes_conv3(ptr(codes), n, ptr(Qall), ptr(b3), T, ptr(out), stream_of(Qall)),
-              "merlin_tower_codes_conv3")
+        check(lib().merlin_tower_codes_conv3_amax(ptr(codes), n, ptr(Qall), ptr(b3), T, ptr(out), ptr(amax),
+                                                  stream_of(Qall)), "merlin_tower_codes_conv3_amax")
     return out
 
 
@@ -890,7 +895,7 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
 # -- fc1 on the f16 matrix cores in two-plane form (csrc/merlin_h3.hip) ----------------------------------------
 # tile configurations of merlin_h3_gemm_nt (N = 512 / 576): the split interleaved into the MFMAs (k_h3_ntp), forward
 # 128 x 256 and input gradient 128 x 192 tiles (scripts/ab_update.py, same update replayed: 204.5 vs 209.0 ms for cfg 0 / 1)
-H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 2}
+H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 11}  # rollout: 4,096 rows; qall: [5^9, 64] x [64, 576]
 H3_TN_CFG = 0
 H3_TN_SPLITS = 32
 
@@ -906,6 +911,14 @@ def h3_amax(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     with KernelTimer.span("k_h3_amax", 4 * T * n):
         check(lib().merlin_h3_amax(ptr(x), n, T, n, ptr(out), stream_of(x)), "merlin_h3_amax")
     return out
+
+
+def h3_zero(amax: torch.Tensor) -> torch.Tensor:
+    """amax[:T] = 0 by a kernel (merlin_h3_amax over no values): safe inside a captured graph, where a memset node
+    replays with a wrong fill value on ROCm 7."""
+    assert amax.dtype == torch.int32 and amax.is_contiguous()
+    check(lib().merlin_h3_amax(None, 0, int(amax.numel()), 0, ptr(amax), stream_of(amax)), "merlin_h3_amax")
+    return amax
 
 
 def h3_split(x: torch.Tensor, amax: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

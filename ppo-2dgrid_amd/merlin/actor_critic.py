@@ -42,6 +42,11 @@ from .utils.utils_rl import layer_init
 
 # (out_channels, kernel, stride) of the three convs -- actor_critic.py:9-14
 _CONV_SPEC = ((32, 8, 4), (64, 4, 2), (64, 3, 1))
+# the rollout's all-windows conv3 table on the f16 two-plane GEMM (False: hipBLASLt's fp32 bmm; 1.1 ms less per
+# rollout, scripts/probe_rollout.py); the rollout's fc1 on it too (False: the x6 kernel -- at 4,096 rows per step
+# the h3 path with its per-step scale was 4.3 ms per rollout slower: 39.0 vs 34.7)
+QALL_H3 = True
+ROLLOUT_FC1_H3 = False
 
 
 class CNNFeatureExtractor(nn.Module):
@@ -540,13 +545,27 @@ class CNNActorCritic(nn.Module):
         if all_windows:
             Z2 = nat.window_lut(self._all_window_rows(T2.device), T2)  # [2, 5**9, 64]
             a2 = torch.relu_(Z2.add_(torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1)))
-            pack["Qall"] = torch.bmm(a2, W3r)  # [2, windows, (ky, kx, co)]
+            if self.fc1_impl in ("x6", "h3") and QALL_H3:
+                # the table GEMM [5^9, 64] x [64, 576] per tower on the f16 two-plane kernels (hipBLASLt's fp32
+                # GEMM took ~3.6 ms per rollout; the error bound is the same, tests/test_gpu_h3.py)
+                W3t = W3r.transpose(1, 2).contiguous()  # [2, 576, 64]: the NT kernel's B rows
+                am = nat.h3_amax(W3t)
+                pack["Qall"] = nat.h3_gemm_nt(a2, nat.h3_amax(a2), nat.h3_split(W3t, am), am,
+                                              cfg=nat.H3_NT_CFG["qall"], name="gemm_rollout_qall")
+            else:
+                pack["Qall"] = torch.bmm(a2, W3r)  # [2, windows, (ky, kx, co)]
         else:
             pack["T2"] = T2
             pack["b2"] = torch.stack([ea[2].bias, ec[2].bias]).contiguous()
             # im2col rows of A3 are (ky, kx, ci): conv3 weights as [2, 576, 64] in that order
             pack["W3t"] = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64).contiguous()
-        if self.fc1_impl in ("x6", "h3"):  # fc1 of every step on the bf16 MFMA, exact fp32 products (merlin_gemm2.hip)
+        if self.fc1_impl == "h3" and all_windows and ROLLOUT_FC1_H3:  # fc1 of every step on merlin_h3.hip
+            amW = nat.h3_amax(W4p.contiguous())
+            pack["W4h"] = (nat.h3_split(W4p.contiguous(), amW), amW)
+            # per step: max |a3| per tower (zeroed by a kernel before each step's conv3: this is built inside the
+            # captured rollout graph, where a memset would replay wrong)
+            pack["am3"] = torch.empty(2, dtype=torch.int32, device=W4p.device)
+        elif self.fc1_impl in ("x6", "h3"):  # fc1 of every step on the bf16 MFMA, exact fp32 products (merlin_gemm2.hip)
             pack["W4pp"] = nat.x6_split(W4p.contiguous())
         else:
             pack["W4t"] = W4p.transpose(1, 2).contiguous()
@@ -572,12 +591,18 @@ class CNNActorCritic(nn.Module):
         from .gemm_tuning import tuned
 
         n = codes.shape[0]
+        am3 = pack.get("am3")
+        if am3 is not None:
+            nat.h3_zero(am3)  # a kernel: this runs inside the captured rollout graph
         if "Qall" in pack:
-            a3 = nat.codes_conv3(codes, pack["Qall"], pack["b3"]).view(2, n, 576)
+            a3 = nat.codes_conv3(codes, pack["Qall"], pack["b3"], amax=am3).view(2, n, 576)
         else:  # per-frame conv2 lookups + conv3 GEMM (small rollouts, rollout_pack)
             A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
             a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
-        if "W4pp" in pack:
+        if "W4h" in pack:
+            P4, amW = pack["W4h"]
+            z = nat.h3_gemm_nt(a3, am3, P4, amW, cfg=nat.H3_NT_CFG["rollout"], name="gemm_rollout_fc1")
+        elif "W4pp" in pack:
             z = nat.x6_gemm_nt(a3, pack["W4pp"], cfg=nat.X6_NT_CFG["rollout"], name="gemm_rollout_fc1")
         else:
             with tuned("rollout"):

@@ -53,8 +53,9 @@ def main():
             W.OVERLAP_WGRAD = {"no_overlap": False, "x6_overlap": True}.get(name, "deferred")
             agent.ac.fc1_impl = "hipblaslt" if name == "hipblaslt" else "x6" if "x6" in name else "h3"
             nat.SEG_FUSED = "segfix" not in name  # the segmented sums' fix-ups in a second launch (k_seg_fix)
-            nat.H3_NT_CFG["fwd"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3f"), 0)
-            nat.H3_NT_CFG["dgrad"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3d"), 1)
+            nat.H3_NT_CFG["fwd"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3f"), 13)
+            nat.H3_NT_CFG["dgrad"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3d"), 11)
+            nat.H3_TN_CFG = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3t"), 0)
             agent._clip_adam = None if name == "torch_opt" else clip_adam
             agent.fast_step = name.startswith("fast")  # merlin/fast_step.py vs the autograd engine
             from merlin import fast_step as FS

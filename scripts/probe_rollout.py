@@ -1,6 +1,6 @@
 """In-process A/B of rollout settings at the bench workload (4096 envs x 256 steps, captured rollout graph):
 one agent, each setting's graph captured once, then rollouts timed alternately.
-    python scripts/probe_rollout.py [rounds] [refill_every values, e.g. 1,2,4]"""
+    python scripts/probe_rollout.py [rounds] [settings, e.g. 1,2,4 (refill_every) or x6,h3r12,h3r2,h3r12_qbmm]"""
 import os
 import statistics
 import sys
@@ -15,7 +15,17 @@ from merlin.ppo import PPO
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    vals = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1,2").split(",")]
+    vals = (sys.argv[2] if len(sys.argv) > 2 else "1,2").split(",")
+    from merlin import _native as nat
+    from merlin import actor_critic as AC
+
+    def setting(v):
+        if v.isdigit():
+            agent.refill_every = int(v)
+            return
+        AC.ROLLOUT_FC1_H3 = v.startswith("h3")
+        nat.H3_NT_CFG["rollout"] = next((int(t[3:]) for t in v.split("_") if t[:3] == "h3r"), 12)
+        AC.QALL_H3 = "qbmm" not in v
     dev = torch.device("cuda", 0)
     env = MerlinVecEnv(4096, "mediumhard", seed=777, device=dev)
     torch.manual_seed(777)
@@ -24,7 +34,7 @@ def main():
         agent.update(agent.collect_rollouts())
     graphs = {}
     for v in vals:
-        agent.refill_every = v
+        setting(v)
         agent._graph = None
         agent.collect_rollouts()  # eager + capture
         graphs[v] = agent._graph
@@ -32,13 +42,14 @@ def main():
     for _ in range(rounds):
         for v in vals:
             agent._graph = graphs[v]
+            setting(v)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             agent.collect_rollouts()
             torch.cuda.synchronize()
             times[v].append((time.perf_counter() - t0) * 1e3)
     for v in vals:
-        print(f"refill_every {v}: median {statistics.median(times[v]):.2f} ms per rollout  all "
+        print(f"{v}: median {statistics.median(times[v]):.2f} ms per rollout  all "
               f"{[round(x, 2) for x in times[v]]}", flush=True)
 
 
