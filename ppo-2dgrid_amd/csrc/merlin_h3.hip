@@ -692,7 +692,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
 // 4 (r & 3)) and RC = 24 (XOR 4 ((r >> 1) & 1)).  Slabs are written already unscaled (x 2^-(eA + eB), exact).
 template <int RC>
 __device__ __forceinline__ int tr_swz(int row) {
-    static_assert(RC % 16 == 0 || RC == 24, "row chunks");
+    // RC = 8 (128-B rows) as RC = 24: two rows per 256-B bank row, rows r and r + 2 on the same slots
+    static_assert(RC % 16 == 0 || RC == 24 || RC == 8, "row chunks");
     return RC % 16 == 0 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
 }
 
@@ -1329,6 +1330,7 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 1: return H3_NT(128, 192, 4, 2, false);
         case 2: return H3_NT(128, 128, 2, 2, false);
         case 3: return H3_NT(128, 256, 2, 4, false);
+        case 5: return H3_NT(128, 64, 4, 1, false);  // N = 64 (the window GEMM's input gradient)
         // k_h3_ntp: the k step's split / staging interleaved into the MFMAs
         case 10: return H3_NT(256, 128, 4, 2, true);
         case 11: return H3_NT(128, 192, 4, 2, true);
@@ -1367,6 +1369,7 @@ hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B
     switch (cfg) {
         case 0: e = H3_TN(128, 192, 4, 2, 0); break;
         case 1: e = H3_TN(128, 192, 2, 2, 0); break;
+        case 2: e = H3_TN(64, 192, 2, 2, 0); break;  // M = 64 (the window GEMM's weight gradient)
         // k_h3_tnp: the split / staging interleaved into the MFMAs
         case 10: e = H3_TN(128, 192, 4, 2, 2); break;
         case 11: e = H3_TN(128, 192, 2, 2, 2); break;

@@ -168,7 +168,10 @@ __device__ __forceinline__ void block_amax2(const uint32_t mx[2], int T, uint32_
     if (threadIdx.x < (unsigned)T) {
         const uint32_t *r = red[threadIdx.x];
         const uint32_t m = max(max(r[0], r[1]), max(r[2], r[3]));
-        if (m) atomicMax(amax + threadIdx.x, m);
+        // the word only grows: a block whose max is not above it (most of them, once a few have reported) skips
+        // the atomic -- thousands of same-address atomics serialise at the memory side
+        if (m && m > __hip_atomic_load(amax + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMax(amax + threadIdx.x, m);
     }
 }
 

@@ -120,66 +120,92 @@ __global__ __launch_bounds__(256) void k_stage_bwd_h(const float *__restrict__ W
     dH[hi] = HT[hi] > 0.0f ? (float)acc : 0.0f;
 }
 
-constexpr int VS = 32;  // combinations per LDS stage of the dW2 blocks
+constexpr int VS = 64;      // combinations per LDS stage of the dW2 blocks
+constexpr int WT = 1024;    // threads of k_stage_bwd_w
+constexpr int WQ = WT / 256;  // combination groups of a dW2 block (each thread of a group: 8 outputs)
 
 // blocks [0, T * 16): (tower, type, j): dW2[co][o][tap] = sum over the type's combinations of HT[v][o] *
-// dT2[4 v + j][co], 8 outputs per thread, combinations staged VS at a time;  blocks [T * 16, T * 16 + T * C1):
-// tower t, conv1 channel o: db1[o] = sum_v dH[v][o] (256 strided partial sums, then a fixed tree), dP[o][k] for
-// the 80 k (combinations in (v, e) order through the CSR kinv), then dW1[o][c][ky][kx]
-__global__ __launch_bounds__(256) void k_stage_bwd_w(const float *__restrict__ HT, const float *__restrict__ dT2,
-                                                     const float *__restrict__ dH, const float *__restrict__ atlas,
-                                                     const int16_t *__restrict__ koff, const int16_t *__restrict__ kv,
-                                                     int T, float *__restrict__ dW1, float *__restrict__ db1,
-                                                     float *__restrict__ dW2) {
+// dT2[4 v + j][co]; group g of the block's four thread groups sums the combinations v with (v - va) % 4 == g in
+// order (8 outputs per thread), the four partials join in a fixed order -- a type-3 block walks 625 combinations,
+// so one group per block made its 20 dependent load-and-sum stages the kernel's time;  blocks [T * 16, T * 16 +
+// T * C1): tower t, conv1 channel o: db1[o] = sum_v dH[v][o] (strided partial sums, then a fixed tree), dP[o][k]
+// for the 80 k (combinations in (v, e) order through the CSR kinv), then dW1[o][c][ky][kx]
+__global__ __launch_bounds__(WT) void k_stage_bwd_w(const float *__restrict__ HT, const float *__restrict__ dT2,
+                                                    const float *__restrict__ dH, const float *__restrict__ atlas,
+                                                    const int16_t *__restrict__ koff, const int16_t *__restrict__ kv,
+                                                    int T, float *__restrict__ dW1, float *__restrict__ db1,
+                                                    float *__restrict__ dW2) {
     __shared__ float Hs[VS][C1], Gs[VS][C2];
-    __shared__ double red[256], dP[80];
+    __shared__ double part[WQ - 1][256 * 8], red[WT], dP[80];
     if ((int)blockIdx.x < T * 16) {
         const int t = blockIdx.x / 16, p = (blockIdx.x / 4) & 3, j = blockIdx.x & 3;
         const int tap = (2 * (j >> 1) + (p >> 1)) * 4 + 2 * (j & 1) + (p & 1);
         const int va = part_off(p), vb = part_off(p + 1);
-        const int o = threadIdx.x & (C1 - 1), cq = threadIdx.x >> 5;  // outputs (co = cq + 8 i, o)
+        const int g = threadIdx.x >> 8, l = threadIdx.x & 255;
+        const int o = l & (C1 - 1), cq = l >> 5;  // outputs (co = cq + 8 i, o)
         double acc[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) acc[i] = 0.0;
         for (int vs = va; vs < vb; vs += VS) {
             const int n = min(VS, vb - vs);
             __syncthreads();
-            for (int q = threadIdx.x; q < n * C1; q += 256) Hs[q / C1][q % C1] = HT[((size_t)t * NV + vs) * C1 + q];
-            for (int q = threadIdx.x; q < n * C2; q += 256) {
+            for (int q = threadIdx.x; q < n * C1; q += WT) Hs[q / C1][q % C1] = HT[((size_t)t * NV + vs) * C1 + q];
+            for (int q = threadIdx.x; q < n * C2; q += WT) {
                 const int vl = q / C2, co = q - vl * C2;
                 Gs[vl][co] = dT2[((size_t)t * NROW + 4 * (vs + vl) + j) * C2 + co];
             }
             __syncthreads();
-            for (int vl = 0; vl < n; vl++) {
+            for (int vl = g; vl < n; vl += WQ) {  // VS % WQ == 0: group g keeps its residue across stages
                 const double h = Hs[vl][o];
 #pragma unroll
                 for (int i = 0; i < 8; i++) acc[i] += h * (double)Gs[vl][cq + 8 * i];
             }
         }
+        if (g > 0) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) dW2[(((size_t)t * C2 + cq + 8 * i) * C1 + o) * 16 + tap] = (float)acc[i];
+            for (int i = 0; i < 8; i++) part[g - 1][i * 256 + l] = acc[i];
+        }
+        __syncthreads();
+        if (g == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const double s = (acc[i] + part[0][i * 256 + l]) + (part[1][i * 256 + l] + part[2][i * 256 + l]);
+                dW2[(((size_t)t * C2 + cq + 8 * i) * C1 + o) * 16 + tap] = (float)s;
+            }
+        }
         return;
     }
     const int b = blockIdx.x - T * 16, t = b / C1, o = b - t * C1;
     const float *d = dH + (size_t)t * NV * C1 + o;
-    {  // db1: thread i sums combinations i, i + 256, ... in order, then a fixed tree
+    {  // db1: thread i sums combinations i, i + WT, ... in order, then a fixed tree
         double s = 0.0;
-        for (int v = threadIdx.x; v < NV; v += 256) s += d[(size_t)v * C1];
+        for (int v = threadIdx.x; v < NV; v += WT) s += d[(size_t)v * C1];
         red[threadIdx.x] = s;
     }
     if (threadIdx.x < 80) {  // dP[o][k]: the (v, e) entries with idx[v][e] = k, in (v, e) order
-        const int k = threadIdx.x;
+        // eight entries' loads in flight at a time (clamped indices, no select next to a load), added in order
+        const int k = threadIdx.x, i1 = koff[k + 1];
         double acc = 0.0;
-        for (int i = koff[k]; i < koff[k + 1]; i++) acc += d[(size_t)kv[i] * C1];
+        for (int i0 = koff[k]; i0 < i1; i0 += 8) {
+            int r[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) r[u] = kv[min(i0 + u, i1 - 1)];
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) x[u] = d[(size_t)r[u] * C1];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (i0 + u < i1) acc += x[u];
+        }
         dP[k] = acc;
     }
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
+    for (int w = WT / 2; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
     if (threadIdx.x == 0) db1[t * C1 + o] = (float)red[0];
-    for (int q = threadIdx.x; q < 3 * 64; q += 256) {  // dW1[t][o][c][ky][kx]
+    for (int q = threadIdx.x; q < 3 * 64; q += WT) {  // dW1[t][o][c][ky][kx]
         const int c = q >> 6, ky = (q >> 3) & 7, kx = q & 7;
         const int dy = ky >> 2, kk = ky & 3, dx = kx >> 2, l = kx & 3, slot = 2 * dy + dx;
         double acc = 0.0;
@@ -205,7 +231,7 @@ hipError_t launch_stage_bwd(const float *W2, const float *HT, const float *dT2, 
     hipLaunchKernelGGL(k_stage_bwd_h, dim3(NCH, T), dim3(256), 0, s, W2, HT, dT2, dH);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_stage_bwd_w, dim3(T * 16 + T * C1), dim3(256), 0, s, HT, dT2, dH, atlas, koff, kv, T, dW1,
+    hipLaunchKernelGGL(k_stage_bwd_w, dim3(T * 16 + T * C1), dim3(WT), 0, s, HT, dT2, dH, atlas, koff, kv, T, dW1,
                        db1, dW2);
     return hipGetLastError();
 }

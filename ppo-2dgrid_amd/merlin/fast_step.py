@@ -87,12 +87,15 @@ class WeightStage:
                 ("W3r", st(ea[4].weight, ec[4].weight).permute(0, 2, 3, 4, 1).reshape(2, 64, 576)),
                 ("b3", st(ea[4].bias, ec[4].bias)), ("b4", st(fa.bias, fc.bias)), ("W4p", W4p),
                 ("W4pT", W4p.transpose(1, 2).contiguous())]
+        W3r = segs[4][1]
+        segs.append(("W3rT", W3r.transpose(1, 2).contiguous()))  # [2, 576, 64]: the window GEMM's B rows
         self.shapes, self.offs, o = {}, {}, 0
         for name, t in segs:
             self.shapes[name], self.offs[name] = tuple(t.shape), o
             o += t.numel()
         dev = flat_params.device
         self.amaxW = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.amaxW3 = torch.zeros(2, dtype=torch.int32, device=dev)
         self.fwd_map = torch.cat([t.reshape(-1) for _, t in segs]).to(dev)
         self.n_grad = self.offs["W4pT"]  # every stage-parameter element once in D[:n_grad]
         assert int(self.fwd_map[:self.n_grad].unique().numel()) == self.n_grad
@@ -120,8 +123,13 @@ class WeightStage:
         if self.fc1 == "h3":
             W4p, W4pT = self.seg(D, "W4p"), self.seg(D, "W4pT")
             nat.h3_amax(W4p, out=self.amaxW)  # W4p^T holds the same values: one scale for both
-            return D, leaves, T2, (nat.h3_split(W4p, self.amaxW), nat.h3_split(W4pT, self.amaxW))
-        planes = nat.x6_split(D[o:].view(-1, 8)).view(-1)  # W4p and W4p^T back to back
+            planes = (nat.h3_split(W4p, self.amaxW), nat.h3_split(W4pT, self.amaxW))
+            if WINDOW_H3:  # conv3's weights for the window GEMMs: W3r^T (forward), W3r (input gradient)
+                W3r, W3rT = self.seg(D, "W3r"), self.seg(D, "W3rT")
+                nat.h3_amax(W3r, out=self.amaxW3)
+                planes += (nat.h3_split(W3rT, self.amaxW3), nat.h3_split(W3r, self.amaxW3))
+            return D, leaves, T2, planes
+        planes = nat.x6_split(D[o:self.offs["W3rT"]].view(-1, 8)).view(-1)  # W4p and W4p^T back to back
         n4 = 2 * H * 576 * 3
         return D, leaves, T2, (planes[:n4].view(2, H, 3 * 576), planes[n4:].view(2, 576, 3 * H))
 
@@ -180,6 +188,11 @@ class WeightStage:
 # too) or from after the input gradient (False: beside conv3's segmented sums only)
 WGRAD_EARLY = False
 WGRAD_SIDE = True  # False: the weight gradient on the main stream (diagnostics)
+# h3: the window GEMMs (conv3's Q = a2w W3r and its two backward products, ~6.6k rows) on the f16 two-plane kernels
+# too (False: hipBLASLt's fp32 GEMMs, the split-K weight gradient and its torch sum).  Off: with their operand scales
+# (two reductions per step) they measured 200.8 vs 199.5 ms per update (scripts/ab_update.py 4 6 fast,fast_nowh3,
+# weight stage captured with the planes either way)
+WINDOW_H3 = False
 # h3: the weight gradient over the planes the NT GEMMs left (False: it splits a3, dz itself).  Off: the planes cost the
 # forward 60-100 us of writes (a3: 2 x U x 576 x 4 B) for 50 us saved in the weight gradient (scripts/probe_h3.py)
 WGRAD_PLANES = False
@@ -216,6 +229,7 @@ class WindowStep:
         self.head = (ac.actor[2].weight, ac.actor[2].bias, ac.critic[2].weight, ac.critic[2].bias)
         self._side = None
         self.amax_act = torch.zeros(4, dtype=torch.int32, device=agent.device)
+        self.amax_win = torch.zeros(4, dtype=torch.int32, device=agent.device)  # a2w's and dQ's scales
 
     def valid(self) -> bool:
         if not (self.stage.valid() and all(p.requires_grad for p in self.params)):
@@ -258,10 +272,17 @@ class WindowStep:
         if h3:
             am.zero_()
         T2, b2, W3r, b3, _, b4 = self.stage.forward()
-        P4, P4t = self.stage.planes
+        P4, P4t = self.stage.planes[:2]
         am3, amz, amW = am[0:2], am[2:4], self.stage.amaxW
         a2w = nat.bias_relu_(nat.window_lut(plan.rows, T2), b2)  # relu(conv2) of every window
-        Q = torch.bmm(a2w, W3r)  # [2, windows, (ky, kx, co)]
+        wh3 = h3 and WINDOW_H3 and len(self.stage.planes) == 4
+        if wh3:
+            P3t, P3 = self.stage.planes[2:]
+            am2, amq, amW3 = self.amax_win[0:2], self.amax_win[2:4], self.stage.amaxW3
+            nat.h3_amax(a2w, out=am2)
+            Q = nat.h3_gemm_nt(a2w, am2, P3t, amW3, cfg=nat.H3_NT_CFG["qwin"], name="gemm_window_fwd")
+        else:
+            Q = torch.bmm(a2w, W3r)  # [2, windows, (ky, kx, co)]
         Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None)
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
@@ -318,9 +339,14 @@ class WindowStep:
         dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]))
         nat.colsum(dQ.view(2, -1, 9, 64)[:, :, 0], out=g[3])  # db3: every (u, p3) has one window at tap 0
         dQ = dQ.view(2, -1, 576)
-        da2w = torch.bmm(dQ, W3r.transpose(1, 2))
-        chunks = max(1, a2w.shape[1] // 256)
-        _splitk_bmm_tn(a2w, dQ, chunks, min_chunk=128, name="gemm_window_wgrad", out=g[2])
+        if wh3:
+            nat.h3_amax(dQ, out=amq)
+            da2w = nat.h3_gemm_nt(dQ, amq, P3, amW3, cfg=nat.H3_NT_CFG["qwin_dgrad"], name="gemm_window_dgrad")
+            nat.h3_gemm_tn(a2w, am2, dQ, amq, cfg=nat.H3_TN_CFG_WIN, name="gemm_window_wgrad", out=g[2])
+        else:
+            da2w = torch.bmm(dQ, W3r.transpose(1, 2))
+            chunks = max(1, a2w.shape[1] // 256)
+            _splitk_bmm_tn(a2w, dQ, chunks, min_chunk=128, name="gemm_window_wgrad", out=g[2])
         nat.relu_bwd(a2w, da2w, out=da2w, out_bias=g[1])
         nat.segment_sum(da2w, plan.hist, nat.LUT2_ROWS, name="k_seg_sum_dT2", out=g[0])
         main.wait_stream(side)

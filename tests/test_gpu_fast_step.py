@@ -39,7 +39,12 @@ def _run(device, fast, iters=3, stage_impl="hip", first_grads=None):
     return agent, stats
 
 
-def test_fast_step_matches_autograd_bitwise(device):
+def test_fast_step_matches_autograd_bitwise(device, monkeypatch):
+    from merlin import fast_step
+
+    # the autograd path runs the window GEMMs on hipBLASLt: the same GEMMs here (the h3 form of them is held to
+    # fp32-GEMM accuracy by tests/test_gpu_h3.py and to the autograd path by the test below)
+    monkeypatch.setattr(fast_step, "WINDOW_H3", False)
     a0, s0 = _run(device, False)
     a1, s1 = _run(device, True, stage_impl="torch")
     assert a1._wstep is not None and a0._wstep is None

@@ -87,8 +87,9 @@ def test_gemm_nt_vs_float64(device, M, N, K, cfg, scale_a, ragged):
     assert torch.equal(Cp, C) and torch.equal(P, nat.h3_split(A, amA))
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
-@pytest.mark.parametrize("Kd,splits,scale", [(1, 1, 1.0), (4093, 7, 1.0), (40000, 32, 1.0), (40000, 32, 1e-7)])
+@pytest.mark.parametrize("cfg", [0, 1, 10, 11])
+@pytest.mark.parametrize("Kd,splits,scale", [(1, 1, 1.0), (4093, 7, 1.0), (40000, 32, 1.0), (40000, 32, 1e-7),
+                                             (40000, 3, 1.0)])
 def test_gemm_tn_vs_float64(device, Kd, splits, scale, cfg):
     from merlin import _native as nat
 
@@ -103,8 +104,10 @@ def test_gemm_tn_vs_float64(device, Kd, splits, scale, cfg):
     W = nat.h3_gemm_tn(dz, amz, a3, am3, splits=splits, cfg=cfg)
     assert _err(W, W64, den) <= tol
     assert torch.equal(W, nat.h3_gemm_tn(dz, amz, a3, am3, splits=splits, cfg=cfg))
+    if cfg:  # every configuration sums each output's products in the same order
+        assert torch.equal(W, nat.h3_gemm_tn(dz, amz, a3, am3, splits=splits, cfg=0))
     # over the operands' planes (what the fast step's NT GEMMs leave): the same images, the same bits
-    Wq = nat.h3_gemm_tn(nat.h3_split(dz, amz), amz, nat.h3_split(a3, am3), am3, splits=splits, cfg=cfg)
+    Wq = nat.h3_gemm_tn(nat.h3_split(dz, amz), amz, nat.h3_split(a3, am3), am3, splits=splits, cfg=cfg % 10)
     assert torch.equal(Wq, W)
 
 
