@@ -146,15 +146,38 @@ __global__ __launch_bounds__(WT) void k_stage_bwd_w(const float *__restrict__ HT
         double acc[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) acc[i] = 0.0;
+        // the next stage's values are loaded into registers while this stage is summed (one stage of HT and dT2
+        // rows: VS * C1 / WT = 2 and VS * C2 / WT = 4 values per thread; rows past the type's end read as 0)
+        constexpr int NH = VS * C1 / WT, NG = VS * C2 / WT;
+        float rh[NH], rg[NG];
+        auto load = [&](int vs) {
+#pragma unroll
+            for (int u = 0; u < NH; u++) {
+                const int q = threadIdx.x + u * WT, vl = q / C1;
+                rh[u] = vs + vl < vb ? HT[((size_t)t * NV + vs) * C1 + q] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < NG; u++) {
+                const int q = threadIdx.x + u * WT, vl = q / C2, co = q - vl * C2;
+                rg[u] = vs + vl < vb ? dT2[((size_t)t * NROW + 4 * (vs + vl) + j) * C2 + co] : 0.0f;
+            }
+        };
+        load(va);
         for (int vs = va; vs < vb; vs += VS) {
             const int n = min(VS, vb - vs);
             __syncthreads();
-            for (int q = threadIdx.x; q < n * C1; q += WT) Hs[q / C1][q % C1] = HT[((size_t)t * NV + vs) * C1 + q];
-            for (int q = threadIdx.x; q < n * C2; q += WT) {
-                const int vl = q / C2, co = q - vl * C2;
-                Gs[vl][co] = dT2[((size_t)t * NROW + 4 * (vs + vl) + j) * C2 + co];
+#pragma unroll
+            for (int u = 0; u < NH; u++) {
+                const int q = threadIdx.x + u * WT;
+                Hs[q / C1][q % C1] = rh[u];
+            }
+#pragma unroll
+            for (int u = 0; u < NG; u++) {
+                const int q = threadIdx.x + u * WT;
+                Gs[q / C2][q % C2] = rg[u];
             }
             __syncthreads();
+            if (vs + VS < vb) load(vs + VS);
             for (int vl = g; vl < n; vl += WQ) {  // VS % WQ == 0: group g keeps its residue across stages
                 const double h = Hs[vl][o];
 #pragma unroll
