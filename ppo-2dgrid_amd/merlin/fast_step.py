@@ -196,6 +196,10 @@ WINDOW_H3 = False
 # h3: the weight gradient over the planes the NT GEMMs left (False: it splits a3, dz itself).  Off: the planes cost the
 # forward 60-100 us of writes (a3: 2 x U x 576 x 4 B) for 50 us saved in the weight gradient (scripts/probe_h3.py)
 WGRAD_PLANES = False
+# h3: the weight gradient's operand planes made by k_h3_split on the side stream, beside the forward and
+# input-gradient GEMMs (which do not store them), so the weight gradient runs on planes (merlin_h3_gemm_tn_planes).
+# Off: the splits take the GEMMs' CUs (scripts/ab_update.py 4 6 fast,fast_nosplit: 218.7 vs 189.9 ms per update)
+WGRAD_SPLIT_SIDE = False
 
 
 class WindowStep:
@@ -287,10 +291,17 @@ class WindowStep:
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
         pa3 = pdz = None
+        main = torch.cuda.current_stream()
+        side = self.side_stream(a3.device)
+        split_side = h3 and WGRAD_SPLIT_SIDE and WGRAD_SIDE and not WGRAD_EARLY
+        if split_side:  # a3's planes for the weight gradient, on the side stream beside the forward GEMM
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                pa3 = nat.h3_split(a3, am3)
         if h3:
             # the forward and input-gradient GEMMs leave their fp32 operand's planes (a3's, dz's) for the weight
             # gradient, which then stages copies instead of splitting both operands again
-            if WGRAD_PLANES:
+            if WGRAD_PLANES and not split_side:
                 pa3 = torch.empty((2, n, 1152), dtype=torch.int16, device=a3.device)
             h = nat.h3_gemm_nt(a3, am3, P4, amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd",
                                planes_out=pa3)
@@ -305,8 +316,10 @@ class WindowStep:
         # ---- backward (_WindowTowerHeadX6.backward, _WindowGemm / _BiasRelu / _WindowConv2 backward)
         dz, _, _, _ = nat.head_bwd(h, dlogits, dvalue, Wa, Wc, out_bias=g[5], out_w_actor=self.views[Wa],
                                    out_w_critic=self.views[Wc], amax=amz if h3 else None)
-        main = torch.cuda.current_stream()
-        side = self.side_stream(dz.device)
+        if split_side:  # and dz's beside the input-gradient GEMM
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                pdz = nat.h3_split(dz, amz)
 
         def wgrad():
             if h3 and pdz is not None:
@@ -321,10 +334,10 @@ class WindowStep:
             with torch.cuda.stream(side):
                 wgrad()
         if h3:
-            if pa3 is not None and not WGRAD_EARLY:
+            if pa3 is not None and not WGRAD_EARLY and not split_side:
                 pdz = torch.empty((2, n, 1024), dtype=torch.int16, device=dz.device)
             da3 = nat.h3_gemm_nt(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad"], name="gemm_fc1_dgrad",
-                                 planes_out=pdz)
+                                 planes_out=None if split_side else pdz)
         else:
             da3 = nat.x6_gemm_nt(dz, P4t, cfg=nat.X6_NT_CFG["dgrad"], name="gemm_fc1_dgrad")
         if not WGRAD_SIDE:

@@ -62,6 +62,7 @@ def main():
 
             FS.WGRAD_EARLY = "wgrad_early" in name
             FS.WINDOW_H3 = "wh3" in name
+            FS.WGRAD_SPLIT_SIDE = "splitside" in name
             nat.X6_NT_CFG["fwd"] = 28 if "fwd28" in name else 20
             nat.X6_NT_CFG["dgrad"] = 27 if "dgrad27" in name else 22
             nat.X6_TN_CFG = next((int(t[2:]) for t in name.split("_") if t[:2] == "tn" and t[2:].isdigit()), 0)
