@@ -59,8 +59,12 @@ def main():
     print(f"lib {os.path.basename(nat.LIB_PATH)}  U={U} patches={plan.num_patches} bands={plan.num_bands} "
           f"fix rows R/S/dQ {plan.patch_plan.fix.shape[0]}/{plan.band_plan.fix.shape[0]}/{plan.dq_plan.fix.shape[0]}",
           flush=True)
-    for name, f in (("R", fR), ("S", fS), ("dQ", fQ)):
-        print(f"  {name}: {ev(f, reps):.1f} us (segmented sum + fix-ups)", flush=True)
+    for fused in (True, False):  # fix-ups inside the launch (merlin_segment_sum_fused) / a k_seg_fix launch
+        nat.SEG_FUSED = fused
+        fR(), fS(), fQ()
+        ts = [ev(f, reps) for f in (fR, fS, fQ)]
+        print(f"  {'in-launch fix-ups' if fused else 'k_seg_fix launches'}: R {ts[0]:.1f}  S {ts[1]:.1f}  "
+              f"dQ {ts[2]:.1f}  sum {sum(ts):.1f} us", flush=True)
     for name, p in (("R", plan.patch_plan), ("S", plan.band_plan), ("dQ", plan.dq_plan)):
         fx = p.fix[p.fix[:, 0] >= 0]
         span = (fx[:, 2] - fx[:, 1]).float()
