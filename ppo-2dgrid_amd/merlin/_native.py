@@ -895,9 +895,9 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
 # -- fc1 on the f16 matrix cores in two-plane form (csrc/merlin_h3.hip) ----------------------------------------
 # tile configurations of merlin_h3_gemm_nt (N = 512 / 576): the split interleaved into the MFMAs (k_h3_ntp), forward
 # 128 x 256 and input gradient 128 x 192 tiles (scripts/ab_update.py, same update replayed: 204.5 vs 209.0 ms for cfg 0 / 1)
-# rollout: 4,096 rows; qall: [5^9, 64] x [64, 576]; qwin / qwin_dgrad: the update's window GEMMs (N = 576, K = 64 /
-# N = 64, K = 576)
-H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 11, "qwin": 11, "qwin_dgrad": 5}
+# rollout: 4,096 rows; qall: [5^9, 64] x [64, 576] (k_h3_nt, not the input gradient's k_h3_ntp instantiation, so
+# profiles keep the two apart); qwin / qwin_dgrad: the update's window GEMMs (N = 576, K = 64 / N = 64, K = 576)
+H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 1, "qwin": 11, "qwin_dgrad": 5}
 H3_TN_CFG = 0
 H3_TN_CFG_WIN = 2  # the window weight gradient (M = 64)
 H3_TN_SPLITS = 32
