@@ -42,11 +42,12 @@ from .utils.utils_rl import layer_init
 
 # (out_channels, kernel, stride) of the three convs -- actor_critic.py:9-14
 _CONV_SPEC = ((32, 8, 4), (64, 4, 2), (64, 3, 1))
-# the rollout's all-windows conv3 table on the f16 two-plane GEMM (False: hipBLASLt's fp32 bmm; 1.1 ms less per
-# rollout, scripts/probe_rollout.py); the rollout's fc1 on it too (False: the x6 kernel -- at 4,096 rows per step
-# the h3 path with its per-step scale was 4.3 ms per rollout slower: 39.0 vs 34.7)
+# the rollout's all-windows conv3 table on the f16 two-plane GEMM (False: hipBLASLt's fp32 bmm; 0.8 ms less per
+# rollout, scripts/probe_rollout.py); the rollout's fc1 on it too (False: the x6 kernel), with a3's scale reduced by
+# k_codes_conv3 as it writes a3: 31.9 vs 33.4 ms per rollout (before the scale reduction skipped its redundant
+# same-address atomics, 39.0 vs 34.7: one atomic per block of a 8,192-block grid serialised)
 QALL_H3 = True
-ROLLOUT_FC1_H3 = False
+ROLLOUT_FC1_H3 = True
 
 
 class CNNFeatureExtractor(nn.Module):
