@@ -338,7 +338,10 @@ __global__ __launch_bounds__(BLK) void k_col2im3_bwd_chunked(const float4 *__res
     // NaN/inf propagate as a non-finite max (the histogram then returns NaN)
     for (int off = 32; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
     if (amax != amax) amax = __int_as_float(0x7f800000);
-    if ((threadIdx.x & 63) == 0) atomicMax(absmax, __float_as_uint(amax));
+    // skip the same-address atomic when the word already holds at least this wave's max (it only grows)
+    if ((threadIdx.x & 63) == 0 &&
+        __float_as_uint(amax) > __hip_atomic_load(absmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(absmax, __float_as_uint(amax));
 }
 
 int grid_cap(int64_t rows) { return (int)std::max<int64_t>(1, std::min<int64_t>(rows, 256 * 16)); }
