@@ -188,6 +188,7 @@ class WeightStage:
 # too) or from after the input gradient (False: beside conv3's segmented sums only)
 WGRAD_EARLY = False
 WGRAD_SIDE = True  # False: the weight gradient on the main stream (diagnostics)
+SIDE_PRIORITY = 0  # the side stream's priority (torch.cuda.Stream priority: lower = higher priority)
 # h3: the window GEMMs (conv3's Q = a2w W3r and its two backward products, ~6.6k rows) on the f16 two-plane kernels
 # too (False: hipBLASLt's fp32 GEMMs, the split-K weight gradient and its torch sum).  Off: with their operand scales
 # (two reductions per step) they measured 200.8 vs 199.5 ms per update (scripts/ab_update.py 4 6 fast,fast_nowh3,
@@ -256,8 +257,9 @@ class WindowStep:
                 p.grad = v
 
     def side_stream(self, device):
-        if self._side is None:
-            self._side = torch.cuda.Stream(device=device)
+        if self._side is None or getattr(self, "_side_prio", 0) != SIDE_PRIORITY:
+            self._side = torch.cuda.Stream(device=device, priority=SIDE_PRIORITY)
+            self._side_prio = SIDE_PRIORITY
         return self._side
 
     def step(self, plan, mb, mb_idx, actions, logp_old, adv, ret, totals):

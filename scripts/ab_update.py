@@ -56,11 +56,13 @@ def main():
             nat.H3_NT_CFG["fwd"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3f"), 13)
             nat.H3_NT_CFG["dgrad"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3d"), 11)
             nat.H3_TN_CFG = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3t"), 0)
+            nat.H3_TN_SPLITS = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3s"), 32)
             agent._clip_adam = None if name == "torch_opt" else clip_adam
             agent.fast_step = name.startswith("fast")  # merlin/fast_step.py vs the autograd engine
             from merlin import fast_step as FS
 
             FS.WGRAD_EARLY = "wgrad_early" in name
+            FS.SIDE_PRIORITY = -1 if "sidehi" in name else 0
             FS.WINDOW_H3 = "wh3" in name
             FS.WGRAD_SPLIT_SIDE = "splitside" in name
             nat.X6_NT_CFG["fwd"] = 28 if "fwd28" in name else 20
