@@ -312,6 +312,16 @@ int merlin_tower_window_conv3_bits(const float *Q_dev, int64_t n_windows, const 
                                    const int64_t *groups_dev, int64_t n, const float *b3_dev,
                                    int32_t towers, float *Y3_dev, uint64_t *relu_bits_dev, uint32_t *amax_dev,
                                    void *stream);
+/* merlin_tower_window_conv3_bits (relu_bits_dev may be NULL here) computing each distinct 5x5-tile patch once:
+ * rows (k, p3) whose frames hold the same patch at p3 read the same windows, so only the representative rows
+ * (rep_row_dev[r] == r; rep_row_dev int32[n*9]: for every row r = k*9 + p3 of this call, a row of this call holding
+ * the same patch, itself a representative) are computed; a second launch copies the other rows from theirs: their
+ * Y3 rows with copy bit 0, their mask words with copy bit 1 (copy = 3: the same outputs as _bits; without a bit
+ * the non-representative rows stay unwritten, for consumers that read rows through rep_row_dev). */
+int merlin_tower_window_conv3_reuse(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
+                                    const int64_t *groups_dev, int64_t n, const float *b3_dev,
+                                    int32_t towers, float *Y3_dev, uint64_t *relu_bits_dev, uint32_t *amax_dev,
+                                    const int32_t *rep_row_dev, int32_t copy, void *stream);
 int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *idx_dev,
                        const int32_t *key_dev, int64_t nnz, const int32_t *slot_dev, int32_t sub,
                        int64_t item_len, const int32_t *fix_dev, int64_t n_fix, int32_t towers,
@@ -479,7 +489,11 @@ int merlin_x6_gemm_tn(const float *A_dev, const float *B_dev, int64_t Kd, int32_
  *          N % 192), the k range cut into <= splits slabs (slab float[merlin_x6_tn_slab_floats(...)]) summed in slab
  *          order.
  * gemm_tn_planes: the same product over operands already in plane form (the a_planes output of gemm_nt for the same
- *          tensor and amax), strides in values. */
+ *          tensor and amax), strides in values.
+ * gemm_nt_gather / gemm_tn_gather: gemm_nt (cfg 10..13) / gemm_tn (cfg 0..2) with the fp32 operand A / B read by
+ *          64-value chunks through a row map: row r's chunk j (values 64 j .. 64 j + 63) is row rows_dev[r * K / 64 + j]
+ *          (NT; TN: r * N / 64 + j) of the operand seen as [*][64] (tower stride as before; K or N % 64 == 0, K <= 576):
+ *          conv3's rows through their patch representatives (merlin_tower_window_conv3_reuse with copy < 1). */
 int merlin_h3_amax(const float *x_dev, int64_t n, int32_t towers, int64_t stride, uint32_t *amax_dev, void *stream);
 int merlin_h3_split(const float *x_dev, int64_t n, int32_t towers, const uint32_t *amax_dev, void *planes_dev,
                     void *stream);
@@ -494,6 +508,14 @@ int merlin_h3_gemm_tn_planes(const void *A_planes_dev, const uint32_t *amax_a_de
                              const uint32_t *amax_b_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
                              int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev, float *out_dev,
                              int32_t cfg, void *stream);
+int merlin_h3_gemm_nt_gather(const float *A_dev, const uint32_t *amax_a_dev, const void *B_dev,
+                             const uint32_t *amax_b_dev, int64_t M, int32_t N, int32_t K, int32_t towers,
+                             int64_t a_stride, int64_t b_stride, const float *bias_dev, float *C_dev, int64_t c_stride,
+                             const int32_t *a_rows_dev, int32_t cfg, void *stream);
+int merlin_h3_gemm_tn_gather(const float *A_dev, const uint32_t *amax_a_dev, const float *B_dev,
+                             const uint32_t *amax_b_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
+                             int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev, float *out_dev,
+                             const int32_t *b_rows_dev, int32_t cfg, void *stream);
 
 /* The conv1 / conv2 tables of both towers and their adjoint (the parameter-only part of PPO.update's
  * minibatch step, merlin/fast_step.py WeightStage; replaces CNNActorCritic.conv2_tables and its autograd

@@ -644,7 +644,8 @@ int merlin_tower_window_conv3(const float *Q, int64_t nw, const int32_t *wid, co
                               const float *b3, int32_t towers, float *Y3, void *stream) {
     if ((!Q || !wid || !b3 || !Y3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, nullptr, nullptr, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, nullptr, nullptr, nullptr, 0,
+                                        (hipStream_t)stream));
     return MERLIN_OK;
 }
 
@@ -653,7 +654,19 @@ int merlin_tower_window_conv3_bits(const float *Q, int64_t nw, const int32_t *wi
                                    void *stream) {
     if ((!Q || !wid || !b3 || !Y3 || !relu_bits) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, amax, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, amax, nullptr, 0,
+                                        (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_window_conv3_reuse(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
+                                    const float *b3, int32_t towers, float *Y3, uint64_t *relu_bits, uint32_t *amax,
+                                    const int32_t *rep_row, int32_t copy, void *stream) {
+    if ((!Q || !wid || !b3 || !Y3 || !rep_row) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (copy < 0 || copy > 3) return fail(MERLIN_E_INVALID, "copy must be 0..3");
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, amax, rep_row, copy,
+                                        (hipStream_t)stream));
     return MERLIN_OK;
 }
 
@@ -899,31 +912,49 @@ int merlin_h3_split(const float *x, int64_t n, int32_t towers, const uint32_t *a
     return MERLIN_OK;
 }
 
-int merlin_h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
+static int h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
                       int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride, const float *bias,
-                      float *C, int64_t c_stride, void *a_planes, int32_t cfg, void *stream) {
+                      float *C, int64_t c_stride, void *a_planes, const int32_t *a_rows, int32_t cfg, void *stream) {
     if (M < 0 || N <= 0 || K <= 0) return fail(MERLIN_E_INVALID, "bad shape");
     if (M > 0 && (!A || !B || !C || !amax_a || !amax_b)) return fail(MERLIN_E_INVALID, "null argument");
     if (K % 32) return fail(MERLIN_E_UNSUPPORTED, "K must be a multiple of 32");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (a_stride % 4 || b_stride % 8) return fail(MERLIN_E_INVALID, "tower strides: A multiple of 4, B of 8");
     const hipError_t e = merlin::launch_h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, bias, C,
-                                                   c_stride, a_planes, cfg, (hipStream_t)stream);
-    if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "N not a multiple of the tile width / bad cfg");
+                                                   c_stride, a_planes, cfg, (hipStream_t)stream, a_rows);
+    if (e == hipErrorInvalidValue)
+        return fail(MERLIN_E_UNSUPPORTED, "N not a multiple of the tile width / bad cfg / unsupported gather");
     HIP_TRY(e);
     return MERLIN_OK;
 }
 
+int merlin_h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
+                      int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride, const float *bias,
+                      float *C, int64_t c_stride, void *a_planes, int32_t cfg, void *stream) {
+    return h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, bias, C, c_stride, a_planes, nullptr,
+                      cfg, stream);
+}
+
+int merlin_h3_gemm_nt_gather(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
+                             int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride,
+                             const float *bias, float *C, int64_t c_stride, const int32_t *a_rows, int32_t cfg,
+                             void *stream) {
+    if (M > 0 && !a_rows) return fail(MERLIN_E_INVALID, "null argument");
+    if (K % 64) return fail(MERLIN_E_UNSUPPORTED, "gathered rows: K must be a multiple of 64");
+    return h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, bias, C, c_stride, nullptr, a_rows,
+                      cfg, stream);
+}
+
 static int h3_gemm_tn(const void *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t Kd,
                       int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride, int32_t splits,
-                      float *slab, float *out, bool planes, int32_t cfg, void *stream) {
+                      float *slab, float *out, bool planes, int32_t cfg, void *stream, const int32_t *b_rows = nullptr) {
     if (Kd < 0 || M <= 0 || N <= 0) return fail(MERLIN_E_INVALID, "bad shape");
     if (!out || (Kd > 0 && (!A || !B || !slab || !amax_a || !amax_b))) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (splits < 1 || splits > merlin::x6_tn_max_splits()) return fail(MERLIN_E_INVALID, "splits out of range");
     if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return fail(MERLIN_E_INVALID, "M, N: multiples of 8");
     const hipError_t e = merlin::launch_h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits,
-                                                   slab, out, planes, cfg, (hipStream_t)stream);
+                                                   slab, out, planes, cfg, (hipStream_t)stream, b_rows);
     if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "M / N not multiples of the tile / bad cfg");
     HIP_TRY(e);
     return MERLIN_OK;
@@ -934,6 +965,15 @@ int merlin_h3_gemm_tn(const float *A, const uint32_t *amax_a, const float *B, co
                       float *slab, float *out, int32_t cfg, void *stream) {
     return h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, false, cfg,
                       stream);
+}
+
+int merlin_h3_gemm_tn_gather(const float *A, const uint32_t *amax_a, const float *B, const uint32_t *amax_b, int64_t Kd,
+                             int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride, int32_t splits,
+                             float *slab, float *out, const int32_t *b_rows, int32_t cfg, void *stream) {
+    if (Kd > 0 && !b_rows) return fail(MERLIN_E_INVALID, "null argument");
+    if (N % 64) return fail(MERLIN_E_UNSUPPORTED, "gathered rows: N must be a multiple of 64");
+    return h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, false, cfg, stream,
+                      b_rows);
 }
 
 int merlin_h3_gemm_tn_planes(const void *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t Kd,

@@ -298,13 +298,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
 // the first (PMC: MFMA busy 38 %, 3.3 VALU per MFMA).  Here the main loop has no conditional parts (the last two
 // steps are peeled), the body reads all its fragments first, and sched_group_barrier hints lay the next step's
 // split (VALU), its LDS stores and the global loads of the step after it between the MFMAs (guide T19).
-template <int BM, int BN, int WGM, int WGN, int EPI>
-__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restrict__ A, const u32x4 *__restrict__ B,
-                                                           const uint32_t *__restrict__ amaxA,
-                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N,
-                                                           int K, int64_t sA, int64_t sB,
-                                                           const float *__restrict__ bias, float *__restrict__ C,
-                                                           int64_t sC, int tiles_n, u32x4 *__restrict__ Pout) {
+// GA: A's rows gathered by 64-value chunks -- row m's chunk j (values 64 j .. 64 j + 63) is row amap[m * K / 64 + j]
+// of A seen as [*][64] (K <= 64 * GA_CHUNKS; the launcher checks): the minibatch's conv3 rows through their patch
+// representatives (merlin_tower_window_conv3_reuse), so the non-representative rows are never written.  The
+// thread's chunk rows are read once into registers; a k step picks its chunk's with a uniform select.
+constexpr int GA_CHUNKS = 9;
+template <int BM, int BN, int WGM, int WGN, int EPI, bool GA>
+__device__ __forceinline__ void h3_ntp_body(const float *__restrict__ A, const u32x4 *__restrict__ B,
+                                            const uint32_t *__restrict__ amaxA, const uint32_t *__restrict__ amaxB,
+                                            int64_t M, int N, int K, int64_t sA, int64_t sB,
+                                            const float *__restrict__ bias, float *__restrict__ C, int64_t sC,
+                                            int tiles_n, u32x4 *__restrict__ Pout, const int32_t *__restrict__ amap) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -332,13 +336,22 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
     const float4 *ga[UA];
     int la[UA];
     u32x4 *pa[UA];
+    int32_t gx[GA ? UA : 1][GA ? GA_CHUNKS : 1];  // GA: the row's chunk rows
 #pragma unroll
     for (int i = 0; i < UA; i++) {
         const int q = tid + i * NT;
         const int row = q >> 2, g = q & 3;
-        ga[i] = reinterpret_cast<const float4 *>(A + t * sA + std::min<int64_t>(m0 + row, M - 1) * K) + g * 2;
+        const int64_t ar = std::min<int64_t>(m0 + row, M - 1);
+        if constexpr (GA) {
+            ga[i] = reinterpret_cast<const float4 *>(A + t * sA) + g * 2;
+            const int kc = K / 64;
+#pragma unroll
+            for (int j = 0; j < GA_CHUNKS; j++) gx[i][j] = j < kc ? amap[ar * kc + j] : 0;
+        } else {
+            ga[i] = reinterpret_cast<const float4 *>(A + t * sA + ar * K) + g * 2;
+        }
         la[i] = row * 4 + (g ^ ((row >> 2) & 3));
-        pa[i] = Pout && tn == 0 && m0 + row < M ? Pout + (t * sA + (m0 + row) * K) / 4 + g * 2 : nullptr;
+        pa[i] = !GA && Pout && tn == 0 && m0 + row < M ? Pout + (t * sA + (m0 + row) * K) / 4 + g * 2 : nullptr;
     }
     int gb[CB], lb[CB];
 #pragma unroll
@@ -353,8 +366,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
     auto load = [&](int kt) {
 #pragma unroll
         for (int i = 0; i < UA; i++) {
-            ra[i][0] = ga[i][(int64_t)kt * 8];
-            ra[i][1] = ga[i][(int64_t)kt * 8 + 1];
+            if constexpr (GA) {
+                const int kj = kt >> 1;
+                int32_t r = gx[i][0];
+#pragma unroll
+                for (int j = 1; j < GA_CHUNKS; j++) r = kj == j ? gx[i][j] : r;
+                const float4 *src = ga[i] + (int64_t)r * 16 + (kt & 1) * 8;
+                ra[i][0] = src[0];
+                ra[i][1] = src[1];
+            } else {
+                ra[i][0] = ga[i][(int64_t)kt * 8];
+                ra[i][1] = ga[i][(int64_t)kt * 8 + 1];
+            }
         }
 #pragma unroll
         for (int i = 0; i < CB; i++) rb[i] = B[gb[i] + kt * 8];
@@ -463,6 +486,25 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
             }
         }
     }
+}
+
+template <int BM, int BN, int WGM, int WGN, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restrict__ A, const u32x4 *__restrict__ B,
+                                                           const uint32_t *__restrict__ amaxA,
+                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N,
+                                                           int K, int64_t sA, int64_t sB,
+                                                           const float *__restrict__ bias, float *__restrict__ C,
+                                                           int64_t sC, int tiles_n, u32x4 *__restrict__ Pout) {
+    h3_ntp_body<BM, BN, WGM, WGN, EPI, false>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, Pout, nullptr);
+}
+template <int BM, int BN, int WGM, int WGN, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntpg(const float *__restrict__ A, const u32x4 *__restrict__ B,
+                                                            const uint32_t *__restrict__ amaxA,
+                                                            const uint32_t *__restrict__ amaxB, int64_t M, int N,
+                                                            int K, int64_t sA, int64_t sB,
+                                                            const float *__restrict__ bias, float *__restrict__ C,
+                                                            int64_t sC, int tiles_n, const int32_t *__restrict__ amap) {
+    h3_ntp_body<BM, BN, WGM, WGN, EPI, true>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, nullptr, amap);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -711,12 +753,15 @@ __device__ __forceinline__ u32x4 tr_frag(const u32x4 *img, int col0, int kh, int
     return __builtin_bit_cast(u32x4, bf16x8{v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]});
 }
 
-template <int BM, int BN, int WGM, int WGN>
-__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restrict__ A, const float4 *__restrict__ B,
-                                                          const uint32_t *__restrict__ amaxA,
-                                                          const uint32_t *__restrict__ amaxB, int64_t Kd, int M, int N,
-                                                          int64_t sA, int64_t sB, int64_t kc, int tiles_n, int tiles,
-                                                          int S, float *__restrict__ slab) {
+// GB: B's rows gathered by 64-column chunks -- row k's chunk j is row bmap[k * N / 64 + j] of B seen as [*][64] (the
+// minibatch's conv3 rows through their patch representatives, as k_h3_ntp's GA).  A unit's chunk is fixed, its row
+// changes every k step: each load issues the next step's chunk-row reads behind its data reads (ready by then).
+template <int BM, int BN, int WGM, int WGN, bool GB>
+__device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const float4 *__restrict__ B,
+                                           const uint32_t *__restrict__ amaxA, const uint32_t *__restrict__ amaxB,
+                                           int64_t Kd, int M, int N, int64_t sA, int64_t sB, int64_t kc, int tiles_n,
+                                           int tiles, int S, float *__restrict__ slab,
+                                           const int32_t *__restrict__ bmap) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -738,12 +783,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
     const float scA = pow2f(eA), scB = pow2f(eB), scA2 = pow2f(eA + 11), scB2 = pow2f(eB + 11);
     const int64_t rowA = M / 4, rowB = N / 4;
     A += t * sA + m0 / 4;
-    B += t * sB + n0 / 4;
+    B += t * sB + (GB ? 0 : n0 / 4);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w / WGN, wn = w - (w / WGN) * WGN;
 
     int ka[UA], la[UA], kb[UB], lb[UB];
     const float4 *pa[UA], *pb[UB];
+    const int32_t *mb[UB];  // GB: the unit's chunk column of bmap (stride N / 64 per k row)
+    int32_t xb[UB];         // GB: the chunk rows of the next load
+    const int nc = N / 64;
 #pragma unroll
     for (int i = 0; i < UA; i++) {
         const int q = std::min(tid + i * NT, QA - 1);
@@ -758,11 +806,39 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
         const int k = q / RCB, g = q - (q / RCB) * RCB;
         kb[i] = k;
         lb[i] = 2 * PSA + k * RCB + (g ^ tr_swz<RCB>(k));
-        pb[i] = B + (k0 + k) * rowB + g * 2;
+        if constexpr (GB) {
+            const int col = n0 + 8 * g;
+            pb[i] = B + (col & 63) / 4;
+            mb[i] = bmap + (col >> 6);
+        } else {
+            pb[i] = B + (k0 + k) * rowB + g * 2;
+        }
     }
+    auto fetch_rows = [&](int64_t kk) {  // GB: chunk rows of step kk (rows past k1 clamped, zeroed when staged)
+        if constexpr (GB) {
+#pragma unroll
+            for (int i = 0; i < UB; i++) xb[i] = mb[i][std::min(kk + kb[i], k1 - 1) * nc];
+        }
+    };
     const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float4 ra[UA][2], rb[UB][2];
     auto load = [&](int64_t kk) {
+        if constexpr (GB) {
+#pragma unroll
+            for (int i = 0; i < UA; i++) {
+                const float4 *src = pa[i] + (std::min(kk + ka[i], k1 - 1) - k0 - ka[i]) * rowA;
+                ra[i][0] = src[0];
+                ra[i][1] = src[1];
+            }
+#pragma unroll
+            for (int i = 0; i < UB; i++) {
+                const float4 *src = pb[i] + (int64_t)xb[i] * 16;
+                rb[i][0] = src[0];
+                rb[i][1] = src[1];
+            }
+            fetch_rows(kk + BK);
+            return;
+        }
         if (kk + BK <= k1) {  // full step: row pointers + a wave-uniform offset
             const int64_t da = (kk - k0) * rowA, db = (kk - k0) * rowB;
 #pragma unroll
@@ -822,6 +898,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
         }
 
     if (k0 < k1) {
+        fetch_rows(k0);
         load(k0);
         store(0, k0);
         if (k0 + BK < k1) load(k0 + BK);
@@ -875,6 +952,24 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
                 St[(int64_t)row * N + n0 + wn * WTN + j * 32 + fr] =
                     (hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB;
             }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restrict__ A, const float4 *__restrict__ B,
+                                                          const uint32_t *__restrict__ amaxA,
+                                                          const uint32_t *__restrict__ amaxB, int64_t Kd, int M, int N,
+                                                          int64_t sA, int64_t sB, int64_t kc, int tiles_n, int tiles,
+                                                          int S, float *__restrict__ slab) {
+    h3_tn_body<BM, BN, WGM, WGN, false>(A, B, amaxA, amaxB, Kd, M, N, sA, sB, kc, tiles_n, tiles, S, slab, nullptr);
+}
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tng(const float4 *__restrict__ A, const float4 *__restrict__ B,
+                                                           const uint32_t *__restrict__ amaxA,
+                                                           const uint32_t *__restrict__ amaxB, int64_t Kd, int M,
+                                                           int N, int64_t sA, int64_t sB, int64_t kc, int tiles_n,
+                                                           int tiles, int S, float *__restrict__ slab,
+                                                           const int32_t *__restrict__ bmap) {
+    h3_tn_body<BM, BN, WGM, WGN, true>(A, B, amaxA, amaxB, Kd, M, N, sA, sB, kc, tiles_n, tiles, S, slab, bmap);
 }
 
 // The TN product with the k step's split and staging interleaved into its MFMAs, as k_h3_ntp does for NT: the
@@ -1214,13 +1309,23 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tnq(const u32x4 *__restri
 template <int BM, int BN, int WGM, int WGN, bool PIPE>
 hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
-                     hipStream_t s) {
+                     const int32_t *amap, hipStream_t s) {
     if (N % BN || (PIPE && K < 2 * BK)) return hipErrorInvalidValue;
     if ((int64_t)N * (K / 8) * 2 > INT32_MAX) return hipErrorInvalidValue;  // 32-bit B chunk offsets
     const int64_t tiles_m = (M + BM - 1) / BM;
     const int tiles_n = N / BN;
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
+    if (amap) {  // gathered A rows: the pipelined kernel only, no plane output
+        if (!PIPE || Pout || K % 64 || K > 64 * GA_CHUNKS) return hipErrorInvalidValue;
+        if (bias)
+            hipLaunchKernelGGL((k_h3_ntpg<BM, BN, WGM, WGN, 1>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
+                               sB, bias, C, sC, tiles_n, amap);
+        else
+            hipLaunchKernelGGL((k_h3_ntpg<BM, BN, WGM, WGN, 0>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
+                               sB, nullptr, C, sC, tiles_n, amap);
+        return hipGetLastError();
+    }
     if (PIPE) {
         if (bias)
             hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 1>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
@@ -1261,8 +1366,10 @@ hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, con
 // Q: the operands are plane images (k_h3_tnq), strides in values as for fp32 operands (4 B per value either way)
 template <int BM, int BN, int WGM, int WGN, int Q>
 hipError_t tn_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t Kd, int M,
-                     int N, int T, int64_t sA, int64_t sB, int splits, float *slab, int *S_out, hipStream_t s) {
+                     int N, int T, int64_t sA, int64_t sB, int splits, float *slab, int *S_out, const int32_t *bmap,
+                     hipStream_t s) {
     if (M % BM || N % BN) return hipErrorInvalidValue;
+    if (bmap && (Q != 0 || N % 64)) return hipErrorInvalidValue;  // gathered B rows: k_h3_tn only
     const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
     int S = std::max(1, splits);
     int64_t kc = (Kd + S - 1) / S;
@@ -1277,6 +1384,10 @@ hipError_t tn_launch(const void *A, const void *B, const uint32_t *amaxA, const 
         hipLaunchKernelGGL((k_h3_tnp<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
                            static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
                            sA / 4, sB / 4, kc, tiles_n, tiles, S, slab);
+    else if (bmap)
+        hipLaunchKernelGGL((k_h3_tng<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
+                           static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
+                           sA / 4, sB / 4, kc, tiles_n, tiles, S, slab, bmap);
     else
         hipLaunchKernelGGL((k_h3_tn<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
                            static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
@@ -1317,14 +1428,14 @@ hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *ama
 
 hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
-                             int64_t c_stride, void *a_planes, int cfg, hipStream_t s) {
+                             int64_t c_stride, void *a_planes, int cfg, hipStream_t s, const int32_t *a_rows) {
     if (M <= 0) return hipSuccess;
     if (K % BK || N <= 0 || a_stride % 4 || b_stride % 8) return hipErrorInvalidValue;
     const u32x4 *b = static_cast<const u32x4 *>(B);
     u32x4 *P = static_cast<u32x4 *>(a_planes);
     const int64_t sB = b_stride / 8 * 2;  // chunks
 #define H3_NT(BM, BN, WM, WN, PIPE) \
-    nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s)
+    nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, s)
     switch (cfg) {
         case 0: return H3_NT(256, 128, 4, 2, false);
         case 1: return H3_NT(128, 192, 4, 2, false);
@@ -1339,7 +1450,8 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
 #undef H3_NT
         // k_h3_ntg: both operands staged by LDS-DMA, three k steps deep
 #define H3_NTG(BM, BN, WM, WN, KP) \
-    ntg_launch<BM, BN, WM, WN, KP>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s)
+    (a_rows ? hipErrorInvalidValue                                                                 \
+            : ntg_launch<BM, BN, WM, WN, KP>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s))
         case 20: return H3_NTG(256, 128, 4, 2, false);
         case 21: return H3_NTG(128, 192, 4, 2, false);
         // the same with each half step's fragment reads under the previous half step's MFMAs
@@ -1352,7 +1464,7 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
 
 hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t Kd,
                              int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits, float *slab,
-                             float *out, bool planes, int cfg, hipStream_t s) {
+                             float *out, bool planes, int cfg, hipStream_t s, const int32_t *b_rows) {
     if (M <= 0 || N <= 0) return hipSuccess;
     if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
     const int64_t total = (int64_t)T * M * N;
@@ -1364,8 +1476,10 @@ hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B
     int S = 1;
     hipError_t e;
 #define H3_TN(BM, BN, WM, WN, PIPE)                                                                              \
-    (planes ? tn_launch<BM, BN, WM, WN, 1>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s)  \
-            : tn_launch<BM, BN, WM, WN, PIPE>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, s))
+    (planes ? tn_launch<BM, BN, WM, WN, 1>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S,   \
+                                           b_rows, s)                                                              \
+            : tn_launch<BM, BN, WM, WN, PIPE>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, \
+                                              b_rows, s))
     switch (cfg) {
         case 0: e = H3_TN(128, 192, 4, 2, 0); break;
         case 1: e = H3_TN(128, 192, 2, 2, 0); break;

@@ -106,7 +106,8 @@ hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *d
 
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                               const float *b3, int T, float *Y3, uint64_t *bits, uint32_t *amax, hipStream_t s);
+                               const float *b3, int T, float *Y3, uint64_t *bits, uint32_t *amax,
+                               const int32_t *rrow, int copy, hipStream_t s);
 hipError_t launch_act_heads(const float *z, const float *b4, int64_t n, int H, const float *wa, const float *ba,
                             const float *wc, const float *bc, int A, int det, uint64_t seed, const int64_t *epoch,
                             int64_t step, int64_t env_offset, int64_t *action, float *logp, float *value,
@@ -192,11 +193,15 @@ hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *ama
 // tile's blocks
 hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
-                             int64_t c_stride, void *a_planes, int cfg, hipStream_t s);
+                             int64_t c_stride, void *a_planes, int cfg, hipStream_t s,
+                             const int32_t *a_rows = nullptr);
 // planes: A and B are plane images (an NT's a_planes) instead of fp32 tensors
+// a_rows / b_rows (nullable): the operand's rows gathered by 64-value chunks -- row r's chunk j is row
+// rows[r * (K or N) / 64 + j] of the operand seen as [*][64] (k_h3_ntp GA, k_h3_tn GB; pipelined NT cfgs and TN
+// cfgs 0-2 only)
 hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t Kd,
                              int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits, float *slab,
-                             float *out, bool planes, int cfg, hipStream_t s);
+                             float *out, bool planes, int cfg, hipStream_t s, const int32_t *b_rows = nullptr);
 
 // clip_grad_norm_ + Adam step over a parameter list (merlin_optim.hip)
 constexpr int OPT_MAX_TENSORS = 32;

@@ -66,8 +66,49 @@ __global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ 
 // Y3[t][u*9 + p3][c4] = relu(b3[t][c4] + sum_tap Q[t][wid[g*25 + p2(p3, tap)]][tap][c4]); 16
 // consecutive lanes read one 256-B row of Q per tap.  bits (optional): bit ch of bits[t][u*9 + p3]
 // = (Y3 channel ch > 0), the row's ReLU mask for the backward (16 lanes OR their nibbles together
-// with xor shuffles inside the row's 16-lane group; rows are 16-lane aligned, so the groups are
-// whole and converged).
+// with xor shuffles inside the row's 16-lane group; the caller keeps the groups whole and converged).
+// mx: max |Y3| per tower as float bits (merlin_h3.hip's operand scale), reduced by block_amax2.
+__device__ __forceinline__ void conv3_row(const float4 *__restrict__ Q, int64_t nw, const int32_t *__restrict__ wid,
+                                          const int64_t *__restrict__ groups, int64_t n,
+                                          const float4 *__restrict__ b3, float4 *__restrict__ Y3,
+                                          uint64_t *__restrict__ bits, bool amax, int64_t r, int c,
+                                          uint32_t (&mx)[2]) {
+    const int64_t tu = r / 9;
+    const int p3 = (int)(r - tu * 9), t = (int)(tu / n);
+    const int64_t u = tu - (int64_t)t * n;
+    const int32_t *wr = wid + (groups ? groups[u] : u) * 25;
+    const int oy = p3 / 3, ox = p3 - 3 * (p3 / 3);
+    const float4 *qt = Q + (size_t)t * nw * 9 * 16 + c;
+    float4 v[9];
+#pragma unroll
+    for (int tap = 0; tap < 9; tap++) {
+        const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+        v[tap] = qt[((size_t)wr[(oy + ky) * 5 + ox + kx] * 9 + tap) * 16];
+    }
+    float4 acc = v[0];
+#pragma unroll
+    for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
+    const float4 b = b3[t * 16 + c];
+    const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
+                                 relu_nan(acc.w + b.w));
+    Y3[r * 16 + c] = y;
+    if (amax) {
+        const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
+                                    std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
+        if (t == 0) mx[0] = std::max(mx[0], m);
+        else mx[1] = std::max(mx[1], m);
+    }
+    if (bits) {
+        uint64_t w = (uint64_t)((y.x > 0.0f ? 1u : 0u) | (y.y > 0.0f ? 2u : 0u) | (y.z > 0.0f ? 4u : 0u) |
+                                (y.w > 0.0f ? 8u : 0u))
+                     << (4 * c);
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) w |= __shfl_xor(w, off);
+        if (c == 0) bits[r] = w;
+    }
+}
+
+// Every row: 16 lanes per row (rows are 16-lane aligned, so the groups are whole and converged).
 __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__ Q, int64_t nw,
                                                       const int32_t *__restrict__ wid,
                                                       const int64_t *__restrict__ groups, int64_t n,
@@ -75,44 +116,63 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
                                                       float4 *__restrict__ Y3, uint64_t *__restrict__ bits,
                                                       uint32_t *__restrict__ amax) {
     const int64_t total = (int64_t)T * n * 9 * 16;
-    uint32_t mx[2] = {0u, 0u};  // max |Y3| per tower as float bits (merlin_h3.hip's operand scale)
-    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-        const int c = (int)(e & 15);
-        const int64_t r = e >> 4, tu = r / 9;
-        const int p3 = (int)(r - tu * 9), t = (int)(tu / n);
-        const int64_t u = tu - (int64_t)t * n;
-        const int32_t *wr = wid + (groups ? groups[u] : u) * 25;
-        const int oy = p3 / 3, ox = p3 - 3 * (p3 / 3);
-        const float4 *qt = Q + (size_t)t * nw * 9 * 16 + c;
-        float4 v[9];
-#pragma unroll
-        for (int tap = 0; tap < 9; tap++) {
-            const int ky = tap / 3, kx = tap - 3 * (tap / 3);
-            v[tap] = qt[((size_t)wr[(oy + ky) * 5 + ox + kx] * 9 + tap) * 16];
+    uint32_t mx[2] = {0u, 0u};
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256)
+        conv3_row(Q, nw, wid, groups, n, b3, Y3, bits, amax != nullptr, e >> 4, (int)(e & 15), mx);
+    if (amax) block_amax2(mx, T, amax);
+}
+
+// Patch reuse: rows (u, p3) whose frames hold the same 5x5-tile patch at p3 read the same 9 windows at the same
+// taps, so their outputs are bit-identical; rrow[u*9 + p3] names one row of the minibatch holding that patch (its
+// representative, rrow[rep] = rep; merlin/windows.py builds it per minibatch).  Only the representatives are
+// computed (~a third of the rows at the bench state): each wave takes 64 consecutive rows of the tower-major row
+// space, packs its representatives into an LDS queue (ballot + prefix count) and computes them 4 at a time, 16
+// lanes per row, so no lane idles on a copied row.  The block walks its 256-row spans in step (block-uniform trip
+// count: the queue barriers are block barriers).
+__global__ __launch_bounds__(256) void k_window_conv3_reps(const float4 *__restrict__ Q, int64_t nw,
+                                                           const int32_t *__restrict__ wid,
+                                                           const int64_t *__restrict__ groups, int64_t n,
+                                                           const float4 *__restrict__ b3, int T,
+                                                           float4 *__restrict__ Y3, uint64_t *__restrict__ bits,
+                                                           uint32_t *__restrict__ amax,
+                                                           const int32_t *__restrict__ rrow) {
+    __shared__ int64_t queue[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const int64_t rows = n * 9, total = (int64_t)T * rows;
+    uint32_t mx[2] = {0u, 0u};
+    for (int64_t base = (int64_t)blockIdx.x * 256; base < total; base += (int64_t)gridDim.x * 256) {
+        const int64_t i = base + threadIdx.x;
+        bool rep = false;
+        if (i < total) {
+            const int64_t r = i - (i >= rows ? rows : 0);  // T <= 2 (the launcher checks)
+            rep = rrow[r] == (int32_t)r;
         }
-        float4 acc = v[0];
-#pragma unroll
-        for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
-        const float4 b = b3[t * 16 + c];
-        const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
-                                     relu_nan(acc.w + b.w));
-        Y3[e] = y;
-        if (amax) {
-            const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
-                                        std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
-            if (t == 0) mx[0] = std::max(mx[0], m);
-            else mx[1] = std::max(mx[1], m);
-        }
-        if (bits) {
-            uint64_t v = (uint64_t)((y.x > 0.0f ? 1u : 0u) | (y.y > 0.0f ? 2u : 0u) | (y.z > 0.0f ? 4u : 0u) |
-                                    (y.w > 0.0f ? 8u : 0u))
-                         << (4 * c);
-#pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) v |= __shfl_xor(v, off);
-            if (c == 0) bits[r] = v;
-        }
+        const unsigned long long m = __ballot(rep);
+        if (rep) queue[wv][__popcll(m & below)] = i;
+        __syncthreads();
+        const int cnt = __popcll(m);
+        for (int p = q; p < cnt; p += 4) conv3_row(Q, nw, wid, groups, n, b3, Y3, bits, amax != nullptr,
+                                                   queue[wv][p], c, mx);
+        __syncthreads();
     }
     if (amax) block_amax2(mx, T, amax);
+}
+
+// The other rows from their representatives (after k_window_conv3_reps): with Y (16 lanes per row) the Y3 row and
+// the mask word, without (one lane per row) the mask word only.
+template <bool Y>
+__global__ __launch_bounds__(256) void k_window_conv3_copy(float4 *Y3, uint64_t *bits, int64_t n, int T,
+                                                           const int32_t *__restrict__ rrow) {
+    const int64_t rows = n * 9, total = (int64_t)T * rows * (Y ? 16 : 1);
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int64_t i = Y ? e >> 4 : e;
+        const int64_t t0 = i >= rows ? rows : 0, r = i - t0;
+        const int32_t src = rrow[r];
+        if (src == (int32_t)r) continue;
+        if (Y) Y3[e] = Y3[(t0 + src) * 16 + (e & 15)];
+        if (bits && (!Y || (e & 15) == 0)) bits[i] = bits[t0 + src];
+    }
 }
 
 // The acting path's conv3 from a table over EVERY possible 3x3 tile window (5^9 = 1,953,125 rows, built
@@ -448,13 +508,28 @@ hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, 
 }
 
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
-                               const float *b3, int T, float *Y3, uint64_t *bits, uint32_t *amax, hipStream_t s) {
+                               const float *b3, int T, float *Y3, uint64_t *bits, uint32_t *amax, const int32_t *rrow,
+                               int copy, hipStream_t s) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
-    hipLaunchKernelGGL(k_window_conv3, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4 *>(Q), nw, wid,
-                       groups, n, reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), bits,
-                       amax);
+    const float4 *q = reinterpret_cast<const float4 *>(Q), *b = reinterpret_cast<const float4 *>(b3);
+    float4 *y = reinterpret_cast<float4 *>(Y3);
+    if (!rrow) {
+        hipLaunchKernelGGL(k_window_conv3, dim3(grid), dim3(256), 0, s, q, nw, wid, groups, n, b, T, y, bits, amax);
+        return hipGetLastError();
+    }
+    if (T > 2) return hipErrorInvalidValue;
+    const int rgrid = (int)std::min<int64_t>((total / 16 + 255) / 256, 256 * 32);
+    hipLaunchKernelGGL(k_window_conv3_reps, dim3(rgrid), dim3(256), 0, s, q, nw, wid, groups, n, b, T, y, bits, amax,
+                       rrow);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !(copy & 3)) return e;
+    if (copy & 1)
+        hipLaunchKernelGGL(k_window_conv3_copy<true>, dim3(grid), dim3(256), 0, s, y, (copy & 2) ? bits : nullptr, n,
+                           T, rrow);
+    else if (bits)
+        hipLaunchKernelGGL(k_window_conv3_copy<false>, dim3(rgrid), dim3(256), 0, s, y, bits, n, T, rrow);
     return hipGetLastError();
 }
 

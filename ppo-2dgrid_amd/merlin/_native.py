@@ -98,6 +98,7 @@ def lib():
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp]
+    L.merlin_tower_window_conv3_reuse.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp, i32, vp]
     L.merlin_tower_all_windows.restype = i64
     L.merlin_tower_codes_conv3.argtypes = [vp, i64, vp, vp, i32, vp, vp]
     L.merlin_tower_codes_conv3_amax.argtypes = [vp, i64, vp, vp, i32, vp, vp, vp]
@@ -134,6 +135,8 @@ def lib():
     L.merlin_h3_gemm_nt.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, vp, i32, vp]
     L.merlin_h3_gemm_tn.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
     L.merlin_h3_gemm_tn_planes.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
+    L.merlin_h3_gemm_nt_gather.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, vp, i32, vp]
+    L.merlin_h3_gemm_tn_gather.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, vp, i32, vp]
     L.merlin_stage_tables_fwd.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_stage_tables_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     check_env_config_layout(L)
@@ -171,7 +174,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
     "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_conv3",
-    "merlin_tower_window_conv3_bits", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
+    "merlin_tower_window_conv3_bits", "merlin_tower_window_conv3_reuse", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
     "merlin_tower_codes_conv3_amax",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_segment_sum_fused", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_tower_colsum",
@@ -179,7 +182,7 @@ EXPORTED_SYMBOLS = (
     "merlin_x6_split", "merlin_x6_join", "merlin_x6_gemm_nt", "merlin_x6_tn_slab_floats", "merlin_x6_gemm_tn",
     "merlin_clip_adam_workspace", "merlin_clip_adam",
     "merlin_h3_amax", "merlin_h3_split", "merlin_h3_gemm_nt", "merlin_h3_gemm_tn",
-    "merlin_h3_gemm_tn_planes",
+    "merlin_h3_gemm_tn_planes", "merlin_h3_gemm_nt_gather", "merlin_h3_gemm_tn_gather",
 )
 
 
@@ -548,12 +551,16 @@ def window_lut(rows, tables):
     return out
 
 
-def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None, amax=None):
+def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None, amax=None, rep_row=None,
+                 copy: int = 3):
     """Y3 f32[T, n*9, 64] = relu(conv3) rows (k, p3) of frames groups[k] from
     Q f32[T, nw, 576], the per-window, per-tap conv3 partial sums (merlin/windows.py).
     bits: also return the rows' ReLU masks, int64[T, n*9] (bit co = Y3 > 0).  rows >= n: the
     outputs hold `rows` frames, those past n zero (Y3) / unwritten (bits).  amax (with bits): int32[T],
-    zeroed by the caller, receives max |Y3| per tower as float bits (h3_amax's format)."""
+    zeroed by the caller, receives max |Y3| per tower as float bits (h3_amax's format).
+    rep_row (int32 [n*9], MinibatchWindows.rep_row: per row, a row holding the same 5x5-tile patch): each distinct
+    patch of the rows computed once and copied to the rows sharing it (merlin_tower_window_conv3_reuse; same
+    outputs); copy (bit 0 Y3 rows, bit 1 mask words) < 3 leaves the other rows' Y3 / masks unwritten."""
     T, nw = int(Q.shape[0]), int(Q.shape[1])
     n = int(groups.numel())
     R = n if rows is None else int(rows)
@@ -564,6 +571,16 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
         out[:, n * 9:].zero_()
     # algorithmic bytes: Y3 written, the frames' ids and window ids, Q read once (its 81 row
     # gathers per frame and tower are L2 / Infinity-Cache hits)
+    if rep_row is not None:
+        assert bits and R == n and T <= 2
+        assert rep_row.dtype == torch.int32 and rep_row.is_contiguous() and rep_row.numel() == n * 9
+        mask = torch.empty((T, R * 9), dtype=torch.int64, device=Q.device)
+        with KernelTimer.span("k_window_conv3", T * n * 9 * 264 + n * 144 + T * nw * 576 * 4):
+            check(lib().merlin_tower_window_conv3_reuse(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
+                                                        ptr(mask), ptr(amax), ptr(rep_row), int(copy),
+                                                        stream_of(Q)),
+                  "merlin_tower_window_conv3_reuse")
+        return out, mask
     if bits:
         mask = torch.empty((T, R * 9), dtype=torch.int64, device=Q.device)
         with KernelTimer.span("k_window_conv3", T * n * 9 * 264 + n * 108 + T * nw * 576 * 4):
@@ -938,10 +955,13 @@ def h3_split(x: torch.Tensor, amax: torch.Tensor, out: torch.Tensor | None = Non
 
 def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,
                bias: torch.Tensor | None = None, cfg: int = 0, out: torch.Tensor | None = None,
-               name: str = "h3_gemm_nt", planes_out: torch.Tensor | None = None) -> torch.Tensor:
+               name: str = "h3_gemm_nt", planes_out: torch.Tensor | None = None,
+               rows: torch.Tensor | None = None) -> torch.Tensor:
     """C f32[T, M, N] = A @ B^T per tower (+ bias[t] and ReLU when bias is given), A f32[T, M, K] with its h3_amax,
     B planes int16[T, N, 2K] (h3_split of an f32 [T, N, K] with amaxB).  planes_out int16[T, M, 2K], if given,
-    receives A's planes (h3_split(A, amaxA), made by the kernel while it stages A) for a later h3_gemm_tn."""
+    receives A's planes (h3_split(A, amaxA), made by the kernel while it stages A) for a later h3_gemm_tn.
+    rows int32[M * K / 64] (merlin_h3_gemm_nt_gather, pipelined cfgs): A read by 64-value chunks, row m's chunk j
+    from row rows[m * K / 64 + j] of A viewed as [T, M * K / 64, 64] (conv3's patch representatives)."""
     T, M, K = (int(v) for v in A.shape)
     N = int(B.shape[1])
     assert A.dtype == torch.float32 and B.dtype == torch.int16 and B.shape == (T, N, 2 * K)
@@ -953,6 +973,14 @@ def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
         assert bias.shape == (T, N) and bias.is_contiguous()
     if planes_out is not None:
         assert planes_out.dtype == torch.int16 and planes_out.shape == (T, M, 2 * K) and planes_out.is_contiguous()
+    if rows is not None:
+        assert planes_out is None and rows.dtype == torch.int32 and rows.is_contiguous() and K % 64 == 0
+        assert rows.numel() == M * K // 64
+        with KernelTimer.span(name, 0, 2 * T * M * N * K):
+            check(lib().merlin_h3_gemm_nt_gather(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, T, M * K, N * K,
+                                                 ptr(bias) if bias is not None else None, ptr(out), M * N, ptr(rows),
+                                                 int(cfg), stream_of(A)), "merlin_h3_gemm_nt_gather")
+        return out
     with KernelTimer.span(name, 0, 2 * T * M * N * K):
         check(lib().merlin_h3_gemm_nt(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, T, M * K, N * K,
                                       ptr(bias) if bias is not None else None, ptr(out), M * N,
@@ -963,10 +991,12 @@ def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
 
 def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,
                splits: int | None = None, cfg: int | None = None, name: str = "h3_gemm_tn",
-               out: torch.Tensor | None = None) -> torch.Tensor:
+               out: torch.Tensor | None = None, rows: torch.Tensor | None = None) -> torch.Tensor:
     """out f32[T, M, N] = A^T @ B per tower, A f32[T, Kd, M], B f32[T, Kd, N] with their h3_amax (the long k range
     split into `splits` slabs summed in order).  A and B may instead both be planes, int16[T, Kd, 2M] / [T, Kd, 2N]
-    (h3_gemm_nt's planes_out of the same tensors and scales): the same product without splitting them again."""
+    (h3_gemm_nt's planes_out of the same tensors and scales): the same product without splitting them again.
+    rows int32[Kd * N / 64] (merlin_h3_gemm_tn_gather, cfgs 0-2): B read by 64-value chunks, row k's chunk j from row
+    rows[k * N / 64 + j] of B viewed as [T, Kd * N / 64, 64]."""
     splits = H3_TN_SPLITS if splits is None else splits
     cfg = H3_TN_CFG if cfg is None else cfg
     planes = A.dtype == torch.int16
@@ -984,6 +1014,14 @@ def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
     assert out.shape == (T, M, N) and out.dtype == torch.float32 and out.is_contiguous()
     slab = torch.empty(int(lib().merlin_x6_tn_slab_floats(M, N, T, int(splits))), dtype=torch.float32,
                        device=A.device)
+    if rows is not None:
+        assert not planes and rows.dtype == torch.int32 and rows.is_contiguous() and N % 64 == 0
+        assert rows.numel() == Kd * N // 64
+        with KernelTimer.span(name, 0, 2 * T * M * N * Kd):
+            check(lib().merlin_h3_gemm_tn_gather(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), Kd, M, N, T, Kd * M, Kd * N,
+                                                 int(splits), ptr(slab), ptr(out), ptr(rows), int(cfg), stream_of(A)),
+                  "merlin_h3_gemm_tn_gather")
+        return out
     fn = lib().merlin_h3_gemm_tn_planes if planes else lib().merlin_h3_gemm_tn
     with KernelTimer.span(name, 0, 2 * T * M * N * Kd):
         check(fn(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), Kd, M, N, T, Kd * M, Kd * N, int(splits), ptr(slab),

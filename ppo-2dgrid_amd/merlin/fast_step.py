@@ -201,6 +201,11 @@ WGRAD_PLANES = False
 # input-gradient GEMMs (which do not store them), so the weight gradient runs on planes (merlin_h3_gemm_tn_planes).
 # Off: the splits take the GEMMs' CUs (scripts/ab_update.py 4 6 fast,fast_nosplit: 218.7 vs 189.9 ms per update)
 WGRAD_SPLIT_SIDE = False
+# conv3's forward computes each distinct 5x5-tile patch of the minibatch once (merlin_tower_window_conv3_reuse,
+# MinibatchWindows.rep_row; same outputs): "gather" -- only the representative rows of a3 are written and fc1's
+# forward and weight-gradient GEMMs read every row through rep_row (merlin_h3_gemm_{nt,tn}_gather; h3 only, else as
+# "copy"); "copy" -- the other rows copied from theirs; False -- every row computed
+PATCH_REUSE = "gather"
 
 
 class WindowStep:
@@ -289,13 +294,17 @@ class WindowStep:
             Q = nat.h3_gemm_nt(a2w, am2, P3t, amW3, cfg=nat.H3_NT_CFG["qwin"], name="gemm_window_fwd")
         else:
             Q = torch.bmm(a2w, W3r)  # [2, windows, (ky, kx, co)]
-        Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None)
+        split_side = h3 and WGRAD_SPLIT_SIDE and WGRAD_SIDE and not WGRAD_EARLY
+        rep_row = getattr(mb, "rep_row", None) if PATCH_REUSE else None
+        # a3's rows through their patch representatives (the other rows never written)
+        arows = rep_row if (PATCH_REUSE == "gather" and h3 and not WGRAD_PLANES and not split_side) else None
+        Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None, rep_row=rep_row,
+                                    copy=2 if arows is not None else 3)
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
         pa3 = pdz = None
         main = torch.cuda.current_stream()
         side = self.side_stream(a3.device)
-        split_side = h3 and WGRAD_SPLIT_SIDE and WGRAD_SIDE and not WGRAD_EARLY
         if split_side:  # a3's planes for the weight gradient, on the side stream beside the forward GEMM
             side.wait_stream(main)
             with torch.cuda.stream(side):
@@ -306,7 +315,7 @@ class WindowStep:
             if WGRAD_PLANES and not split_side:
                 pa3 = torch.empty((2, n, 1152), dtype=torch.int16, device=a3.device)
             h = nat.h3_gemm_nt(a3, am3, P4, amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd",
-                               planes_out=pa3)
+                               planes_out=pa3, rows=arows)
         else:
             h = nat.x6_gemm_nt(a3, P4, bias=b4, cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
         logits, value = nat.heads_fwd(h, Wa, Wc)  # both heads in one pass over h (the loss adds their biases)
@@ -327,7 +336,7 @@ class WindowStep:
             if h3 and pdz is not None:
                 nat.h3_gemm_tn(pdz, amz, pa3, am3, name="gemm_wgrad", out=g[4])
             elif h3:
-                nat.h3_gemm_tn(dz, amz, a3, am3, name="gemm_wgrad", out=g[4])
+                nat.h3_gemm_tn(dz, amz, a3, am3, name="gemm_wgrad", out=g[4], rows=arows)
             else:
                 nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
 

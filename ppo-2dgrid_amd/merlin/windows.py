@@ -314,13 +314,22 @@ class WindowPlan:
         offs[goff[1:] + torch.arange(nmb, device=dev)] = span
         live = self.kid.index_select(0, gall)  # [G, 9] patch ids
         kmap = torch.full((nmb, K), -1, dtype=torch.int32, device=dev)
-        kmap.view(-1)[(mbg.unsqueeze(1) * K + live).reshape(-1)] = live.reshape(-1)
+        at = (mbg.unsqueeze(1) * K + live).reshape(-1)
+        kmap.view(-1)[at] = live.reshape(-1)
+        # conv3's patch reuse (merlin_tower_window_conv3_reuse): rep_row = per row j*9 + p3 of its minibatch, one row
+        # of the minibatch holding the same patch (rmap[m][k]: the row that won the scatter -- which one does not
+        # matter, they compute the same bits)
+        rmap = torch.full((nmb, K), -1, dtype=torch.int32, device=dev)
+        rmap.view(-1)[at] = (j.unsqueeze(1) * 9 + torch.arange(9, device=dev)).to(torch.int32).reshape(-1)
+        rep_row = rmap.view(-1)[at]  # [G * 9], minibatch m's rows at goff[m] * 9 ..
+        del rmap
         out = []
         for m, c in enumerate(counts):
             g0 = goff_h[m]
             mw = MinibatchWindows(gall[g0:g0 + c], inv_local[lo_h[m]:hi_h[m]], slot[m], order[lo_h[m]:hi_h[m]],
                                   offs[g0 + m:g0 + m + c + 1])
             mw.kmap = kmap[m]
+            mw.rep_row = rep_row[g0 * 9:(g0 + c) * 9]
             out.append(mw)
         return out
 

@@ -65,6 +65,7 @@ def main():
             FS.SIDE_PRIORITY = -1 if "sidehi" in name else 0
             FS.WINDOW_H3 = "wh3" in name
             FS.WGRAD_SPLIT_SIDE = "splitside" in name
+            FS.PATCH_REUSE = False if "noreuse" in name else "copy" if "reusecopy" in name else "gather"
             nat.X6_NT_CFG["fwd"] = 28 if "fwd28" in name else 20
             nat.X6_NT_CFG["dgrad"] = 27 if "dgrad27" in name else 22
             nat.X6_TN_CFG = next((int(t[2:]) for t in name.split("_") if t[:2] == "tn" and t[2:].isdigit()), 0)
@@ -78,6 +79,7 @@ def main():
     names = sys.argv[3].split(",") if len(sys.argv) > 3 else ["x6_overlap", "no_overlap", "hipblaslt"]
     settings = {n: setter(n) for n in names}
     times = {n: [] for n in settings}
+    kt = {}
     for _ in range(iters):
         for n, s in settings.items():
             s()
@@ -89,7 +91,14 @@ def main():
             t0 = time.perf_counter()
             agent.update(lv)
             torch.cuda.synchronize()
-            nat.KernelTimer.stop()
+            recs = nat.KernelTimer.stop()
+            if recs:  # per-kernel HIP-event times of this run (the last repeat's are printed)
+                agg = {}
+                for name_, e0, e1, _, _ in recs:
+                    a = agg.setdefault(name_, [0, 0.0])
+                    a[0] += 1
+                    a[1] += e0.elapsed_time(e1)
+                kt[n] = agg
             times[n].append((time.perf_counter() - t0) * 1e3)
             host.setdefault(n, []).append(agent.last_host_loop_ms)
     for n, t in times.items():
@@ -98,6 +107,10 @@ def main():
         print(f"{n:12s} median {t[len(t) // 2]:.1f} ms/update  min {t[0]:.1f}  all {[round(x, 1) for x in times[n]]}"
               f"  host queueing median {h[len(h) // 2]:.1f} ms")
     print("distinct frames per sample", agent.last_distinct_frac)
+    for n, agg in kt.items():
+        print(f"-- {n}: per-kernel HIP events (launches, total ms, avg us)")
+        for name_, (c, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:16]:
+            print(f"   {name_:28s} {c:5d} {ms:9.2f} {ms / c * 1e3:9.1f}")
 
 
 if __name__ == "__main__":

@@ -33,19 +33,32 @@ def main():
     nw = plan.num_windows
     Q = torch.randn(2, nw, 576, device=dev, generator=g)
     b3 = torch.randn(2, 64, device=dev, generator=g)
-    f = lambda: nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True)  # noqa: E731
-    Y3, bits = f()
-    ts = []
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        f()
-        e1.record()
-        torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1) * 1e3)
-    print(f"lib {os.path.basename(nat.LIB_PATH)} U={int(mb.groups.numel())} windows={nw}: "
-          f"{statistics.median(ts):.1f} us  Y3 sum {float(Y3.double().sum()):.10e}  "
-          f"bits xor {int(bits.view(-1).cpu().numpy().astype('uint64').sum(dtype='uint64'))}", flush=True)
+    am = torch.zeros(2, dtype=torch.int32, device=dev)
+    variants = {"all rows": lambda: nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am),
+                "patch reuse": lambda: nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am, rep_row=mb.rep_row),
+                "reps only + masks": lambda: nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am,
+                                                              rep_row=mb.rep_row, copy=2),
+                "reps only": lambda: nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am, rep_row=mb.rep_row,
+                                                      copy=0)}
+    outs = {}
+    for name, f in variants.items():
+        am.zero_()
+        Y3, bits = f()
+        outs[name] = (Y3, bits, am.clone())
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            f()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        print(f"{name}: lib {os.path.basename(nat.LIB_PATH)} U={int(mb.groups.numel())} windows={nw} "
+              f"reps={int((mb.rep_row == torch.arange(mb.rep_row.numel(), device=dev, dtype=torch.int32)).sum())}: {statistics.median(ts):.1f} us  "
+              f"Y3 sum {float(Y3.double().sum()):.10e}  "
+              f"bits xor {int(bits.view(-1).cpu().numpy().astype('uint64').sum(dtype='uint64'))}", flush=True)
+    (a, ab, aa), (b, bb, ba) = list(outs.values())[:2]
+    print("identical:", torch.equal(a, b), torch.equal(ab, bb), torch.equal(aa, ba), flush=True)
 
 
 if __name__ == "__main__":

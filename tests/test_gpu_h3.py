@@ -125,3 +125,49 @@ def test_gemm_tn_cancellation(device, cfg):
     rel = lambda W: float((W.double() - W64).norm() / W64.norm())  # noqa: E731
     ref = rel(sum(torch.bmm(dz[:, i:i + 2000].transpose(1, 2), a3[:, i:i + 2000]) for i in range(0, Kd, 2000)))
     assert rel(nat.h3_gemm_tn(dz, nat.h3_amax(dz), a3, nat.h3_amax(a3), cfg=cfg)) <= ref
+
+
+@pytest.mark.parametrize("cfg", [10, 11, 12, 13])
+def test_gemm_nt_gather_rows_bitwise(device, cfg):
+    """merlin_h3_gemm_nt_gather (A's rows read by 64-value chunks through a row map, as the update's forward reads
+    conv3's patch representatives) == the same GEMM on the gathered matrix, bit for bit; tile-ragged row count,
+    both towers, with and without the bias + ReLU epilogue."""
+    from merlin import _native as nat
+
+    M, K = 1000, 576
+    N = 576 if cfg == 11 else 512
+    A, B = _operands(device, M, N, K, 41 + cfg, ragged=True)
+    g = torch.Generator(device=device).manual_seed(cfg)
+    nc = M * K // 64
+    rows = torch.randint(0, nc, (nc,), device=device, generator=g, dtype=torch.int32)
+    keep = torch.rand(nc, device=device, generator=g) < 0.4  # some chunk rows read in place
+    rows[keep] = torch.arange(nc, device=device, dtype=torch.int32)[keep]
+    Ad = A.view(2, nc, 64)[:, rows.long()].reshape(2, M, K).contiguous()
+    amA, amB = nat.h3_amax(Ad), nat.h3_amax(B)
+    Bp = nat.h3_split(B, amB)
+    bias = torch.randn(2, N, device=device, generator=g)
+    for b in (None, bias):
+        ref = nat.h3_gemm_nt(Ad, amA, Bp, amB, bias=b, cfg=cfg)
+        got = nat.h3_gemm_nt(A, amA, Bp, amB, bias=b, cfg=cfg, rows=rows)
+        assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("Kd,splits,cfg", [(3001, 32, 0), (40000, 32, 0), (700, 3, 1), (257, 1, 0)])
+def test_gemm_tn_gather_rows_bitwise(device, Kd, splits, cfg):
+    """merlin_h3_gemm_tn_gather (B's rows read by 64-column chunks through a row map: the weight gradient over
+    conv3's patch representatives) == the same GEMM on the gathered matrix, bit for bit, split-K and ragged."""
+    from merlin import _native as nat
+
+    g = torch.Generator(device=device).manual_seed(Kd)
+    M, N = 512, 576
+    dz = torch.randn(2, Kd, M, device=device, generator=g) * 1e-7
+    a3 = torch.relu(torch.randn(2, Kd, N, device=device, generator=g))
+    nc = Kd * N // 64
+    rows = torch.randint(0, nc, (nc,), device=device, generator=g, dtype=torch.int32)
+    keep = torch.rand(nc, device=device, generator=g) < 0.4
+    rows[keep] = torch.arange(nc, device=device, dtype=torch.int32)[keep]
+    ad = a3.view(2, nc, 64)[:, rows.long()].reshape(2, Kd, N).contiguous()
+    amz, am3 = nat.h3_amax(dz), nat.h3_amax(ad)
+    ref = nat.h3_gemm_tn(dz, amz, ad, am3, splits=splits, cfg=cfg)
+    got = nat.h3_gemm_tn(dz, amz, a3, am3, splits=splits, cfg=cfg, rows=rows)
+    assert torch.equal(got, ref)

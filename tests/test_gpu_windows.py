@@ -71,6 +71,49 @@ def test_window_lut_and_conv3_match_gathers(device):
     assert torch.equal(a, b)
 
 
+def test_window_conv3_patch_reuse_bitwise(device):
+    """merlin_tower_window_conv3_reuse (each distinct patch of a minibatch computed once, the rows sharing it
+    copied) == every row computed: Y3, ReLU bit words and the operand scale, bit for bit, on every bulk
+    minibatch of two epochs (the last one ragged); copy=2 / 0 write the representative rows (and the masks)
+    only."""
+    from merlin import _native as nat
+
+    codes, plan = _plan(device)
+    B = codes.shape[0]
+    g = torch.Generator(device=device)
+    g.manual_seed(11)
+    perms = [torch.randperm(B, device=device, generator=g) for _ in range(2)]
+    mbs = plan.update_minibatches(perms, 3000, bulk=True)
+    Q = torch.randn(2, plan.num_windows, 576, device=device, generator=g)
+    b3 = torch.randn(2, 64, device=device, generator=g)
+    shared = 0
+    for epoch in mbs:
+        for mb in epoch:
+            n = int(mb.groups.numel())
+            rr = mb.rep_row.long()
+            assert rr.numel() == n * 9 and bool((rr >= 0).all()) and bool((rr < n * 9).all())
+            assert torch.equal(rr[rr], rr)  # representatives represent themselves
+            live = plan.kid[mb.groups].reshape(-1)
+            assert torch.equal(live[rr], live)  # and hold the row's patch
+            own = torch.arange(n * 9, device=device)
+            shared += int((rr != own).sum())
+            am0 = torch.zeros(2, dtype=torch.int32, device=device)
+            am1 = torch.zeros(2, dtype=torch.int32, device=device)
+            Y0, b0 = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am0)
+            Y1, b1 = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am1, rep_row=mb.rep_row)
+            assert torch.equal(Y0, Y1) and torch.equal(b0, b1) and torch.equal(am0, am1)
+            for copy in (2, 0):
+                am1.zero_()
+                Y2, b2 = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am1, rep_row=mb.rep_row,
+                                          copy=copy)
+                reps = rr == own
+                assert torch.equal(Y2.view(2, -1, 64)[:, reps], Y0.view(2, -1, 64)[:, reps])
+                assert torch.equal(b2[:, reps], b0[:, reps]) and torch.equal(am1, am0)
+                if copy == 2:
+                    assert torch.equal(b2, b0)
+    assert shared > 0  # rows actually copied
+
+
 @pytest.mark.parametrize("n,nkeys,L,use_slot", [(1, 3, 4, False), (5000, 37, 64, True),
                                                 (200000, 3000, 1024, True), (70000, 2, 256, False)])
 def test_segment_sum_matches_index_add(device, n, nkeys, L, use_slot):
