@@ -809,26 +809,41 @@ __device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const f
         if constexpr (GB) {
             const int col = n0 + 8 * g;
             pb[i] = B + (col & 63) / 4;
-            mb[i] = bmap + (col >> 6);
+            mb[i] = bmap + (k0 + k) * nc + (col >> 6);
         } else {
             pb[i] = B + (k0 + k) * rowB + g * 2;
         }
     }
     auto fetch_rows = [&](int64_t kk) {  // GB: chunk rows of step kk (rows past k1 clamped, zeroed when staged)
         if constexpr (GB) {
+            if (kk + BK <= k1) {  // full step: a wave-uniform offset
+                const int64_t dm = (kk - k0) * nc;
 #pragma unroll
-            for (int i = 0; i < UB; i++) xb[i] = mb[i][std::min(kk + kb[i], k1 - 1) * nc];
+                for (int i = 0; i < UB; i++) xb[i] = mb[i][dm];
+            } else {
+#pragma unroll
+                for (int i = 0; i < UB; i++) xb[i] = mb[i][(std::min(kk + kb[i], k1 - 1) - k0 - kb[i]) * nc];
+            }
         }
     };
     const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float4 ra[UA][2], rb[UB][2];
     auto load = [&](int64_t kk) {
         if constexpr (GB) {
+            if (kk + BK <= k1) {
+                const int64_t da = (kk - k0) * rowA;
 #pragma unroll
-            for (int i = 0; i < UA; i++) {
-                const float4 *src = pa[i] + (std::min(kk + ka[i], k1 - 1) - k0 - ka[i]) * rowA;
-                ra[i][0] = src[0];
-                ra[i][1] = src[1];
+                for (int i = 0; i < UA; i++) {
+                    ra[i][0] = pa[i][da];
+                    ra[i][1] = pa[i][da + 1];
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < UA; i++) {
+                    const float4 *src = pa[i] + (std::min(kk + ka[i], k1 - 1) - k0 - ka[i]) * rowA;
+                    ra[i][0] = src[0];
+                    ra[i][1] = src[1];
+                }
             }
 #pragma unroll
             for (int i = 0; i < UB; i++) {
