@@ -307,6 +307,10 @@ PMC_ALIAS = {"k_seg_sum_R": ("k_seg_sum<2, 1>", "k_seg_fix<1>"),
              "k_window_lut": ("k_window_lut<0>",),
              "k_window_lut_all": ("k_window_lut<1>",),
              "gemm_wgrad": ("k_h3_tn<128, 192, 4, 2>", "k_x6_fold")}
+# with conv3's patch reuse (merlin/fast_step.py PATCH_REUSE = "gather") the update's k_window_conv3 span is the
+# representatives' kernel + the mask-word copy, and fc1's forward / weight gradient read a3 through the row map
+PMC_ALIAS_GATHER = {"k_window_conv3": ("k_window_conv3_reps", "k_window_conv3_copy<false>"),
+                    "gemm_wgrad": ("k_h3_tng<128, 192, 4, 2>", "k_x6_fold")}
 # rocprofv3 names of merlin_h3_gemm_nt's configurations (csrc/merlin_h3.hip launch_h3_gemm_nt)
 H3_NT_NAMES = {0: "k_h3_nt<256, 128, 4, 2, {}>", 1: "k_h3_nt<128, 192, 4, 2, {}>", 2: "k_h3_nt<128, 128, 2, 2, {}>",
                3: "k_h3_nt<128, 256, 2, 4, {}>", 10: "k_h3_ntp<256, 128, 4, 2, {}>", 11: "k_h3_ntp<128, 192, 4, 2, {}>",
@@ -314,9 +318,15 @@ H3_NT_NAMES = {0: "k_h3_nt<256, 128, 4, 2, {}>", 1: "k_h3_nt<128, 192, 4, 2, {}>
 
 
 def h3_gemm_names(nat):
-    """PMC_ALIAS entries of the update's fc1 forward (bias + ReLU epilogue) and input gradient."""
-    return {"gemm_fc1_fwd": (H3_NT_NAMES.get(nat.H3_NT_CFG["fwd"], "?").format(1),),
-            "gemm_fc1_dgrad": (H3_NT_NAMES.get(nat.H3_NT_CFG["dgrad"], "?").format(0),)}
+    """PMC_ALIAS entries of the update's fc1 forward (bias + ReLU epilogue) and input gradient (and, with the patch
+    reuse's gathered rows, of conv3 and the weight gradient)."""
+    from merlin import fast_step as FS
+
+    fwd = H3_NT_NAMES.get(nat.H3_NT_CFG["fwd"], "?").format(1)
+    out = {"gemm_fc1_dgrad": (H3_NT_NAMES.get(nat.H3_NT_CFG["dgrad"], "?").format(0),)}
+    if FS.PATCH_REUSE == "gather":
+        return {**out, **PMC_ALIAS_GATHER, "gemm_fc1_fwd": (fwd.replace("k_h3_ntp<", "k_h3_ntpg<"),)}
+    return {**out, "gemm_fc1_fwd": (fwd,)}
 PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 
 
@@ -346,6 +356,10 @@ def gather_note(name, k):
     (MI355X_MICROARCH.md 'Indexed rows': 16.8-18.8 TB/s for L2-resident rows), not HBM."""
     if name != "k_window_conv3":
         return {}
+    from merlin import fast_step as FS
+
+    if FS.PATCH_REUSE:  # only the patch representatives' rows are computed (their count is not read back)
+        return {"cache_gather": {"note": "patch reuse: 81 Q rows per representative row only (~1/3 of the rows)"}}
     gathered = 9 * k["bytes_per_launch"]  # ~ 9 Q rows of 256 B per written Y3 row
     tbs = gathered / (k["avg_us"] * 1e-6) / 1e12
     return {"cache_gather": {"bytes_per_launch": gathered, "achieved_tbs": round(tbs, 2),
