@@ -789,6 +789,7 @@ __device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const f
 
     int ka[UA], la[UA], kb[UB], lb[UB];
     const float4 *pa[UA], *pb[UB];
+    constexpr bool PAIR = GB && 8 % UB == 0 && RCB % UB == 0;
     const int32_t *mb[UB];  // GB: the unit's chunk column of bmap (stride N / 64 per k row)
     int32_t xb[UB];         // GB: the chunk rows of the next load
     const int nc = N / 64;
@@ -802,7 +803,9 @@ __device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const f
     }
 #pragma unroll
     for (int i = 0; i < UB; i++) {
-        const int q = std::min(tid + i * NT, QB - 1);
+        // GB with PAIR: a thread's UB units are adjacent column groups of one row and one 64-column chunk, so they
+        // share one chunk row (one index read per thread and step)
+        const int q = std::min(PAIR ? UB * tid + i : tid + i * NT, QB - 1);
         const int k = q / RCB, g = q - (q / RCB) * RCB;
         kb[i] = k;
         lb[i] = 2 * PSA + k * RCB + (g ^ tr_swz<RCB>(k));
@@ -816,14 +819,17 @@ __device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const f
     }
     auto fetch_rows = [&](int64_t kk) {  // GB: chunk rows of step kk (rows past k1 clamped, zeroed when staged)
         if constexpr (GB) {
+            constexpr int NX = PAIR ? 1 : UB;
             if (kk + BK <= k1) {  // full step: a wave-uniform offset
                 const int64_t dm = (kk - k0) * nc;
 #pragma unroll
-                for (int i = 0; i < UB; i++) xb[i] = mb[i][dm];
+                for (int i = 0; i < NX; i++) xb[i] = mb[i][dm];
             } else {
 #pragma unroll
-                for (int i = 0; i < UB; i++) xb[i] = mb[i][(std::min(kk + kb[i], k1 - 1) - k0 - kb[i]) * nc];
+                for (int i = 0; i < NX; i++) xb[i] = mb[i][(std::min(kk + kb[i], k1 - 1) - k0 - kb[i]) * nc];
             }
+#pragma unroll
+            for (int i = NX; i < UB; i++) xb[i] = xb[0];
         }
     };
     const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -894,7 +900,7 @@ __device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const f
             }
 #pragma unroll
         for (int i = 0; i < UB; i++)
-            if (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB) {
+            if (PAIR ? UB * tid + i < QB : (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB)) {
                 const bool in = kk + kb[i] < k1;
                 u32x4 p0, p1;
                 h3_split8(in ? rb[i][0] : zero, in ? rb[i][1] : zero, scB, scB2, p0, p1);
