@@ -477,7 +477,8 @@ int merlin_x6_gemm_tn(const float *A_dev, const float *B_dev, int64_t Kd, int32_
  * plane products h h, h l, l h (fp32 accumulation, the lo sum scaled by 2^-11 once), the result scaled back by
  * 2^-(eA + eB).  Error per output below the fp32 GEMM's (hipBLASLt) on the same operands (tests/test_gpu_h3.py).
  * Replaces the same three fp32 GEMMs as merlin_x6_* (forward src/actor_critic.py:40, backward src/ppo.py:153-155).
- * amax:  amax_dev[t] = float bits of max |x| over tower t's n values (x + t * stride; n, stride % 4 == 0).
+ * amax:  amax_dev[t] = float bits of max |x| over tower t's n values (x + t * stride; n, stride % 4 == 0); with n = 0
+ *        it zeroes amax_dev[0 .. towers) (any count up to 2^20, by a kernel: safe inside a captured graph).
  * split: weight planes f16 [t][n/8][2][8] (per group of 8 values a hi and a lo 16-byte chunk), scaled by the
  *        exponent of amax_dev[t]; 4 bytes per value.
  * gemm_nt: C[t][m][n] = sum_k A[t][m][k] B[t][n][k], A fp32 [M][K] with its amax, B planes [N][K] (K % 32 == 0;

@@ -898,7 +898,9 @@ int merlin_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int32_t M, int
 
 int merlin_h3_amax(const float *x, int64_t n, int32_t towers, int64_t stride, uint32_t *amax, void *stream) {
     if (!amax || (n > 0 && !x)) return fail(MERLIN_E_INVALID, "null argument");
-    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    // n == 0: zero amax[0 .. towers) only (any count up to 2^20: a rollout's per-step scales at once)
+    if (towers < 1 || (n > 0 && towers > 2) || towers > (1 << 20))
+        return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (n < 0 || n % 4 || stride % 4 || (towers > 1 && stride < n)) return fail(MERLIN_E_INVALID, "n, stride: multiples of 4");
     HIP_TRY(merlin::launch_h3_amax(x, n, towers, stride, amax, (hipStream_t)stream));
     return MERLIN_OK;

@@ -115,7 +115,8 @@ __global__ __launch_bounds__(256) void k_h3_amax(const float4 *__restrict__ x, i
 }
 
 __global__ void k_h3_zero(uint32_t *__restrict__ amax, int T) {
-    if ((int)threadIdx.x < T) amax[threadIdx.x] = 0u;
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i < T) amax[i] = 0u;
 }
 
 // planes of a row-major [T][R][C] fp32 tensor: [T][R][C/8][2][8] f16 (per group of 8 values a hi chunk and a lo
@@ -1426,7 +1427,7 @@ __global__ void k_h3_fill0(float4 *__restrict__ out, int64_t n4) {
 hipError_t launch_h3_amax(const float *x, int64_t n, int T, int64_t stride, uint32_t *amax, hipStream_t s) {
     // zeroed by a kernel, not hipMemsetAsync: this runs inside the fast step's captured forward graph, and a
     // captured memset node replays with a wrong fill value on ROCm 7 (scripts/probe_graph_then.py: 0x80808080)
-    hipLaunchKernelGGL(k_h3_zero, dim3(1), dim3(64), 0, s, amax, T);
+    hipLaunchKernelGGL(k_h3_zero, dim3((T + 63) / 64), dim3(64), 0, s, amax, T);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || n <= 0) return e;
     if (n % 4 || stride % 4) return hipErrorInvalidValue;

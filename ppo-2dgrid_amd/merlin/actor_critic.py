@@ -514,7 +514,7 @@ class CNNActorCritic(nn.Module):
     # the all-windows table (Qall: 9 GB and ~288 GFLOP per rollout, whatever the rollout's size)
     ALL_WINDOWS_MIN_FRAMES = 1 << 18
 
-    def rollout_pack(self, frames: int | None = None, all_windows: bool | None = None):
+    def rollout_pack(self, frames: int | None = None, all_windows: bool | None = None, steps: int | None = None):
         """The weights of the acting path in the layouts its kernels and GEMMs read, built once
         per rollout (the weights do not change while acting).
 
@@ -527,7 +527,9 @@ class CNNActorCritic(nn.Module):
         position and runs conv3 as a GEMM over the im2col rows (merlin_tower_conv2_lut_fwd +
         conv3_im2col_fwd, a few MB).  Both: fc1 with columns permuted to (p3, co), biases stacked.
         all_windows: the layout decided by the caller (PPO decides once, before its rollout is captured: the
-        free-memory reading changes between the eager rollout and the capture); None = decide here."""
+        free-memory reading changes between the eager rollout and the capture); None = decide here.
+        steps: the act_codes_packed steps the pack serves (0 .. steps - 1): each gets its own operand-scale row, all
+        zeroed here at once (None: one row, zeroed before every step)."""
         from . import _native as nat
 
         ea, ec = self.actor_extractor.network, self.critic_extractor.network
@@ -563,9 +565,10 @@ class CNNActorCritic(nn.Module):
         if self.fc1_impl == "h3" and all_windows and ROLLOUT_FC1_H3:  # fc1 of every step on merlin_h3.hip
             amW = nat.h3_amax(W4p.contiguous())
             pack["W4h"] = (nat.h3_split(W4p.contiguous(), amW), amW)
-            # per step: max |a3| per tower (zeroed by a kernel before each step's conv3: this is built inside the
-            # captured rollout graph, where a memset would replay wrong)
-            pack["am3"] = torch.empty(2, dtype=torch.int32, device=W4p.device)
+            # per step: max |a3| per tower, one row per step of the rollout when the caller says how many (all zeroed
+            # here by one kernel: this is built inside the captured rollout graph, where a memset would replay
+            # wrong), else one row zeroed before each step's conv3
+            pack["am3"] = nat.h3_zero(torch.empty((max(1, int(steps or 1)), 2), dtype=torch.int32, device=W4p.device))
         elif self.fc1_impl in ("x6", "h3"):  # fc1 of every step on the bf16 MFMA, exact fp32 products (merlin_gemm2.hip)
             pack["W4pp"] = nat.x6_split(W4p.contiguous())
         else:
@@ -594,7 +597,10 @@ class CNNActorCritic(nn.Module):
         n = codes.shape[0]
         am3 = pack.get("am3")
         if am3 is not None:
-            nat.h3_zero(am3)  # a kernel: this runs inside the captured rollout graph
+            if am3.shape[0] > step:  # this step's own row, zeroed with the others when the pack was built
+                am3 = am3[step]
+            else:
+                am3 = nat.h3_zero(am3[0])  # a kernel: this runs inside the captured rollout graph
         if "Qall" in pack:
             a3 = nat.codes_conv3(codes, pack["Qall"], pack["b3"], amax=am3).view(2, n, 576)
         else:  # per-frame conv2 lookups + conv3 GEMM (small rollouts, rollout_pack)

@@ -69,6 +69,10 @@ class _PPOLoss(torch.autograd.Function):
         return tuple(d * g for d in ctx.saved_tensors) + (None,) * 10
 
 
+# the acting path's fc1 operand scales: one row per rollout step, all zeroed by one kernel when the rollout starts
+# (False: one row zeroed by a kernel before every step -- 256 more launches per captured rollout)
+ROLLOUT_SCALE_ROWS = True
+
 class PPO:
     def __init__(self, env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=10,
                  batch_size=2048, minibatch_size=256, vf_coef=0.5, ent_coef=0.01, device="cuda",
@@ -235,7 +239,8 @@ class PPO:
             self._act_epoch.add_(1)
             if self.conv1_from_codes and self.rollout_all_windows is None:  # decided once, before any capture
                 self.rollout_all_windows = self.ac._use_all_windows((T + 1) * buf.N, self.device)
-            pack = (self.ac.rollout_pack(frames=(T + 1) * buf.N, all_windows=self.rollout_all_windows)
+            pack = (self.ac.rollout_pack(frames=(T + 1) * buf.N, all_windows=self.rollout_all_windows,
+                                         steps=T + 1 if ROLLOUT_SCALE_ROWS else None)
                     if self.conv1_from_codes else None)
             pending = False
             for t in range(T):

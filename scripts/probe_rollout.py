@@ -26,6 +26,9 @@ def main():
         AC.ROLLOUT_FC1_H3 = v.startswith("h3")
         nat.H3_NT_CFG["rollout"] = next((int(t[3:]) for t in v.split("_") if t[:3] == "h3r"), 12)
         AC.QALL_H3 = "qbmm" not in v
+        from merlin import ppo as PPO_MOD
+
+        PPO_MOD.ROLLOUT_SCALE_ROWS = "zero" not in v  # e.g. h3r12_zero: the per-step zeroing launch
     dev = torch.device("cuda", 0)
     env = MerlinVecEnv(4096, "mediumhard", seed=777, device=dev)
     torch.manual_seed(777)
