@@ -513,6 +513,19 @@ int merlin_h3_gemm_nt_gather(const float *A_dev, const uint32_t *amax_a_dev, con
                              const uint32_t *amax_b_dev, int64_t M, int32_t N, int32_t K, int32_t towers,
                              int64_t a_stride, int64_t b_stride, const float *bias_dev, float *C_dev, int64_t c_stride,
                              const int32_t *a_rows_dev, int32_t cfg, void *stream);
+/* gemm_nt_heads: the update's fc1 forward (both towers, bias + ReLU, cfg 10 / 12 / 13, a_rows_dev nullable as in
+ *          gemm_nt_gather) with the policy / value heads (src/actor_critic.py:41-46) folded into the epilogue: per
+ *          row, merlin_h3_heads_parts(N, cfg) partial dot products of h with head_w0 [n_actions][N] (tower 0, the
+ *          actor; n_actions <= 4) and head_w1 [N] (tower 1, the critic), head_partials_dev float
+ *          [2][parts][M][4]; merlin_heads_combine sums them in order: logits [M][n_actions], value [M] (no biases). */
+int merlin_h3_gemm_nt_heads(const float *A_dev, const uint32_t *amax_a_dev, const void *B_dev,
+                            const uint32_t *amax_b_dev, int64_t M, int32_t N, int32_t K, int64_t a_stride,
+                            int64_t b_stride, const float *bias_dev, float *C_dev, int64_t c_stride,
+                            const int32_t *a_rows_dev, const float *head_w0_dev, int32_t n_actions,
+                            const float *head_w1_dev, float *head_partials_dev, int32_t cfg, void *stream);
+int32_t merlin_h3_heads_parts(int32_t N, int32_t cfg);
+int merlin_heads_combine(const float *partials_dev, int32_t parts, int64_t M, int32_t n_actions, float *logits_dev,
+                         float *value_dev, void *stream);
 int merlin_h3_gemm_tn_gather(const float *A_dev, const uint32_t *amax_a_dev, const float *B_dev,
                              const uint32_t *amax_b_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
                              int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev, float *out_dev,

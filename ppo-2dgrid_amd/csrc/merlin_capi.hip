@@ -916,14 +916,17 @@ int merlin_h3_split(const float *x, int64_t n, int32_t towers, const uint32_t *a
 
 static int h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
                       int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride, const float *bias,
-                      float *C, int64_t c_stride, void *a_planes, const int32_t *a_rows, int32_t cfg, void *stream) {
+                      float *C, int64_t c_stride, void *a_planes, const int32_t *a_rows, int32_t cfg, void *stream,
+                      const float *head_w0 = nullptr, int32_t n_actions = 0, const float *head_w1 = nullptr,
+                      float *head_part = nullptr) {
     if (M < 0 || N <= 0 || K <= 0) return fail(MERLIN_E_INVALID, "bad shape");
     if (M > 0 && (!A || !B || !C || !amax_a || !amax_b)) return fail(MERLIN_E_INVALID, "null argument");
     if (K % 32) return fail(MERLIN_E_UNSUPPORTED, "K must be a multiple of 32");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (a_stride % 4 || b_stride % 8) return fail(MERLIN_E_INVALID, "tower strides: A multiple of 4, B of 8");
     const hipError_t e = merlin::launch_h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, bias, C,
-                                                   c_stride, a_planes, cfg, (hipStream_t)stream, a_rows);
+                                                   c_stride, a_planes, cfg, (hipStream_t)stream, a_rows, head_w0,
+                                                   n_actions, head_w1, head_part);
     if (e == hipErrorInvalidValue)
         return fail(MERLIN_E_UNSUPPORTED, "N not a multiple of the tile width / bad cfg / unsupported gather");
     HIP_TRY(e);
@@ -967,6 +970,28 @@ int merlin_h3_gemm_tn(const float *A, const uint32_t *amax_a, const float *B, co
                       float *slab, float *out, int32_t cfg, void *stream) {
     return h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, false, cfg,
                       stream);
+}
+
+int merlin_h3_gemm_nt_heads(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
+                            int32_t N, int32_t K, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
+                            int64_t c_stride, const int32_t *a_rows, const float *head_w0, int32_t n_actions,
+                            const float *head_w1, float *head_partials, int32_t cfg, void *stream) {
+    if (M > 0 && (!bias || !head_w0 || !head_w1 || !head_partials)) return fail(MERLIN_E_INVALID, "null argument");
+    if (n_actions < 1 || n_actions > 4) return fail(MERLIN_E_UNSUPPORTED, "heads epilogue: 1..4 actions");
+    if (merlin::h3_heads_parts(N, cfg) == 0) return fail(MERLIN_E_UNSUPPORTED, "heads epilogue: cfg 10, 12 or 13");
+    if (a_rows && K % 64) return fail(MERLIN_E_UNSUPPORTED, "gathered rows: K must be a multiple of 64");
+    return h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, 2, a_stride, b_stride, bias, C, c_stride, nullptr, a_rows, cfg,
+                      stream, head_w0, n_actions, head_w1, head_partials);
+}
+
+int32_t merlin_h3_heads_parts(int32_t N, int32_t cfg) { return merlin::h3_heads_parts(N, cfg); }
+
+int merlin_heads_combine(const float *partials, int32_t parts, int64_t M, int32_t n_actions, float *logits,
+                         float *value, void *stream) {
+    if (M < 0 || parts < 1 || n_actions < 1 || n_actions > 4) return fail(MERLIN_E_INVALID, "bad shape");
+    if (M > 0 && (!partials || !logits || !value)) return fail(MERLIN_E_INVALID, "null argument");
+    HIP_TRY(merlin::launch_heads_combine(partials, parts, M, n_actions, logits, value, (hipStream_t)stream));
+    return MERLIN_OK;
 }
 
 int merlin_h3_gemm_tn_gather(const float *A, const uint32_t *amax_a, const float *B, const uint32_t *amax_b, int64_t Kd,

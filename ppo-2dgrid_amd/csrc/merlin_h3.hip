@@ -304,12 +304,23 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_nt(const float *__restric
 // representatives (merlin_tower_window_conv3_reuse), so the non-representative rows are never written.  The
 // thread's chunk rows are read once into registers; a k step picks its chunk's with a uniform select.
 constexpr int GA_CHUNKS = 9;
+// EPI 2 (the update's fc1 forward): bias + ReLU as EPI 1, and the policy / value heads' dot products of the rows
+// (src/actor_critic.py:41-46, Linear(512, A) on the actor tower's h, Linear(512, 1) on the critic's) folded into the
+// epilogue, so h is not read again for them: every wave leaves, per row, the dot products of its WTN columns with
+// the head weights (w0 [na][N] for tower 0, w1 [N] for tower 1) as partial [t][tn * WGN + wn][row][o], o < 4, and
+// merlin_heads_combine adds a row's tiles_n * WGN partials in order.
+struct HeadsArg {
+    const float *w0, *w1;
+    int na;
+    float *part;
+};
 template <int BM, int BN, int WGM, int WGN, int EPI, bool GA>
 __device__ __forceinline__ void h3_ntp_body(const float *__restrict__ A, const u32x4 *__restrict__ B,
                                             const uint32_t *__restrict__ amaxA, const uint32_t *__restrict__ amaxB,
                                             int64_t M, int N, int K, int64_t sA, int64_t sB,
                                             const float *__restrict__ bias, float *__restrict__ C, int64_t sC,
-                                            int tiles_n, u32x4 *__restrict__ Pout, const int32_t *__restrict__ amap) {
+                                            int tiles_n, u32x4 *__restrict__ Pout, const int32_t *__restrict__ amap,
+                                            HeadsArg hd) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -471,6 +482,58 @@ __device__ __forceinline__ void h3_ntp_body(const float *__restrict__ A, const u
 
     const float inv = pow2f(-eA), invB = pow2f(-eB);
     float *Ct = C + t * sC;
+    if constexpr (EPI == 2) {
+        // per i: the 16 rows x 4 head outputs of this lane's two columns, then a reduce-scatter over the 32 column
+        // lanes of the half-wave (xor 16 .. 1, each step keeping the half of the values its lane bit selects): lane fr
+        // ends with output o = fr >> 3 of rows r = 2 (fr & 7) + k, k < 2, summed over the wave's WTN columns
+        static_assert(TN == 2 && WTN == 64, "heads epilogue: a wave tile 64 columns wide");
+        const float *hw = t == 0 ? hd.w0 : hd.w1;
+        const int nh = t == 0 ? hd.na : 1;
+        float wv[4][TN], bv[TN];
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int col = n0 + wn * WTN + j * 32 + fr;
+            bv[j] = bias[(int64_t)t * N + col];
+#pragma unroll
+            for (int o = 0; o < 4; o++) wv[o][j] = o < nh ? hw[(int64_t)o * N + col] : 0.0f;
+        }
+        float *part = hd.part + ((int64_t)(t * tiles_n + tn) * WGN + wn) * M * 4;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            float pv[64];  // [o][r]
+#pragma unroll
+            for (int q = 0; q < 64; q++) pv[q] = 0.0f;
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                const int col = n0 + wn * WTN + j * 32 + fr;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                    const float v = relu_nan((hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB + bv[j]);
+                    if (row < M) Ct[row * N + col] = v;
+#pragma unroll
+                    for (int o = 0; o < 4; o++) pv[o * 16 + r] += v * wv[o][j];
+                }
+            }
+#pragma unroll
+            for (int c = 64, off = 16; off >= 1; c >>= 1, off >>= 1) {
+                const bool up = (fr & off) != 0;
+#pragma unroll
+                for (int k = 0; k < c / 2; k++) {
+                    const float send = up ? pv[k] : pv[k + c / 2], keep = up ? pv[k + c / 2] : pv[k];
+                    pv[k] = keep + __shfl_xor(send, off);
+                }
+            }
+            const int o = fr >> 3;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int r = 2 * (fr & 7) + k;
+                const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (row < M) part[row * 4 + o] = pv[k];
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < TN; j++) {
         const int col = n0 + wn * WTN + j * 32 + fr;
@@ -495,8 +558,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
                                                            const uint32_t *__restrict__ amaxB, int64_t M, int N,
                                                            int K, int64_t sA, int64_t sB,
                                                            const float *__restrict__ bias, float *__restrict__ C,
-                                                           int64_t sC, int tiles_n, u32x4 *__restrict__ Pout) {
-    h3_ntp_body<BM, BN, WGM, WGN, EPI, false>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, Pout, nullptr);
+                                                           int64_t sC, int tiles_n, u32x4 *__restrict__ Pout,
+                                                           HeadsArg hd) {
+    h3_ntp_body<BM, BN, WGM, WGN, EPI, false>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, Pout, nullptr,
+                                              hd);
 }
 template <int BM, int BN, int WGM, int WGN, int EPI>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntpg(const float *__restrict__ A, const u32x4 *__restrict__ B,
@@ -504,8 +569,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntpg(const float *__restr
                                                             const uint32_t *__restrict__ amaxB, int64_t M, int N,
                                                             int K, int64_t sA, int64_t sB,
                                                             const float *__restrict__ bias, float *__restrict__ C,
-                                                            int64_t sC, int tiles_n, const int32_t *__restrict__ amap) {
-    h3_ntp_body<BM, BN, WGM, WGN, EPI, true>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, nullptr, amap);
+                                                            int64_t sC, int tiles_n, const int32_t *__restrict__ amap,
+                                                            HeadsArg hd) {
+    h3_ntp_body<BM, BN, WGM, WGN, EPI, true>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, nullptr, amap,
+                                             hd);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1331,30 +1398,46 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tnq(const u32x4 *__restri
 template <int BM, int BN, int WGM, int WGN, bool PIPE>
 hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
-                     const int32_t *amap, hipStream_t s) {
+                     const int32_t *amap, const HeadsArg &hd, hipStream_t s) {
     if (N % BN || (PIPE && K < 2 * BK)) return hipErrorInvalidValue;
     if ((int64_t)N * (K / 8) * 2 > INT32_MAX) return hipErrorInvalidValue;  // 32-bit B chunk offsets
     const int64_t tiles_m = (M + BM - 1) / BM;
     const int tiles_n = N / BN;
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
+    if (hd.part) {  // heads in the epilogue: the pipelined kernel with bias + ReLU, both towers, 64-column wave tiles
+        if constexpr (!PIPE || BN / WGN != 64) {
+            return hipErrorInvalidValue;
+        } else {
+            if (!bias || T != 2 || Pout || hd.na < 1 || hd.na > 4 || !hd.w0 || !hd.w1) return hipErrorInvalidValue;
+            if (amap) {
+                if (K % 64 || K > 64 * GA_CHUNKS) return hipErrorInvalidValue;
+                hipLaunchKernelGGL((k_h3_ntpg<BM, BN, WGM, WGN, 2>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K,
+                                   sA, sB, bias, C, sC, tiles_n, amap, hd);
+            } else {
+                hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 2>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
+                                   sB, bias, C, sC, tiles_n, nullptr, hd);
+            }
+            return hipGetLastError();
+        }
+    }
     if (amap) {  // gathered A rows: the pipelined kernel only, no plane output
         if (!PIPE || Pout || K % 64 || K > 64 * GA_CHUNKS) return hipErrorInvalidValue;
         if (bias)
             hipLaunchKernelGGL((k_h3_ntpg<BM, BN, WGM, WGN, 1>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
-                               sB, bias, C, sC, tiles_n, amap);
+                               sB, bias, C, sC, tiles_n, amap, hd);
         else
             hipLaunchKernelGGL((k_h3_ntpg<BM, BN, WGM, WGN, 0>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
-                               sB, nullptr, C, sC, tiles_n, amap);
+                               sB, nullptr, C, sC, tiles_n, amap, hd);
         return hipGetLastError();
     }
     if (PIPE) {
         if (bias)
             hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 1>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
-                               bias, C, sC, tiles_n, Pout);
+                               bias, C, sC, tiles_n, Pout, hd);
         else
             hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 0>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
-                               nullptr, C, sC, tiles_n, Pout);
+                               nullptr, C, sC, tiles_n, Pout, hd);
     } else {
         if (bias)
             hipLaunchKernelGGL((k_h3_nt<BM, BN, WGM, WGN, 1>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
@@ -1450,14 +1533,16 @@ hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *ama
 
 hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
-                             int64_t c_stride, void *a_planes, int cfg, hipStream_t s, const int32_t *a_rows) {
+                             int64_t c_stride, void *a_planes, int cfg, hipStream_t s, const int32_t *a_rows,
+                             const float *head_w0, int n_actions, const float *head_w1, float *head_part) {
+    const HeadsArg hd{head_w0, head_w1, n_actions, head_part};
     if (M <= 0) return hipSuccess;
     if (K % BK || N <= 0 || a_stride % 4 || b_stride % 8) return hipErrorInvalidValue;
     const u32x4 *b = static_cast<const u32x4 *>(B);
     u32x4 *P = static_cast<u32x4 *>(a_planes);
     const int64_t sB = b_stride / 8 * 2;  // chunks
 #define H3_NT(BM, BN, WM, WN, PIPE) \
-    nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, s)
+    nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, hd, s)
     switch (cfg) {
         case 0: return H3_NT(256, 128, 4, 2, false);
         case 1: return H3_NT(128, 192, 4, 2, false);
@@ -1472,7 +1557,7 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
 #undef H3_NT
         // k_h3_ntg: both operands staged by LDS-DMA, three k steps deep
 #define H3_NTG(BM, BN, WM, WN, KP) \
-    (a_rows ? hipErrorInvalidValue                                                                 \
+    ((a_rows || head_part) ? hipErrorInvalidValue                                                  \
             : ntg_launch<BM, BN, WM, WN, KP>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s))
         case 20: return H3_NTG(256, 128, 4, 2, false);
         case 21: return H3_NTG(128, 192, 4, 2, false);
@@ -1514,6 +1599,48 @@ hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B
 #undef H3_TN
     if (e != hipSuccess) return e;
     return launch_x6_fold(slab, S, total, out, s);
+}
+
+namespace {
+// logits[r][a] = sum over p < P of part[0][p][r][a] (a < na), value[r] = sum over p of part[1][p][r][0]: the heads'
+// partials of the forward GEMM's epilogue (EPI 2) added in partial order (no biases: the loss adds them)
+__global__ __launch_bounds__(256) void k_heads_combine(const float4 *__restrict__ part, int P, int64_t M, int na,
+                                                       float *__restrict__ logits, float *__restrict__ value) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= M) return;
+    float4 a = part[r], v = part[(int64_t)P * M + r];
+    for (int p = 1; p < P; p++) {
+        const float4 x = part[(int64_t)p * M + r], y = part[(int64_t)(P + p) * M + r];
+        a.x += x.x;
+        a.y += x.y;
+        a.z += x.z;
+        a.w += x.w;
+        v.x += y.x;
+    }
+    const float av[4] = {a.x, a.y, a.z, a.w};
+    for (int o = 0; o < na; o++) logits[r * na + o] = av[o];
+    value[r] = v.x;
+}
+}  // namespace
+
+// partials per row of the heads epilogue: tiles_n * WGN of the configuration (0 if it has none)
+int h3_heads_parts(int N, int cfg) {
+    switch (cfg) {
+        case 10: return N % 128 ? 0 : N / 128 * 2;
+        // cfg 11: 96-column wave tiles, no heads epilogue
+        case 12: return N % 128 ? 0 : N / 128 * 2;
+        case 13: return N % 256 ? 0 : N / 256 * 4;
+        default: return 0;
+    }
+}
+
+hipError_t launch_heads_combine(const float *part, int P, int64_t M, int na, float *logits, float *value,
+                                hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    if (P < 1 || na < 1 || na > 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_heads_combine, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(part), P, M, na, logits, value);
+    return hipGetLastError();
 }
 
 }  // namespace merlin

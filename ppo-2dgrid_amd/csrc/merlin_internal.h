@@ -194,7 +194,14 @@ hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *ama
 hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
                              int64_t c_stride, void *a_planes, int cfg, hipStream_t s,
-                             const int32_t *a_rows = nullptr);
+                             const int32_t *a_rows = nullptr, const float *head_w0 = nullptr, int n_actions = 0,
+                             const float *head_w1 = nullptr, float *head_part = nullptr);
+// head_part (nullable; pipelined cfgs 10 / 12 / 13 with bias, 2 towers): the heads' dot products of h folded into the
+// forward GEMM's epilogue, h3_heads_parts(N, cfg) float4 partials per row and tower, [2][parts][M][4]; summed by
+// launch_heads_combine into logits [M][n_actions] and value [M]
+int h3_heads_parts(int N, int cfg);
+hipError_t launch_heads_combine(const float *part, int P, int64_t M, int na, float *logits, float *value,
+                                hipStream_t s);
 // planes: A and B are plane images (an NT's a_planes) instead of fp32 tensors
 // a_rows / b_rows (nullable): the operand's rows gathered by 64-value chunks -- row r's chunk j is row
 // rows[r * (K or N) / 64 + j] of the operand seen as [*][64] (k_h3_ntp GA, k_h3_tn GB; pipelined NT cfgs and TN

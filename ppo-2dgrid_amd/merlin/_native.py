@@ -137,6 +137,11 @@ def lib():
     L.merlin_h3_gemm_tn_planes.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
     L.merlin_h3_gemm_nt_gather.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, vp, i32, vp]
     L.merlin_h3_gemm_tn_gather.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, vp, i32, vp]
+    L.merlin_h3_gemm_nt_heads.argtypes = [vp, vp, vp, vp, i64, i32, i32, i64, i64, vp, vp, i64, vp, vp, i32, vp, vp,
+                                          i32, vp]
+    L.merlin_h3_heads_parts.argtypes = [i32, i32]
+    L.merlin_h3_heads_parts.restype = i32
+    L.merlin_heads_combine.argtypes = [vp, i32, i64, i32, vp, vp, vp]
     L.merlin_stage_tables_fwd.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_stage_tables_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     check_env_config_layout(L)
@@ -183,6 +188,7 @@ EXPORTED_SYMBOLS = (
     "merlin_clip_adam_workspace", "merlin_clip_adam",
     "merlin_h3_amax", "merlin_h3_split", "merlin_h3_gemm_nt", "merlin_h3_gemm_tn",
     "merlin_h3_gemm_tn_planes", "merlin_h3_gemm_nt_gather", "merlin_h3_gemm_tn_gather",
+    "merlin_h3_gemm_nt_heads", "merlin_h3_heads_parts", "merlin_heads_combine",
 )
 
 
@@ -916,6 +922,9 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
 # profiles keep the two apart); qwin / qwin_dgrad: the update's window GEMMs (N = 576, K = 64 / N = 64, K = 576)
 H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 1, "qwin": 11, "qwin_dgrad": 5}
 H3_TN_CFG = 0
+# the update's fc1 forward (h3, cfg "fwd" with a heads epilogue) computes the policy / value heads in its epilogue
+# (merlin_h3_gemm_nt_heads + merlin_heads_combine) instead of a pass over h (merlin_heads_fwd)
+H3_HEADS_EPILOGUE = True
 H3_TN_CFG_WIN = 2  # the window weight gradient (M = 64)
 H3_TN_SPLITS = 32
 
@@ -987,6 +996,36 @@ def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
                                       ptr(planes_out) if planes_out is not None else None, int(cfg),
                                       stream_of(A)), "merlin_h3_gemm_nt")
     return out
+
+
+def h3_gemm_nt_heads(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor, bias: torch.Tensor,
+                     Wa: torch.Tensor, Wc: torch.Tensor, cfg: int, rows: torch.Tensor | None = None,
+                     name: str = "h3_gemm_nt") -> tuple:
+    """(h, logits, value): h = relu(A @ B^T + bias) per tower as h3_gemm_nt (A f32[2, M, K], B planes), with the heads
+    logits [M, A] = h[0] Wa^T and value [M] = h[1] wc (no biases) from partial dot products made in the GEMM's
+    epilogue (merlin_h3_gemm_nt_heads) and summed in order (merlin_heads_combine, span "k_heads_fwd")."""
+    T, M, K = (int(v) for v in A.shape)
+    N = int(B.shape[1])
+    NA = int(Wa.shape[0])
+    assert T == 2 and A.dtype == torch.float32 and B.dtype == torch.int16 and B.shape == (T, N, 2 * K)
+    assert A.is_contiguous() and B.is_contiguous() and bias.shape == (T, N) and bias.is_contiguous()
+    assert Wa.shape == (NA, N) and Wa.is_contiguous() and Wc.numel() == N and Wc.is_contiguous() and 1 <= NA <= 4
+    P = int(lib().merlin_h3_heads_parts(N, int(cfg)))
+    assert P > 0, f"cfg {cfg}: no heads epilogue"
+    if rows is not None:
+        assert rows.dtype == torch.int32 and rows.is_contiguous() and rows.numel() == M * K // 64
+    out = torch.empty((T, M, N), dtype=torch.float32, device=A.device)
+    part = torch.empty((T, P, M, 4), dtype=torch.float32, device=A.device)
+    with KernelTimer.span(name, 0, 2 * T * M * N * K):
+        check(lib().merlin_h3_gemm_nt_heads(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, M * K, N * K, ptr(bias),
+                                            ptr(out), M * N, ptr(rows), ptr(Wa), NA, ptr(Wc), ptr(part), int(cfg),
+                                            stream_of(A)), "merlin_h3_gemm_nt_heads")
+    logits = torch.empty((M, NA), dtype=torch.float32, device=A.device)
+    value = torch.empty(M, dtype=torch.float32, device=A.device)
+    with KernelTimer.span("k_heads_fwd", T * P * M * 16 + M * (NA + 1) * 4):
+        check(lib().merlin_heads_combine(ptr(part), P, M, NA, ptr(logits), ptr(value), stream_of(A)),
+              "merlin_heads_combine")
+    return out, logits, value
 
 
 def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,

@@ -314,11 +314,18 @@ class WindowStep:
             # gradient, which then stages copies instead of splitting both operands again
             if WGRAD_PLANES and not split_side:
                 pa3 = torch.empty((2, n, 1152), dtype=torch.int16, device=a3.device)
-            h = nat.h3_gemm_nt(a3, am3, P4, amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd",
-                               planes_out=pa3, rows=arows)
+            if (pa3 is None and nat.H3_HEADS_EPILOGUE
+                    and nat.lib().merlin_h3_heads_parts(P4.shape[1], nat.H3_NT_CFG["fwd"]) > 0):
+                # both heads in the GEMM's epilogue (the loss adds their biases)
+                h, logits, value = nat.h3_gemm_nt_heads(a3, am3, P4, amW, b4, Wa, Wc, cfg=nat.H3_NT_CFG["fwd"],
+                                                        rows=arows, name="gemm_fc1_fwd")
+            else:
+                h = nat.h3_gemm_nt(a3, am3, P4, amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd",
+                                   planes_out=pa3, rows=arows)
+                logits, value = nat.heads_fwd(h, Wa, Wc)  # both heads in one pass over h (the loss adds the biases)
         else:
             h = nat.x6_gemm_nt(a3, P4, bias=b4, cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
-        logits, value = nat.heads_fwd(h, Wa, Wc)  # both heads in one pass over h (the loss adds their biases)
+            logits, value = nat.heads_fwd(h, Wa, Wc)  # both heads in one pass over h (the loss adds their biases)
         # ---- loss and its gradient per frame (merlin.ppo._PPOLoss); the head-bias gradients land in .grad
         _, dlogits, dvalue, _, _ = nat.ppo_loss(
             logits, value, mb.offs, mb.order, mb.inv, mb_idx, actions, logp_old, adv, ret, ag.clip_eps, ag.vf_coef,

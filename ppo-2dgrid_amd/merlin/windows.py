@@ -601,8 +601,19 @@ class _WindowTowerHeadX6(torch.autograd.Function):
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
         fc1 = _Fc1(impl, W4p)
-        h = fc1.fwd(a3, b4.detach(), am[0:2] if am is not None else None)
-        logits, value = nat.heads_fwd(h, Wa, Wc, ba, bc)  # both heads in one pass over h
+        if impl == "h3" and nat.H3_HEADS_EPILOGUE and nat.lib().merlin_h3_heads_parts(W4p.shape[1],
+                                                                                        nat.H3_NT_CFG["fwd"]) > 0:
+            # both heads in the forward GEMM's epilogue (merlin_h3_gemm_nt_heads), biases added after the sums
+            h, logits, value = nat.h3_gemm_nt_heads(a3, am[0:2], fc1.P, fc1.amW, b4.detach().contiguous(),
+                                                    Wa.detach().contiguous(), Wc.detach().contiguous(),
+                                                    cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd")
+            if ba is not None:
+                logits = logits + ba.detach()
+            if bc is not None:
+                value = value + bc.detach()
+        else:
+            h = fc1.fwd(a3, b4.detach(), am[0:2] if am is not None else None)
+            logits, value = nat.heads_fwd(h, Wa, Wc, ba, bc)  # both heads in one pass over h
         ctx.save_for_backward(a3, bits, W4p, h, Wa, Wc)
         ctx.fc1, ctx.am = fc1, am
         ctx.head_bias = (ba is not None, bc is not None)

@@ -171,3 +171,40 @@ def test_gemm_tn_gather_rows_bitwise(device, Kd, splits, cfg):
     ref = nat.h3_gemm_tn(dz, amz, ad, am3, splits=splits, cfg=cfg)
     got = nat.h3_gemm_tn(dz, amz, a3, am3, splits=splits, cfg=cfg, rows=rows)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("cfg,gather", [(13, False), (13, True), (12, False), (10, True)])
+def test_gemm_nt_heads_epilogue(device, cfg, gather):
+    """merlin_h3_gemm_nt_heads (the policy / value heads folded into the forward GEMM's epilogue): h bit for bit as
+    the plain bias + ReLU GEMM, logits / value against a float64 product of that h with the head weights (error no
+    larger than merlin_heads_fwd's, which sums the same products in another order); ragged rows, 3 actions."""
+    from merlin import _native as nat
+
+    M, K, N = 1000, 576, 512
+    A, B = _operands(device, M, N, K, 77 + cfg, ragged=True)
+    g = torch.Generator(device=device).manual_seed(cfg)
+    rows = None
+    if gather:
+        nc = M * K // 64
+        rows = torch.randint(0, nc, (nc,), device=device, generator=g, dtype=torch.int32)
+        A_eff = A.view(2, nc, 64)[:, rows.long()].reshape(2, M, K).contiguous()
+    else:
+        A_eff = A
+    amA, amB = nat.h3_amax(A_eff), nat.h3_amax(B)
+    Bp = nat.h3_split(B, amB)
+    bias = torch.randn(2, N, device=device, generator=g)
+    Wa = torch.randn(3, N, device=device, generator=g) / N ** 0.5
+    Wc = torch.randn(1, N, device=device, generator=g) / N ** 0.5
+    h_ref = nat.h3_gemm_nt(A_eff, amA, Bp, amB, bias=bias, cfg=cfg)
+    h, logits, value = nat.h3_gemm_nt_heads(A, amA, Bp, amB, bias, Wa, Wc, cfg=cfg, rows=rows)
+    assert torch.equal(h, h_ref)
+    l64 = h_ref[0].double() @ Wa.double().T
+    v64 = h_ref[1].double() @ Wc.double().view(-1)
+    lf, vf = nat.heads_fwd(h_ref, Wa, Wc)
+    den_l = h_ref[0].double().abs() @ Wa.double().abs().T
+    den_v = h_ref[1].double().abs() @ Wc.double().abs().view(-1)
+    assert _err(logits, l64, den_l) <= max(2 * _err(lf, l64, den_l), 2.0 ** -20)
+    assert _err(value, v64, den_v) <= max(2 * _err(vf, v64, den_v), 2.0 ** -20)
+    # fixed order: the same bits again
+    h2, logits2, value2 = nat.h3_gemm_nt_heads(A, amA, Bp, amB, bias, Wa, Wc, cfg=cfg, rows=rows)
+    assert torch.equal(logits2, logits) and torch.equal(value2, value) and torch.equal(h2, h)
