@@ -322,8 +322,11 @@ def h3_gemm_names(nat):
     reuse's gathered rows, of conv3 and the weight gradient)."""
     from merlin import fast_step as FS
 
-    fwd = H3_NT_NAMES.get(nat.H3_NT_CFG["fwd"], "?").format(1)
+    heads = nat.H3_HEADS_EPILOGUE and nat.lib().merlin_h3_heads_parts(512, nat.H3_NT_CFG["fwd"]) > 0
+    fwd = H3_NT_NAMES.get(nat.H3_NT_CFG["fwd"], "?").format(2 if heads else 1)  # EPI 2: the heads in the epilogue
     out = {"gemm_fc1_dgrad": (H3_NT_NAMES.get(nat.H3_NT_CFG["dgrad"], "?").format(0),)}
+    if heads:
+        out["k_heads_fwd"] = ("k_heads_combine",)
     if FS.PATCH_REUSE == "gather":
         return {**out, **PMC_ALIAS_GATHER, "gemm_fc1_fwd": (fwd.replace("k_h3_ntp<", "k_h3_ntpg<"),)}
     return {**out, "gemm_fc1_fwd": (fwd,)}
