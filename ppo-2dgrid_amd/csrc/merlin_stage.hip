@@ -46,12 +46,24 @@ __device__ void load_w2_slice(const float *__restrict__ W2, int p, float *__rest
     }
 }
 
+// W2[t] slice of type p into LDS as [j][o][co] (co fastest, rows padded to WSP words): the forward's T2 loop has
+// consecutive threads on consecutive co (in load_w2_slice's [co][j][o] layout they read 128 words apart: one bank,
+// 64-way conflicts); the padding keeps the stores (consecutive o) on distinct banks too
+constexpr int WSP = C2 + 1;
+__device__ void load_w2_slice_co(const float *__restrict__ W2, int p, float *__restrict__ Ws) {
+    const int yp = p >> 1, xp = p & 1;
+    for (int q = threadIdx.x; q < C2 * 4 * C1; q += blockDim.x) {  // o fastest: W2 read 64 B apart
+        const int co = q / (4 * C1), r = q - co * 4 * C1, j = r / C1, o = r - j * C1;
+        Ws[(j * C1 + o) * WSP + co] = W2[((size_t)co * C1 + o) * 16 + (2 * (j >> 1) + yp) * 4 + 2 * (j & 1) + xp];
+    }
+}
+
 // grid (NCH, T): HT rows of one chunk and their T2 rows; HT saved for the backward
 __global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1, const float *__restrict__ b1,
                                                    const float *__restrict__ W2, const float *__restrict__ atlas,
                                                    const int16_t *__restrict__ idx, float *__restrict__ HT,
                                                    float *__restrict__ T2) {
-    __shared__ float Wl[C1 * 3 * 64], Al[5 * 3 * 64], H[VB][C1], Ws[C2 * 4 * C1];
+    __shared__ float Wl[C1 * 3 * 64], Al[5 * 3 * 64], H[VB][C1], Ws[4 * C1 * WSP];
     __shared__ double P[C1 * 80];
     const int t = blockIdx.y;
     int p, v0, nv;
@@ -59,7 +71,7 @@ __global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1,
     W1 += (size_t)t * C1 * 3 * 64;
     for (int q = threadIdx.x; q < C1 * 3 * 64; q += 256) Wl[q] = W1[q];
     for (int q = threadIdx.x; q < 5 * 3 * 64; q += 256) Al[q] = atlas[q];
-    load_w2_slice(W2 + (size_t)t * C2 * C1 * 16, p, Ws);
+    load_w2_slice_co(W2 + (size_t)t * C2 * C1 * 16, p, Ws);
     __syncthreads();
     for (int q = threadIdx.x; q < C1 * 80; q += 256) {  // P[o][k], 48 products each
         const int o = q / 80, k = q - o * 80;
@@ -91,10 +103,10 @@ __global__ __launch_bounds__(256) void k_stage_fwd(const float *__restrict__ W1,
     __syncthreads();
     for (int q = threadIdx.x; q < nv * 4 * C2; q += 256) {  // T2 rows 4 v + j
         const int vl = q / (4 * C2), r = q - vl * 4 * C2, j = r / C2, co = r - j * C2;
-        const float *w = Ws + (co * 4 + j) * C1;
+        const float *w = Ws + j * C1 * WSP + co;
         double acc = 0.0;
 #pragma unroll 8
-        for (int o = 0; o < C1; o++) acc += (double)H[vl][o] * (double)w[o];
+        for (int o = 0; o < C1; o++) acc += (double)H[vl][o] * (double)w[o * WSP];
         T2[((size_t)t * NROW + 4 * (v0 + vl) + j) * C2 + co] = (float)acc;
     }
 }
