@@ -517,13 +517,20 @@ int merlin_h3_gemm_nt_gather(const float *A_dev, const uint32_t *amax_a_dev, con
  *          gemm_nt_gather) with the policy / value heads (src/actor_critic.py:41-46) folded into the epilogue: per
  *          row, merlin_h3_heads_parts(N, cfg) partial dot products of h with head_w0 [n_actions][N] (tower 0, the
  *          actor; n_actions <= 4) and head_w1 [N] (tower 1, the critic), head_partials_dev float
- *          [2][parts][M][4]; merlin_heads_combine sums them in order: logits [M][n_actions], value [M] (no biases). */
+ *          [2][parts][M][4]; merlin_heads_combine sums them in order: logits [M][n_actions], value [M] (no biases).
+ *          C_dev may be NULL (towers' h not written; merlin_act_draw then finishes the acting step). */
 int merlin_h3_gemm_nt_heads(const float *A_dev, const uint32_t *amax_a_dev, const void *B_dev,
                             const uint32_t *amax_b_dev, int64_t M, int32_t N, int32_t K, int64_t a_stride,
                             int64_t b_stride, const float *bias_dev, float *C_dev, int64_t c_stride,
                             const int32_t *a_rows_dev, const float *head_w0_dev, int32_t n_actions,
                             const float *head_w1_dev, float *head_partials_dev, int32_t cfg, void *stream);
 int32_t merlin_h3_heads_parts(int32_t N, int32_t cfg);
+/* The acting tail (merlin_act_heads' log-softmax, argmax or draw, action / logp / value) from the partials of a
+ * merlin_h3_gemm_nt_heads call with C_dev = NULL (the acting path: h itself is never written), biases added here. */
+int merlin_act_draw(const float *partials_dev, int32_t parts, int64_t n, const float *b_actor_dev,
+                    const float *b_critic_dev, int32_t n_actions, int32_t deterministic, uint64_t seed,
+                    const int64_t *epoch_dev, int64_t step, int64_t env_offset, int64_t *action_dev, float *logp_dev,
+                    float *value_dev, void *stream);
 int merlin_heads_combine(const float *partials_dev, int32_t parts, int64_t M, int32_t n_actions, float *logits_dev,
                          float *value_dev, void *stream);
 int merlin_h3_gemm_tn_gather(const float *A_dev, const uint32_t *amax_a_dev, const float *B_dev,

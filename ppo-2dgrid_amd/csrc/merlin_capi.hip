@@ -920,7 +920,7 @@ static int h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, con
                       const float *head_w0 = nullptr, int32_t n_actions = 0, const float *head_w1 = nullptr,
                       float *head_part = nullptr) {
     if (M < 0 || N <= 0 || K <= 0) return fail(MERLIN_E_INVALID, "bad shape");
-    if (M > 0 && (!A || !B || !C || !amax_a || !amax_b)) return fail(MERLIN_E_INVALID, "null argument");
+    if (M > 0 && (!A || !B || (!C && !head_part) || !amax_a || !amax_b)) return fail(MERLIN_E_INVALID, "null argument");
     if (K % 32) return fail(MERLIN_E_UNSUPPORTED, "K must be a multiple of 32");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (a_stride % 4 || b_stride % 8) return fail(MERLIN_E_INVALID, "tower strides: A multiple of 4, B of 8");
@@ -985,6 +985,17 @@ int merlin_h3_gemm_nt_heads(const float *A, const uint32_t *amax_a, const void *
 }
 
 int32_t merlin_h3_heads_parts(int32_t N, int32_t cfg) { return merlin::h3_heads_parts(N, cfg); }
+
+int merlin_act_draw(const float *partials, int32_t parts, int64_t n, const float *b_actor, const float *b_critic,
+                    int32_t n_actions, int32_t deterministic, uint64_t seed, const int64_t *epoch, int64_t step,
+                    int64_t env_offset, int64_t *action, float *logp, float *value, void *stream) {
+    if (n < 0 || parts < 1 || n_actions < 1 || n_actions > 4) return fail(MERLIN_E_INVALID, "bad shape");
+    if (n > 0 && (!partials || !b_actor || !b_critic || !action || !logp || !value))
+        return fail(MERLIN_E_INVALID, "null argument");
+    HIP_TRY(merlin::launch_act_draw(partials, parts, n, b_actor, b_critic, n_actions, deterministic, seed, epoch, step,
+                                    env_offset, action, logp, value, (hipStream_t)stream));
+    return MERLIN_OK;
+}
 
 int merlin_heads_combine(const float *partials, int32_t parts, int64_t M, int32_t n_actions, float *logits,
                          float *value, void *stream) {

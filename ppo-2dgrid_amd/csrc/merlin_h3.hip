@@ -482,7 +482,7 @@ __device__ __forceinline__ void h3_ntp_body(const float *__restrict__ A, const u
 
     const float inv = pow2f(-eA), invB = pow2f(-eB);
     float *Ct = C + t * sC;
-    if constexpr (EPI == 2) {
+    if constexpr (EPI >= 2) {  // EPI 3: the heads only (the acting path: h itself is not needed)
         // per i: the 16 rows x 4 head outputs of this lane's two columns, then a reduce-scatter over the 32 column
         // lanes of the half-wave (xor 16 .. 1, each step keeping the half of the values its lane bit selects): lane fr
         // ends with output o = fr >> 3 of rows r = 2 (fr & 7) + k, k < 2, summed over the wave's WTN columns
@@ -510,7 +510,7 @@ __device__ __forceinline__ void h3_ntp_body(const float *__restrict__ A, const u
                 for (int r = 0; r < 16; r++) {
                     const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
                     const float v = relu_nan((hi[i][j][r] + lo[i][j][r] * LO_INV) * inv * invB + bv[j]);
-                    if (row < M) Ct[row * N + col] = v;
+                    if (EPI == 2 && row < M) Ct[row * N + col] = v;
 #pragma unroll
                     for (int o = 0; o < 4; o++) pv[o * 16 + r] += v * wv[o][j];
                 }
@@ -1411,12 +1411,15 @@ hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, cons
         } else {
             if (!bias || T != 2 || Pout || hd.na < 1 || hd.na > 4 || !hd.w0 || !hd.w1) return hipErrorInvalidValue;
             if (amap) {
-                if (K % 64 || K > 64 * GA_CHUNKS) return hipErrorInvalidValue;
+                if (K % 64 || K > 64 * GA_CHUNKS || !C) return hipErrorInvalidValue;
                 hipLaunchKernelGGL((k_h3_ntpg<BM, BN, WGM, WGN, 2>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K,
                                    sA, sB, bias, C, sC, tiles_n, amap, hd);
-            } else {
+            } else if (C) {
                 hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 2>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
                                    sB, bias, C, sC, tiles_n, nullptr, hd);
+            } else {  // heads only
+                hipLaunchKernelGGL((k_h3_ntp<BM, BN, WGM, WGN, 3>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
+                                   sB, bias, nullptr, sC, tiles_n, nullptr, hd);
             }
             return hipGetLastError();
         }

@@ -112,6 +112,10 @@ hipError_t launch_act_heads(const float *z, const float *b4, int64_t n, int H, c
                             const float *wc, const float *bc, int A, int det, uint64_t seed, const int64_t *epoch,
                             int64_t step, int64_t env_offset, int64_t *action, float *logp, float *value,
                             hipStream_t s);
+// the acting tail from the heads' partials of the acting GEMM's epilogue (merlin_h3.hip EPI 3), part [2][P][n][4]
+hipError_t launch_act_draw(const float *part, int P, int64_t n, const float *ba, const float *bc, int A, int det,
+                           uint64_t seed, const int64_t *epoch, int64_t step, int64_t env_offset, int64_t *action,
+                           float *logp, float *value, hipStream_t s);
 int64_t ppo_loss_workspace_doubles(int64_t n_samples);
 hipError_t launch_ppo_loss(const float *logits, const float *value, const float *bias_a, const float *bias_c,
                            int64_t U, int A, const int32_t *offs, const int32_t *order, const int64_t *inv, int64_t n,

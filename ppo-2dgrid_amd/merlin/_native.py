@@ -142,6 +142,7 @@ def lib():
     L.merlin_h3_heads_parts.argtypes = [i32, i32]
     L.merlin_h3_heads_parts.restype = i32
     L.merlin_heads_combine.argtypes = [vp, i32, i64, i32, vp, vp, vp]
+    L.merlin_act_draw.argtypes = [vp, i32, i64, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp, vp]
     L.merlin_stage_tables_fwd.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_stage_tables_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     check_env_config_layout(L)
@@ -188,7 +189,7 @@ EXPORTED_SYMBOLS = (
     "merlin_clip_adam_workspace", "merlin_clip_adam",
     "merlin_h3_amax", "merlin_h3_split", "merlin_h3_gemm_nt", "merlin_h3_gemm_tn",
     "merlin_h3_gemm_tn_planes", "merlin_h3_gemm_nt_gather", "merlin_h3_gemm_tn_gather",
-    "merlin_h3_gemm_nt_heads", "merlin_h3_heads_parts", "merlin_heads_combine",
+    "merlin_h3_gemm_nt_heads", "merlin_h3_heads_parts", "merlin_heads_combine", "merlin_act_draw",
 )
 
 
@@ -1000,10 +1001,12 @@ def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
 
 def h3_gemm_nt_heads(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor, bias: torch.Tensor,
                      Wa: torch.Tensor, Wc: torch.Tensor, cfg: int, rows: torch.Tensor | None = None,
-                     name: str = "h3_gemm_nt") -> tuple:
+                     name: str = "h3_gemm_nt", partials_only: bool = False) -> tuple:
     """(h, logits, value): h = relu(A @ B^T + bias) per tower as h3_gemm_nt (A f32[2, M, K], B planes), with the heads
     logits [M, A] = h[0] Wa^T and value [M] = h[1] wc (no biases) from partial dot products made in the GEMM's
-    epilogue (merlin_h3_gemm_nt_heads) and summed in order (merlin_heads_combine, span "k_heads_fwd")."""
+    epilogue (merlin_h3_gemm_nt_heads) and summed in order (merlin_heads_combine, span "k_heads_fwd").
+    partials_only: h is not written and the heads' partials float[2, parts, M, 4] are returned as they are (for
+    act_draw)."""
     T, M, K = (int(v) for v in A.shape)
     N = int(B.shape[1])
     NA = int(Wa.shape[0])
@@ -1014,18 +1017,42 @@ def h3_gemm_nt_heads(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amax
     assert P > 0, f"cfg {cfg}: no heads epilogue"
     if rows is not None:
         assert rows.dtype == torch.int32 and rows.is_contiguous() and rows.numel() == M * K // 64
-    out = torch.empty((T, M, N), dtype=torch.float32, device=A.device)
+    out = None if partials_only else torch.empty((T, M, N), dtype=torch.float32, device=A.device)
     part = torch.empty((T, P, M, 4), dtype=torch.float32, device=A.device)
     with KernelTimer.span(name, 0, 2 * T * M * N * K):
         check(lib().merlin_h3_gemm_nt_heads(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, M * K, N * K, ptr(bias),
                                             ptr(out), M * N, ptr(rows), ptr(Wa), NA, ptr(Wc), ptr(part), int(cfg),
                                             stream_of(A)), "merlin_h3_gemm_nt_heads")
+    if partials_only:
+        return part
     logits = torch.empty((M, NA), dtype=torch.float32, device=A.device)
     value = torch.empty(M, dtype=torch.float32, device=A.device)
     with KernelTimer.span("k_heads_fwd", T * P * M * 16 + M * (NA + 1) * 4):
         check(lib().merlin_heads_combine(ptr(part), P, M, NA, ptr(logits), ptr(value), stream_of(A)),
               "merlin_heads_combine")
     return out, logits, value
+
+
+def act_draw(part, b_actor, b_critic, deterministic=False, seed=0, epoch=None, step=0, out=None, env_offset=0):
+    """act_heads' tail (log-softmax, argmax or the counter-keyed draw; action / logp / value) from the heads' partials
+    of h3_gemm_nt_heads(partials_only=True): part f32[2, P, n, 4] summed in order, the biases added here."""
+    T, P, n, _ = (int(x) for x in part.shape)
+    A = int(b_actor.numel())
+    assert T == 2 and part.dtype == torch.float32 and part.is_contiguous() and 1 <= A <= 4 and b_critic.numel() == 1
+    if not deterministic and epoch is None:
+        raise ValueError("act_draw: a sampled action needs an epoch counter tensor (int64[1] on the device)")
+    dev = part.device
+    if out is None:
+        out = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.float32, device=dev),
+               torch.empty(n, dtype=torch.float32, device=dev))
+    action, logp, value = out
+    assert action.dtype == torch.int64 and logp.dtype == value.dtype == torch.float32
+    assert action.numel() == logp.numel() == value.numel() == n
+    with KernelTimer.span("k_act_heads", part.numel() * 4 + n * 16):
+        check(lib().merlin_act_draw(ptr(part), P, n, ptr(b_actor), ptr(b_critic), A, int(bool(deterministic)),
+                                    int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(epoch), int(step), int(env_offset), ptr(action),
+                                    ptr(logp), ptr(value), stream_of(part)), "merlin_act_draw")
+    return action, logp, value
 
 
 def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,

@@ -606,6 +606,14 @@ class CNNActorCritic(nn.Module):
         else:  # per-frame conv2 lookups + conv3 GEMM (small rollouts, rollout_pack)
             A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
             a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
+        if "W4h" in pack and nat.H3_HEADS_EPILOGUE and self.actor[2].weight.shape[0] <= 4 and \
+                nat.lib().merlin_h3_heads_parts(pack["W4h"][0].shape[1], nat.H3_NT_CFG["rollout"]) > 0:
+            # fc1 + bias + ReLU + both heads in the GEMM's epilogue (h never written), then the draw from the sums
+            P4, amW = pack["W4h"]
+            part = nat.h3_gemm_nt_heads(a3, am3, P4, amW, pack["b4"], self.actor[2].weight, self.critic[2].weight,
+                                        cfg=nat.H3_NT_CFG["rollout"], name="gemm_rollout_fc1", partials_only=True)
+            return nat.act_draw(part, self.actor[2].bias, self.critic[2].bias, deterministic, seed=seed, epoch=epoch,
+                                step=step, out=out, env_offset=env_offset)
         if "W4h" in pack:
             P4, amW = pack["W4h"]
             z = nat.h3_gemm_nt(a3, am3, P4, amW, cfg=nat.H3_NT_CFG["rollout"], name="gemm_rollout_fc1")

@@ -29,6 +29,7 @@ def main():
         from merlin import ppo as PPO_MOD
 
         PPO_MOD.ROLLOUT_SCALE_ROWS = "zero" not in v  # e.g. h3r12_zero: the per-step zeroing launch
+        nat.H3_HEADS_EPILOGUE = "noheadsepi" not in v  # e.g. h3r12_noheadsepi: fc1's z + merlin_act_heads
     dev = torch.device("cuda", 0)
     env = MerlinVecEnv(4096, "mediumhard", seed=777, device=dev)
     torch.manual_seed(777)

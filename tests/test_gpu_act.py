@@ -122,3 +122,33 @@ def test_act_heads_keys_on_the_global_env_index(device):
     zz = torch.cat([z, z], 1)
     both, _, _ = nat.act_heads(zz, b4, wa, ba, wc, bc, seed=9, epoch=epoch, step=2)
     assert torch.equal(both[:n], r0) and torch.equal(both[n:], r1)
+
+
+@pytest.mark.parametrize("n,A", [(4096, 3), (1000, 4), (77, 1)])
+def test_act_draw_from_gemm_heads_matches_act_heads(device, n, A):
+    """The acting path's heads folded into fc1's h3 GEMM (merlin_h3_gemm_nt_heads without h, then merlin_act_draw)
+    == fc1's GEMM then merlin_act_heads: deterministic actions equal (no near-ties at these scales), logp / value
+    within fp32 reordering, and a sampled draw keyed by the same (seed, epoch, step, env) picks the same actions."""
+    from merlin import _native as nat
+
+    g = torch.Generator(device=device).manual_seed(n + A)
+    a3 = torch.relu(torch.randn(2, n, 576, device=device, generator=g))
+    W4 = torch.randn(2, 512, 576, device=device, generator=g) / 24
+    b4 = torch.randn(2, 512, device=device, generator=g) * 0.1
+    wa = torch.randn(A, 512, device=device, generator=g) * 0.05
+    ba = torch.randn(A, device=device, generator=g) * 0.1
+    wc = torch.randn(1, 512, device=device, generator=g) * 0.05
+    bc = torch.randn(1, device=device, generator=g) * 0.1
+    am3, amW = nat.h3_amax(a3), nat.h3_amax(W4)
+    P4 = nat.h3_split(W4, amW)
+    cfg = nat.H3_NT_CFG["rollout"]
+    z = nat.h3_gemm_nt(a3, am3, P4, amW, cfg=cfg)
+    part = nat.h3_gemm_nt_heads(a3, am3, P4, amW, b4, wa, wc, cfg=cfg, partials_only=True)
+    epoch = torch.tensor([3], dtype=torch.int64, device=device)
+    for det in (True, False):
+        a1, lp1, v1 = nat.act_heads(z, b4, wa, ba, wc, bc, deterministic=det, seed=5, epoch=epoch, step=2)
+        a2, lp2, v2 = nat.act_draw(part, ba, bc, deterministic=det, seed=5, epoch=epoch, step=2)
+        assert float((a1 == a2).float().mean()) >= 0.999
+        same = a1 == a2
+        torch.testing.assert_close(lp2[same], lp1[same], rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(v2, v1, rtol=1e-4, atol=1e-5)
