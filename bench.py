@@ -327,6 +327,10 @@ def h3_gemm_names(nat):
     out = {"gemm_fc1_dgrad": (H3_NT_NAMES.get(nat.H3_NT_CFG["dgrad"], "?").format(0),)}
     if heads:
         out["k_heads_fwd"] = ("k_heads_combine",)
+    if nat.H3_HEADS_EPILOGUE and nat.lib().merlin_h3_heads_parts(512, nat.H3_NT_CFG["rollout"]) > 0:
+        # the acting GEMM with the heads only in its epilogue (EPI 3) and the draw from its partials
+        out["gemm_rollout_fc1"] = (H3_NT_NAMES.get(nat.H3_NT_CFG["rollout"], "?").format(3),)
+        out["k_act_heads"] = ("k_act_draw",)
     if FS.PATCH_REUSE == "gather":
         return {**out, **PMC_ALIAS_GATHER, "gemm_fc1_fwd": (fwd.replace("k_h3_ntp<", "k_h3_ntpg<"),)}
     return {**out, "gemm_fc1_fwd": (fwd,)}
