@@ -288,6 +288,9 @@ int merlin_tower_conv2_lut_bwd_grouped(const uint32_t *codes_dev, int64_t group_
  *               (a list split by source block into several calls sums in call order). */
 int merlin_tower_window_lut(const int32_t *rows_dev, int64_t n_windows, const float *tables_dev,
                             int32_t towers, float *Z2w_dev, void *stream);
+/* window_lut with conv2's bias and ReLU applied as the rows are written: a2w[t][w] = relu(Z2w[t][w] + b2[t]). */
+int merlin_tower_window_lut_bias_relu(const int32_t *rows_dev, int64_t n_windows, const float *tables_dev,
+                                      int32_t towers, const float *b2_dev, float *a2w_dev, void *stream);
 int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
                               const int64_t *groups_dev, int64_t n, const float *b3_dev,
                               int32_t towers, float *Y3_dev, void *stream);

@@ -640,6 +640,14 @@ int merlin_tower_window_lut(const int32_t *rows, int64_t nw, const float *tables
     return MERLIN_OK;
 }
 
+int merlin_tower_window_lut_bias_relu(const int32_t *rows, int64_t nw, const float *tables, int32_t towers,
+                                      const float *b2, float *a2w, void *stream) {
+    if ((!rows || !tables || !a2w || !b2) && nw > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    HIP_TRY(merlin::launch_window_lut(rows, nw, tables, towers, a2w, (hipStream_t)stream, b2));
+    return MERLIN_OK;
+}
+
 int merlin_tower_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
                               const float *b3, int32_t towers, float *Y3, void *stream) {
     if ((!Q || !wid || !b3 || !Y3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");

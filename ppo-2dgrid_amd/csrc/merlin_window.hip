@@ -42,10 +42,11 @@ __device__ __forceinline__ float4 f4_mask(const float4 y, const float4 g) {
 // Z2w[t][w][c4] = sum_{k<16} T2[t][rows[w][k]][c4], taps in k_conv2_lut_fwd's order.  ALL only names the
 // instantiation: 1 for the rollout's table over every possible window (5^9 rows, once per rollout), 0 for an
 // update's windows (every minibatch) -- so a profile tells the two apart
+// b2 (optional): relu(Z2w + b2[t]) written instead (conv2's bias and ReLU, as k_bias_relu computes them)
 template <int ALL>
 __global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ rows, int64_t nw,
                                                     const float4 *__restrict__ tab, int T,
-                                                    float4 *__restrict__ Z2w) {
+                                                    float4 *__restrict__ Z2w, const float4 *__restrict__ b2) {
     const int64_t total = (int64_t)T * nw * 16;
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
         const int c = (int)(e & 15);
@@ -59,6 +60,11 @@ __global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ 
         float4 acc = v[0];
 #pragma unroll
         for (int k = 1; k < 16; k++) f4_add(acc, v[k]);
+        if (b2) {
+            const float4 b = b2[t * 16 + c];
+            acc = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
+                              relu_nan(acc.w + b.w));
+        }
         Z2w[e] = acc;
     }
 }
@@ -494,16 +500,17 @@ __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carr
 
 }  // namespace
 
-hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s) {
+hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s,
+                             const float *b2) {
     const int64_t total = (int64_t)T * nw * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
     if (nw == 1953125)  // 5^9: merlin_tower_all_windows()
         hipLaunchKernelGGL(k_window_lut<1>, dim3(grid), dim3(256), 0, s, rows, nw, reinterpret_cast<const float4 *>(tab),
-                           T, reinterpret_cast<float4 *>(Z2w));
+                           T, reinterpret_cast<float4 *>(Z2w), reinterpret_cast<const float4 *>(b2));
     else
         hipLaunchKernelGGL(k_window_lut<0>, dim3(grid), dim3(256), 0, s, rows, nw, reinterpret_cast<const float4 *>(tab),
-                           T, reinterpret_cast<float4 *>(Z2w));
+                           T, reinterpret_cast<float4 *>(Z2w), reinterpret_cast<const float4 *>(b2));
     return hipGetLastError();
 }
 

@@ -97,6 +97,7 @@ def lib():
     L.merlin_tower_conv2_lut_bwd_grouped.argtypes = [vp, i64, vp, vp, i32, vp, vp, vp]
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
+    L.merlin_tower_window_lut_bias_relu.argtypes = [vp, i64, vp, i32, vp, vp, vp]
     L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp]
     L.merlin_tower_window_conv3_reuse.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp, i32, vp]
     L.merlin_tower_all_windows.restype = i64
@@ -179,7 +180,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
-    "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_conv3",
+    "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_lut_bias_relu", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_window_conv3_reuse", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
     "merlin_tower_codes_conv3_amax",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_segment_sum_fused", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
@@ -543,9 +544,10 @@ def conv2_lut_bwd(codes, dZ2c, absmax=None):
 
 
 # -- receptive-field windows (merlin/windows.py, csrc/merlin_window.hip) -----------------------
-def window_lut(rows, tables):
+def window_lut(rows, tables, bias=None):
     """Z2w f32[T, nw, 64]: the sum of the 16 conv2-table rows rows[w] (int32 [nw, 16]) of
-    tables f32[T, 2720, 64] for every window w."""
+    tables f32[T, 2720, 64] for every window w; with bias f32[T, 64]: relu(Z2w + bias) instead (bias_relu_ fused,
+    merlin_tower_window_lut_bias_relu)."""
     T, nw = int(tables.shape[0]), int(rows.shape[0])
     assert tables.shape == (T, LUT2_ROWS, 64) and tables.dtype == torch.float32
     assert rows.dtype == torch.int32 and rows.shape == (nw, 16)
@@ -553,8 +555,13 @@ def window_lut(rows, tables):
     # algorithmic bytes: row indices + Z2w written (table rows are L2-resident gathers)
     # the rollout's all-windows table (5^9 rows) is its own kernel instantiation and span (k_window_lut<1>)
     with KernelTimer.span("k_window_lut_all" if nw == 5 ** 9 else "k_window_lut", nw * (64 + T * 256)):
-        check(lib().merlin_tower_window_lut(ptr(rows), nw, ptr(tables), T, ptr(out), stream_of(tables)),
-              "merlin_tower_window_lut")
+        if bias is not None:
+            assert bias.shape == (T, 64) and bias.dtype == torch.float32 and bias.is_contiguous()
+            check(lib().merlin_tower_window_lut_bias_relu(ptr(rows), nw, ptr(tables), T, ptr(bias), ptr(out),
+                                                          stream_of(tables)), "merlin_tower_window_lut_bias_relu")
+        else:
+            check(lib().merlin_tower_window_lut(ptr(rows), nw, ptr(tables), T, ptr(out), stream_of(tables)),
+                  "merlin_tower_window_lut")
     return out
 
 

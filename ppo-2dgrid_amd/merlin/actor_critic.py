@@ -546,8 +546,9 @@ class CNNActorCritic(nn.Module):
         if all_windows is None:
             all_windows = self._use_all_windows(frames, T2.device)
         if all_windows:
-            Z2 = nat.window_lut(self._all_window_rows(T2.device), T2)  # [2, 5**9, 64]
-            a2 = torch.relu_(Z2.add_(torch.stack([ea[2].bias, ec[2].bias]).unsqueeze(1)))
+            # relu(conv2) of every possible window [2, 5**9, 64] (bias and ReLU in the lookup kernel)
+            a2 = nat.window_lut(self._all_window_rows(T2.device), T2,
+                                bias=torch.stack([ea[2].bias, ec[2].bias]).contiguous())
             if self.fc1_impl in ("x6", "h3") and QALL_H3:
                 # the table GEMM [5^9, 64] x [64, 576] per tower on the f16 two-plane kernels (hipBLASLt's fp32
                 # GEMM took ~3.6 ms per rollout; the error bound is the same, tests/test_gpu_h3.py)

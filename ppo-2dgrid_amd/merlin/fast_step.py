@@ -285,7 +285,7 @@ class WindowStep:
         T2, b2, W3r, b3, _, b4 = self.stage.forward()
         P4, P4t = self.stage.planes[:2]
         am3, amz, amW = am[0:2], am[2:4], self.stage.amaxW
-        a2w = nat.bias_relu_(nat.window_lut(plan.rows, T2), b2)  # relu(conv2) of every window
+        a2w = nat.window_lut(plan.rows, T2, bias=b2)  # relu(conv2) of every window (bias and ReLU fused)
         wh3 = h3 and WINDOW_H3 and len(self.stage.planes) == 4
         if wh3:
             P3t, P3 = self.stage.planes[2:]
