@@ -320,7 +320,8 @@ int merlin_tower_window_conv3_bits(const float *Q_dev, int64_t n_windows, const 
  * (rep_row_dev[r] == r; rep_row_dev int32[n*9]: for every row r = k*9 + p3 of this call, a row of this call holding
  * the same patch, itself a representative) are computed; a second launch copies the other rows from theirs: their
  * Y3 rows with copy bit 0, their mask words with copy bit 1 (copy = 3: the same outputs as _bits; without a bit
- * the non-representative rows stay unwritten, for consumers that read rows through rep_row_dev). */
+ * the non-representative rows stay unwritten, for consumers that read rows through rep_row_dev); copy bit 2: the
+ * copies only, after a call that computed the representatives (e.g. on another stream). */
 int merlin_tower_window_conv3_reuse(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
                                     const int64_t *groups_dev, int64_t n, const float *b3_dev,
                                     int32_t towers, float *Y3_dev, uint64_t *relu_bits_dev, uint32_t *amax_dev,

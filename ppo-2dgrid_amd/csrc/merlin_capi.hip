@@ -670,9 +670,10 @@ int merlin_tower_window_conv3_bits(const float *Q, int64_t nw, const int32_t *wi
 int merlin_tower_window_conv3_reuse(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
                                     const float *b3, int32_t towers, float *Y3, uint64_t *relu_bits, uint32_t *amax,
                                     const int32_t *rep_row, int32_t copy, void *stream) {
-    if ((!Q || !wid || !b3 || !Y3 || !rep_row) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
+    if ((!rep_row || !Y3 || (!(copy & 4) && (!Q || !wid || !b3))) && n > 0)
+        return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    if (copy < 0 || copy > 3) return fail(MERLIN_E_INVALID, "copy must be 0..3");
+    if (copy < 0 || copy > 7) return fail(MERLIN_E_INVALID, "copy must be 0..7");
     HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, Y3, relu_bits, amax, rep_row, copy,
                                         (hipStream_t)stream));
     return MERLIN_OK;

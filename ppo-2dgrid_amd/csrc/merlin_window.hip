@@ -528,10 +528,13 @@ hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, c
     }
     if (T > 2) return hipErrorInvalidValue;
     const int rgrid = (int)std::min<int64_t>((total / 16 + 255) / 256, 256 * 32);
-    hipLaunchKernelGGL(k_window_conv3_reps, dim3(rgrid), dim3(256), 0, s, q, nw, wid, groups, n, b, T, y, bits, amax,
-                       rrow);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !(copy & 3)) return e;
+    if (!(copy & 4)) {  // copy bit 2: the copies only (the representatives were computed by an earlier call)
+        hipLaunchKernelGGL(k_window_conv3_reps, dim3(rgrid), dim3(256), 0, s, q, nw, wid, groups, n, b, T, y, bits,
+                           amax, rrow);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (!(copy & 3)) return hipSuccess;
     if (copy & 1)
         hipLaunchKernelGGL(k_window_conv3_copy<true>, dim3(grid), dim3(256), 0, s, y, (copy & 2) ? bits : nullptr, n,
                            T, rrow);

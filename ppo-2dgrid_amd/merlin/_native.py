@@ -611,6 +611,19 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
 ALL_WINDOWS = 5 ** 9  # merlin_tower_all_windows()
 
 
+def window_conv3_copy_masks(Y3, bits, rep_row):
+    """The mask words of the rows that are not their patch's representative, copied from it (the second half of
+    window_conv3(rep_row=..., copy=2), for a launch on another stream after the representatives' one)."""
+    T, rows = int(bits.shape[0]), int(bits.shape[1])
+    n = rows // 9
+    assert bits.dtype == torch.int64 and rep_row.dtype == torch.int32 and rep_row.numel() == rows
+    with KernelTimer.span("k_window_conv3_copy", T * rows * 12):
+        check(lib().merlin_tower_window_conv3_reuse(None, 0, None, None, n, None, T, ptr(Y3), ptr(bits), None,
+                                                    ptr(rep_row), 6, stream_of(bits)),
+              "merlin_tower_window_conv3_reuse")
+    return bits
+
+
 def codes_conv3(codes, Qall, b3, amax=None):
     """Y3 f32[T, n*9, 64]: relu(conv3) rows (k, p3) of frames codes[k] (int32 [n, 8]) from Qall
     f32[T, 5**9, 576], the per-window, per-tap conv3 partial sums of every possible window

@@ -206,6 +206,10 @@ WGRAD_SPLIT_SIDE = False
 # forward and weight-gradient GEMMs read every row through rep_row (merlin_h3_gemm_{nt,tn}_gather; h3 only, else as
 # "copy"); "copy" -- the other rows copied from theirs; False -- every row computed
 PATCH_REUSE = "gather"
+# with "gather": the other rows' mask words copied on the side stream beside the forward GEMM (False: right after the
+# representatives, on the main stream).  Off: the 15-us copy beside the GEMM slowed the update, 194.8 vs 189.6 ms
+# (scripts/ab_update.py 5 6 fast,fast_maskmain), as every side-stream kernel beside the NT GEMMs has
+MASK_COPY_SIDE = False
 
 
 class WindowStep:
@@ -298,13 +302,24 @@ class WindowStep:
         rep_row = getattr(mb, "rep_row", None) if PATCH_REUSE else None
         # a3's rows through their patch representatives (the other rows never written)
         arows = rep_row if (PATCH_REUSE == "gather" and h3 and not WGRAD_PLANES and not split_side) else None
+        # with gathered rows: the representatives only here; the other rows' mask words (read by the backward's patch
+        # sums) are copied on the side stream beside the forward GEMM, joined by an event before that pass
         Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None, rep_row=rep_row,
-                                    copy=2 if arows is not None else 3)
+                                    copy=(0 if MASK_COPY_SIDE else 2) if arows is not None else 3)
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
         pa3 = pdz = None
         main = torch.cuda.current_stream()
         side = self.side_stream(a3.device)
+        masks_ready = None
+        if arows is not None and MASK_COPY_SIDE:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                nat.window_conv3_copy_masks(Y3, bits, rep_row)
+                masks_ready = torch.cuda.Event()
+                masks_ready.record(side)
+            bits.record_stream(side)
+            Y3.record_stream(side)
         if split_side:  # a3's planes for the weight gradient, on the side stream beside the forward GEMM
             side.wait_stream(main)
             with torch.cuda.stream(side):
@@ -367,6 +382,8 @@ class WindowStep:
         for x in (dz, a3, pdz, pa3):
             if x is not None:
                 x.record_stream(side)
+        if masks_ready is not None:
+            main.wait_event(masks_ready)
         dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]))
         nat.colsum(dQ.view(2, -1, 9, 64)[:, :, 0], out=g[3])  # db3: every (u, p3) has one window at tap 0
         dQ = dQ.view(2, -1, 576)
