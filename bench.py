@@ -474,6 +474,10 @@ def hard22_tier(device, N, T, epochs, minibatches, warmup=2, iters=3):
     from merlin import MerlinVecEnv
     from merlin.ppo import PPO
 
+    # the tiers before this one leave blocks in torch's caching allocator: release them, so the acting path's
+    # free-memory check (CNNActorCritic._use_all_windows, 12 GB for the all-windows table) sees the device as the main
+    # loop did
+    torch.cuda.empty_cache()
     env = MerlinVecEnv(N, difficulty="hard", size=22, seed=777, device=device)
     torch.manual_seed(777)
     agent = PPO(env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=epochs, batch_size=N * T,
@@ -483,7 +487,8 @@ def hard22_tier(device, N, T, epochs, minibatches, warmup=2, iters=3):
            "config": f"hard 22x22, {N} envs x k_steps {T}, {epochs} epochs x {minibatches} minibatches",
            "state": f"iterations {warmup + 1}..{warmup + iters} from random init",
            "distinct_frames_per_sample": round(agent.last_distinct_frac, 4),
-           "windows_per_update": agent.last_num_windows}
+           "windows_per_update": agent.last_num_windows,
+           "rollout_acting": "all-windows conv3 table" if agent.rollout_all_windows else "per-frame conv2 lookups"}
     env.close()
     del agent
     torch.cuda.empty_cache()
