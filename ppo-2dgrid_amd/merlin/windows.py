@@ -76,21 +76,20 @@ def unpack_classes(codes: torch.Tensor) -> torch.Tensor:
 def window_keys(cls: torch.Tensor) -> torch.Tensor:
     """[n, 7, 7] classes -> int64 [n, 25]: the 3x3 window at each conv2 position as 9 base-5
     digits, window tile (0, 0) most significant."""
-    k = torch.zeros((cls.shape[0], 5, 5), dtype=torch.int64, device=cls.device)
-    for a in range(3):
-        for b in range(3):
-            k = k * 5 + cls[:, a:a + 5, b:b + 5]
-    return k.reshape(-1, 25)
+    r = cls[:, :, 0:5] * 25 + cls[:, :, 1:6] * 5 + cls[:, :, 2:7]  # [n, 7, 5]: 3-tile row keys
+    return (r[:, 0:5] * 15625 + r[:, 1:6] * 125 + r[:, 2:7]).reshape(-1, 25)
 
 
 def patch_keys(cls: torch.Tensor) -> torch.Tensor:
     """[n, 7, 7] classes -> int64 [n, 9]: the 5x5-tile patch under each conv3 output p3 =
     (oy, ox) (conv2 positions oy..oy+2 x ox..ox+2, i.e. tiles oy..oy+4 x ox..ox+4) as 25 base-5
     digits, patch tile (0, 0) most significant."""
-    k = torch.zeros((cls.shape[0], 3, 3), dtype=torch.int64, device=cls.device)
-    for a in range(5):
-        for b in range(5):
-            k = k * 5 + cls[:, a:a + 3, b:b + 3]
+    r = cls[:, :, 0:3]
+    for b in range(1, 5):
+        r = r * 5 + cls[:, :, b:b + 3]  # [n, 7, 3]: 5-tile row keys
+    k = r[:, 0:3]
+    for a in range(1, 5):
+        k = k * 3125 + r[:, a:a + 3]
     return k.reshape(-1, 9)
 
 
@@ -256,27 +255,31 @@ class WindowPlan:
         self.kid = kid.view(F, 9).to(torch.int32).contiguous()
         ks, ko = torch.sort(kid.to(torch.int32), stable=True)
         self.patch_plan = SegmentPlan(ks, ko, item_len)
-        # band lists: entry (patch k, ky) -> S row band_off[ky] + (k's band ky); source R row k
+        # band lists: entry (patch k, ky) -> S row (k's band ky), bands numbered by (ky, band key); source R row k.
+        # Band ky of a patch is its tile rows ky..ky+2, digits 5 ky .. 5 ky + 14 of the patch key: one division and
+        # one remainder; the three rows' bands are numbered by one unique over (ky, band key) (one host read)
         K = self.num_patches
-        pd = digits5(pk, 25).view(K, 5, 5)
-        bdst, bsrc, wdst, off = [], [], [], 0
-        ar = torch.arange(K, dtype=torch.int64, device=dev)
-        for ky in range(3):
-            ub, bid = torch.unique(base5(pd[:, ky:ky + 3, :].reshape(K, 15)), return_inverse=True)
-            bdst.append(off + bid)
-            bsrc.append(ar)
-            # dQ entries of these bands: (band j, kx) -> Q row w*9 + ky*3 + kx, w = the band's
-            # window at column kx (numbered by searching the sorted window keys)
-            bd = digits5(ub, 15).view(-1, 3, 5)
-            for kx in range(3):
-                w = torch.searchsorted(uniq, base5(bd[:, :, kx:kx + 3].reshape(-1, 9)).to(torch.int32))
-                wdst.append((w * 9 + ky * 3 + kx, off + torch.arange(ub.numel(), dtype=torch.int64, device=dev)))
-            off += int(ub.numel())
-        self.num_bands = off
-        bk, bo = torch.sort(torch.cat(bdst).to(torch.int32), stable=True)
-        self.band_plan = SegmentPlan(bk, torch.cat(bsrc)[bo], item_len)
-        dk, do = torch.sort(torch.cat([d for d, _ in wdst]).to(torch.int32), stable=True)
-        self.dq_plan = SegmentPlan(dk, torch.cat([s for _, s in wdst])[do], item_len)
+        B15 = 5 ** 15
+        ky3 = torch.arange(3, dtype=torch.int64, device=dev)
+        bkeys = ky3.unsqueeze(1) * B15 + (pk.unsqueeze(0) // (5 ** (10 - 5 * ky3)).unsqueeze(1)) % B15  # [3, K]
+        ub, bid = torch.unique(bkeys.reshape(-1), return_inverse=True)
+        self.num_bands = int(ub.numel())
+        bk, bo = torch.sort(bid.to(torch.int32), stable=True)
+        self.band_plan = SegmentPlan(bk, (bo % K), item_len)
+        # dQ entries of the bands: (band j, kx) -> Q row w*9 + ky*3 + kx, w = the band's window at column kx: rows
+        # r < 3 of the band (5 digits each), their columns kx..kx+2 (3 digits), numbered by searching the sorted
+        # window keys
+        bky, bkey = ub // B15, ub % B15
+        brow = (bkey.unsqueeze(1) // (3125 ** (2 - ky3)).unsqueeze(0)) % 3125  # [nb, 3]
+        jb = torch.arange(self.num_bands, dtype=torch.int64, device=dev)
+        ddst, dsrc = [], []
+        for kx in range(3):
+            c = (brow // 5 ** (2 - kx)) % 125
+            w = torch.searchsorted(uniq, ((c[:, 0] * 125 + c[:, 1]) * 125 + c[:, 2]).to(torch.int32))
+            ddst.append(w * 9 + bky * 3 + kx)
+            dsrc.append(jb)
+        dk, do = torch.sort(torch.cat(ddst).to(torch.int32), stable=True)
+        self.dq_plan = SegmentPlan(dk, torch.cat(dsrc)[do], item_len)
 
     def update_minibatches(self, perms: list, minibatch_size: int, bulk: bool = False) -> list:
         """epoch_minibatches for every epoch's permutation at once: one stable sort and one host

@@ -211,3 +211,22 @@ def test_epoch_minibatches_match_per_minibatch_grouping():
                 assert torch.equal(rr[rr], rr) and torch.equal(live.reshape(-1)[rr], live.reshape(-1))
                 # one representative per distinct patch of the minibatch
                 assert int((rr == torch.arange(rr.numel())).sum()) == int(lv.sum())
+
+
+def test_window_and_patch_keys_match_digit_loops():
+    """window_keys / patch_keys (built from per-row keys) == the tile-by-tile base-5 accumulation, tile (0, 0) most
+    significant, on random class grids including the all-4 corner case."""
+    from merlin.windows import patch_keys, window_keys
+
+    cls = torch.randint(0, 5, (300, 7, 7), generator=torch.Generator().manual_seed(2), dtype=torch.int64)
+    cls[0] = 4
+    wk = torch.zeros((300, 5, 5), dtype=torch.int64)
+    for a in range(3):
+        for b in range(3):
+            wk = wk * 5 + cls[:, a:a + 5, b:b + 5]
+    pk = torch.zeros((300, 3, 3), dtype=torch.int64)
+    for a in range(5):
+        for b in range(5):
+            pk = pk * 5 + cls[:, a:a + 3, b:b + 3]
+    assert torch.equal(window_keys(cls), wk.reshape(-1, 25)) and torch.equal(patch_keys(cls), pk.reshape(-1, 9))
+    assert int(pk.max()) == 5 ** 25 - 1
