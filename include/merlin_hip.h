@@ -288,6 +288,13 @@ int merlin_tower_conv2_lut_bwd_grouped(const uint32_t *codes_dev, int64_t group_
  *               (a list split by source block into several calls sums in call order). */
 int merlin_tower_window_lut(const int32_t *rows_dev, int64_t n_windows, const float *tables_dev,
                             int32_t towers, float *Z2w_dev, void *stream);
+/* The live-patch maps of every minibatch of an update (merlin/windows.py WindowPlan._bulk_minibatches): group g
+ * (group_keys[g] = minibatch m * n_frames + frame; group_offsets[m] = first group of minibatch m), position p3 ->
+ * patch k = kid[frame * 9 + p3]: kmap[m * n_patches + k] = k (preset to -1 by the caller), rmap[...] = one row
+ * j * 9 + p3 of m holding k (scratch, no preset), rep_row[g * 9 + p3] = that row (conv3's patch representatives). */
+int merlin_minibatch_patch_maps(const int32_t *kid_dev, const int64_t *group_keys_dev, int64_t n_groups,
+                                int64_t n_frames, const int64_t *group_offsets_dev, int32_t n_patches, int32_t *kmap_dev,
+                                int32_t *rmap_dev, int32_t *rep_row_dev, void *stream);
 /* window_lut with conv2's bias and ReLU applied as the rows are written: a2w[t][w] = relu(Z2w[t][w] + b2[t]). */
 int merlin_tower_window_lut_bias_relu(const int32_t *rows_dev, int64_t n_windows, const float *tables_dev,
                                       int32_t towers, const float *b2_dev, float *a2w_dev, void *stream);

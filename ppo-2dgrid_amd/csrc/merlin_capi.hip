@@ -640,6 +640,18 @@ int merlin_tower_window_lut(const int32_t *rows, int64_t nw, const float *tables
     return MERLIN_OK;
 }
 
+int merlin_minibatch_patch_maps(const int32_t *kid, const int64_t *group_keys, int64_t n_groups, int64_t n_frames,
+                                const int64_t *group_offsets, int32_t n_patches, int32_t *kmap, int32_t *rmap,
+                                int32_t *rep_row, void *stream) {
+    if (n_groups < 0 || n_frames < 1 || n_patches < 1) return fail(MERLIN_E_INVALID, "bad shape");
+    if (n_groups > 0 && (!kid || !group_keys || !group_offsets || !kmap || !rmap || !rep_row))
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (n_groups * 9 > INT32_MAX) return fail(MERLIN_E_UNSUPPORTED, "more than 2^31 rows");
+    HIP_TRY(merlin::launch_patch_maps(kid, group_keys, n_groups, n_frames, group_offsets, n_patches, kmap, rmap,
+                                      rep_row, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
 int merlin_tower_window_lut_bias_relu(const int32_t *rows, int64_t nw, const float *tables, int32_t towers,
                                       const float *b2, float *a2w, void *stream) {
     if ((!rows || !tables || !a2w || !b2) && nw > 0) return fail(MERLIN_E_INVALID, "null argument");

@@ -104,6 +104,8 @@ hipError_t launch_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int
 hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
                                 int towers, float *dT, void *slabs, hipStream_t s, int64_t gstride = 0);
 
+hipError_t launch_patch_maps(const int32_t *kid, const int64_t *gkey, int64_t G, int64_t F, const int64_t *goff, int K,
+                             int32_t *kmap, int32_t *rmap, int32_t *rep_row, hipStream_t s);
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s,
                              const float *b2 = nullptr);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,

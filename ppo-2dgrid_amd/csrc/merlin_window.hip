@@ -498,7 +498,43 @@ __global__ __launch_bounds__(256) void k_seg_fix(const float2 *__restrict__ carr
     }
 }
 
+// The minibatches' live-patch maps for a whole update (merlin/windows.py WindowPlan._bulk_minibatches): group g
+// (minibatch m = key / F, frame key % F, position j = g - goff[m] in its minibatch), position p3 -> patch k =
+// kid[frame][p3]: kmap[m][k] = k (the S pass's slot map; racing writers store the same value) and rmap[m][k] = j*9 +
+// p3 (one row of the minibatch holding k: any writer wins, they compute the same bits); then, after that launch,
+// rep_row[g*9 + p3] = rmap[m][k].  One thread per (group, position), 32-bit indices throughout.
+template <int PASS>
+__global__ __launch_bounds__(256) void k_patch_maps(const int32_t *__restrict__ kid, const int64_t *__restrict__ gkey,
+                                                    int64_t G, int64_t F, const int64_t *__restrict__ goff, int K,
+                                                    int32_t *__restrict__ kmap, int32_t *__restrict__ rmap,
+                                                    int32_t *__restrict__ rep_row) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= G * 9) return;
+    const int64_t g = e / 9;
+    const int p3 = (int)(e - g * 9);
+    const int64_t key = gkey[g], m = key / F, frame = key - m * F;
+    const int32_t k = kid[frame * 9 + p3];
+    const int64_t at = m * K + k;
+    if (PASS == 0) {
+        kmap[at] = k;
+        rmap[at] = (int32_t)((g - goff[m]) * 9 + p3);
+    } else {
+        rep_row[e] = rmap[at];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_patch_maps(const int32_t *kid, const int64_t *gkey, int64_t G, int64_t F, const int64_t *goff, int K,
+                             int32_t *kmap, int32_t *rmap, int32_t *rep_row, hipStream_t s) {
+    if (G <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((G * 9 + 255) / 256));
+    hipLaunchKernelGGL(k_patch_maps<0>, grid, dim3(256), 0, s, kid, gkey, G, F, goff, K, kmap, rmap, rep_row);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_patch_maps<1>, grid, dim3(256), 0, s, kid, gkey, G, F, goff, K, kmap, rmap, rep_row);
+    return hipGetLastError();
+}
 
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s,
                              const float *b2) {

@@ -98,6 +98,7 @@ def lib():
     L.merlin_tower_window_lut.argtypes = [vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_lut_bias_relu.argtypes = [vp, i64, vp, i32, vp, vp, vp]
+    L.merlin_minibatch_patch_maps.argtypes = [vp, vp, i64, i64, vp, i32, vp, vp, vp, vp]
     L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp]
     L.merlin_tower_window_conv3_reuse.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp, i32, vp]
     L.merlin_tower_all_windows.restype = i64
@@ -180,7 +181,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
-    "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_lut_bias_relu", "merlin_tower_window_conv3",
+    "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_lut_bias_relu", "merlin_minibatch_patch_maps", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_window_conv3_reuse", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
     "merlin_tower_codes_conv3_amax",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_segment_sum_fused", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
@@ -609,6 +610,23 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
 
 
 ALL_WINDOWS = 5 ** 9  # merlin_tower_all_windows()
+
+
+def minibatch_patch_maps(kid, group_keys, num_frames, group_offsets, nmb, num_patches):
+    """(kmap int32 [nmb, K], rep_row int32 [G * 9]) of WindowPlan._bulk_minibatches in two launches
+    (merlin_minibatch_patch_maps): kid int32 [F, 9], group_keys int64 [G] (minibatch * F + frame), group_offsets
+    int64 [nmb] (first group of each minibatch)."""
+    G, K = int(group_keys.numel()), int(num_patches)
+    dev = group_keys.device
+    assert kid.dtype == torch.int32 and kid.is_contiguous() and group_keys.dtype == torch.int64
+    assert group_offsets.dtype == torch.int64 and group_offsets.numel() >= nmb
+    kmap = torch.full((nmb, K), -1, dtype=torch.int32, device=dev)
+    rmap = torch.empty((nmb, K), dtype=torch.int32, device=dev)
+    rep_row = torch.empty(G * 9, dtype=torch.int32, device=dev)
+    check(lib().merlin_minibatch_patch_maps(ptr(kid), ptr(group_keys), G, int(num_frames), ptr(group_offsets), K,
+                                            ptr(kmap), ptr(rmap), ptr(rep_row), stream_of(group_keys)),
+          "merlin_minibatch_patch_maps")
+    return kmap, rep_row
 
 
 def window_conv3_copy_masks(Y3, bits, rep_row):

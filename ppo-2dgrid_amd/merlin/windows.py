@@ -315,17 +315,11 @@ class WindowPlan:
         offs = torch.empty(G + nmb, dtype=torch.int32, device=dev)
         offs[torch.arange(G, device=dev) + mbg] = (starts - lo[mbg]).to(torch.int32)
         offs[goff[1:] + torch.arange(nmb, device=dev)] = span
-        live = self.kid.index_select(0, gall)  # [G, 9] patch ids
-        kmap = torch.full((nmb, K), -1, dtype=torch.int32, device=dev)
-        at = (mbg.unsqueeze(1) * K + live).reshape(-1)
-        kmap.view(-1)[at] = live.reshape(-1)
-        # conv3's patch reuse (merlin_tower_window_conv3_reuse): rep_row = per row j*9 + p3 of its minibatch, one row
-        # of the minibatch holding the same patch (rmap[m][k]: the row that won the scatter -- which one does not
-        # matter, they compute the same bits)
-        rmap = torch.full((nmb, K), -1, dtype=torch.int32, device=dev)
-        rmap.view(-1)[at] = (j.unsqueeze(1) * 9 + torch.arange(9, device=dev)).to(torch.int32).reshape(-1)
-        rep_row = rmap.view(-1)[at]  # [G * 9], minibatch m's rows at goff[m] * 9 ..
-        del rmap
+        # the live-patch maps kmap [nmb, K] (the S pass's slot maps) and conv3's patch reuse rows rep_row [G * 9]
+        # (merlin_tower_window_conv3_reuse: per row j*9 + p3 of its minibatch, one row of the minibatch holding the
+        # same patch -- which one wins does not matter, they compute the same bits): two launches over the G * 9
+        # (group, position)s (merlin_minibatch_patch_maps; the torch scatter / gather chain took ~3.6 ms per update)
+        kmap, rep_row = nat.minibatch_patch_maps(self.kid, uniq, F, goff, nmb, K)
         out = []
         for m, c in enumerate(counts):
             g0 = goff_h[m]

@@ -28,7 +28,7 @@ def main():
     codes = agent.buf.flat_codes
     B = codes.shape[0]
     perms = [torch.randperm(B, device=dev) for _ in range(10)]
-    ts = {"FrameGroups": [], "WindowPlan": [], "update_minibatches": []}
+    ts = {"FrameGroups": [], "WindowPlan": [], "update_minibatches": [], "update_minibatches(lazy)": []}
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -41,6 +41,9 @@ def main():
         plan.update_minibatches(perms, B // 8, bulk=True)
         torch.cuda.synchronize()
         t3 = time.perf_counter()
+        plan.update_minibatches(perms, B // 8, bulk=False)
+        torch.cuda.synchronize()
+        ts["update_minibatches(lazy)"].append((time.perf_counter() - t3) * 1e3)
         ts["FrameGroups"].append((t1 - t0) * 1e3)
         ts["WindowPlan"].append((t2 - t1) * 1e3)
         ts["update_minibatches"].append((t3 - t2) * 1e3)

@@ -75,7 +75,7 @@ def test_window_conv3_patch_reuse_bitwise(device):
     """merlin_tower_window_conv3_reuse (each distinct patch of a minibatch computed once, the rows sharing it
     copied) == every row computed: Y3, ReLU bit words and the operand scale, bit for bit, on every bulk
     minibatch of two epochs (the last one ragged); copy=2 / 0 write the representative rows (and the masks)
-    only."""
+    only.  The bulk builder's maps (merlin_minibatch_patch_maps): rep_row and the live-patch map kmap."""
     from merlin import _native as nat
 
     codes, plan = _plan(device)
@@ -97,6 +97,13 @@ def test_window_conv3_patch_reuse_bitwise(device):
             assert torch.equal(live[rr], live)  # and hold the row's patch
             own = torch.arange(n * 9, device=device)
             shared += int((rr != own).sum())
+            # the live-patch map of the S pass: kmap[k] = k exactly for the minibatch's patches, else -1
+            lv = torch.zeros(plan.num_patches, dtype=torch.bool, device=device)
+            lv[live.long()] = True
+            assert torch.equal(mb.kmap >= 0, lv)
+            assert torch.equal(mb.kmap[lv], torch.nonzero(lv).view(-1).to(torch.int32))
+            # one representative per distinct patch
+            assert int((rr == own).sum()) == int(lv.sum())
             am0 = torch.zeros(2, dtype=torch.int32, device=device)
             am1 = torch.zeros(2, dtype=torch.int32, device=device)
             Y0, b0 = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am0)

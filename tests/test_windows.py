@@ -193,24 +193,6 @@ def test_epoch_minibatches_match_per_minibatch_grouping():
             for m, r in zip(allm[e], ref):
                 for a in ("groups", "inv", "slot", "order", "offs"):
                     assert torch.equal(getattr(m, a), getattr(r, a)), a
-    # the bulk builder (merlin/fast_step.py's minibatches): same groups, plus the live-patch map kmap and the
-    # patch-reuse rows rep_row (per row, a row of the minibatch holding its patch; merlin_tower_window_conv3_reuse)
-    for mbs in (128, 300):
-        allm = plan.update_minibatches(perms, mbs, bulk=True)
-        for e, p in enumerate(perms):
-            ref = plan.epoch_minibatches(p, mbs)
-            for m, r in zip(allm[e], ref):
-                assert torch.equal(m.groups, r.groups) and torch.equal(m.slot, r.slot)
-                live = plan.kid[m.groups]  # [n, 9]
-                lv = torch.zeros(plan.num_patches, dtype=torch.bool)
-                lv[live.reshape(-1).long()] = True
-                assert torch.equal(m.kmap >= 0, lv)
-                assert torch.equal(m.kmap[lv], torch.nonzero(lv).view(-1).to(torch.int32))
-                rr = m.rep_row.long()
-                assert m.rep_row.dtype == torch.int32 and rr.numel() == live.numel()
-                assert torch.equal(rr[rr], rr) and torch.equal(live.reshape(-1)[rr], live.reshape(-1))
-                # one representative per distinct patch of the minibatch
-                assert int((rr == torch.arange(rr.numel())).sum()) == int(lv.sum())
 
 
 def test_window_and_patch_keys_match_digit_loops():
