@@ -380,6 +380,15 @@ int merlin_segment_sum_fused(const float *src_dev, const void *mask_dev, int64_t
                              const int32_t *fix_dev, int64_t n_fix, int32_t towers, float *out_dev,
                              int64_t out_rows, float *carry_dev, int32_t flags, int32_t *mark_dev,
                              const int32_t *head_fix_dev, int32_t *counters_dev, void *stream);
+/* merlin_segment_sum_fused with the mask's bit words read through a row map: the mask of source row r is
+ * mask[t][mask_rows[r]] (conv3's patch representatives, merlin_tower_window_conv3_reuse with copy = 0: rows of one
+ * patch share their ReLU mask and only the representatives' words are written). */
+int merlin_segment_sum_mask_rows(const float *src_dev, const void *mask_dev, int64_t src_rows, const int32_t *idx_dev,
+                                 const int32_t *key_dev, int64_t nnz, const int32_t *slot_dev, int32_t sub,
+                                 int64_t item_len, const int32_t *fix_dev, int64_t n_fix, int32_t towers, float *out_dev,
+                                 int64_t out_rows, float *carry_dev, int32_t flags, int32_t *mark_dev,
+                                 const int32_t *head_fix_dev, int32_t *counters_dev, const int32_t *mask_rows_dev,
+                                 void *stream);
 
 /* Acting tail (src/actor_critic.py:48-55 act, src/ppo.py:69-71): z float[2][n][hidden] = fc1's
  * pre-activation of the actor / critic tower, b4 float[2][hidden]; h = relu(z + b4); logits =

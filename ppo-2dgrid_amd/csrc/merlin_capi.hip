@@ -706,11 +706,11 @@ int merlin_tower_codes_conv3(const uint32_t *codes, int64_t n, const float *Qall
     return merlin_tower_codes_conv3_amax(codes, n, Qall, b3, towers, Y3, nullptr, stream);
 }
 
-int merlin_segment_sum_fused(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,
+static int segment_sum_fused(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,
                              const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub, int64_t item_len,
                              const int32_t *fix, int64_t n_fix, int32_t towers, float *out, int64_t out_rows,
                              float *carry, int32_t flags, int32_t *mark, const int32_t *head_fix, int32_t *counters,
-                             void *stream) {
+                             const int32_t *mask_rows, void *stream) {
     if (!out && out_rows > 0) return fail(MERLIN_E_INVALID, "null output");
     if (nnz > 0 && (!src || !idx || !key || !carry)) return fail(MERLIN_E_INVALID, "null argument");
     if (n_fix > 0 && !fix) return fail(MERLIN_E_INVALID, "null fix-up list");
@@ -725,8 +725,28 @@ int merlin_segment_sum_fused(const float *src, const void *mask, int64_t src_row
                                    sub, item_len, fix, n_fix, towers, out, out_rows, carry,
                                    (flags & MERLIN_SEG_ACCUMULATE) ? 1 : 0, (flags & MERLIN_SEG_NO_FILL) ? 0 : 1,
                                    (flags & MERLIN_SEG_ROLE_MASK) >> MERLIN_SEG_ROLE_SHIFT, mark, head_fix, counters,
-                                   (hipStream_t)stream));
+                                   (hipStream_t)stream, mask_rows));
     return MERLIN_OK;
+}
+
+int merlin_segment_sum_fused(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,
+                             const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub, int64_t item_len,
+                             const int32_t *fix, int64_t n_fix, int32_t towers, float *out, int64_t out_rows,
+                             float *carry, int32_t flags, int32_t *mark, const int32_t *head_fix, int32_t *counters,
+                             void *stream) {
+    return segment_sum_fused(src, mask, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
+                             out_rows, carry, flags, mark, head_fix, counters, nullptr, stream);
+}
+
+int merlin_segment_sum_mask_rows(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,
+                                 const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub, int64_t item_len,
+                                 const int32_t *fix, int64_t n_fix, int32_t towers, float *out, int64_t out_rows,
+                                 float *carry, int32_t flags, int32_t *mark, const int32_t *head_fix,
+                                 int32_t *counters, const int32_t *mask_rows, void *stream) {
+    if (nnz > 0 && (!mask || !mask_rows || !(flags & MERLIN_SEG_MASK_BITS)))
+        return fail(MERLIN_E_INVALID, "mask_rows needs MERLIN_SEG_MASK_BITS words");
+    return segment_sum_fused(src, mask, src_rows, idx, key, nnz, slot, sub, item_len, fix, n_fix, towers, out,
+                             out_rows, carry, flags, mark, head_fix, counters, mask_rows, stream);
 }
 
 int merlin_segment_sum_marked(const float *src, const void *mask, int64_t src_rows, const int32_t *idx,

@@ -142,7 +142,8 @@ hipError_t launch_heads_fwd(const float *h, int64_t n, int H, const float *wa, i
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill, int role,
-                          int32_t *mark, const int32_t *hfix, int32_t *cnt, hipStream_t s);
+                          int32_t *mark, const int32_t *hfix, int32_t *cnt, hipStream_t s,
+                          const int32_t *mrow = nullptr);
 
 // GEMM epilogues (merlin_head.hip); partial sums use a per-device workspace of
 // epilogue_work_floats() floats

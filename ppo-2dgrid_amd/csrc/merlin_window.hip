@@ -323,14 +323,17 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
                                                            int acc_out, int32_t *__restrict__ mark,
                                                            const int4 *__restrict__ fix,
                                                            const int32_t *__restrict__ hfix,
-                                                           int32_t *__restrict__ cnt) {
+                                                           int32_t *__restrict__ cnt,
+                                                           const int32_t *__restrict__ mrow) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int t = lane >> 5, q = (lane >> 4) & 1, c = lane & 15;
     const bool live = t < T;
     const float4 *srct = src + (size_t)(live ? t : 0) * src_rows * 16 + c;
     const float4 *maskt =
         MASK == 1 ? static_cast<const float4 *>(mask) + (size_t)(live ? t : 0) * src_rows * 16 + c : nullptr;
-    const uint64_t *bitst = MASK == 2 ? static_cast<const uint64_t *>(mask) + (size_t)(live ? t : 0) * src_rows
+    // MASK 3: the bit words of MASK 2 read through a row map, bits[mrow[row]] (conv3's patch representatives: rows of
+    // one patch share their ReLU mask, only the representatives' words are written)
+    const uint64_t *bitst = MASK >= 2 ? static_cast<const uint64_t *>(mask) + (size_t)(live ? t : 0) * src_rows
                                       : nullptr;
     const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int64_t it = (int64_t)blockIdx.x * SEG_WAVES + wv; it < nitems; it += (int64_t)gridDim.x * SEG_WAVES) {
@@ -411,10 +414,11 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
                     for (int u = 0; u < SEG_UNROLL; u++) mq[u] = maskt[(size_t)rq[u] * 16];
 #pragma unroll
                     for (int u = 0; u < SEG_UNROLL; u++) vq[u] = f4_mask(mq[u], vq[u]);
-                } else if constexpr (MASK == 2) {
+                } else if constexpr (MASK >= 2) {
                     uint32_t mb[SEG_UNROLL];
 #pragma unroll
-                    for (int u = 0; u < SEG_UNROLL; u++) mb[u] = (uint32_t)(bitst[rq[u]] >> (4 * c));
+                    for (int u = 0; u < SEG_UNROLL; u++)
+                        mb[u] = (uint32_t)(bitst[MASK == 3 ? mrow[rq[u]] : rq[u]] >> (4 * c));
 #pragma unroll
                     for (int u = 0; u < SEG_UNROLL; u++)
                         vq[u] = make_float4(mb[u] & 1u ? vq[u].x : 0.0f, mb[u] & 2u ? vq[u].y : 0.0f,
@@ -594,7 +598,7 @@ template <int ROLE>
 hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                       const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                       int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int32_t *mark,
-                      const int32_t *hfix, int32_t *cnt, hipStream_t s) {
+                      const int32_t *hfix, int32_t *cnt, const int32_t *mrow, hipStream_t s) {
     const int64_t nitems = (nnz + L - 1) / L;
     if (cnt && nfix != nitems) return hipErrorInvalidValue;  // in-launch fix-ups: one fix row per item
     const int grid = (int)std::min<int64_t>((nitems + SEG_WAVES - 1) / SEG_WAVES, 256 * 8);
@@ -602,15 +606,18 @@ hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t
     const int32_t *hf = cnt ? hfix : nullptr;
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
     float4 *o4 = reinterpret_cast<float4 *>(out), *c4 = reinterpret_cast<float4 *>(carry);
-    if (mask && mask_bits)
+    if (mask && mask_bits && mrow)
+        hipLaunchKernelGGL((k_seg_sum<3, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, mask, src_rows, idx, key,
+                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, mrow);
+    else if (mask && mask_bits)
         hipLaunchKernelGGL((k_seg_sum<2, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, mask, src_rows, idx, key,
-                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt);
+                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, nullptr);
     else if (mask)
         hipLaunchKernelGGL((k_seg_sum<1, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, mask, src_rows, idx, key,
-                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt);
+                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, nullptr);
     else
         hipLaunchKernelGGL((k_seg_sum<0, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, nullptr, src_rows, idx,
-                           key, nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt);
+                           key, nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || nfix <= 0 || cnt) return e;
     const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);
@@ -624,13 +631,14 @@ hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                           const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
                           int64_t nfix, int T, float *out, int64_t out_rows, float *carry, int acc_out, int fill,
-                          int role, int32_t *mark, const int32_t *hfix, int32_t *cnt, hipStream_t s) {
+                          int role, int32_t *mark, const int32_t *hfix, int32_t *cnt, hipStream_t s,
+                          const int32_t *mrow) {
     hipError_t e = (acc_out || !fill) ? hipSuccess
                                       : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
     if (e != hipSuccess || nnz <= 0) return e;
 #define SEG_ROLE(R) \
     seg_launch<R>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out, out_rows, carry, \
-                  acc_out, mark, hfix, cnt, s)
+                  acc_out, mark, hfix, cnt, mrow, s)
     switch (role) {
         case 1: return SEG_ROLE(1);
         case 2: return SEG_ROLE(2);

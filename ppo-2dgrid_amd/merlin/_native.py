@@ -112,6 +112,8 @@ def lib():
                                             vp, vp]
     L.merlin_segment_sum_fused.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                            vp, vp, vp, vp]
+    L.merlin_segment_sum_mask_rows.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
+                                               vp, vp, vp, vp, vp]
     L.merlin_tower_bias_relu.argtypes = [vp, vp, i64, i32, i32, vp]
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_colsum.argtypes = [vp, i64, i32, i64, i64, i32, vp, vp]
@@ -181,7 +183,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",
     "merlin_tower_conv3_col2im_bwd_chunked", "merlin_tower_conv2_lut_rows", "merlin_tower_conv2_lut_fwd",
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
-    "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_lut_bias_relu", "merlin_minibatch_patch_maps", "merlin_tower_window_conv3",
+    "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_lut_bias_relu", "merlin_minibatch_patch_maps", "merlin_segment_sum_mask_rows", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_window_conv3_reuse", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
     "merlin_tower_codes_conv3_amax",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_segment_sum_fused", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
@@ -673,7 +675,7 @@ SEG_FUSED = True
 
 
 def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum", out=None,
-                accumulate: bool = False, carry=None, mask=None, fill: bool = True, mark=None):
+                accumulate: bool = False, carry=None, mask=None, fill: bool = True, mark=None, mask_rows=None):
     """out f32[T, out_rows, 64]: out[t][key] = the sum, in entry order, of src[t][row(e)] over
     the plan's entries e with that key (merlin.windows.SegmentPlan); row(e) = idx[e], or
     slot[idx[e] // sub] * sub + idx[e] % sub with entries whose slot is -1 skipped.  With
@@ -682,7 +684,8 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
     int64 [T, src_rows] bit words (window_conv3(bits=True)).  fill=False leaves the rows of keys
     without a live entry unwritten (merlin_segment_sum_masked).  mark (int32 [out_rows], preset to -1):
     mark[key] = key for every key that received a live entry (merlin_segment_sum_marked), the slot map of
-    a following pass over these rows."""
+    a following pass over these rows.  mask_rows (int32 [src_rows], with bit-word masks): row r's mask word is
+    mask[t][mask_rows[r]] (merlin_segment_sum_mask_rows; conv3's patch representatives)."""
     T, src_rows = int(src.shape[0]), int(src.shape[1])
     assert src.shape[2] == 64 and src.dtype == torch.float32 and src.is_contiguous()
     mask_bits = mask is not None and mask.dtype == torch.int64
@@ -707,6 +710,15 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
     if mark is not None:
         assert mark.dtype == torch.int32 and mark.shape == (out_rows,) and mark.is_contiguous()
     fused = SEG_FUSED and getattr(plan, "counters", None) is not None
+    if mask_rows is not None:
+        assert mask_bits and mask_rows.dtype == torch.int32 and mask_rows.numel() == src_rows and fused
+        with KernelTimer.span(name, nb):
+            check(lib().merlin_segment_sum_mask_rows(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key),
+                                                     plan.nnz, ptr(slot), int(sub), plan.item_len, ptr(plan.fix),
+                                                     int(plan.fix.shape[0]), T, ptr(out), int(out_rows), ptr(carry),
+                                                     flags, ptr(mark), ptr(plan.head_fix), ptr(plan.counters),
+                                                     ptr(mask_rows), stream_of(src)), "merlin_segment_sum_mask_rows")
+        return out
     with KernelTimer.span(name, nb):
         check(lib().merlin_segment_sum_fused(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key), plan.nnz,
                                              ptr(slot), int(sub), plan.item_len, ptr(plan.fix),

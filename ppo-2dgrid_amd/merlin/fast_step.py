@@ -210,6 +210,9 @@ PATCH_REUSE = "gather"
 # representatives, on the main stream).  Off: the 15-us copy beside the GEMM slowed the update, 194.8 vs 189.6 ms
 # (scripts/ab_update.py 5 6 fast,fast_maskmain), as every side-stream kernel beside the NT GEMMs has
 MASK_COPY_SIDE = False
+# with "gather": the non-representative rows' mask words are not copied at all; the patch sums (R pass) read each row's
+# word through rep_row (merlin_segment_sum_mask_rows)
+MASK_ROWS = True
 
 
 class WindowStep:
@@ -304,15 +307,16 @@ class WindowStep:
         arows = rep_row if (PATCH_REUSE == "gather" and h3 and not WGRAD_PLANES and not split_side) else None
         # with gathered rows: the representatives only here; the other rows' mask words (read by the backward's patch
         # sums) are copied on the side stream beside the forward GEMM, joined by an event before that pass
+        # MASK_ROWS: no copy at all, the patch sums read each row's mask word through its representative
         Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None, rep_row=rep_row,
-                                    copy=(0 if MASK_COPY_SIDE else 2) if arows is not None else 3)
+                                    copy=(0 if (MASK_COPY_SIDE or MASK_ROWS) else 2) if arows is not None else 3)
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
         pa3 = pdz = None
         main = torch.cuda.current_stream()
         side = self.side_stream(a3.device)
         masks_ready = None
-        if arows is not None and MASK_COPY_SIDE:
+        if arows is not None and MASK_COPY_SIDE and not MASK_ROWS:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 nat.window_conv3_copy_masks(Y3, bits, rep_row)
@@ -384,7 +388,8 @@ class WindowStep:
                 x.record_stream(side)
         if masks_ready is not None:
             main.wait_event(masks_ready)
-        dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]))
+        dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]),
+                                  mask_rows=arows if MASK_ROWS else None)
         nat.colsum(dQ.view(2, -1, 9, 64)[:, :, 0], out=g[3])  # db3: every (u, p3) has one window at tap 0
         dQ = dQ.view(2, -1, 576)
         if wh3:
@@ -401,11 +406,11 @@ class WindowStep:
         self.stage.backward()
 
 
-def _conv3_backward_bulk(plan, mb, bits, dY3, nw):
+def _conv3_backward_bulk(plan, mb, bits, dY3, nw, mask_rows=None):
     """dQ [T, nw*9, 64] of merlin.windows._conv3_backward with the minibatch's live-patch map taken from
     the update-wide array (mb.kmap, WindowPlan.update_minibatches(bulk=True))."""
     R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
-                        name="k_seg_sum_R", mask=bits, fill=False)
+                        name="k_seg_sum_R", mask=bits, fill=False, mask_rows=mask_rows)
     # band sums over the live patches, marking the bands that got one (merlin_segment_sum_marked); dQ reads only
     # those: the dead bands' rows are never zeroed (a 128-MB fill per step) nor read
     bslot = getattr(plan, "_bslot", None)

@@ -69,6 +69,7 @@ def main():
             nat.H3_HEADS_EPILOGUE = "noheadsepi" not in name
             FS.WGRAD_SIDE = "wgradmain" not in name  # the weight gradient on the main stream (no overlap)
             FS.MASK_COPY_SIDE = "maskside" in name  # the mask-word copy on the side stream
+            FS.MASK_ROWS = "maskcopy" not in name  # the mask-word copy instead of the R pass's row map
             nat.X6_NT_CFG["fwd"] = 28 if "fwd28" in name else 20
             nat.X6_NT_CFG["dgrad"] = 27 if "dgrad27" in name else 22
             nat.X6_TN_CFG = next((int(t[2:]) for t in name.split("_") if t[:2] == "tn" and t[2:].isdigit()), 0)

@@ -118,6 +118,12 @@ def test_window_conv3_patch_reuse_bitwise(device):
                 assert torch.equal(b2[:, reps], b0[:, reps]) and torch.equal(am1, am0)
                 if copy == 2:
                     assert torch.equal(b2, b0)
+                else:  # no copies: the patch sums read every row's mask word through its representative
+                    dY = torch.randn(2, n * 9, 64, device=device, generator=g)
+                    ref = nat.segment_sum(dY, plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9, mask=b0)
+                    got = nat.segment_sum(dY, plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9, mask=b2,
+                                          mask_rows=mb.rep_row)
+                    assert torch.equal(got, ref)
     assert shared > 0  # rows actually copied
 
 
