@@ -358,15 +358,12 @@ def pmc_traffic(kernel: str):
 
 
 def gather_note(name, k):
-    """k_window_conv3 reads no HBM to speak of: every output row sums 9 rows of the per-minibatch Q
-    table (~15 MB per tower, L2 / Infinity-Cache resident), so its bound is the cache gather rate
-    (MI355X_MICROARCH.md 'Indexed rows': 16.8-18.8 TB/s for L2-resident rows), not HBM."""
+    """k_window_conv3 reads little HBM: every computed output row sums 9 rows of the per-minibatch Q table (~15 MB
+    per tower, L2 / Infinity-Cache resident), so its bound is the cache gather rate (MI355X_MICROARCH.md 'Indexed
+    rows': 16.8-18.8 TB/s for L2-resident rows), not HBM.  bytes_per_launch counts the rows written (with the patch
+    reuse: the representatives', 256 + 8 B per row and tower), so 9 x that is the Q-row gather."""
     if name != "k_window_conv3":
         return {}
-    from merlin import fast_step as FS
-
-    if FS.PATCH_REUSE:  # only the patch representatives' rows are computed (their count is not read back)
-        return {"cache_gather": {"note": "patch reuse: 81 Q rows per representative row only (~1/3 of the rows)"}}
     gathered = 9 * k["bytes_per_launch"]  # ~ 9 Q rows of 256 B per written Y3 row
     tbs = gathered / (k["avg_us"] * 1e-6) / 1e12
     return {"cache_gather": {"bytes_per_launch": gathered, "achieved_tbs": round(tbs, 2),
@@ -401,21 +398,31 @@ def kernel_table(records, counts=None):
 
 
 # the MFMA each plane-form GEMM runs on (merlin._native.H3_* / X6_NT_CFG / X6_TN_CFG)
-PLANE_MFMA = {"h3": {k: "f16 32x32x16" for k in X6_GEMMS},
-              "x6": {"gemm_fc1_fwd": "bf16 32x32x16", "gemm_fc1_dgrad": "bf16 32x32x16", "gemm_wgrad": "bf16 16x16x32"}}
+PLANE_MFMA = {"h3": "f16 32x32x16", "x6": "bf16 32x32x16 (forward / input gradient), 16x16x32 (weight gradient)"}
+
+
+def plane_impl(name):
+    """'h3' / 'x6' when the span `name` was timed through that plane-form GEMM wrapper (merlin._native.H3_SPANS /
+    X6_SPANS), else None (a hipBLASLt fp32 GEMM)."""
+    from merlin import _native as nat
+
+    return "h3" if name in nat.H3_SPANS else "x6" if name in nat.X6_SPANS else None
 
 
 def roofline_of(name, k, impl=None):
     traffic = pmc_traffic(name)
-    if "tflops" in k and impl in PLANE_PRODUCTS and name in X6_GEMMS:  # fc1 on the 16-bit matrix cores
+    impl = plane_impl(name) if "tflops" in k else None
+    if impl is not None:  # fp32 products on the 16-bit matrix cores in plane form
         P = PLANE_PRODUCTS[impl]
         ex = k["tflops"] * P
         return {"kernel": name, "bound": "mfma", "achieved": round(ex, 2), "peak": BF16_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ex / BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                 "flops_per_launch": k["flops_per_launch"] * P, "avg_launch_us": k["avg_us"],
-                "launches": k["launches"], "mfma": f"{PLANE_MFMA[impl][name]}, {P} plane products per fp32 product",
-                "fp32_equivalent_tflops": k["tflops"],
-                "fp32_equivalent_frac_of_f32_peak": round(k["tflops"] / FP32_PEAK_TFLOPS, 4)}
+                "launches": k["launches"], "mfma": f"{PLANE_MFMA[impl]}, {P} plane products per fp32 product",
+                # the same rate counted in fp32 products, against the ceiling of the instructions that run
+                # (dense 16-bit MFMA peak / plane products); frac equals the executed-MFMA frac above
+                "fp32_equivalent": {"achieved": k["tflops"], "ceiling": round(BF16_PEAK_TFLOPS / P, 1),
+                                    "unit": "TFLOP/s (fp32 products)"}}
     if "tflops" in k:  # a hipBLASLt GEMM: f32 MFMA bound
         return {"kernel": name, "bound": "mfma", "achieved": k["tflops"], "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(k["tflops"] / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
@@ -623,6 +630,7 @@ def main():
         upd = 3 * args.epochs * GEMM_FWD_MACS * frac
     exec_flop_per_step = 2 * (FC_FWD_MACS + ROLLOUT_TABLE_MACS / B + upd)
     loop_tflops = value / world * exec_flop_per_step / 1e12
+    loop_peak = round(BF16_PEAK_TFLOPS / PLANE_PRODUCTS[fc1], 1) if x6 else FP32_PEAK_TFLOPS
     out = {
         "metric": "env-steps/sec (rollout+GAE+PPO update), 4096 envs, 16x16 mediumhard",
         "value": round(value, 1),
@@ -634,10 +642,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        # fp32 arithmetic throughout; fc1's GEMMs compute their fp32 products from exact three-way bf16
-        # splits of the fp32 operands on the matrix cores (error vs float64 below hipBLASLt's fp32 GEMM,
-        # tests/test_gpu_gemm.py)
+        # fp32 operands and results throughout; fc1's and the window GEMMs form their fp32 products from two f16
+        # planes per operand (h3: three f16 MFMA products; error vs float64 no larger than hipBLASLt's fp32 GEMM,
+        # tests/test_gpu_h3.py), exact to 2^-23 relative for values within 2^26 of each tensor's max |x|
         "dtype": "fp32",
+        "dtype_note": ("fp32 operands/results; GEMM products as f16 two-plane (h3) splits with per-tensor power-of-two "
+                       "scales: each value held to 2^-23 relative when within 2^26 of its tensor's max |x| (smaller "
+                       "values to 2^-50 of the max, absolute)") if fc1 == "h3" else None,
         "data": "synthetic: procedurally generated mediumhard maps (numpy-PCG64-exact, seeds 777+i), "
                 "random-init CNNActorCritic (torch seed 777), timed after the warm-up iterations",
         "config": {"workload": f"{args.difficulty} {args.size}x{args.size}, {N} envs/GPU x k_steps {T}, "
@@ -660,19 +671,22 @@ def main():
         # dominant hand-written kernel
         "roofline_handwritten": dict(roofline_of(handwritten, kernels[handwritten]),
                                      **gather_note(handwritten, kernels[handwritten])),
-        # every GEMM family timed in the loop: fc1's (x6) against the bf16 MFMA peak with the executed
-        # plane products, hipBLASLt's against the f32 MFMA peak
+        # every GEMM family timed in the loop: the plane-form ones (h3 / x6) against the 16-bit MFMA peak with the
+        # executed plane products, hipBLASLt's against the f32 MFMA peak
         "roofline_gemm": {k: roofline_of(k, v, fc1) for k, v in kernels.items() if "tflops" in v},
         # fc1's GEMM form: h3 = f16 two-plane (3 products, error below hipBLASLt's fp32 GEMM), x6 = bf16 three-plane
         "fc1_impl": fc1,
         # the env-step kernel inside the timed loop (absent when the rollout replays as a graph:
         # no per-kernel events inside it); the HBM-scale measurement is tiers.env_only_2M_envs
         "roofline_env_step": roofline_of("k_env_step", kernels["k_env_step"]) if "k_env_step" in kernels else None,
-        # whole iteration against the FP32 peak, counting the FLOPs actually executed
-        # (GEMMs of conv3/fc1/heads on the evaluated frames); the reference formulation's
-        # count is given for comparison (reference-equivalent rate = value x that)
-        "roofline_loop": {"bound": "mfma", "achieved": round(loop_tflops, 2), "peak": FP32_PEAK_TFLOPS,
-                          "unit": "TFLOP/s", "frac": round(loop_tflops / FP32_PEAK_TFLOPS, 4),
+        # whole iteration, counting the fp32 products actually computed (GEMMs of conv3 / fc1 / heads on the
+        # evaluated frames and windows), against the ceiling of the instructions that compute them: with the h3 form
+        # every such GEMM runs 3 f16 MFMA products per fp32 product, so the ceiling is the dense f16 peak / 3; the
+        # reference formulation's count is given for comparison (reference-equivalent rate = value x that)
+        "roofline_loop": {"bound": "mfma", "achieved": round(loop_tflops, 2), "peak": loop_peak,
+                          "unit": "TFLOP/s (fp32 products)", "frac": round(loop_tflops / loop_peak, 4),
+                          "peak_basis": (f"dense 16-bit MFMA {BF16_PEAK_TFLOPS:.0f} / {PLANE_PRODUCTS[fc1]} plane "
+                                         f"products per fp32 product ({fc1})") if x6 else "f32 MFMA",
                           "executed_flop_per_env_step": round(exec_flop_per_step),
                           "reference_flop_per_env_step": ref_flop_per_step,
                           "reference_equivalent_tflops": round(value / world * ref_flop_per_step / 1e12, 2)},

@@ -23,77 +23,7 @@ namespace merlin {
 namespace {
 
 constexpr int ACT_WAVES = 4;
-constexpr int MAXA = 8;
-
-__device__ __forceinline__ float relu_nan(float v) { return v != v ? v : fmaxf(v, 0.0f); }  // torch.relu keeps NaN
-
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
-    x ^= x >> 30;
-    x *= 0xbf58476d1ce4e5b9ull;
-    x ^= x >> 27;
-    x *= 0x94d049bb133111ebull;
-    x ^= x >> 31;
-    return x;
-}
-
-// uniform in (0, 1]: 53 random bits of the hash of (seed, epoch, step, env, j)
-__device__ __forceinline__ double uniform01(uint64_t seed, uint64_t epoch, uint64_t step, uint64_t env, int j) {
-    uint64_t x = mix64(seed + 0x9e3779b97f4a7c15ull);
-    x = mix64(x ^ (epoch + 0x632be59bd9b4e019ull));
-    x = mix64(x ^ (step * 0x8cb92ba72f3d8dd7ull));
-    x = mix64(x ^ (env * 0xd6e8feb86659fd93ull + (uint64_t)j));
-    return (double)((x >> 11) + 1) * (1.0 / 9007199254740992.0);
-}
-
-// acc[j < A]: the actor's head dot products, acc[MAXA]: the critic's; biases added here.  Log-softmax, argmax or the
-// exponential-race draw, action / logp / value of env k written.
-__device__ __forceinline__ void act_finish(const float (&acc)[MAXA + 1], const float *__restrict__ ba,
-                                           const float *__restrict__ bc, int A, int det, uint64_t seed, uint64_t ep,
-                                           int64_t step, int64_t env_offset, int64_t k, int64_t *__restrict__ action,
-                                           float *__restrict__ logp, float *__restrict__ value) {
-    float zl[MAXA], m = -INFINITY;
-    int amax = 0;
-#pragma unroll
-    for (int j = 0; j < MAXA; j++) {
-        zl[j] = j < A ? acc[j] + ba[j] : -INFINITY;
-        if (zl[j] > m) {  // first maximum (torch.argmax)
-            m = zl[j];
-            amax = j;
-        }
-    }
-    float s = 0.0f;
-#pragma unroll
-    for (int j = 0; j < MAXA; j++) s += j < A ? expf(zl[j] - m) : 0.0f;
-    const float lse = m + logf(s);
-    int a = amax;
-    if (!det) {
-        double best = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < MAXA; j++) {
-            if (j < A) {
-                // log(p_j / E_j) = logp_j - log(-log u)
-                const double sc = (double)(zl[j] - lse) -
-                                  log(-log(uniform01(seed, ep, (uint64_t)step, (uint64_t)(env_offset + k), j)));
-                if (sc > best) {
-                    best = sc;
-                    a = j;
-                }
-            }
-        }
-    }
-    float la = zl[0] - lse;
-#pragma unroll
-    for (int j = 1; j < MAXA; j++)
-        if (j == a) la = zl[j] - lse;
-    // non-finite logits (a diverged update): Categorical(logits) raises in the reference;
-    // here the action is the sentinel -1, which the next env step rejects
-    // (MERLIN_DEVERR_BAD_ACTION, read once per rollout by merlin_env_errors)
-    if (!isfinite(lse)) a = -1;
-    action[k] = a;
-    logp[k] = la;
-    value[k] = acc[MAXA] + bc[0];
-}
-
+constexpr int MAXA = ACT_MAXA;
 __global__ __launch_bounds__(64 * ACT_WAVES) void k_act_heads(const float4 *__restrict__ z,
                                                               const float4 *__restrict__ b4, int64_t n, int H4,
                                                               const float4 *__restrict__ wa,
@@ -147,25 +77,8 @@ __global__ __launch_bounds__(256) void k_act_draw(const float4 *__restrict__ par
                                                   float *__restrict__ logp, float *__restrict__ value) {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
-    const uint64_t ep = epoch ? (uint64_t)epoch[0] : 0ull;
-    float4 a = part[k], v = part[(int64_t)P * n + k];
-    for (int p = 1; p < P; p++) {
-        const float4 x = part[(int64_t)p * n + k], y = part[(int64_t)(P + p) * n + k];
-        a.x += x.x;
-        a.y += x.y;
-        a.z += x.z;
-        a.w += x.w;
-        v.x += y.x;
-    }
-    float acc[MAXA + 1];
-#pragma unroll
-    for (int j = 0; j <= MAXA; j++) acc[j] = 0.0f;
-    acc[0] = a.x;
-    acc[1] = a.y;
-    acc[2] = a.z;
-    acc[3] = a.w;
-    acc[MAXA] = v.x;
-    act_finish(acc, ba, bc, A, det, seed, ep, step, env_offset, k, action, logp, value);
+    const ActIn c{part, P, ba, bc, A, det, seed, epoch, step, env_offset, action, logp, value};
+    act_from_parts(c, n, k);
 }
 
 }  // namespace

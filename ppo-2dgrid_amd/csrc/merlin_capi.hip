@@ -231,7 +231,31 @@ int device_ws(DeviceWs **out) {
     return MERLIN_OK;
 }
 
+
+// zero_async's kernel: a 16-B aligned body by grid-stride uint4 stores; the unaligned head and the tail (< 16 B each)
+// by block 0's first lanes, byte stores
+__global__ void k_zero_fill(uint8_t *__restrict__ p, uint32_t head, size_t n16, uint32_t tail) {
+    uint4 *v = reinterpret_cast<uint4 *>(p + head);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+        v[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < head) p[threadIdx.x] = 0;
+        if (threadIdx.x < tail) p[head + n16 * 16 + threadIdx.x] = 0;
+    }
+}
 }  // namespace
+
+hipError_t merlin::zero_async(void *p, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    auto *b = static_cast<uint8_t *>(p);
+    size_t head = (16 - (reinterpret_cast<uintptr_t>(b) & 15)) & 15;
+    if (head > bytes) head = bytes;
+    const size_t n16 = (bytes - head) / 16;
+    const size_t tail = bytes - head - n16 * 16;
+    const int grid = (int)std::max<size_t>(1, std::min<size_t>((n16 + 255) / 256, 2048));
+    hipLaunchKernelGGL(k_zero_fill, dim3(grid), dim3(256), 0, s, b, (uint32_t)head, n16, (uint32_t)tail);
+    return hipGetLastError();
+}
 
 extern "C" {
 
@@ -348,8 +372,8 @@ int merlin_env_seed(merlin_env *e, const uint64_t *seeds, int32_t n, void *strea
     hipError_t err = hipMemcpyAsync(e->dev.rng_s, st, N * sizeof(ulonglong2), hipMemcpyHostToDevice, s);
     if (err == hipSuccess)
         err = hipMemcpyAsync(e->dev.rng_i, inc, N * sizeof(ulonglong2), hipMemcpyHostToDevice, s);
-    if (err == hipSuccess) err = hipMemsetAsync(e->dev.rng_b, 0, N * sizeof(uint2), s);
-    if (err == hipSuccess) err = hipMemsetAsync(e->dev.pg_valid, 0, N, s);  // look-ahead maps are stale
+    if (err == hipSuccess) err = merlin::zero_async(e->dev.rng_b, N * sizeof(uint2), s);
+    if (err == hipSuccess) err = merlin::zero_async(e->dev.pg_valid, N, s);  // look-ahead maps are stale
     if (err == hipSuccess) err = hipStreamSynchronize(s);  // host staging buffers are freed below
     delete[] st;
     delete[] inc;
@@ -373,7 +397,7 @@ int merlin_env_step(merlin_env *e, const int64_t *actions, int32_t n_steps, int6
     if (n_steps <= 0) return MERLIN_OK;
     if (action_stride < e->dev.n && n_steps > 1)
         return fail(MERLIN_E_INVALID, "action_stride must be >= num_envs");
-    merlin::StepOut o;
+    merlin::StepOut o{};
     o.actions = actions;
     o.action_stride = action_stride;
     o.n_steps = n_steps;
@@ -385,6 +409,36 @@ int merlin_env_step(merlin_env *e, const int64_t *actions, int32_t n_steps, int6
     o.done = done;
     o.ep_ret_out = ep_ret;
     o.ep_len_out = ep_len;
+    const bool refill = e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
+    if (refill) e->steps_since_refill = 0;
+    HIP_TRY(merlin::launch_env_step(e->dev, o, refill, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_env_act_step(merlin_env *e, const float *head_part, int32_t n_parts, const float *b_actor,
+                        const float *b_critic, int32_t act_dim, int32_t deterministic, uint64_t seed,
+                        const int64_t *epoch, int64_t step, int64_t env_offset, int64_t *action, float *logp,
+                        float *value, uint32_t *obs, float *reward, uint8_t *term, uint8_t *trunc, float *done,
+                        double *ep_ret, int32_t *ep_len, void *stream) {
+    if (!e || !head_part || !b_actor || !b_critic || !action || !logp || !value)
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (!e->has_state) return fail(MERLIN_E_INVALID, "merlin_env_act_step before merlin_env_reset");
+    if (n_parts < 1 || act_dim < 1 || act_dim > 4) return fail(MERLIN_E_INVALID, "n_parts >= 1, act_dim in [1, 4]");
+    if (!deterministic && !epoch) return fail(MERLIN_E_INVALID, "a sampled action needs the epoch counter");
+    merlin::StepOut o{};
+    o.actions = action;
+    o.action_stride = e->dev.n;
+    o.n_steps = 1;
+    o.autoreset = 1;
+    o.obs = obs;
+    o.reward = reward;
+    o.term = term;
+    o.trunc = trunc;
+    o.done = done;
+    o.ep_ret_out = ep_ret;
+    o.ep_len_out = ep_len;
+    o.act = merlin::ActIn{reinterpret_cast<const float4 *>(head_part), n_parts, b_actor, b_critic, act_dim,
+                          deterministic ? 1 : 0, seed, epoch, step, env_offset, action, logp, value};
     const bool refill = e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
     if (refill) e->steps_since_refill = 0;
     HIP_TRY(merlin::launch_env_step(e->dev, o, refill, (hipStream_t)stream));
@@ -475,7 +529,7 @@ int merlin_env_errors(merlin_env *e, uint32_t *flags, uint32_t *fallbacks, void 
     uint32_t h[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(h, e->dev.err, sizeof(h), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    HIP_TRY(hipMemsetAsync(e->dev.err, 0, sizeof(h), s));
+    HIP_TRY(merlin::zero_async(e->dev.err, sizeof(h), s));
     if (flags) *flags = h[0];
     if (fallbacks) *fallbacks = h[1];
     return MERLIN_OK;

@@ -193,8 +193,8 @@ hipError_t launch_conv1_lut_bwd(const uint32_t *codes, const int64_t *index, int
                                 const float *grad, int towers, float *dtables, float *dbias, float *slabs,
                                 int max_slabs, hipStream_t s) {
     if (n <= 0) {
-        hipError_t e = hipMemsetAsync(dtables, 0, sizeof(float) * towers * TAB, s);
-        if (e == hipSuccess) e = hipMemsetAsync(dbias, 0, sizeof(float) * towers * C1, s);
+        hipError_t e = zero_async(dtables, sizeof(float) * towers * TAB, s);
+        if (e == hipSuccess) e = zero_async(dbias, sizeof(float) * towers * C1, s);
         return e;
     }
     const int grid = (int)std::min<int64_t>(n, (int64_t)max_slabs);

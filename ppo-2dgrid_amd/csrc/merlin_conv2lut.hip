@@ -308,7 +308,7 @@ int conv2_lut_fblocks(int64_t n) {
 
 hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
                                 int towers, float *dT, void *slabs, hipStream_t s, int64_t gstride) {
-    if (n <= 0) return hipMemsetAsync(dT, 0, sizeof(float) * towers * NROW * C2, s);
+    if (n <= 0) return zero_async(dT, sizeof(float) * towers * NROW * C2, s);
     const int fblocks = conv2_lut_fblocks(n);
     auto *sl = reinterpret_cast<unsigned long long *>(slabs);
     hipLaunchKernelGGL(k_conv2_lut_hist, dim3(towers * NHCHUNK * fblocks), dim3(64 * HIST_WAVES), 0, s, codes,

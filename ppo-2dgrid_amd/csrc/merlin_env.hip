@@ -748,7 +748,10 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
     const size_t N = (size_t)E.n;
 
     for (int t = 0; t < O.n_steps; t++) {
-        const int64_t a = O.actions[(size_t)t * O.action_stride + i];
+        // merlin_env_act_step: the action is drawn here from the acting GEMM's head partials (one launch instead of
+        // k_act_draw + this kernel); otherwise read from the caller's actions
+        const int64_t a = O.act.part ? (int64_t)act_from_parts(O.act, E.n, i)
+                                     : O.actions[(size_t)t * O.action_stride + i];
         steps += 1;
         const int fx = ax + ((dir == 0) - (dir == 2));
         const int fy = ay + ((dir == 1) - (dir == 3));
@@ -900,6 +903,11 @@ static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t 
     const int nb = (E.n + SBLK - 1) / SBLK;
     if (!O.autoreset) {  // no resets: the lean kernel
         hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
+    } else if (O.act.part) {
+        // the fused draw + step of the rollout (merlin_env_act_step): a reset whose look-ahead slot is empty
+        // generates its map in this launch (the multi-step kernel's form) instead of in a k_env_fallback launch --
+        // the rollout refills every slot beside each act, so that launch found nothing to do in almost every step
+        hipLaunchKernelGGL((k_env_step<SP, false>), dim3(nb), dim3(SBLK), 0, s, E, O);
     } else if (O.n_steps == 1) {  // empty look-ahead slots reset in k_env_fallback
         hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
         hipError_t e = hipGetLastError();

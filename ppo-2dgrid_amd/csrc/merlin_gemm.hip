@@ -782,7 +782,7 @@ hipError_t launch_x6_gemm_tn(const float *A, const float *B, int64_t Kd, int M, 
                              int64_t b_stride, int splits, float *slab, float *out, int cfg, hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;
     if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
-    if (Kd <= 0) return hipMemsetAsync(out, 0, sizeof(float) * (size_t)T * M * N, s);
+    if (Kd <= 0) return zero_async(out, sizeof(float) * (size_t)T * M * N, s);
     if (cfg >= 20) {  // the 32x32x16 MFMA kernels (merlin_gemm2.hip), then the same fold
         int S = 1;
         hipError_t e = launch_x6_gemm_tn32(A, B, Kd, M, N, T, a_stride, b_stride, splits, slab, cfg, s, &S);

@@ -587,7 +587,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntpg(const float *__restr
 // counted vmcnt: the DMA of step kt + 2 stays in flight across the barrier that publishes step kt + 1.
 __device__ __forceinline__ int g_swz(int r) { return (r >> 1) & 7; }
 
-template <int BM, int BN, int WGM, int WGN, int EPI, bool KP>
+// AP: A arrives as plane images too ([M][K/8][2][8] f16, h3_split's layout: 4 B per value like fp32, so the DMA
+// addressing is the same) -- no split at all, A's fragments read like B's.
+template <int BM, int BN, int WGM, int WGN, int EPI, bool KP, bool AP = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restrict__ A, const u32x4 *__restrict__ B,
                                                            const uint32_t *__restrict__ amaxA,
                                                            const uint32_t *__restrict__ amaxB, int64_t M, int N,
@@ -679,9 +681,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
             f.a[i][0] = sAl[r * 8 + (c ^ g_swz(r))];
             f.a[i][1] = sAl[r * 8 + ((c + 1) ^ g_swz(r))];
         }
-    };
+    };  // AP: chunk c = 2 g + p is plane p of k chunk g -- the same reads give (h, l)
     // A's fragments split into planes (in place: a[i][0] = hi plane, a[i][1] = lo plane), then the MFMAs
     auto split = [&](Frag &f) {
+        if constexpr (AP) return;
 #pragma unroll
         for (int i = 0; i < TM; i++) {
             u32x4 ah, al;
@@ -1452,7 +1455,7 @@ hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, cons
     return hipGetLastError();
 }
 
-template <int BM, int BN, int WGM, int WGN, bool KP>
+template <int BM, int BN, int WGM, int WGN, bool KP, bool AP = false>
 hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                       int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
                       hipStream_t s) {
@@ -1463,11 +1466,11 @@ hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, con
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
     if (bias)
-        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
-                           bias, C, sC, tiles_n);
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP, AP>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
+                           sB, bias, C, sC, tiles_n);
     else
-        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA, sB,
-                           nullptr, C, sC, tiles_n);
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP, AP>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
+                           sB, nullptr, C, sC, tiles_n);
     return hipGetLastError();
 }
 
@@ -1568,6 +1571,15 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 30: return H3_NTG(256, 128, 4, 2, true);
         case 31: return H3_NTG(128, 192, 4, 2, true);
 #undef H3_NTG
+        // probe (round 5): A as plane images (h3_split of A with amaxA, passed as A), both operands by LDS-DMA
+#define H3_NTGP(BM, BN, WM, WN, KP) \
+    ((a_rows || head_part) ? hipErrorInvalidValue                                                  \
+            : ntg_launch<BM, BN, WM, WN, KP, true>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s))
+        case 40: return H3_NTGP(256, 128, 4, 2, true);
+        case 41: return H3_NTGP(128, 192, 4, 2, true);
+        case 42: return H3_NTGP(128, 256, 2, 4, true);
+        case 43: return H3_NTGP(256, 128, 4, 2, false);
+#undef H3_NTGP
         default: return hipErrorInvalidValue;
     }
 }

@@ -326,7 +326,7 @@ hipError_t launch_bias_relu(float *Z, const float *b, int64_t rows, int cols, in
 
 hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, int64_t rows, int cols, int T,
                                   float *dbias, float *work, hipStream_t s) {
-    if (rows <= 0) return hipMemsetAsync(dbias, 0, sizeof(float) * T * cols, s);
+    if (rows <= 0) return zero_async(dbias, sizeof(float) * T * cols, s);
     const int nblk = blocks_for(rows);
     const int64_t per = (rows + nblk - 1) / nblk;
     hipLaunchKernelGGL(k_relu_bwd_colsum, dim3(nblk, T), dim3(EBLK), 0, s, reinterpret_cast<const float4 *>(Y),
@@ -341,7 +341,7 @@ hipError_t launch_relu_bwd_colsum(const float *Y, const float *dY, float *dZ, in
 
 hipError_t launch_colsum(const float *X, int64_t rows, int cols, int64_t row_stride, int64_t tower_stride, int T,
                          float *out, float *work, hipStream_t s) {
-    if (rows <= 0) return hipMemsetAsync(out, 0, sizeof(float) * T * cols, s);
+    if (rows <= 0) return zero_async(out, sizeof(float) * T * cols, s);
     const int nblk = blocks_for(rows);
     const int64_t per = (rows + nblk - 1) / nblk;
     hipLaunchKernelGGL(k_colsum, dim3(nblk, T), dim3(EBLK), 0, s, reinterpret_cast<const float4 *>(X), rows, cols / 4,
@@ -357,9 +357,9 @@ hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dv
                            const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
                            float *work, uint32_t *amax, hipStream_t s) {
     if (n <= 0) {
-        hipError_t e = hipMemsetAsync(db4, 0, sizeof(float) * 2 * H, s);
-        if (e == hipSuccess) e = hipMemsetAsync(dwa, 0, sizeof(float) * A * H, s);
-        return e == hipSuccess ? hipMemsetAsync(dwc, 0, sizeof(float) * H, s) : e;
+        hipError_t e = zero_async(db4, sizeof(float) * 2 * H, s);
+        if (e == hipSuccess) e = zero_async(dwa, sizeof(float) * A * H, s);
+        return e == hipSuccess ? zero_async(dwc, sizeof(float) * H, s) : e;
     }
     const int nblk = blocks_for(n);
     const int64_t per = (n + nblk - 1) / nblk;

@@ -53,6 +53,120 @@ struct EnvDev {
 // step launches between two look-ahead refills (merlin_env_step)
 constexpr int REFILL_EVERY = 16;
 
+// ---------------------------------------------------------------------------------------------------------------
+// The acting tail shared by merlin_act.hip (k_act_heads, k_act_draw) and the fused draw + env step
+// (merlin_env.hip, merlin_env_act_step): log-softmax, argmax or the counter-keyed exponential-race draw.
+constexpr int ACT_MAXA = 8;
+
+
+__device__ __forceinline__ float relu_nan(float v) { return v != v ? v : fmaxf(v, 0.0f); }  // torch.relu keeps NaN
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+// uniform in (0, 1]: 53 random bits of the hash of (seed, epoch, step, env, j)
+__device__ __forceinline__ double uniform01(uint64_t seed, uint64_t epoch, uint64_t step, uint64_t env, int j) {
+    uint64_t x = mix64(seed + 0x9e3779b97f4a7c15ull);
+    x = mix64(x ^ (epoch + 0x632be59bd9b4e019ull));
+    x = mix64(x ^ (step * 0x8cb92ba72f3d8dd7ull));
+    x = mix64(x ^ (env * 0xd6e8feb86659fd93ull + (uint64_t)j));
+    return (double)((x >> 11) + 1) * (1.0 / 9007199254740992.0);
+}
+
+// acc[j < A]: the actor's head dot products, acc[ACT_MAXA]: the critic's; biases added here.  Log-softmax, argmax or the
+// exponential-race draw, action / logp / value of env k written.
+__device__ __forceinline__ int act_finish(const float (&acc)[ACT_MAXA + 1], const float *__restrict__ ba,
+                                           const float *__restrict__ bc, int A, int det, uint64_t seed, uint64_t ep,
+                                           int64_t step, int64_t env_offset, int64_t k, int64_t *__restrict__ action,
+                                           float *__restrict__ logp, float *__restrict__ value) {
+    float zl[ACT_MAXA], m = -INFINITY;
+    int amax = 0;
+#pragma unroll
+    for (int j = 0; j < ACT_MAXA; j++) {
+        zl[j] = j < A ? acc[j] + ba[j] : -INFINITY;
+        if (zl[j] > m) {  // first maximum (torch.argmax)
+            m = zl[j];
+            amax = j;
+        }
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < ACT_MAXA; j++) s += j < A ? expf(zl[j] - m) : 0.0f;
+    const float lse = m + logf(s);
+    int a = amax;
+    if (!det) {
+        double best = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < ACT_MAXA; j++) {
+            if (j < A) {
+                // log(p_j / E_j) = logp_j - log(-log u)
+                const double sc = (double)(zl[j] - lse) -
+                                  log(-log(uniform01(seed, ep, (uint64_t)step, (uint64_t)(env_offset + k), j)));
+                if (sc > best) {
+                    best = sc;
+                    a = j;
+                }
+            }
+        }
+    }
+    float la = zl[0] - lse;
+#pragma unroll
+    for (int j = 1; j < ACT_MAXA; j++)
+        if (j == a) la = zl[j] - lse;
+    // non-finite logits (a diverged update): Categorical(logits) raises in the reference;
+    // here the action is the sentinel -1, which the next env step rejects
+    // (MERLIN_DEVERR_BAD_ACTION, read once per rollout by merlin_env_errors)
+    if (!isfinite(lse)) a = -1;
+    action[k] = a;
+    logp[k] = la;
+    value[k] = acc[ACT_MAXA] + bc[0];
+    return a;
+}
+
+
+// the fused draw of merlin_env_act_step: the heads' partial dot products of the acting GEMM's epilogue
+// (part[t][p][k][4], P partials per env summed in order; tower 0: the actor's A <= 4 logits, tower 1: the critic's
+// value in .x), drawn and written to action / logp / value, the action then stepped by the same thread
+struct ActIn {
+    const float4 *part;  // null: the actions are read from StepOut::actions
+    int P;
+    const float *ba, *bc;
+    int A, det;
+    uint64_t seed;
+    const int64_t *epoch;
+    int64_t step, env_offset;
+    int64_t *action;
+    float *logp, *value;
+};
+
+__device__ __forceinline__ int act_from_parts(const ActIn &c, int64_t n, int64_t k) {
+    float4 a = c.part[k], v = c.part[(int64_t)c.P * n + k];
+    for (int p = 1; p < c.P; p++) {
+        const float4 x = c.part[(int64_t)p * n + k], y = c.part[(int64_t)(c.P + p) * n + k];
+        a.x += x.x;
+        a.y += x.y;
+        a.z += x.z;
+        a.w += x.w;
+        v.x += y.x;
+    }
+    float acc[ACT_MAXA + 1];
+#pragma unroll
+    for (int j = 0; j <= ACT_MAXA; j++) acc[j] = 0.0f;
+    acc[0] = a.x;
+    acc[1] = a.y;
+    acc[2] = a.z;
+    acc[3] = a.w;
+    acc[ACT_MAXA] = v.x;
+    const uint64_t ep = c.epoch ? (uint64_t)c.epoch[0] : 0ull;
+    return act_finish(acc, c.ba, c.bc, c.A, c.det, c.seed, ep, c.step, c.env_offset, k, c.action, c.logp, c.value);
+}
+
 struct StepOut {
     const int64_t *actions;
     int64_t action_stride;
@@ -65,8 +179,13 @@ struct StepOut {
     float *done;
     double *ep_ret_out;
     int32_t *ep_len_out;
+    ActIn act;  // act.part != null (n_steps == 1): the action of env i is drawn from the heads' partials first
 };
 
+// Zero `bytes` bytes at p on stream s with a kernel (vector stores).  Every zero-fill of the library goes
+// through this, never hipMemsetAsync: a memset node captured into a HIP graph replays with a wrong fill value on
+// ROCm 7 (scripts/probe_graph_then.py: 0x80 per byte), and any entry point may end up inside a capture.
+hipError_t zero_async(void *p, size_t bytes, hipStream_t s);
 hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s);
 hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s);
 hipError_t launch_env_full_obs(const EnvDev &E, uint8_t *out, hipStream_t s);

@@ -361,8 +361,8 @@ hipError_t launch_conv1_im2col_bwd(const uint32_t *codes, const int64_t *index, 
                                    const float *bias, const float *dA2, int T, float *dtables, float *dbias,
                                    float *slabs, int max_slabs, hipStream_t s) {
     if (n <= 0) {
-        hipError_t e = hipMemsetAsync(dtables, 0, sizeof(float) * T * TAB, s);
-        return e == hipSuccess ? hipMemsetAsync(dbias, 0, sizeof(float) * T * C1, s) : e;
+        hipError_t e = zero_async(dtables, sizeof(float) * T * TAB, s);
+        return e == hipSuccess ? zero_async(dbias, sizeof(float) * T * C1, s) : e;
     }
     const int grid = (int)std::min<int64_t>((n + BWD_WAVES - 1) / BWD_WAVES, (int64_t)max_slabs);
     hipLaunchKernelGGL(k_conv1_im2col_bwd, dim3(grid), dim3(64 * BWD_WAVES), 0, s, codes, index, n, tables, bias,
@@ -384,7 +384,7 @@ hipError_t launch_im2col3_fwd(const float *Z2, const float *b2, int64_t n, int T
 hipError_t launch_col2im3_bwd(const float *dA3, const float *Z2, const float *b2, int64_t n, int T, int chunked,
                               float *dZ2, uint32_t *absmax, hipStream_t s) {
     if (chunked) {
-        hipError_t e = hipMemsetAsync(absmax, 0, sizeof(uint32_t), s);
+        hipError_t e = zero_async(absmax, sizeof(uint32_t), s);
         if (e != hipSuccess || n <= 0) return e;
         const int64_t groups = (n + CF - 1) / CF;
         hipLaunchKernelGGL(k_col2im3_bwd_chunked, dim3(grid_cap((int64_t)T * groups)), dim3(BLK), 0, s,

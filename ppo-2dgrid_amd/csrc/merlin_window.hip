@@ -469,6 +469,14 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
             __hip_atomic_store(cr + 33, __builtin_bit_cast(uint64_t, make_float2(tail.z, tail.w)), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
+        // Memory-model note: the publish / count pair is relaxed on purpose.  Its ordering rests on two
+        // gfx950 facts -- vector stores are counted by vmcnt, so the wait below retires the carry stores before the
+        // counter's fetch_add issues, and agent-scope (sc1) stores and loads go through to the coherence point that
+        // every XCD's L2 sees -- not on a release / acquire pair: an agent-scope release here is an L2 write-back per
+        // item (buffer_wbl2), measured in round 3 at 265 -> 495 ms per update.  Other targets are refused below.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "k_seg_sum's in-launch fix-ups rely on gfx950's vmcnt-counted stores and sc1 write-through (see above)"
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int f0 = hfix[it];
         const int f1 = fix[it].x >= 0 ? (int)it : -1;
@@ -634,7 +642,7 @@ hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int
                           int role, int32_t *mark, const int32_t *hfix, int32_t *cnt, hipStream_t s,
                           const int32_t *mrow) {
     hipError_t e = (acc_out || !fill) ? hipSuccess
-                                      : hipMemsetAsync(out, 0, sizeof(float) * 64 * (size_t)T * out_rows, s);
+                                      : zero_async(out, sizeof(float) * 64 * (size_t)T * out_rows, s);
     if (e != hipSuccess || nnz <= 0) return e;
 #define SEG_ROLE(R) \
     seg_launch<R>(src, mask, mask_bits, src_rows, idx, key, nnz, slot, S, L, fix, nfix, T, out, out_rows, carry, \

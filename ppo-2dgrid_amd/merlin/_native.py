@@ -72,6 +72,8 @@ def lib():
     L.merlin_env_seed.argtypes = [vp, u64p, i32, vp]
     L.merlin_env_reset.argtypes = [vp, vp, vp, vp]
     L.merlin_env_step.argtypes = [vp, vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, i32, vp]
+    L.merlin_env_act_step.argtypes = [vp, vp, i32, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp, vp, vp,
+                                      vp, vp, vp, vp, vp, vp]
     L.merlin_env_set_refill_interval.argtypes = [vp, i32]
     L.merlin_env_refill.argtypes = [vp, vp]
     L.merlin_env_get_state.argtypes = [vp, vp, vp, vp, vp]
@@ -175,7 +177,7 @@ def check_env_config_layout(L) -> None:
 
 EXPORTED_SYMBOLS = (
     "merlin_version", "merlin_last_error", "merlin_tile_atlas", "merlin_env_config_layout", "merlin_env_create",
-    "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step",
+    "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step", "merlin_env_act_step",
     "merlin_env_set_refill_interval", "merlin_env_refill",
     "merlin_env_get_state", "merlin_env_full_obs", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
     "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
@@ -210,6 +212,7 @@ def capture_guard():
     the collector off until the capture ends, and have native handles released while a capture is open
     (merlin.envs.MerlinVecEnv.close) queue their release until it has ended."""
     global _CAPTURE_DEPTH
+    drain_deferred()
     gc.collect()
     was_enabled = gc.isenabled()
     gc.disable()
@@ -235,16 +238,31 @@ def capturing() -> bool:
 
 
 def defer_release(fn) -> None:
-    """Run `fn` (a native release: hipFree underneath) now, or after the open capture ends."""
+    """Run `fn` (a native release: hipFree underneath) now, or after the open capture ends.  Releases queued during a
+    capture outside capture_guard (a user's own torch.cuda.graph) run at the next call here, at the next env creation
+    or capture_guard entry -- whichever comes first with no capture open."""
     if capturing():
         _DEFERRED.append(fn)
     else:
+        run_deferred()
         fn()
 
 
 def run_deferred() -> None:
     while _DEFERRED:
         _DEFERRED.pop(0)()
+
+
+def drain_deferred() -> None:
+    """Run the queued releases if no capture is open now."""
+    if _DEFERRED and not capturing():
+        run_deferred()
+
+
+# span names of the GEMMs timed through the plane-form wrappers (h3 / x6): bench.py prices them against the 16-bit
+# MFMA peak with their plane products counted, every other GEMM span against the f32 MFMA peak
+H3_SPANS: set = set()
+X6_SPANS: set = set()
 
 
 class KernelTimer:
@@ -264,8 +282,14 @@ class KernelTimer:
 
     @classmethod
     def stop(cls):
+        """The records, with byte counts given as callables (known on the device only, e.g. conv3's representative
+        rows per minibatch) resolved now, after the timed region."""
         recs, cls.records = cls.records, None
-        return recs or []
+        return [(n, e0, e1, nb() if callable(nb) else nb, fl) for n, e0, e1, nb, fl in (recs or [])]
+
+    @classmethod
+    def active(cls) -> bool:
+        return cls.records is not None
 
     @classmethod
     def span(cls, name: str, nbytes: int, flops: int = 0):
@@ -569,7 +593,7 @@ def window_lut(rows, tables, bias=None):
 
 
 def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None, amax=None, rep_row=None,
-                 copy: int = 3):
+                 copy: int = 3, n_reps=None):
     """Y3 f32[T, n*9, 64] = relu(conv3) rows (k, p3) of frames groups[k] from
     Q f32[T, nw, 576], the per-window, per-tap conv3 partial sums (merlin/windows.py).
     bits: also return the rows' ReLU masks, int64[T, n*9] (bit co = Y3 > 0).  rows >= n: the
@@ -577,7 +601,12 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
     zeroed by the caller, receives max |Y3| per tower as float bits (h3_amax's format).
     rep_row (int32 [n*9], MinibatchWindows.rep_row: per row, a row holding the same 5x5-tile patch): each distinct
     patch of the rows computed once and copied to the rows sharing it (merlin_tower_window_conv3_reuse; same
-    outputs); copy (bit 0 Y3 rows, bit 1 mask words) < 3 leaves the other rows' Y3 / masks unwritten."""
+    outputs); copy (bit 0 Y3 rows, bit 1 mask words) < 3 leaves the other rows' Y3 / masks unwritten: THE RETURNED
+    Y3 / MASK THEN HOLD VALID DATA ONLY IN THE REPRESENTATIVE ROWS (rep_row[r] == r) -- read row r as
+    Y3[:, rep_row[r]] (the gathered-row GEMMs and merlin_segment_sum_mask_rows do); with POISON_PARTIAL set, the
+    unwritten rows are filled with NaN / all-ones words first, so a direct reader shows up in tests.
+    n_reps (int32/int64 0-dim device tensor, MinibatchWindows.n_reps, bench timing only): the number of
+    representative rows, for the span's algorithmic bytes (256 + 8 B per representative row and tower)."""
     T, nw = int(Q.shape[0]), int(Q.shape[1])
     n = int(groups.numel())
     R = n if rows is None else int(rows)
@@ -592,7 +621,15 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
         assert bits and R == n and T <= 2
         assert rep_row.dtype == torch.int32 and rep_row.is_contiguous() and rep_row.numel() == n * 9
         mask = torch.empty((T, R * 9), dtype=torch.int64, device=Q.device)
-        with KernelTimer.span("k_window_conv3", T * n * 9 * 264 + n * 144 + T * nw * 576 * 4):
+        if POISON_PARTIAL and copy < 3:
+            out.fill_(float("nan"))
+            mask.fill_(-1)
+        fixed = n * 144 + T * nw * 576 * 4  # ids (window ids, group, rep_row) + Q read once
+        if copy < 3 and n_reps is not None:  # only the representatives' rows are computed and written
+            nb = (lambda: T * int(n_reps) * 264 + fixed)
+        else:
+            nb = T * n * 9 * 264 + fixed
+        with KernelTimer.span("k_window_conv3", nb):
             check(lib().merlin_tower_window_conv3_reuse(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
                                                         ptr(mask), ptr(amax), ptr(rep_row), int(copy),
                                                         stream_of(Q)),
@@ -612,6 +649,8 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
 
 
 ALL_WINDOWS = 5 ** 9  # merlin_tower_all_windows()
+# debug: window_conv3 fills the rows it leaves unwritten (copy < 3) with NaN / all-ones mask words
+POISON_PARTIAL = os.environ.get("MERLIN_POISON_PARTIAL", "0") == "1"
 
 
 def minibatch_patch_maps(kid, group_keys, num_frames, group_offsets, nmb, num_patches):
@@ -711,12 +750,13 @@ def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "
         assert mark.dtype == torch.int32 and mark.shape == (out_rows,) and mark.is_contiguous()
     fused = SEG_FUSED and getattr(plan, "counters", None) is not None
     if mask_rows is not None:
-        assert mask_bits and mask_rows.dtype == torch.int32 and mask_rows.numel() == src_rows and fused
+        assert mask_bits and mask_rows.dtype == torch.int32 and mask_rows.numel() == src_rows
         with KernelTimer.span(name, nb):
             check(lib().merlin_segment_sum_mask_rows(ptr(src), ptr(mask), src_rows, ptr(plan.idx), ptr(plan.key),
                                                      plan.nnz, ptr(slot), int(sub), plan.item_len, ptr(plan.fix),
                                                      int(plan.fix.shape[0]), T, ptr(out), int(out_rows), ptr(carry),
-                                                     flags, ptr(mark), ptr(plan.head_fix), ptr(plan.counters),
+                                                     flags, ptr(mark), ptr(plan.head_fix) if fused else None,
+                                                     ptr(plan.counters) if fused else None,
                                                      ptr(mask_rows), stream_of(src)), "merlin_segment_sum_mask_rows")
         return out
     with KernelTimer.span(name, nb):
@@ -918,6 +958,7 @@ def x6_gemm_nt(A: torch.Tensor, B: torch.Tensor, bias: torch.Tensor | None = Non
                out: torch.Tensor | None = None, name: str = "x6_gemm_nt") -> torch.Tensor:
     """C f32[T, M, N] = A @ B^T per tower (+ bias[t] and ReLU when bias is given), A f32[T, M, K],
     B planes int16[T, N, 3K] (x6_split of an f32 [T, N, K])."""
+    X6_SPANS.add(name)
     T, M, K = (int(v) for v in A.shape)
     if A.dtype == torch.int16:  # A as planes too (x6_split of an f32 [T, M, K]): the cfg >= 30 kernels
         assert cfg >= 30 and K % 24 == 0, "planes A needs an x6 planes-A configuration (cfg >= 30)"
@@ -943,6 +984,7 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
                name: str = "x6_gemm_tn", out: torch.Tensor | None = None) -> torch.Tensor:
     """out f32[T, M, N] = A^T @ B per tower, A f32[T, Kd, M], B f32[T, Kd, N] (the long k range split
     into `splits` slabs summed in order)."""
+    X6_SPANS.add(name)
     splits = X6_TN_SPLITS if splits is None else splits  # module settings read at call time
     cfg = X6_TN_CFG if cfg is None else cfg
     T, Kd, M = (int(v) for v in A.shape)
@@ -1022,6 +1064,7 @@ def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
     receives A's planes (h3_split(A, amaxA), made by the kernel while it stages A) for a later h3_gemm_tn.
     rows int32[M * K / 64] (merlin_h3_gemm_nt_gather, pipelined cfgs): A read by 64-value chunks, row m's chunk j
     from row rows[m * K / 64 + j] of A viewed as [T, M * K / 64, 64] (conv3's patch representatives)."""
+    H3_SPANS.add(name)
     T, M, K = (int(v) for v in A.shape)
     N = int(B.shape[1])
     assert A.dtype == torch.float32 and B.dtype == torch.int16 and B.shape == (T, N, 2 * K)
@@ -1057,6 +1100,7 @@ def h3_gemm_nt_heads(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amax
     epilogue (merlin_h3_gemm_nt_heads) and summed in order (merlin_heads_combine, span "k_heads_fwd").
     partials_only: h is not written and the heads' partials float[2, parts, M, 4] are returned as they are (for
     act_draw)."""
+    H3_SPANS.add(name)
     T, M, K = (int(v) for v in A.shape)
     N = int(B.shape[1])
     NA = int(Wa.shape[0])
@@ -1113,6 +1157,7 @@ def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
     (h3_gemm_nt's planes_out of the same tensors and scales): the same product without splitting them again.
     rows int32[Kd * N / 64] (merlin_h3_gemm_tn_gather, cfgs 0-2): B read by 64-value chunks, row k's chunk j from row
     rows[k * N / 64 + j] of B viewed as [T, Kd * N / 64, 64]."""
+    H3_SPANS.add(name)
     splits = H3_TN_SPLITS if splits is None else splits
     cfg = H3_TN_CFG if cfg is None else cfg
     planes = A.dtype == torch.int16

@@ -563,7 +563,7 @@ class CNNActorCritic(nn.Module):
             pack["b2"] = torch.stack([ea[2].bias, ec[2].bias]).contiguous()
             # im2col rows of A3 are (ky, kx, ci): conv3 weights as [2, 576, 64] in that order
             pack["W3t"] = torch.stack([ea[4].weight, ec[4].weight]).permute(0, 3, 4, 2, 1).reshape(2, 576, 64).contiguous()
-        if self.fc1_impl == "h3" and all_windows and ROLLOUT_FC1_H3:  # fc1 of every step on merlin_h3.hip
+        if self.fc1_impl == "h3" and ROLLOUT_FC1_H3:  # fc1 of every step on merlin_h3.hip, either conv3 layout
             amW = nat.h3_amax(W4p.contiguous())
             pack["W4h"] = (nat.h3_split(W4p.contiguous(), amW), amW)
             # per step: max |a3| per tower, one row per step of the rollout when the caller says how many (all zeroed
@@ -577,21 +577,35 @@ class CNNActorCritic(nn.Module):
         return pack
 
     def _use_all_windows(self, frames, device) -> bool:
+        """The acting layout from the rollout's frame count and the device's total memory only (not the memory
+        free at the time: the same seed must act through the same layout whatever else is allocated, and every
+        DP rank decides alike); PPO records the choice (PPO.rollout_all_windows, the bench line's
+        rollout_acting)."""
         if frames is not None and frames < self.ALL_WINDOWS_MIN_FRAMES:
             return False
         try:
-            free, _ = torch.cuda.mem_get_info(device)
+            _, total = torch.cuda.mem_get_info(device)
         except Exception:
             return True
-        return free >= (12 << 30)
+        return total >= (64 << 30)
 
     @torch.no_grad()
-    def act_codes_packed(self, codes, pack, deterministic=False, seed=0, epoch=None, step=0, out=None, env_offset=0):
+    def heads_partials_ok(self, pack) -> bool:
+        """The acting GEMM can leave the heads' partial dot products (h3 fc1 with the heads epilogue), so the draw
+        can run elsewhere (act_draw, or fused into the env step: MerlinVecEnv.act_step_into)."""
+        from . import _native as nat
+
+        return ("W4h" in pack and nat.H3_HEADS_EPILOGUE and self.actor[2].weight.shape[0] <= 4 and
+                nat.lib().merlin_h3_heads_parts(pack["W4h"][0].shape[1], nat.H3_NT_CFG["rollout"]) > 0)
+
+    def act_codes_packed(self, codes, pack, deterministic=False, seed=0, epoch=None, step=0, out=None, env_offset=0,
+                         partials=False):
         """act_codes with the layouts of rollout_pack(): conv1+conv2+conv3 from the all-windows
         table (merlin_tower_codes_conv3: 81 table rows per frame and tower), fc1 as a plain bmm,
         then fc1's bias/ReLU, the heads, the log-probs and the categorical draw in one HIP pass
         (merlin_act_heads; draws keyed by (seed, epoch[0], step, env_offset + env)).
-        out = (action, logp, value) tensors to write in place."""
+        out = (action, logp, value) tensors to write in place.  partials=True: return the heads' partial dot
+        products f32[2, P, n, 4] instead of drawing (heads_partials_ok packs only)."""
         from . import _native as nat
         from .gemm_tuning import tuned
 
@@ -607,14 +621,18 @@ class CNNActorCritic(nn.Module):
         else:  # per-frame conv2 lookups + conv3 GEMM (small rollouts, rollout_pack)
             A3 = nat.conv3_im2col_fwd(nat.conv2_lut_fwd(codes, None, pack["T2"]), pack["b2"])
             a3 = nat.bias_relu_(torch.bmm(A3, pack["W3t"]), pack["b3"]).view(2, n, 576)
-        if "W4h" in pack and nat.H3_HEADS_EPILOGUE and self.actor[2].weight.shape[0] <= 4 and \
-                nat.lib().merlin_h3_heads_parts(pack["W4h"][0].shape[1], nat.H3_NT_CFG["rollout"]) > 0:
+            if am3 is not None:  # fc1 on h3: the operand scale of this step's a3 (zeroed by a kernel inside)
+                am3 = nat.h3_amax(a3, out=am3)
+        if self.heads_partials_ok(pack):
             # fc1 + bias + ReLU + both heads in the GEMM's epilogue (h never written), then the draw from the sums
             P4, amW = pack["W4h"]
             part = nat.h3_gemm_nt_heads(a3, am3, P4, amW, pack["b4"], self.actor[2].weight, self.critic[2].weight,
                                         cfg=nat.H3_NT_CFG["rollout"], name="gemm_rollout_fc1", partials_only=True)
+            if partials:  # the caller draws (merlin_env_act_step: the draw fused into the env step)
+                return part
             return nat.act_draw(part, self.actor[2].bias, self.critic[2].bias, deterministic, seed=seed, epoch=epoch,
                                 step=step, out=out, env_offset=env_offset)
+        assert not partials, "head partials need the h3 acting GEMM with the heads epilogue (heads_partials_ok)"
         if "W4h" in pack:
             P4, amW = pack["W4h"]
             z = nat.h3_gemm_nt(a3, am3, P4, amW, cfg=nat.H3_NT_CFG["rollout"], name="gemm_rollout_fc1")

@@ -83,6 +83,7 @@ class MerlinVecEnv:
                             int(stuck_penalty), int(max_stay), float(penalty), int(exploration_bonus),
                             float(bonus), int(reseed_each_reset))
         self._lib = nat.lib()
+        nat.drain_deferred()  # releases queued by a capture outside capture_guard (merlin._native.defer_release)
         with torch.cuda.device(self.device):
             h = C.c_void_p()
             nat.check(self._lib.merlin_env_create(C.byref(cfg), C.byref(h)), "merlin_env_create")
@@ -177,6 +178,27 @@ class MerlinVecEnv:
                 self._h, nat.ptr(actions), int(n_steps), stride, nat.ptr(obs_out), nat.ptr(reward),
                 nat.ptr(term), nat.ptr(trunc), nat.ptr(done), nat.ptr(ep_return), nat.ptr(ep_length),
                 int(bool(autoreset)), self._stream), "merlin_env_step")
+
+    def act_step_into(self, part: torch.Tensor, b_actor: torch.Tensor, b_critic: torch.Tensor, out, obs_out=None,
+                      reward=None, term=None, trunc=None, done=None, ep_return=None, ep_length=None,
+                      deterministic: bool = False, seed: int = 0, epoch=None, step: int = 0) -> None:
+        """act -> step in one launch (merlin_env_act_step): the actions drawn from the acting GEMM's head partials
+        part f32[2, P, N, 4] (merlin._native.h3_gemm_nt_heads(partials_only=True)) exactly as merlin._native.act_draw
+        draws them, written to out = (action, logp, value), then one auto-reset step into the other buffers."""
+        action, logp, value = out
+        P = int(part.shape[1])
+        A = int(b_actor.numel())
+        assert part.dtype == torch.float32 and part.is_contiguous() and part.shape == (2, P, self.num_envs, 4)
+        assert action.dtype == torch.int64 and action.numel() == logp.numel() == value.numel() == self.num_envs
+        assert b_critic.numel() == 1 and 1 <= A <= 4
+        if not deterministic and epoch is None:
+            raise ValueError("act_step_into: a sampled action needs an epoch counter tensor (int64[1] on the device)")
+        with torch.cuda.device(self.device), nat.KernelTimer.span("k_env_step", self.num_envs * ENV_STEP_BYTES):
+            nat.check(self._lib.merlin_env_act_step(
+                self._h, nat.ptr(part), P, nat.ptr(b_actor), nat.ptr(b_critic), A, int(bool(deterministic)),
+                int(seed) & 0xFFFFFFFFFFFFFFFF, nat.ptr(epoch), int(step), int(self.env_offset), nat.ptr(action),
+                nat.ptr(logp), nat.ptr(value), nat.ptr(obs_out), nat.ptr(reward), nat.ptr(term), nat.ptr(trunc),
+                nat.ptr(done), nat.ptr(ep_return), nat.ptr(ep_length), self._stream), "merlin_env_act_step")
 
     def set_refill_interval(self, every: int) -> None:
         """Refill the used look-ahead map slots every `every` step calls (default 16); 0 leaves the

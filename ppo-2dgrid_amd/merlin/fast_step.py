@@ -309,7 +309,8 @@ class WindowStep:
         # sums) are copied on the side stream beside the forward GEMM, joined by an event before that pass
         # MASK_ROWS: no copy at all, the patch sums read each row's mask word through its representative
         Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None, rep_row=rep_row,
-                                    copy=(0 if (MASK_COPY_SIDE or MASK_ROWS) else 2) if arows is not None else 3)
+                                    copy=(0 if (MASK_COPY_SIDE or MASK_ROWS) else 2) if arows is not None else 3,
+                                    n_reps=getattr(mb, "n_reps", None))
         n = int(mb.groups.numel())
         a3 = Y3.view(2, n, 576)
         pa3 = pdz = None

@@ -22,7 +22,7 @@ usual path.  Nothing is timed or written at run time.  The file's validator line
 HIP / hipBLASLt / rocBLAS versions, gfx950) make TunableOp reject it on any other stack.
 MERLIN_GEMM_TUNING=0 switches it off; MERLIN_UNTUNED=rollout,dgrad,window switches groups off.
 The file is loaded lazily, by the first GEMM that asks for it (`tuned()` / `padded_*`): the default
-training path (x6 fc1, all-windows acting table) never does, so TunableOp stays off there."""
+training path (h3 fc1 and window GEMMs, all-windows acting table) never does, so TunableOp stays off there."""
 from __future__ import annotations
 
 import contextlib

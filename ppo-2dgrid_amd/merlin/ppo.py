@@ -72,6 +72,10 @@ class _PPOLoss(torch.autograd.Function):
 # the acting path's fc1 operand scales: one row per rollout step, all zeroed by one kernel when the rollout starts
 # (False: one row zeroed by a kernel before every step -- 256 more launches per captured rollout)
 ROLLOUT_SCALE_ROWS = True
+# the rollout's draw from the acting GEMM's head partials fused into the env step (merlin_env_act_step; False:
+# k_act_draw + merlin_env_step + k_env_fallback, three launches per step instead of one)
+FUSE_ACT_STEP = True
+
 
 class PPO:
     def __init__(self, env, lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=10,
@@ -243,13 +247,24 @@ class PPO:
                                          steps=T + 1 if ROLLOUT_SCALE_ROWS else None)
                     if self.conv1_from_codes else None)
             pending = False
+            # the draw fused into the env step (merlin_env_act_step): one launch fewer per step
+            fused = FUSE_ACT_STEP and pack is not None and self.ac.heads_partials_ok(pack)
             for t in range(T):
-                self._act(buf.codes[t], pack, t, out=(buf.actions[t], buf.logprobs[t], buf.values[t]))
+                if fused:
+                    part = self.ac.act_codes_packed(buf.codes[t], pack, step=t, partials=True)
+                else:
+                    self._act(buf.codes[t], pack, t, out=(buf.actions[t], buf.logprobs[t], buf.values[t]))
                 if pending:
                     main.wait_stream(side)
                     pending = False
-                env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
-                              buf.ep_return[t], buf.ep_length[t])
+                if fused:
+                    env.act_step_into(part, self.ac.actor[2].bias, self.ac.critic[2].bias,
+                                      (buf.actions[t], buf.logprobs[t], buf.values[t]), buf.codes[t + 1],
+                                      buf.rewards[t], None, None, buf.dones[t], buf.ep_return[t], buf.ep_length[t],
+                                      seed=self._act_seed, epoch=self._act_epoch, step=t)
+                else:
+                    env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
+                                  buf.ep_return[t], buf.ep_length[t])
                 if side is not None and (t % every == every - 1 or t == T - 1):
                     side.wait_stream(main)
                     with torch.cuda.stream(side):

@@ -7,8 +7,9 @@ RGBImgPartialObsWrapper -> ImgObsWrapper -> ThreeActionWrapper (scenario_creator
 Like the reference, ``seed`` does not seed the env (scenario_creator.py:35-57 ignores
 it); seed through ``env.reset(seed=...)``.
 ``create_vec_env(difficulty, num_envs, seed, ...)`` builds the GPU vector env used by
-the fast path.  Only the RGB partial-observation mode exists (fully_observable /
-flatten are rejected: no BASELINE config uses them).
+the fast path.  The single env also takes the config's other observation modes
+(``fully_observable``: the encoded grid; ``flatten``: the flattened RGB view, PPO's MLP path,
+src/ppo.py:38-41); the batched vector env refuses them (its CNN path needs the (56, 56, 3) view).
 """
 from __future__ import annotations
 

@@ -320,6 +320,9 @@ class WindowPlan:
         # same patch -- which one wins does not matter, they compute the same bits): two launches over the G * 9
         # (group, position)s (merlin_minibatch_patch_maps; the torch scatter / gather chain took ~3.6 ms per update)
         kmap, rep_row = nat.minibatch_patch_maps(self.kid, uniq, F, goff, nmb, K)
+        # bench timing only: representative rows per minibatch = its distinct patches (the k_window_conv3 span's
+        # algorithmic bytes; one reduction per update, read back after the timed region)
+        n_reps = (kmap >= 0).sum(dim=1) if nat.KernelTimer.active() else None
         out = []
         for m, c in enumerate(counts):
             g0 = goff_h[m]
@@ -327,6 +330,7 @@ class WindowPlan:
                                   offs[g0 + m:g0 + m + c + 1])
             mw.kmap = kmap[m]
             mw.rep_row = rep_row[g0 * 9:(g0 + c) * 9]
+            mw.n_reps = n_reps[m] if n_reps is not None else None
             out.append(mw)
         return out
 

@@ -2,9 +2,13 @@
 
     python scripts/prof_summary.py <tag> [dest]
 writes <dest, default profiles>/<tag>_kernel_stats.md (+ .csv copy) from the --kernel-trace --stats pass and
-profiles/<tag>_pmc.json from the FETCH_SIZE / WRITE_SIZE passes: per kernel, the mean over
-its largest-grid launches, HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950:
-FETCH_SIZE counts half of a wide coalesced read stream, MI355X_MICROARCH.md §HBM).
+profiles/<tag>_pmc.json from the FETCH_SIZE / WRITE_SIZE passes: per kernel, the mean over its launches,
+HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half of a wide coalesced read
+stream, MI355X_MICROARCH.md §HBM).
+PMC_TIMED_FRAC (env, default 1): keep only the last fraction of each kernel's launches, in dispatch order -- with
+the bench run as `--steps K --warmup W --no-tiers --no-cpu-baseline` that is K / (K + W), the launches of the timed
+iterations, so the kernel times and PMC bytes describe the same training state as the bench line's HIP events
+(the update's work grows with the distinct frames per minibatch as the policy trains).
 """
 import csv
 import re
@@ -15,6 +19,17 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
+TIMED_FRAC = float(os.environ.get("PMC_TIMED_FRAC", "1"))
+
+
+def timed_tail(vals):
+    """The last TIMED_FRAC of a kernel's launches (in dispatch order)."""
+    import math
+
+    k = max(1, math.ceil(len(vals) * TIMED_FRAC))
+    return vals[-k:]
+
+
 DEST = os.path.join(REPO, "profiles")
 
 
@@ -31,18 +46,21 @@ def kname(raw):
 def stats(tag):
     """Per-kernel table from the per-dispatch kernel trace (untruncated names), plus the ordered
     launches of one optimizer step (scripts/kernel_sequence.py)."""
-    src = os.path.join(OUT, "prof_trace", "run_kernel_trace.csv")
+    src = os.path.join(OUT, os.environ.get("PROF_TRACE_DIR", "prof_trace"), "run_kernel_trace.csv")
     if not os.path.exists(src):
         return
-    agg = {}
+    per = {}
     for r in csv.DictReader(open(src)):
-        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        a = agg.setdefault(kname(r["Kernel_Name"]), [0, 0])
-        a[0] += 1
-        a[1] += d
+        per.setdefault(kname(r["Kernel_Name"]), []).append(
+            (int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    agg = {}
+    for k, v in per.items():
+        v = timed_tail(sorted(v))
+        agg[k] = [len(v), sum(d for _, d in v)]
     rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
     tot = sum(v[1] for v in agg.values())
-    lines = [f"# {tag}: rocprofv3 --kernel-trace of `bench.py` (per-dispatch durations, untruncated names)", "",
+    scope = "every launch" if TIMED_FRAC >= 1 else f"the last {TIMED_FRAC:.3f} of each kernel's launches (timed iterations)"
+    lines = [f"# {tag}: rocprofv3 --kernel-trace of `bench.py` (per-dispatch durations, untruncated names; {scope})", "",
              f"total kernel time {tot / 1e6:.1f} ms", "",
              "| kernel | calls | total ms | % | avg us |", "|---|---|---|---|---|"]
     os.makedirs(DEST, exist_ok=True)
@@ -85,12 +103,12 @@ def collect(res, src, counter, rename):
     for r in csv.DictReader(open(src)):
         name = kname(r["Kernel_Name"])
         name = rename.get(name, name)
-        per.setdefault(name, []).append((int(r["Grid_Size"]), float(r["Counter_Value"])))
+        per.setdefault(name, []).append((int(r["Dispatch_Id"]), int(r["Grid_Size"]), float(r["Counter_Value"])))
     for k, vals in per.items():
-        g = max(v[0] for v in vals)
-        big = [v[1] for v in vals if v[0] == g]
-        d = res.setdefault(k, {"grid": g, "launches": len(big)})
-        d[counter.lower() + "_kb"] = sum(big) / len(big)
+        vals = timed_tail(sorted(vals))  # dispatch order; the timed iterations' launches
+        d = res.setdefault(k, {"grid_max": max(v[1] for v in vals), "launches": len(vals),
+                               "timed_frac": TIMED_FRAC})
+        d[counter.lower() + "_kb"] = sum(v[2] for v in vals) / len(vals)
 
 
 if __name__ == "__main__":

@@ -41,3 +41,24 @@ def test_bench_two_ranks_on_one_gpu_ends_with_one_line():
         assert len(ranks[k]) == 2, (k, ranks)
     # whole-job rate: both ranks' env-steps over the max-over-ranks time
     assert abs(out["value"] - 2 * 2 * 256 * 16 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 0.01
+
+
+def test_bench_eight_ranks_on_one_gpu_ends_with_one_line():
+    """Round-4 verdict item 1: bench.py's launch form for cfg 3 at its world size (8 ranks through
+    torch.distributed.run, gloo, all on device 0) at a small per-rank shape: one JSON line, 8 entries per rank
+    field."""
+    env = dict(os.environ, MERLIN_DIST_BACKEND="gloo", MERLIN_BENCH_DEVICE="0", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "2", "--warmup", "1",
+           "--num-envs", "128", "--k-steps", "16", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-4000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8"
+    assert out["config"]["global_batch"] == 8 * 128 * 16
+    for k in ("rollout_ms", "update_ms", "kernel_ms_per_iter", "distinct_frames_per_sample"):
+        assert len(out["ranks"][k]) == 8, (k, out["ranks"])
+    assert abs(out["value"] - 2 * 8 * 128 * 16 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 0.01

@@ -144,3 +144,89 @@ def test_captured_scale_reduction_replays_correctly(device):
     torch.cuda.synchronize()
     want = torch.tensor([[k + 1.0, (k + 1.0) / 2] for k in range(20)], device=device)
     assert torch.equal(R.view(torch.float32), want)
+
+
+def _zero_branch_cases(device):
+    """Every library entry point that zero-fills an output without running its main kernel (empty row / frame /
+    entry lists, K = 0, or the chunked conv3 backward's scale word), as (name, fn) with fn() -> output tensors."""
+    from merlin import _native as nat
+    from merlin.windows import SegmentPlan
+
+    f32 = dict(dtype=torch.float32, device=device)
+    codes = torch.zeros((4, nat.OBS_WORDS), dtype=torch.int32, device=device)
+    T, H, A = 2, 512, 3
+    outs = {
+        "colsum": torch.empty((T, 64), **f32),
+        "relu_bwd_bias": torch.empty((T, 64), **f32),
+        "head_b": torch.empty((2, H), **f32), "head_wa": torch.empty((A, H), **f32), "head_wc": torch.empty(H, **f32),
+        "x6_tn": torch.empty((T, 16, 24), **f32),
+        "seg": torch.empty((T, 10, 64), **f32),
+    }
+    empty = torch.empty((T, 0, 64), **f32)
+    plan = SegmentPlan(torch.empty(0, dtype=torch.int32, device=device), torch.empty(0, dtype=torch.int32,
+                                                                                      device=device))
+    return outs, [
+        ("conv1_lut_bwd", lambda: nat.conv1_lut_bwd(codes, None, torch.empty((T, 0, 13, 13, 32), **f32),
+                                                    torch.empty((T, 0, 13, 13, 32), **f32))),
+        ("conv2_im2col_bwd", lambda: nat.conv2_im2col_bwd(codes, None, torch.zeros((T, 32, 4, 20), **f32),
+                                                          torch.zeros((T, 32), **f32), torch.empty((T, 0, 512), **f32))),
+        ("conv3_col2im_bwd_chunked", lambda: nat.conv3_col2im_bwd_chunked(
+            torch.empty((T, 0, 576), **f32), torch.empty((T, 0, 64), **f32), torch.zeros((T, 64), **f32))[1:]),
+        ("conv2_lut_bwd", lambda: (nat.conv2_lut_bwd(codes, torch.empty((T, 16, 0, 4), **f32),
+                                                     torch.zeros(1, dtype=torch.int32, device=device)),)),
+        ("relu_bwd", lambda: nat.relu_bwd(empty, empty, out_bias=outs["relu_bwd_bias"])[1:]),
+        ("colsum", lambda: (nat.colsum(empty, out=outs["colsum"]),)),
+        ("head_bwd", lambda: nat.head_bwd(torch.empty((2, 0, H), **f32), torch.empty((0, A), **f32),
+                                          torch.empty(0, **f32), torch.zeros((A, H), **f32), torch.zeros(H, **f32),
+                                          out_bias=outs["head_b"], out_w_actor=outs["head_wa"],
+                                          out_w_critic=outs["head_wc"])[1:]),
+        ("x6_gemm_tn", lambda: (nat.x6_gemm_tn(torch.empty((T, 0, 16), **f32), torch.empty((T, 0, 24), **f32),
+                                               out=outs["x6_tn"]),)),
+        ("segment_sum", lambda: (nat.segment_sum(empty, plan, 10, out=outs["seg"]),)),
+    ]
+
+
+def test_captured_zero_fills_replay_zero(device):
+    """Round-4 verdict item 6: no entry point zero-fills with hipMemsetAsync any more (csrc: merlin::zero_async, a
+    kernel), so each zero-fill branch captured into a HIP graph and replayed over poisoned outputs writes zeros, on
+    every replay."""
+    _, cases = _zero_branch_cases(device)
+    for name, fn in cases:
+        res = fn()  # eager once (allocations, plans)
+        torch.cuda.synchronize()
+        for r in res:
+            assert torch.count_nonzero(r) == 0, name
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            res = fn()
+        for rep in range(3):
+            for r in res:
+                r.view(torch.int32).fill_(0x7fc00001 + rep)  # NaN payload: nothing but a write of zeros clears it
+            g.replay()
+            torch.cuda.synchronize()
+            for r in res:
+                assert torch.count_nonzero(r.view(torch.int32)) == 0, (name, rep)
+        del g
+
+
+def test_release_deferred_by_a_plain_capture_is_drained(device):
+    """ADVICE r4: an env closed inside a user's own torch.cuda.graph capture (no capture_guard) queues its release;
+    the queue drains at the next env creation with no capture open, not only at a capture_guard exit."""
+    from merlin import MerlinVecEnv
+    from merlin import _native as nat
+
+    victim = MerlinVecEnv(64, "mediumhard", seed=9, device=device)
+    victim.reset()
+    x = torch.zeros(16, device=device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        x.add_(1.0)
+        victim.close()
+        assert len(nat._DEFERRED) == 1
+    assert len(nat._DEFERRED) == 1  # nothing drained it yet
+    other = MerlinVecEnv(64, "mediumhard", seed=10, device=device)
+    assert not nat._DEFERRED and victim._h is None
+    other.close()
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(x[0]) == 1.0

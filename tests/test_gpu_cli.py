@@ -109,10 +109,12 @@ def test_cli_single_env_seed_reproducible(tmp_path, monkeypatch, device):
     assert not (r1 == r3).all()
 
 
-def test_fomaml_cli_smoke(tmp_path, monkeypatch, device):
+def test_fomaml_cli_smoke(tmp_path, monkeypatch, capsys, device):
     """fomaml_train.py (drop-in for the reference's fomaml/fomaml_train.py:37-178) end to end at a tiny budget:
-    two meta-iterations of 4 tasks, checkpoints in the reference's layout, loadable with the model's keys."""
+    ten meta-iterations of 4 tasks; the reference's output files (best_model.pth :128-132, fomaml_iter_<k>.pth and
+    training_curves.png :138-157) and its per-10-iteration log fields (:136)."""
     import importlib.util
+    import re
 
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ppo-2dgrid_amd",
                         "fomaml_train.py")
@@ -120,14 +122,22 @@ def test_fomaml_cli_smoke(tmp_path, monkeypatch, device):
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     monkeypatch.chdir(tmp_path)
-    args = mod.parse_args(["--device", "cuda", "--difficulty", "mediumhard", "--seed", "7", "--iterations", "2",
-                           "--tasks_per_batch", "4", "--k_steps", "32", "--save_every", "2"])
+    args = mod.parse_args(["--device", "cuda", "--difficulty", "mediumhard", "--seed", "7", "--iterations", "10",
+                           "--tasks_per_batch", "4", "--k_steps", "32", "--save_every", "5"])
     fomaml = mod.train_fomaml(args)
+    out = capsys.readouterr().out
     runs = os.listdir(tmp_path / "checkpoints")
     assert len(runs) == 1 and runs[0].startswith("MERLIN-MediumHard-v0_16x16_mediumhard_FOMAML_")
     d = tmp_path / "checkpoints" / runs[0] / "seed_7"
     names = sorted(os.listdir(d))
-    assert names == ["fomaml_best.pth", "fomaml_final.pth", "fomaml_iter_2.pth"]
-    sd = torch.load(d / "fomaml_final.pth", weights_only=True)
-    assert set(sd) == set(fomaml.meta_policy.state_dict())
-    assert all(torch.isfinite(v).all() for v in sd.values())
+    assert names == ["best_model.pth", "fomaml_iter_10.pth", "fomaml_iter_5.pth", "training_curves.png"]
+    assert (d / "training_curves.png").read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"
+    for name in ("best_model.pth", "fomaml_iter_10.pth"):
+        sd = torch.load(d / name, weights_only=True)
+        assert set(sd) == set(fomaml.meta_policy.state_dict())
+        assert all(torch.isfinite(v).all() for v in sd.values())
+    line = [ln for ln in out.splitlines() if ln.startswith("Iter ")]
+    assert len(line) == 1
+    assert re.fullmatch(r"Iter\s+10 \| R: -?[\d.]+ \| L: -?[\d.]+ \| pi: -?[\d.]+ \| V: -?[\d.]+ \| Ent: -?[\d.]+ \| "
+                        r"KL: -?[\d.]+ \| Steps: [\d.]+ \| Best: -?[\d.]+ \| T: [\d.]+m", line[0]), line[0]
+    assert "[*] New Best Model Saved (Rew: " in out and "[*] Saved training curves to: " in out

@@ -1,5 +1,5 @@
-"""GPU: data parallelism of merlin.PPO itself (cfg 3's shape), two ranks on one GPU
-(torch.distributed, gloo: RCCL needs one GPU per rank) against ONE process over the 2N
+"""GPU: data parallelism of merlin.PPO itself (cfg 3's shape), W ranks on one GPU (W = 2, and 8 as cfg
+3's world size; torch.distributed, gloo: RCCL needs one GPU per rank) against ONE process over the W*N
 concatenated envs.  Rank r owns envs [rN, (r+1)N) seeded 777 + global index, and the action draws
 are keyed by the global env index, so each rank's rollout must equal its columns of the single
 run bit for bit; the advantages are normalised with the all-reduced global moments
@@ -16,50 +16,51 @@ pytestmark = pytest.mark.gpu
 
 SMALL = (96, 16, 4, 2)  # N envs per rank, T steps, minibatches, epochs
 CFG3 = (4096, 256, 8, 1)  # cfg 3's per-rank shape (4096 envs x 256 steps, 8 minibatches of 131,072)
+WORLD8 = (128, 16, 4, 2)  # cfg 3's world size, 8 ranks, at a small per-rank shape
 
 
-def _perm(rank_or_none, epoch, shape):
-    """Local permutation of rank r (n = N*T), or the single run's (2N*T) made of both ranks'."""
+def _perm(rank_or_none, epoch, shape, world=2):
+    """Local permutation of rank r (n = N*T), or the single run's (W*N*T) made of every rank's."""
     N, T, MB, _ = shape
     n, m = N * T, N * T // MB
     g = torch.Generator().manual_seed(1000 + epoch)
-    local = [torch.randperm(n, generator=g) for _ in range(2)]
+    local = [torch.randperm(n, generator=g) for _ in range(world)]
     if rank_or_none is not None:
         return local[rank_or_none]
 
-    def to_global(j, r):  # local sample t*N + i -> t*2N + r*N + i
-        return (j // N) * 2 * N + r * N + j % N
+    def to_global(j, r):  # local sample t*N + i -> t*W*N + r*N + i
+        return (j // N) * world * N + r * N + j % N
 
     parts = []
     for k in range(MB):
-        for r in range(2):
+        for r in range(world):
             parts.append(to_global(local[r][k * m:(k + 1) * m], r))
     return torch.cat(parts)
 
 
-def _agent(env, shape, dp=None, rank=None):
+def _agent(env, shape, dp=None, rank=None, world=2):
     from merlin.ppo import PPO
 
     _, T, MB, EPOCHS = shape
     torch.manual_seed(5)
     n_envs = env.num_envs
     return PPO(env, batch_size=n_envs * T, minibatch_size=n_envs * T // MB, update_epochs=EPOCHS, ent_coef=0.05,
-               device=env.device, dp=dp, perm_fn=lambda n, e: _perm(rank, e, shape))
+               device=env.device, dp=dp, perm_fn=lambda n, e: _perm(rank, e, shape, world))
 
 
-def _rank_main(rank, port, out_dir, shape):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+def _rank_main(rank, port, out_dir, shape, world=2):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     import torch.distributed as dist
 
     from merlin import MerlinVecEnv
     from merlin.distributed import DataParallel
 
-    dist.init_process_group("gloo", rank=rank, world_size=2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     N = shape[0]
     env = MerlinVecEnv(N, "mediumhard", seed=777, device=dev, env_offset=rank * N)
-    agent = _agent(env, shape, DataParallel(), rank)
+    agent = _agent(env, shape, DataParallel(), rank, world)
     lv = agent.collect_rollouts()
     buf = agent.buf
     roll = {k: getattr(buf, k).clone().cpu() for k in ("codes", "actions", "rewards", "dones", "logprobs", "values")}
@@ -78,20 +79,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _two_ranks_vs_one_process(device, tmp_path, shape):
+def _ranks_vs_one_process(device, tmp_path, shape, world=2):
     import torch.multiprocessing as mp
 
     from merlin import MerlinVecEnv
 
     N, T, MB, EPOCHS = shape
-    mp.start_processes(_rank_main, args=(_free_port(), str(tmp_path), shape), nprocs=2, join=True,
+    mp.start_processes(_rank_main, args=(_free_port(), str(tmp_path), shape, world), nprocs=world, join=True,
                        start_method="spawn")
-    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2)]
-    env = MerlinVecEnv(2 * N, "mediumhard", seed=777, device=device)
-    agent = _agent(env, shape)
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    env = MerlinVecEnv(world * N, "mediumhard", seed=777, device=device)
+    agent = _agent(env, shape, world=world)
     lv = agent.collect_rollouts()
     buf = agent.buf
-    for r in range(2):  # the rank's rollout is its columns of the single run
+    for r in range(world):  # the rank's rollout is its columns of the single run
         for k, v in res[r]["roll"].items():
             cols = getattr(buf, k).cpu()[:, r * N:(r + 1) * N]
             if k in ("logprobs", "values"):  # the policy GEMMs run at another batch size: fp32 order
@@ -100,25 +101,30 @@ def _two_ranks_vs_one_process(device, tmp_path, shape):
                 assert torch.equal(v, cols), (r, k)
     stats = agent.update(lv)
     # global-moment normalisation: each rank's advantages == the single run's columns
-    for r in range(2):
+    for r in range(world):
         torch.testing.assert_close(res[r]["adv"], agent.last_adv_normalized.cpu()[:, r * N:(r + 1) * N],
                                    rtol=1e-5, atol=1e-5)
     for k in stats:
-        dp_val = 0.5 * (res[0]["stats"][k] + res[1]["stats"][k]) if k != "gradnorm" else res[0]["stats"][k]
+        dp_val = sum(res[r]["stats"][k] for r in range(world)) / world if k != "gradnorm" else res[0]["stats"][k]
         # clipfrac counts samples with |ratio - 1| > clip: a ratio within fp32 noise of the boundary flips with the
         # summation order (4 samples per minibatch, or 1 in 10^4 at cfg 3's 262,144-sample minibatches)
-        tol = max(4.0 / (2 * N * T // MB), 1e-4) if k == "clipfrac" else 1e-4 * max(1.0, abs(stats[k]))
+        tol = max(4.0 / (world * N * T // MB), 1e-4) if k == "clipfrac" else 1e-4 * max(1.0, abs(stats[k]))
         assert abs(dp_val - stats[k]) <= tol, (k, dp_val, stats[k])
-    # replicated parameters: both ranks identical; vs the single run within the Adam-step bound of
+    # replicated parameters: every rank identical; vs the single run within the Adam-step bound of
     # test_gpu_windows.py (fp32 summation order differs: per-rank dedup groups, all-reduced sums)
-    for a, b in zip(res[0]["params"], res[1]["params"]):
-        assert torch.equal(a, b)
+    for r in range(1, world):
+        for a, b in zip(res[0]["params"], res[r]["params"]):
+            assert torch.equal(a, b), r
     ds = [(a - b.detach().cpu()).abs().flatten() for a, b in zip(res[0]["params"], agent.ac.parameters())]
     steps = EPOCHS * MB
     for d in ds:
         assert d.max().item() <= 2 * 3e-4 * steps
     assert (torch.cat(ds) > 5e-5).float().mean().item() < 0.05
     return res, agent
+
+
+def _two_ranks_vs_one_process(device, tmp_path, shape):
+    return _ranks_vs_one_process(device, tmp_path, shape, 2)
 
 
 def test_two_rank_ppo_equals_one_process_over_concatenated_envs(device, tmp_path):
@@ -132,3 +138,12 @@ def test_two_rank_ppo_cfg3_per_rank_shape(device, tmp_path):
     res, agent = _two_ranks_vs_one_process(device, tmp_path, CFG3)
     assert all(r["fast"] for r in res) and agent._wstep is not None  # the benched step ran on both sides
     assert all(r["windows"] and r["windows"] > 1000 for r in res)
+
+
+def test_eight_rank_ppo_equals_one_process_over_concatenated_envs(device, tmp_path):
+    """Round-4 verdict item 1: cfg 3's world size.  8 ranks (gloo, all on device 0) with env_offset = rank * N, the
+    global-moment advantage all-reduce over 8 ranks and the gradient average with world = 8, against one process over
+    the 1,024 concatenated envs: rollouts bit for bit, global-moment advantages, averaged statistics, replicated
+    parameters."""
+    res, agent = _ranks_vs_one_process(device, tmp_path, WORLD8, 8)
+    assert len(res) == 8

@@ -118,3 +118,17 @@ def test_fast_step_recaptures_after_parameter_swap(device):
     w = agent.ac.actor[0].weight
     w.data = w.data.clone()
     assert not st.valid()
+
+
+def test_patch_reuse_partial_rows_never_read_directly(device, monkeypatch):
+    """with conv3's patch reuse, window_conv3 leaves the non-representative rows of Y3 / the mask words
+    unwritten; every consumer reads them through rep_row.  With those rows poisoned (NaN / all-ones words) an update
+    gives the same bits as without."""
+    from merlin import _native as nat
+
+    a0, s0 = _run(device, True, iters=2)
+    monkeypatch.setattr(nat, "POISON_PARTIAL", True)
+    a1, s1 = _run(device, True, iters=2)
+    assert s0 == s1
+    for (k, p0), p1 in zip(a0.ac.named_parameters(), a1.ac.parameters()):
+        assert torch.equal(p0, p1), k

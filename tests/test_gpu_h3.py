@@ -208,3 +208,51 @@ def test_gemm_nt_heads_epilogue(device, cfg, gather):
     # fixed order: the same bits again
     h2, logits2, value2 = nat.h3_gemm_nt_heads(A, amA, Bp, amB, bias, Wa, Wc, cfg=cfg, rows=rows)
     assert torch.equal(logits2, logits) and torch.equal(value2, value) and torch.equal(h2, h)
+
+
+@pytest.mark.parametrize("N,K,cfg", [(512, 576, 13), (576, 512, 11), (512, 576, 12)])
+def test_gemm_nt_dynamic_range(device, N, K, cfg):
+    """The h3 form's documented range (the bench line's dtype_note): rows spread over 2^-30 .. 2^3 of one
+    scale.  Rows whose max lies within 2^26 of the tensor's max are held to the fp32 GEMM's own error (as above);
+    below that the planes hold each value to 2^-50 of the tensor max, absolute, so those outputs' error stays under
+    that absolute bound (x the row's sum of |b|) on top of the fp32 one."""
+    from merlin import _native as nat
+
+    M = 4099
+    g = torch.Generator(device=device).manual_seed(N + cfg)
+    A = torch.relu(torch.randn(2, M, K, device=device, generator=g))
+    A = A * torch.exp2(torch.randint(-30, 4, (2, M, 1), device=device, generator=g).float())
+    B = torch.randn(2, N, K, device=device, generator=g) / K ** 0.5
+    C64 = torch.bmm(A.double(), B.double().transpose(1, 2))
+    den = torch.bmm(A.abs().double(), B.abs().double().transpose(1, 2))
+    amA, amB = nat.h3_amax(A), nat.h3_amax(B)
+    C = nat.h3_gemm_nt(A, amA, nat.h3_split(B, amB), amB, cfg=cfg)
+    Cf = torch.bmm(A, B.transpose(1, 2))
+    tmax = A.abs().amax(dim=(1, 2), keepdim=True)  # [2, 1, 1]
+    inr = (A.abs().amax(dim=2, keepdim=True) >= tmax * 2.0 ** -26).expand_as(C)  # [2, M, N]
+    assert inr.any() and (~inr).any()
+    tol = max(_err(Cf[inr], C64[inr], den[inr]), FLOOR)
+    assert _err(C[inr], C64[inr], den[inr]) <= tol
+    absb = B.abs().double().sum(dim=2).unsqueeze(1)  # [2, 1, N]: sum_k |b_nk|
+    bound = tol * den + 2.0 ** -49 * tmax.double() * absb
+    assert ((C.double() - C64).abs() <= bound)[~inr].all()
+
+
+def test_gemm_tn_dynamic_range(device):
+    """The weight gradient with dz rows spread over 2^-30 .. 2^0 of one scale (the update's per-sample gradient
+    magnitudes vary that much): within the fp32 error plus the documented absolute bound for values below 2^-26 of
+    the max."""
+    from merlin import _native as nat
+
+    Kd = 20000
+    g = torch.Generator(device=device).manual_seed(11)
+    dz = torch.randn(2, Kd, 512, device=device, generator=g) * 1e-6
+    dz = dz * torch.exp2(torch.randint(-30, 1, (2, Kd, 1), device=device, generator=g).float())
+    a3 = torch.relu(torch.randn(2, Kd, 576, device=device, generator=g))
+    W64 = torch.bmm(dz.double().transpose(1, 2), a3.double())
+    den = torch.bmm(dz.abs().double().transpose(1, 2), a3.abs().double())
+    tol = max(_err(torch.bmm(dz.transpose(1, 2), a3), W64, den), FLOOR)
+    W = nat.h3_gemm_tn(dz, nat.h3_amax(dz), a3, nat.h3_amax(a3))
+    zmax = dz.abs().amax(dim=(1, 2)).double().view(2, 1, 1)
+    absa = a3.abs().double().sum(dim=1).unsqueeze(1)  # [2, 1, 576]
+    assert ((W.double() - W64).abs() <= tol * den + 2.0 ** -49 * zmax * absa).all()

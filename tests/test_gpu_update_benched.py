@@ -9,7 +9,7 @@ checksums of the post-Adam parameters):
 Here they run through exactly what bench.py times: the vectorised code-storage path (MerlinVecEnv
 storage layout [T][N]), GAE + normalisation on the HIP kernels, the distinct-frame grouping
 (merlin/dedup.py), conv2 / conv3 once per receptive-field window (merlin/windows.py), fc1's three
-GEMMs on the bf16 matrix cores in exact three-plane form (k_x6_nt / k_x6_tn), the fused loss
+GEMMs on the f16 matrix cores in two-plane form (h3: k_h3_ntpg / k_h3_ntp / k_h3_tng), the fused loss
 (merlin_ppo_loss) and clip_grad_norm_ + Adam as two HIP launches (merlin_clip_adam).
 Tolerances as tests/test_gpu_ppo.py::test_update_matches_reference (reference on CPU vs fp32 on the
 GPU: ~1e-6 per-op differences; after the Adam steps metrics agree to ~1e-4 relative)."""

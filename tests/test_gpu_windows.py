@@ -124,6 +124,15 @@ def test_window_conv3_patch_reuse_bitwise(device):
                     got = nat.segment_sum(dY, plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9, mask=b2,
                                           mask_rows=mb.rep_row)
                     assert torch.equal(got, ref)
+                    # the same through the two-launch fix-up form (SEG_FUSED off: no head_fix / counters passed)
+                    fused0 = nat.SEG_FUSED
+                    nat.SEG_FUSED = False
+                    try:
+                        got2 = nat.segment_sum(dY, plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9, mask=b2,
+                                               mask_rows=mb.rep_row)
+                    finally:
+                        nat.SEG_FUSED = fused0
+                    assert torch.equal(got2, ref)
     assert shared > 0  # rows actually copied
 
 
