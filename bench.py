@@ -49,7 +49,7 @@ BWD_MACS = 2 * FWD_MACS - 2 * 1_038_336
 # (merlin/windows.py: the [windows, 64] x [64, 576] product per tower); backward = input grad +
 # weight grad (2x).
 GEMM_FWD_MACS = 2 * (331_776 + 294_912) + 512 * 3 + 512  # the per-frame formulation (no windows)
-ROLLOUT_TABLE_MACS = 2 * 5 ** 9 * 64 * 576  # per rollout
+ROLLOUT_TABLE_MACS = 2 * (4 ** 9 + 3 * 4 ** 8) * 64 * 576  # per rollout (the acting table's compact keys)
 FC_FWD_MACS = 2 * 294_912 + 512 * 3 + 512
 WINDOW_FWD_MACS = 2 * 64 * 576  # per window per minibatch
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)

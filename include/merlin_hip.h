@@ -313,10 +313,12 @@ int merlin_tower_window_lut_bias_relu(const int32_t *rows_dev, int64_t n_windows
 int merlin_tower_window_conv3(const float *Q_dev, int64_t n_windows, const int32_t *wid_dev,
                               const int64_t *groups_dev, int64_t n, const float *b3_dev,
                               int32_t towers, float *Y3_dev, void *stream);
-/* conv3 of the acting path from a table over every possible 3x3 tile window:
- * Qall_dev float[towers][merlin_tower_all_windows() = 5^9][9][64] (Q of merlin_tower_window_conv3
- * for window id = the window's 9 tile classes in base 5, tile (0,0) most significant; built once
- * per rollout, merlin/actor_critic.py rollout_pack);
+/* conv3 of the acting path from a table over every 3x3 tile window an observation can hold:
+ * Qall_dev float[towers][merlin_tower_all_windows() = 4^9 + 3 * 4^8 = 458,752][9][64] (Q of
+ * merlin_tower_window_conv3 for the window with compact key k: a window away from the agent's view cell (3, 6) =
+ * its 9 tile classes 0..3 in base 4, tile (0,0) most significant; a window at conv2 position (4, wx), wx = 1..3,
+ * which holds the agent's tile (class 4) at local (2, 3 - wx) = 4^9 + (wx - 1) 4^8 + its other 8 classes in
+ * base 4 -- merlin/windows.py compact_window_keys; built once per rollout, merlin/actor_critic.py rollout_pack);
  * Y3[t][k*9 + p3][co] = relu(b3[t][co] + sum over the 9 taps of Qall[t][id of frame k's window at
  * p3 + tap][tap][co]) for frames codes_dev[k] (8 words of tile-class nibbles, merlin_env_step). */
 int64_t merlin_tower_all_windows(void);

@@ -745,7 +745,7 @@ int merlin_tower_window_conv3_reuse(const float *Q, int64_t nw, const int32_t *w
     return MERLIN_OK;
 }
 
-int64_t merlin_tower_all_windows(void) { return 1953125; }
+int64_t merlin_tower_all_windows(void) { return 458752; }  // 4^9 + 3 * 4^8 (merlin_window.hip k_codes_conv3)
 
 int merlin_tower_codes_conv3_amax(const uint32_t *codes, int64_t n, const float *Qall, const float *b3,
                                   int32_t towers, float *Y3, uint32_t *amax, void *stream) {

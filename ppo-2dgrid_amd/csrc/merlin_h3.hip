@@ -589,7 +589,7 @@ __device__ __forceinline__ int g_swz(int r) { return (r >> 1) & 7; }
 
 // AP: A arrives as plane images too ([M][K/8][2][8] f16, h3_split's layout: 4 B per value like fp32, so the DMA
 // addressing is the same) -- no split at all, A's fragments read like B's.
-template <int BM, int BN, int WGM, int WGN, int EPI, bool KP, bool AP = false>
+template <int BM, int BN, int WGM, int WGN, int EPI, bool KP, bool AP = false, bool PR = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restrict__ A, const u32x4 *__restrict__ B,
                                                            const uint32_t *__restrict__ amaxA,
                                                            const uint32_t *__restrict__ amaxB, int64_t M, int N,
@@ -694,6 +694,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
         }
     };
     auto mfmas = [&](const Frag &f) {
+        if constexpr (PR) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < TM; i++)
 #pragma unroll
@@ -702,6 +703,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
                 lo[i][j] = mfma16(f.a[i][0], f.b[j][1], lo[i][j]);
                 hi[i][j] = mfma16(f.a[i][0], f.b[j][0], hi[i][j]);
             }
+        if constexpr (PR) __builtin_amdgcn_s_setprio(0);
     };
     auto mma = [&](Frag &f) {
         split(f);
@@ -1455,7 +1457,7 @@ hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, cons
     return hipGetLastError();
 }
 
-template <int BM, int BN, int WGM, int WGN, bool KP, bool AP = false>
+template <int BM, int BN, int WGM, int WGN, bool KP, bool AP = false, bool PR = false>
 hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                       int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
                       hipStream_t s) {
@@ -1466,11 +1468,11 @@ hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, con
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
     if (bias)
-        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP, AP>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
-                           sB, bias, C, sC, tiles_n);
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP, AP, PR>), grid, block, 0, s, A, B, amaxA, amaxB, M, N,
+                           K, sA, sB, bias, C, sC, tiles_n);
     else
-        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP, AP>), grid, block, 0, s, A, B, amaxA, amaxB, M, N, K, sA,
-                           sB, nullptr, C, sC, tiles_n);
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP, AP, PR>), grid, block, 0, s, A, B, amaxA, amaxB, M, N,
+                           K, sA, sB, nullptr, C, sC, tiles_n);
     return hipGetLastError();
 }
 
@@ -1580,6 +1582,13 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 42: return H3_NTGP(128, 256, 2, 4, true);
         case 43: return H3_NTGP(256, 128, 4, 2, false);
 #undef H3_NTGP
+#define H3_NTGQ(BM, BN, WM, WN, KP) \
+    ((a_rows || head_part) ? hipErrorInvalidValue                                                  \
+            : ntg_launch<BM, BN, WM, WN, KP, true, true>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s))
+        case 44: return H3_NTGQ(128, 256, 2, 4, true);
+        case 45: return H3_NTGQ(256, 128, 4, 2, true);
+        case 46: return H3_NTGQ(256, 128, 4, 2, false);
+#undef H3_NTGQ
         default: return hipErrorInvalidValue;
     }
 }

@@ -181,12 +181,17 @@ __global__ __launch_bounds__(256) void k_window_conv3_copy(float4 *Y3, uint64_t 
     }
 }
 
-// The acting path's conv3 from a table over EVERY possible 3x3 tile window (5^9 = 1,953,125 rows, built
-// once per rollout from the fixed weights): Y3[t][u*9 + p3][c4] = relu(b3[t][c4] + sum_tap
-// Qall[t][key(u, p2(p3, tap))][tap][c4]), key = the frame's 3x3 tile classes at conv2 position p2 as 9
-// base-5 digits, tile (0, 0) most significant (merlin/windows.py window_keys) -- computed from the
-// frame's 49 class nibbles in registers, so conv2's lookups, conv3's im2col and its GEMM all drop out.
-constexpr int64_t ALL_WINDOWS = 1953125;
+// The acting path's conv3 from a table over every 3x3 tile window an observation can hold (built once per rollout
+// from the fixed weights): Y3[t][u*9 + p3][c4] = relu(b3[t][c4] + sum_tap Qall[t][key(u, p2(p3, tap))][tap][c4]),
+// computed from the frame's 49 class nibbles in registers, so conv2's lookups, conv3's im2col and its GEMM all drop
+// out.  The agent's tile (class 4) is always at view cell (3, 6) (minigrid's egocentric view: the agent at the bottom
+// centre), so a window holds it exactly when it covers that cell -- conv2 position (4, 1..3), the tile at local (2,
+// 3 - wx) -- and nowhere else; every other tile is one of the four classes 0..3.  Keys (merlin/windows.py
+// compact_window_keys): a window away from the agent = its 9 classes in base 4 (tile (0, 0) most significant,
+// 4^9 keys); a window over the agent = 4^9 + (wx - 1) 4^8 + its other 8 classes in base 4.  458,752 keys instead of
+// all 5^9 = 1,953,125 class patterns: a 4.3x smaller table (2.1 GB for both towers), built in that fraction of the
+// time.  (Valid observations only: a class-4 tile elsewhere is read as class 3.)
+constexpr int64_t ALL_WINDOWS = 458752;  // 4^9 + 3 * 4^8
 __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict__ codes, int64_t n,
                                                      const float4 *__restrict__ Q, const float4 *__restrict__ b3,
                                                      int T, float4 *__restrict__ Y3, uint32_t *__restrict__ amax) {
@@ -200,9 +205,9 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
         const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + u * 8);
         const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + u * 8 + 4);
         const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        auto cls = [&](int y, int x) -> uint32_t {  // tile class, clamped to 4 like the other kernels
+        auto cls = [&](int y, int x) -> uint32_t {  // tile class, 0..3 (the agent's tile is keyed by position)
             const int cell = y * 7 + x;
-            return min((w[cell >> 3] >> (4 * (cell & 7))) & 15u, 4u);
+            return min((w[cell >> 3] >> (4 * (cell & 7))) & 15u, 3u);
         };
         const int oy = p3 / 3, ox = p3 - 3 * (p3 / 3);
         const float4 *qt = Q + (size_t)t * ALL_WINDOWS * 9 * 16 + c;
@@ -210,11 +215,15 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
 #pragma unroll
         for (int tap = 0; tap < 9; tap++) {
             const int wy = oy + tap / 3, wx = ox + tap - 3 * (tap / 3);
+            const bool agent = wy == 4 && wx >= 1 && wx <= 3;
+            const int skip = agent ? 9 - wx : -1;  // local slot 3 * 2 + (3 - wx) of the agent's tile
             uint32_t key = 0;
 #pragma unroll
             for (int a = 0; a < 3; a++)
 #pragma unroll
-                for (int b = 0; b < 3; b++) key = key * 5u + cls(wy + a, wx + b);
+                for (int b = 0; b < 3; b++)
+                    if (3 * a + b != skip) key = key * 4u + cls(wy + a, wx + b);
+            if (agent) key += 262144u + (uint32_t)(wx - 1) * 65536u;
             v[tap] = qt[((size_t)key * 9 + tap) * 16];
         }
         float4 acc = v[0];
@@ -553,7 +562,7 @@ hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, 
     const int64_t total = (int64_t)T * nw * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
-    if (nw == 1953125)  // 5^9: merlin_tower_all_windows()
+    if (nw == ALL_WINDOWS)  // merlin_tower_all_windows(): the acting path's table
         hipLaunchKernelGGL(k_window_lut<1>, dim3(grid), dim3(256), 0, s, rows, nw, reinterpret_cast<const float4 *>(tab),
                            T, reinterpret_cast<float4 *>(Z2w), reinterpret_cast<const float4 *>(b2));
     else

@@ -581,7 +581,7 @@ def window_lut(rows, tables, bias=None):
     out = torch.empty((T, nw, 64), dtype=torch.float32, device=tables.device)
     # algorithmic bytes: row indices + Z2w written (table rows are L2-resident gathers)
     # the rollout's all-windows table (5^9 rows) is its own kernel instantiation and span (k_window_lut<1>)
-    with KernelTimer.span("k_window_lut_all" if nw == 5 ** 9 else "k_window_lut", nw * (64 + T * 256)):
+    with KernelTimer.span("k_window_lut_all" if nw == ALL_WINDOWS else "k_window_lut", nw * (64 + T * 256)):
         if bias is not None:
             assert bias.shape == (T, 64) and bias.dtype == torch.float32 and bias.is_contiguous()
             check(lib().merlin_tower_window_lut_bias_relu(ptr(rows), nw, ptr(tables), T, ptr(bias), ptr(out),
@@ -648,7 +648,7 @@ def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None
     return out
 
 
-ALL_WINDOWS = 5 ** 9  # merlin_tower_all_windows()
+ALL_WINDOWS = 4 ** 9 + 3 * 4 ** 8  # merlin_tower_all_windows(): the acting table's compact keys
 # debug: window_conv3 fills the rows it leaves unwritten (copy < 3) with NaN / all-ones mask words
 POISON_PARTIAL = os.environ.get("MERLIN_POISON_PARTIAL", "0") == "1"
 
@@ -685,7 +685,8 @@ def window_conv3_copy_masks(Y3, bits, rep_row):
 
 def codes_conv3(codes, Qall, b3, amax=None):
     """Y3 f32[T, n*9, 64]: relu(conv3) rows (k, p3) of frames codes[k] (int32 [n, 8]) from Qall
-    f32[T, 5**9, 576], the per-window, per-tap conv3 partial sums of every possible window
+    f32[T, ALL_WINDOWS, 576], the per-window, per-tap conv3 partial sums of every window an observation can hold
+    (compact keys: merlin/windows.py compact_window_keys)
     (merlin_tower_codes_conv3).  amax (int32 [T], zeroed by the caller): receives max |Y3| per tower as float
     bits (h3_amax's format)."""
     T, n = int(Qall.shape[0]), int(codes.shape[0])

@@ -374,7 +374,7 @@ class CNNActorCritic(nn.Module):
         self._atlas = None  # f32 [5, 3, 8, 8] / 255 on the model's device (codes path only)
         self._lut2_idx = None
         self._lut2_gather = None
-        self._all_rows = None  # int32 [5**9, 16] table rows of every window (acting path)
+        self._all_rows = None  # int32 [458752, 16] table rows of every observable window (acting path)
         # "lut2": conv1+conv2 as table lookups, conv3/fc as hipBLASLt GEMMs (default)
         # "gemm": conv1 lookups, conv2/conv3/fc as GEMMs | "lut_nchw": conv1 lookups + MIOpen convs
         self.codes_impl = "lut2"
@@ -501,17 +501,19 @@ class CNNActorCritic(nn.Module):
         return self.actor(fa), self.critic(fc).squeeze(-1)
 
     def _all_window_rows(self, device):
-        """int32 [5**9, 16]: the conv2 table rows of every possible 3x3 tile window, window id =
-        its 9 classes in base 5 (merlin/windows.py window_rows), built once per device."""
+        """int32 [458,752, 16]: the conv2 table rows of every 3x3 tile window an observation can hold, in the acting
+        table's compact key order (merlin/windows.py compact_window_keys, window_rows), built once per device."""
         if self._all_rows is None or self._all_rows.device != device:
             from . import _native as nat
-            from .windows import window_rows
+            from .windows import compact_window_keys, window_rows
 
-            self._all_rows = window_rows(torch.arange(nat.ALL_WINDOWS, dtype=torch.int64, device=device)).contiguous()
+            keys = compact_window_keys(device)
+            assert keys.numel() == nat.ALL_WINDOWS
+            self._all_rows = window_rows(keys).contiguous()
         return self._all_rows
 
     # below this many frames per rollout the acting path looks conv2 up per frame instead of building
-    # the all-windows table (Qall: 9 GB and ~288 GFLOP per rollout, whatever the rollout's size)
+    # the all-windows table (Qall: 2.1 GB and ~68 GFLOP per rollout, whatever the rollout's size)
     ALL_WINDOWS_MIN_FRAMES = 1 << 18
 
     def rollout_pack(self, frames: int | None = None, all_windows: bool | None = None, steps: int | None = None):
@@ -519,10 +521,10 @@ class CNNActorCritic(nn.Module):
         per rollout (the weights do not change while acting).
 
         Large rollouts (frames >= ALL_WINDOWS_MIN_FRAMES, or frames not given): conv2 (from the
-        conv1+conv2 tables) and conv3's per-tap products for EVERY possible 3x3 tile window, Qall
-        [2, 5**9, 576] (9 GB + 1 GB of conv2 rows while it is built: conv2 + ReLU of all 1,953,125
-        windows and one [5**9, 64] x [64, 576] GEMM per tower, a few ms per rollout); each step then
-        sums 81 table rows per frame.  Small rollouts, or when the device has less than ~12 GB free:
+        conv1+conv2 tables) and conv3's per-tap products for every 3x3 tile window an observation can hold, Qall
+        [2, 458752, 576] (2.1 GB + 0.23 GB of conv2 rows while it is built: conv2 + ReLU of the 458,752 windows of
+        merlin/windows.py compact_window_keys and one [458752, 64] x [64, 576] GEMM per tower, ~1 ms per rollout);
+        each step then sums 81 table rows per frame.  Small rollouts, or when the device has less than ~12 GB free:
         the conv2 table T2 (2,720 rows) and conv3's weights, and each step looks conv2 up per frame
         position and runs conv3 as a GEMM over the im2col rows (merlin_tower_conv2_lut_fwd +
         conv3_im2col_fwd, a few MB).  Both: fc1 with columns permuted to (p3, co), biases stacked.
@@ -546,7 +548,7 @@ class CNNActorCritic(nn.Module):
         if all_windows is None:
             all_windows = self._use_all_windows(frames, T2.device)
         if all_windows:
-            # relu(conv2) of every possible window [2, 5**9, 64] (bias and ReLU in the lookup kernel)
+            # relu(conv2) of every observable window [2, 458752, 64] (bias and ReLU in the lookup kernel)
             a2 = nat.window_lut(self._all_window_rows(T2.device), T2,
                                 bias=torch.stack([ea[2].bias, ec[2].bias]).contiguous())
             if self.fc1_impl in ("x6", "h3") and QALL_H3:

@@ -126,6 +126,29 @@ def window_rows(keys: torch.Tensor) -> torch.Tensor:
     return torch.stack(rows, 1).to(torch.int32)
 
 
+def compact_window_keys(device) -> torch.Tensor:
+    """int64 [4^9 + 3 * 4^8]: the base-5 window key (window_rows' input) of every compact key of the acting path's
+    table (csrc/merlin_window.hip k_codes_conv3): keys 0 .. 4^9 - 1 = 9 tile classes 0..3 in base 4 (windows away
+    from the agent's view cell); 4^9 + (wx - 1) 4^8 + m = the window at conv2 position (4, wx) with the agent's tile
+    (class 4) at local (2, 3 - wx) and its other 8 classes m in base 4."""
+    d9 = torch.arange(4 ** 9, dtype=torch.int64, device=device)
+    digits = [(d9 // 4 ** (8 - i)) % 4 for i in range(9)]  # digits[3a + b] = class of tile (a, b)
+    out = [sum(digits[i] * 5 ** (8 - i) for i in range(9))]
+    m = torch.arange(4 ** 8, dtype=torch.int64, device=device)
+    d8 = [(m // 4 ** (7 - i)) % 4 for i in range(8)]
+    for wx in (1, 2, 3):
+        skip = 9 - wx  # local slot 3 * 2 + (3 - wx)
+        cls, j = [], 0
+        for i in range(9):
+            if i == skip:
+                cls.append(torch.full_like(m, 4))
+            else:
+                cls.append(d8[j])
+                j += 1
+        out.append(sum(cls[i] * 5 ** (8 - i) for i in range(9)))
+    return torch.cat(out)
+
+
 class SegmentPlan:
     """A destination-sorted entry list for merlin_segment_sum: out[key[e]] = sum of src[row(e)]
     over the entries e of that key, in list order.  The list is cut into items of item_len

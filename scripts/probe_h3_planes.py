@@ -39,7 +39,7 @@ def main():
     pdz = nat.h3_split(dz, amz).view(torch.float32)
     flop = 2 * 2 * U * 576 * 512
     runs = {"fwd ntp13": (lambda: nat.h3_gemm_nt(a3, am3, Hp, amW, bias=b, cfg=13), "fwd")}
-    for c in (40, 41, 42, 43):
+    for c in (40, 41, 42, 43, 44, 45, 46):
         if 512 % {41: 192, 42: 256}.get(c, 128) == 0:
             runs[f"fwd planes{c}"] = ((lambda c=c: nat.h3_gemm_nt(pa3, am3, Hp, amW, bias=b, cfg=c)), "fwd")
     runs["dgrad ntp11"] = (lambda: nat.h3_gemm_nt(dz, amz, Htp, amWt, cfg=11), "dgrad")

@@ -9,14 +9,35 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+def _observable_codes(device, n, seed):
+    """Frames an env can show: random tile classes 0..3 (empty-dark, empty-lit, wall, goal) with the agent's tile
+    (class 4) at its view cell (3, 6) only -- the acting table's compact keys cover exactly these (merlin/windows.py
+    compact_window_keys) -- followed by real observations of a stepped vector env."""
+    import numpy as np
+
+    from merlin import MerlinVecEnv
+    from test_gpu_obs_gae import pack
+
+    rs = np.random.RandomState(seed)
+    c = rs.randint(0, 4, size=(n, 49)).astype(np.uint8)
+    c[:, 45] = 4
+    rand = torch.from_numpy(pack(c)).to(device)
+    env = MerlinVecEnv(n, "mediumhard", seed=seed, device=device)
+    frames = [env.reset().clone()]
+    g = torch.Generator(device=device).manual_seed(seed)
+    for _ in range(3):
+        frames.append(env.step(torch.randint(0, 3, (n,), device=device, generator=g))[0].clone())
+    env.close()
+    return torch.cat([rand] + frames)
+
+
 @pytest.mark.parametrize("frames", [None, 1000])
 def test_packed_act_matches_act_codes(device, frames):
     """Both acting layouts of rollout_pack: the all-windows table (large rollouts) and the per-frame
-    conv2 lookups + conv3 GEMM (small rollouts, no 9-GB table)."""
+    conv2 lookups + conv3 GEMM (small rollouts, no 2-GB table)."""
     from merlin.actor_critic import CNNActorCritic
-    from test_gpu_conv2lut import _codes
 
-    _, codes = _codes(device, 700, seed=3)
+    codes = _observable_codes(device, 700, seed=3)
     torch.manual_seed(4)
     ac = CNNActorCritic((56, 56, 3), 3).to(device)
     with torch.no_grad():
@@ -35,9 +56,8 @@ def test_codes_conv3_matches_im2col_path(device):
     conv3 im2col -> GEMM -> bias + ReLU (the per-frame path of evaluate_codes) on the same frames."""
     from merlin import _native as nat
     from merlin.actor_critic import CNNActorCritic
-    from test_gpu_conv2lut import _codes
 
-    _, codes = _codes(device, 900, seed=5)
+    codes = _observable_codes(device, 900, seed=5)
     torch.manual_seed(6)
     ac = CNNActorCritic((56, 56, 3), 3).to(device)
     ea, ec = ac.actor_extractor.network, ac.critic_extractor.network

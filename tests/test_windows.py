@@ -212,3 +212,36 @@ def test_window_and_patch_keys_match_digit_loops():
             pk = pk * 5 + cls[:, a:a + 3, b:b + 3]
     assert torch.equal(window_keys(cls), wk.reshape(-1, 25)) and torch.equal(patch_keys(cls), pk.reshape(-1, 9))
     assert int(pk.max()) == 5 ** 25 - 1
+
+
+def test_compact_window_keys_cover_observable_windows():
+    """The acting table's compact keys (csrc/merlin_window.hip k_codes_conv3, round 5): every window an observation
+    can hold has exactly one key, and the key the kernel computes for a window (restated here) names a table row
+    built for that same window (merlin/windows.py compact_window_keys -> window_rows)."""
+    import torch
+
+    from merlin.windows import compact_window_keys
+
+    keys = compact_window_keys("cpu")
+    assert keys.numel() == 4 ** 9 + 3 * 4 ** 8 and torch.unique(keys).numel() == keys.numel()
+    digits = torch.stack([(keys // 5 ** (8 - i)) % 5 for i in range(9)], 1)
+    agent = digits == 4
+    assert int(agent[: 4 ** 9].sum()) == 0 and bool((agent[4 ** 9:].sum(1) == 1).all())
+
+    def kernel_key(view, wy, wx):  # k_codes_conv3's key of the window at conv2 position (wy, wx)
+        skip = 9 - wx if (wy == 4 and 1 <= wx <= 3) else -1
+        k = 0
+        for a in range(3):
+            for b in range(3):
+                if 3 * a + b != skip:
+                    k = k * 4 + min(int(view[wy + a][wx + b]), 3)
+        return k + (262144 + (wx - 1) * 65536 if skip >= 0 else 0)
+
+    g = torch.Generator().manual_seed(0)
+    for _ in range(200):
+        view = torch.randint(0, 4, (7, 7), generator=g)
+        view[6][3] = 4  # the agent's tile, always at view cell (3, 6)
+        for wy in range(5):
+            for wx in range(5):
+                base5 = sum(int(view[wy + a][wx + b]) * 5 ** (8 - 3 * a - b) for a in range(3) for b in range(3))
+                assert int(keys[kernel_key(view, wy, wx)]) == base5
