@@ -160,6 +160,18 @@ int merlin_env_act_step(merlin_env *env, const float *head_part_dev, int32_t n_p
                         float *logp_dev, float *value_dev, uint32_t *obs_dev, float *reward_dev,
                         uint8_t *terminated_dev, uint8_t *truncated_dev, float *done_dev, double *ep_return_dev,
                         int32_t *ep_length_dev, void *stream);
+/* FOMAML's acting step (src/fomaml.py:54-108: each task's fast_policy.act(state), src/actor_critic.py:48-56), one
+ * frame per task g < groups, each task with its own weights (merlin/grouped_policy.py pack: towers 2g = actor,
+ * 2g + 1 = critic): codes_dev int32[groups][8]; T2 float[2G][2720][64] + b2 [2G][64] (conv1 + conv2 tables);
+ * W3t [2G][576][64] ((ky, kx, ci) x co) + b3 [2G][64]; W4p [2G][512][576] (fc1, columns (p3, co)) + b4 [2G][512];
+ * Wa [G][act_dim][512] + ba [G][act_dim], Wc [G][512] + bc [G] (the heads).  Writes a3_ws [2G][576] (conv3's
+ * output) and head_part float[2][8][G][4]: tower t, fc1 column chunk p (64 columns), the chunk's dot products of
+ * relu(fc1) with the task's head weights (the biases added in chunk 0) -- the partials merlin_env_act_step reads
+ * (with zero biases) to draw and step every task's env.  fp32. */
+int merlin_group_act(const uint32_t *codes_dev, int32_t groups, const float *T2_dev, const float *b2_dev,
+                     const float *W3t_dev, const float *b3_dev, const float *W4p_dev, const float *b4_dev,
+                     const float *Wa_dev, const float *ba_dev, const float *Wc_dev, const float *bc_dev,
+                     int32_t act_dim, float *a3_ws_dev, float *head_part_dev, void *stream);
 /* Look-ahead maps (no reference counterpart: an implementation detail of the auto-reset above).
  * An env's next map depends only on its RNG stream, so it is generated ahead of time into a
  * per-env slot, and an auto-reset takes the slot instead of generating in the step.

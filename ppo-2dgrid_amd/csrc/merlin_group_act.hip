@@ -1,0 +1,179 @@
+// merlin_group_act.hip -- FOMAML's acting step: one frame per task, each task with its own policy weights
+// (src/fomaml.py:54-108 collect_trajectory: fast_policy.act(state) per step; src/actor_critic.py:48-56 act).
+//
+// The batched FOMAML rollout (merlin/fomaml.py) steps G tasks (G = tasks_per_batch = 32 at cfg 5) with G different
+// weight sets, one env each.  Through the generic torch / library path a step was ~15 launches of a few threads'
+// work each (grouped conv2 lookups over 2 blocks, im2col, 4 batched GEMMs, log-softmax, Gumbel draw, copies): ~180 us
+// per step, latency-bound (profiles/r05a_fomaml_kernel_stats.md).  Here a step is two launches plus the fused draw
+// + env step (merlin_env_act_step):
+//
+//   k_group_conv   one block per (task, tower): the frame's 49 tile classes -> conv1 + conv2 by the tower's
+//                  2,720-row table T2 (16 rows per conv2 position, merlin_conv2lut.hip's row layout) + b2, ReLU
+//                  -> conv3 (9 x 64 outputs, 576 MACs each; the 4 waves split the 576-long reduction, summed in
+//                  wave order) + b3, ReLU -> a3 [tower][576] in fc1's (p3, co) column order
+//   k_group_fc1    one block per (task, tower, 64-column chunk of fc1): h = relu(b4 + W4p a3) of its 64 columns
+//                  (a wave per column, lanes over k, a fixed xor tree), then the head dot products of those 64
+//                  columns (actor: the task's A logits' weights, critic: its value weights) summed in wave order;
+//                  chunk 0 adds the task's head biases -> part[tower][chunk][task][4], the partial-sum layout
+//                  merlin_env_act_step / merlin_act_draw read (then called with zero biases)
+//
+// fp32 throughout (products and sums in fp32, as the reference's CPU/torch forward; different summation order).
+#include <algorithm>
+
+#include "merlin_internal.h"
+
+namespace merlin {
+namespace {
+
+constexpr int GA_NROW = 2720, GA_H = 512, GA_K = 576;
+
+__global__ __launch_bounds__(256) void k_group_conv(const uint32_t *__restrict__ codes, const float4 *__restrict__ T2,
+                                                    const float *__restrict__ b2, const float *__restrict__ W3t,
+                                                    const float *__restrict__ b3, float *__restrict__ a3) {
+    __shared__ uint8_t cls[52];
+    __shared__ float4 a2[25][16];
+    __shared__ float red[4][9][64];
+    const int tt = blockIdx.x, g = tt >> 1;  // tower tt = 2 g (actor) / 2 g + 1 (critic) of task g
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid < 49) {
+        const uint32_t word = codes[(size_t)g * MERLIN_OBS_WORDS + (tid >> 3)];
+        cls[tid] = (uint8_t)min((word >> ((tid & 7) * 4)) & 0xfu, 4u);
+    }
+    __syncthreads();
+    // conv2 + b2 + ReLU at the 25 positions (16 float4 columns each)
+    const float4 *tab = T2 + (size_t)tt * GA_NROW * 16;
+    for (int e = tid; e < 25 * 16; e += 256) {
+        const int p = e >> 4, q = e & 15, py = p / 5, px = p - py * 5;
+        int w[9];
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+            for (int b = 0; b < 3; b++) w[a * 3 + b] = cls[(py + a) * 7 + px + b];
+        float4 v[16];
+#pragma unroll
+        for (int ky = 0; ky < 4; ky++)
+#pragma unroll
+            for (int kx = 0; kx < 4; kx++) {
+                const int a = ky >> 1, b = kx >> 1, j = 2 * a + b, c00 = w[a * 3 + b];
+                int row;
+                if (!(ky & 1) && !(kx & 1))
+                    row = 4 * c00 + j;
+                else if (!(ky & 1))
+                    row = 20 + 4 * (5 * c00 + w[a * 3 + b + 1]) + j;
+                else if (!(kx & 1))
+                    row = 120 + 4 * (5 * c00 + w[(a + 1) * 3 + b]) + j;
+                else
+                    row = 220 + 4 * (125 * c00 + 25 * w[a * 3 + b + 1] + 5 * w[(a + 1) * 3 + b] + w[(a + 1) * 3 + b + 1]) +
+                          j;
+                v[ky * 4 + kx] = tab[(size_t)row * 16 + q];
+            }
+        float4 s = v[0];
+#pragma unroll
+        for (int i = 1; i < 16; i++) {
+            s.x += v[i].x;
+            s.y += v[i].y;
+            s.z += v[i].z;
+            s.w += v[i].w;
+        }
+        const float *bb = b2 + (size_t)tt * 64 + q * 4;
+        a2[p][q] = make_float4(fmaxf(s.x + bb[0], 0.0f), fmaxf(s.y + bb[1], 0.0f), fmaxf(s.z + bb[2], 0.0f),
+                               fmaxf(s.w + bb[3], 0.0f));
+    }
+    __syncthreads();
+    // conv3: lane = output channel co, wave wv takes k = tap * 64 + ci in [144 wv, 144 wv + 144) for all 9 positions
+    const float *a2f = reinterpret_cast<const float *>(&a2[0][0]);
+    const float *w3 = W3t + (size_t)tt * GA_K * 64 + lane;
+    float acc[9];
+#pragma unroll
+    for (int p3 = 0; p3 < 9; p3++) acc[p3] = 0.0f;
+    for (int k0 = wv * 144; k0 < wv * 144 + 144; k0 += 8) {
+        float wk[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) wk[u] = w3[(size_t)(k0 + u) * 64];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int k = k0 + u, tap = k >> 6, ci = k & 63, ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+            for (int p3 = 0; p3 < 9; p3++) {
+                const int oy = p3 / 3, ox = p3 - oy * 3;
+                acc[p3] += a2f[((oy + ky) * 5 + ox + kx) * 64 + ci] * wk[u];
+            }
+        }
+    }
+#pragma unroll
+    for (int p3 = 0; p3 < 9; p3++) red[wv][p3][lane] = acc[p3];
+    __syncthreads();
+    for (int e = tid; e < 9 * 64; e += 256) {
+        const int p3 = e >> 6, co = e & 63;
+        const float s = ((red[0][p3][co] + red[1][p3][co]) + red[2][p3][co]) + red[3][p3][co];
+        a3[(size_t)tt * GA_K + e] = fmaxf(s + b3[(size_t)tt * 64 + co], 0.0f);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_group_fc1(const float *__restrict__ a3, const float *__restrict__ W4p,
+                                                   const float *__restrict__ b4, const float *__restrict__ Wa,
+                                                   const float *__restrict__ ba, const float *__restrict__ Wc,
+                                                   const float *__restrict__ bc, int G, int A,
+                                                   float *__restrict__ part) {
+    __shared__ float red[4][4];
+    const int j = blockIdx.x, tt = blockIdx.y, g = tt >> 1, tower = tt & 1;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    float x[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) x[i] = a3[(size_t)tt * GA_K + lane + 64 * i];
+    float hp[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // this wave's head partials over its 16 columns
+    const float *wrow = W4p + (size_t)tt * GA_H * GA_K;
+    for (int n0 = j * 64 + wv * 16; n0 < j * 64 + wv * 16 + 16; n0 += 4) {
+        float d[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float *r = wrow + (size_t)(n0 + c) * GA_K + lane;
+            float s = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 9; i++) s += r[64 * i] * x[i];
+            d[c] = s;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+            for (int c = 0; c < 4; c++) d[c] += __shfl_xor(d[c], off);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const int n = n0 + c;
+            const float h = fmaxf(d[c] + b4[(size_t)tt * GA_H + n], 0.0f);
+            if (tower == 0) {
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+                    if (a < A) hp[a] += h * Wa[((size_t)g * A + a) * GA_H + n];
+            } else {
+                hp[0] += h * Wc[(size_t)g * GA_H + n];
+            }
+        }
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int a = 0; a < 4; a++) red[wv][a] = hp[a];
+    __syncthreads();
+    if (tid < 4) {
+        float s = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+        if (j == 0) s += tower == 0 ? (tid < A ? ba[(size_t)g * A + tid] : 0.0f) : (tid == 0 ? bc[g] : 0.0f);
+        part[(((size_t)tower * gridDim.x + j) * G + g) * 4 + tid] = s;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_group_act(const uint32_t *codes, int G, const float *T2, const float *b2, const float *W3t,
+                            const float *b3, const float *W4p, const float *b4, const float *Wa, const float *ba,
+                            const float *Wc, const float *bc, int A, float *a3, float *part, hipStream_t s) {
+    if (G <= 0) return hipSuccess;
+    if (A < 1 || A > 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_group_conv, dim3(2 * G), dim3(256), 0, s, codes, reinterpret_cast<const float4 *>(T2), b2,
+                       W3t, b3, a3);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_group_fc1, dim3(GA_H / 64, 2 * G), dim3(256), 0, s, a3, W4p, b4, Wa, ba, Wc, bc, G, A, part);
+    return hipGetLastError();
+}
+
+}  // namespace merlin

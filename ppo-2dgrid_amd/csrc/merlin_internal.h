@@ -186,6 +186,9 @@ struct StepOut {
 // through this, never hipMemsetAsync: a memset node captured into a HIP graph replays with a wrong fill value on
 // ROCm 7 (scripts/probe_graph_then.py: 0x80 per byte), and any entry point may end up inside a capture.
 hipError_t zero_async(void *p, size_t bytes, hipStream_t s);
+hipError_t launch_group_act(const uint32_t *codes, int G, const float *T2, const float *b2, const float *W3t,
+                            const float *b3, const float *W4p, const float *b4, const float *Wa, const float *ba,
+                            const float *Wc, const float *bc, int A, float *a3, float *part, hipStream_t s);
 hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s);
 hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s);
 hipError_t launch_env_full_obs(const EnvDev &E, uint8_t *out, hipStream_t s);

@@ -72,6 +72,7 @@ def lib():
     L.merlin_env_seed.argtypes = [vp, u64p, i32, vp]
     L.merlin_env_reset.argtypes = [vp, vp, vp, vp]
     L.merlin_env_step.argtypes = [vp, vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, i32, vp]
+    L.merlin_group_act.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_env_act_step.argtypes = [vp, vp, i32, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp, vp, vp,
                                       vp, vp, vp, vp, vp, vp]
     L.merlin_env_set_refill_interval.argtypes = [vp, i32]
@@ -177,7 +178,7 @@ def check_env_config_layout(L) -> None:
 
 EXPORTED_SYMBOLS = (
     "merlin_version", "merlin_last_error", "merlin_tile_atlas", "merlin_env_config_layout", "merlin_env_create",
-    "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step", "merlin_env_act_step",
+    "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step", "merlin_env_act_step", "merlin_group_act",
     "merlin_env_set_refill_interval", "merlin_env_refill",
     "merlin_env_get_state", "merlin_env_full_obs", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
     "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
@@ -1021,6 +1022,28 @@ H3_TN_CFG = 0
 H3_HEADS_EPILOGUE = True
 H3_TN_CFG_WIN = 2  # the window weight gradient (M = 64)
 H3_TN_SPLITS = 32
+
+
+def group_act(codes, T2, b2, W3t, b3, W4p, b4, Wa, ba, Wc, bc, a3_ws=None, part=None):
+    """FOMAML's acting step over G tasks with per-task weights (merlin_group_act): head partials f32[2, 8, G, 4]
+    (biases added in chunk 0) for merlin_env_act_step / act_draw with zero biases."""
+    G = int(codes.shape[0])
+    A = int(Wa.shape[1])
+    assert codes.dtype == torch.int32 and codes.shape == (G, OBS_WORDS) and codes.is_contiguous()
+    assert T2.shape == (2 * G, 2720, 64) and W3t.shape == (2 * G, 576, 64) and W4p.shape == (2 * G, 512, 576)
+    assert b2.numel() == 2 * G * 64 and b3.numel() == 2 * G * 64 and b4.numel() == 2 * G * 512
+    assert Wa.shape == (G, A, 512) and ba.numel() == G * A and Wc.numel() == G * 512 and bc.numel() == G
+    for t in (T2, b2, W3t, b3, W4p, b4, Wa, ba, Wc, bc):
+        assert t.dtype == torch.float32 and t.is_contiguous()
+    if a3_ws is None:
+        a3_ws = torch.empty((2 * G, 576), dtype=torch.float32, device=codes.device)
+    if part is None:
+        part = torch.empty((2, 8, G, 4), dtype=torch.float32, device=codes.device)
+    with KernelTimer.span("k_group_act", G * 2 * (25 * 16 * 256 + 576 * 64 * 4 + 512 * 576 * 4)):
+        check(lib().merlin_group_act(ptr(codes), G, ptr(T2), ptr(b2), ptr(W3t), ptr(b3), ptr(W4p), ptr(b4), ptr(Wa),
+                                     ptr(ba), ptr(Wc), ptr(bc), A, ptr(a3_ws), ptr(part), stream_of(codes)),
+              "merlin_group_act")
+    return part
 
 
 def h3_amax(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -32,6 +32,10 @@ from . import grouped_policy as gp
 from .actor_critic import CNNActorCritic
 from .envs import MerlinVecEnv
 
+# the rollouts' acting step through merlin_group_act + merlin_env_act_step (False: grouped_policy.act_packed)
+FUSED_ACT = True
+
+
 class FOMAML:
     def __init__(self, scenario_creator, lr_inner=0.01, lr_outer=3e-4, device="cuda", difficulty="medium"):
         self.sc = scenario_creator
@@ -49,6 +53,13 @@ class FOMAML:
         self._task_seeds = None
         self._rollouts = {}  # per rollout kind: storage, weight pack and its captured HIP graph
         self.rollout_graph = True
+        # the acting step as merlin_group_act + merlin_env_act_step (two library launches + the draw fused into the
+        # env step) instead of grouped_policy.act_packed (~15 torch / library launches) + merlin_env_step; the draws
+        # are counter-based (keyed by this seed, the rollout counter, the step and the task's env), so a captured
+        # rollout draws afresh on every replay once the counter is bumped inside it
+        self.fused_act = FUSED_ACT
+        self._act_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self._act_epoch = torch.zeros(1, dtype=torch.int64, device=self.device)
 
     # ------------------------------------------------------------------ envs
     def _task_env(self, task_seeds) -> MerlinVecEnv:
@@ -77,7 +88,10 @@ class FOMAML:
               "epr": torch.zeros((steps, G), dtype=torch.float64, device=dev),
               "epl": torch.zeros((steps, G), dtype=torch.int32, device=dev),
               "last": torch.zeros(G, dtype=torch.float32, device=dev),
-              "pack": gp.pack(params)}
+              "pack": gp.pack(params),
+              "part": torch.zeros((2, 8, G, 4), dtype=torch.float32, device=dev),
+              "a3ws": torch.zeros((2 * G, 576), dtype=torch.float32, device=dev),
+              "zb": torch.zeros(4, dtype=torch.float32, device=dev)}
         self._rollouts[key] = st
         return st
 
@@ -85,6 +99,17 @@ class FOMAML:
         steps = st["steps"]
         pk = st["pack"]
         env.reset(out=st["codes"][0])  # = env.reset(seed=task_seed) for every task
+        if self.fused_act:
+            self._act_epoch.add_(1)  # a fresh draw on every replay
+            A = int(pk["ba_r"].shape[1])
+            for t in range(steps):
+                part = gp.act_parts(pk, st["codes"][t], part=st["part"], a3_ws=st["a3ws"])
+                env.act_step_into(part, st["zb"][:A], st["zb"][:1], (st["act"][t], st["logp"][t], st["val"][t]),
+                                  st["codes"][t + 1], st["rew"][t], None, None, st["done"][t], st["epr"][t],
+                                  st["epl"][t], seed=self._act_seed, epoch=self._act_epoch, step=t)
+            part = gp.act_parts(pk, st["codes"][steps], part=st["part"], a3_ws=st["a3ws"])
+            st["last"].copy_(part[1, :, :, 0].sum(0))
+            return
         for t in range(steps):
             gp.act_packed(pk, st["codes"][t], out=(st["act"][t], st["logp"][t], st["val"][t]))
             env.step_into(st["act"][t], st["codes"][t + 1], st["rew"][t], None, None, st["done"][t], st["epr"][t],

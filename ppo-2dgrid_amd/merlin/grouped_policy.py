@@ -118,7 +118,11 @@ def pack(params):
             "W4t": W4.reshape(T, H, 64, 9).transpose(2, 3).reshape(T, H, 576).transpose(1, 2).contiguous(),
             "b4": torch.stack([params["actor.0.bias"], params["critic.0.bias"]], 1).reshape(T, 1, H).contiguous(),
             "Wa": params["actor.2.weight"].transpose(1, 2).contiguous(), "ba": params["actor.2.bias"].unsqueeze(1),
-            "Wc": params["critic.2.weight"].transpose(1, 2).contiguous(), "bc": params["critic.2.bias"].unsqueeze(1)}
+            "Wc": params["critic.2.weight"].transpose(1, 2).contiguous(), "bc": params["critic.2.bias"].unsqueeze(1),
+            # merlin_group_act's layouts: fc1 rows with (p3, co) columns, the heads' weight rows and biases per task
+            "W4p": W4.reshape(T, H, 64, 9).transpose(2, 3).reshape(T, H, 576).contiguous(),
+            "Wa_r": params["actor.2.weight"].contiguous(), "ba_r": params["actor.2.bias"].contiguous(),
+            "Wc_r": params["critic.2.weight"].contiguous(), "bc_r": params["critic.2.bias"].contiguous()}
 
 
 @torch.no_grad()
@@ -154,3 +158,12 @@ def act_packed(pk, codes, deterministic=False, out=None):
         out[2].copy_(value)
         return out
     return a, lp, value
+
+
+def act_parts(pk, codes, part=None, a3_ws=None):
+    """The acting step of every group's frame codes int32 [G, 8] with its own weights in one library call
+    (merlin_group_act: conv tables + conv3 per (task, tower), fc1 + the heads' dot products per 64-column chunk):
+    head partials f32[2, 8, G, 4] with the head biases folded into chunk 0, for merlin_env_act_step (draw + env step
+    in one launch, zero biases) or act_draw.  The logits / value are the sums over the 8 chunks."""
+    return nat.group_act(codes, pk["T2"], pk["b2"], pk["W3t"], pk["b3"], pk["W4p"], pk["b4"], pk["Wa_r"], pk["ba_r"],
+                         pk["Wc_r"], pk["bc_r"], a3_ws=a3_ws, part=part)

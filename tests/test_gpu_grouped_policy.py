@@ -81,3 +81,30 @@ def test_grouped_act_packed_matches_per_task_models(device):
         p = lp3.exp()
         freq = cnt[g] / 400
         assert ((freq - p).abs() <= 5 * torch.sqrt(p * (1 - p) / 400) + 0.01).all(), (g, freq, p)
+
+
+@pytest.mark.parametrize("G", [1, 6, 32])
+def test_group_act_parts_match_per_task_models(device, G):
+    """merlin_group_act (FOMAML's acting step in two launches, round 5): the head partials summed (biases folded into
+    chunk 0) give each task's logits / value of its own model on its own frame; drawn deterministically through
+    act_draw with zero biases they give that model's argmax action and log-prob."""
+    from merlin import _native as nat
+    from merlin import grouped_policy as gp
+
+    models, params = _tasks(device, G, seed=13 + G)
+    codes = _codes(device, G, seed=G)
+    pk = gp.pack({k: v.detach() for k, v in params.items()})
+    part = gp.act_parts(pk, codes)
+    assert part.shape == (2, 8, G, 4)
+    logits, value = part[0].sum(0)[:, :3], part[1].sum(0)[:, 0]
+    zb = torch.zeros(4, device=device)
+    a, lp, v = nat.act_draw(part.contiguous(), zb[:3], zb[:1], deterministic=True)
+    for g, m in enumerate(models):
+        with torch.no_grad():
+            lg, vv = m._forward_codes(codes[g:g + 1], None)
+            a2, lp2, v2 = m.act_codes(codes[g:g + 1], deterministic=True)
+        torch.testing.assert_close(logits[g], lg[0], rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(value[g], vv[0], rtol=1e-5, atol=1e-5)
+        assert int(a[g]) == int(a2[0])
+        torch.testing.assert_close(lp[g], lp2[0], rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(v[g], v2[0], rtol=1e-5, atol=1e-5)
