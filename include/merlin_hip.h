@@ -152,8 +152,8 @@ int merlin_env_step(merlin_env *env, const int64_t *actions_dev, int32_t n_steps
  * the action of env i is drawn from the acting GEMM's head partials head_part float[2][n_parts][N][4] exactly as
  * merlin_act_draw draws it (log-softmax, argmax or the counter-keyed race keyed by seed, *epoch, step and
  * env_offset + i; biases added; action / logp / value written to action / logp / value, int64 / float / float[N]),
- * then stepped as merlin_env_step with n_steps = 1 and auto-reset (a reset whose look-ahead slot is empty
- * generates its map in the same launch).  Output pointers other than action / logp / value may be NULL. */
+ * then stepped as merlin_env_step with n_steps = 1 and auto-reset.  Output pointers other than action / logp /
+ * value may be NULL. */
 int merlin_env_act_step(merlin_env *env, const float *head_part_dev, int32_t n_parts, const float *b_actor_dev,
                         const float *b_critic_dev, int32_t act_dim, int32_t deterministic, uint64_t seed,
                         const int64_t *epoch_dev, int64_t step, int64_t env_offset, int64_t *action_dev,

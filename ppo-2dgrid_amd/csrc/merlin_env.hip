@@ -903,12 +903,9 @@ static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t 
     const int nb = (E.n + SBLK - 1) / SBLK;
     if (!O.autoreset) {  // no resets: the lean kernel
         hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
-    } else if (O.act.part) {
-        // the fused draw + step of the rollout (merlin_env_act_step): a reset whose look-ahead slot is empty
-        // generates its map in this launch (the multi-step kernel's form) instead of in a k_env_fallback launch --
-        // the rollout refills every slot beside each act, so that launch found nothing to do in almost every step
-        hipLaunchKernelGGL((k_env_step<SP, false>), dim3(nb), dim3(SBLK), 0, s, E, O);
-    } else if (O.n_steps == 1) {  // empty look-ahead slots reset in k_env_fallback
+    } else if (O.n_steps == 1) {  // also the fused draw + step (merlin_env_act_step): the generator stays out of the
+        // step kernel (k_env_step<SP, false> with it inlined takes 241 VGPRs + 92 B of scratch per lane: 15.7 against
+        // 8 us per 4096-env step, profiles/r05c_kernel_stats.md)  // empty look-ahead slots reset in k_env_fallback
         hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -589,7 +589,9 @@ __device__ __forceinline__ int g_swz(int r) { return (r >> 1) & 7; }
 
 // AP: A arrives as plane images too ([M][K/8][2][8] f16, h3_split's layout: 4 B per value like fp32, so the DMA
 // addressing is the same) -- no split at all, A's fragments read like B's.
-template <int BM, int BN, int WGM, int WGN, int EPI, bool KP, bool AP = false, bool PR = false>
+// ABL (probe ablations, round 5): 1 = no DMA in the main loop (compute on whatever the stages hold), 2 = no MFMAs
+// (fragment reads kept live), 3 = neither fragment reads nor MFMAs (the DMA stream alone)
+template <int BM, int BN, int WGM, int WGN, int EPI, bool KP, bool AP = false, bool PR = false, int ABL = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restrict__ A, const u32x4 *__restrict__ B,
                                                            const uint32_t *__restrict__ amaxA,
                                                            const uint32_t *__restrict__ amaxB, int64_t M, int N,
@@ -634,6 +636,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
     typedef __attribute__((address_space(3))) void lds_void;
     typedef __attribute__((address_space(1))) void gbl_void;
     auto issue = [&](int kt, int st) {
+        if constexpr (ABL == 1) {
+            if (kt >= 2) return;
+        }
         u32x4 *base = lds + st * STG + w * 64;
 #pragma unroll
         for (int i = 0; i < GA; i++)
@@ -668,6 +673,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
         u32x4 a[TM][2], b[TN][2];
     };
     auto read = [&](int st, int kh, Frag &f) {
+        if constexpr (ABL == 3) return;
         const u32x4 *sAl = lds + st * STG, *sBl = sAl + BM * 8;
 #pragma unroll
         for (int j = 0; j < TN; j++) {
@@ -694,6 +700,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
         }
     };
     auto mfmas = [&](const Frag &f) {
+        if constexpr (ABL >= 2) {
+#pragma unroll
+            for (int i = 0; i < TM; i++) asm volatile("" ::"v"(f.a[i][0]), "v"(f.a[i][1]));
+#pragma unroll
+            for (int j = 0; j < TN; j++) asm volatile("" ::"v"(f.b[j][0]), "v"(f.b[j][1]));
+            return;
+        }
         if constexpr (PR) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < TM; i++)
@@ -1457,7 +1470,7 @@ hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, cons
     return hipGetLastError();
 }
 
-template <int BM, int BN, int WGM, int WGN, bool KP, bool AP = false, bool PR = false>
+template <int BM, int BN, int WGM, int WGN, bool KP, bool AP = false, bool PR = false, int ABL = 0>
 hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                       int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
                       hipStream_t s) {
@@ -1468,11 +1481,11 @@ hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, con
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
     if (bias)
-        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP, AP, PR>), grid, block, 0, s, A, B, amaxA, amaxB, M, N,
-                           K, sA, sB, bias, C, sC, tiles_n);
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP, AP, PR, ABL>), grid, block, 0, s, A, B, amaxA, amaxB, M,
+                           N, K, sA, sB, bias, C, sC, tiles_n);
     else
-        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP, AP, PR>), grid, block, 0, s, A, B, amaxA, amaxB, M, N,
-                           K, sA, sB, nullptr, C, sC, tiles_n);
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP, AP, PR, ABL>), grid, block, 0, s, A, B, amaxA, amaxB, M,
+                           N, K, sA, sB, nullptr, C, sC, tiles_n);
     return hipGetLastError();
 }
 
@@ -1589,6 +1602,13 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 45: return H3_NTGQ(256, 128, 4, 2, true);
         case 46: return H3_NTGQ(256, 128, 4, 2, false);
 #undef H3_NTGQ
+#define H3_NTGA(BM, BN, WM, WN, ABL) \
+    ((a_rows || head_part) ? hipErrorInvalidValue                                                  \
+            : ntg_launch<BM, BN, WM, WN, true, true, false, ABL>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s))
+        case 47: return H3_NTGA(128, 256, 2, 4, 1);
+        case 48: return H3_NTGA(128, 256, 2, 4, 2);
+        case 49: return H3_NTGA(128, 256, 2, 4, 3);
+#undef H3_NTGA
         default: return hipErrorInvalidValue;
     }
 }

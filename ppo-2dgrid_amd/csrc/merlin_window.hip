@@ -192,53 +192,63 @@ __global__ __launch_bounds__(256) void k_window_conv3_copy(float4 *Y3, uint64_t 
 // all 5^9 = 1,953,125 class patterns: a 4.3x smaller table (2.1 GB for both towers), built in that fraction of the
 // time.  (Valid observations only: a class-4 tile elsewhere is read as class 3.)
 constexpr int64_t ALL_WINDOWS = 458752;  // 4^9 + 3 * 4^8
+// The 25 window keys of a frame are computed once per block (CC_F frames per block, keys in LDS), not by each of the
+// 16 lanes of each of the 9 output rows that read them: round 4's per-lane key arithmetic (81 class lookups per lane)
+// made the kernel VALU-bound (35 us per 4096-frame step; 57 us once the compact key's slot skipping was added).
+constexpr int CC_F = 4;  // 1,024 blocks of 256 threads at 4,096 frames: ~4.5 outputs (9 row gathers each) per thread
 __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict__ codes, int64_t n,
                                                      const float4 *__restrict__ Q, const float4 *__restrict__ b3,
                                                      int T, float4 *__restrict__ Y3, uint32_t *__restrict__ amax) {
-    const int64_t total = (int64_t)T * n * 9 * 16;
+    __shared__ uint32_t keys[CC_F][25];
     uint32_t mx[2] = {0u, 0u};  // max |Y3| per tower as float bits (fc1's h3 operand scale), when amax != null
-    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-        const int c = (int)(e & 15);
-        const int64_t r = e >> 4, tu = r / 9;
-        const int p3 = (int)(r - tu * 9), t = (int)(tu / n);
-        const int64_t u = tu - (int64_t)t * n;
-        const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + u * 8);
-        const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + u * 8 + 4);
-        const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        auto cls = [&](int y, int x) -> uint32_t {  // tile class, 0..3 (the agent's tile is keyed by position)
-            const int cell = y * 7 + x;
-            return min((w[cell >> 3] >> (4 * (cell & 7))) & 15u, 3u);
-        };
-        const int oy = p3 / 3, ox = p3 - 3 * (p3 / 3);
-        const float4 *qt = Q + (size_t)t * ALL_WINDOWS * 9 * 16 + c;
-        float4 v[9];
-#pragma unroll
-        for (int tap = 0; tap < 9; tap++) {
-            const int wy = oy + tap / 3, wx = ox + tap - 3 * (tap / 3);
+    for (int64_t f0 = (int64_t)blockIdx.x * CC_F; f0 < n; f0 += (int64_t)gridDim.x * CC_F) {
+        const int nf = (int)std::min<int64_t>(CC_F, n - f0);
+        for (int e = threadIdx.x; e < nf * 25; e += 256) {
+            const int f = e / 25, p = e - f * 25, wy = p / 5, wx = p - wy * 5;
+            const uint4 w0 = *reinterpret_cast<const uint4 *>(codes + (f0 + f) * 8);
+            const uint4 w1 = *reinterpret_cast<const uint4 *>(codes + (f0 + f) * 8 + 4);
+            const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
             const bool agent = wy == 4 && wx >= 1 && wx <= 3;
             const int skip = agent ? 9 - wx : -1;  // local slot 3 * 2 + (3 - wx) of the agent's tile
             uint32_t key = 0;
 #pragma unroll
             for (int a = 0; a < 3; a++)
 #pragma unroll
-                for (int b = 0; b < 3; b++)
-                    if (3 * a + b != skip) key = key * 4u + cls(wy + a, wx + b);
+                for (int b = 0; b < 3; b++) {
+                    const int cell = (wy + a) * 7 + wx + b;
+                    const uint32_t c = min((w[cell >> 3] >> (4 * (cell & 7))) & 15u, 3u);  // 0..3: see above
+                    if (3 * a + b != skip) key = key * 4u + c;
+                }
             if (agent) key += 262144u + (uint32_t)(wx - 1) * 65536u;
-            v[tap] = qt[((size_t)key * 9 + tap) * 16];
+            keys[f][p] = key;
         }
-        float4 acc = v[0];
+        __syncthreads();
+        const int per_t = nf * 9 * 16;
+        for (int e = threadIdx.x; e < T * per_t; e += 256) {
+            const int t = e / per_t, r = e - t * per_t, c = r & 15, fp = r >> 4, f = fp / 9, p3 = fp - f * 9;
+            const int oy = p3 / 3, ox = p3 - oy * 3;
+            const float4 *qt = Q + (size_t)t * ALL_WINDOWS * 9 * 16 + c;
+            float4 v[9];
 #pragma unroll
-        for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
-        const float4 b = b3[t * 16 + c];
-        const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
-                                     relu_nan(acc.w + b.w));
-        Y3[e] = y;
-        if (amax) {
-            const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
-                                        std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
-            if (t == 0) mx[0] = std::max(mx[0], m);
-            else mx[1] = std::max(mx[1], m);
+            for (int tap = 0; tap < 9; tap++) {
+                const int ky = tap / 3, kx = tap - ky * 3;
+                v[tap] = qt[((size_t)keys[f][(oy + ky) * 5 + ox + kx] * 9 + tap) * 16];
+            }
+            float4 acc = v[0];
+#pragma unroll
+            for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
+            const float4 b = b3[t * 16 + c];
+            const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
+                                         relu_nan(acc.w + b.w));
+            Y3[(((size_t)t * n + f0 + f) * 9 + p3) * 16 + c] = y;
+            if (amax) {
+                const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
+                                            std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
+                if (t == 0) mx[0] = std::max(mx[0], m);
+                else mx[1] = std::max(mx[1], m);
+            }
         }
+        __syncthreads();
     }
     if (amax) block_amax2(mx, T, amax);
 }
@@ -604,7 +614,7 @@ hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, 
                               uint32_t *amax, hipStream_t s) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
-    const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
+    const int grid = (int)std::min<int64_t>((n + CC_F - 1) / CC_F, 256 * 32);
     hipLaunchKernelGGL(k_codes_conv3, dim3(grid), dim3(256), 0, s, codes, n, reinterpret_cast<const float4 *>(Q),
                        reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), amax);
     return hipGetLastError();

@@ -73,7 +73,7 @@ class _PPOLoss(torch.autograd.Function):
 # (False: one row zeroed by a kernel before every step -- 256 more launches per captured rollout)
 ROLLOUT_SCALE_ROWS = True
 # the rollout's draw from the acting GEMM's head partials fused into the env step (merlin_env_act_step; False:
-# k_act_draw + merlin_env_step + k_env_fallback, three launches per step instead of one)
+# k_act_draw + merlin_env_step, one launch more per step)
 FUSE_ACT_STEP = True
 
 

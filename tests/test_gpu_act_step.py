@@ -1,7 +1,7 @@
 """GPU: the rollout's draw fused into the env step (merlin_env_act_step, round 5) against the two launches it replaces
 (merlin_act_draw, then merlin_env_step): the same actions / log-probs / values and the same env trajectory bit for
 bit, over many steps with frequent episode ends (short max_steps, so resets take look-ahead slots and, when a slot is
-empty, generate their map in the fused launch), sampled and deterministic, 16x16 and the 22x22 layout."""
+empty, take the k_env_fallback path), sampled and deterministic, 16x16 and the 22x22 layout."""
 import pytest
 import torch
 
