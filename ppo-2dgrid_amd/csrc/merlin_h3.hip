@@ -591,7 +591,12 @@ __device__ __forceinline__ int g_swz(int r) { return (r >> 1) & 7; }
 // addressing is the same) -- no split at all, A's fragments read like B's.
 // ABL (probe ablations, round 5): 1 = no DMA in the main loop (compute on whatever the stages hold), 2 = no MFMAs
 // (fragment reads kept live), 3 = neither fragment reads nor MFMAs (the DMA stream alone)
-template <int BM, int BN, int WGM, int WGN, int EPI, bool KP, bool AP = false, bool PR = false, int ABL = 0>
+// ORD (round 5): in the first half step the MFMAs are issued before the reads of the second half -- with the reads
+// first, hipcc waits lgkmcnt(0) for them before the first MFMA (the MFMAs' operands come from the reads issued after
+// the previous barrier, and it does not count the newer ones out), so every other half step's MFMAs waited for a
+// full LDS read round trip (the .s of cfg 42)
+template <int BM, int BN, int WGM, int WGN, int EPI, bool KP, bool AP = false, bool PR = false, int ABL = 0,
+          bool ORD = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restrict__ A, const u32x4 *__restrict__ B,
                                                            const uint32_t *__restrict__ amaxA,
                                                            const uint32_t *__restrict__ amaxB, int64_t M, int N,
@@ -722,6 +727,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
         split(f);
         mfmas(f);
     };
+    auto touch = [&](const Frag &f) {
+#pragma unroll
+        for (int i = 0; i < TM; i++) asm volatile("" ::"v"(f.a[i][0]), "v"(f.a[i][1]));
+#pragma unroll
+        for (int j = 0; j < TN; j++) asm volatile("" ::"v"(f.b[j][0]), "v"(f.b[j][1]));
+    };
     int st = 0;
     if constexpr (KP) {
         // each half step's MFMAs run while the next half step's fragments are read: split kh 0, [read kh 1 | MFMA
@@ -737,11 +748,24 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
             const int sn = next(st);
             issue(kt + 2, next(sn));  // the stage read in step kt - 1
             split(f0);
-            read(st, 1, f1);
+            if constexpr (ORD) {
+                mfmas(f0);
+                __builtin_amdgcn_sched_barrier(0);
+                read(st, 1, f1);
+            } else {
+                read(st, 1, f1);
+                __builtin_amdgcn_sched_barrier(0);
+                mfmas(f0);
+            }
             __builtin_amdgcn_sched_barrier(0);
-            mfmas(f0);
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+            if constexpr (ORD) {
+                // the compiler's own wait for f1 here (a use of its registers), so it does not add one after the
+                // barrier, where it would also cover the reads of the next half
+                touch(f1);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+            }
             __builtin_amdgcn_s_barrier();
             split(f1);
             read(sn, 0, f0);
@@ -753,10 +777,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntg(const float *__restri
         if (kt + 1 < nk) {  // step nk - 2: no DMA left to issue
             const int sn = next(st);
             split(f0);
-            read(st, 1, f1);
+            if constexpr (ORD) {
+                mfmas(f0);
+                __builtin_amdgcn_sched_barrier(0);
+                read(st, 1, f1);
+            } else {
+                read(st, 1, f1);
+                __builtin_amdgcn_sched_barrier(0);
+                mfmas(f0);
+            }
             __builtin_amdgcn_sched_barrier(0);
-            mfmas(f0);
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ORD) touch(f1);
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             split(f1);
@@ -1470,7 +1501,7 @@ hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, cons
     return hipGetLastError();
 }
 
-template <int BM, int BN, int WGM, int WGN, bool KP, bool AP = false, bool PR = false, int ABL = 0>
+template <int BM, int BN, int WGM, int WGN, bool KP, bool AP = false, bool PR = false, int ABL = 0, bool ORD = false>
 hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                       int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
                       hipStream_t s) {
@@ -1481,11 +1512,11 @@ hipError_t ntg_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, con
     if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
     if (bias)
-        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP, AP, PR, ABL>), grid, block, 0, s, A, B, amaxA, amaxB, M,
-                           N, K, sA, sB, bias, C, sC, tiles_n);
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 1, KP, AP, PR, ABL, ORD>), grid, block, 0, s, A, B, amaxA, amaxB,
+                           M, N, K, sA, sB, bias, C, sC, tiles_n);
     else
-        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP, AP, PR, ABL>), grid, block, 0, s, A, B, amaxA, amaxB, M,
-                           N, K, sA, sB, nullptr, C, sC, tiles_n);
+        hipLaunchKernelGGL((k_h3_ntg<BM, BN, WGM, WGN, 0, KP, AP, PR, ABL, ORD>), grid, block, 0, s, A, B, amaxA, amaxB,
+                           M, N, K, sA, sB, nullptr, C, sC, tiles_n);
     return hipGetLastError();
 }
 
@@ -1564,6 +1595,10 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
     const int64_t sB = b_stride / 8 * 2;  // chunks
 #define H3_NT(BM, BN, WM, WN, PIPE) \
     nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, hd, s)
+    if (cfg >= 60 && cfg < 70) {  // both operands as plane images (merlin_h3p.hip)
+        if (a_rows || head_part || P) return hipErrorInvalidValue;
+        return launch_h3p_gemm_nt(A, amaxA, B, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, cfg, s);
+    }
     switch (cfg) {
         case 0: return H3_NT(256, 128, 4, 2, false);
         case 1: return H3_NT(128, 192, 4, 2, false);
@@ -1609,6 +1644,15 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 48: return H3_NTGA(128, 256, 2, 4, 2);
         case 49: return H3_NTGA(128, 256, 2, 4, 3);
 #undef H3_NTGA
+#define H3_NTGO(BM, BN, WM, WN, AP, ABL) \
+    ((a_rows || head_part) ? hipErrorInvalidValue                                                  \
+            : ntg_launch<BM, BN, WM, WN, true, AP, false, ABL, true>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s))
+        case 50: return H3_NTGO(128, 256, 2, 4, true, 0);
+        case 51: return H3_NTGO(256, 128, 4, 2, true, 0);
+        case 52: return H3_NTGO(128, 192, 4, 2, true, 0);
+        case 53: return H3_NTGO(128, 256, 2, 4, true, 1);  // ablation: no DMA in the main loop
+        case 54: return H3_NTGO(128, 256, 2, 4, false, 0);  // fp32 A split at the fragment reads
+#undef H3_NTGO
         default: return hipErrorInvalidValue;
     }
 }

@@ -1,0 +1,274 @@
+// merlin_h3p.hip -- fc1's NT GEMM with BOTH operands already in h3 plane form (round 5): no split in the kernel,
+// both operands staged by LDS-DMA three k steps deep, the LDS fragment reads interleaved with the MFMAs.
+//
+// Why hand-placed waits (profiles/r05a_probe_h3_planes.log, the .s of k_h3_ntg): with the fragment reads as plain
+// loads, hipcc waited lgkmcnt(0) before the first MFMA of every other half step -- the MFMAs' operands came from
+// reads issued after the previous barrier, and the wait also covered the reads issued for the next half -- so the
+// matrix pipe drained for an LDS round trip twice per k step.  Ablations of that kernel at the update's shape: 505
+// us with everything, 400 us with no DMA in the loop, 384 us for the DMA stream alone.
+//
+// Here every half step is 3 TM TN MFMAs (TM x TN tiles of 32x32x16 x {hi, lo, lo}) with the 2 (TM + TN) fragment
+// reads of the next half interleaved one per MFMA (sched_group_barrier), and the k loop is unrolled (one
+// instantiation per K), so the compiler's lgkmcnt waits are exact counts: the reads of a half are waited for once,
+// by the first MFMA that needs them (the MFMAs still in the pipe cover it).
+//
+// Layouts as merlin_h3.hip's k_h3_ntg: operand rows of K/8 groups x (hi, lo) x 8 f16 (h3_split), a k step (32
+// values) = 8 16-B chunks per row; LDS image rows of 8 chunks, chunk c of row r at slot c ^ ((r >> 1) & 7), the
+// permutation applied to the DMA's global source address (a DMA writes lane-linear).
+#include <algorithm>
+#include <type_traits>
+
+#include "merlin_internal.h"
+
+namespace merlin {
+namespace {
+
+typedef _Float16 p_f16x8 __attribute__((ext_vector_type(8)));
+typedef float p_f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t p_u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr float P_LO_INV = 1.0f / 2048.0f;
+
+__device__ __forceinline__ p_f32x16 p_mfma(const p_u32x4 a, const p_u32x4 b, p_f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(p_f16x8, a), __builtin_bit_cast(p_f16x8, b), c, 0,
+                                                   0, 0);
+}
+__device__ __forceinline__ float p_relu(float v) { return v != v ? v : fmaxf(v, 0.0f); }
+__device__ __forceinline__ int p_xcd_tile(int b, int nb) {
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+__device__ __forceinline__ int p_exp(uint32_t amax) {  // merlin_h3.hip h3_exp
+    if (amax == 0u) return 0;
+    const int e = (int)((amax >> 23) & 0xffu) - 127;
+    return std::min(std::max(14 - e, -120), 115);
+}
+__device__ __forceinline__ float p_pow2(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+__device__ __forceinline__ uint32_t p_amax(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int p_swz(int r) { return (r >> 1) & 7; }
+
+template <int V>
+using IC = std::integral_constant<int, V>;
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(IC<I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+
+typedef __attribute__((address_space(3))) p_u32x4 lds_u32x4;
+// one 16-B LDS fragment read (a plain load: the k loop is unrolled, so the compiler's waits are exact counts)
+__device__ __forceinline__ void lds_rd(p_u32x4 &d, uint32_t addr) { d = *(const lds_u32x4 *)(uintptr_t)addr; }
+
+template <int BM, int BN, int WGM, int WGN, int EPI, int NK>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restrict__ A, const p_u32x4 *__restrict__ B,
+                                                          const uint32_t *__restrict__ amaxA,
+                                                          const uint32_t *__restrict__ amaxB, int64_t M, int N, int K,
+                                                          int64_t sA, int64_t sB, const float *__restrict__ bias,
+                                                          float *__restrict__ C, int64_t sC, int tiles_n) {
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int NR = 2 * (TM + TN), NM = 3 * TM * TN;  // fragment reads / MFMAs per half step
+    static_assert(NM >= NR, "a read behind every MFMA");
+    constexpr int G = (BM + BN) * 8 / NT;  // DMA instructions per thread and k step
+    static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "whole DMA instructions per thread");
+    constexpr int STG = (BM + BN) * 8;  // chunks per stage
+    constexpr uint32_t STG_B = STG * 16;
+    __shared__ p_u32x4 lds[3 * STG];
+
+    const int t = blockIdx.y;
+    const int L = p_xcd_tile(blockIdx.x, gridDim.x);
+    const int tm = L / tiles_n, tn = L - tm * tiles_n;
+    const int64_t m0 = (int64_t)tm * BM;
+    const int n0 = tn * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+    const int64_t row_ch = K / 4;  // chunks per operand row (4 B per value, planes)
+
+    // the scales first: an ordinary load consumed after a DMA is issued makes the compiler wait for the DMA too
+    const int eA = p_exp(p_amax(amaxA + t)), eB = p_exp(p_amax(amaxB + t));
+    // DMA sources as 32-bit chunk offsets from the uniform row-block bases (6 VGPRs, not 6 64-bit pointers): A's
+    // block rows m0.. and B's n0.. (the last A rows clamped to M - 1: read, never stored)
+    const p_u32x4 *baseA = A + t * sA + m0 * row_ch, *baseB = B + t * sB + (int64_t)n0 * row_ch;
+    uint32_t off[G];
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+        const int q = i * NT + tid, r = q >> 3, c = (q & 7) ^ p_swz(r);
+        off[i] = r < BM ? (uint32_t)(std::min<int64_t>(r, M - 1 - m0) * row_ch + c) : (uint32_t)((r - BM) * row_ch + c);
+    }
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef __attribute__((address_space(1))) void gbl_void;
+    auto issue = [&](int kt, int st) __attribute__((always_inline)) {
+        p_u32x4 *base = lds + st * STG + w * 64;
+#pragma unroll
+        for (int i = 0; i < G; i++) {
+            const int q0 = i * NT;  // instruction-uniform: which operand
+            const p_u32x4 *b = (q0 >> 3) < BM ? baseA : baseB;
+            __builtin_amdgcn_global_load_lds((gbl_void *)(b + off[i] + kt * 8), (lds_void *)(base + i * NT), 16, 0, 0);
+        }
+    };
+
+    // fragment addresses (bytes, stage 0): A tile i / B tile j at half kh, plane p -> row r, chunk 2 (2 kh + fh) + p
+    const int fr = lane & 31, fh = lane >> 5;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) p_u32x4 *)lds;
+    uint32_t adA[2][2], adB[2][2];  // [kh][p], tile 0; tile i is +32 i rows (same swizzle)
+    {
+        const int ra = wm * WTM + fr, rb = BM + wn * WTN + fr;
+#pragma unroll
+        for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+                const int c = 2 * (2 * kh + fh) + p;
+                adA[kh][p] = lds0 + (uint32_t)(ra * 8 + (c ^ p_swz(ra))) * 16u;
+                adB[kh][p] = lds0 + (uint32_t)(rb * 8 + (c ^ p_swz(rb))) * 16u;
+            }
+    }
+    struct Frag {
+        p_u32x4 a[TM][2], b[TN][2];  // [tile][plane]
+    };
+    // the 8 reads of half kh of stage st, interleaved behind the 12 MFMAs on f (fenced one by one)
+    p_f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = p_f32x16{};
+            lo[i][j] = p_f32x16{};
+        }
+    // the k-th of the NR fragment reads of half KH into g (k, KH compile-time: no runtime-indexed fragment arrays)
+    auto rd = [&](Frag &g, auto K_, uint32_t so, auto KH) __attribute__((always_inline)) {
+        constexpr int k = decltype(K_)::value, kh = decltype(KH)::value;
+        if constexpr (k < 2 * TM)
+            lds_rd(g.a[k >> 1][k & 1], adA[kh][k & 1] + so + (k >> 1) * 32 * 128);
+        else
+            lds_rd(g.b[(k - 2 * TM) >> 1][k & 1], adB[kh][k & 1] + so + ((k - 2 * TM) >> 1) * 32 * 128);
+    };
+    auto mf = [&](const Frag &f, auto M_) __attribute__((always_inline)) {  // MFMA m: tile (i, j), product m % 3
+        constexpr int m = decltype(M_)::value, i = m / (3 * TN), j = (m / 3) % TN, pr = m % 3;
+        if constexpr (pr == 0)
+            lo[i][j] = p_mfma(f.a[i][1], f.b[j][0], lo[i][j]);
+        else if constexpr (pr == 1)
+            lo[i][j] = p_mfma(f.a[i][0], f.b[j][1], lo[i][j]);
+        else
+            hi[i][j] = p_mfma(f.a[i][0], f.b[j][0], hi[i][j]);
+    };
+    // half step: the 12 MFMAs on f, with the 8 reads of g (stage offset so, half KH) one behind each of the first 8
+    // (sched_group_barrier: MFMA, read, MFMA, read, ...)
+    auto half = [&](const Frag &f, Frag &g, uint32_t so, auto KH, auto READS) __attribute__((always_inline)) {
+        static_for<NM>([&](auto M_) __attribute__((always_inline)) {
+            mf(f, M_);
+            if constexpr (decltype(READS)::value && decltype(M_)::value < NR) rd(g, M_, so, KH);
+        });
+        if constexpr (decltype(READS)::value) {
+            static_for<NR>([&](auto) __attribute__((always_inline)) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            });
+            if constexpr (NM > NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto touch = [&](const Frag &f) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < TM; i++) asm volatile("" ::"v"(f.a[i][0]), "v"(f.a[i][1]));
+#pragma unroll
+        for (int j = 0; j < TN; j++) asm volatile("" ::"v"(f.b[j][0]), "v"(f.b[j][1]));
+    };
+
+    static_assert(NK >= 2, "two k steps at least");
+    issue(0, 0);
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    Frag f0, f1;
+    static_for<NR>([&](auto K_) __attribute__((always_inline)) { rd(f0, K_, 0, IC<0>{}); });
+    static_for<NK>([&](auto KT) __attribute__((always_inline)) {
+        constexpr int kt = decltype(KT)::value, st = kt % 3, sn = (kt + 1) % 3;
+        if constexpr (kt + 2 < NK) issue(kt + 2, (kt + 2) % 3);  // the stage read in step kt - 1
+        __builtin_amdgcn_sched_barrier(0);
+        half(f0, f1, (uint32_t)st * STG_B, IC<1>{}, IC<1>{});  // MFMAs of half 0, reads of half 1
+        if constexpr (kt + 1 < NK) {
+            touch(f1);  // the compiler's wait for f1 here, before the barrier
+            if constexpr (kt + 2 < NK)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // step kt + 1 published; every wave is past its reads of step kt - 1
+            __builtin_amdgcn_sched_barrier(0);
+            half(f1, f0, (uint32_t)sn * STG_B, IC<0>{}, IC<1>{});  // MFMAs of half 1, reads of the next half 0
+        } else {
+            half(f1, f0, 0u, IC<0>{}, IC<0>{});
+        }
+    });
+
+    const float inv = p_pow2(-eA), invB = p_pow2(-eB);
+    float *Ct = C + t * sC;
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+        const int col = n0 + wn * WTN + j * 32 + fr;
+        const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (row < M) {
+                    const float v = (hi[i][j][r] + lo[i][j][r] * P_LO_INV) * inv * invB;
+                    Ct[row * N + col] = EPI == 1 ? p_relu(v + bv) : v;
+                }
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int WGM, int WGN>
+hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
+                     int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
+    if (N % BN || K % 32 || K < 64) return hipErrorInvalidValue;
+    const int64_t tiles_m = (M + BM - 1) / BM;
+    const int tiles_n = N / BN;
+    if (tiles_m * tiles_n > INT32_MAX) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(64 * WGM * WGN);
+    const auto *a = static_cast<const p_u32x4 *>(A);
+    const auto *b = static_cast<const p_u32x4 *>(B);
+#define PQ_K(NK)                                                                                                   \
+    do {                                                                                                           \
+        if (bias)                                                                                                  \
+            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 1, NK>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K,   \
+                               sA / 4, sB / 4, bias, C, sC, tiles_n);                                              \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 0, NK>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K,   \
+                               sA / 4, sB / 4, nullptr, C, sC, tiles_n);                                           \
+    } while (0)
+    switch (K) {  // the k loop is unrolled: one instantiation per depth (fc1's forward K = 576, input gradient 512)
+        case 576: PQ_K(18); break;
+        case 512: PQ_K(16); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef PQ_K
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// A, B: plane images (4 B per value, strides in values); cfg 60: 128 x 256 tiles (2 x 4 waves), 61: 256 x 128 (4 x 2),
+// 62: 128 x 192 (4 x 2 waves of 32 x 96: N = 576)
+hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
+                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
+                              int64_t c_stride, int cfg, hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    if (a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
+    switch (cfg) {
+        case 60: return pq_launch<128, 256, 2, 4>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 61: return pq_launch<256, 128, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 62: return pq_launch<128, 192, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace merlin

@@ -39,11 +39,11 @@ def main():
     pdz = nat.h3_split(dz, amz).view(torch.float32)
     flop = 2 * 2 * U * 576 * 512
     runs = {"fwd ntp13": (lambda: nat.h3_gemm_nt(a3, am3, Hp, amW, bias=b, cfg=13), "fwd")}
-    for c in (40, 41, 42, 43, 44, 45, 46):
-        if 512 % {41: 192, 42: 256}.get(c, 128) == 0:
+    for c in (50, 51, 60, 61):
+        if 512 % {41: 192, 42: 256, 50: 256, 60: 256}.get(c, 128) == 0:
             runs[f"fwd planes{c}"] = ((lambda c=c: nat.h3_gemm_nt(pa3, am3, Hp, amW, bias=b, cfg=c)), "fwd")
     runs["dgrad ntp11"] = (lambda: nat.h3_gemm_nt(dz, amz, Htp, amWt, cfg=11), "dgrad")
-    for c in (41,):
+    for c in (52, 62):
         runs[f"dgrad planes{c}"] = ((lambda c=c: nat.h3_gemm_nt(pdz, amz, Htp, amWt, cfg=c)), "dgrad")
     runs["split a3"] = (lambda: nat.h3_split(a3, am3), None)
     runs["split dz"] = (lambda: nat.h3_split(dz, amz), None)
