@@ -359,6 +359,15 @@ int merlin_tower_window_conv3_reuse(const float *Q_dev, int64_t n_windows, const
                                     const int64_t *groups_dev, int64_t n, const float *b3_dev,
                                     int32_t towers, float *Y3_dev, uint64_t *relu_bits_dev, uint32_t *amax_dev,
                                     const int32_t *rep_row_dev, int32_t copy, void *stream);
+/* window_conv3_planes: window_conv3_reuse with copy = 0 (representatives only; the bits of the other rows are read
+ * through rep_row by merlin_segment_sum_mask_rows) writing Y3 as its h3 planes (Y3_planes [t][n*9][8][2][8] f16, the
+ * fp32 Y3's byte layout) for fc1's plane-operand GEMMs.  The plane scale of tower t comes from a bound on max Y3
+ * computed first from Q: bound[t] (written, float bits) = max over c of relu(b3[t][c] + sum over taps of
+ * max_w Q[t][w][tap][c]) >= every Y3 value; colmax_ws uint32[towers * 64 * 576] is scratch (per-block column maxima). */
+int merlin_tower_window_conv3_planes(const float *Q_dev, int64_t nw, const int32_t *wid_dev, const int64_t *groups_dev,
+                                     int64_t n, const float *b3_dev, int32_t towers, void *Y3_planes_dev,
+                                     uint64_t *relu_bits_dev, const int32_t *rep_row_dev, uint32_t *colmax_ws_dev,
+                                     uint32_t *bound_dev, void *stream);
 int merlin_segment_sum(const float *src_dev, int64_t src_rows, const int32_t *idx_dev,
                        const int32_t *key_dev, int64_t nnz, const int32_t *slot_dev, int32_t sub,
                        int64_t item_len, const int32_t *fix_dev, int64_t n_fix, int32_t towers,
@@ -457,6 +466,17 @@ int merlin_ppo_loss(const float *logits_dev, const float *value_dev, const float
                     const float *adv_dev, const float *ret_dev, double clip_eps, double vf_coef, double ent_coef,
                     float *dlogits_dev, float *dvalue_dev, float *dbias_actor_dev, float *dbias_critic_dev,
                     float *loss_dev, double *stats_dev, double *workspace_dev, void *stream);
+/* merlin_ppo_loss plus grad_absmax_dev uint32[9] (or NULL): atomicMax of max over the frames of |dlogits[u][j]|
+ * into [j] (j < act_dim) and of max |dvalue[u]| into [8], as float bits (the caller zeroes it) -- the bound
+ * merlin_tower_head_bwd_planes derives dz's plane scale from. */
+int merlin_ppo_loss_absmax(const float *logits_dev, const float *value_dev, const float *bias_actor_dev,
+                           const float *bias_critic_dev, int64_t n_frames, int32_t act_dim, const int32_t *offs_dev,
+                           const int32_t *order_dev, const int64_t *frame_of_dev, int64_t n_samples,
+                           const int64_t *sample_index_dev, const int64_t *actions_dev, const float *logp_old_dev,
+                           const float *adv_dev, const float *ret_dev, double clip_eps, double vf_coef,
+                           double ent_coef, float *dlogits_dev, float *dvalue_dev, float *dbias_actor_dev,
+                           float *dbias_critic_dev, float *loss_dev, double *stats_dev, double *workspace_dev,
+                           uint32_t *grad_absmax_dev, void *stream);
 
 /* Tower GEMM epilogues (csrc/merlin_head.hip): towers = 1 or 2, `rows` per tower; cols (hidden)
  * a multiple of 4 dividing 1024 (4 x a divisor of 256).  Column sums use a per-device library
@@ -484,6 +504,17 @@ int merlin_tower_head_bwd(const float *h_dev, const float *dlogits_dev, const fl
                           const float *w_actor_dev, const float *w_critic_dev, int64_t n, int32_t hidden,
                           int32_t act_dim, float *dz_dev, float *dbias_dev, float *dw_actor_dev,
                           float *dw_critic_dev, uint32_t *amax_dev, void *stream);
+/* head_bwd_planes: head_bwd with dz written as its h3 planes dz_planes [2][n][hidden/8][2][8] f16 (merlin_h3_split's
+ * layout, 4 B per value) instead of fp32, scaled by the power of two from a bound on max |dz| known before the pass:
+ * dz_bound_dev[t] (written, float bits) = max over k of sum_j grad_absmax[j] |w_actor[j][k]| (tower 0) /
+ * grad_absmax[8] |w_critic[k]| (tower 1), grad_absmax_dev from merlin_ppo_loss_absmax.  dz_bound_dev is then the
+ * operand scale of the planes for merlin_h3_gemm_nt_planes / merlin_h3_gemm_tn_gather_planes_a.  hidden a multiple
+ * of 8 dividing 1024. */
+int merlin_tower_head_bwd_planes(const float *h_dev, const float *dlogits_dev, const float *dvalue_dev,
+                                 const float *w_actor_dev, const float *w_critic_dev, int64_t n, int32_t hidden,
+                                 int32_t act_dim, void *dz_planes_dev, float *dbias_dev, float *dw_actor_dev,
+                                 float *dw_critic_dev, const uint32_t *grad_absmax_dev, uint32_t *dz_bound_dev,
+                                 void *stream);
 /* heads_fwd: the two heads (actor_critic.py:41-46, Linear(512, act_dim) / Linear(512, 1)) on h
  * float[2][n][hidden] = relu(fc1) of the actor / critic tower: logits float[n][act_dim] = h0 w_actor^T
  * (+ b_actor), value float[n] = h1 . w_critic (+ b_critic); biases may be NULL (not added).  hidden 512,
@@ -571,6 +602,33 @@ int merlin_h3_gemm_nt_heads(const float *A_dev, const uint32_t *amax_a_dev, cons
                             const int32_t *a_rows_dev, const float *head_w0_dev, int32_t n_actions,
                             const float *head_w1_dev, float *head_partials_dev, int32_t cfg, void *stream);
 int32_t merlin_h3_heads_parts(int32_t N, int32_t cfg);
+/* gemm_nt_planes: gemm_nt with A already in plane form too (A_planes [t][M][K/8][2][8] f16 scaled by amax_a_dev's
+ *          exponent, e.g. merlin_tower_head_bwd_planes' dz), both operands staged into LDS by DMA (csrc/merlin_h3p.hip):
+ *          cfg 60 128x256 / 61 256x128 / 62 128x192 tiles, K = 512 or 576, bias as gemm_nt.  Same products and
+ *          order as gemm_nt on the fp32 A with the same scale: the same bits.
+ * gemm_tn_gather_planes_a: gemm_tn_gather with A already in plane form (strides in values). */
+int merlin_h3_gemm_nt_planes(const void *A_planes_dev, const uint32_t *amax_a_dev, const void *B_dev,
+                             const uint32_t *amax_b_dev, int64_t M, int32_t N, int32_t K, int32_t towers,
+                             int64_t a_stride, int64_t b_stride, const float *bias_dev, float *C_dev, int64_t c_stride,
+                             int32_t cfg, void *stream);
+/* gemm_nt_heads_planes: gemm_nt_heads (cfg 10 / 12 / 13, gathered rows, bias + ReLU, C_dev required) with A's
+ *          gathered rows already h3 planes (merlin_tower_window_conv3_planes): staged as copies, no split; head_*
+ *          NULL: h only.  With the planes of the same values and scale: gemm_nt_heads' bits.
+ * gemm_tn_gather_planes: gemm_tn_gather with both operands as planes (dz from merlin_tower_head_bwd_planes, the
+ *          gathered B from merlin_tower_window_conv3_planes). */
+int merlin_h3_gemm_nt_heads_planes(const void *A_planes_dev, const uint32_t *amax_a_dev, const void *B_dev,
+                                   const uint32_t *amax_b_dev, int64_t M, int32_t N, int32_t K, int64_t a_stride,
+                                   int64_t b_stride, const float *bias_dev, float *C_dev, int64_t c_stride,
+                                   const int32_t *a_rows_dev, const float *head_w0_dev, int32_t n_actions,
+                                   const float *head_w1_dev, float *head_partials_dev, int32_t cfg, void *stream);
+int merlin_h3_gemm_tn_gather_planes(const void *A_planes_dev, const uint32_t *amax_a_dev, const void *B_planes_dev,
+                                    const uint32_t *amax_b_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
+                                    int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev,
+                                    float *out_dev, const int32_t *b_rows_dev, int32_t cfg, void *stream);
+int merlin_h3_gemm_tn_gather_planes_a(const void *A_planes_dev, const uint32_t *amax_a_dev, const float *B_dev,
+                                      const uint32_t *amax_b_dev, int64_t Kd, int32_t M, int32_t N, int32_t towers,
+                                      int64_t a_stride, int64_t b_stride, int32_t splits, float *slab_dev,
+                                      float *out_dev, const int32_t *b_rows_dev, int32_t cfg, void *stream);
 /* The acting tail (merlin_act_heads' log-softmax, argmax or draw, action / logp / value) from the partials of a
  * merlin_h3_gemm_nt_heads call with C_dev = NULL (the acting path: h itself is never written), biases added here. */
 int merlin_act_draw(const float *partials_dev, int32_t parts, int64_t n, const float *b_actor_dev,

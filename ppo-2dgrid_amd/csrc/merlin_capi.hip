@@ -759,6 +759,18 @@ int merlin_tower_window_conv3_reuse(const float *Q, int64_t nw, const int32_t *w
     return MERLIN_OK;
 }
 
+int merlin_tower_window_conv3_planes(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
+                                     const float *b3, int32_t towers, void *Y3_planes, uint64_t *relu_bits,
+                                     const int32_t *rep_row, uint32_t *colmax_ws, uint32_t *bound, void *stream) {
+    if ((!rep_row || !Y3_planes || !Q || !wid || !b3 || !relu_bits || !colmax_ws || !bound) && n > 0)
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (n > 0 && nw <= 0) return fail(MERLIN_E_INVALID, "no windows");
+    HIP_TRY(merlin::launch_window_conv3(Q, nw, wid, groups, n, b3, towers, static_cast<float *>(Y3_planes), relu_bits,
+                                        nullptr, rep_row, 0, (hipStream_t)stream, colmax_ws, bound));
+    return MERLIN_OK;
+}
+
 int64_t merlin_tower_all_windows(void) { return 458752; }  // 4^9 + 3 * 4^8 (merlin_window.hip k_codes_conv3)
 
 int merlin_tower_codes_conv3_amax(const uint32_t *codes, int64_t n, const float *Qall, const float *b3,
@@ -864,6 +876,18 @@ int merlin_ppo_loss(const float *logits, const float *value, const float *bias_a
                     const float *logp_old, const float *adv, const float *ret, double clip_eps, double vf_coef,
                     double ent_coef, float *dlogits, float *dvalue, float *dbias_actor, float *dbias_critic,
                     float *loss, double *stats, double *workspace, void *stream) {
+    return merlin_ppo_loss_absmax(logits, value, bias_actor, bias_critic, n_frames, act_dim, offs, order, frame_of,
+                                  n_samples, sample_index, actions, logp_old, adv, ret, clip_eps, vf_coef, ent_coef,
+                                  dlogits, dvalue, dbias_actor, dbias_critic, loss, stats, workspace, nullptr, stream);
+}
+
+int merlin_ppo_loss_absmax(const float *logits, const float *value, const float *bias_actor, const float *bias_critic,
+                           int64_t n_frames, int32_t act_dim, const int32_t *offs, const int32_t *order,
+                           const int64_t *frame_of, int64_t n_samples, const int64_t *sample_index,
+                           const int64_t *actions, const float *logp_old, const float *adv, const float *ret,
+                           double clip_eps, double vf_coef, double ent_coef, float *dlogits, float *dvalue,
+                           float *dbias_actor, float *dbias_critic, float *loss, double *stats, double *workspace,
+                           uint32_t *grad_absmax, void *stream) {
     if (n_frames < 0 || n_samples < 0) return fail(MERLIN_E_INVALID, "negative size");
     if (n_frames > n_samples) return fail(MERLIN_E_INVALID, "every frame needs at least one sample");
     if (act_dim < 1 || act_dim > 8) return fail(MERLIN_E_INVALID, "act_dim must be in [1, 8]");
@@ -876,7 +900,7 @@ int merlin_ppo_loss(const float *logits, const float *value, const float *bias_a
     HIP_TRY(merlin::launch_ppo_loss(logits, value, bias_actor, bias_critic, n_frames, act_dim, offs, order, frame_of,
                                     n_samples, sample_index, actions, logp_old, adv, ret, clip_eps, vf_coef, ent_coef,
                                     dlogits, dvalue, dbias_actor, dbias_critic, loss, stats, workspace,
-                                    (hipStream_t)stream));
+                                    (hipStream_t)stream, grad_absmax));
     return MERLIN_OK;
 }
 
@@ -926,6 +950,24 @@ int merlin_tower_head_bwd(const float *h, const float *dlogits, const float *dva
     if (rc) return rc;
     HIP_TRY(merlin::launch_head_bwd(h, dlogits, dvalue, w_actor, w_critic, n, hidden, act_dim, dz, dbias, dw_actor,
                                     dw_critic, ws->epi_work, amax, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_head_bwd_planes(const float *h, const float *dlogits, const float *dvalue, const float *w_actor,
+                                 const float *w_critic, int64_t n, int32_t hidden, int32_t act_dim, void *dz_planes,
+                                 float *dbias, float *dw_actor, float *dw_critic, const uint32_t *grad_absmax,
+                                 uint32_t *dz_bound, void *stream) {
+    if (!dbias || !dw_actor || !dw_critic || !grad_absmax || !dz_bound ||
+        ((!h || !dlogits || !dvalue || !w_actor || !w_critic || !dz_planes) && n > 0))
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (act_dim < 1 || act_dim > 8) return fail(MERLIN_E_UNSUPPORTED, "act_dim must be 1..8");
+    if (!merlin::epilogue_cols_ok(hidden) || hidden % 8) return fail(MERLIN_E_UNSUPPORTED, "hidden must be 8 x a divisor of 128");
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc) return rc;
+    HIP_TRY(merlin::launch_head_bwd(h, dlogits, dvalue, w_actor, w_critic, n, hidden, act_dim, nullptr, dbias,
+                                    dw_actor, dw_critic, ws->epi_work, dz_bound, (hipStream_t)stream, grad_absmax,
+                                    dz_planes));
     return MERLIN_OK;
 }
 
@@ -1027,7 +1069,7 @@ static int h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, con
                       int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride, const float *bias,
                       float *C, int64_t c_stride, void *a_planes, const int32_t *a_rows, int32_t cfg, void *stream,
                       const float *head_w0 = nullptr, int32_t n_actions = 0, const float *head_w1 = nullptr,
-                      float *head_part = nullptr) {
+                      float *head_part = nullptr, bool a_is_planes = false) {
     if (M < 0 || N <= 0 || K <= 0) return fail(MERLIN_E_INVALID, "bad shape");
     if (M > 0 && (!A || !B || (!C && !head_part) || !amax_a || !amax_b)) return fail(MERLIN_E_INVALID, "null argument");
     if (K % 32) return fail(MERLIN_E_UNSUPPORTED, "K must be a multiple of 32");
@@ -1035,7 +1077,7 @@ static int h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, con
     if (a_stride % 4 || b_stride % 8) return fail(MERLIN_E_INVALID, "tower strides: A multiple of 4, B of 8");
     const hipError_t e = merlin::launch_h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, bias, C,
                                                    c_stride, a_planes, cfg, (hipStream_t)stream, a_rows, head_w0,
-                                                   n_actions, head_w1, head_part);
+                                                   n_actions, head_w1, head_part, a_is_planes);
     if (e == hipErrorInvalidValue)
         return fail(MERLIN_E_UNSUPPORTED, "N not a multiple of the tile width / bad cfg / unsupported gather");
     HIP_TRY(e);
@@ -1047,6 +1089,14 @@ int merlin_h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, con
                       float *C, int64_t c_stride, void *a_planes, int32_t cfg, void *stream) {
     return h3_gemm_nt(A, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, bias, C, c_stride, a_planes, nullptr,
                       cfg, stream);
+}
+
+int merlin_h3_gemm_nt_planes(const void *A_planes, const uint32_t *amax_a, const void *B, const uint32_t *amax_b,
+                             int64_t M, int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride,
+                             const float *bias, float *C, int64_t c_stride, int32_t cfg, void *stream) {
+    if (cfg < 60 || cfg >= 70) return fail(MERLIN_E_UNSUPPORTED, "plane-operand cfgs are 60..69");
+    return h3_gemm_nt(static_cast<const float *>(A_planes), amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride,
+                      bias, C, c_stride, nullptr, nullptr, cfg, stream);
 }
 
 int merlin_h3_gemm_nt_gather(const float *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t M,
@@ -1061,14 +1111,16 @@ int merlin_h3_gemm_nt_gather(const float *A, const uint32_t *amax_a, const void 
 
 static int h3_gemm_tn(const void *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t Kd,
                       int32_t M, int32_t N, int32_t towers, int64_t a_stride, int64_t b_stride, int32_t splits,
-                      float *slab, float *out, bool planes, int32_t cfg, void *stream, const int32_t *b_rows = nullptr) {
+                      float *slab, float *out, bool planes, int32_t cfg, void *stream, const int32_t *b_rows = nullptr,
+                      bool a_planes = false, bool b_planes = false) {
     if (Kd < 0 || M <= 0 || N <= 0) return fail(MERLIN_E_INVALID, "bad shape");
     if (!out || (Kd > 0 && (!A || !B || !slab || !amax_a || !amax_b))) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (splits < 1 || splits > merlin::x6_tn_max_splits()) return fail(MERLIN_E_INVALID, "splits out of range");
     if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return fail(MERLIN_E_INVALID, "M, N: multiples of 8");
     const hipError_t e = merlin::launch_h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits,
-                                                   slab, out, planes, cfg, (hipStream_t)stream, b_rows);
+                                                   slab, out, planes, cfg, (hipStream_t)stream, b_rows, a_planes,
+                                                   b_planes);
     if (e == hipErrorInvalidValue) return fail(MERLIN_E_UNSUPPORTED, "M / N not multiples of the tile / bad cfg");
     HIP_TRY(e);
     return MERLIN_OK;
@@ -1121,6 +1173,41 @@ int merlin_h3_gemm_tn_gather(const float *A, const uint32_t *amax_a, const float
     if (N % 64) return fail(MERLIN_E_UNSUPPORTED, "gathered rows: N must be a multiple of 64");
     return h3_gemm_tn(A, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, false, cfg, stream,
                       b_rows);
+}
+
+int merlin_h3_gemm_nt_heads_planes(const void *A_planes, const uint32_t *amax_a, const void *B,
+                                   const uint32_t *amax_b, int64_t M, int32_t N, int32_t K, int64_t a_stride,
+                                   int64_t b_stride, const float *bias, float *C, int64_t c_stride,
+                                   const int32_t *a_rows, const float *head_w0, int32_t n_actions,
+                                   const float *head_w1, float *head_partials, int32_t cfg, void *stream) {
+    if (M > 0 && (!bias || !C || !a_rows || (head_partials && (!head_w0 || !head_w1))))
+        return fail(MERLIN_E_INVALID, "null argument");
+    if (head_partials && (n_actions < 1 || n_actions > 4))
+        return fail(MERLIN_E_UNSUPPORTED, "heads epilogue: 1..4 actions");
+    if (merlin::h3_heads_parts(N, cfg) == 0) return fail(MERLIN_E_UNSUPPORTED, "planes forward: cfg 10, 12 or 13");
+    if (K % 64) return fail(MERLIN_E_UNSUPPORTED, "gathered rows: K must be a multiple of 64");
+    return h3_gemm_nt(static_cast<const float *>(A_planes), amax_a, B, amax_b, M, N, K, 2, a_stride, b_stride, bias,
+                      C, c_stride, nullptr, a_rows, cfg, stream, head_w0, n_actions, head_w1, head_partials, true);
+}
+
+int merlin_h3_gemm_tn_gather_planes(const void *A_planes, const uint32_t *amax_a, const void *B_planes,
+                                    const uint32_t *amax_b, int64_t Kd, int32_t M, int32_t N, int32_t towers,
+                                    int64_t a_stride, int64_t b_stride, int32_t splits, float *slab, float *out,
+                                    const int32_t *b_rows, int32_t cfg, void *stream) {
+    if (Kd > 0 && !b_rows) return fail(MERLIN_E_INVALID, "null argument");
+    if (N % 64) return fail(MERLIN_E_UNSUPPORTED, "gathered rows: N must be a multiple of 64");
+    return h3_gemm_tn(A_planes, amax_a, B_planes, amax_b, Kd, M, N, towers, a_stride, b_stride, splits, slab, out,
+                      false, cfg, stream, b_rows, true, true);
+}
+
+int merlin_h3_gemm_tn_gather_planes_a(const void *A_planes, const uint32_t *amax_a, const float *B,
+                                      const uint32_t *amax_b, int64_t Kd, int32_t M, int32_t N, int32_t towers,
+                                      int64_t a_stride, int64_t b_stride, int32_t splits, float *slab, float *out,
+                                      const int32_t *b_rows, int32_t cfg, void *stream) {
+    if (Kd > 0 && !b_rows) return fail(MERLIN_E_INVALID, "null argument");
+    if (N % 64) return fail(MERLIN_E_UNSUPPORTED, "gathered rows: N must be a multiple of 64");
+    return h3_gemm_tn(A_planes, amax_a, B, amax_b, Kd, M, N, towers, a_stride, b_stride, splits, slab, out, false, cfg,
+                      stream, b_rows, true);
 }
 
 int merlin_h3_gemm_tn_planes(const void *A, const uint32_t *amax_a, const void *B, const uint32_t *amax_b, int64_t Kd,

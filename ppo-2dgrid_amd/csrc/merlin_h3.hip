@@ -52,33 +52,12 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
-// the scale exponent e of a tensor whose max |x| has float bits `amax`: max |x| 2^e in [2^14, 2^15)
-__device__ __forceinline__ int h3_exp(uint32_t amax) {
-    if (amax == 0u) return 0;
-    const int e = (int)((amax >> 23) & 0xffu) - 127;  // floor(log2) for a normal max (inf / nan: e = 128)
-    return std::min(std::max(14 - e, -120), 115);  // e + 11 stays a normal power of two
-}
-__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+// h3_exp / pow2f / h3_pair: merlin_internal.h (shared with the producers that write planes)
 
 // an operand scale written by another kernel's atomics: read with a vector load at agent scope (L2-coherent), not
 // through the scalar data cache a wave-uniform load would take
 __device__ __forceinline__ uint32_t load_amax(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// planes of two unscaled values a, b (sc = 2^e, sc2 = 2^(e + 11)): hi word (h of a, h of b) = f16(x'), lo word =
-// f16(2^11 x' - 2^11 h), each by one v_fma_mix{lo,hi}_f16 (the mixed fma rounds its exact result once to f16; in
-// the lo ones h is read as an f16 operand from its half of the hi word, so x' - h is never formed in f32): six
-// vector instructions per pair (the compiler's version of the same expressions took nine, computing h twice)
-__device__ __forceinline__ void h3_pair(float a, float b, float sc, float sc2, uint32_t &hi, uint32_t &lo) {
-    const float m2048 = -LO_SCALE, za = a * sc2, zb = b * sc2;
-    uint32_t h, l;
-    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(a), "v"(sc));
-    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(b), "v"(sc));
-    asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(h), "v"(m2048), "v"(za));
-    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(h), "v"(m2048), "v"(zb));
-    hi = h;
-    lo = l;
 }
 
 // 8 consecutive values (two float4) scaled by sc (sc2 = 2^11 sc) -> hi chunk p0, lo chunk p1
@@ -314,7 +293,9 @@ struct HeadsArg {
     int na;
     float *part;
 };
-template <int BM, int BN, int WGM, int WGN, int EPI, bool GA>
+// AP (round 5): A arrives as h3 plane images (the same 4 B per value and addressing; conv3's representatives written
+// as planes, merlin_tower_window_conv3_planes): staged as copies, no split
+template <int BM, int BN, int WGM, int WGN, int EPI, bool GA, bool AP = false>
 __device__ __forceinline__ void h3_ntp_body(const float *__restrict__ A, const u32x4 *__restrict__ B,
                                             const uint32_t *__restrict__ amaxA, const uint32_t *__restrict__ amaxB,
                                             int64_t M, int N, int K, int64_t sA, int64_t sB,
@@ -399,7 +380,12 @@ __device__ __forceinline__ void h3_ntp_body(const float *__restrict__ A, const u
 #pragma unroll
         for (int i = 0; i < UA; i++) {
             u32x4 p0, p1;
-            h3_split8(ra[i][0], ra[i][1], scA, scA2, p0, p1);
+            if constexpr (AP) {
+                p0 = __builtin_bit_cast(u32x4, ra[i][0]);
+                p1 = __builtin_bit_cast(u32x4, ra[i][1]);
+            } else {
+                h3_split8(ra[i][0], ra[i][1], scA, scA2, p0, p1);
+            }
             st[la[i]] = p0;
             st[PSA + la[i]] = p1;
             if (pa[i]) {
@@ -563,7 +549,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntp(const float *__restri
     h3_ntp_body<BM, BN, WGM, WGN, EPI, false>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, Pout, nullptr,
                                               hd);
 }
-template <int BM, int BN, int WGM, int WGN, int EPI>
+template <int BM, int BN, int WGM, int WGN, int EPI, bool AP = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntpg(const float *__restrict__ A, const u32x4 *__restrict__ B,
                                                             const uint32_t *__restrict__ amaxA,
                                                             const uint32_t *__restrict__ amaxB, int64_t M, int N,
@@ -571,8 +557,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_ntpg(const float *__restr
                                                             const float *__restrict__ bias, float *__restrict__ C,
                                                             int64_t sC, int tiles_n, const int32_t *__restrict__ amap,
                                                             HeadsArg hd) {
-    h3_ntp_body<BM, BN, WGM, WGN, EPI, true>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, nullptr, amap,
-                                             hd);
+    h3_ntp_body<BM, BN, WGM, WGN, EPI, true, AP>(A, B, amaxA, amaxB, M, N, K, sA, sB, bias, C, sC, tiles_n, nullptr,
+                                                 amap, hd);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -873,7 +859,10 @@ __device__ __forceinline__ u32x4 tr_frag(const u32x4 *img, int col0, int kh, int
 // GB: B's rows gathered by 64-column chunks -- row k's chunk j is row bmap[k * N / 64 + j] of B seen as [*][64] (the
 // minibatch's conv3 rows through their patch representatives, as k_h3_ntp's GA).  A unit's chunk is fixed, its row
 // changes every k step: each load issues the next step's chunk-row reads behind its data reads (ready by then).
-template <int BM, int BN, int WGM, int WGN, bool GB>
+// AQ: A arrives as plane images ([Kd][M/8][2][8] f16, 4 B per value like fp32, so the addressing is the same): its
+// staging copies the hi / lo chunks instead of splitting (k_head_bwd's dz planes, merlin_tower_head_bwd_planes)
+// BQ: B (gathered) arrives as plane images too (conv3's representatives as planes)
+template <int BM, int BN, int WGM, int WGN, bool GB, bool AQ = false, bool BQ = false>
 __device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const float4 *__restrict__ B,
                                            const uint32_t *__restrict__ amaxA, const uint32_t *__restrict__ amaxB,
                                            int64_t Kd, int M, int N, int64_t sA, int64_t sB, int64_t kc, int tiles_n,
@@ -1011,7 +1000,12 @@ __device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const f
             if (QA % NT == 0 || i + 1 < UA || tid + i * NT < QA) {
                 const bool in = kk + ka[i] < k1;
                 u32x4 p0, p1;
-                h3_split8(in ? ra[i][0] : zero, in ? ra[i][1] : zero, scA, scA2, p0, p1);
+                if constexpr (AQ) {
+                    p0 = __builtin_bit_cast(u32x4, in ? ra[i][0] : zero);
+                    p1 = __builtin_bit_cast(u32x4, in ? ra[i][1] : zero);
+                } else {
+                    h3_split8(in ? ra[i][0] : zero, in ? ra[i][1] : zero, scA, scA2, p0, p1);
+                }
                 st[la[i]] = p0;
                 st[PSA + la[i]] = p1;
             }
@@ -1020,7 +1014,12 @@ __device__ __forceinline__ void h3_tn_body(const float4 *__restrict__ A, const f
             if (PAIR ? UB * tid + i < QB : (QB % NT == 0 || i + 1 < UB || tid + i * NT < QB)) {
                 const bool in = kk + kb[i] < k1;
                 u32x4 p0, p1;
-                h3_split8(in ? rb[i][0] : zero, in ? rb[i][1] : zero, scB, scB2, p0, p1);
+                if constexpr (BQ) {
+                    p0 = __builtin_bit_cast(u32x4, in ? rb[i][0] : zero);
+                    p1 = __builtin_bit_cast(u32x4, in ? rb[i][1] : zero);
+                } else {
+                    h3_split8(in ? rb[i][0] : zero, in ? rb[i][1] : zero, scB, scB2, p0, p1);
+                }
                 st[lb[i]] = p0;
                 st[PSB + lb[i]] = p1;
             }
@@ -1100,14 +1099,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tn(const float4 *__restri
                                                           int S, float *__restrict__ slab) {
     h3_tn_body<BM, BN, WGM, WGN, false>(A, B, amaxA, amaxB, Kd, M, N, sA, sB, kc, tiles_n, tiles, S, slab, nullptr);
 }
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, bool AQ = false, bool BQ = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tng(const float4 *__restrict__ A, const float4 *__restrict__ B,
                                                            const uint32_t *__restrict__ amaxA,
                                                            const uint32_t *__restrict__ amaxB, int64_t Kd, int M,
                                                            int N, int64_t sA, int64_t sB, int64_t kc, int tiles_n,
                                                            int tiles, int S, float *__restrict__ slab,
                                                            const int32_t *__restrict__ bmap) {
-    h3_tn_body<BM, BN, WGM, WGN, true>(A, B, amaxA, amaxB, Kd, M, N, sA, sB, kc, tiles_n, tiles, S, slab, bmap);
+    h3_tn_body<BM, BN, WGM, WGN, true, AQ, BQ>(A, B, amaxA, amaxB, Kd, M, N, sA, sB, kc, tiles_n, tiles, S, slab,
+                                               bmap);
 }
 
 // The TN product with the k step's split and staging interleaved into its MFMAs, as k_h3_ntp does for NT: the
@@ -1447,8 +1447,26 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tnq(const u32x4 *__restri
 template <int BM, int BN, int WGM, int WGN, bool PIPE>
 hipError_t nt_launch(const float *A, const u32x4 *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, u32x4 *Pout,
-                     const int32_t *amap, const HeadsArg &hd, hipStream_t s) {
+                     const int32_t *amap, const HeadsArg &hd, hipStream_t s, bool ap = false) {
     if (N % BN || (PIPE && K < 2 * BK)) return hipErrorInvalidValue;
+    if (ap) {  // A as planes: the gathered pipelined kernel (the update's forward), with or without the heads
+        if constexpr (!PIPE || BN / WGN != 64) {
+            return hipErrorInvalidValue;
+        } else {
+            if (!amap || !C || !bias || Pout || K % 64 || K > 64 * GA_CHUNKS) return hipErrorInvalidValue;
+            const int64_t tiles_m = (M + BM - 1) / BM;
+            const dim3 grid((unsigned)(tiles_m * (N / BN)), T), block(64 * WGM * WGN);
+            if (hd.part) {
+                if (T != 2 || hd.na < 1 || hd.na > 4 || !hd.w0 || !hd.w1) return hipErrorInvalidValue;
+                hipLaunchKernelGGL((k_h3_ntpg<BM, BN, WGM, WGN, 2, true>), grid, block, 0, s, A, B, amaxA, amaxB, M, N,
+                                   K, sA, sB, bias, C, sC, N / BN, amap, hd);
+            } else {
+                hipLaunchKernelGGL((k_h3_ntpg<BM, BN, WGM, WGN, 1, true>), grid, block, 0, s, A, B, amaxA, amaxB, M, N,
+                                   K, sA, sB, bias, C, sC, N / BN, amap, hd);
+            }
+            return hipGetLastError();
+        }
+    }
     if ((int64_t)N * (K / 8) * 2 > INT32_MAX) return hipErrorInvalidValue;  // 32-bit B chunk offsets
     const int64_t tiles_m = (M + BM - 1) / BM;
     const int tiles_n = N / BN;
@@ -1526,7 +1544,8 @@ hipError_t tn_launch(const void *A, const void *B, const uint32_t *amaxA, const 
                      int N, int T, int64_t sA, int64_t sB, int splits, float *slab, int *S_out, const int32_t *bmap,
                      hipStream_t s) {
     if (M % BM || N % BN) return hipErrorInvalidValue;
-    if (bmap && (Q != 0 || N % 64)) return hipErrorInvalidValue;  // gathered B rows: k_h3_tn only
+    if (bmap && ((Q != 0 && Q != 3 && Q != 4) || N % 64)) return hipErrorInvalidValue;  // gathered B: k_h3_tng only
+    if (Q >= 3 && !bmap) return hipErrorInvalidValue;
     const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
     int S = std::max(1, splits);
     int64_t kc = (Kd + S - 1) / S;
@@ -1541,6 +1560,14 @@ hipError_t tn_launch(const void *A, const void *B, const uint32_t *amaxA, const 
         hipLaunchKernelGGL((k_h3_tnp<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
                            static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
                            sA / 4, sB / 4, kc, tiles_n, tiles, S, slab);
+    else if (Q == 4)  // both as planes, B gathered
+        hipLaunchKernelGGL((k_h3_tng<BM, BN, WGM, WGN, true, true>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
+                           static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
+                           sA / 4, sB / 4, kc, tiles_n, tiles, S, slab, bmap);
+    else if (Q == 3)  // A as planes (AQ), B fp32 gathered
+        hipLaunchKernelGGL((k_h3_tng<BM, BN, WGM, WGN, true>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
+                           static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
+                           sA / 4, sB / 4, kc, tiles_n, tiles, S, slab, bmap);
     else if (bmap)
         hipLaunchKernelGGL((k_h3_tng<BM, BN, WGM, WGN>), dim3(tiles * S * T), dim3(64 * WGM * WGN), 0, s,
                            static_cast<const float4 *>(A), static_cast<const float4 *>(B), amaxA, amaxB, Kd, M, N,
@@ -1586,7 +1613,8 @@ hipError_t launch_h3_split(const float *x, int64_t n, int T, const uint32_t *ama
 hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
                              int64_t c_stride, void *a_planes, int cfg, hipStream_t s, const int32_t *a_rows,
-                             const float *head_w0, int n_actions, const float *head_w1, float *head_part) {
+                             const float *head_w0, int n_actions, const float *head_w1, float *head_part,
+                             bool a_is_planes) {
     const HeadsArg hd{head_w0, head_w1, n_actions, head_part};
     if (M <= 0) return hipSuccess;
     if (K % BK || N <= 0 || a_stride % 4 || b_stride % 8) return hipErrorInvalidValue;
@@ -1594,7 +1622,9 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
     u32x4 *P = static_cast<u32x4 *>(a_planes);
     const int64_t sB = b_stride / 8 * 2;  // chunks
 #define H3_NT(BM, BN, WM, WN, PIPE) \
-    nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, hd, s)
+    nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, hd, s, \
+                                    a_is_planes)
+    if (a_is_planes && (cfg < 10 || cfg > 13)) return hipErrorInvalidValue;
     if (cfg >= 60 && cfg < 70) {  // both operands as plane images (merlin_h3p.hip)
         if (a_rows || head_part || P) return hipErrorInvalidValue;
         return launch_h3p_gemm_nt(A, amaxA, B, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, cfg, s);
@@ -1659,7 +1689,9 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
 
 hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t Kd,
                              int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits, float *slab,
-                             float *out, bool planes, int cfg, hipStream_t s, const int32_t *b_rows) {
+                             float *out, bool planes, int cfg, hipStream_t s, const int32_t *b_rows, bool a_planes,
+                             bool b_planes) {
+    if (b_planes && !a_planes) return hipErrorInvalidValue;
     if (M <= 0 || N <= 0) return hipSuccess;
     if (M % 8 || N % 8 || a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
     const int64_t total = (int64_t)T * M * N;
@@ -1673,6 +1705,10 @@ hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B
 #define H3_TN(BM, BN, WM, WN, PIPE)                                                                              \
     (planes ? tn_launch<BM, BN, WM, WN, 1>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S,   \
                                            b_rows, s)                                                              \
+     : a_planes ? (b_planes ? tn_launch<BM, BN, WM, WN, 4>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride,    \
+                                                           splits, slab, &S, b_rows, s)                            \
+                           : tn_launch<BM, BN, WM, WN, 3>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride,    \
+                                                          splits, slab, &S, b_rows, s))                            \
             : tn_launch<BM, BN, WM, WN, PIPE>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S, \
                                               b_rows, s))
     switch (cfg) {

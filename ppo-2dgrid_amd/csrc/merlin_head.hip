@@ -139,12 +139,22 @@ __global__ __launch_bounds__(FOLD_COLS * FOLD_SLICES) void k_fold_cols(const flo
 //   db4[t] += dz[t][k]
 // partials[t][b][(1 + A) * H4] (float4): tower 0 = (db4_0, dWa rows 0..A-1), tower 1 = (db4_1, dwc).
 // NA: the register arrays' size (A <= NA; the bench's A = 3 instance keeps 4 waves per SIMD resident)
-template <int NA>
+//
+// PL (dz as h3 planes, merlin_h3.hip's operand form, for fc1's input- and weight-gradient GEMMs): dz is not written
+// as fp32 but as its planes dzp [2][n][H/8][2][8] f16, scaled by 2^e from a BOUND on max |dz| instead of its max --
+// |dz[r][k]| <= sum_j max_r' |dlogits[r'][j]| |Wa[j][k]| (tower 0; tower 1: max |dvalue| |wc[k]|), the maxima from
+// the loss (k_ppo_loss_fix's dmax, float bits: [0, A) the logits, [DMAX_VALUE] the value) -- so the scale is known
+// before any dz value is, and the split costs no pass of its own.  Every block computes the same bound (the same
+// operations in the same order); block 0 of tower t stores it to amax[t] (bits), from which the GEMMs derive the same
+// e.  A bound above the max only shifts where the planes' 2^26 dynamic range starts (below 2^-26 of the bound).
+constexpr int DMAX_VALUE = 8;
+template <int NA, bool PL>
 __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h, const float *__restrict__ dlogits,
                                                    const float *__restrict__ dvalue, const float4 *__restrict__ wa,
                                                    const float4 *__restrict__ wc, int64_t n, int H4, int A,
                                                    int64_t per, float4 *__restrict__ dz,
-                                                   float4 *__restrict__ partials, uint32_t *__restrict__ amax) {
+                                                   float4 *__restrict__ partials, uint32_t *__restrict__ amax,
+                                                   const uint32_t *__restrict__ dmax, uint2 *__restrict__ dzp) {
     __shared__ float4 red[EBLK];
     const int t = blockIdx.y, R = EBLK / H4;
     const int c = threadIdx.x % H4, r0 = threadIdx.x / H4;
@@ -154,6 +164,33 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
     for (int j = 0; j < NA; j++) {
         w[j] = j < nw ? (t == 0 ? wa[j * H4 + c] : wc[c]) : f4_zero();
         accw[j] = f4_zero();
+    }
+    float sc = 1.0f, sc2 = H3_LO_SCALE;
+    if constexpr (PL) {
+        float4 b = f4_zero();
+#pragma unroll
+        for (int j = 0; j < NA; j++) {
+            if (j < nw) {
+                const float D = __uint_as_float(__hip_atomic_load(dmax + (t == 0 ? j : DMAX_VALUE), __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT));
+                b.x += D * fabsf(w[j].x);
+                b.y += D * fabsf(w[j].y);
+                b.z += D * fabsf(w[j].z);
+                b.w += D * fabsf(w[j].w);
+            }
+        }
+        uint32_t m = max(max(__float_as_uint(b.x), __float_as_uint(b.y)), max(__float_as_uint(b.z), __float_as_uint(b.w)));
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+        __shared__ uint32_t bred[EBLK / 64];
+        if ((threadIdx.x & 63) == 0) bred[threadIdx.x >> 6] = m;
+        __syncthreads();
+        m = bred[0];
+#pragma unroll
+        for (int q = 1; q < EBLK / 64; q++) m = max(m, bred[q]);
+        if (blockIdx.x == 0 && threadIdx.x == 0) amax[t] = m;
+        const int e = h3_exp(m);
+        sc = pow2f(e);
+        sc2 = pow2f(e + 11);
     }
     float4 acc = f4_zero();
     uint32_t mz = 0u;  // max |dz| of the block as float bits (merlin_h3.hip's operand scale)
@@ -192,13 +229,16 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
                 }
             }
             const float4 o = f4_mask(hv[k], g);
-            dz[base + (size_t)(r + k * R) * H4 + c] = o;
+            if constexpr (PL)
+                h3_store4_pair(reinterpret_cast<uint4 *>(dzp) + base + (size_t)(r + k * R) * H4, c, o, sc, sc2);
+            else
+                dz[base + (size_t)(r + k * R) * H4 + c] = o;
             f4_add(acc, o);
-            mz = std::max(mz, std::max(std::max(__float_as_uint(o.x) & 0x7fffffffu, __float_as_uint(o.y) & 0x7fffffffu),
+            if constexpr (!PL) mz = std::max(mz, std::max(std::max(__float_as_uint(o.x) & 0x7fffffffu, __float_as_uint(o.y) & 0x7fffffffu),
                                        std::max(__float_as_uint(o.z) & 0x7fffffffu, __float_as_uint(o.w) & 0x7fffffffu)));
         }
     }
-    if (amax) {  // block-uniform
+    if (!PL && amax) {  // block-uniform
         const uint32_t mx[2] = {t == 0 ? mz : 0u, t == 1 ? mz : 0u};
         block_amax2(mx, 2, amax);
     }
@@ -355,7 +395,8 @@ hipError_t launch_colsum(const float *X, int64_t rows, int cols, int64_t row_str
 
 hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
                            const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
-                           float *work, uint32_t *amax, hipStream_t s) {
+                           float *work, uint32_t *amax, hipStream_t s, const uint32_t *dmax, void *dz_planes) {
+    if (dz_planes && (!dmax || !amax || A > DMAX_VALUE)) return hipErrorInvalidValue;
     if (n <= 0) {
         hipError_t e = zero_async(db4, sizeof(float) * 2 * H, s);
         if (e == hipSuccess) e = zero_async(dwa, sizeof(float) * A * H, s);
@@ -363,10 +404,12 @@ hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dv
     }
     const int nblk = blocks_for(n);
     const int64_t per = (n + nblk - 1) / nblk;
-    hipLaunchKernelGGL(A <= 3 ? k_head_bwd<3> : k_head_bwd<MAXA>, dim3(nblk, 2), dim3(EBLK), 0, s,
+    const auto kern = dz_planes ? (A <= 3 ? k_head_bwd<3, true> : k_head_bwd<MAXA, true>)
+                                : (A <= 3 ? k_head_bwd<3, false> : k_head_bwd<MAXA, false>);
+    hipLaunchKernelGGL(kern, dim3(nblk, 2), dim3(EBLK), 0, s,
                        reinterpret_cast<const float4 *>(h), dlogits, dvalue, reinterpret_cast<const float4 *>(wa),
                        reinterpret_cast<const float4 *>(wc), n, H / 4, A, per, reinterpret_cast<float4 *>(dz),
-                       reinterpret_cast<float4 *>(work), amax);
+                       reinterpret_cast<float4 *>(work), amax, dmax, static_cast<uint2 *>(dz_planes));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int total = (1 + A) * H + 2 * H;

@@ -235,7 +235,8 @@ hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, 
                              const float *b2 = nullptr);
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
                                const float *b3, int T, float *Y3, uint64_t *bits, uint32_t *amax,
-                               const int32_t *rrow, int copy, hipStream_t s);
+                               const int32_t *rrow, int copy, hipStream_t s, uint32_t *colmax = nullptr,
+                               uint32_t *bound = nullptr);
 hipError_t launch_act_heads(const float *z, const float *b4, int64_t n, int H, const float *wa, const float *ba,
                             const float *wc, const float *bc, int A, int det, uint64_t seed, const int64_t *epoch,
                             int64_t step, int64_t env_offset, int64_t *action, float *logp, float *value,
@@ -250,7 +251,7 @@ hipError_t launch_ppo_loss(const float *logits, const float *value, const float 
                            const int64_t *sample_index, const int64_t *actions, const float *lp_old, const float *adv,
                            const float *ret, double clip_eps, double vf_coef, double ent_coef, float *dlogits,
                            float *dvalue, float *dbias_a, float *dbias_c, float *loss, double *stats,
-                           double *workspace, hipStream_t s);
+                           double *workspace, hipStream_t s, uint32_t *dmax = nullptr);
 hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, const float *b3, int T, float *Y3,
                               uint32_t *amax, hipStream_t s);
 hipError_t launch_x6_gemm_nt32(const float *A, const void *B, int64_t M, int N, int K, int T, int64_t a_stride,
@@ -283,7 +284,8 @@ hipError_t launch_colsum(const float *X, int64_t rows, int cols, int64_t row_str
                          float *out, float *work, hipStream_t s);
 hipError_t launch_head_bwd(const float *h, const float *dlogits, const float *dvalue, const float *wa,
                            const float *wc, int64_t n, int H, int A, float *dz, float *db4, float *dwa, float *dwc,
-                           float *work, uint32_t *amax, hipStream_t s);
+                           float *work, uint32_t *amax, hipStream_t s, const uint32_t *dmax = nullptr,
+                           void *dz_planes = nullptr);
 
 // atomicMax of each tower's block maximum (float bits of non-negative values) into amax[t], t < T <= 2; every
 // thread of the 256-thread block calls it
@@ -309,6 +311,58 @@ __device__ __forceinline__ void block_amax2(const uint32_t mx[2], int T, uint32_
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// The h3 operand form (merlin_h3.hip's header comment): per tower one power-of-two scale 2^e from a bound on max |x|,
+// per value an f16 hi plane and an f16 lo plane (x 2^11).  Shared by merlin_h3.hip's splits and the producers that
+// write their output as planes directly (k_head_bwd's dz, conv3's representatives).
+constexpr float H3_LO_SCALE = 2048.0f;
+// the scale exponent e of a tensor whose max |x| (or a bound on it) has float bits `amax`: amax 2^e in [2^14, 2^15)
+__device__ __forceinline__ int h3_exp(uint32_t amax) {
+    if (amax == 0u) return 0;
+    const int e = (int)((amax >> 23) & 0xffu) - 127;  // floor(log2) for a normal max (inf / nan: e = 128)
+    return min(max(14 - e, -120), 115);                // e + 11 stays a normal power of two
+}
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+
+// planes of two unscaled values a, b (sc = 2^e, sc2 = 2^(e + 11)): hi word (h of a, h of b) = f16(x'), lo word =
+// f16(2^11 x' - 2^11 h), each by one v_fma_mix{lo,hi}_f16 (the mixed fma rounds its exact result once to f16; in
+// the lo ones h is read as an f16 operand from its half of the hi word, so x' - h is never formed in f32): six
+// vector instructions per pair (the compiler's version of the same expressions took nine, computing h twice)
+__device__ __forceinline__ void h3_pair(float a, float b, float sc, float sc2, uint32_t &hi, uint32_t &lo) {
+    const float m2048 = -H3_LO_SCALE, za = a * sc2, zb = b * sc2;
+    uint32_t h, l;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(a), "v"(sc));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(b), "v"(sc));
+    asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(h), "v"(m2048), "v"(za));
+    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(h), "v"(m2048), "v"(zb));
+    hi = h;
+    lo = l;
+}
+
+// 4 consecutive values (columns 4 q .. 4 q + 3 of a row) -> their halves of the row's plane image: hi at uint2 index
+// 4 (q >> 1) + (q & 1), lo 2 uint2 further (a group of 8 values = a 16-B hi chunk + a 16-B lo chunk)
+__device__ __forceinline__ void h3_store4(uint2 *__restrict__ row, int q, const float4 v, float sc, float sc2) {
+    uint32_t h0, h1, l0, l1;
+    h3_pair(v.x, v.y, sc, sc2, h0, l0);
+    h3_pair(v.z, v.w, sc, sc2, h1, l1);
+    const int o = 4 * (q >> 1) + (q & 1);
+    row[o] = make_uint2(h0, h1);
+    row[o + 2] = make_uint2(l0, l1);
+}
+
+// h3_store4 with adjacent lanes paired (lane q and q ^ 1, both active, holding the two halves of one 8-value group):
+// one 16-B store per lane instead of two 8-B ones -- the even lane writes the group's hi chunk, the odd lane its lo
+// chunk (uint4 index q of the row's plane image), after one exchange of two words
+__device__ __forceinline__ void h3_store4_pair(uint4 *__restrict__ row, int q, const float4 v, float sc, float sc2) {
+    uint32_t h0, h1, l0, l1;
+    h3_pair(v.x, v.y, sc, sc2, h0, l0);
+    h3_pair(v.z, v.w, sc, sc2, h1, l1);
+    const bool odd = q & 1;
+    const uint32_t r0 = (uint32_t)__shfl_xor((int)(odd ? h0 : l0), 1);
+    const uint32_t r1 = (uint32_t)__shfl_xor((int)(odd ? h1 : l1), 1);
+    row[q] = odd ? make_uint4(r0, r1, l0, l1) : make_uint4(h0, h1, r0, r1);
+}
+
 // fc1 on the bf16 matrix cores in exact three-plane form (merlin_gemm.hip, merlin_x6.h)
 hipError_t launch_x6_split(const float *x, int64_t n, void *planes, hipStream_t s);
 hipError_t launch_x6_join(const void *planes, int64_t n, float *x, hipStream_t s);
@@ -328,7 +382,7 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
                              int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
                              int64_t c_stride, void *a_planes, int cfg, hipStream_t s,
                              const int32_t *a_rows = nullptr, const float *head_w0 = nullptr, int n_actions = 0,
-                             const float *head_w1 = nullptr, float *head_part = nullptr);
+                             const float *head_w1 = nullptr, float *head_part = nullptr, bool a_is_planes = false);
 // head_part (nullable; pipelined cfgs 10 / 12 / 13 with bias, 2 towers): the heads' dot products of h folded into the
 // forward GEMM's epilogue, h3_heads_parts(N, cfg) float4 partials per row and tower, [2][parts][M][4]; summed by
 // launch_heads_combine into logits [M][n_actions] and value [M]
@@ -341,7 +395,8 @@ hipError_t launch_heads_combine(const float *part, int P, int64_t M, int na, flo
 // cfgs 0-2 only)
 hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t Kd,
                              int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits, float *slab,
-                             float *out, bool planes, int cfg, hipStream_t s, const int32_t *b_rows = nullptr);
+                             float *out, bool planes, int cfg, hipStream_t s, const int32_t *b_rows = nullptr,
+                             bool a_planes = false, bool b_planes = false);
 
 // clip_grad_norm_ + Adam step over a parameter list (merlin_optim.hip)
 constexpr int OPT_MAX_TENSORS = 32;

@@ -24,6 +24,25 @@ constexpr int MAXA = 8;
 constexpr int NSTAT = 5;  // -pi, (v - R)^2, H, logp_old - logp, clipped
 constexpr int NSUM = NSTAT + MAXA + 1;  // + the heads' bias gradients (sum of every sample's dz, dv)
 
+// atomicMax of the block's maxima m[j] (float bits of non-negative values) into dmax[j], j < A and j = MAXA; every
+// thread of the 256-thread block calls it
+__device__ __forceinline__ void block_max9(const uint32_t (&m)[MAXA + 1], int A, uint32_t *__restrict__ dmax) {
+    __shared__ uint32_t red9[MAXA + 1][4];
+#pragma unroll
+    for (int j = 0; j <= MAXA; j++) {
+        uint32_t x = m[j];
+        for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+        if ((threadIdx.x & 63) == 0) red9[j][threadIdx.x >> 6] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x <= MAXA && (threadIdx.x < (unsigned)A || threadIdx.x == MAXA)) {
+        const uint32_t *r = red9[threadIdx.x];
+        const uint32_t x = max(max(r[0], r[1]), max(r[2], r[3]));
+        if (x && x > __hip_atomic_load(dmax + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMax(dmax + threadIdx.x, x);
+    }
+}
+
 // One lane per sample in frame-sorted order (position k -> sample order[k] of frame
 // inv[order[k]]), one wave per item of 64 positions.  Each lane forms its sample's loss
 // gradient wrt its frame's logits / value; a segmented inclusive scan over the wave (fixed
@@ -45,7 +64,8 @@ __global__ __launch_bounds__(LOSS_BLK) void k_ppo_loss(const float *__restrict__
                                                        const float *__restrict__ ret, float lo, float hi,
                                                        float clip, float vf2_n, float ent_n, float inv_n,
                                                        float *__restrict__ dlogits, float *__restrict__ dvalue,
-                                                       float *__restrict__ carry, double *__restrict__ partial) {
+                                                       float *__restrict__ carry, double *__restrict__ partial,
+                                                       uint32_t *__restrict__ dmax) {
     __shared__ double red[NSUM][LOSS_BLK];
     const int lane = threadIdx.x & 63;
     const int64_t item = (int64_t)blockIdx.x * LOSS_WAVES + (threadIdx.x >> 6);
@@ -144,6 +164,13 @@ __global__ __launch_bounds__(LOSS_BLK) void k_ppo_loss(const float *__restrict__
             dvalue[u] = g[MAXA];
         }
     }
+    if (dmax) {  // block-uniform: max |.| of the frames this block finished (the spanning ones: k_ppo_loss_fix)
+        uint32_t m[MAXA + 1];
+        const bool fin = last && offs[u] >= item * 64 && offs[u + 1] <= item * 64 + 64;
+#pragma unroll
+        for (int j = 0; j <= MAXA; j++) m[j] = fin ? __float_as_uint(g[j]) & 0x7fffffffu : 0u;
+        block_max9(m, A, dmax);
+    }
 #pragma unroll
     for (int q = 0; q < NSUM; q++) red[q][threadIdx.x] = st[q];
     __syncthreads();
@@ -157,14 +184,43 @@ __global__ __launch_bounds__(LOSS_BLK) void k_ppo_loss(const float *__restrict__
     if (threadIdx.x < NSUM) partial[(size_t)blockIdx.x * NSUM + threadIdx.x] = red[threadIdx.x][0];
 }
 
-// frames whose samples span items j0 < j1: carry[j0][1] + sum_{j0 < j <= j1} carry[j][0]
+__device__ void loss_fix_frame(const int32_t *__restrict__ offs, int64_t u, int A, const float *__restrict__ carry,
+                               float *__restrict__ dlogits, float *__restrict__ dvalue, uint32_t *m);
+
+// frames whose samples span items j0 < j1: carry[j0][1] + sum_{j0 < j <= j1} carry[j][0].
+// dmax (nullable, zeroed by the caller): dmax[j] = max over the frames of |dlogits[u][j]| (j < A) and dmax[MAXA] =
+// max |dvalue[u]|, as float bits (atomicMax of non-negative floats) -- the bound merlin_head.hip's k_head_bwd
+// derives dz's plane scale from, so that it can write dz as h3 planes in its one pass.  k_ppo_loss takes the
+// maximum over the frames it finishes, this kernel over the frames that span items.
 __global__ __launch_bounds__(256) void k_ppo_loss_fix(const int32_t *__restrict__ offs, int64_t U, int A,
                                                       const float *__restrict__ carry, float *__restrict__ dlogits,
-                                                      float *__restrict__ dvalue) {
+                                                      float *__restrict__ dvalue, uint32_t *__restrict__ dmax) {
     const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (u >= U) return;
+    if (!dmax) {
+        if (u < U) loss_fix_frame(offs, u, A, carry, dlogits, dvalue, nullptr);
+        return;
+    }
+    uint32_t m[MAXA + 1];
+    if (u < U) {
+        loss_fix_frame(offs, u, A, carry, dlogits, dvalue, m);
+    } else {
+#pragma unroll
+        for (int j = 0; j <= MAXA; j++) m[j] = 0u;
+    }
+    block_max9(m, A, dmax);
+}
+
+// one frame of k_ppo_loss_fix; m (nullable) receives |dlogits[u][j]| / |dvalue[u]| as float bits (0 for j >= A)
+__device__ void loss_fix_frame(const int32_t *__restrict__ offs, int64_t u, int A, const float *__restrict__ carry,
+                               float *__restrict__ dlogits, float *__restrict__ dvalue, uint32_t *m) {
     const int64_t j0 = offs[u] / 64, j1 = (offs[u + 1] - 1) / 64;
-    if (j1 <= j0) return;
+    if (j1 <= j0) {  // the frame's sum was written (and its max taken) by k_ppo_loss
+        if (m) {
+#pragma unroll
+            for (int j = 0; j <= MAXA; j++) m[j] = 0u;
+        }
+        return;
+    }
     float acc[MAXA + 1];
     const float *c = carry + ((size_t)j0 * 2 + 1) * (MAXA + 1);
 #pragma unroll
@@ -201,6 +257,10 @@ __global__ __launch_bounds__(256) void k_ppo_loss_fix(const int32_t *__restrict_
     for (int j = 0; j < MAXA; j++)
         if (j < A) dlogits[u * A + j] = acc[j];
     dvalue[u] = acc[MAXA];
+    if (m) {
+#pragma unroll
+        for (int j = 0; j <= MAXA; j++) m[j] = j < A || j == MAXA ? __float_as_uint(acc[j]) & 0x7fffffffu : 0u;
+    }
 }
 
 // stats[q] += (sum over the block partials) / n; loss = -pi + vf * v - ent * H (means); the
@@ -248,7 +308,7 @@ hipError_t launch_ppo_loss(const float *logits, const float *value, const float 
                            const int64_t *sample_index, const int64_t *actions, const float *lp_old, const float *adv,
                            const float *ret, double clip_eps, double vf_coef, double ent_coef, float *dlogits,
                            float *dvalue, float *dbias_a, float *dbias_c, float *loss, double *stats,
-                           double *workspace, hipStream_t s) {
+                           double *workspace, hipStream_t s, uint32_t *dmax) {
     const int64_t items = (n + 63) / 64, nblk = (items + LOSS_WAVES - 1) / LOSS_WAVES;
     const double inv_n = n > 0 ? 1.0 / (double)n : 0.0;
     double *partial = workspace;
@@ -258,11 +318,11 @@ hipError_t launch_ppo_loss(const float *logits, const float *value, const float 
                            order, inv, n,
                            sample_index, actions, lp_old, adv, ret, (float)(1.0 - clip_eps), (float)(1.0 + clip_eps),
                            (float)clip_eps, (float)(2.0 * vf_coef * inv_n), (float)(ent_coef * inv_n),
-                           (float)inv_n, dlogits, dvalue, carry, partial);
+                           (float)inv_n, dlogits, dvalue, carry, partial, dmax);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_ppo_loss_fix, dim3((unsigned)((U + 255) / 256)), dim3(256), 0, s, offs, U, A, carry,
-                           dlogits, dvalue);
+                           dlogits, dvalue, dmax);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -74,11 +74,13 @@ __global__ __launch_bounds__(256) void k_window_lut(const int32_t *__restrict__ 
 // = (Y3 channel ch > 0), the row's ReLU mask for the backward (16 lanes OR their nibbles together
 // with xor shuffles inside the row's 16-lane group; the caller keeps the groups whole and converged).
 // mx: max |Y3| per tower as float bits (merlin_h3.hip's operand scale), reduced by block_amax2.
+// pl (h3 planes, round 5): the row is written as its h3 planes (merlin_internal.h h3_store4_pair; 256 B like the fp32
+// row) scaled by psc = (2^e0, 2^e1, 2^(e0 + 11), 2^(e1 + 11)) of the two towers
 __device__ __forceinline__ void conv3_row(const float4 *__restrict__ Q, int64_t nw, const int32_t *__restrict__ wid,
                                           const int64_t *__restrict__ groups, int64_t n,
                                           const float4 *__restrict__ b3, float4 *__restrict__ Y3,
                                           uint64_t *__restrict__ bits, bool amax, int64_t r, int c,
-                                          uint32_t (&mx)[2]) {
+                                          uint32_t (&mx)[2], bool pl = false, float4 psc = float4{}) {
     const int64_t tu = r / 9;
     const int p3 = (int)(r - tu * 9), t = (int)(tu / n);
     const int64_t u = tu - (int64_t)t * n;
@@ -97,7 +99,10 @@ __device__ __forceinline__ void conv3_row(const float4 *__restrict__ Q, int64_t 
     const float4 b = b3[t * 16 + c];
     const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
                                  relu_nan(acc.w + b.w));
-    Y3[r * 16 + c] = y;
+    if (pl)
+        h3_store4_pair(reinterpret_cast<uint4 *>(Y3) + r * 16, c, y, t == 0 ? psc.x : psc.y, t == 0 ? psc.z : psc.w);
+    else
+        Y3[r * 16 + c] = y;
     if (amax) {
         const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
                                     std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
@@ -135,18 +140,28 @@ __global__ __launch_bounds__(256) void k_window_conv3(const float4 *__restrict__
 // space, packs its representatives into an LDS queue (ballot + prefix count) and computes them 4 at a time, 16
 // lanes per row, so no lane idles on a copied row.  The block walks its 256-row spans in step (block-uniform trip
 // count: the queue barriers are block barriers).
+// bound (nullable, round 5): the rows are written as h3 planes scaled by the exponent of bound[t] (k_q_bound's bound
+// on max Y3, known before any row is), amax unused
 __global__ __launch_bounds__(256) void k_window_conv3_reps(const float4 *__restrict__ Q, int64_t nw,
                                                            const int32_t *__restrict__ wid,
                                                            const int64_t *__restrict__ groups, int64_t n,
                                                            const float4 *__restrict__ b3, int T,
                                                            float4 *__restrict__ Y3, uint64_t *__restrict__ bits,
                                                            uint32_t *__restrict__ amax,
-                                                           const int32_t *__restrict__ rrow) {
+                                                           const int32_t *__restrict__ rrow,
+                                                           const uint32_t *__restrict__ bound) {
     __shared__ int64_t queue[4][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
     const unsigned long long below = (1ull << lane) - 1ull;
     const int64_t rows = n * 9, total = (int64_t)T * rows;
     uint32_t mx[2] = {0u, 0u};
+    const bool pl = bound != nullptr;
+    float4 psc = float4{};
+    if (pl) {
+        const int e0 = h3_exp(__hip_atomic_load(bound, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const int e1 = T > 1 ? h3_exp(__hip_atomic_load(bound + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0;
+        psc = make_float4(pow2f(e0), pow2f(e1), pow2f(e0 + 11), pow2f(e1 + 11));
+    }
     for (int64_t base = (int64_t)blockIdx.x * 256; base < total; base += (int64_t)gridDim.x * 256) {
         const int64_t i = base + threadIdx.x;
         bool rep = false;
@@ -158,11 +173,76 @@ __global__ __launch_bounds__(256) void k_window_conv3_reps(const float4 *__restr
         if (rep) queue[wv][__popcll(m & below)] = i;
         __syncthreads();
         const int cnt = __popcll(m);
-        for (int p = q; p < cnt; p += 4) conv3_row(Q, nw, wid, groups, n, b3, Y3, bits, amax != nullptr,
-                                                   queue[wv][p], c, mx);
+        for (int p = q; p < cnt; p += 4) conv3_row(Q, nw, wid, groups, n, b3, Y3, bits, !pl && amax != nullptr,
+                                                   queue[wv][p], c, mx, pl, psc);
         __syncthreads();
     }
-    if (amax) block_amax2(mx, T, amax);
+    if (!pl && amax) block_amax2(mx, T, amax);
+}
+
+// A bound on max Y3 per tower before conv3 runs, so its representatives can be written as h3 planes directly (the
+// plane scale must be known when a value is stored): Y3[u, p3][c] = relu(b3[c] + sum over taps of Q[w][tap][c]) <=
+// relu(b3[c] + sum over taps of max_w Q[w][tap][c]), the maxima summed in conv3_row's order (fp32 addition is
+// monotonic, so the bound holds for the rounded sums too).  A bound above the max only moves the planes' 2^26 dynamic
+// range up by the ratio.
+// ordered-uint image of a float: monotonic over all floats, NaN above +inf (so a NaN column max propagates)
+__device__ __forceinline__ uint32_t f2ord(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t o) {
+    return o == 0u ? -INFINITY : __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+// part[t][b][k] = max over block b's windows of Q[t][w][k] (ordered images; k = tap * 64 + c): QB_BLOCKS blocks per
+// tower over contiguous window ranges, 2 x 144 threads each (a half takes every other row, 8 rows' loads in flight),
+// plain stores -- k_q_bound reduces over the blocks (same-address atomics from every block serialised: 152 us)
+constexpr int QB_BLOCKS = 64;
+__global__ __launch_bounds__(288) void k_q_colmax(const float4 *__restrict__ Q, int64_t nw, uint4 *__restrict__ part) {
+    const int t = blockIdx.y, j = threadIdx.x % 144, h = threadIdx.x / 144;
+    const int64_t per = (nw + QB_BLOCKS - 1) / QB_BLOCKS;
+    const int64_t w0 = (int64_t)blockIdx.x * per, w1 = std::min<int64_t>(nw, w0 + per);
+    const float4 *q = Q + (size_t)t * nw * 144 + j;
+    uint32_t m[4] = {0u, 0u, 0u, 0u};
+    for (int64_t w = w0 + h; w < w1; w += 16) {
+        float4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = q[(size_t)std::min<int64_t>(w + 2 * i, w1 - 1) * 144];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            m[0] = max(m[0], f2ord(v[i].x));
+            m[1] = max(m[1], f2ord(v[i].y));
+            m[2] = max(m[2], f2ord(v[i].z));
+            m[3] = max(m[3], f2ord(v[i].w));
+        }
+    }
+    __shared__ uint4 hm[144];
+    if (h == 1) hm[j] = make_uint4(m[0], m[1], m[2], m[3]);
+    __syncthreads();
+    if (h == 0) {
+        const uint4 o = hm[j];
+        part[((size_t)t * QB_BLOCKS + blockIdx.x) * 144 + j] =
+            make_uint4(max(m[0], o.x), max(m[1], o.y), max(m[2], o.z), max(m[3], o.w));
+    }
+}
+// bound[t] = float bits of max over c of relu(sum_tap colmax[t][tap][c] + b3[t][c]), colmax[t][k] the max over the
+// blocks' partials (one block of 576 threads per tower)
+__global__ __launch_bounds__(576) void k_q_bound(const uint32_t *__restrict__ part, const float *__restrict__ b3,
+                                                 uint32_t *__restrict__ bound) {
+    const int t = blockIdx.x, k = threadIdx.x;
+    uint32_t m = 0u;
+#pragma unroll 8
+    for (int b = 0; b < QB_BLOCKS; b++) m = max(m, part[((size_t)t * QB_BLOCKS + b) * 576 + k]);
+    __shared__ float col[576];
+    col[k] = ord2f(m);
+    __syncthreads();
+    if (k < 64) {
+        float acc = col[k];
+#pragma unroll
+        for (int tap = 1; tap < 9; tap++) acc += col[tap * 64 + k];
+        uint32_t y = __float_as_uint(relu_nan(acc + b3[t * 64 + k])) & 0x7fffffffu;
+        for (int o = 32; o > 0; o >>= 1) y = max(y, (uint32_t)__shfl_xor((int)y, o));
+        if (k == 0) bound[t] = y;
+    }
 }
 
 // The other rows from their representatives (after k_window_conv3_reps): with Y (16 lanes per row) the Y3 row and
@@ -583,7 +663,7 @@ hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, 
 
 hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, const int64_t *groups, int64_t n,
                                const float *b3, int T, float *Y3, uint64_t *bits, uint32_t *amax, const int32_t *rrow,
-                               int copy, hipStream_t s) {
+                               int copy, hipStream_t s, uint32_t *colmax, uint32_t *bound) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
@@ -595,9 +675,21 @@ hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, c
     }
     if (T > 2) return hipErrorInvalidValue;
     const int rgrid = (int)std::min<int64_t>((total / 16 + 255) / 256, 256 * 32);
+    if (bound) {  // planes: the representatives only, scaled by the bound from Q's column maxima
+        if (!colmax || (copy & 7) || nw <= 0) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_q_colmax, dim3(QB_BLOCKS, T), dim3(288), 0, s, q, nw, reinterpret_cast<uint4 *>(colmax));
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_q_bound, dim3(T), dim3(576), 0, s, colmax, b3, bound);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_window_conv3_reps, dim3(rgrid), dim3(256), 0, s, q, nw, wid, groups, n, b, T, y, bits,
+                           nullptr, rrow, bound);
+        return hipGetLastError();
+    }
     if (!(copy & 4)) {  // copy bit 2: the copies only (the representatives were computed by an earlier call)
         hipLaunchKernelGGL(k_window_conv3_reps, dim3(rgrid), dim3(256), 0, s, q, nw, wid, groups, n, b, T, y, bits,
-                           amax, rrow);
+                           amax, rrow, nullptr);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -121,6 +121,7 @@ def lib():
     L.merlin_tower_relu_bwd.argtypes = [vp, vp, vp, i64, i32, i32, vp, vp]
     L.merlin_tower_colsum.argtypes = [vp, i64, i32, i64, i64, i32, vp, vp]
     L.merlin_tower_head_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]
+    L.merlin_tower_head_bwd_planes.argtypes = [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
     L.merlin_act_heads.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp,
                                    vp]
     L.merlin_ppo_loss_workspace.argtypes = [i64]
@@ -131,6 +132,8 @@ def lib():
                                    vp, vp, vp]
     L.merlin_ppo_loss.argtypes = [vp, vp, vp, vp, i64, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp, C.c_double,
                                   C.c_double, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.merlin_ppo_loss_absmax.argtypes = [vp, vp, vp, vp, i64, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp, C.c_double,
+                                         C.c_double, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.merlin_x6_split.argtypes = [vp, i64, vp, vp]
     L.merlin_x6_join.argtypes = [vp, i64, vp, vp]
     L.merlin_x6_gemm_nt.argtypes = [vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, i32, vp]
@@ -144,6 +147,14 @@ def lib():
     L.merlin_h3_gemm_tn_planes.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, i32, vp]
     L.merlin_h3_gemm_nt_gather.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, vp, i32, vp]
     L.merlin_h3_gemm_tn_gather.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, vp, i32, vp]
+    L.merlin_h3_gemm_tn_gather_planes_a.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, vp, i32,
+                                                    vp]
+    L.merlin_h3_gemm_nt_planes.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, vp, i64, i32, vp]
+    L.merlin_h3_gemm_nt_heads_planes.argtypes = [vp, vp, vp, vp, i64, i32, i32, i64, i64, vp, vp, i64, vp, vp, i32,
+                                                 vp, vp, i32, vp]
+    L.merlin_h3_gemm_tn_gather_planes.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, i32, vp, vp, vp, i32,
+                                                  vp]
+    L.merlin_tower_window_conv3_planes.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp, vp, vp]
     L.merlin_h3_gemm_nt_heads.argtypes = [vp, vp, vp, vp, i64, i32, i32, i64, i64, vp, vp, i64, vp, vp, i32, vp, vp,
                                           i32, vp]
     L.merlin_h3_heads_parts.argtypes = [i32, i32]
@@ -197,6 +208,9 @@ EXPORTED_SYMBOLS = (
     "merlin_h3_amax", "merlin_h3_split", "merlin_h3_gemm_nt", "merlin_h3_gemm_tn",
     "merlin_h3_gemm_tn_planes", "merlin_h3_gemm_nt_gather", "merlin_h3_gemm_tn_gather",
     "merlin_h3_gemm_nt_heads", "merlin_h3_heads_parts", "merlin_heads_combine", "merlin_act_draw",
+    "merlin_ppo_loss_absmax", "merlin_tower_head_bwd_planes", "merlin_h3_gemm_nt_planes",
+    "merlin_h3_gemm_tn_gather_planes_a", "merlin_h3_gemm_nt_heads_planes", "merlin_h3_gemm_tn_gather_planes",
+    "merlin_tower_window_conv3_planes",
 )
 
 
@@ -593,6 +607,38 @@ def window_lut(rows, tables, bias=None):
     return out
 
 
+_COLMAX_WS: dict = {}
+
+
+def window_conv3_planes(Q, wid, groups, b3, rep_row, bound, n_reps=None):
+    """(Y3 planes int16[T, n*9, 128], mask int64[T, n*9]): window_conv3(bits=True, rep_row=..., copy=0) with the
+    representatives' rows written as h3 planes (merlin_tower_window_conv3_planes), scaled by bound int32[T] (written:
+    float bits of relu(b3 + sum over taps of Q's column maxima) per tower, >= every Y3 value).  Only the
+    representatives' rows hold data (read through rep_row, as with copy=0)."""
+    T, nw = int(Q.shape[0]), int(Q.shape[1])
+    n = int(groups.numel())
+    assert Q.shape[2] == 576 and Q.dtype == torch.float32 and Q.is_contiguous() and b3.shape == (T, 64) and T <= 2
+    assert wid.dtype == torch.int32 and wid.shape[1] == 25 and groups.dtype == torch.int64
+    assert rep_row.dtype == torch.int32 and rep_row.is_contiguous() and rep_row.numel() == n * 9
+    assert bound.dtype == torch.int32 and bound.numel() >= T
+    dev = Q.device
+    ws = _COLMAX_WS.get(dev)
+    if ws is None:
+        ws = _COLMAX_WS[dev] = torch.empty(2 * 64 * 576, dtype=torch.int32, device=dev)  # per-block column maxima
+    out = torch.empty((T, n * 9, 128), dtype=torch.int16, device=dev)
+    mask = torch.empty((T, n * 9), dtype=torch.int64, device=dev)
+    if POISON_PARTIAL:
+        out.fill_(-1)
+        mask.fill_(-1)
+    fixed = n * 144 + 2 * T * nw * 576 * 4  # ids + Q read twice (column maxima, then the gathers' first touch)
+    nb = (lambda: T * int(n_reps) * 264 + fixed) if n_reps is not None else T * n * 9 * 264 + fixed
+    with KernelTimer.span("k_window_conv3", nb):
+        check(lib().merlin_tower_window_conv3_planes(ptr(Q), nw, ptr(wid), ptr(groups), n, ptr(b3), T, ptr(out),
+                                                     ptr(mask), ptr(rep_row), ptr(ws), ptr(bound), stream_of(Q)),
+              "merlin_tower_window_conv3_planes")
+    return out, mask
+
+
 def window_conv3(Q, wid, groups, b3, bits: bool = False, rows: int | None = None, amax=None, rep_row=None,
                  copy: int = 3, n_reps=None):
     """Y3 f32[T, n*9, 64] = relu(conv3) rows (k, p3) of frames groups[k] from
@@ -826,21 +872,36 @@ def heads_fwd(h: torch.Tensor, w_actor: torch.Tensor, w_critic: torch.Tensor, b_
     return logits, value
 
 
-def head_bwd(h, dlogits, dvalue, w_actor, w_critic, out_bias=None, out_w_actor=None, out_w_critic=None, amax=None):
+def head_bwd(h, dlogits, dvalue, w_actor, w_critic, out_bias=None, out_w_actor=None, out_w_critic=None, amax=None,
+             grad_absmax=None, dz_planes=None):
     """Heads backward through fc1's ReLU: h f32[2, n, H] = relu(fc1) of both towers, dlogits
     f32[n, A], dvalue f32[n], w_actor f32[A, H], w_critic f32[1, H] or [H] ->
     (dz f32[2, n, H], dbias f32[2, H], dw_actor f32[A, H], dw_critic f32[H]); the out_* tensors, when
     given, receive the bias / head-weight gradients (e.g. views of a flat gradient buffer).  amax int32[2], zeroed by
-    the caller, receives max |dz| per tower as float bits (h3_amax's format)."""
+    the caller, receives max |dz| per tower as float bits (h3_amax's format).
+    grad_absmax int32[9] (ppo_loss's, merlin_tower_head_bwd_planes): dz is written as its h3 planes instead, into
+    dz_planes int16[2, n, 2H] (allocated if None; returned in dz's place), and amax[t] receives the bound on max |dz|
+    the planes are scaled by."""
     _, n, H = (int(x) for x in h.shape)
     A = int(w_actor.shape[0])
     assert h.shape[0] == 2 and dlogits.shape == (n, A) and dvalue.numel() == n and w_critic.numel() == H
-    dz = torch.empty_like(h)
     db = torch.empty((2, H), dtype=torch.float32, device=h.device) if out_bias is None else out_bias
     dwa = torch.empty((A, H), dtype=torch.float32, device=h.device) if out_w_actor is None else out_w_actor
     dwc = torch.empty((H,), dtype=torch.float32, device=h.device) if out_w_critic is None else out_w_critic
     assert db.shape == (2, H) and dwa.shape == (A, H) and dwc.numel() == H
     assert db.is_contiguous() and dwa.is_contiguous() and dwc.is_contiguous()
+    if grad_absmax is not None:
+        assert amax is not None and amax.dtype == grad_absmax.dtype == torch.int32 and grad_absmax.numel() >= 9
+        if dz_planes is None:
+            dz_planes = torch.empty((2, n, 2 * H), dtype=torch.int16, device=h.device)
+        assert dz_planes.shape == (2, n, 2 * H) and dz_planes.dtype == torch.int16 and dz_planes.is_contiguous()
+        with KernelTimer.span("k_head_bwd", 2 * h.numel() * 4 + n * (A + 1) * 4):
+            check(lib().merlin_tower_head_bwd_planes(ptr(h), ptr(dlogits), ptr(dvalue), ptr(w_actor), ptr(w_critic),
+                                                     n, H, A, ptr(dz_planes), ptr(db), ptr(dwa), ptr(dwc),
+                                                     ptr(grad_absmax), ptr(amax), stream_of(h)),
+                  "merlin_tower_head_bwd_planes")
+        return dz_planes, db, dwa, dwc
+    dz = torch.empty_like(h)
     with KernelTimer.span("k_head_bwd", 2 * h.numel() * 4 + n * (A + 1) * 4):
         check(lib().merlin_tower_head_bwd(ptr(h), ptr(dlogits), ptr(dvalue), ptr(w_actor), ptr(w_critic), n, H, A,
                                           ptr(dz), ptr(db), ptr(dwa), ptr(dwc), ptr(amax), stream_of(h)),
@@ -850,13 +911,16 @@ def head_bwd(h, dlogits, dvalue, w_actor, w_critic, out_bias=None, out_w_actor=N
 
 # -- PPO loss (csrc/merlin_loss.hip) -------------------------------------------------------------
 def ppo_loss(logits, value, offs, order, frame_of, sample_index, actions, logp_old, adv, ret, clip_eps, vf_coef,
-             ent_coef, stats=None, bias_actor=None, bias_critic=None, out_bias_actor=None, out_bias_critic=None):
+             ent_coef, stats=None, bias_actor=None, bias_critic=None, out_bias_actor=None, out_bias_critic=None,
+             grad_absmax=None):
     """(loss f32[], dlogits f32[U, A], dvalue f32[U], dbias_actor f32[A] | None, dbias_critic f32[1] |
     None): the PPO minibatch loss of src/ppo.py:136-150 over the samples of U distinct frames (CSR
     offs int32[U+1] / order int32[n], frame_of int64[n] = the frame of sample i; sample i reads
     actions / logp_old / adv / ret at sample_index[i]) and its gradient per frame.  With the
     heads' biases given, logits / value exclude them and their gradients are returned too.
-    stats f64[>=5], when given, gets (pi_loss, v_loss, entropy, approx_kl, clipfrac) added."""
+    stats f64[>=5], when given, gets (pi_loss, v_loss, entropy, approx_kl, clipfrac) added.
+    grad_absmax int32[9] (zeroed by the caller): max |dlogits[:, j]| into [j], max |dvalue| into [8], float bits
+    (merlin_ppo_loss_absmax; head_bwd's plane bound)."""
     U, A = (int(x) for x in logits.shape)
     n = int(order.numel())
     assert logits.dtype == value.dtype == torch.float32 and value.shape == (U,)
@@ -884,12 +948,15 @@ def ppo_loss(logits, value, offs, order, frame_of, sample_index, actions, logp_o
         assert dbc.numel() == 1 and dbc.is_contiguous()
     ws = torch.empty(max(int(lib().merlin_ppo_loss_workspace(n)), 1), dtype=torch.float64, device=dev)
     with KernelTimer.span("k_ppo_loss", U * (4 * A + 4) * 2 + n * (4 + 8 + 8 + 12)):
-        check(lib().merlin_ppo_loss(ptr(logits.contiguous()), ptr(value.contiguous()), ptr(bias_actor),
-                                    ptr(bias_critic), U, A, ptr(offs), ptr(order), ptr(frame_of), n,
-                                    ptr(sample_index), ptr(actions.contiguous()), ptr(logp_old.contiguous()),
-                                    ptr(adv.contiguous()), ptr(ret.contiguous()), float(clip_eps), float(vf_coef),
-                                    float(ent_coef), ptr(dlogits), ptr(dvalue), ptr(dba), ptr(dbc), ptr(loss),
-                                    ptr(stats), ptr(ws), stream_of(logits)), "merlin_ppo_loss")
+        if grad_absmax is not None:
+            assert grad_absmax.dtype == torch.int32 and grad_absmax.numel() >= 9 and grad_absmax.is_contiguous()
+        check(lib().merlin_ppo_loss_absmax(ptr(logits.contiguous()), ptr(value.contiguous()), ptr(bias_actor),
+                                           ptr(bias_critic), U, A, ptr(offs), ptr(order), ptr(frame_of), n,
+                                           ptr(sample_index), ptr(actions.contiguous()), ptr(logp_old.contiguous()),
+                                           ptr(adv.contiguous()), ptr(ret.contiguous()), float(clip_eps),
+                                           float(vf_coef), float(ent_coef), ptr(dlogits), ptr(dvalue), ptr(dba),
+                                           ptr(dbc), ptr(loss), ptr(stats), ptr(ws), ptr(grad_absmax),
+                                           stream_of(logits)), "merlin_ppo_loss_absmax")
     return loss, dlogits, dvalue, dba, dbc
 
 
@@ -1015,7 +1082,7 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
 # 128 x 256 and input gradient 128 x 192 tiles (scripts/ab_update.py, same update replayed: 204.5 vs 209.0 ms for cfg 0 / 1)
 # rollout: 4,096 rows; qall: [5^9, 64] x [64, 576] (k_h3_nt, not the input gradient's k_h3_ntp instantiation, so
 # profiles keep the two apart); qwin / qwin_dgrad: the update's window GEMMs (N = 576, K = 64 / N = 64, K = 576)
-H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 1, "qwin": 11, "qwin_dgrad": 5}
+H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 1, "qwin": 11, "qwin_dgrad": 5, "dgrad_planes": 62}
 H3_TN_CFG = 0
 # the update's fc1 forward (h3, cfg "fwd" with a heads epilogue) computes the policy / value heads in its epilogue
 # (merlin_h3_gemm_nt_heads + merlin_heads_combine) instead of a pass over h (merlin_heads_fwd)
@@ -1116,6 +1183,29 @@ def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
     return out
 
 
+def h3_gemm_nt_planes(Ap: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,
+                      bias: torch.Tensor | None = None, cfg: int = 62, out: torch.Tensor | None = None,
+                      name: str = "h3_gemm_nt") -> torch.Tensor:
+    """h3_gemm_nt with A already in plane form, Ap int16[T, M, 2K] scaled by amaxA's exponent (e.g. head_bwd's dz
+    planes): merlin_h3_gemm_nt_planes, both operands by LDS-DMA (cfg 60 / 61 / 62, K = 512 or 576)."""
+    H3_SPANS.add(name)
+    T, M, K2 = (int(v) for v in Ap.shape)
+    K = K2 // 2
+    N = int(B.shape[1])
+    assert Ap.dtype == B.dtype == torch.int16 and B.shape == (T, N, 2 * K) and Ap.is_contiguous() and B.is_contiguous()
+    assert amaxA.dtype == amaxB.dtype == torch.int32
+    if out is None:
+        out = torch.empty((T, M, N), dtype=torch.float32, device=Ap.device)
+    assert out.shape == (T, M, N) and out.is_contiguous()
+    if bias is not None:
+        assert bias.shape == (T, N) and bias.is_contiguous()
+    with KernelTimer.span(name, 0, 2 * T * M * N * K):
+        check(lib().merlin_h3_gemm_nt_planes(ptr(Ap), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, T, M * K, N * K,
+                                             ptr(bias) if bias is not None else None, ptr(out), M * N, int(cfg),
+                                             stream_of(Ap)), "merlin_h3_gemm_nt_planes")
+    return out
+
+
 def h3_gemm_nt_heads(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor, bias: torch.Tensor,
                      Wa: torch.Tensor, Wc: torch.Tensor, cfg: int, rows: torch.Tensor | None = None,
                      name: str = "h3_gemm_nt", partials_only: bool = False) -> tuple:
@@ -1126,9 +1216,13 @@ def h3_gemm_nt_heads(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amax
     act_draw)."""
     H3_SPANS.add(name)
     T, M, K = (int(v) for v in A.shape)
+    ap = A.dtype == torch.int16  # A as planes (window_conv3_planes): merlin_h3_gemm_nt_heads_planes, gathered only
+    if ap:
+        K //= 2
+        assert rows is not None and not partials_only
     N = int(B.shape[1])
     NA = int(Wa.shape[0])
-    assert T == 2 and A.dtype == torch.float32 and B.dtype == torch.int16 and B.shape == (T, N, 2 * K)
+    assert T == 2 and A.dtype in (torch.float32, torch.int16) and B.dtype == torch.int16 and B.shape == (T, N, 2 * K)
     assert A.is_contiguous() and B.is_contiguous() and bias.shape == (T, N) and bias.is_contiguous()
     assert Wa.shape == (NA, N) and Wa.is_contiguous() and Wc.numel() == N and Wc.is_contiguous() and 1 <= NA <= 4
     P = int(lib().merlin_h3_heads_parts(N, int(cfg)))
@@ -1137,10 +1231,10 @@ def h3_gemm_nt_heads(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amax
         assert rows.dtype == torch.int32 and rows.is_contiguous() and rows.numel() == M * K // 64
     out = None if partials_only else torch.empty((T, M, N), dtype=torch.float32, device=A.device)
     part = torch.empty((T, P, M, 4), dtype=torch.float32, device=A.device)
+    fn = lib().merlin_h3_gemm_nt_heads_planes if ap else lib().merlin_h3_gemm_nt_heads
     with KernelTimer.span(name, 0, 2 * T * M * N * K):
-        check(lib().merlin_h3_gemm_nt_heads(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, M * K, N * K, ptr(bias),
-                                            ptr(out), M * N, ptr(rows), ptr(Wa), NA, ptr(Wc), ptr(part), int(cfg),
-                                            stream_of(A)), "merlin_h3_gemm_nt_heads")
+        check(fn(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, M * K, N * K, ptr(bias), ptr(out), M * N, ptr(rows),
+                 ptr(Wa), NA, ptr(Wc), ptr(part), int(cfg), stream_of(A)), "merlin_h3_gemm_nt_heads")
     if partials_only:
         return part
     logits = torch.empty((M, NA), dtype=torch.float32, device=A.device)
@@ -1185,9 +1279,17 @@ def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
     splits = H3_TN_SPLITS if splits is None else splits
     cfg = H3_TN_CFG if cfg is None else cfg
     planes = A.dtype == torch.int16
+    a_planes = planes and (B.dtype == torch.float32 or rows is not None)  # A planes (head_bwd's dz), B through rows
+    b_planes = a_planes and B.dtype == torch.int16  # ... B planes too (window_conv3_planes)
+    if a_planes:
+        planes = False
     T, Kd, M = (int(v) for v in A.shape)
-    N = int(B.shape[2])
-    if planes:
+    if a_planes:
+        M //= 2
+    N = int(B.shape[2]) // (2 if b_planes else 1)
+    if a_planes:
+        assert rows is not None and M % 8 == 0, "A planes: the gathered form only"
+    elif planes:
         assert B.dtype == torch.int16 and M % 2 == 0 and N % 2 == 0
         M, N = M // 2, N // 2
     else:
@@ -1202,10 +1304,11 @@ def h3_gemm_tn(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
     if rows is not None:
         assert not planes and rows.dtype == torch.int32 and rows.is_contiguous() and N % 64 == 0
         assert rows.numel() == Kd * N // 64
+        fn = (lib().merlin_h3_gemm_tn_gather_planes if b_planes else lib().merlin_h3_gemm_tn_gather_planes_a
+              if a_planes else lib().merlin_h3_gemm_tn_gather)
         with KernelTimer.span(name, 0, 2 * T * M * N * Kd):
-            check(lib().merlin_h3_gemm_tn_gather(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), Kd, M, N, T, Kd * M, Kd * N,
-                                                 int(splits), ptr(slab), ptr(out), ptr(rows), int(cfg), stream_of(A)),
-                  "merlin_h3_gemm_tn_gather")
+            check(fn(ptr(A), ptr(amaxA), ptr(B), ptr(amaxB), Kd, M, N, T, Kd * M, Kd * N, int(splits), ptr(slab),
+                     ptr(out), ptr(rows), int(cfg), stream_of(A)), "merlin_h3_gemm_tn_gather")
         return out
     fn = lib().merlin_h3_gemm_tn_planes if planes else lib().merlin_h3_gemm_tn
     with KernelTimer.span(name, 0, 2 * T * M * N * Kd):

@@ -213,6 +213,17 @@ MASK_COPY_SIDE = False
 # with "gather": the non-representative rows' mask words are not copied at all; the patch sums (R pass) read each row's
 # word through rep_row (merlin_segment_sum_mask_rows)
 MASK_ROWS = True
+# h3 with gathered a3 rows: dz leaves k_head_bwd as h3 planes scaled by a bound on max |dz| known before the pass (the
+# loss's per-output maxima of dlogits / dvalue through the heads' weights: merlin_ppo_loss_absmax,
+# merlin_tower_head_bwd_planes) instead of fp32 + its max, so the input gradient runs on both operands as planes
+# (merlin_h3_gemm_nt_planes, LDS-DMA staged, cfg H3_NT_CFG["dgrad_planes"]) and the weight gradient stages dz's
+# planes as copies (merlin_h3_gemm_tn_gather_planes_a).  False: dz in fp32, split by the GEMMs.
+DZ_PLANES = True
+# with DZ_PLANES: conv3's representative rows leave k_window_conv3_reps as h3 planes too, scaled by a bound on max Y3
+# from Q's column maxima (merlin_tower_window_conv3_planes), so the forward GEMM stages a3 as copies
+# (merlin_h3_gemm_nt_heads_planes) and the weight gradient runs on both operands' planes
+# (merlin_h3_gemm_tn_gather_planes).  False: a3 in fp32, split by the GEMMs.
+A3_PLANES = True
 
 
 class WindowStep:
@@ -245,7 +256,8 @@ class WindowStep:
         self.stage = WeightStage(ac, flat_params, flat, impl=getattr(agent, "stage_impl", "hip"), fc1=self.fc1)
         self.head = (ac.actor[2].weight, ac.actor[2].bias, ac.critic[2].weight, ac.critic[2].bias)
         self._side = None
-        self.amax_act = torch.zeros(4, dtype=torch.int32, device=agent.device)
+        # [0:2] max |a3|, [2:4] max |dz| (or its bound), [4:13] the loss's max |dlogits[:, j]| / |dvalue| (DZ_PLANES)
+        self.amax_act = torch.zeros(16, dtype=torch.int32, device=agent.device)
         self.amax_win = torch.zeros(4, dtype=torch.int32, device=agent.device)  # a2w's and dQ's scales
 
     def valid(self) -> bool:
@@ -308,11 +320,19 @@ class WindowStep:
         # with gathered rows: the representatives only here; the other rows' mask words (read by the backward's patch
         # sums) are copied on the side stream beside the forward GEMM, joined by an event before that pass
         # MASK_ROWS: no copy at all, the patch sums read each row's mask word through its representative
-        Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None, rep_row=rep_row,
-                                    copy=(0 if (MASK_COPY_SIDE or MASK_ROWS) else 2) if arows is not None else 3,
-                                    n_reps=getattr(mb, "n_reps", None))
         n = int(mb.groups.numel())
-        a3 = Y3.view(2, n, 576)
+        a3p = (arows is not None and DZ_PLANES and A3_PLANES and MASK_ROWS and not MASK_COPY_SIDE
+               and nat.H3_HEADS_EPILOGUE and int(Wa.shape[0]) <= 4)
+        if a3p:  # the representatives as h3 planes, am3 = the bound they are scaled by
+            Y3, bits = nat.window_conv3_planes(Q, plan.wid, mb.groups, b3, rep_row, am3,
+                                               n_reps=getattr(mb, "n_reps", None))
+            a3 = Y3.view(2, n, 1152)
+        else:
+            Y3, bits = nat.window_conv3(Q, plan.wid, mb.groups, b3, bits=True, amax=am3 if h3 else None,
+                                        rep_row=rep_row,
+                                        copy=(0 if (MASK_COPY_SIDE or MASK_ROWS) else 2) if arows is not None else 3,
+                                        n_reps=getattr(mb, "n_reps", None))
+            a3 = Y3.view(2, n, 576)
         pa3 = pdz = None
         main = torch.cuda.current_stream()
         side = self.side_stream(a3.device)
@@ -347,13 +367,17 @@ class WindowStep:
             h = nat.x6_gemm_nt(a3, P4, bias=b4, cfg=nat.X6_NT_CFG["fwd"], name="gemm_fc1_fwd")
             logits, value = nat.heads_fwd(h, Wa, Wc)  # both heads in one pass over h (the loss adds their biases)
         # ---- loss and its gradient per frame (merlin.ppo._PPOLoss); the head-bias gradients land in .grad
+        dzp = h3 and DZ_PLANES and arows is not None and pa3 is None and int(Wa.shape[0]) <= 8
+        assert dzp or not a3p
+        dmax = am[4:13] if dzp else None
         _, dlogits, dvalue, _, _ = nat.ppo_loss(
             logits, value, mb.offs, mb.order, mb.inv, mb_idx, actions, logp_old, adv, ret, ag.clip_eps, ag.vf_coef,
             ag.ent_coef, totals, bias_actor=ba, bias_critic=bc, out_bias_actor=self.views[ba],
-            out_bias_critic=self.views[bc])
+            out_bias_critic=self.views[bc], grad_absmax=dmax)
         # ---- backward (_WindowTowerHeadX6.backward, _WindowGemm / _BiasRelu / _WindowConv2 backward)
+        # (dzp: dz is its h3 planes, int16 [2, n, 1024], scaled by the bound left in amz)
         dz, _, _, _ = nat.head_bwd(h, dlogits, dvalue, Wa, Wc, out_bias=g[5], out_w_actor=self.views[Wa],
-                                   out_w_critic=self.views[Wc], amax=amz if h3 else None)
+                                   out_w_critic=self.views[Wc], amax=amz if h3 else None, grad_absmax=dmax)
         if split_side:  # and dz's beside the input-gradient GEMM
             side.wait_stream(main)
             with torch.cuda.stream(side):
@@ -371,7 +395,9 @@ class WindowStep:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 wgrad()
-        if h3:
+        if dzp:
+            da3 = nat.h3_gemm_nt_planes(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad_planes"], name="gemm_fc1_dgrad")
+        elif h3:
             if pa3 is not None and not WGRAD_EARLY and not split_side:
                 pdz = torch.empty((2, n, 1024), dtype=torch.int16, device=dz.device)
             da3 = nat.h3_gemm_nt(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad"], name="gemm_fc1_dgrad",

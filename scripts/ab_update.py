@@ -70,6 +70,9 @@ def main():
             FS.WGRAD_SIDE = "wgradmain" not in name  # the weight gradient on the main stream (no overlap)
             FS.MASK_COPY_SIDE = "maskside" in name  # the mask-word copy on the side stream
             FS.MASK_ROWS = "maskcopy" not in name  # the mask-word copy instead of the R pass's row map
+            FS.DZ_PLANES = "nodzp" not in name  # dz in fp32 (split by the GEMMs) instead of head_bwd's planes
+            FS.A3_PLANES = "noa3p" not in name  # a3 in fp32 instead of conv3's planes
+            nat.H3_NT_CFG["dgrad_planes"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3p"), 62)
             nat.X6_NT_CFG["fwd"] = 28 if "fwd28" in name else 20
             nat.X6_NT_CFG["dgrad"] = 27 if "dgrad27" in name else 22
             nat.X6_TN_CFG = next((int(t[2:]) for t in name.split("_") if t[:2] == "tn" and t[2:].isdigit()), 0)

@@ -82,6 +82,16 @@ def test_ppo_loss_matches_torch(device, U, n, A, indexed):
     l1, d1, v1, _, _ = nat.ppo_loss(logits, value, mb.offs, mb.order, inv, sample_index, actions, lp_full, adv, ret, clip, vf,
                               ent_coef)
     assert torch.equal(l1, l2) and torch.equal(d1, d2) and torch.equal(v1, v2)
+    # merlin_ppo_loss_absmax: the same outputs, and the per-output maxima of |dlogits| / |dvalue| (the bound the
+    # heads' backward scales dz's planes by) exactly
+    gm = torch.zeros(9, dtype=torch.int32, device=device)
+    l3, d3, v3, _, _ = nat.ppo_loss(logits, value, mb.offs, mb.order, inv, sample_index, actions, lp_full, adv, ret,
+                                    clip, vf, ent_coef, grad_absmax=gm)
+    assert torch.equal(l3, l1) and torch.equal(d3, d1) and torch.equal(v3, v1)
+    want = torch.zeros(9, dtype=torch.float32, device=device)
+    want[:A] = d1.abs().amax(0)
+    want[8] = v1.abs().amax()
+    assert torch.equal(gm.view(torch.float32), want)
 
 
 def test_ppo_loss_bad_action_is_nan(device):
