@@ -238,11 +238,20 @@ def x6_standalone(torch, U, device, impl="h3", reps=10):
     Wt = W.transpose(1, 2).contiguous()
     b = torch.zeros(2, 512, device=device)
     if impl == "h3":
+        from merlin import fast_step as FS
+
         am3, amz, amW = nat.h3_amax(a3), nat.h3_amax(dz), nat.h3_amax(W)
         Wp, Wtp = nat.h3_split(W, amW), nat.h3_split(Wt, amW)
-        runs = {"gemm_fc1_fwd": lambda: nat.h3_gemm_nt(a3, am3, Wp, amW, bias=b, cfg=nat.H3_NT_CFG["fwd"]),
-                "gemm_fc1_dgrad": lambda: nat.h3_gemm_nt(dz, amz, Wtp, amW, cfg=nat.H3_NT_CFG["dgrad"]),
-                "gemm_wgrad": lambda: nat.h3_gemm_tn(dz, amz, a3, am3)}
+        # the update's forms: a3 read through a row map (here the identity), dz as planes (DZ_PLANES: the
+        # plane-operand input gradient, the weight gradient staging dz's planes as copies)
+        rows = torch.arange(U * 9, dtype=torch.int32, device=device)
+        dzo = nat.h3_split(dz, amz) if FS.DZ_PLANES else dz
+        dgrad = ((lambda: nat.h3_gemm_nt_planes(dzo, amz, Wtp, amW, cfg=nat.H3_NT_CFG["dgrad_planes"]))
+                 if FS.DZ_PLANES else (lambda: nat.h3_gemm_nt(dz, amz, Wtp, amW, cfg=nat.H3_NT_CFG["dgrad"])))
+        runs = {"gemm_fc1_fwd": lambda: nat.h3_gemm_nt(a3, am3, Wp, amW, bias=b, cfg=nat.H3_NT_CFG["fwd"],
+                                                       rows=rows),
+                "gemm_fc1_dgrad": dgrad,
+                "gemm_wgrad": lambda: nat.h3_gemm_tn(dzo, amz, a3, am3, rows=rows)}
     else:
         Wp, Wtp = nat.x6_split(W), nat.x6_split(Wt)
         runs = {"gemm_fc1_fwd": lambda: nat.x6_gemm_nt(a3, Wp, bias=b, cfg=nat.X6_NT_CFG["fwd"]),
@@ -325,6 +334,10 @@ def h3_gemm_names(nat):
     heads = nat.H3_HEADS_EPILOGUE and nat.lib().merlin_h3_heads_parts(512, nat.H3_NT_CFG["fwd"]) > 0
     fwd = H3_NT_NAMES.get(nat.H3_NT_CFG["fwd"], "?").format(2 if heads else 1)  # EPI 2: the heads in the epilogue
     out = {"gemm_fc1_dgrad": (H3_NT_NAMES.get(nat.H3_NT_CFG["dgrad"], "?").format(0),)}
+    dzp = FS.DZ_PLANES and FS.PATCH_REUSE == "gather"
+    if dzp:  # dz leaves the heads' backward as planes: the input gradient on the plane-operand DMA kernel (cfg 62)
+        out["gemm_fc1_dgrad"] = ("k_h3_pq<128, 192, 4, 2, 0, 16>",)
+    out["k_head_bwd"] = (f"k_head_bwd<3, {'true' if dzp else 'false'}>", "k_head_fold")
     if heads:
         out["k_heads_fwd"] = ("k_heads_combine",)
     if nat.H3_HEADS_EPILOGUE and nat.lib().merlin_h3_heads_parts(512, nat.H3_NT_CFG["rollout"]) > 0:
@@ -332,7 +345,10 @@ def h3_gemm_names(nat):
         out["gemm_rollout_fc1"] = (H3_NT_NAMES.get(nat.H3_NT_CFG["rollout"], "?").format(3),)
         out["k_act_heads"] = ("k_act_draw",)
     if FS.PATCH_REUSE == "gather":
-        return {**out, **PMC_ALIAS_GATHER, "gemm_fc1_fwd": (fwd.replace("k_h3_ntp<", "k_h3_ntpg<"),)}
+        a3p = dzp and FS.A3_PLANES
+        wg = f"k_h3_tng<128, 192, 4, 2, {'true' if dzp else 'false'}, {'true' if a3p else 'false'}>"
+        return {**out, **PMC_ALIAS_GATHER, "gemm_wgrad": (wg, "k_x6_fold"),
+                "gemm_fc1_fwd": (fwd.replace("k_h3_ntp<", "k_h3_ntpg<").replace(">", ", true>" if a3p else ", false>"),)}
     return {**out, "gemm_fc1_fwd": (fwd,)}
 PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 

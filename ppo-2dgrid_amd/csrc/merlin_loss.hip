@@ -26,7 +26,9 @@ constexpr int NSUM = NSTAT + MAXA + 1;  // + the heads' bias gradients (sum of e
 
 // atomicMax of the block's maxima m[j] (float bits of non-negative values) into dmax[j], j < A and j = MAXA; every
 // thread of the 256-thread block calls it
-__device__ __forceinline__ void block_max9(const uint32_t (&m)[MAXA + 1], int A, uint32_t *__restrict__ dmax) {
+// (atomic false: stored to dmax[j] instead, every j <= MAXA)
+__device__ __forceinline__ void block_max9(const uint32_t (&m)[MAXA + 1], int A, uint32_t *__restrict__ dmax,
+                                           bool atomic = true) {
     __shared__ uint32_t red9[MAXA + 1][4];
 #pragma unroll
     for (int j = 0; j <= MAXA; j++) {
@@ -35,10 +37,13 @@ __device__ __forceinline__ void block_max9(const uint32_t (&m)[MAXA + 1], int A,
         if ((threadIdx.x & 63) == 0) red9[j][threadIdx.x >> 6] = x;
     }
     __syncthreads();
-    if (threadIdx.x <= MAXA && (threadIdx.x < (unsigned)A || threadIdx.x == MAXA)) {
+    if (threadIdx.x <= MAXA) {
         const uint32_t *r = red9[threadIdx.x];
         const uint32_t x = max(max(r[0], r[1]), max(r[2], r[3]));
-        if (x && x > __hip_atomic_load(dmax + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        if (!atomic)
+            dmax[threadIdx.x] = x;
+        else if ((threadIdx.x < (unsigned)A || threadIdx.x == MAXA) && x &&
+                 x > __hip_atomic_load(dmax + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
             atomicMax(dmax + threadIdx.x, x);
     }
 }
@@ -65,7 +70,7 @@ __global__ __launch_bounds__(LOSS_BLK) void k_ppo_loss(const float *__restrict__
                                                        float clip, float vf2_n, float ent_n, float inv_n,
                                                        float *__restrict__ dlogits, float *__restrict__ dvalue,
                                                        float *__restrict__ carry, double *__restrict__ partial,
-                                                       uint32_t *__restrict__ dmax) {
+                                                       uint32_t *__restrict__ bmax) {
     __shared__ double red[NSUM][LOSS_BLK];
     const int lane = threadIdx.x & 63;
     const int64_t item = (int64_t)blockIdx.x * LOSS_WAVES + (threadIdx.x >> 6);
@@ -164,12 +169,13 @@ __global__ __launch_bounds__(LOSS_BLK) void k_ppo_loss(const float *__restrict__
             dvalue[u] = g[MAXA];
         }
     }
-    if (dmax) {  // block-uniform: max |.| of the frames this block finished (the spanning ones: k_ppo_loss_fix)
+    if (bmax) {  // block-uniform: max |.| of the frames this block finished (the spanning ones: k_ppo_loss_fix),
+                 // stored per block (same-address atomics from every block serialised: +9 us per launch)
         uint32_t m[MAXA + 1];
         const bool fin = last && offs[u] >= item * 64 && offs[u + 1] <= item * 64 + 64;
 #pragma unroll
         for (int j = 0; j <= MAXA; j++) m[j] = fin ? __float_as_uint(g[j]) & 0x7fffffffu : 0u;
-        block_max9(m, A, dmax);
+        block_max9(m, A, bmax + (size_t)blockIdx.x * (MAXA + 1), false);
     }
 #pragma unroll
     for (int q = 0; q < NSUM; q++) red[q][threadIdx.x] = st[q];
@@ -190,11 +196,12 @@ __device__ void loss_fix_frame(const int32_t *__restrict__ offs, int64_t u, int 
 // frames whose samples span items j0 < j1: carry[j0][1] + sum_{j0 < j <= j1} carry[j][0].
 // dmax (nullable, zeroed by the caller): dmax[j] = max over the frames of |dlogits[u][j]| (j < A) and dmax[MAXA] =
 // max |dvalue[u]|, as float bits (atomicMax of non-negative floats) -- the bound merlin_head.hip's k_head_bwd
-// derives dz's plane scale from, so that it can write dz as h3 planes in its one pass.  k_ppo_loss takes the
-// maximum over the frames it finishes, this kernel over the frames that span items.
+// derives dz's plane scale from, so that it can write dz as h3 planes in its one pass.  k_ppo_loss leaves the
+// maxima over the frames each block finishes (bmax, nbmax blocks), this kernel adds the frames that span items.
 __global__ __launch_bounds__(256) void k_ppo_loss_fix(const int32_t *__restrict__ offs, int64_t U, int A,
                                                       const float *__restrict__ carry, float *__restrict__ dlogits,
-                                                      float *__restrict__ dvalue, uint32_t *__restrict__ dmax) {
+                                                      float *__restrict__ dvalue, uint32_t *__restrict__ dmax,
+                                                      const uint32_t *__restrict__ bmax, int64_t nbmax) {
     const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (!dmax) {
         if (u < U) loss_fix_frame(offs, u, A, carry, dlogits, dvalue, nullptr);
@@ -207,6 +214,10 @@ __global__ __launch_bounds__(256) void k_ppo_loss_fix(const int32_t *__restrict_
 #pragma unroll
         for (int j = 0; j <= MAXA; j++) m[j] = 0u;
     }
+    if (blockIdx.x == 0)  // k_ppo_loss's per-block maxima, folded in by this block's threads
+        for (int64_t b = threadIdx.x; b < nbmax; b += 256)
+#pragma unroll
+            for (int j = 0; j <= MAXA; j++) m[j] = max(m[j], bmax[b * (MAXA + 1) + j]);
     block_max9(m, A, dmax);
 }
 
@@ -300,7 +311,8 @@ __global__ __launch_bounds__(256) void k_ppo_loss_final(const double *__restrict
 
 int64_t ppo_loss_workspace_doubles(int64_t n) {
     const int64_t items = (n + 63) / 64, blocks = (items + LOSS_WAVES - 1) / LOSS_WAVES;
-    return blocks * NSUM + (items * 2 * (MAXA + 1) + 1) / 2;  // block partials + f32 carries
+    // block partials + f32 carries + the blocks' |gradient| maxima (u32)
+    return blocks * NSUM + (items * 2 * (MAXA + 1) + 1) / 2 + (blocks * (MAXA + 1) + 1) / 2;
 }
 
 hipError_t launch_ppo_loss(const float *logits, const float *value, const float *bias_a, const float *bias_c,
@@ -313,16 +325,18 @@ hipError_t launch_ppo_loss(const float *logits, const float *value, const float 
     const double inv_n = n > 0 ? 1.0 / (double)n : 0.0;
     double *partial = workspace;
     float *carry = reinterpret_cast<float *>(workspace + nblk * NSUM);
+    uint32_t *bmax = dmax ? reinterpret_cast<uint32_t *>(workspace + nblk * NSUM + (items * 2 * (MAXA + 1) + 1) / 2)
+                          : nullptr;
     if (nblk > 0) {
         hipLaunchKernelGGL(k_ppo_loss, dim3((unsigned)nblk), dim3(LOSS_BLK), 0, s, logits, value, bias_a, bias_c, A, offs,
                            order, inv, n,
                            sample_index, actions, lp_old, adv, ret, (float)(1.0 - clip_eps), (float)(1.0 + clip_eps),
                            (float)clip_eps, (float)(2.0 * vf_coef * inv_n), (float)(ent_coef * inv_n),
-                           (float)inv_n, dlogits, dvalue, carry, partial, dmax);
+                           (float)inv_n, dlogits, dvalue, carry, partial, bmax);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_ppo_loss_fix, dim3((unsigned)((U + 255) / 256)), dim3(256), 0, s, offs, U, A, carry,
-                           dlogits, dvalue, dmax);
+                           dlogits, dvalue, dmax, bmax, nblk);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

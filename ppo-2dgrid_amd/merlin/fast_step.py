@@ -222,8 +222,11 @@ DZ_PLANES = True
 # with DZ_PLANES: conv3's representative rows leave k_window_conv3_reps as h3 planes too, scaled by a bound on max Y3
 # from Q's column maxima (merlin_tower_window_conv3_planes), so the forward GEMM stages a3 as copies
 # (merlin_h3_gemm_nt_heads_planes) and the weight gradient runs on both operands' planes
-# (merlin_h3_gemm_tn_gather_planes).  False: a3 in fp32, split by the GEMMs.
-A3_PLANES = True
+# (merlin_h3_gemm_tn_gather_planes).  False: a3 in fp32, split by the GEMMs.  Off: kernel traces of one setting per
+# process (scripts/update_timeline.py, profiles/r05n_*_timeline.txt) show the copy-staged forward no faster in the
+# loop (414 vs 400-420 us), the weight gradient on both planes 732 vs 716 us and conv3's patch sums (R) beside it 223
+# vs 192 us, +32 us of main-queue time per step; scripts/ab_update.py one setting per process: 172.5 vs 169.9 ms
+A3_PLANES = False
 
 
 class WindowStep:
