@@ -189,6 +189,10 @@ class WeightStage:
 WGRAD_EARLY = False
 WGRAD_SIDE = True  # False: the weight gradient on the main stream (diagnostics)
 SIDE_PRIORITY = 0  # the side stream's priority (torch.cuda.Stream priority: lower = higher priority)
+# < 0: the step's main-stream kernels on a stream of that (higher) priority, so that conv3's backward chain gets CUs
+# ahead of the side-stream weight gradient.  Off: on the high-priority queue every small kernel took 4-6x longer
+# (k_zero_fill 44 vs 8 us, k_colsum 50 vs 7), 286 vs 168 ms per update (profiles/r05n_fast_mainhi_timeline.txt)
+MAIN_PRIORITY = 0
 # h3: the window GEMMs (conv3's Q = a2w W3r and its two backward products, ~6.6k rows) on the f16 two-plane kernels
 # too (False: hipBLASLt's fp32 GEMMs, the split-K weight gradient and its torch sum).  Off: with their operand scales
 # (two reductions per step) they measured 200.8 vs 199.5 ms per update (scripts/ab_update.py 4 6 fast,fast_nowh3,
@@ -292,6 +296,20 @@ class WindowStep:
     def step(self, plan, mb, mb_idx, actions, logp_old, adv, ret, totals):
         """Forward, loss (statistics added to `totals`), backward of one minibatch: every parameter's gradient
         is left in its .grad view (the optimizer step follows in PPO._sgd)."""
+        if MAIN_PRIORITY >= 0:
+            return self._step(plan, mb, mb_idx, actions, logp_old, adv, ret, totals)
+        # the step's main-stream work on a high-priority stream, so that conv3's backward chain gets CUs ahead of the
+        # side stream's weight gradient when both are queued (torch's default stream has the lowest priority)
+        cur = torch.cuda.current_stream()
+        hp = getattr(self, "_hi", None)
+        if hp is None:
+            hp = self._hi = torch.cuda.Stream(device=cur.device, priority=MAIN_PRIORITY)
+        hp.wait_stream(cur)
+        with torch.cuda.stream(hp):
+            self._step(plan, mb, mb_idx, actions, logp_old, adv, ret, totals)
+        cur.wait_stream(hp)
+
+    def _step(self, plan, mb, mb_idx, actions, logp_old, adv, ret, totals):
         ag = self._agent()
         Wa, ba, Wc, bc = self.head
         g = self.stage.grads  # (dT2, db2, dW3r, db3, dW4p, db4)
