@@ -246,12 +246,17 @@ def x6_standalone(torch, U, device, impl="h3", reps=10):
         # plane-operand input gradient, the weight gradient staging dz's planes as copies)
         rows = torch.arange(U * 9, dtype=torch.int32, device=device)
         dzo = nat.h3_split(dz, amz) if FS.DZ_PLANES else dz
+        a3p = FS.DZ_PLANES and FS.A3_PLANES  # a3 as planes too: the forward stages copies, the LDS-DMA TN
+        a3o = nat.h3_split(a3, am3) if a3p else a3
+        Wa = torch.randn(3, 512, device=device, generator=g) / 24
+        Wc = torch.randn(1, 512, device=device, generator=g) / 24
         dgrad = ((lambda: nat.h3_gemm_nt_planes(dzo, amz, Wtp, amW, cfg=nat.H3_NT_CFG["dgrad_planes"]))
                  if FS.DZ_PLANES else (lambda: nat.h3_gemm_nt(dz, amz, Wtp, amW, cfg=nat.H3_NT_CFG["dgrad"])))
-        runs = {"gemm_fc1_fwd": lambda: nat.h3_gemm_nt(a3, am3, Wp, amW, bias=b, cfg=nat.H3_NT_CFG["fwd"],
-                                                       rows=rows),
+        runs = {"gemm_fc1_fwd": lambda: nat.h3_gemm_nt_heads(a3o, am3, Wp, amW, b, Wa, Wc, cfg=nat.H3_NT_CFG["fwd"],
+                                                             rows=rows),
                 "gemm_fc1_dgrad": dgrad,
-                "gemm_wgrad": lambda: nat.h3_gemm_tn(dzo, amz, a3, am3, rows=rows)}
+                "gemm_wgrad": lambda: nat.h3_gemm_tn(dzo, amz, a3o, am3, rows=rows,
+                                                     cfg=nat.H3_TN_CFG_PLANES if a3p else None)}
     else:
         Wp, Wtp = nat.x6_split(W), nat.x6_split(Wt)
         runs = {"gemm_fc1_fwd": lambda: nat.x6_gemm_nt(a3, Wp, bias=b, cfg=nat.X6_NT_CFG["fwd"]),
@@ -346,7 +351,8 @@ def h3_gemm_names(nat):
         out["k_act_heads"] = ("k_act_draw",)
     if FS.PATCH_REUSE == "gather":
         a3p = dzp and FS.A3_PLANES
-        wg = f"k_h3_tng<128, 192, 4, 2, {'true' if dzp else 'false'}, {'true' if a3p else 'false'}>"
+        wg = (f"k_h3_tq<128, 192, 4, 2>" if a3p and nat.H3_TN_CFG_PLANES == 20 else
+              f"k_h3_tng<128, 192, 4, 2, {'true' if dzp else 'false'}, {'true' if a3p else 'false'}>")
         return {**out, **PMC_ALIAS_GATHER, "gemm_wgrad": (wg, "k_x6_fold"),
                 "gemm_fc1_fwd": (fwd.replace("k_h3_ntp<", "k_h3_ntpg<").replace(">", ", true>" if a3p else ", false>"),)}
     return {**out, "gemm_fc1_fwd": (fwd,)}

@@ -37,7 +37,6 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr int BK = 32;           // k per step
-constexpr float LO_SCALE = 2048.0f;
 constexpr float LO_INV = 1.0f / 2048.0f;
 
 __device__ __forceinline__ f32x16 mfma16(const u32x4 a, const u32x4 b, f32x16 c) {
@@ -1702,6 +1701,13 @@ hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B
     }
     int S = 1;
     hipError_t e;
+    if (cfg == 20) {  // both operands as planes, B gathered, LDS-DMA staged (merlin_h3p.hip k_h3_tq)
+        if (!(a_planes && b_planes)) return hipErrorInvalidValue;
+        e = launch_h3p_gemm_tn_gather(A, amaxA, B, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, b_rows, cfg,
+                                      &S, s);
+        if (e != hipSuccess) return e;
+        return launch_x6_fold(slab, S, total, out, s);
+    }
 #define H3_TN(BM, BN, WM, WN, PIPE)                                                                              \
     (planes ? tn_launch<BM, BN, WM, WN, 1>(A, B, amaxA, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, &S,   \
                                            b_rows, s)                                                              \

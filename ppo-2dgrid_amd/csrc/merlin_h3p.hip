@@ -254,6 +254,250 @@ hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const 
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// TN over plane operands with LDS-DMA staging (round 5; the weight gradient dz^T a3, merlin_h3_gemm_tn_gather_planes
+// with cfg 20): slab[s][t][m][n] = sum over the split's rows k of A[t][k][m] B[t][k][n], A planes [Kd][M/8][2][8]
+// (k_head_bwd's dz), B planes gathered by 64-column chunks (row k's chunk j is row bmap[k * N / 64 + j] of B seen
+// as [*][64]: conv3's representatives).  The LDS images are k_h3_tn's -- per operand and plane [32 k rows][RC chunks
+// of 8 columns], chunk c of row r at c ^ swz(r), fragments k-contiguous through ds_read_b64_tr_b16 -- but filled by
+// DMA three k steps deep: a DMA writes its 64 lanes' 16-B chunks lane-linear, so each lane's source is the chunk
+// whose image slot that is (the swizzle and the plane deinterleave are in the source addresses).  B's chunk rows
+// come from bmap through a 3-slot LDS ring, itself filled by DMA four steps ahead, so the data DMA's addresses need
+// no global load in the loop.  Rows past the split's end read a zero chunk; a split's step count is padded to a
+// multiple of three (the ring's period: compile-time stages) with such steps.
+// The DMAs are inline asm (s_mov_b32 m0 + global_load_lds_*): issued through the builtin, hipcc treats every LDS read
+// that follows as possibly aliasing an in-flight DMA and waits vmcnt(0) before the first fragment read of each step
+// (profiles/r05 .s of the first version), which serialises the pipeline; here the waits are all explicit: vmcnt
+// counts this wave's DMAs in issue order and the barrier after each wait publishes every wave's.
+// Same products in the same order as k_h3_tn / k_h3_tng: the same bits.
+__device__ uint4 p_zero16[1] = {{0u, 0u, 0u, 0u}};
+
+__device__ __forceinline__ void p_dma16(const void *src, uint32_t lds) {  // lds: wave-uniform byte address
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void p_dma4(const void *src, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds) : "memory");
+}
+
+template <int RC>
+__device__ __forceinline__ int p_tr_swz(int row) {
+    static_assert(RC % 16 == 0 || RC == 24, "row chunks");
+    return RC % 16 == 0 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
+}
+typedef __bf16 p_bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 p_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) p_bf16x4 lds_p_bf16x4;
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tq(const p_u32x4 *__restrict__ A, const p_u32x4 *__restrict__ B,
+                                                          const uint32_t *__restrict__ amaxA,
+                                                          const uint32_t *__restrict__ amaxB, int64_t Kd, int M,
+                                                          int N, int64_t sA, int64_t sB, int64_t kc, int tiles_n,
+                                                          int tiles, int S, float *__restrict__ slab,
+                                                          const int32_t *__restrict__ bmap) {
+    constexpr int NT = 64 * WGM * WGN, NW = NT / 64;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int RCA = BM / 8, RCB = BN / 8;
+    constexpr int PSA = 32 * RCA, PSB = 32 * RCB;  // chunks per plane image
+    constexpr int STG = 2 * (PSA + PSB);
+    constexpr uint32_t STG_B = STG * 16;
+    static_assert((2 * PSA) % NT == 0 && (2 * PSB) % NT == 0, "whole DMA instructions per operand");
+    constexpr int GA = 2 * PSA / NT, GB = 2 * PSB / NT, G = GA + GB + 1;  // + the index DMA
+    constexpr int JB = BN / 64;   // 64-column chunks of B per tile (bmap entries per row)
+    constexpr int XS = 64 * NW;   // index ring slot (ints; 32 * JB used)
+    static_assert(32 * JB <= XS, "index slot");
+    constexpr int NF = 2 * (TM + TN);             // fragments per half step (tiles x planes)
+    constexpr int NR = 2 * NF, NM = 3 * TM * TN;  // tr reads (two per fragment) / MFMAs per half step
+    __shared__ p_u32x4 lds[3 * STG];
+    __shared__ int32_t ixr[3 * XS];
+
+    const int P = p_xcd_tile(blockIdx.x, gridDim.x);
+    const int t = P / (S * tiles), s = (P / tiles) % S, Lt = P % tiles;
+    const int tm = Lt / tiles_n, tn = Lt - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int64_t k0 = (int64_t)s * kc, k1 = std::min<int64_t>(Kd, k0 + kc);
+    const int eA = p_exp(p_amax(amaxA + t)), eB = p_exp(p_amax(amaxB + t));
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+    const int nc = N / 64, j0 = n0 / 64;
+    const int64_t rowA = M / 4;  // chunks per A row
+    const p_u32x4 *At = A + t * sA, *Bt = B + t * sB;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) p_u32x4 *)lds;
+    const uint32_t ix0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t *)ixr;
+    const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane(w) * 64u;  // the wave's first slot
+
+    // the thread's DMA slots: A (instructions 0 .. GA-1): row ra, chunk offset oa; B: row rb, ring entry xb, offset gp
+    int ra[GA], rb[GB], xb[GB];
+    uint32_t oa[GA], gp[GB];
+#pragma unroll
+    for (int i = 0; i < GA; i++) {
+        const int q = i * NT + tid, p = q / PSA, rem = q - p * PSA, r = rem / RCA, cs = rem - r * RCA;
+        const int c = cs ^ p_tr_swz<RCA>(r);
+        ra[i] = r;
+        oa[i] = (uint32_t)((m0 / 8 + c) * 2 + p);
+    }
+#pragma unroll
+    for (int i = 0; i < GB; i++) {
+        const int q = (GA + i) * NT + tid - 2 * PSA, p = q / PSB, rem = q - p * PSB, r = rem / RCB,
+                  cs = rem - r * RCB;
+        const int c = cs ^ p_tr_swz<RCB>(r), col = 8 * c;
+        rb[i] = r;
+        xb[i] = r * JB + (col >> 6);
+        gp[i] = (uint32_t)(((col & 63) >> 3) * 2 + p);
+    }
+    // the index DMA: this thread's ring entry e = tid (< 32 JB used): row e / JB, chunk j0 + e % JB
+    const int xr = tid / JB, xj = j0 + tid % JB;
+    const int64_t nk = (k1 - k0 + 31) / 32, nk3 = (nk + 2) / 3 * 3;
+
+    auto issue_ix = [&](int64_t kt, int slot) __attribute__((always_inline)) {
+        const int64_t row = std::min<int64_t>(k0 + kt * 32 + (tid < 32 * JB ? xr : 0), k1 - 1);
+        p_dma4(bmap + row * nc + (tid < 32 * JB ? xj : j0), ix0 + (uint32_t)(slot * XS) * 4u + wbase * 4u);
+    };
+    // this thread's chunk rows of a step from its index slot (read a step before they are used)
+    auto read_ix = [&](int slot, int32_t (&x)[GB]) __attribute__((always_inline)) {
+        const lds_i32 *xs = (const lds_i32 *)(uintptr_t)(ix0 + (uint32_t)(slot * XS) * 4u);
+#pragma unroll
+        for (int i = 0; i < GB; i++) x[i] = xs[xb[i]];
+    };
+    auto issue = [&](int64_t kt, int st, const int32_t (&x)[GB]) __attribute__((always_inline)) {
+        const uint32_t base = lds0 + (uint32_t)(st * STG) * 16u + wbase * 16u;
+        const int64_t kk = k0 + kt * 32;
+        const bool full = kk + 32 <= k1;  // block-uniform
+#pragma unroll
+        for (int i = 0; i < GA; i++) {
+            const p_u32x4 *src = full || kk + ra[i] < k1 ? At + (kk + ra[i]) * rowA + oa[i]
+                                                          : reinterpret_cast<const p_u32x4 *>(p_zero16);
+            p_dma16(src, base + (uint32_t)(i * NT) * 16u);
+        }
+#pragma unroll
+        for (int i = 0; i < GB; i++) {
+            const p_u32x4 *src = full || kk + rb[i] < k1 ? Bt + (int64_t)x[i] * 16 + gp[i]
+                                                          : reinterpret_cast<const p_u32x4 *>(p_zero16);
+            p_dma16(src, base + (uint32_t)((GA + i) * NT) * 16u);
+        }
+    };
+
+    // fragment reads: fragment f < NF (A tiles x planes, then B tiles x planes), its two transposed halves
+    const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+    struct Frag {
+        p_bf16x4 v[NF][2];
+    };
+    auto rd = [&](Frag &g, auto K_, uint32_t so, auto KH) __attribute__((always_inline)) {
+        constexpr int k = decltype(K_)::value, kh = decltype(KH)::value, f = k >> 1, h2 = k & 1;
+        constexpr bool isA = f < 2 * TM;
+        constexpr int tile = isA ? f >> 1 : (f - 2 * TM) >> 1, pl = f & 1;
+        constexpr int RC = isA ? RCA : RCB;
+        const int col0 = isA ? wm * WTM + tile * 32 : wn * WTN + tile * 32;
+        const uint32_t img = lds0 + so + (uint32_t)(isA ? pl * PSA : 2 * PSA + pl * PSB) * 16u;
+        const int chunk = ((col0 + 16 * (fg & 1)) >> 3) + (fp >> 1);
+        const int row = 16 * kh + 8 * (fg >> 1) + 4 * h2 + fq;
+        const uint32_t off = img + (uint32_t)((row * RC + (chunk ^ p_tr_swz<RC>(row))) * 16 + (fp & 1) * 8);
+        g.v[f][h2] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_p_bf16x4 *)(uintptr_t)off);
+    };
+    auto frag = [](const Frag &g, int f) __attribute__((always_inline)) {
+        return __builtin_bit_cast(p_u32x4, p_bf16x8{g.v[f][0][0], g.v[f][0][1], g.v[f][0][2], g.v[f][0][3],
+                                                   g.v[f][1][0], g.v[f][1][1], g.v[f][1][2], g.v[f][1][3]});
+    };
+    p_f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = p_f32x16{};
+            lo[i][j] = p_f32x16{};
+        }
+    // MFMA m of a half step: tile (i, j) = (m / (3 TN), (m / 3) % TN), product m % 3 (k_h3_tn's order per tile)
+    auto mf = [&](const Frag &f, auto M_) __attribute__((always_inline)) {
+        constexpr int m = decltype(M_)::value, i = m / (3 * TN), j = (m / 3) % TN, pr = m % 3;
+        constexpr int fa0 = 2 * i, fa1 = 2 * i + 1, fb0 = 2 * TM + 2 * j, fb1 = 2 * TM + 2 * j + 1;
+        if constexpr (pr == 0)
+            lo[i][j] = p_mfma(frag(f, fa1), frag(f, fb0), lo[i][j]);
+        else if constexpr (pr == 1)
+            lo[i][j] = p_mfma(frag(f, fa0), frag(f, fb1), lo[i][j]);
+        else
+            hi[i][j] = p_mfma(frag(f, fa0), frag(f, fb0), hi[i][j]);
+    };
+    constexpr int RPM = (NR + NM - 1) / NM;  // reads behind each MFMA
+    auto half = [&](const Frag &f, Frag &g, uint32_t so, auto KH) __attribute__((always_inline)) {
+        static_for<NM>([&](auto M_) __attribute__((always_inline)) {
+            mf(f, M_);
+            static_for<RPM>([&](auto R_) __attribute__((always_inline)) {
+                constexpr int k = decltype(M_)::value * RPM + decltype(R_)::value;
+                if constexpr (k < NR) rd(g, IC<k>{}, so, KH);
+            });
+        });
+        static_for<NM>([&](auto M_) __attribute__((always_inline)) {
+            constexpr int left = NR - decltype(M_)::value * RPM;
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if constexpr (left > 0) __builtin_amdgcn_sched_group_barrier(0x100, left < RPM ? left : RPM, 0);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto touch = [&](const Frag &f) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < NF; q++) asm volatile("" ::"v"(f.v[q][0]), "v"(f.v[q][1]));
+    };
+    auto publish = [&](auto CNT) __attribute__((always_inline)) {  // this wave's DMAs but the last CNT landed, then
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(CNT)::value) : "memory");  // every wave's
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: indices of steps 0..2 (slot = step % 3); DMA of steps 0 and 1; once every wave has read slot 0, the
+    // indices of step 3 into it
+    int32_t x0[GB], x1[GB], x2[GB];  // chunk rows of the steps issued next (step k's in x[k % 3])
+    issue_ix(0, 0);
+    issue_ix(1, 1);
+    issue_ix(2, 2);
+    publish(IC<0>{});
+    read_ix(0, x0);
+    read_ix(1, x1);
+    read_ix(2, x2);
+    issue(0, 0, x0);
+    issue(1, 1, x1);
+    publish(IC<G - 1>{});  // DMA 0 landed (DMA 1 may not); every wave has read slots 0 .. 2
+    issue_ix(3, 0);
+    Frag f0, f1;
+    static_for<NR>([&](auto K_) __attribute__((always_inline)) { rd(f0, K_, 0u, IC<0>{}); });
+    // step kt (stage st = kt % 3): the indices of kt + 4 (slot (kt + 1) % 3, last read at step kt - 1), the DMA of
+    // kt + 2 (stage (kt + 2) % 3, its chunk rows read a step ago), half 0, publish kt + 1 (the two DMA groups just
+    // issued may stay in flight; the indices of kt + 3 have landed), read those, half 1
+    auto step = [&](int64_t kt, auto ST, int32_t (&xu)[GB], int32_t (&xn)[GB]) __attribute__((always_inline)) {
+        constexpr int st = decltype(ST)::value, sn = (st + 1) % 3, s2 = (st + 2) % 3;
+        issue_ix(kt + 4, sn);
+        issue(kt + 2, s2, xu);
+        __builtin_amdgcn_sched_barrier(0);
+        half(f0, f1, (uint32_t)st * STG_B, IC<1>{});
+        touch(f1);
+        publish(IC<G>{});
+        read_ix(st, xn);  // slot st = (kt + 3) % 3
+        half(f1, f0, (uint32_t)sn * STG_B, IC<0>{});
+    };
+    for (int64_t kt = 0; kt < nk3; kt += 3) {
+        step(kt, IC<0>{}, x2, x0);
+        step(kt + 1, IC<1>{}, x0, x1);
+        step(kt + 2, IC<2>{}, x1, x2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the padded steps' DMAs drained before the block ends
+
+    const float inv = p_pow2(-eA), invB = p_pow2(-eB);
+    float *St = slab + ((int64_t)s * (gridDim.x / (S * tiles)) + t) * (int64_t)M * N;
+    const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                St[(int64_t)row * N + n0 + wn * WTN + j * 32 + fr] = (hi[i][j][r] + lo[i][j][r] * P_LO_INV) * inv * invB;
+            }
+}
+
 }  // namespace
 
 // A, B: plane images (4 B per value, strides in values); cfg 60: 128 x 256 tiles (2 x 4 waves), 61: 256 x 128 (4 x 2),
@@ -269,6 +513,26 @@ hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *
         case 62: return pq_launch<128, 192, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+
+// the weight gradient over plane operands with B's rows gathered (cfg 20: 128 x 192 tiles, 4 x 2 waves); slab as
+// merlin_h3_gemm_tn's (S slabs of [T][M][N], summed in order by the caller's fold); strides in values
+hipError_t launch_h3p_gemm_tn_gather(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB,
+                                     int64_t Kd, int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits,
+                                     float *slab, const int32_t *b_rows, int cfg, int *S_out, hipStream_t s) {
+    constexpr int BM = 128, BN = 192, BK = 32;
+    if (cfg != 20 || M % BM || N % BN || N % 64 || a_stride % 4 || b_stride % 4 || !b_rows) return hipErrorInvalidValue;
+    const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
+    int S = std::max(1, splits);
+    int64_t kc = (Kd + S - 1) / S;
+    kc = (kc + BK - 1) / BK * BK;
+    S = (int)std::max<int64_t>(1, (Kd + kc - 1) / kc);
+    *S_out = S;
+    hipLaunchKernelGGL((k_h3_tq<BM, BN, 4, 2>), dim3(tiles * S * T), dim3(512), 0, s, static_cast<const p_u32x4 *>(A),
+                       static_cast<const p_u32x4 *>(B), amaxA, amaxB, Kd, M, N, a_stride / 4, b_stride / 4, kc,
+                       tiles_n, tiles, S, slab, b_rows);
+    return hipGetLastError();
 }
 
 }  // namespace merlin

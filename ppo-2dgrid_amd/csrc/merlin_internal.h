@@ -192,6 +192,9 @@ hipError_t launch_group_act(const uint32_t *codes, int G, const float *T2, const
 hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                               int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
                               int64_t c_stride, int cfg, hipStream_t s);
+hipError_t launch_h3p_gemm_tn_gather(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB,
+                                     int64_t Kd, int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits,
+                                     float *slab, const int32_t *b_rows, int cfg, int *S_out, hipStream_t s);
 hipError_t launch_env_reset(const EnvDev &E, const uint8_t *mask, uint32_t *obs, hipStream_t s);
 hipError_t launch_env_step(const EnvDev &E, const StepOut &O, bool refill, hipStream_t s);
 hipError_t launch_env_full_obs(const EnvDev &E, uint8_t *out, hipStream_t s);

@@ -1084,6 +1084,7 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
 # profiles keep the two apart); qwin / qwin_dgrad: the update's window GEMMs (N = 576, K = 64 / N = 64, K = 576)
 H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 1, "qwin": 11, "qwin_dgrad": 5, "dgrad_planes": 62}
 H3_TN_CFG = 0
+H3_TN_CFG_PLANES = 20  # the weight gradient over both operands' planes: the LDS-DMA TN (merlin_h3p.hip k_h3_tq)
 # the update's fc1 forward (h3, cfg "fwd" with a heads epilogue) computes the policy / value heads in its epilogue
 # (merlin_h3_gemm_nt_heads + merlin_heads_combine) instead of a pass over h (merlin_heads_fwd)
 H3_HEADS_EPILOGUE = True

@@ -223,14 +223,16 @@ MASK_ROWS = True
 # (merlin_h3_gemm_nt_planes, LDS-DMA staged, cfg H3_NT_CFG["dgrad_planes"]) and the weight gradient stages dz's
 # planes as copies (merlin_h3_gemm_tn_gather_planes_a).  False: dz in fp32, split by the GEMMs.
 DZ_PLANES = True
+# conv3's backward chain's fills made before the side-stream weight gradient starts (_conv3_backward_prefill)
+PREFILL = True
 # with DZ_PLANES: conv3's representative rows leave k_window_conv3_reps as h3 planes too, scaled by a bound on max Y3
 # from Q's column maxima (merlin_tower_window_conv3_planes), so the forward GEMM stages a3 as copies
 # (merlin_h3_gemm_nt_heads_planes) and the weight gradient runs on both operands' planes
-# (merlin_h3_gemm_tn_gather_planes).  False: a3 in fp32, split by the GEMMs.  Off: kernel traces of one setting per
-# process (scripts/update_timeline.py, profiles/r05n_*_timeline.txt) show the copy-staged forward no faster in the
-# loop (414 vs 400-420 us), the weight gradient on both planes 732 vs 716 us and conv3's patch sums (R) beside it 223
-# vs 192 us, +32 us of main-queue time per step; scripts/ab_update.py one setting per process: 172.5 vs 169.9 ms
-A3_PLANES = False
+# (merlin_h3_gemm_tn_gather_planes; with both operands as planes, the LDS-DMA TN k_h3_tq, H3_TN_CFG_PLANES).  False:
+# a3 in fp32, split by the GEMMs.  (Before k_h3_tq, with the register-staged TN: off -- kernel traces of one setting
+# per process, profiles/r05n_*_timeline.txt, had the forward no faster in the loop, the weight gradient 732 vs 716 us
+# and conv3's patch sums beside it 223 vs 192 us; 172.5 vs 169.9 ms per update.)
+A3_PLANES = True
 
 
 class WindowStep:
@@ -408,7 +410,8 @@ class WindowStep:
             if h3 and pdz is not None:
                 nat.h3_gemm_tn(pdz, amz, pa3, am3, name="gemm_wgrad", out=g[4])
             elif h3:
-                nat.h3_gemm_tn(dz, amz, a3, am3, name="gemm_wgrad", out=g[4], rows=arows)
+                nat.h3_gemm_tn(dz, amz, a3, am3, name="gemm_wgrad", out=g[4], rows=arows,
+                               cfg=nat.H3_TN_CFG_PLANES if a3p else None)
             else:
                 nat.x6_gemm_tn(dz, a3, name="gemm_wgrad", out=g[4])
 
@@ -416,6 +419,10 @@ class WindowStep:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 wgrad()
+        # conv3's backward chain's fills (the band marks preset to -1, the dQ table zeroed) ahead of the side-stream
+        # weight gradient: launched beside it, a small fill waits for a CU the GEMM's blocks free (~90 us each with
+        # the LDS-DMA weight gradient, whose blocks hold a CU's LDS and VGPRs whole; profiles/r05u_* trace)
+        pre = _conv3_backward_prefill(plan, int(Q.shape[1]), dz.device) if PREFILL else None
         if dzp:
             da3 = nat.h3_gemm_nt_planes(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad_planes"], name="gemm_fc1_dgrad")
         elif h3:
@@ -437,7 +444,7 @@ class WindowStep:
         if masks_ready is not None:
             main.wait_event(masks_ready)
         dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]),
-                                  mask_rows=arows if MASK_ROWS else None)
+                                  mask_rows=arows if MASK_ROWS else None, pre=pre)
         nat.colsum(dQ.view(2, -1, 9, 64)[:, :, 0], out=g[3])  # db3: every (u, p3) has one window at tap 0
         dQ = dQ.view(2, -1, 576)
         if wh3:
@@ -454,17 +461,34 @@ class WindowStep:
         self.stage.backward()
 
 
-def _conv3_backward_bulk(plan, mb, bits, dY3, nw, mask_rows=None):
+def _conv3_backward_prefill(plan, nw, device):
+    """(band marks preset to -1, zeroed dQ table) for _conv3_backward_bulk, made ahead of the weight gradient."""
+    bslot = getattr(plan, "_bslot", None)
+    if bslot is None:
+        bslot = plan._bslot = torch.empty(plan.num_bands, dtype=torch.int32, device=device)
+    bslot.fill_(-1)
+    dq = torch.zeros((2, nw * 9, 64), dtype=torch.float32, device=device)
+    return bslot, dq
+
+
+def _conv3_backward_bulk(plan, mb, bits, dY3, nw, mask_rows=None, pre=None):
     """dQ [T, nw*9, 64] of merlin.windows._conv3_backward with the minibatch's live-patch map taken from
-    the update-wide array (mb.kmap, WindowPlan.update_minibatches(bulk=True))."""
+    the update-wide array (mb.kmap, WindowPlan.update_minibatches(bulk=True)).  pre: (bslot preset to -1, zeroed
+    dQ) from _conv3_backward_prefill."""
     R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
                         name="k_seg_sum_R", mask=bits, fill=False, mask_rows=mask_rows)
     # band sums over the live patches, marking the bands that got one (merlin_segment_sum_marked); dQ reads only
     # those: the dead bands' rows are never zeroed (a 128-MB fill per step) nor read
-    bslot = getattr(plan, "_bslot", None)
-    if bslot is None:
-        bslot = plan._bslot = torch.empty(plan.num_bands, dtype=torch.int32, device=dY3.device)
-    bslot.fill_(-1)
+    if pre is None:
+        bslot = getattr(plan, "_bslot", None)
+        if bslot is None:
+            bslot = plan._bslot = torch.empty(plan.num_bands, dtype=torch.int32, device=dY3.device)
+        bslot.fill_(-1)
+    else:
+        bslot = pre[0]
     S = nat.segment_sum(R, plan.band_plan, plan.num_bands, slot=mb.kmap, sub=1, name="k_seg_sum_S", fill=False,
                         mark=bslot)
+    if pre is not None:  # the table was zeroed ahead: only the sums are written
+        return nat.segment_sum(S, plan.dq_plan, nw * 9, slot=bslot, sub=1, name="k_seg_sum_dQ", out=pre[1],
+                               fill=False)
     return nat.segment_sum(S, plan.dq_plan, nw * 9, slot=bslot, sub=1, name="k_seg_sum_dQ")

@@ -202,3 +202,22 @@ def test_forward_and_wgrad_over_a3_planes(device):
     ref = nat.h3_gemm_tn(dz, amz, a3, bound, rows=mb.rep_row)
     got = nat.h3_gemm_tn(dzp, amz, a3p, bound, rows=mb.rep_row)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("Kd,splits", [(1, 1), (31, 1), (257, 3), (3001, 32), (40000, 32), (111111, 32)])
+def test_wgrad_dma_kernel_bitwise(device, Kd, splits):
+    """The weight gradient's LDS-DMA TN kernel over both operands' planes (cfg 20, k_h3_tq: B's rows through a row
+    map read from an LDS ring, rows past a split's end zero-sourced, the step count padded to the ring's period) ==
+    the register-staged TN on the same planes (cfg 0), bit for bit; split-K and ragged row counts."""
+    from merlin import _native as nat
+
+    g = torch.Generator(device=device).manual_seed(Kd + splits)
+    dz = torch.randn(2, Kd, 512, device=device, generator=g) * 1e-6
+    a3 = torch.relu(torch.randn(2, Kd, 576, device=device, generator=g))
+    nc = Kd * 576 // 64
+    rows = torch.randint(0, nc, (nc,), device=device, generator=g, dtype=torch.int32)
+    amz, am3 = nat.h3_amax(dz), nat.h3_amax(a3)
+    dzp, a3p = nat.h3_split(dz, amz), nat.h3_split(a3, am3)
+    ref = nat.h3_gemm_tn(dzp, amz, a3p, am3, splits=splits, cfg=0, rows=rows)
+    got = nat.h3_gemm_tn(dzp, amz, a3p, am3, splits=splits, cfg=20, rows=rows)
+    assert torch.equal(got, ref)
