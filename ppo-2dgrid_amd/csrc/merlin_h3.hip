@@ -1623,10 +1623,11 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
 #define H3_NT(BM, BN, WM, WN, PIPE) \
     nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, hd, s, \
                                     a_is_planes)
-    if (a_is_planes && (cfg < 10 || cfg > 13)) return hipErrorInvalidValue;
+    if (a_is_planes && (cfg < 10 || cfg > 13) && cfg != 60) return hipErrorInvalidValue;
     if (cfg >= 60 && cfg < 70) {  // both operands as plane images (merlin_h3p.hip)
-        if (a_rows || head_part || P) return hipErrorInvalidValue;
-        return launch_h3p_gemm_nt(A, amaxA, B, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, cfg, s);
+        if (P || ((a_rows || head_part) && !a_is_planes)) return hipErrorInvalidValue;
+        return launch_h3p_gemm_nt(A, amaxA, B, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, cfg, s, a_rows,
+                                  head_w0, n_actions, head_w1, head_part);
     }
     switch (cfg) {
         case 0: return H3_NT(256, 128, 4, 2, false);
@@ -1760,6 +1761,7 @@ int h3_heads_parts(int N, int cfg) {
         // cfg 11: 96-column wave tiles, no heads epilogue
         case 12: return N % 128 ? 0 : N / 128 * 2;
         case 13: return N % 256 ? 0 : N / 256 * 4;
+        case 60: return N % 256 ? 0 : N / 256 * 4;  // k_h3_pqg (planes, gathered rows): cfg 13's tiles
         default: return 0;
     }
 }

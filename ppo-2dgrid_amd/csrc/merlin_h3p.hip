@@ -498,15 +498,275 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_tq(const p_u32x4 *__restr
             }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// The update's forward over a3's planes with the rows gathered (round 5; merlin_h3_gemm_nt_heads_planes cfg 60):
+// k_h3_pq's schedule (LDS-DMA three steps deep, K = 576 unrolled, fragment reads under the MFMAs) with A's rows read
+// through the row map by 64-value chunks -- row m's chunk j is row amap[m * 9 + j] of A seen as [*][64] (conv3's
+// patch representatives) -- and k_h3_ntp's epilogues (EPI 1 bias + ReLU; EPI 2 the same plus the policy / value
+// heads' partial dot products, merlin_heads_combine's layout).  The block's 9 BM chunk rows are read into LDS once;
+// a step's A sources are read from there one step ahead.  DMAs by inline asm as in k_h3_tq (no compiler-inserted
+// vmcnt before LDS reads).  The same products in the same order as k_h3_ntpg: the same bits.
+template <int BM, int BN, int WGM, int WGN, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pqg(const p_u32x4 *__restrict__ A, const p_u32x4 *__restrict__ B,
+                                                           const uint32_t *__restrict__ amaxA,
+                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N,
+                                                           int64_t sA, int64_t sB, const float *__restrict__ bias,
+                                                           float *__restrict__ C, int64_t sC, int tiles_n,
+                                                           const int32_t *__restrict__ amap,
+                                                           const float *__restrict__ hw0, const float *__restrict__ hw1,
+                                                           int na, float *__restrict__ hpart) {
+    constexpr int K = 576, NK = 18, KC = K / 64;
+    constexpr int NT = 64 * WGM * WGN;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int NR = 2 * (TM + TN), NM = 3 * TM * TN;
+    static_assert(NM >= NR, "a read behind every MFMA");
+    constexpr int GA = BM * 8 / NT, GB = BN * 8 / NT, G = GA + GB;
+    static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "whole DMA instructions per thread");
+    constexpr int STG = (BM + BN) * 8;
+    constexpr uint32_t STG_B = STG * 16;
+    __shared__ p_u32x4 lds[3 * STG];
+    __shared__ int32_t gmap[BM * KC];
+
+    const int t = blockIdx.y;
+    const int L = p_xcd_tile(blockIdx.x, gridDim.x);
+    const int tm = L / tiles_n, tn = L - tm * tiles_n;
+    const int64_t m0 = (int64_t)tm * BM;
+    const int n0 = tn * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WGN, wn = w - (w / WGN) * WGN;
+    const int eA = p_exp(p_amax(amaxA + t)), eB = p_exp(p_amax(amaxB + t));
+    for (int e = tid; e < BM * KC; e += NT) {
+        const int r = e / KC;
+        gmap[e] = amap[std::min<int64_t>(m0 + r, M - 1) * KC + (e - r * KC)];
+    }
+    __syncthreads();
+    const p_u32x4 *At = A + t * sA, *baseB = B + t * sB + (int64_t)n0 * (K / 4);
+    int ga[GA];       // gmap entry base r * KC of the thread's A slots
+    uint32_t ca[GA];  // their chunk within a k step
+    uint32_t offB[GB];
+#pragma unroll
+    for (int i = 0; i < GA; i++) {
+        const int q = i * NT + tid, r = q >> 3;
+        ga[i] = r * KC;
+        ca[i] = (uint32_t)((q & 7) ^ p_swz(r));
+    }
+#pragma unroll
+    for (int i = 0; i < GB; i++) {
+        const int q = i * NT + tid, r = q >> 3;
+        offB[i] = (uint32_t)(r * (K / 4) + ((q & 7) ^ p_swz(r)));
+    }
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) p_u32x4 *)lds;
+    const uint32_t gm0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t *)gmap;
+    const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane(w) * 64u;
+    // the chunk rows of step kt's A slots (plain LDS loads, read a step ahead of their issue)
+    auto read_g = [&](int kt, int32_t (&g)[GA]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < GA; i++) g[i] = *(const lds_i32 *)(uintptr_t)(gm0 + (uint32_t)(ga[i] + kt / 2) * 4u);
+    };
+    auto issue = [&](int kt, int st, const int32_t (&g)[GA]) __attribute__((always_inline)) {
+        const uint32_t base = lds0 + (uint32_t)(st * STG) * 16u + wbase * 16u;
+#pragma unroll
+        for (int i = 0; i < GA; i++)
+            p_dma16(At + (int64_t)g[i] * 16 + 8 * (kt & 1) + ca[i], base + (uint32_t)(i * NT) * 16u);
+#pragma unroll
+        for (int i = 0; i < GB; i++) p_dma16(baseB + offB[i] + kt * 8, base + (uint32_t)((GA + i) * NT) * 16u);
+    };
+
+    const int fr = lane & 31, fh = lane >> 5;
+    uint32_t adA[2][2], adB[2][2];
+    {
+        const int ra = wm * WTM + fr, rb = BM + wn * WTN + fr;
+#pragma unroll
+        for (int kh = 0; kh < 2; kh++)
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+                const int c = 2 * (2 * kh + fh) + p;
+                adA[kh][p] = lds0 + (uint32_t)(ra * 8 + (c ^ p_swz(ra))) * 16u;
+                adB[kh][p] = lds0 + (uint32_t)(rb * 8 + (c ^ p_swz(rb))) * 16u;
+            }
+    }
+    struct Frag {
+        p_u32x4 a[TM][2], b[TN][2];
+    };
+    p_f32x16 hi[TM][TN], lo[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            hi[i][j] = p_f32x16{};
+            lo[i][j] = p_f32x16{};
+        }
+    auto rd = [&](Frag &g, auto K_, uint32_t so, auto KH) __attribute__((always_inline)) {
+        constexpr int k = decltype(K_)::value, kh = decltype(KH)::value;
+        if constexpr (k < 2 * TM)
+            lds_rd(g.a[k >> 1][k & 1], adA[kh][k & 1] + so + (k >> 1) * 32 * 128);
+        else
+            lds_rd(g.b[(k - 2 * TM) >> 1][k & 1], adB[kh][k & 1] + so + ((k - 2 * TM) >> 1) * 32 * 128);
+    };
+    auto mf = [&](const Frag &f, auto M_) __attribute__((always_inline)) {
+        constexpr int m = decltype(M_)::value, i = m / (3 * TN), j = (m / 3) % TN, pr = m % 3;
+        if constexpr (pr == 0)
+            lo[i][j] = p_mfma(f.a[i][1], f.b[j][0], lo[i][j]);
+        else if constexpr (pr == 1)
+            lo[i][j] = p_mfma(f.a[i][0], f.b[j][1], lo[i][j]);
+        else
+            hi[i][j] = p_mfma(f.a[i][0], f.b[j][0], hi[i][j]);
+    };
+    auto half = [&](const Frag &f, Frag &g, uint32_t so, auto KH, auto READS) __attribute__((always_inline)) {
+        static_for<NM>([&](auto M_) __attribute__((always_inline)) {
+            mf(f, M_);
+            if constexpr (decltype(READS)::value && decltype(M_)::value < NR) rd(g, M_, so, KH);
+        });
+        if constexpr (decltype(READS)::value) {
+            static_for<NR>([&](auto) __attribute__((always_inline)) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            });
+            if constexpr (NM > NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto touch = [&](const Frag &f) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < TM; i++) asm volatile("" ::"v"(f.a[i][0]), "v"(f.a[i][1]));
+#pragma unroll
+        for (int j = 0; j < TN; j++) asm volatile("" ::"v"(f.b[j][0]), "v"(f.b[j][1]));
+    };
+
+    int32_t g0[GA], g1[GA];  // chunk rows of the next issue (ping-pong, compile-time choice)
+    read_g(0, g0);
+    issue(0, 0, g0);
+    read_g(1, g1);
+    issue(1, 1, g1);
+    read_g(2, g0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    Frag f0, f1;
+    static_for<NR>([&](auto K_) __attribute__((always_inline)) { rd(f0, K_, 0, IC<0>{}); });
+    static_for<NK>([&](auto KT) __attribute__((always_inline)) {
+        constexpr int kt = decltype(KT)::value, st = kt % 3, sn = (kt + 1) % 3;
+        int32_t(&gu)[GA] = (kt % 2 == 0) ? g0 : g1;  // holds step kt + 2's rows
+        int32_t(&gn)[GA] = (kt % 2 == 0) ? g1 : g0;
+        if constexpr (kt + 2 < NK) issue(kt + 2, (kt + 2) % 3, gu);
+        __builtin_amdgcn_sched_barrier(0);
+        half(f0, f1, (uint32_t)st * STG_B, IC<1>{}, IC<1>{});
+        if constexpr (kt + 1 < NK) {
+            touch(f1);
+            if constexpr (kt + 2 < NK)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (kt + 3 < NK) read_g(kt + 3, gn);
+            half(f1, f0, (uint32_t)sn * STG_B, IC<0>{}, IC<1>{});
+        } else {
+            half(f1, f0, 0u, IC<0>{}, IC<0>{});
+        }
+    });
+
+    const float inv = p_pow2(-eA), invB = p_pow2(-eB);
+    float *Ct = C + t * sC;
+    if constexpr (EPI == 2) {  // k_h3_ntp's heads epilogue (merlin_h3.hip h3_ntp_body EPI 2)
+        static_assert(TN == 2 && WTN == 64, "heads epilogue: a wave tile 64 columns wide");
+        const float *hw = t == 0 ? hw0 : hw1;
+        const int nh = t == 0 ? na : 1;
+        float wv[4][TN], bv[TN];
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int col = n0 + wn * WTN + j * 32 + fr;
+            bv[j] = bias[(int64_t)t * N + col];
+#pragma unroll
+            for (int o = 0; o < 4; o++) wv[o][j] = o < nh ? hw[(int64_t)o * N + col] : 0.0f;
+        }
+        float *part = hpart + ((int64_t)(t * tiles_n + tn) * WGN + wn) * M * 4;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            float pv[64];
+#pragma unroll
+            for (int q = 0; q < 64; q++) pv[q] = 0.0f;
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                const int col = n0 + wn * WTN + j * 32 + fr;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                    const float v = p_relu((hi[i][j][r] + lo[i][j][r] * P_LO_INV) * inv * invB + bv[j]);
+                    if (row < M) Ct[row * N + col] = v;
+#pragma unroll
+                    for (int o = 0; o < 4; o++) pv[o * 16 + r] += v * wv[o][j];
+                }
+            }
+#pragma unroll
+            for (int c = 64, off = 16; off >= 1; c >>= 1, off >>= 1) {
+                const bool up = (fr & off) != 0;
+#pragma unroll
+                for (int k = 0; k < c / 2; k++) {
+                    const float send = up ? pv[k] : pv[k + c / 2], keep = up ? pv[k + c / 2] : pv[k];
+                    pv[k] = keep + __shfl_xor(send, off);
+                }
+            }
+            const int o = fr >> 3;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int r = 2 * (fr & 7) + k;
+                const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (row < M) part[row * 4 + o] = pv[k];
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+        const int col = n0 + wn * WTN + j * 32 + fr;
+        const float bv = EPI == 1 ? bias[(int64_t)t * N + col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (row < M) {
+                    const float v = (hi[i][j][r] + lo[i][j][r] * P_LO_INV) * inv * invB;
+                    Ct[row * N + col] = EPI == 1 ? p_relu(v + bv) : v;
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // A, B: plane images (4 B per value, strides in values); cfg 60: 128 x 256 tiles (2 x 4 waves), 61: 256 x 128 (4 x 2),
 // 62: 128 x 192 (4 x 2 waves of 32 x 96: N = 576)
 hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                               int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
-                              int64_t c_stride, int cfg, hipStream_t s) {
+                              int64_t c_stride, int cfg, hipStream_t s, const int32_t *a_rows, const float *head_w0,
+                              int n_actions, const float *head_w1, float *head_part) {
     if (M <= 0) return hipSuccess;
     if (a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
+    if (a_rows) {  // the forward over a3's gathered planes (cfg 60 tiles, K = 576), bias + ReLU, heads optional
+        constexpr int BM = 128, BN = 256;
+        if (cfg != 60 || K != 576 || N % BN || !bias || !C) return hipErrorInvalidValue;
+        if (head_part && (T != 2 || n_actions < 1 || n_actions > 4 || !head_w0 || !head_w1)) return hipErrorInvalidValue;
+        const int64_t tiles_m = (M + BM - 1) / BM;
+        const int tiles_n = N / BN;
+        const dim3 grid((unsigned)(tiles_m * tiles_n), T), block(512);
+        const auto *a = static_cast<const p_u32x4 *>(A);
+        const auto *b = static_cast<const p_u32x4 *>(B);
+        if (head_part)
+            hipLaunchKernelGGL((k_h3_pqg<BM, BN, 2, 4, 2>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, a_stride / 4,
+                               b_stride / 4, bias, C, c_stride, tiles_n, a_rows, head_w0, head_w1, n_actions,
+                               head_part);
+        else
+            hipLaunchKernelGGL((k_h3_pqg<BM, BN, 2, 4, 1>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, a_stride / 4,
+                               b_stride / 4, bias, C, c_stride, tiles_n, a_rows, nullptr, nullptr, 0, nullptr);
+        return hipGetLastError();
+    }
     switch (cfg) {
         case 60: return pq_launch<128, 256, 2, 4>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 61: return pq_launch<256, 128, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);

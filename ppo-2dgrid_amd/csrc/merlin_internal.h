@@ -191,7 +191,9 @@ hipError_t launch_group_act(const uint32_t *codes, int G, const float *T2, const
                             const float *Wc, const float *bc, int A, float *a3, float *part, hipStream_t s);
 hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                               int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
-                              int64_t c_stride, int cfg, hipStream_t s);
+                              int64_t c_stride, int cfg, hipStream_t s, const int32_t *a_rows = nullptr,
+                              const float *head_w0 = nullptr, int n_actions = 0, const float *head_w1 = nullptr,
+                              float *head_part = nullptr);
 hipError_t launch_h3p_gemm_tn_gather(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB,
                                      int64_t Kd, int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits,
                                      float *slab, const int32_t *b_rows, int cfg, int *S_out, hipStream_t s);

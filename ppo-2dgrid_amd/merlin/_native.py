@@ -1082,7 +1082,7 @@ def x6_gemm_tn(A: torch.Tensor, B: torch.Tensor, splits: int | None = None, cfg:
 # 128 x 256 and input gradient 128 x 192 tiles (scripts/ab_update.py, same update replayed: 204.5 vs 209.0 ms for cfg 0 / 1)
 # rollout: 4,096 rows; qall: [5^9, 64] x [64, 576] (k_h3_nt, not the input gradient's k_h3_ntp instantiation, so
 # profiles keep the two apart); qwin / qwin_dgrad: the update's window GEMMs (N = 576, K = 64 / N = 64, K = 576)
-H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 1, "qwin": 11, "qwin_dgrad": 5, "dgrad_planes": 62}
+H3_NT_CFG = {"fwd": 13, "dgrad": 11, "rollout": 12, "qall": 1, "qwin": 11, "qwin_dgrad": 5, "dgrad_planes": 62, "fwd_planes": 60}
 H3_TN_CFG = 0
 H3_TN_CFG_PLANES = 20  # the weight gradient over both operands' planes: the LDS-DMA TN (merlin_h3p.hip k_h3_tq)
 # the update's fc1 forward (h3, cfg "fwd" with a heads epilogue) computes the policy / value heads in its epilogue

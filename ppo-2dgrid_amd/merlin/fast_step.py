@@ -380,7 +380,8 @@ class WindowStep:
             if (pa3 is None and nat.H3_HEADS_EPILOGUE
                     and nat.lib().merlin_h3_heads_parts(P4.shape[1], nat.H3_NT_CFG["fwd"]) > 0):
                 # both heads in the GEMM's epilogue (the loss adds their biases)
-                h, logits, value = nat.h3_gemm_nt_heads(a3, am3, P4, amW, b4, Wa, Wc, cfg=nat.H3_NT_CFG["fwd"],
+                h, logits, value = nat.h3_gemm_nt_heads(a3, am3, P4, amW, b4, Wa, Wc,
+                                                        cfg=nat.H3_NT_CFG["fwd_planes" if a3p else "fwd"],
                                                         rows=arows, name="gemm_fc1_fwd")
             else:
                 h = nat.h3_gemm_nt(a3, am3, P4, amW, bias=b4, cfg=nat.H3_NT_CFG["fwd"], name="gemm_fc1_fwd",

@@ -192,6 +192,9 @@ def test_forward_and_wgrad_over_a3_planes(device):
     h0, l0, v0 = nat.h3_gemm_nt_heads(a3, bound, P4, amW, b4, Wa, Wc, cfg=13, rows=mb.rep_row)
     h1, l1, v1 = nat.h3_gemm_nt_heads(a3p, bound, P4, amW, b4, Wa, Wc, cfg=13, rows=mb.rep_row)
     assert torch.equal(h1, h0) and torch.equal(l1, l0) and torch.equal(v1, v0)
+    # the LDS-DMA forward over the gathered planes (cfg 60, k_h3_pqg): the same bits
+    h2, l2, v2 = nat.h3_gemm_nt_heads(a3p, bound, P4, amW, b4, Wa, Wc, cfg=60, rows=mb.rep_row)
+    assert torch.equal(h2, h0) and torch.equal(l2, l0) and torch.equal(v2, v0)
     _, dlogits, dvalue, _, _, _ = _heads_case(device, n, seed=n)
     gm = torch.zeros(9, dtype=torch.int32, device=device)
     gm.view(torch.float32)[:3] = dlogits.abs().amax(0)
