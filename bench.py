@@ -252,8 +252,8 @@ def x6_standalone(torch, U, device, impl="h3", reps=10):
         Wc = torch.randn(1, 512, device=device, generator=g) / 24
         dgrad = ((lambda: nat.h3_gemm_nt_planes(dzo, amz, Wtp, amW, cfg=nat.H3_NT_CFG["dgrad_planes"]))
                  if FS.DZ_PLANES else (lambda: nat.h3_gemm_nt(dz, amz, Wtp, amW, cfg=nat.H3_NT_CFG["dgrad"])))
-        runs = {"gemm_fc1_fwd": lambda: nat.h3_gemm_nt_heads(a3o, am3, Wp, amW, b, Wa, Wc, cfg=nat.H3_NT_CFG["fwd"],
-                                                             rows=rows),
+        fcfg = nat.H3_NT_CFG["fwd_planes" if a3p else "fwd"]
+        runs = {"gemm_fc1_fwd": lambda: nat.h3_gemm_nt_heads(a3o, am3, Wp, amW, b, Wa, Wc, cfg=fcfg, rows=rows),
                 "gemm_fc1_dgrad": dgrad,
                 "gemm_wgrad": lambda: nat.h3_gemm_tn(dzo, amz, a3o, am3, rows=rows,
                                                      cfg=nat.H3_TN_CFG_PLANES if a3p else None)}
@@ -323,7 +323,7 @@ PMC_ALIAS = {"k_seg_sum_R": ("k_seg_sum<2, 1>", "k_seg_fix<1>"),
              "gemm_wgrad": ("k_h3_tn<128, 192, 4, 2>", "k_x6_fold")}
 # with conv3's patch reuse (merlin/fast_step.py PATCH_REUSE = "gather") the update's k_window_conv3 span is the
 # representatives' kernel + the mask-word copy, and fc1's forward / weight gradient read a3 through the row map
-PMC_ALIAS_GATHER = {"k_window_conv3": ("k_window_conv3_reps", "k_window_conv3_copy<false>"),
+PMC_ALIAS_GATHER = {"k_window_conv3": ("k_window_conv3_reps", "k_window_conv3_copy<false>", "k_q_colmax", "k_q_bound"),
                     "gemm_wgrad": ("k_h3_tng<128, 192, 4, 2>", "k_x6_fold")}
 # rocprofv3 names of merlin_h3_gemm_nt's configurations (csrc/merlin_h3.hip launch_h3_gemm_nt)
 H3_NT_NAMES = {0: "k_h3_nt<256, 128, 4, 2, {}>", 1: "k_h3_nt<128, 192, 4, 2, {}>", 2: "k_h3_nt<128, 128, 2, 2, {}>",
@@ -353,8 +353,9 @@ def h3_gemm_names(nat):
         a3p = dzp and FS.A3_PLANES
         wg = (f"k_h3_tq<128, 192, 4, 2>" if a3p and nat.H3_TN_CFG_PLANES == 20 else
               f"k_h3_tng<128, 192, 4, 2, {'true' if dzp else 'false'}, {'true' if a3p else 'false'}>")
-        return {**out, **PMC_ALIAS_GATHER, "gemm_wgrad": (wg, "k_x6_fold"),
-                "gemm_fc1_fwd": (fwd.replace("k_h3_ntp<", "k_h3_ntpg<").replace(">", ", true>" if a3p else ", false>"),)}
+        fw = ("k_h3_pqg<128, 256, 2, 4, 2>" if a3p and nat.H3_NT_CFG["fwd_planes"] == 60 else
+              fwd.replace("k_h3_ntp<", "k_h3_ntpg<").replace(">", ", true>" if a3p else ", false>"))
+        return {**out, **PMC_ALIAS_GATHER, "gemm_wgrad": (wg, "k_x6_fold"), "gemm_fc1_fwd": (fw,)}
     return {**out, "gemm_fc1_fwd": (fwd,)}
 PMC_FILE = os.environ.get("MERLIN_PMC_FILE")  # default: the newest profiles/*_pmc.json holding the kernel
 
