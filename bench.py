@@ -670,8 +670,11 @@ def main():
         # tests/test_gpu_h3.py), exact to 2^-23 relative for values within 2^26 of each tensor's max |x|
         "dtype": "fp32",
         "dtype_note": ("fp32 operands/results; GEMM products as f16 two-plane (h3) splits with per-tensor power-of-two "
-                       "scales: each value held to 2^-23 relative when within 2^26 of its tensor's max |x| (smaller "
-                       "values to 2^-50 of the max, absolute)") if fc1 == "h3" else None,
+                       "scales: each value held to 2^-23 relative when within 2^26 of its tensor's scale reference "
+                       "(smaller values to 2^-50 of it, absolute); the reference is max |x| for the weights and a "
+                       "bound >= max |x| known before the producer runs for fc1's activations (dz: the loss's "
+                       "gradient maxima through the heads' weights; a3: relu(b3 + sum over taps of Q's column maxima))"
+                       ) if fc1 == "h3" else None,
         "data": "synthetic: procedurally generated mediumhard maps (numpy-PCG64-exact, seeds 777+i), "
                 "random-init CNNActorCritic (torch seed 777), timed after the warm-up iterations",
         "config": {"workload": f"{args.difficulty} {args.size}x{args.size}, {N} envs/GPU x k_steps {T}, "
