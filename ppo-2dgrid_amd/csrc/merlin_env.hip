@@ -190,31 +190,37 @@ struct Grid {
     // _is_reachable (medium_hard_env.py:47-74): the BFS's boolean equals "goal in
     // the 4-connected component of non-wall cells containing the agent"; computed
     // as a bit-parallel flood fill over row masks (Gauss-Seidel sweeps in registers).
+    // A row takes in one visit every free run that holds a seed (run_fill: the carry of f + x runs from
+    // the lowest seed of a run to its end, the same on the bit-reversed row for the other direction),
+    // so the sweeps only have to carry the component between rows; the fixed point, hence the boolean,
+    // is the same component as with one cell of horizontal spread per visit.
+    __device__ static __forceinline__ uint32_t run_fill(uint32_t f, uint32_t rf, uint32_t x) {
+        const uint32_t u = (f & ~(f + x)) | x;  // from the lowest seed of each run up to the run's end
+        const uint32_t ru = __brev(u);
+        return __brev((rf & ~(rf + ru)) | ru);  // and down to the run's start
+    }
     __device__ bool reachable() const {
-        uint32_t F[SP], R[SP];
+        uint32_t F[SP], RF[SP], R[SP];
         const uint32_t fm = full();
 #pragma unroll
         for (int y = 0; y < SP; y++) {
             F[y] = (y < S) ? (~row(y) & fm) : 0u;
-            R[y] = (y == ay) ? (1u << ax) : 0u;
+            RF[y] = __brev(F[y]);
+            R[y] = (y == ay) ? run_fill(F[y], RF[y], 1u << ax) : 0u;
         }
         for (int it = 0; it < SP * SP; it++) {
             uint32_t changed = 0u;
 #pragma unroll
-            for (int y = 0; y < SP; y++) {
-                uint32_t n = R[y] | (R[y] << 1) | (R[y] >> 1);
-                if (y > 0) n |= R[y - 1];
-                if (y < SP - 1) n |= R[y + 1];
-                n &= F[y];
+            for (int y = 1; y < SP; y++) {
+                const uint32_t x = (R[y - 1] | (y < SP - 1 ? R[y + 1] : 0u)) & F[y] & ~R[y];
+                const uint32_t n = x ? run_fill(F[y], RF[y], x | R[y]) : R[y];
                 changed |= n ^ R[y];
                 R[y] = n;
             }
 #pragma unroll
-            for (int y = SP - 1; y >= 0; y--) {
-                uint32_t n = R[y] | (R[y] << 1) | (R[y] >> 1);
-                if (y > 0) n |= R[y - 1];
-                if (y < SP - 1) n |= R[y + 1];
-                n &= F[y];
+            for (int y = SP - 2; y >= 0; y--) {
+                const uint32_t x = ((y > 0 ? R[y - 1] : 0u) | R[y + 1]) & F[y] & ~R[y];
+                const uint32_t n = x ? run_fill(F[y], RF[y], x | R[y]) : R[y];
                 changed |= n ^ R[y];
                 R[y] = n;
             }
