@@ -650,7 +650,9 @@ int merlin_h3_gemm_tn_gather(const float *A_dev, const uint32_t *amax_a_dev, con
  * combination, CNNActorCritic._lut2_h1_index order).  Forward: HT f32[t][680][32] (relu(conv1) of every
  * combination, kept for the backward), T2 f32[t][2720][64].  Backward from dT2 f32[t][2720][64]: dH
  * f32[t][680][32] (scratch), dW1 / db1 / dW2 in the layouts of W1 / b1 / W2; koff int16[81] / kv int16[2720]
- * = the combinations v of each table entry k (CSR, (v, e) order).  Fixed-order sums (bitwise reproducible). */
+ * = the combinations v of each table entry k (CSR, (v, e) order).  Fixed-order sums (bitwise reproducible).
+ * The backward keeps partial sums in a per-device library workspace: calls on one device run one at a time
+ * (one stream, or ordered streams). */
 int merlin_stage_tables_fwd(const float *W1_dev, const float *b1_dev, const float *W2_dev, const float *atlas_dev,
                             const int16_t *idx_dev, int32_t towers, float *HT_dev, float *T2_dev, void *stream);
 int merlin_stage_tables_bwd(const float *W2_dev, const float *HT_dev, const float *dT2_dev, const float *atlas_dev,

@@ -203,6 +203,7 @@ struct DeviceWs {
     int max_slabs = 0;
     void *lut2_slabs = nullptr;  // conv2 table histogram: per-block 4-channel u64 slices
     float *epi_work = nullptr;   // GEMM epilogues: per-block column-sum partials
+    double *stage_part = nullptr;  // conv tables' adjoint: the 625-combination type's partial dW2 sums
 };
 constexpr int MAX_DEV = 64;
 DeviceWs g_dev[MAX_DEV];
@@ -225,6 +226,7 @@ int device_ws(DeviceWs **out) {
         w.max_slabs = WS_SLABS;
         HIP_TRY(hipMalloc(&w.lut2_slabs, merlin::conv2_lut_slab_bytes(2, merlin::conv2_lut_fblocks(INT64_MAX / 64))));
         HIP_TRY(hipMalloc(&w.epi_work, sizeof(float) * merlin::epilogue_work_floats()));
+        HIP_TRY(hipMalloc(&w.stage_part, sizeof(double) * merlin::STAGE_WS_DOUBLES));
         w.ready = true;
     }
     *out = &w;
@@ -1004,7 +1006,11 @@ int merlin_stage_tables_bwd(const float *W2, const float *HT, const float *dT2, 
     if (!W2 || !HT || !dT2 || !atlas || !koff || !kv || !dH || !dW1 || !db1 || !dW2)
         return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_stage_bwd(W2, HT, dT2, atlas, koff, kv, towers, dH, dW1, db1, dW2, (hipStream_t)stream));
+    DeviceWs *ws = nullptr;
+    int rc = device_ws(&ws);
+    if (rc != MERLIN_OK) return rc;
+    HIP_TRY(merlin::launch_stage_bwd(W2, HT, dT2, atlas, koff, kv, towers, dH, dW1, db1, dW2, ws->stage_part,
+                                     (hipStream_t)stream));
     return MERLIN_OK;
 }
 

@@ -267,7 +267,9 @@ hipError_t launch_stage_fwd(const float *W1, const float *b1, const float *W2, c
                             int T, float *HT, float *T2, hipStream_t s);
 hipError_t launch_stage_bwd(const float *W2, const float *HT, const float *dT2, const float *atlas,
                             const int16_t *koff, const int16_t *kv, int T, float *dH, float *dW1, float *db1,
-                            float *dW2, hipStream_t s);
+                            float *dW2, double *ws, hipStream_t s);
+// k_stage_bwd_w's partials (towers x taps x parts x outputs)
+constexpr size_t STAGE_WS_DOUBLES = 2 * 4 * 10 * 2048;
 hipError_t launch_heads_fwd(const float *h, int64_t n, int H, const float *wa, int A, const float *wc, const float *ba,
                             const float *bc, float *logits, float *value, hipStream_t s);
 hipError_t launch_seg_sum(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,

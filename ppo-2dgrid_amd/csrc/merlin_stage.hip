@@ -133,26 +133,31 @@ __global__ __launch_bounds__(256) void k_stage_bwd_h(const float *__restrict__ W
 }
 
 constexpr int VS = 64;      // combinations per LDS stage of the dW2 blocks
+constexpr int NP3 = 10;  // the 625-combination type's dW2 sums split over this many blocks (63 combinations each)
+constexpr int NI = 12 + 4 * NP3;  // dW2 work items per tower: (type < 3, j), then (j, part) of type 3
 constexpr int WT = 1024;    // threads of k_stage_bwd_w
 constexpr int WQ = WT / 256;  // combination groups of a dW2 block (each thread of a group: 8 outputs)
 
-// blocks [0, T * 16): (tower, type, j): dW2[co][o][tap] = sum over the type's combinations of HT[v][o] *
-// dT2[4 v + j][co]; group g of the block's four thread groups sums the combinations v with (v - va) % 4 == g in
-// order (8 outputs per thread), the four partials join in a fixed order -- a type-3 block walks 625 combinations,
-// so one group per block made its 20 dependent load-and-sum stages the kernel's time;  blocks [T * 16, T * 16 +
-// T * C1): tower t, conv1 channel o: db1[o] = sum_v dH[v][o] (strided partial sums, then a fixed tree), dP[o][k]
+// blocks [0, T * NI): work item (tower, type, j[, part]): dW2[co][o][tap] = sum over the type's combinations of
+// HT[v][o] * dT2[4 v + j][co]; group g of the block's four thread groups sums the combinations v with (v - va) % 4 ==
+// g in order (8 outputs per thread), the four partials join in a fixed order -- a type-3 block walked 625
+// combinations, 10 dependent load-and-sum stages, the kernel's time: type 3's sums are split into NP3 blocks of
+// 63 combinations whose f64 partials k_stage_fold adds in part order;  blocks [T * NI, T * NI + T * C1): tower t,
+// conv1 channel o: db1[o] = sum_v dH[v][o] (strided partial sums, then a fixed tree), dP[o][k]
 // for the 80 k (combinations in (v, e) order through the CSR kinv), then dW1[o][c][ky][kx]
 __global__ __launch_bounds__(WT) void k_stage_bwd_w(const float *__restrict__ HT, const float *__restrict__ dT2,
                                                     const float *__restrict__ dH, const float *__restrict__ atlas,
                                                     const int16_t *__restrict__ koff, const int16_t *__restrict__ kv,
                                                     int T, float *__restrict__ dW1, float *__restrict__ db1,
-                                                    float *__restrict__ dW2) {
+                                                    float *__restrict__ dW2, double *__restrict__ ws) {
     __shared__ float Hs[VS][C1], Gs[VS][C2];
     __shared__ double part[WQ - 1][256 * 8], red[WT], dP[80];
-    if ((int)blockIdx.x < T * 16) {
-        const int t = blockIdx.x / 16, p = (blockIdx.x / 4) & 3, j = blockIdx.x & 3;
+    if ((int)blockIdx.x < T * NI) {
+        const int t = blockIdx.x / NI, it = blockIdx.x % NI;
+        const int p = it < 12 ? it >> 2 : 3, j = it < 12 ? it & 3 : (it - 12) / NP3, q = it < 12 ? 0 : (it - 12) % NP3;
         const int tap = (2 * (j >> 1) + (p >> 1)) * 4 + 2 * (j & 1) + (p & 1);
-        const int va = part_off(p), vb = part_off(p + 1);
+        constexpr int CH3 = (625 + NP3 - 1) / NP3;
+        const int va = p < 3 ? part_off(p) : part_off(3) + q * CH3, vb = p < 3 ? part_off(p + 1) : min(va + CH3, NV);
         const int g = threadIdx.x >> 8, l = threadIdx.x & 255;
         const int o = l & (C1 - 1), cq = l >> 5;  // outputs (co = cq + 8 i, o)
         double acc[8];
@@ -205,34 +210,34 @@ __global__ __launch_bounds__(WT) void k_stage_bwd_w(const float *__restrict__ HT
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 const double s = (acc[i] + part[0][i * 256 + l]) + (part[1][i * 256 + l] + part[2][i * 256 + l]);
-                dW2[(((size_t)t * C2 + cq + 8 * i) * C1 + o) * 16 + tap] = (float)s;
+                if (p < 3)
+                    dW2[(((size_t)t * C2 + cq + 8 * i) * C1 + o) * 16 + tap] = (float)s;
+                else
+                    ws[(((size_t)t * 4 + j) * NP3 + q) * 2048 + i * 256 + l] = s;
             }
         }
         return;
     }
-    const int b = blockIdx.x - T * 16, t = b / C1, o = b - t * C1;
+    const int b = blockIdx.x - T * NI, t = b / C1, o = b - t * C1;
     const float *d = dH + (size_t)t * NV * C1 + o;
     {  // db1: thread i sums combinations i, i + WT, ... in order, then a fixed tree
         double s = 0.0;
         for (int v = threadIdx.x; v < NV; v += WT) s += d[(size_t)v * C1];
         red[threadIdx.x] = s;
     }
-    if (threadIdx.x < 80) {  // dP[o][k]: the (v, e) entries with idx[v][e] = k, in (v, e) order
-        // eight entries' loads in flight at a time (clamped indices, no select next to a load), added in order
-        const int k = threadIdx.x, i1 = koff[k + 1];
-        double acc = 0.0;
-        for (int i0 = koff[k]; i0 < i1; i0 += 8) {
-            int r[8];
+    {  // dP[o][k]: the sum over the (v, e) entries with idx[v][e] = k.  One wave per k (five k per wave): lane l adds
+       // entries l, l + 64, ... in order (one round of loads for most k; a bin of the 625-combination type has ~125
+       // entries, which one thread walked as ~16 dependent rounds of two loads: the kernel's critical path), then a
+       // fixed butterfly over the lanes -- the same order on every call
+        const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        for (int k = wv; k < 80; k += WT / 64) {
+            const int i0 = koff[k], i1 = koff[k + 1];
+            double acc = 0.0;
+            for (int i = i0 + ln; i < i1; i += 64) acc += d[(size_t)kv[i] * C1];
 #pragma unroll
-            for (int u = 0; u < 8; u++) r[u] = kv[min(i0 + u, i1 - 1)];
-            float x[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) x[u] = d[(size_t)r[u] * C1];
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (i0 + u < i1) acc += x[u];
+            for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
+            if (ln == 0) dP[k] = acc;
         }
-        dP[k] = acc;
     }
     __syncthreads();
     for (int w = WT / 2; w > 0; w >>= 1) {
@@ -252,6 +257,19 @@ __global__ __launch_bounds__(WT) void k_stage_bwd_w(const float *__restrict__ HT
     }
 }
 
+// grid (T * 4): type 3's dW2 at tap j from its NP3 partial sums, added in part order
+__global__ __launch_bounds__(256) void k_stage_fold(const double *__restrict__ ws, float *__restrict__ dW2) {
+    const int t = blockIdx.x >> 2, j = blockIdx.x & 3, l = threadIdx.x, o = l & (C1 - 1), cq = l >> 5;
+    const int tap = (2 * (j >> 1) + 1) * 4 + 2 * (j & 1) + 1;
+    const double *w = ws + ((size_t)t * 4 + j) * NP3 * 2048;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        double s = w[i * 256 + l];
+        for (int q = 1; q < NP3; q++) s += w[q * 2048 + i * 256 + l];
+        dW2[(((size_t)t * C2 + cq + 8 * i) * C1 + o) * 16 + tap] = (float)s;
+    }
+}
+
 }  // namespace
 
 hipError_t launch_stage_fwd(const float *W1, const float *b1, const float *W2, const float *atlas, const int16_t *idx,
@@ -262,12 +280,15 @@ hipError_t launch_stage_fwd(const float *W1, const float *b1, const float *W2, c
 
 hipError_t launch_stage_bwd(const float *W2, const float *HT, const float *dT2, const float *atlas,
                             const int16_t *koff, const int16_t *kv, int T, float *dH, float *dW1, float *db1,
-                            float *dW2, hipStream_t s) {
+                            float *dW2, double *ws, hipStream_t s) {
     hipLaunchKernelGGL(k_stage_bwd_h, dim3(NCH, T), dim3(256), 0, s, W2, HT, dT2, dH);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_stage_bwd_w, dim3(T * 16 + T * C1), dim3(WT), 0, s, HT, dT2, dH, atlas, koff, kv, T, dW1,
-                       db1, dW2);
+    hipLaunchKernelGGL(k_stage_bwd_w, dim3(T * NI + T * C1), dim3(WT), 0, s, HT, dT2, dH, atlas, koff, kv, T, dW1,
+                       db1, dW2, ws);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_stage_fold, dim3(T * 4), dim3(256), 0, s, ws, dW2);
     return hipGetLastError();
 }
 
