@@ -334,7 +334,7 @@ int merlin_env_create(const merlin_env_config *cfg, merlin_env **out) {
     alloc((void **)&d.pg_rng_b, n * sizeof(uint2));
     alloc((void **)&d.pg_valid, n * sizeof(uint8_t));
     alloc((void **)&d.rflag, n * sizeof(uint8_t));
-    alloc((void **)&d.bflag, (n + 255) / 256);
+    alloc((void **)&d.bflag, (n + 63) / 64);  // one flag per step block (merlin_env.hip SBLK >= 64 envs)
     if (d.explore_on) alloc((void **)&d.visited, n * d.sp * sizeof(uint32_t));
     if (err != hipSuccess) {
         merlin_env_destroy(e);
@@ -1011,6 +1011,21 @@ int merlin_stage_tables_bwd(const float *W2, const float *HT, const float *dT2, 
     if (rc != MERLIN_OK) return rc;
     HIP_TRY(merlin::launch_stage_bwd(W2, HT, dT2, atlas, koff, kv, towers, dH, dW1, db1, dW2, ws->stage_part,
                                      (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int64_t merlin_window_gemm_bwd_work(int32_t towers, int64_t nw) {
+    if (towers < 1 || towers > 2 || nw <= 0) return -1;
+    return merlin::winbwd_work_floats(towers, nw);
+}
+
+int merlin_window_gemm_bwd(const float *a2w, const float *dQ, const float *W3r, int32_t towers, int64_t nw,
+                           float *da2w, float *db2, float *dW3r, float *work, int64_t work_floats, void *stream) {
+    if (!a2w || !dQ || !W3r || !da2w || !db2 || !dW3r || !work) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (nw <= 0) return fail(MERLIN_E_INVALID, "nw must be > 0");
+    if (work_floats < merlin::winbwd_work_floats(towers, nw)) return fail(MERLIN_E_INVALID, "work too small");
+    HIP_TRY(merlin::launch_winbwd(a2w, dQ, W3r, towers, nw, da2w, db2, dW3r, work, (hipStream_t)stream));
     return MERLIN_OK;
 }
 

@@ -27,7 +27,8 @@ namespace merlin {
 namespace {
 
 constexpr int BLK = 64;    // reset kernels: one wave per block (map generation is long and divergent)
-constexpr int SBLK = 256;  // step kernel: 4 waves per block
+constexpr int SBLK = 128;  // step kernel: 2 waves per block (4096 envs: rollout 21.43 vs 21.90 ms at 256, r05ag_*)
+static_assert(SBLK % BLK == 0 && SBLK >= 64, "step blocks: whole waves; one bflag each (merlin_capi.hip: n / 64)");
 
 // ---------------------------------------------------------------------------
 // numpy PCG64 + bounded integers
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(BLK) void k_env_fallback(EnvDev E, uint32_t *__rest
 }
 
 // DEFER (single-step launches): a reset takes the env's look-ahead slot; when the slot is empty the env
-// is flagged (rflag, and its 256-env block in bflag) and k_env_fallback, launched next on the stream,
+// is flagged (rflag, and its SBLK-env block in bflag) and k_env_fallback, launched next on the stream,
 // generates its map and writes its observation, so this kernel carries no generator (lean registers).
 template <int SP, bool DEFER>
 __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {

@@ -24,7 +24,7 @@ namespace merlin {
 //           pg_agent uint4[n] (agent format above), pg_rng_s / pg_rng_b (RNG state after it),
 //           pg_valid uint8[n] (1 = the slot holds the env's next map)
 //   rflag   uint8[n]        1 = reset due, its slot was empty (single-step launch; k_env_fallback)
-//   bflag   uint8[ceil(n/256)] 1 = some env of that 256-env step block is flagged
+//   bflag   uint8[ceil(n/64)] 1 = some env of that step block (SBLK envs, merlin_env.hip) is flagged
 struct EnvDev {
     int n, size, sp, difficulty, max_steps;
     int stuck_on, max_stay;
@@ -268,6 +268,10 @@ hipError_t launch_stage_fwd(const float *W1, const float *b1, const float *W2, c
 hipError_t launch_stage_bwd(const float *W2, const float *HT, const float *dT2, const float *atlas,
                             const int16_t *koff, const int16_t *kv, int T, float *dH, float *dW1, float *db1,
                             float *dW2, double *ws, hipStream_t s);
+// the window GEMM's backward (csrc/merlin_winbwd.hip): work = winbwd_work_floats(T, nw) floats of scratch
+int64_t winbwd_work_floats(int T, int64_t nw);
+hipError_t launch_winbwd(const float *a2w, const float *dQ, const float *W3r, int T, int64_t nw, float *da2w,
+                         float *db2, float *dW3r, float *work, hipStream_t s);
 // k_stage_bwd_w's partials (towers x taps x parts x outputs)
 constexpr size_t STAGE_WS_DOUBLES = 2 * 4 * 10 * 2048;
 hipError_t launch_heads_fwd(const float *h, int64_t n, int H, const float *wa, int A, const float *wc, const float *ba,

@@ -163,6 +163,9 @@ def lib():
     L.merlin_act_draw.argtypes = [vp, i32, i64, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp, vp]
     L.merlin_stage_tables_fwd.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_stage_tables_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
+    L.merlin_window_gemm_bwd_work.argtypes = [i32, i64]
+    L.merlin_window_gemm_bwd_work.restype = i64
+    L.merlin_window_gemm_bwd.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp, vp, i64, vp]
     check_env_config_layout(L)
     _lib = L
     return L
@@ -210,7 +213,7 @@ EXPORTED_SYMBOLS = (
     "merlin_h3_gemm_nt_heads", "merlin_h3_heads_parts", "merlin_heads_combine", "merlin_act_draw",
     "merlin_ppo_loss_absmax", "merlin_tower_head_bwd_planes", "merlin_h3_gemm_nt_planes",
     "merlin_h3_gemm_tn_gather_planes_a", "merlin_h3_gemm_nt_heads_planes", "merlin_h3_gemm_tn_gather_planes",
-    "merlin_tower_window_conv3_planes",
+    "merlin_tower_window_conv3_planes", "merlin_window_gemm_bwd_work", "merlin_window_gemm_bwd",
 )
 
 
@@ -838,6 +841,32 @@ def relu_bwd(y, dy, out=None, out_bias=None):
         check(lib().merlin_tower_relu_bwd(ptr(y), ptr(dy), ptr(dz), rows, cols, T, ptr(db), stream_of(y)),
               "merlin_tower_relu_bwd")
     return dz, db
+
+
+_WINBWD_WORK = {}
+
+
+def window_gemm_bwd(a2w, dQ, W3r, out_da2w=None, out_db2=None, out_dW3r=None):
+    """The window GEMM's backward (merlin_window_gemm_bwd): a2w f32[T, nw, 64], dQ f32[T, nw, 576], W3r f32[T, 64,
+    576] -> (da2w = [a2w > 0] * dQ W3r^T, db2 = its column sums f32[T, 64], dW3r = a2w^T dQ f32[T, 64, 576])."""
+    T, nw, ci = (int(v) for v in a2w.shape)
+    assert ci == 64 and dQ.shape == (T, nw, 576) and W3r.shape == (T, 64, 576)
+    assert all(x.dtype == torch.float32 and x.is_contiguous() for x in (a2w, dQ, W3r))
+    dev = a2w.device
+    da2w = torch.empty_like(a2w) if out_da2w is None else out_da2w
+    db2 = torch.empty((T, 64), dtype=torch.float32, device=dev) if out_db2 is None else out_db2
+    dW3r = torch.empty((T, 64, 576), dtype=torch.float32, device=dev) if out_dW3r is None else out_dW3r
+    assert da2w.shape == a2w.shape and db2.shape == (T, 64) and dW3r.shape == (T, 64, 576)
+    assert all(x.dtype == torch.float32 and x.is_contiguous() for x in (da2w, db2, dW3r))
+    need = int(lib().merlin_window_gemm_bwd_work(T, nw))
+    key = (dev, T)
+    work = _WINBWD_WORK.get(key)
+    if work is None or work.numel() < need:  # grown once to the largest window count seen (no free inside a capture)
+        work = _WINBWD_WORK[key] = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=dev)
+    with KernelTimer.span("k_winbwd", (2 * T * nw * (64 + 576) + T * 64 * 576) * 4):
+        check(lib().merlin_window_gemm_bwd(ptr(a2w), ptr(dQ), ptr(W3r), T, nw, ptr(da2w), ptr(db2), ptr(dW3r),
+                                           ptr(work), int(work.numel()), stream_of(a2w)), "merlin_window_gemm_bwd")
+    return da2w, db2, dW3r
 
 
 def colsum(x, out=None):

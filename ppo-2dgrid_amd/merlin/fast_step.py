@@ -198,6 +198,10 @@ MAIN_PRIORITY = 0
 # (two reductions per step) they measured 200.8 vs 199.5 ms per update (scripts/ab_update.py 4 6 fast,fast_nowh3,
 # weight stage captured with the planes either way)
 WINDOW_H3 = False
+# the window GEMM's backward (da2w with conv2's ReLU mask and db2, dW3r) as merlin_window_gemm_bwd: exact-f32 MFMA
+# kernels, one launch + a fold (False: hipBLASLt's input-gradient GEMM, the split-K weight gradient and its torch sum,
+# the ReLU backward: 137.6 us standalone at the bench's 6,571 windows, scripts/probe_window_bwd.py)
+WINDOW_BWD_HIP = True
 # h3: the weight gradient over the planes the NT GEMMs left (False: it splits a3, dz itself).  Off: the planes cost the
 # forward 60-100 us of writes (a3: 2 x U x 576 x 4 B) for 50 us saved in the weight gradient (scripts/probe_h3.py)
 WGRAD_PLANES = False
@@ -452,11 +456,14 @@ class WindowStep:
             nat.h3_amax(dQ, out=amq)
             da2w = nat.h3_gemm_nt(dQ, amq, P3, amW3, cfg=nat.H3_NT_CFG["qwin_dgrad"], name="gemm_window_dgrad")
             nat.h3_gemm_tn(a2w, am2, dQ, amq, cfg=nat.H3_TN_CFG_WIN, name="gemm_window_wgrad", out=g[2])
+        elif WINDOW_BWD_HIP:  # both products, the ReLU mask and db2 in one launch + an ordered fold
+            da2w, _, _ = nat.window_gemm_bwd(a2w, dQ, W3r, out_db2=g[1], out_dW3r=g[2])
         else:
             da2w = torch.bmm(dQ, W3r.transpose(1, 2))
             chunks = max(1, a2w.shape[1] // 256)
             _splitk_bmm_tn(a2w, dQ, chunks, min_chunk=128, name="gemm_window_wgrad", out=g[2])
-        nat.relu_bwd(a2w, da2w, out=da2w, out_bias=g[1])
+        if wh3 or not WINDOW_BWD_HIP:
+            nat.relu_bwd(a2w, da2w, out=da2w, out_bias=g[1])
         nat.segment_sum(da2w, plan.hist, nat.LUT2_ROWS, name="k_seg_sum_dT2", out=g[0])
         main.wait_stream(side)
         self.stage.backward()

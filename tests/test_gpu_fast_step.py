@@ -45,6 +45,7 @@ def test_fast_step_matches_autograd_bitwise(device, monkeypatch):
     # the autograd path runs the window GEMMs on hipBLASLt: the same GEMMs here (the h3 form of them is held to
     # fp32-GEMM accuracy by tests/test_gpu_h3.py and to the autograd path by the test below)
     monkeypatch.setattr(fast_step, "WINDOW_H3", False)
+    monkeypatch.setattr(fast_step, "WINDOW_BWD_HIP", False)  # its own bounds: tests/test_gpu_window_bwd.py
     # and dz in fp32 as the autograd path has it (the bound-scaled planes: tests/test_gpu_dz_planes.py)
     monkeypatch.setattr(fast_step, "DZ_PLANES", False)
     a0, s0 = _run(device, False)
