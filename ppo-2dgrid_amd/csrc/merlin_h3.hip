@@ -1623,7 +1623,7 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
 #define H3_NT(BM, BN, WM, WN, PIPE) \
     nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, hd, s, \
                                     a_is_planes)
-    if (a_is_planes && (cfg < 10 || cfg > 13) && cfg != 60) return hipErrorInvalidValue;
+    if (a_is_planes && (cfg < 10 || cfg > 14) && cfg != 60) return hipErrorInvalidValue;
     if (cfg >= 60 && cfg < 70) {  // both operands as plane images (merlin_h3p.hip)
         if (P || ((a_rows || head_part) && !a_is_planes)) return hipErrorInvalidValue;
         return launch_h3p_gemm_nt(A, amaxA, B, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, cfg, s, a_rows,
@@ -1640,6 +1640,7 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 11: return H3_NT(128, 192, 4, 2, true);
         case 12: return H3_NT(128, 128, 2, 2, true);
         case 13: return H3_NT(128, 256, 2, 4, true);
+        case 14: return H3_NT(64, 128, 2, 2, true);  // twice cfg 12's blocks (the rollout's 4096-row fc1)
 #undef H3_NT
         // k_h3_ntg: both operands staged by LDS-DMA, three k steps deep
 #define H3_NTG(BM, BN, WM, WN, KP) \
@@ -1761,6 +1762,7 @@ int h3_heads_parts(int N, int cfg) {
         // cfg 11: 96-column wave tiles, no heads epilogue
         case 12: return N % 128 ? 0 : N / 128 * 2;
         case 13: return N % 256 ? 0 : N / 256 * 4;
+        case 14: return N % 128 ? 0 : N / 128 * 2;
         case 60: return N % 256 ? 0 : N / 256 * 4;  // k_h3_pqg (planes, gathered rows): cfg 13's tiles
         default: return 0;
     }

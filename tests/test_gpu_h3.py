@@ -58,6 +58,7 @@ def _operands(device, M, N, K, seed, scale_a=1.0, ragged=False):
 
 @pytest.mark.parametrize("N,K,cfg", [(512, 576, 0), (576, 512, 1), (512, 576, 2), (576, 512, 2), (512, 576, 3),
                                      (512, 576, 10), (576, 512, 11), (512, 576, 12), (576, 512, 12), (512, 576, 13),
+                                     (512, 576, 14),
                                      (512, 576, 20), (576, 512, 21), (512, 576, 30), (576, 512, 31)])
 @pytest.mark.parametrize("M,scale_a,ragged", [(1, 1.0, False), (777, 1.0, False), (20011, 1.0, False),
                                               (20011, 1e-7, False), (9999, 1.0, True)])
@@ -173,7 +174,7 @@ def test_gemm_tn_gather_rows_bitwise(device, Kd, splits, cfg):
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("cfg,gather", [(13, False), (13, True), (12, False), (10, True)])
+@pytest.mark.parametrize("cfg,gather", [(13, False), (13, True), (12, False), (10, True), (14, False)])
 def test_gemm_nt_heads_epilogue(device, cfg, gather):
     """merlin_h3_gemm_nt_heads (the policy / value heads folded into the forward GEMM's epilogue): h bit for bit as
     the plain bias + ReLU GEMM, logits / value against a float64 product of that h with the head weights (error no
