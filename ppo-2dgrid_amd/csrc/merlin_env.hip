@@ -37,18 +37,24 @@ struct Rng {
     uint32_t has, buf;
 };
 
-__device__ __forceinline__ uint64_t rng_next64(Rng &r) {
+// the next output and the state after it, r unchanged
+__device__ __forceinline__ uint64_t rng_peek64(const Rng &r, uint64_t &nlo, uint64_t &hi) {
     // state = state * 0x2360ed051fc65da44385df649fccf645 + inc (mod 2^128), then XSL-RR
     const uint64_t MLO = 0x4385df649fccf645ULL, MHI = 0x2360ed051fc65da4ULL;
-    uint64_t lo = r.slo * MLO;
-    uint64_t hi = __umul64hi(r.slo, MLO) + r.slo * MHI + r.shi * MLO;
-    uint64_t nlo = lo + r.ilo;
+    const uint64_t lo = r.slo * MLO;
+    hi = __umul64hi(r.slo, MLO) + r.slo * MHI + r.shi * MLO;
+    nlo = lo + r.ilo;
     hi += r.ihi + (nlo < lo ? 1ULL : 0ULL);
+    const uint64_t x = hi ^ nlo;
+    const unsigned rot = (unsigned)(hi >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+__device__ __forceinline__ uint64_t rng_next64(Rng &r) {
+    uint64_t nlo, hi;
+    const uint64_t v = rng_peek64(r, nlo, hi);
     r.slo = nlo;
     r.shi = hi;
-    uint64_t x = hi ^ nlo;
-    unsigned rot = (unsigned)(hi >> 58);
-    return (x >> rot) | (x << ((64u - rot) & 63u));
+    return v;
 }
 
 __device__ __forceinline__ uint32_t rng_next32(Rng &r) {
@@ -84,6 +90,27 @@ __device__ __forceinline__ int rng_int(R &r, int lo, int hi) {
     uint32_t rng = (uint32_t)(hi - lo - 1);
     if (rng == 0u) return lo;
     return lo + (int)rng_lemire(r, rng);
+}
+
+// x = integers(0, S); y = integers(0, S) (place_obj over the whole grid) with ONE PCG64 step on the common path: the
+// pair's 32-bit draws are the buffered half and the next output's low half (has = 1) or both halves of it (has = 0),
+// so the lanes of a wave no longer diverge on which of them needs a fresh output; a pair Lemire would not accept at
+// once (low product word < S, probability < 2^-27) takes the two sequential draws from the unchanged state
+__device__ __forceinline__ void rng_xy(Rng &r, int S, int &x, int &y) {
+    uint64_t nlo, hi;
+    const uint64_t v = rng_peek64(r, nlo, hi);
+    const uint32_t u1 = r.has ? r.buf : (uint32_t)v, u2 = r.has ? (uint32_t)v : (uint32_t)(v >> 32);
+    const uint64_t m1 = (uint64_t)u1 * (uint32_t)S, m2 = (uint64_t)u2 * (uint32_t)S;
+    if ((uint32_t)m1 >= (uint32_t)S && (uint32_t)m2 >= (uint32_t)S) {
+        r.slo = nlo;
+        r.shi = hi;
+        r.buf = (uint32_t)(v >> 32);  // has: as it was (two halves drawn)
+        x = (int)(m1 >> 32);
+        y = (int)(m2 >> 32);
+        return;
+    }
+    x = rng_int(r, 0, S);
+    y = rng_int(r, 0, S);
 }
 
 __device__ __forceinline__ Rng load_rng(const EnvDev &E, int i) {
@@ -279,8 +306,8 @@ struct Grid {
                     return;
                 }
                 tries++;
-                const int x = rng_int(r, 0, S);
-                const int y = rng_int(r, 0, S);
+                int x, y;
+                rng_xy(r, S, x, y);
                 if (occupied(x, y) || (x == ax && y == ay)) continue;
                 set_wall(x, y);
                 k++;
