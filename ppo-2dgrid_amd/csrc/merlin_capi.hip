@@ -1014,6 +1014,14 @@ int merlin_stage_tables_bwd(const float *W2, const float *HT, const float *dT2, 
     return MERLIN_OK;
 }
 
+int merlin_window_gemm_fwd(const float *a2w, const float *W3r, int32_t towers, int64_t nw, float *Q, void *stream) {
+    if (!a2w || !W3r || !Q) return fail(MERLIN_E_INVALID, "null argument");
+    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
+    if (nw < 0) return fail(MERLIN_E_INVALID, "nw must be >= 0");
+    HIP_TRY(merlin::launch_winfwd(a2w, W3r, towers, nw, Q, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
 int64_t merlin_window_gemm_bwd_work(int32_t towers, int64_t nw) {
     if (towers < 1 || towers > 2 || nw <= 0) return -1;
     return merlin::winbwd_work_floats(towers, nw);

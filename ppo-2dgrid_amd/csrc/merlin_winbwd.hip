@@ -1,4 +1,4 @@
-// merlin_winbwd.hip -- the backward of the window GEMM Q = a2w W3r (conv3 seen per window: a2w [T][nw][64] the
+// merlin_winbwd.hip -- the window GEMM Q = a2w W3r (k_winfwd) and its backward (conv3 seen per window: a2w [T][nw][64] the
 // relu(conv2) rows of the update's windows, W3r [T][64][576] conv3's weights as (ci) x (tap, co), src/actor_critic.py
 // :13 conv3) in one launch plus an ordered fold, replacing hipBLASLt's input-gradient GEMM, the split-K weight
 // gradient's batched GEMMs + torch sum, and the ReLU backward with its bias-gradient column sums (merlin/fast_step.py;
@@ -147,7 +147,61 @@ __global__ __launch_bounds__(256) void k_winbwd_fold(const float *__restrict__ c
     if (lane == 0) db2[k] = s;
 }
 
+// The forward Q = a2w W3r [T][nw][576] (hipBLASLt's fp32 GEMM before, 22.7 us in the r05h step sequence): one wave per
+// 32 x 64 output tile, K = 64: A = a2w rows by 16-B runs of k, B[k][j] = W3r[k][j] one coalesced row per lane half;
+// k slot h of step s of an 8-k iteration is k = k0 + 4 h + s for both operands (as the input gradient above)
+__global__ __launch_bounds__(64) void k_winfwd(const float *__restrict__ a2w, const float *__restrict__ W3r, int64_t nw,
+                                               float *__restrict__ Q) {
+    const int lane = threadIdx.x, fr = lane & 31, fh = lane >> 5;
+    const int64_t rt = (nw + 31) / 32;
+    const int b = blockIdx.x, per_t = (int)rt * 9, t = b / per_t, rem = b - t * per_t;
+    const int64_t tile = rem / 9;
+    const int jt = rem % 9;
+    const int64_t w0 = tile * 32, wr = std::min<int64_t>(w0 + fr, nw - 1);
+    const float4 *A = reinterpret_cast<const float4 *>(a2w + ((size_t)t * nw + wr) * WB_CI) + fh;
+    const float *B = W3r + (size_t)t * WB_CI * WB_CJ + jt * 64 + fr;
+    float4 ra[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) ra[i] = A[2 * i];
+    float rb[8][4][2];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = 8 * i + 4 * fh + u;
+            rb[i][u][0] = B[(size_t)k * WB_CJ];
+            rb[i][u][1] = B[(size_t)k * WB_CJ + 32];
+        }
+    wb_f32x16 acc = {}, acc2 = {};
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const float av[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            acc = wb_mfma(av[u], rb[i][u][0], acc);
+            acc2 = wb_mfma(av[u], rb[i][u][1], acc2);
+        }
+    }
+    float *Qt = Q + (size_t)t * nw * WB_CJ + jt * 64 + fr;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int64_t row = w0 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        if (row < nw) {
+            Qt[(size_t)row * WB_CJ] = acc[r];
+            Qt[(size_t)row * WB_CJ + 32] = acc2[r];
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_winfwd(const float *a2w, const float *W3r, int T, int64_t nw, float *Q, hipStream_t s) {
+    if (nw <= 0 || T < 1) return nw == 0 ? hipSuccess : hipErrorInvalidValue;
+    const int64_t nb = (int64_t)T * ((nw + 31) / 32) * 9;
+    if (nb > INT32_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_winfwd, dim3((unsigned)nb), dim3(64), 0, s, a2w, W3r, nw, Q);
+    return hipGetLastError();
+}
 
 int64_t winbwd_work_floats(int T, int64_t nw) {
     const int64_t rt = (nw + 31) / 32, splits = (nw + WB_SPLIT - 1) / WB_SPLIT;

@@ -163,6 +163,7 @@ def lib():
     L.merlin_act_draw.argtypes = [vp, i32, i64, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp, vp]
     L.merlin_stage_tables_fwd.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp]
     L.merlin_stage_tables_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
+    L.merlin_window_gemm_fwd.argtypes = [vp, vp, i32, i64, vp, vp]
     L.merlin_window_gemm_bwd_work.argtypes = [i32, i64]
     L.merlin_window_gemm_bwd_work.restype = i64
     L.merlin_window_gemm_bwd.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp, vp, i64, vp]
@@ -214,6 +215,7 @@ EXPORTED_SYMBOLS = (
     "merlin_ppo_loss_absmax", "merlin_tower_head_bwd_planes", "merlin_h3_gemm_nt_planes",
     "merlin_h3_gemm_tn_gather_planes_a", "merlin_h3_gemm_nt_heads_planes", "merlin_h3_gemm_tn_gather_planes",
     "merlin_tower_window_conv3_planes", "merlin_window_gemm_bwd_work", "merlin_window_gemm_bwd",
+    "merlin_window_gemm_fwd",
 )
 
 
@@ -841,6 +843,19 @@ def relu_bwd(y, dy, out=None, out_bias=None):
         check(lib().merlin_tower_relu_bwd(ptr(y), ptr(dy), ptr(dz), rows, cols, T, ptr(db), stream_of(y)),
               "merlin_tower_relu_bwd")
     return dz, db
+
+
+def window_gemm_fwd(a2w, W3r, out=None):
+    """Q = a2w W3r (merlin_window_gemm_fwd): a2w f32[T, nw, 64], W3r f32[T, 64, 576] -> f32[T, nw, 576]."""
+    T, nw, ci = (int(v) for v in a2w.shape)
+    assert ci == 64 and W3r.shape == (T, 64, 576) and a2w.dtype == W3r.dtype == torch.float32
+    assert a2w.is_contiguous() and W3r.is_contiguous()
+    Q = torch.empty((T, nw, 576), dtype=torch.float32, device=a2w.device) if out is None else out
+    assert Q.shape == (T, nw, 576) and Q.is_contiguous()
+    with KernelTimer.span("gemm_window_fwd", 0, flops=2 * T * nw * 64 * 576):
+        check(lib().merlin_window_gemm_fwd(ptr(a2w), ptr(W3r), T, nw, ptr(Q), stream_of(a2w)),
+              "merlin_window_gemm_fwd")
+    return Q
 
 
 _WINBWD_WORK = {}

@@ -198,9 +198,10 @@ MAIN_PRIORITY = 0
 # (two reductions per step) they measured 200.8 vs 199.5 ms per update (scripts/ab_update.py 4 6 fast,fast_nowh3,
 # weight stage captured with the planes either way)
 WINDOW_H3 = False
-# the window GEMM's backward (da2w with conv2's ReLU mask and db2, dW3r) as merlin_window_gemm_bwd: exact-f32 MFMA
-# kernels, one launch + a fold (False: hipBLASLt's input-gradient GEMM, the split-K weight gradient and its torch sum,
-# the ReLU backward: 137.6 us standalone at the bench's 6,571 windows, scripts/probe_window_bwd.py)
+# the window GEMM (Q = a2w W3r, merlin_window_gemm_fwd) and its backward (da2w with conv2's ReLU mask and db2, dW3r,
+# merlin_window_gemm_bwd) on exact-f32 MFMA kernels, the backward in one launch + a fold (False: hipBLASLt's GEMMs,
+# the split-K weight gradient and its torch sum, the ReLU backward: 137.6 us standalone at the bench's 6,571 windows,
+# scripts/probe_window_bwd.py)
 WINDOW_BWD_HIP = True
 # h3: the weight gradient over the planes the NT GEMMs left (False: it splits a3, dz itself).  Off: the planes cost the
 # forward 60-100 us of writes (a3: 2 x U x 576 x 4 B) for 50 us saved in the weight gradient (scripts/probe_h3.py)
@@ -338,6 +339,8 @@ class WindowStep:
             am2, amq, amW3 = self.amax_win[0:2], self.amax_win[2:4], self.stage.amaxW3
             nat.h3_amax(a2w, out=am2)
             Q = nat.h3_gemm_nt(a2w, am2, P3t, amW3, cfg=nat.H3_NT_CFG["qwin"], name="gemm_window_fwd")
+        elif WINDOW_BWD_HIP:  # the same exact-f32 MFMA kernels as its backward (csrc/merlin_winbwd.hip)
+            Q = nat.window_gemm_fwd(a2w, W3r)  # [2, windows, (ky, kx, co)]
         else:
             Q = torch.bmm(a2w, W3r)  # [2, windows, (ky, kx, co)]
         split_side = h3 and WGRAD_SPLIT_SIDE and WGRAD_SIDE and not WGRAD_EARLY

@@ -1,5 +1,5 @@
-"""GPU: the window GEMM's backward (csrc/merlin_winbwd.hip, merlin_window_gemm_bwd; the conv3-per-window part of
-src/actor_critic.py:13's backward in merlin/fast_step.py): da2w = [a2w > 0] * dQ W3r^T, db2 = its column sums,
+"""GPU: the window GEMM's backward and forward (csrc/merlin_winbwd.hip, merlin_window_gemm_bwd / _fwd; the
+conv3-per-window part of src/actor_critic.py:13 in merlin/fast_step.py): da2w = [a2w > 0] * dQ W3r^T, db2 = its column sums,
 dW3r = a2w^T dQ, against float64 products of the same fp32 operands.  Each output's error relative to the sum of
 |products| may be no larger than torch's own fp32 GEMM's on the same operands (floor: one fp32 product, 2^-23); the
 mask is exact; two calls give the same bits.  Window counts: one window, tile edges (31 / 32 / 33), split edges
@@ -49,6 +49,23 @@ def test_window_gemm_bwd_vs_float64(device, T, nw):
     # fixed order: the same bits again
     again = nat.window_gemm_bwd(a2w, dQ, W3r)
     assert all(torch.equal(x, y) for x, y in zip(again, (da2w, db2, dW3r)))
+
+
+@pytest.mark.parametrize("T,nw", [(2, 1), (2, 33), (1, 256), (2, 6571)])
+def test_window_gemm_fwd_vs_float64(device, T, nw):
+    """Q = a2w W3r (merlin_window_gemm_fwd, the forward of the same window GEMM)."""
+    from merlin import _native as nat
+
+    g = torch.Generator(device=device).manual_seed(3 * nw + T)
+    a2w = torch.relu(torch.randn(T, nw, 64, device=device, generator=g))
+    a2w[:, ::5] *= 1e-5
+    W3r = torch.randn(T, 64, 576, device=device, generator=g) * 0.05
+    Q = nat.window_gemm_fwd(a2w, W3r)
+    Q64 = torch.bmm(a2w.double(), W3r.double())
+    den = torch.bmm(a2w.abs().double(), W3r.abs().double())
+    tol = max(_err(torch.bmm(a2w, W3r), Q64, den), FLOOR)
+    assert _err(Q, Q64, den) <= 2 * tol
+    assert torch.equal(nat.window_gemm_fwd(a2w, W3r), Q)
 
 
 def test_window_gemm_bwd_rejects_bad_arguments(device):
