@@ -1703,7 +1703,7 @@ hipError_t launch_h3_gemm_tn(const void *A, const uint32_t *amaxA, const void *B
     }
     int S = 1;
     hipError_t e;
-    if (cfg == 20) {  // both operands as planes, B gathered, LDS-DMA staged (merlin_h3p.hip k_h3_tq)
+    if (cfg == 20 || cfg == 21) {  // both operands as planes, B gathered, LDS-DMA staged (merlin_h3p.hip k_h3_tq)
         if (!(a_planes && b_planes)) return hipErrorInvalidValue;
         e = launch_h3p_gemm_tn_gather(A, amaxA, B, amaxB, Kd, M, N, T, a_stride, b_stride, splits, slab, b_rows, cfg,
                                       &S, s);

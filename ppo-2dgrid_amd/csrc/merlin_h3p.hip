@@ -282,7 +282,7 @@ __device__ __forceinline__ void p_dma4(const void *src, uint32_t lds) {
 
 template <int RC>
 __device__ __forceinline__ int p_tr_swz(int row) {
-    static_assert(RC % 16 == 0 || RC == 24, "row chunks");
+    static_assert(RC % 16 == 0 || RC == 24 || RC == 8, "row chunks");  // 8 (128-B rows): as 24
     return RC % 16 == 0 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
 }
 typedef __bf16 p_bf16x4 __attribute__((ext_vector_type(4)));
@@ -781,17 +781,27 @@ hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *
 hipError_t launch_h3p_gemm_tn_gather(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB,
                                      int64_t Kd, int M, int N, int T, int64_t a_stride, int64_t b_stride, int splits,
                                      float *slab, const int32_t *b_rows, int cfg, int *S_out, hipStream_t s) {
-    constexpr int BM = 128, BN = 192, BK = 32;
-    if (cfg != 20 || M % BM || N % BN || N % 64 || a_stride % 4 || b_stride % 4 || !b_rows) return hipErrorInvalidValue;
+    // cfg 20: 128 x 192 tiles, 8 waves (the whole CU: 256 VGPRs x 2 waves per SIMD, 126 KB of LDS); cfg 21: 64 x 192,
+    // 4 waves of the same wave tile (one per SIMD, ~99 KB of LDS), which leaves half of each SIMD's registers to
+    // kernels queued beside it (conv3's backward sums)
+    const int BM = cfg == 21 ? 64 : 128;
+    constexpr int BN = 192, BK = 32;
+    if ((cfg != 20 && cfg != 21) || M % BM || N % BN || N % 64 || a_stride % 4 || b_stride % 4 || !b_rows)
+        return hipErrorInvalidValue;
     const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
     int S = std::max(1, splits);
     int64_t kc = (Kd + S - 1) / S;
     kc = (kc + BK - 1) / BK * BK;
     S = (int)std::max<int64_t>(1, (Kd + kc - 1) / kc);
     *S_out = S;
-    hipLaunchKernelGGL((k_h3_tq<BM, BN, 4, 2>), dim3(tiles * S * T), dim3(512), 0, s, static_cast<const p_u32x4 *>(A),
-                       static_cast<const p_u32x4 *>(B), amaxA, amaxB, Kd, M, N, a_stride / 4, b_stride / 4, kc,
-                       tiles_n, tiles, S, slab, b_rows);
+    if (cfg == 21)
+        hipLaunchKernelGGL((k_h3_tq<64, BN, 2, 2>), dim3(tiles * S * T), dim3(256), 0, s,
+                           static_cast<const p_u32x4 *>(A), static_cast<const p_u32x4 *>(B), amaxA, amaxB, Kd, M, N,
+                           a_stride / 4, b_stride / 4, kc, tiles_n, tiles, S, slab, b_rows);
+    else
+        hipLaunchKernelGGL((k_h3_tq<128, BN, 4, 2>), dim3(tiles * S * T), dim3(512), 0, s,
+                           static_cast<const p_u32x4 *>(A), static_cast<const p_u32x4 *>(B), amaxA, amaxB, Kd, M, N,
+                           a_stride / 4, b_stride / 4, kc, tiles_n, tiles, S, slab, b_rows);
     return hipGetLastError();
 }
 

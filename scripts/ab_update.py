@@ -75,7 +75,7 @@ def main():
             FS.A3_PLANES = "noa3p" not in name  # a3 in fp32 instead of conv3's planes
             FS.PREFILL = "noprefill" not in name  # conv3's backward fills beside the weight gradient
             FS.WINDOW_BWD_HIP = "nowinbwd" not in name  # the window GEMM's backward on hipBLASLt + torch
-            nat.H3_TN_CFG_PLANES = 0 if "tngplanes" in name else 20  # the register-staged TN over the planes
+            nat.H3_TN_CFG_PLANES = 0 if "tngplanes" in name else 21 if "tq21" in name else 20  # register-staged / 64-row
             nat.H3_NT_CFG["fwd_planes"] = 13 if "ntpgplanes" in name else 60  # the copy-staged forward over planes
             nat.H3_NT_CFG["dgrad_planes"] = next((int(t[3:]) for t in name.split("_") if t[:3] == "h3p"), 62)
             nat.X6_NT_CFG["fwd"] = 28 if "fwd28" in name else 20

@@ -207,11 +207,13 @@ def test_forward_and_wgrad_over_a3_planes(device):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("cfg", [20, 21])
 @pytest.mark.parametrize("Kd,splits", [(1, 1), (31, 1), (257, 3), (3001, 32), (40000, 32), (111111, 32)])
-def test_wgrad_dma_kernel_bitwise(device, Kd, splits):
-    """The weight gradient's LDS-DMA TN kernel over both operands' planes (cfg 20, k_h3_tq: B's rows through a row
-    map read from an LDS ring, rows past a split's end zero-sourced, the step count padded to the ring's period) ==
-    the register-staged TN on the same planes (cfg 0), bit for bit; split-K and ragged row counts."""
+def test_wgrad_dma_kernel_bitwise(device, Kd, splits, cfg):
+    """The weight gradient's LDS-DMA TN kernel over both operands' planes (cfg 20 / 21, k_h3_tq on 128 / 64 x 192
+    tiles: B's rows through a row map read from an LDS ring, rows past a split's end zero-sourced, the step count
+    padded to the ring's period) == the register-staged TN on the same planes (cfg 0), bit for bit; split-K and
+    ragged row counts."""
     from merlin import _native as nat
 
     g = torch.Generator(device=device).manual_seed(Kd + splits)
@@ -222,5 +224,5 @@ def test_wgrad_dma_kernel_bitwise(device, Kd, splits):
     amz, am3 = nat.h3_amax(dz), nat.h3_amax(a3)
     dzp, a3p = nat.h3_split(dz, amz), nat.h3_split(a3, am3)
     ref = nat.h3_gemm_tn(dzp, amz, a3p, am3, splits=splits, cfg=0, rows=rows)
-    got = nat.h3_gemm_tn(dzp, amz, a3p, am3, splits=splits, cfg=20, rows=rows)
+    got = nat.h3_gemm_tn(dzp, amz, a3p, am3, splits=splits, cfg=cfg, rows=rows)
     assert torch.equal(got, ref)
