@@ -657,14 +657,15 @@ int merlin_h3_gemm_tn_gather(const float *A_dev, const uint32_t *amax_a_dev, con
  * replacing CNNActorCritic's bmm / split-K bmm / relu backward in merlin/fast_step.py), csrc/merlin_winbwd.hip.
  * Per tower t < towers: a2w f32[t][nw][64] (relu(conv2) of the windows), dQ f32[t][nw][576], W3r f32[t][64][576] ->
  * da2w = [a2w > 0] * (dQ W3r^T) f32[t][nw][64], db2 = column sums of da2w f32[t][64], dW3r = a2w^T dQ
- * f32[t][64][576].  exact-f32 MFMA products and sums, fixed order (bitwise reproducible).  work: scratch of at least
+ * f32[t][64][576]; db3 (nullable) = column sums of dQ's first 64 columns f32[t][64] (tap 0: conv3's bias gradient).
+ * exact-f32 MFMA products and sums, fixed order (bitwise reproducible).  work: scratch of at least
  * merlin_window_gemm_bwd_work(towers, nw) floats (-1: invalid arguments). */
 int merlin_window_gemm_fwd(const float *a2w_dev, const float *W3r_dev, int32_t towers, int64_t nw, float *Q_dev,
                            void *stream);  /* Q = a2w W3r f32[t][nw][576], exact-f32 MFMA, fixed order */
 int64_t merlin_window_gemm_bwd_work(int32_t towers, int64_t nw);
 int merlin_window_gemm_bwd(const float *a2w_dev, const float *dQ_dev, const float *W3r_dev, int32_t towers, int64_t nw,
-                           float *da2w_dev, float *db2_dev, float *dW3r_dev, float *work_dev, int64_t work_floats,
-                           void *stream);
+                           float *da2w_dev, float *db2_dev, float *dW3r_dev, float *db3_dev, float *work_dev,
+                           int64_t work_floats, void *stream);
 int merlin_stage_tables_fwd(const float *W1_dev, const float *b1_dev, const float *W2_dev, const float *atlas_dev,
                             const int16_t *idx_dev, int32_t towers, float *HT_dev, float *T2_dev, void *stream);
 int merlin_stage_tables_bwd(const float *W2_dev, const float *HT_dev, const float *dT2_dev, const float *atlas_dev,

@@ -1028,12 +1028,13 @@ int64_t merlin_window_gemm_bwd_work(int32_t towers, int64_t nw) {
 }
 
 int merlin_window_gemm_bwd(const float *a2w, const float *dQ, const float *W3r, int32_t towers, int64_t nw,
-                           float *da2w, float *db2, float *dW3r, float *work, int64_t work_floats, void *stream) {
+                           float *da2w, float *db2, float *dW3r, float *db3, float *work, int64_t work_floats,
+                           void *stream) {
     if (!a2w || !dQ || !W3r || !da2w || !db2 || !dW3r || !work) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
     if (nw <= 0) return fail(MERLIN_E_INVALID, "nw must be > 0");
     if (work_floats < merlin::winbwd_work_floats(towers, nw)) return fail(MERLIN_E_INVALID, "work too small");
-    HIP_TRY(merlin::launch_winbwd(a2w, dQ, W3r, towers, nw, da2w, db2, dW3r, work, (hipStream_t)stream));
+    HIP_TRY(merlin::launch_winbwd(a2w, dQ, W3r, towers, nw, da2w, db2, dW3r, work, (hipStream_t)stream, db3));
     return MERLIN_OK;
 }
 

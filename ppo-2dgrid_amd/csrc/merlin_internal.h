@@ -271,7 +271,7 @@ hipError_t launch_stage_bwd(const float *W2, const float *HT, const float *dT2, 
 // the window GEMM's backward (csrc/merlin_winbwd.hip): work = winbwd_work_floats(T, nw) floats of scratch
 int64_t winbwd_work_floats(int T, int64_t nw);
 hipError_t launch_winbwd(const float *a2w, const float *dQ, const float *W3r, int T, int64_t nw, float *da2w,
-                         float *db2, float *dW3r, float *work, hipStream_t s);
+                         float *db2, float *dW3r, float *work, hipStream_t s, float *db3 = nullptr);
 hipError_t launch_winfwd(const float *a2w, const float *W3r, int T, int64_t nw, float *Q, hipStream_t s);
 // k_stage_bwd_w's partials (towers x taps x parts x outputs)
 constexpr size_t STAGE_WS_DOUBLES = 2 * 4 * 10 * 2048;

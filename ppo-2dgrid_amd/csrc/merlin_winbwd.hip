@@ -5,7 +5,7 @@
 // 137.6 us standalone at nw = 6,571, scripts/probe_window_bwd.py):
 //
 //   da2w[w][c] = [a2w[w][c] > 0] * sum_j dQ[w][j] W3r[c][j]     db2[c] = sum_w da2w[w][c]
-//   dW3r[c][j] = sum_w a2w[w][c] dQ[w][j]
+//   dW3r[c][j] = sum_w a2w[w][c] dQ[w][j]          (optionally db3[c] = sum_w dQ[w][c], tap 0: conv3's bias gradient)
 //
 // On the exact-f32 MFMA (v_mfma_f32_32x32x2_f32: every product and sum an f32 fmaf, fp32 GEMM arithmetic), one wave per
 // 32 x 32 (input gradient) or 32 x 64 (weight gradient, K split over the windows) output tile, operands straight from
@@ -36,7 +36,7 @@ __device__ __forceinline__ wb_f32x16 wb_mfma(float a, float b, wb_f32x16 c) {
 __global__ __launch_bounds__(64) void k_winbwd(const float *__restrict__ a2w, const float *__restrict__ dQ,
                                                const float *__restrict__ W3r, int64_t nw, int T, int nd, int splits,
                                                float *__restrict__ da2w, float *__restrict__ colpart,
-                                               float *__restrict__ wpart) {
+                                               float *__restrict__ wpart, float *__restrict__ tpart) {
     const int lane = threadIdx.x, fr = lane & 31, fh = lane >> 5;
     const int64_t rt = (nw + 31) / 32;
     wb_f32x16 acc = {};
@@ -91,6 +91,8 @@ __global__ __launch_bounds__(64) void k_winbwd(const float *__restrict__ a2w, co
     const float *Aw = a2w + (size_t)t * nw * WB_CI + ch * 32 + fr;        // A[c][w] = a2w[w][c]
     const float *Bw = dQ + (size_t)t * nw * WB_CJ + jt * 64 + fr;         // B[w][j] = dQ[w][j]
     wb_f32x16 acc2 = {};
+    float ts0 = 0.0f, ts1 = 0.0f;  // tap 0's column sums (j < 64: the conv3 bias gradient), in the (j0 = 0, c half 0) waves
+    const bool tap0 = tpart && jt == 0 && ch == 0;
     const int64_t nst = (k1 - k0 + 1) / 2;  // MFMA steps: rows k0 + 2 st + fh
     float pa[WB_PW], pb0[WB_PW], pb1[WB_PW];
     auto ld = [&](int64_t st, float &a, float &b0, float &b1) __attribute__((always_inline)) {
@@ -111,7 +113,19 @@ __global__ __launch_bounds__(64) void k_winbwd(const float *__restrict__ a2w, co
             if (st0 + u < nst) {
                 acc = wb_mfma(a, b0, acc);
                 acc2 = wb_mfma(a, b1, acc2);
+                if (tap0) {
+                    ts0 += b0;
+                    ts1 += b1;
+                }
             }
+        }
+    }
+    if (tap0) {  // the two row parities, then one store per column
+        ts0 += __shfl_xor(ts0, 32);
+        ts1 += __shfl_xor(ts1, 32);
+        if (fh == 0) {
+            tpart[((size_t)t * splits + s) * WB_CI + fr] = ts0;
+            tpart[((size_t)t * splits + s) * WB_CI + 32 + fr] = ts1;
         }
     }
     float *P = wpart + (((size_t)s * T + t) * WB_CI) * WB_CJ;
@@ -126,8 +140,9 @@ __global__ __launch_bounds__(64) void k_winbwd(const float *__restrict__ a2w, co
 // blocks [0, nb): dW3r = the splits' partials added in split order; then one wave per (tower, column): db2 = the
 // column partials, lane q adding tiles q, q + 64, ... in order, then a fixed butterfly
 __global__ __launch_bounds__(256) void k_winbwd_fold(const float *__restrict__ colpart, const float *__restrict__ wpart,
-                                                     int T, int64_t rt, int splits, int nb, float *__restrict__ db2,
-                                                     float *__restrict__ dW3r) {
+                                                     const float *__restrict__ tpart, int T, int64_t rt, int splits,
+                                                     int nb, float *__restrict__ db2, float *__restrict__ dW3r,
+                                                     float *__restrict__ db3) {
     if ((int)blockIdx.x < nb) {
         const int64_t n = (int64_t)T * WB_CI * WB_CJ, i = (int64_t)blockIdx.x * 256 + threadIdx.x;
         if (i >= n) return;
@@ -135,6 +150,14 @@ __global__ __launch_bounds__(256) void k_winbwd_fold(const float *__restrict__ c
 #pragma unroll 8
         for (int q = 1; q < splits; q++) s += wpart[(size_t)q * n + i];
         dW3r[i] = s;
+        return;
+    }
+    if ((int)blockIdx.x == nb + (T * WB_CI + 3) / 4) {  // db3 = tap 0's split sums in split order
+        if (!db3 || (int)threadIdx.x >= T * WB_CI) return;
+        const int t = threadIdx.x / WB_CI, c = threadIdx.x - t * WB_CI;
+        float s = 0.0f;
+        for (int q = 0; q < splits; q++) s += tpart[((size_t)t * splits + q) * WB_CI + c];
+        db3[threadIdx.x] = s;
         return;
     }
     const int k = ((int)blockIdx.x - nb) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -205,23 +228,23 @@ hipError_t launch_winfwd(const float *a2w, const float *W3r, int T, int64_t nw, 
 
 int64_t winbwd_work_floats(int T, int64_t nw) {
     const int64_t rt = (nw + 31) / 32, splits = (nw + WB_SPLIT - 1) / WB_SPLIT;
-    return (int64_t)T * rt * WB_CI + splits * T * WB_CI * WB_CJ;
+    return (int64_t)T * rt * WB_CI + splits * T * WB_CI * WB_CJ + splits * T * WB_CI;
 }
 
 hipError_t launch_winbwd(const float *a2w, const float *dQ, const float *W3r, int T, int64_t nw, float *da2w,
-                         float *db2, float *dW3r, float *work, hipStream_t s) {
+                         float *db2, float *dW3r, float *work, hipStream_t s, float *db3) {
     if (nw <= 0 || T < 1) return hipErrorInvalidValue;
     const int64_t rt = (nw + 31) / 32, splits = (nw + WB_SPLIT - 1) / WB_SPLIT;
     const int64_t nd = (int64_t)T * rt * 2, nwg = (int64_t)T * splits * 18;
     if (nd + nwg > INT32_MAX) return hipErrorInvalidValue;
-    float *colpart = work, *wpart = work + (size_t)T * rt * WB_CI;
+    float *colpart = work, *wpart = work + (size_t)T * rt * WB_CI, *tpart = wpart + (size_t)splits * T * WB_CI * WB_CJ;
     hipLaunchKernelGGL(k_winbwd, dim3((unsigned)(nd + nwg)), dim3(64), 0, s, a2w, dQ, W3r, nw, T, (int)nd, (int)splits,
-                       da2w, colpart, wpart);
+                       da2w, colpart, wpart, db3 ? tpart : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int nb = (T * WB_CI * WB_CJ + 255) / 256;
-    hipLaunchKernelGGL(k_winbwd_fold, dim3((unsigned)(nb + (T * WB_CI + 3) / 4)), dim3(256), 0, s, colpart, wpart, T,
-                       rt, (int)splits, nb, db2, dW3r);
+    hipLaunchKernelGGL(k_winbwd_fold, dim3((unsigned)(nb + (T * WB_CI + 3) / 4 + 1)), dim3(256), 0, s, colpart, wpart,
+                       tpart, T, rt, (int)splits, nb, db2, dW3r, db3);
     return hipGetLastError();
 }
 

@@ -166,7 +166,7 @@ def lib():
     L.merlin_window_gemm_fwd.argtypes = [vp, vp, i32, i64, vp, vp]
     L.merlin_window_gemm_bwd_work.argtypes = [i32, i64]
     L.merlin_window_gemm_bwd_work.restype = i64
-    L.merlin_window_gemm_bwd.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp, vp, i64, vp]
+    L.merlin_window_gemm_bwd.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp, vp, vp, i64, vp]
     check_env_config_layout(L)
     _lib = L
     return L
@@ -861,9 +861,10 @@ def window_gemm_fwd(a2w, W3r, out=None):
 _WINBWD_WORK = {}
 
 
-def window_gemm_bwd(a2w, dQ, W3r, out_da2w=None, out_db2=None, out_dW3r=None):
+def window_gemm_bwd(a2w, dQ, W3r, out_da2w=None, out_db2=None, out_dW3r=None, out_db3=None):
     """The window GEMM's backward (merlin_window_gemm_bwd): a2w f32[T, nw, 64], dQ f32[T, nw, 576], W3r f32[T, 64,
-    576] -> (da2w = [a2w > 0] * dQ W3r^T, db2 = its column sums f32[T, 64], dW3r = a2w^T dQ f32[T, 64, 576])."""
+    576] -> (da2w = [a2w > 0] * dQ W3r^T, db2 = its column sums f32[T, 64], dW3r = a2w^T dQ f32[T, 64, 576]); with
+    out_db3 f32[T, 64] also the column sums of dQ's tap-0 columns (conv3's bias gradient)."""
     T, nw, ci = (int(v) for v in a2w.shape)
     assert ci == 64 and dQ.shape == (T, nw, 576) and W3r.shape == (T, 64, 576)
     assert all(x.dtype == torch.float32 and x.is_contiguous() for x in (a2w, dQ, W3r))
@@ -879,8 +880,11 @@ def window_gemm_bwd(a2w, dQ, W3r, out_da2w=None, out_db2=None, out_dW3r=None):
     if work is None or work.numel() < need:  # grown once to the largest window count seen (no free inside a capture)
         work = _WINBWD_WORK[key] = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=dev)
     with KernelTimer.span("k_winbwd", (2 * T * nw * (64 + 576) + T * 64 * 576) * 4):
+        if out_db3 is not None:
+            assert out_db3.shape == (T, 64) and out_db3.dtype == torch.float32 and out_db3.is_contiguous()
         check(lib().merlin_window_gemm_bwd(ptr(a2w), ptr(dQ), ptr(W3r), T, nw, ptr(da2w), ptr(db2), ptr(dW3r),
-                                           ptr(work), int(work.numel()), stream_of(a2w)), "merlin_window_gemm_bwd")
+                                           ptr(out_db3), ptr(work), int(work.numel()), stream_of(a2w)),
+              "merlin_window_gemm_bwd")
     return da2w, db2, dW3r
 
 

@@ -453,14 +453,15 @@ class WindowStep:
             main.wait_event(masks_ready)
         dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]),
                                   mask_rows=arows if MASK_ROWS else None, pre=pre)
-        nat.colsum(dQ.view(2, -1, 9, 64)[:, :, 0], out=g[3])  # db3: every (u, p3) has one window at tap 0
+        if wh3 or not WINDOW_BWD_HIP:  # (else summed by merlin_window_gemm_bwd below)
+            nat.colsum(dQ.view(2, -1, 9, 64)[:, :, 0], out=g[3])  # db3: every (u, p3) has one window at tap 0
         dQ = dQ.view(2, -1, 576)
         if wh3:
             nat.h3_amax(dQ, out=amq)
             da2w = nat.h3_gemm_nt(dQ, amq, P3, amW3, cfg=nat.H3_NT_CFG["qwin_dgrad"], name="gemm_window_dgrad")
             nat.h3_gemm_tn(a2w, am2, dQ, amq, cfg=nat.H3_TN_CFG_WIN, name="gemm_window_wgrad", out=g[2])
         elif WINDOW_BWD_HIP:  # both products, the ReLU mask and db2 in one launch + an ordered fold
-            da2w, _, _ = nat.window_gemm_bwd(a2w, dQ, W3r, out_db2=g[1], out_dW3r=g[2])
+            da2w, _, _ = nat.window_gemm_bwd(a2w, dQ, W3r, out_db2=g[1], out_dW3r=g[2], out_db3=g[3])
         else:
             da2w = torch.bmm(dQ, W3r.transpose(1, 2))
             chunks = max(1, a2w.shape[1] // 256)

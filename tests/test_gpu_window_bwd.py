@@ -25,8 +25,13 @@ def test_window_gemm_bwd_vs_float64(device, T, nw):
     W3r = torch.randn(T, 64, 576, device=device, generator=g) * 0.05
     dQ = torch.randn(T, nw, 576, device=device, generator=g) * 1e-3
     dQ[:, ::7] *= 1e-4  # rows of very different scales
-    da2w, db2, dW3r = nat.window_gemm_bwd(a2w, dQ, W3r)
+    db3 = torch.empty(T, 64, device=device)
+    da2w, db2, dW3r = nat.window_gemm_bwd(a2w, dQ, W3r, out_db3=db3)
     torch.cuda.synchronize()
+    # db3: the tap-0 columns' sums (conv3's bias gradient)
+    t64 = dQ[:, :, :64].double().sum(1)
+    tden = dQ[:, :, :64].abs().double().sum(1)
+    assert _err(db3, t64, tden) <= nw * 2.0 ** -24 + FLOOR
     mask = a2w > 0
     assert torch.equal(da2w[~mask], torch.zeros_like(da2w[~mask]))
     # input gradient (unmasked entries)
@@ -47,8 +52,11 @@ def test_window_gemm_bwd_vs_float64(device, T, nw):
     wtol = max(_err(Wf, W64, wden), FLOOR)
     assert _err(dW3r, W64, wden) <= 2 * wtol + 2.0 ** -22
     # fixed order: the same bits again
-    again = nat.window_gemm_bwd(a2w, dQ, W3r)
-    assert all(torch.equal(x, y) for x, y in zip(again, (da2w, db2, dW3r)))
+    db3b = torch.empty_like(db3)
+    again = nat.window_gemm_bwd(a2w, dQ, W3r, out_db3=db3b)
+    assert all(torch.equal(x, y) for x, y in zip(again + (db3b,), (da2w, db2, dW3r, db3)))
+    # without db3: the same three outputs
+    assert all(torch.equal(x, y) for x, y in zip(nat.window_gemm_bwd(a2w, dQ, W3r), (da2w, db2, dW3r)))
 
 
 @pytest.mark.parametrize("T,nw", [(2, 1), (2, 33), (1, 256), (2, 6571)])
@@ -80,5 +88,5 @@ def test_window_gemm_bwd_rejects_bad_arguments(device):
     b, w = torch.empty(2, 64, device=device), torch.empty(2, 64, 576, device=device)
     work = torch.empty(4, device=device)
     rc = L.merlin_window_gemm_bwd(nat.ptr(a2w), nat.ptr(dQ), nat.ptr(W3r), 2, 40, nat.ptr(out), nat.ptr(b),
-                                  nat.ptr(w), nat.ptr(work), 4, None)
+                                  nat.ptr(w), None, nat.ptr(work), 4, None)
     assert rc != 0 and b"work too small" in L.merlin_last_error()
