@@ -309,22 +309,15 @@ def cpu_baseline():
 # bench names -> rocprofv3 kernel names (untruncated: template arguments kept).  A span made of several
 # kernels adds their bytes; the first name of a tuple must be present, the rest (e.g. a segmented sum's
 # fix-up pass, absent when no destination crosses an item) count when they are.
-PMC_ALIAS = {"k_seg_sum_R": ("k_seg_sum<2, 1>", "k_seg_fix<1>"),
-             "k_seg_sum_S": ("k_seg_sum<0, 2>", "k_seg_fix<2>"),
-             "k_seg_sum_dQ": ("k_seg_sum<0, 3>", "k_seg_fix<3>"),
-             "k_seg_sum_dT2": ("k_seg_sum<0, 4>", "k_seg_fix<4>"),
-             # the rollout's fc1 (x6); the update's fc1 GEMMs follow H3_NT_CFG (h3_gemm_names); the weight
-             # gradient's span covers the split-K kernel and its slab fold
-             "gemm_rollout_fc1": ("k_x6_nt32<128, 128, 2, 2, 0, 1, 0>",),
-             "k_head_bwd": ("k_head_bwd<3>", "k_head_fold"),
-             "k_heads_fwd": ("k_heads_fwd<3>",),
+PMC_ALIAS = {"k_seg_sum_R": ("k_seg_sum<3, 1>",),  # the R pass reading each row's mask word through its representative
+             "k_seg_sum_S": ("k_seg_sum<0, 2>",),
+             "k_seg_sum_dQ": ("k_seg_sum<0, 3>",),
+             "k_seg_sum_dT2": ("k_seg_sum<0, 4>",),
              "k_window_lut": ("k_window_lut<0>",),
-             "k_window_lut_all": ("k_window_lut<1>",),
-             "gemm_wgrad": ("k_h3_tn<128, 192, 4, 2>", "k_x6_fold")}
+             "k_window_lut_all": ("k_window_lut<1>",)}
 # with conv3's patch reuse (merlin/fast_step.py PATCH_REUSE = "gather") the update's k_window_conv3 span is the
 # representatives' kernel + the mask-word copy, and fc1's forward / weight gradient read a3 through the row map
-PMC_ALIAS_GATHER = {"k_window_conv3": ("k_window_conv3_reps", "k_window_conv3_copy<false>", "k_q_colmax", "k_q_bound"),
-                    "gemm_wgrad": ("k_h3_tng<128, 192, 4, 2>", "k_x6_fold")}
+PMC_ALIAS_GATHER = {"k_window_conv3": ("k_window_conv3_reps", "k_window_conv3_copy<false>", "k_q_colmax", "k_q_bound")}
 # rocprofv3 names of merlin_h3_gemm_nt's configurations (csrc/merlin_h3.hip launch_h3_gemm_nt)
 H3_NT_NAMES = {0: "k_h3_nt<256, 128, 4, 2, {}>", 1: "k_h3_nt<128, 192, 4, 2, {}>", 2: "k_h3_nt<128, 128, 2, 2, {}>",
                3: "k_h3_nt<128, 256, 2, 4, {}>", 10: "k_h3_ntp<256, 128, 4, 2, {}>", 11: "k_h3_ntp<128, 192, 4, 2, {}>",
@@ -369,6 +362,12 @@ def pmc_traffic(kernel: str):
     names = {**PMC_ALIAS, **h3_gemm_names(nat)}.get(kernel, kernel)
     names = names if isinstance(names, tuple) else (names,)
     files = [PMC_FILE] if PMC_FILE else sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True)
+    if not PMC_FILE:
+        # only PMC passes at least as new as the newest kernel trace (profile names start with their round tag,
+        # e.g. r05j_): an older pass measured other code, and a kernel it holds under the same name is not this one
+        stats = sorted(glob.glob(os.path.join(REPO, "profiles", "*_kernel_stats.md")))
+        newest = os.path.basename(stats[-1]).split("_")[0] if stats else ""
+        files = [f for f in files if os.path.basename(f).split("_")[0] >= newest]
     for f in files:
         try:
             dd = json.load(open(f))

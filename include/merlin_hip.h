@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define MERLIN_ABI_VERSION 2
+#define MERLIN_ABI_VERSION 3  /* 3: compact acting-table keys (round 5), plane-operand GEMMs */
 
 #define MERLIN_OK 0
 #define MERLIN_E_INVALID 1     /* bad argument / config */
@@ -83,6 +83,8 @@ extern "C" {
 /* device error bits reported by merlin_env_errors */
 #define MERLIN_DEVERR_BAD_ACTION 1u  /* action not in {0,1,2}: ThreeActionWrapper IndexError */
 #define MERLIN_DEVERR_PLACE_OBJ 2u   /* place_obj max_tries exceeded: RecursionError */
+#define MERLIN_DEVERR_BAD_TILE 4u    /* merlin_tower_codes_conv3: a frame that is no observation (the agent tile (class
+                                      * 4) missing at view cell (3, 6) or present elsewhere): merlin_tower_errors */
 
 /* observation layouts for merlin_obs_expand_f32 */
 #define MERLIN_LAYOUT_NCHW 0 /* [n][3][56][56]: what CNNActorCritic._format_obs hands the convs */
@@ -341,6 +343,10 @@ int merlin_tower_codes_conv3(const uint32_t *codes_dev, int64_t n, const float *
 int merlin_tower_codes_conv3_amax(const uint32_t *codes_dev, int64_t n, const float *Qall_dev,
                                   const float *b3_dev, int32_t towers, float *Y3_dev, uint32_t *amax_dev,
                                   void *stream);
+/* tower_errors: the device error flags the tower kernels raised on this device since the last call
+ * (MERLIN_DEVERR_BAD_TILE from merlin_tower_codes_conv3: a frame whose compact table key is not its window), then
+ * clears them; synchronises `stream` (PPO reads it once per rollout, with merlin_env_errors). */
+int merlin_tower_errors(uint32_t *flags, void *stream);
 /* Same, also writing relu_bits_dev uint64[towers][n*9]: bit co of row (k*9 + p3) = Y3 > 0 there; amax_dev
  * (or NULL): atomicMax of max |Y3| per tower as float bits into amax_dev[t] (zeroed by the caller), the operand
  * scale of fc1's f16 two-plane GEMMs (merlin_h3_gemm_*). */

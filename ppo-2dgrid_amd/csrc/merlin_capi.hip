@@ -204,6 +204,7 @@ struct DeviceWs {
     void *lut2_slabs = nullptr;  // conv2 table histogram: per-block 4-channel u64 slices
     float *epi_work = nullptr;   // GEMM epilogues: per-block column-sum partials
     double *stage_part = nullptr;  // conv tables' adjoint: the 625-combination type's partial dW2 sums
+    uint32_t *tower_err = nullptr;  // device error flags of the tower kernels (merlin_tower_errors)
 };
 constexpr int MAX_DEV = 64;
 DeviceWs g_dev[MAX_DEV];
@@ -227,6 +228,9 @@ int device_ws(DeviceWs **out) {
         HIP_TRY(hipMalloc(&w.lut2_slabs, merlin::conv2_lut_slab_bytes(2, merlin::conv2_lut_fblocks(INT64_MAX / 64))));
         HIP_TRY(hipMalloc(&w.epi_work, sizeof(float) * merlin::epilogue_work_floats()));
         HIP_TRY(hipMalloc(&w.stage_part, sizeof(double) * merlin::STAGE_WS_DOUBLES));
+        HIP_TRY(hipMalloc(&w.tower_err, sizeof(uint32_t)));
+        HIP_TRY(hipMemset(w.tower_err, 0, sizeof(uint32_t)));  // once, outside any capture
+        HIP_TRY(hipDeviceSynchronize());
         w.ready = true;
     }
     *out = &w;
@@ -779,7 +783,21 @@ int merlin_tower_codes_conv3_amax(const uint32_t *codes, int64_t n, const float 
                                   int32_t towers, float *Y3, uint32_t *amax, void *stream) {
     if ((!codes || !Qall || !b3 || !Y3) && n > 0) return fail(MERLIN_E_INVALID, "null argument");
     if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    HIP_TRY(merlin::launch_codes_conv3(codes, n, Qall, b3, towers, Y3, amax, (hipStream_t)stream));
+    DeviceWs *ws = nullptr;
+    if (int r = device_ws(&ws)) return r;
+    HIP_TRY(merlin::launch_codes_conv3(codes, n, Qall, b3, towers, Y3, amax, ws->tower_err, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_tower_errors(uint32_t *flags, void *stream) {
+    DeviceWs *ws = nullptr;
+    if (int r = device_ws(&ws)) return r;
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, ws->tower_err, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(merlin::zero_async(ws->tower_err, sizeof(h), s));
+    if (flags) *flags = h;
     return MERLIN_OK;
 }
 

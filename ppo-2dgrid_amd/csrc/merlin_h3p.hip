@@ -273,11 +273,22 @@ hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const 
 // Same products in the same order as k_h3_tn / k_h3_tng: the same bits.
 __device__ uint4 p_zero16[1] = {{0u, 0u, 0u, 0u}};
 
+// m0 is a reserved register to LLVM (a clobber entry is ignored, with a warning), so the asm saves it in a scratch
+// SGPR and puts it back behind the DMA: the compiler's view of m0 is unchanged by these statements whatever it keeps
+// there.  (The DMA reads m0 at issue: the compiler's own code rewrites m0 right behind each global_load_lds too.)
 __device__ __forceinline__ void p_dma16(const void *src, uint32_t lds) {  // lds: wave-uniform byte address
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory");
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
 }
 __device__ __forceinline__ void p_dma4(const void *src, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds) : "memory");
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
 }
 
 template <int RC>

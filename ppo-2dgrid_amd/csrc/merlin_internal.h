@@ -258,7 +258,7 @@ hipError_t launch_ppo_loss(const float *logits, const float *value, const float 
                            float *dvalue, float *dbias_a, float *dbias_c, float *loss, double *stats,
                            double *workspace, hipStream_t s, uint32_t *dmax = nullptr);
 hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, const float *b3, int T, float *Y3,
-                              uint32_t *amax, hipStream_t s);
+                              uint32_t *amax, uint32_t *err, hipStream_t s);
 hipError_t launch_x6_gemm_nt32(const float *A, const void *B, int64_t M, int N, int K, int T, int64_t a_stride,
                                int64_t b_stride, const float *bias, float *C, int64_t c_stride, int cfg, hipStream_t s);
 hipError_t launch_x6_gemm_tn32(const float *A, const float *B, int64_t Kd, int M, int N, int T, int64_t a_stride,

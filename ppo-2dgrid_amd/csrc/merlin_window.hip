@@ -270,7 +270,8 @@ __global__ __launch_bounds__(256) void k_window_conv3_copy(float4 *Y3, uint64_t 
 // compact_window_keys): a window away from the agent = its 9 classes in base 4 (tile (0, 0) most significant,
 // 4^9 keys); a window over the agent = 4^9 + (wx - 1) 4^8 + its other 8 classes in base 4.  458,752 keys instead of
 // all 5^9 = 1,953,125 class patterns: a 4.3x smaller table (2.1 GB for both towers), built in that fraction of the
-// time.  (Valid observations only: a class-4 tile elsewhere is read as class 3.)
+// time.  (Valid observations only: a class-4 tile elsewhere is read as class 3, so a frame that is not an observation
+// -- no agent tile at (3, 6), or one elsewhere -- raises MERLIN_DEVERR_BAD_TILE in `err`, merlin_tower_errors.)
 constexpr int64_t ALL_WINDOWS = 458752;  // 4^9 + 3 * 4^8
 // The 25 window keys of a frame are computed once per block (CC_F frames per block, keys in LDS), not by each of the
 // 16 lanes of each of the 9 output rows that read them: round 4's per-lane key arithmetic (81 class lookups per lane)
@@ -278,8 +279,10 @@ constexpr int64_t ALL_WINDOWS = 458752;  // 4^9 + 3 * 4^8
 constexpr int CC_F = 4;  // 1,024 blocks of 256 threads at 4,096 frames: ~4.5 outputs (9 row gathers each) per thread
 __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict__ codes, int64_t n,
                                                      const float4 *__restrict__ Q, const float4 *__restrict__ b3,
-                                                     int T, float4 *__restrict__ Y3, uint32_t *__restrict__ amax) {
+                                                     int T, float4 *__restrict__ Y3, uint32_t *__restrict__ amax,
+                                                     uint32_t *__restrict__ err) {
     __shared__ uint32_t keys[CC_F][25];
+    bool bad = false;  // a tile this compact table cannot hold (see above)
     uint32_t mx[2] = {0u, 0u};  // max |Y3| per tower as float bits (fc1's h3 operand scale), when amax != null
     for (int64_t f0 = (int64_t)blockIdx.x * CC_F; f0 < n; f0 += (int64_t)gridDim.x * CC_F) {
         const int nf = (int)std::min<int64_t>(CC_F, n - f0);
@@ -296,7 +299,9 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
 #pragma unroll
                 for (int b = 0; b < 3; b++) {
                     const int cell = (wy + a) * 7 + wx + b;
-                    const uint32_t c = min((w[cell >> 3] >> (4 * (cell & 7))) & 15u, 3u);  // 0..3: see above
+                    const uint32_t raw = (w[cell >> 3] >> (4 * (cell & 7))) & 15u;
+                    bad |= cell == 45 ? raw != 4u : raw > 3u;  // the agent at view cell (3, 6), nowhere else
+                    const uint32_t c = min(raw, 3u);  // 0..3: see above
                     if (3 * a + b != skip) key = key * 4u + c;
                 }
             if (agent) key += 262144u + (uint32_t)(wx - 1) * 65536u;
@@ -331,6 +336,7 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
         __syncthreads();
     }
     if (amax) block_amax2(mx, T, amax);
+    if (bad && err) atomicOr(err, MERLIN_DEVERR_BAD_TILE);
 }
 
 // One wave per item of L entries; lane = (tower t, entry parity q, float4 column c): one wave
@@ -703,12 +709,12 @@ hipError_t launch_window_conv3(const float *Q, int64_t nw, const int32_t *wid, c
 }
 
 hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, const float *b3, int T, float *Y3,
-                              uint32_t *amax, hipStream_t s) {
+                              uint32_t *amax, uint32_t *err, hipStream_t s) {
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((n + CC_F - 1) / CC_F, 256 * 32);
     hipLaunchKernelGGL(k_codes_conv3, dim3(grid), dim3(256), 0, s, codes, n, reinterpret_cast<const float4 *>(Q),
-                       reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), amax);
+                       reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), amax, err);
     return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@ LAYOUT_NHWC = 1
 OBS_WORDS = 8
 DEVERR_BAD_ACTION = 1
 DEVERR_PLACE_OBJ = 2
+DEVERR_BAD_TILE = 4  # merlin_tower_codes_conv3 saw a frame that is no observation (merlin_tower_errors)
 
 DIFFICULTY_IDS = {"easy": 0, "medium": 1, "mediumhard": 2, "hard": 3, "hardest": 4}
 
@@ -47,6 +48,9 @@ class EnvConfig(C.Structure):
 
 
 _lib = None
+# MERLIN_ABI_VERSION of include/merlin_hip.h this binding is written against (3: the compact 4^9 + 3 4^8 acting-table
+# keys of merlin_tower_codes_conv3 / merlin_tower_all_windows, the plane-operand GEMM entry points)
+ABI_VERSION = 3
 
 
 def lib():
@@ -63,6 +67,9 @@ def lib():
         raise MerlinNativeError(f"failed to load {LIB_PATH}: {e}") from e
     vp, i32, i64, u64p = C.c_void_p, C.c_int32, C.c_int64, C.POINTER(C.c_uint64)
     L.merlin_version.restype = C.c_int
+    if L.merlin_version() != ABI_VERSION:  # a library built from another header: its tables / layouts differ
+        raise MerlinNativeError(f"{LIB_PATH} has ABI version {L.merlin_version()}, this package binds version "
+                                f"{ABI_VERSION} (include/merlin_hip.h MERLIN_ABI_VERSION); rebuild it")
     L.merlin_last_error.restype = C.c_char_p
     L.merlin_tile_atlas.argtypes = [vp]
     L.merlin_env_config_layout.argtypes = [C.POINTER(C.c_int64), i32]
@@ -107,6 +114,7 @@ def lib():
     L.merlin_tower_all_windows.restype = i64
     L.merlin_tower_codes_conv3.argtypes = [vp, i64, vp, vp, i32, vp, vp]
     L.merlin_tower_codes_conv3_amax.argtypes = [vp, i64, vp, vp, i32, vp, vp, vp]
+    L.merlin_tower_errors.argtypes = [C.POINTER(C.c_uint32), vp]
     L.merlin_segment_sum.argtypes = [vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32, vp]
     L.merlin_segment_sum_masked.argtypes = [vp, vp, i64, vp, vp, i64, vp, i32, i64, vp, i64, i32, vp, i64, vp, i32,
                                             vp]
@@ -203,7 +211,7 @@ EXPORTED_SYMBOLS = (
     "merlin_tower_conv2_lut_bwd", "merlin_tower_conv2_lut_fwd_grouped", "merlin_tower_conv2_lut_slab_bytes",
     "merlin_tower_conv2_lut_bwd_grouped", "merlin_tower_window_lut", "merlin_tower_window_lut_bias_relu", "merlin_minibatch_patch_maps", "merlin_segment_sum_mask_rows", "merlin_tower_window_conv3",
     "merlin_tower_window_conv3_bits", "merlin_tower_window_conv3_reuse", "merlin_tower_all_windows", "merlin_tower_codes_conv3",
-    "merlin_tower_codes_conv3_amax",
+    "merlin_tower_codes_conv3_amax", "merlin_tower_errors",
     "merlin_segment_sum", "merlin_segment_sum_masked", "merlin_segment_sum_marked", "merlin_segment_sum_fused", "merlin_tower_heads_fwd", "merlin_tower_bias_relu", "merlin_tower_relu_bwd", "merlin_tower_head_bwd",
     "merlin_tower_colsum",
     "merlin_ppo_loss_workspace", "merlin_ppo_loss", "merlin_act_heads",
@@ -765,6 +773,20 @@ SEG_ROLES = {"k_seg_sum_R": 1, "k_seg_sum_S": 2, "k_seg_sum_dQ": 3, "k_seg_sum_d
 # carries and an arrival counter per row), not by a second k_seg_fix launch; the same bits either way
 SEG_FUSED = True
 
+
+
+def tower_errors(device=None, raise_on_error: bool = True) -> int:
+    """The device error flags of the tower kernels since the last call (merlin_tower_errors; clears them).
+    DEVERR_BAD_TILE: the acting path's compact conv3 table was handed a frame that is not an observation."""
+    flags = C.c_uint32()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    with torch.cuda.device(dev):
+        check(lib().merlin_tower_errors(C.byref(flags), C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+              "merlin_tower_errors")
+    if raise_on_error and flags.value & DEVERR_BAD_TILE:
+        raise MerlinNativeError("merlin_tower_codes_conv3: a frame without the agent tile at view cell (3, 6), or with "
+                                "it elsewhere -- not an observation; its windows were read as other windows")
+    return flags.value
 
 def segment_sum(src, plan, out_rows: int, slot=None, sub: int = 1, name: str = "k_seg_sum", out=None,
                 accumulate: bool = False, carry=None, mask=None, fill: bool = True, mark=None, mask_rows=None):

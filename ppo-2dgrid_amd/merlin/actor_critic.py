@@ -515,6 +515,7 @@ class CNNActorCritic(nn.Module):
     # below this many frames per rollout the acting path looks conv2 up per frame instead of building
     # the all-windows table (Qall: 2.1 GB and ~68 GFLOP per rollout, whatever the rollout's size)
     ALL_WINDOWS_MIN_FRAMES = 1 << 18
+    ALL_WINDOWS_HEADROOM = 5 << 29  # 2.5 GiB: the all-windows tables plus their GEMM's planes
 
     def rollout_pack(self, frames: int | None = None, all_windows: bool | None = None, steps: int | None = None):
         """The weights of the acting path in the layouts its kernels and GEMMs read, built once
@@ -586,10 +587,24 @@ class CNNActorCritic(nn.Module):
         if frames is not None and frames < self.ALL_WINDOWS_MIN_FRAMES:
             return False
         try:
-            _, total = torch.cuda.mem_get_info(device)
+            free, total = torch.cuda.mem_get_info(device)
         except Exception:
             return True
-        return total >= (64 << 30)
+        if total < (64 << 30):
+            return False
+        # the all-windows layout allocates its tables once per rollout (Qall [2, 458752, 576] fp32, 2.1 GB, plus
+        # relu(conv2) of every window, 0.23 GB): check the headroom once, here, before any capture -- running out
+        # inside the captured rollout would fail there, and switching layouts by free memory would make the acting
+        # draws depend on what else the device holds
+        need = self.ALL_WINDOWS_HEADROOM
+        if free + torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device) < need:
+            from ._native import MerlinNativeError
+
+            raise MerlinNativeError(
+                f"the all-windows acting layout needs ~{need / 2**30:.1f} GiB of free device memory "
+                f"({free / 2**30:.1f} GiB free); free memory or set CNNActorCritic.ALL_WINDOWS_MIN_FRAMES above the "
+                f"rollout's frame count for the per-frame layout")
+        return True
 
     @torch.no_grad()
     def heads_partials_ok(self, pack) -> bool:

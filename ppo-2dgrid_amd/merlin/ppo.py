@@ -223,6 +223,8 @@ class PPO:
                 self._capture_rollout()
         self._record_episodes()
         self.vec.errors()
+        if self.rollout_all_windows:
+            nat.tower_errors(self.device)  # the compact acting table saw only observations
         lv = self.buf.last_value
         return float(lv[0].item()) if self.num_envs == 1 else lv
 

@@ -21,6 +21,10 @@ Sources, per fixture:
                   replay batch, with the randperm draws recorded for replay.
   update_rollout_ref.npz  the same on a real single-env rollout of the C oracle's env (repeated
                   observations, episode ends), the fixture the benched update path is pinned to.
+  update_grad_ref.npz  the REFERENCE PPO.update at a real minibatch size (8,192-step single-env rollout,
+                  minibatches of 2,048) with the first optimizer step's clipped gradient of every tensor
+                  and that step's parameter change recorded whole (wrappers around the reference optimizer's
+                  step and torch's clip_grad_norm_, defined here).
   fomaml_ref.npz  the REFERENCE FOMAML.compute_loss (src/fomaml.py:110-156) and the
                   per-task inner SGD step + query-gradient accumulation of
                   meta_train_step (:158-212) on recorded support / query batches of
@@ -337,6 +341,93 @@ def gen_update_rollout():
     )
 
 
+def gen_update_grad():
+    """update_grad_ref.npz: the REFERENCE PPO.update (src/ppo.py:122-168) at a real minibatch size -- an 8,192-step
+    single-env rollout of the C oracle's mediumhard env (seed 777, uniformly random actions, the env's own max_steps
+    1,024), one epoch of 4 minibatches of 2,048 -- with the FIRST optimizer step's gradient recorded whole: a wrapper
+    around the reference optimizer's `step` (after clip_grad_norm_, :153-155) saves every parameter's clipped
+    .grad and the parameters' change by that step; a wrapper around torch's clip_grad_norm_ keeps its returned
+    (pre-clip) norm.  Nothing in the reference is edited: both wrappers live here, around objects it creates."""
+    import torch
+
+    PPO, _, _ = _import_reference()
+    atlas = build_atlas()
+    B, MB, EPOCHS = 8192, 2048, 1
+    rs = np.random.RandomState(47)
+    actions = rs.randint(0, 3, size=(B, 1)).astype(np.int64)
+    codes, rew, term, trunc, _ = O.batch_rollout(np.array([777], dtype=np.uint64), actions)
+    codes = codes[:B, 0]
+    imgs = O.render(codes, atlas)
+    rewards = rew[:, 0].astype(np.float32)
+    dones = np.maximum(term, trunc)[:, 0].astype(np.float32)
+    actions = actions[:, 0]
+
+    class _StubEnv:
+        action_space = types.SimpleNamespace(n=3)
+
+        def reset(self, seed=None):
+            return imgs[0].copy(), {}
+
+    torch.manual_seed(0)
+    agent = PPO(_StubEnv(), lr=3e-4, gamma=0.99, lam=0.95, clip_eps=0.2, update_epochs=EPOCHS,
+                batch_size=B, minibatch_size=MB, vf_coef=0.5, ent_coef=0.05, device="cpu")
+    keys, sums0 = _param_checksums(agent.ac)
+    names = [n for n, _ in agent.ac.named_parameters()]
+    with torch.no_grad():
+        lp, _, v = agent.ac.evaluate(torch.from_numpy(imgs.astype(np.float32)), torch.from_numpy(actions))
+    for t in range(B):
+        agent.buffer.add(torch.from_numpy(imgs[t].astype(np.float32)), torch.tensor(actions[t]), lp[t], v[t],
+                         torch.tensor(rewards[t]), torch.tensor(dones[t]))
+    last_value = float(v[-1].item())
+    rec = {}
+    norms = []
+    clip_orig = torch.nn.utils.clip_grad_norm_
+
+    def clip_wrap(*a, **k):
+        n = clip_orig(*a, **k)
+        norms.append(float(n))
+        return n
+
+    step_orig = agent.optimizer.step
+
+    def step_wrap(*a, **k):
+        first = not rec
+        if first:
+            params = [p for _, p in agent.ac.named_parameters()]
+            rec["p0"] = [p.detach().clone() for p in params]
+            rec["grads"] = [p.grad.detach().clone() for p in params]
+        out = step_orig(*a, **k)
+        if first:
+            rec["delta"] = [p.detach() - p0 for p, p0 in zip(params, rec["p0"])]
+        return out
+
+    agent.optimizer.step = step_wrap
+    torch.nn.utils.clip_grad_norm_ = clip_wrap
+    try:
+        torch.manual_seed(4747)
+        perms = np.stack([torch.randperm(B).numpy() for _ in range(EPOCHS)])
+        torch.manual_seed(4747)
+        stats = agent.update(last_value)
+    finally:
+        torch.nn.utils.clip_grad_norm_ = clip_orig
+    keys1, sums1 = _param_checksums(agent.ac)
+    assert (keys1 == keys).all() and len(norms) == EPOCHS * (B // MB)
+    out = dict(
+        cfg=np.array([B, MB, EPOCHS], dtype=np.int64), codes=codes, actions=actions,
+        logp=lp.numpy(), values=v.numpy(), rewards=rewards, dones=dones,
+        last_value=np.float32(last_value), perms=perms, keys=keys, sums0=sums0, sums1=sums1,
+        stat_names=np.array(sorted(stats)), stat_vals=np.array([stats[k] for k in sorted(stats)]),
+        hparams=np.array([3e-4, 0.99, 0.95, 0.2, 0.5, 0.05]), param_names=np.array(names),
+        first_norm=np.float64(norms[0]), norms=np.array(norms),
+    )
+    for i, (g, d) in enumerate(zip(rec["grads"], rec["delta"])):
+        out[f"grad{i}"] = g.numpy().astype(np.float32)  # the clipped gradient Adam consumed
+        out[f"step{i}"] = (d.double() / 3e-4).numpy().astype(np.float16)  # the first Adam step in units of lr
+    np.savez_compressed(os.path.join(HERE, "update_grad_ref.npz"), **out)
+    print(f"update_grad_ref: {len(np.unique(codes, axis=0))} distinct frames of {B}, {int(dones.sum())} dones, "
+          f"first-step norm {norms[0]:.5f}")
+
+
 def gen_fomaml():
     import copy
 
@@ -426,5 +517,6 @@ if __name__ == "__main__":
     gen_cnn()
     gen_update()
     gen_update_rollout()
+    gen_update_grad()
     gen_fomaml()
     print("golden fixtures written to", HERE)

@@ -62,3 +62,23 @@ def test_bench_eight_ranks_on_one_gpu_ends_with_one_line():
     for k in ("rollout_ms", "update_ms", "kernel_ms_per_iter", "distinct_frames_per_sample"):
         assert len(out["ranks"][k]) == 8, (k, out["ranks"])
     assert abs(out["value"] - 2 * 8 * 128 * 16 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 0.01
+
+
+def test_bench_eight_ranks_cfg3_envs_on_one_gpu():
+    """Round-5 verdict item 1: bench.py at cfg 3's workload, 8 ranks x 4096 envs x 256 steps (32,768 envs; gloo, all
+    on device 0), one timed iteration: one JSON line whose global batch is 8 * 4096 * 256."""
+    env = dict(os.environ, MERLIN_DIST_BACKEND="gloo", MERLIN_BENCH_DEVICE="0", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1",
+           "--num-envs", "4096", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-4000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8"
+    assert out["config"]["global_batch"] == 8 * 4096 * 256
+    for k in ("rollout_ms", "update_ms", "kernel_ms_per_iter", "distinct_frames_per_sample"):
+        assert len(out["ranks"][k]) == 8, (k, out["ranks"])
+    assert abs(out["value"] - 8 * 4096 * 256 / (out["ms_per_step"] / 1e3)) / out["value"] < 0.01

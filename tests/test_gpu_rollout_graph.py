@@ -106,3 +106,37 @@ def test_graph_rollout_matches_eager_env(device):
     assert not torch.equal(seen[1], seen[2])
     mirror.errors()
 
+
+
+def test_codes_conv3_flags_frames_that_are_no_observation(device):
+    """The compact acting table holds windows of classes 0..3 plus the agent tile at view cell (3, 6) only
+    (csrc/merlin_window.hip k_codes_conv3).  A frame outside that set -- the agent tile elsewhere, or missing at
+    (3, 6) -- raises MERLIN_DEVERR_BAD_TILE (merlin_tower_errors) instead of being read silently as another window;
+    observations leave the flags clear."""
+    from merlin import _native as nat
+    from merlin.actor_critic import CNNActorCritic
+
+    torch.manual_seed(6)
+    ac = CNNActorCritic((56, 56, 3), 3).to(device)
+    with torch.no_grad():
+        pack = ac.rollout_pack()
+    nat.tower_errors(device, raise_on_error=False)  # clear
+    codes = _observable_codes(device, 300, seed=9)
+    nat.codes_conv3(codes, pack["Qall"], pack["b3"])
+    assert nat.tower_errors(device, raise_on_error=False) == 0
+    import numpy as np
+
+    from test_gpu_obs_gae import pack as pack_codes
+
+    c = np.random.RandomState(9).randint(0, 4, size=(64, 49)).astype(np.uint8)
+    c[:, 45] = 4
+    for cell, cls in ((10, 4), (45, 2)):  # an agent tile at (3, 1); no agent tile at (3, 6)
+        b = c.copy()
+        b[7, cell] = cls
+        bad = torch.from_numpy(pack_codes(b)).to(device)
+        nat.codes_conv3(bad, pack["Qall"], pack["b3"])
+        assert nat.tower_errors(device, raise_on_error=False) == nat.DEVERR_BAD_TILE, cell
+        nat.codes_conv3(bad, pack["Qall"], pack["b3"])
+        with pytest.raises(nat.MerlinNativeError):
+            nat.tower_errors(device)
+    assert nat.tower_errors(device, raise_on_error=False) == 0
