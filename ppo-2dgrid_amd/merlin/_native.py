@@ -230,6 +230,36 @@ EXPORTED_SYMBOLS = (
 _CAPTURE_DEPTH = 0
 _DEFERRED: list = []
 
+_hip_rt = None
+_cu_streams = []  # raw handles of the CU-masked streams (kept for the process's lifetime)
+
+
+def cu_masked_stream(device, keep) -> torch.cuda.ExternalStream:
+    """A stream whose kernels run only on the compute units i with keep(i) true (hipExtStreamCreateWithCUMask;
+    bit i of the mask = CU i).  The fast step's weight gradient on such a stream leaves the other CUs to conv3's
+    backward sums queued beside it on the main stream (merlin/fast_step.py SIDE_CU_GROUPS)."""
+    global _hip_rt
+    if _hip_rt is None:
+        _hip_rt = C.CDLL("libamdhip64.so")
+        _hip_rt.hipExtStreamCreateWithCUMask.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_uint32)]
+    dev = torch.device(device)
+    n = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (n + 31) // 32
+    mask = (C.c_uint32 * words)()
+    for i in range(n):
+        if keep(i):
+            mask[i // 32] |= 1 << (i % 32)
+    if not any(mask):
+        raise MerlinNativeError("cu_masked_stream: empty CU mask")
+    h = C.c_void_p()
+    with torch.cuda.device(dev):
+        err = _hip_rt.hipExtStreamCreateWithCUMask(C.byref(h), words, mask)
+    if err != 0:
+        raise MerlinNativeError(f"hipExtStreamCreateWithCUMask failed ({err})")
+    _cu_streams.append(h.value)
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
 
 @contextlib.contextmanager
 def capture_guard():

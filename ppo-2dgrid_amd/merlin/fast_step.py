@@ -189,6 +189,10 @@ class WeightStage:
 WGRAD_EARLY = False
 WGRAD_SIDE = True  # False: the weight gradient on the main stream (diagnostics)
 SIDE_PRIORITY = 0  # the side stream's priority (torch.cuda.Stream priority: lower = higher priority)
+# the side stream restricted to this many of every 4 groups of 8 compute units (0: all CUs).  The LDS-DMA weight
+# gradient's blocks hold a CU's LDS and registers whole, so beside it conv3's backward sums only get the CUs its
+# retiring blocks free; a CU mask keeps the other groups for them
+SIDE_CU_GROUPS = 0
 # < 0: the step's main-stream kernels on a stream of that (higher) priority, so that conv3's backward chain gets CUs
 # ahead of the side-stream weight gradient.  Off: on the high-priority queue every small kernel took 4-6x longer
 # (k_zero_fill 44 vs 8 us, k_colsum 50 vs 7), 286 vs 168 ms per update (profiles/r05n_fast_mainhi_timeline.txt)
@@ -295,9 +299,13 @@ class WindowStep:
                 p.grad = v
 
     def side_stream(self, device):
-        if self._side is None or getattr(self, "_side_prio", 0) != SIDE_PRIORITY:
-            self._side = torch.cuda.Stream(device=device, priority=SIDE_PRIORITY)
-            self._side_prio = SIDE_PRIORITY
+        key = (SIDE_PRIORITY, SIDE_CU_GROUPS)
+        if self._side is None or getattr(self, "_side_key", None) != key:
+            if SIDE_CU_GROUPS:  # the weight gradient on SIDE_CU_GROUPS of every 4 groups of 8 CUs
+                self._side = nat.cu_masked_stream(device, lambda i: (i // 8) % 4 < SIDE_CU_GROUPS)
+            else:
+                self._side = torch.cuda.Stream(device=device, priority=SIDE_PRIORITY)
+            self._side_key = key
         return self._side
 
     def step(self, plan, mb, mb_idx, actions, logp_old, adv, ret, totals):

@@ -63,6 +63,7 @@ def main():
 
             FS.WGRAD_EARLY = "wgrad_early" in name
             FS.SIDE_PRIORITY = -1 if "sidehi" in name else 0
+            FS.SIDE_CU_GROUPS = next((int(t[2:]) for t in name.split("_") if t[:2] == "cu" and t[2:].isdigit()), 0)
             FS.MAIN_PRIORITY = -1 if "mainhi" in name else 0
             FS.WINDOW_H3 = "wh3" in name
             FS.WGRAD_SPLIT_SIDE = "splitside" in name
