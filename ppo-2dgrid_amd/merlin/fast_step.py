@@ -187,7 +187,11 @@ class WeightStage:
 # fc1's weight gradient on the side stream from right after the heads' backward (True: beside the input gradient
 # too) or from after the input gradient (False: beside conv3's segmented sums only)
 WGRAD_EARLY = False
-WGRAD_SIDE = True  # False: the weight gradient on the main stream (diagnostics)
+# the weight gradient on a side stream beside conv3's backward sums (True), or on the main stream after the input
+# gradient (False, round 6): the LDS-DMA kernel's blocks hold a CU whole, so the two only time-share the chip, and
+# serial was as fast or faster (scripts/ab_update.py 3 5 fast,fast_wgradmain: 167.1 vs 168.7 ms per update,
+# profiles/r06a_ab.log; a CU-masked side stream was far slower, 229-388 ms) -- and each kernel's time is its own
+WGRAD_SIDE = False
 SIDE_PRIORITY = 0  # the side stream's priority (torch.cuda.Stream priority: lower = higher priority)
 # the side stream restricted to this many of every 4 groups of 8 compute units (0: all CUs).  The LDS-DMA weight
 # gradient's blocks hold a CU's LDS and registers whole, so beside it conv3's backward sums only get the CUs its

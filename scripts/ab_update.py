@@ -69,7 +69,7 @@ def main():
             FS.WGRAD_SPLIT_SIDE = "splitside" in name
             FS.PATCH_REUSE = False if "noreuse" in name else "copy" if "reusecopy" in name else "gather"
             nat.H3_HEADS_EPILOGUE = "noheadsepi" not in name
-            FS.WGRAD_SIDE = "wgradmain" not in name  # the weight gradient on the main stream (no overlap)
+            FS.WGRAD_SIDE = "wgradside" in name  # the weight gradient on a side stream beside conv3's sums
             FS.MASK_COPY_SIDE = "maskside" in name  # the mask-word copy on the side stream
             FS.MASK_ROWS = "maskcopy" not in name  # the mask-word copy instead of the R pass's row map
             FS.DZ_PLANES = "nodzp" not in name  # dz in fp32 (split by the GEMMs) instead of head_bwd's planes

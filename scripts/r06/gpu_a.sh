@@ -9,7 +9,7 @@ tail -30 gpurun_out/r06a_grad.log; crash $rc && exit $rc
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_dz_planes.py \
     tests/test_gpu_h3.py > gpurun_out/r06a_tests.log 2>&1 || { tail -30 gpurun_out/r06a_tests.log; exit 1; }
 tail -3 gpurun_out/r06a_tests.log
-timeout -k 10 300 python -u scripts/ab_update.py 3 5 fast_timers4,fast_wgradmain_timers4 > gpurun_out/r06a_ab.log 2>&1 \
+timeout -k 10 300 python -u scripts/ab_update.py 3 5 fast_timers4,fast_wgradmain_timers4,fast_cu3_timers4,fast_cu2_timers4 > gpurun_out/r06a_ab.log 2>&1 \
     || { tail -30 gpurun_out/r06a_ab.log; exit 1; }
 tail -40 gpurun_out/r06a_ab.log
 timeout -k 10 200 python -u scripts/probe_cfg3.py 4096 256 8 1 > gpurun_out/r06a_cfg3_rank.log 2>&1 \
