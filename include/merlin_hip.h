@@ -169,11 +169,13 @@ int merlin_env_act_step(merlin_env *env, const float *head_part_dev, int32_t n_p
  * Wa [G][act_dim][512] + ba [G][act_dim], Wc [G][512] + bc [G] (the heads).  Writes a3_ws [2G][576] (conv3's
  * output) and head_part float[2][8][G][4]: tower t, fc1 column chunk p (64 columns), the chunk's dot products of
  * relu(fc1) with the task's head weights (the biases added in chunk 0) -- the partials merlin_env_act_step reads
- * (with zero biases) to draw and step every task's env.  fp32. */
+ * (with zero biases) to draw and step every task's env.  fp32.  shared_weights = 1: every task acts with ONE weight set
+ * (the tensors hold one task's: T2 [2][2720][64], ..., Wa [1][act_dim][512]) -- the support rollout, where every fast
+ * policy is still the meta policy (src/fomaml.py:164-171), reads 2 towers' weights instead of 2G copies. */
 int merlin_group_act(const uint32_t *codes_dev, int32_t groups, const float *T2_dev, const float *b2_dev,
                      const float *W3t_dev, const float *b3_dev, const float *W4p_dev, const float *b4_dev,
                      const float *Wa_dev, const float *ba_dev, const float *Wc_dev, const float *bc_dev,
-                     int32_t act_dim, float *a3_ws_dev, float *head_part_dev, void *stream);
+                     int32_t act_dim, float *a3_ws_dev, float *head_part_dev, int32_t shared_weights, void *stream);
 /* Look-ahead maps (no reference counterpart: an implementation detail of the auto-reset above).
  * An env's next map depends only on its RNG stream, so it is generated ahead of time into a
  * per-env slot, and an auto-reset takes the slot instead of generating in the step.

@@ -454,14 +454,14 @@ int merlin_env_act_step(merlin_env *e, const float *head_part, int32_t n_parts, 
 int merlin_group_act(const uint32_t *codes, int32_t groups, const float *T2, const float *b2, const float *W3t,
                      const float *b3, const float *W4p, const float *b4, const float *Wa, const float *ba,
                      const float *Wc, const float *bc, int32_t act_dim, float *a3_ws, float *head_part,
-                     void *stream) {
+                     int32_t shared_weights, void *stream) {
     if (groups < 0) return fail(MERLIN_E_INVALID, "negative group count");
     if (act_dim < 1 || act_dim > 4) return fail(MERLIN_E_INVALID, "act_dim must be in [1, 4]");
     if (groups > 0 && (!codes || !T2 || !b2 || !W3t || !b3 || !W4p || !b4 || !Wa || !ba || !Wc || !bc || !a3_ws ||
                        !head_part))
         return fail(MERLIN_E_INVALID, "null argument");
     HIP_TRY(merlin::launch_group_act(codes, groups, T2, b2, W3t, b3, W4p, b4, Wa, ba, Wc, bc, act_dim, a3_ws,
-                                     head_part, (hipStream_t)stream));
+                                     head_part, shared_weights != 0, (hipStream_t)stream));
     return MERLIN_OK;
 }
 

@@ -26,14 +26,19 @@ namespace merlin {
 namespace {
 
 constexpr int GA_NROW = 2720, GA_H = 512, GA_K = 576;
+// k_group_conv's waves: conv3's 576-long reduction is split over GC_W waves (36 k values each, all loads of a wave's
+// W3 slice issued before its FMAs); with 4 waves (round 5) each lane walked 144 k values in 18 dependent load batches
+// and the launch took ~19 us at 32 tasks (profiles/r05b_fomaml_kernel_stats.md)
+constexpr int GC_W = 16, GC_T = 64 * GC_W, GC_KW = GA_K / GC_W;
 
-__global__ __launch_bounds__(256) void k_group_conv(const uint32_t *__restrict__ codes, const float4 *__restrict__ T2,
+__global__ __launch_bounds__(GC_T) void k_group_conv(const uint32_t *__restrict__ codes, const float4 *__restrict__ T2,
                                                     const float *__restrict__ b2, const float *__restrict__ W3t,
-                                                    const float *__restrict__ b3, float *__restrict__ a3) {
+                                                    const float *__restrict__ b3, float *__restrict__ a3, int shared) {
     __shared__ uint8_t cls[52];
     __shared__ float4 a2[25][16];
-    __shared__ float red[4][9][64];
+    __shared__ float red[GC_W][9][64];
     const int tt = blockIdx.x, g = tt >> 1;  // tower tt = 2 g (actor) / 2 g + 1 (critic) of task g
+    const int wt = shared ? (tt & 1) : tt;   // its weights' tower (one weight set for every task when shared)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid < 49) {
         const uint32_t word = codes[(size_t)g * MERLIN_OBS_WORDS + (tid >> 3)];
@@ -41,8 +46,8 @@ __global__ __launch_bounds__(256) void k_group_conv(const uint32_t *__restrict__
     }
     __syncthreads();
     // conv2 + b2 + ReLU at the 25 positions (16 float4 columns each)
-    const float4 *tab = T2 + (size_t)tt * GA_NROW * 16;
-    for (int e = tid; e < 25 * 16; e += 256) {
+    const float4 *tab = T2 + (size_t)wt * GA_NROW * 16;
+    for (int e = tid; e < 25 * 16; e += GC_T) {
         const int p = e >> 4, q = e & 15, py = p / 5, px = p - py * 5;
         int w[9];
 #pragma unroll
@@ -75,38 +80,40 @@ __global__ __launch_bounds__(256) void k_group_conv(const uint32_t *__restrict__
             s.z += v[i].z;
             s.w += v[i].w;
         }
-        const float *bb = b2 + (size_t)tt * 64 + q * 4;
+        const float *bb = b2 + (size_t)wt * 64 + q * 4;
         a2[p][q] = make_float4(fmaxf(s.x + bb[0], 0.0f), fmaxf(s.y + bb[1], 0.0f), fmaxf(s.z + bb[2], 0.0f),
                                fmaxf(s.w + bb[3], 0.0f));
     }
     __syncthreads();
-    // conv3: lane = output channel co, wave wv takes k = tap * 64 + ci in [144 wv, 144 wv + 144) for all 9 positions
+    // conv3: lane = output channel co, wave wv takes k = tap * 64 + ci in [36 wv, 36 wv + 36) for all 9 positions
+    // (its 36 weights loaded before the FMAs: one load round trip per wave)
     const float *a2f = reinterpret_cast<const float *>(&a2[0][0]);
-    const float *w3 = W3t + (size_t)tt * GA_K * 64 + lane;
+    const float *w3 = W3t + (size_t)wt * GA_K * 64 + lane;
     float acc[9];
 #pragma unroll
     for (int p3 = 0; p3 < 9; p3++) acc[p3] = 0.0f;
-    for (int k0 = wv * 144; k0 < wv * 144 + 144; k0 += 8) {
-        float wk[8];
+    const int k0 = wv * GC_KW;
+    float wk[GC_KW];
 #pragma unroll
-        for (int u = 0; u < 8; u++) wk[u] = w3[(size_t)(k0 + u) * 64];
+    for (int u = 0; u < GC_KW; u++) wk[u] = w3[(size_t)(k0 + u) * 64];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int k = k0 + u, tap = k >> 6, ci = k & 63, ky = tap / 3, kx = tap - ky * 3;
+    for (int u = 0; u < GC_KW; u++) {
+        const int k = k0 + u, tap = k >> 6, ci = k & 63, ky = tap / 3, kx = tap - ky * 3;
 #pragma unroll
-            for (int p3 = 0; p3 < 9; p3++) {
-                const int oy = p3 / 3, ox = p3 - oy * 3;
-                acc[p3] += a2f[((oy + ky) * 5 + ox + kx) * 64 + ci] * wk[u];
-            }
+        for (int p3 = 0; p3 < 9; p3++) {
+            const int oy = p3 / 3, ox = p3 - oy * 3;
+            acc[p3] += a2f[((oy + ky) * 5 + ox + kx) * 64 + ci] * wk[u];
         }
     }
 #pragma unroll
     for (int p3 = 0; p3 < 9; p3++) red[wv][p3][lane] = acc[p3];
     __syncthreads();
-    for (int e = tid; e < 9 * 64; e += 256) {
+    for (int e = tid; e < 9 * 64; e += GC_T) {
         const int p3 = e >> 6, co = e & 63;
-        const float s = ((red[0][p3][co] + red[1][p3][co]) + red[2][p3][co]) + red[3][p3][co];
-        a3[(size_t)tt * GA_K + e] = fmaxf(s + b3[(size_t)tt * 64 + co], 0.0f);
+        float s = red[0][p3][co];
+#pragma unroll
+        for (int v = 1; v < GC_W; v++) s += red[v][p3][co];  // wave order
+        a3[(size_t)tt * GA_K + e] = fmaxf(s + b3[(size_t)wt * 64 + co], 0.0f);
     }
 }
 
@@ -114,15 +121,16 @@ __global__ __launch_bounds__(256) void k_group_fc1(const float *__restrict__ a3,
                                                    const float *__restrict__ b4, const float *__restrict__ Wa,
                                                    const float *__restrict__ ba, const float *__restrict__ Wc,
                                                    const float *__restrict__ bc, int G, int A,
-                                                   float *__restrict__ part) {
+                                                   float *__restrict__ part, int shared) {
     __shared__ float red[4][4];
     const int j = blockIdx.x, tt = blockIdx.y, g = tt >> 1, tower = tt & 1;
+    const int wt = shared ? tower : tt, wg = shared ? 0 : g;  // the weights' tower and task
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     float x[9];
 #pragma unroll
     for (int i = 0; i < 9; i++) x[i] = a3[(size_t)tt * GA_K + lane + 64 * i];
     float hp[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // this wave's head partials over its 16 columns
-    const float *wrow = W4p + (size_t)tt * GA_H * GA_K;
+    const float *wrow = W4p + (size_t)wt * GA_H * GA_K;
     for (int n0 = j * 64 + wv * 16; n0 < j * 64 + wv * 16 + 16; n0 += 4) {
         float d[4];
 #pragma unroll
@@ -140,13 +148,13 @@ __global__ __launch_bounds__(256) void k_group_fc1(const float *__restrict__ a3,
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const int n = n0 + c;
-            const float h = fmaxf(d[c] + b4[(size_t)tt * GA_H + n], 0.0f);
+            const float h = fmaxf(d[c] + b4[(size_t)wt * GA_H + n], 0.0f);
             if (tower == 0) {
 #pragma unroll
                 for (int a = 0; a < 4; a++)
-                    if (a < A) hp[a] += h * Wa[((size_t)g * A + a) * GA_H + n];
+                    if (a < A) hp[a] += h * Wa[((size_t)wg * A + a) * GA_H + n];
             } else {
-                hp[0] += h * Wc[(size_t)g * GA_H + n];
+                hp[0] += h * Wc[(size_t)wg * GA_H + n];
             }
         }
     }
@@ -156,7 +164,7 @@ __global__ __launch_bounds__(256) void k_group_fc1(const float *__restrict__ a3,
     __syncthreads();
     if (tid < 4) {
         float s = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-        if (j == 0) s += tower == 0 ? (tid < A ? ba[(size_t)g * A + tid] : 0.0f) : (tid == 0 ? bc[g] : 0.0f);
+        if (j == 0) s += tower == 0 ? (tid < A ? ba[(size_t)wg * A + tid] : 0.0f) : (tid == 0 ? bc[wg] : 0.0f);
         part[(((size_t)tower * gridDim.x + j) * G + g) * 4 + tid] = s;
     }
 }
@@ -165,14 +173,16 @@ __global__ __launch_bounds__(256) void k_group_fc1(const float *__restrict__ a3,
 
 hipError_t launch_group_act(const uint32_t *codes, int G, const float *T2, const float *b2, const float *W3t,
                             const float *b3, const float *W4p, const float *b4, const float *Wa, const float *ba,
-                            const float *Wc, const float *bc, int A, float *a3, float *part, hipStream_t s) {
+                            const float *Wc, const float *bc, int A, float *a3, float *part, bool shared,
+                            hipStream_t s) {
     if (G <= 0) return hipSuccess;
     if (A < 1 || A > 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_group_conv, dim3(2 * G), dim3(256), 0, s, codes, reinterpret_cast<const float4 *>(T2), b2,
-                       W3t, b3, a3);
+    hipLaunchKernelGGL(k_group_conv, dim3(2 * G), dim3(GC_T), 0, s, codes, reinterpret_cast<const float4 *>(T2), b2,
+                       W3t, b3, a3, (int)shared);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_group_fc1, dim3(GA_H / 64, 2 * G), dim3(256), 0, s, a3, W4p, b4, Wa, ba, Wc, bc, G, A, part);
+    hipLaunchKernelGGL(k_group_fc1, dim3(GA_H / 64, 2 * G), dim3(256), 0, s, a3, W4p, b4, Wa, ba, Wc, bc, G, A, part,
+                       (int)shared);
     return hipGetLastError();
 }
 

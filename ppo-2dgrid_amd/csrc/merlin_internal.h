@@ -188,7 +188,7 @@ struct StepOut {
 hipError_t zero_async(void *p, size_t bytes, hipStream_t s);
 hipError_t launch_group_act(const uint32_t *codes, int G, const float *T2, const float *b2, const float *W3t,
                             const float *b3, const float *W4p, const float *b4, const float *Wa, const float *ba,
-                            const float *Wc, const float *bc, int A, float *a3, float *part, hipStream_t s);
+                            const float *Wc, const float *bc, int A, float *a3, float *part, bool shared, hipStream_t s);
 hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                               int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
                               int64_t c_stride, int cfg, hipStream_t s, const int32_t *a_rows = nullptr,

@@ -79,7 +79,7 @@ def lib():
     L.merlin_env_seed.argtypes = [vp, u64p, i32, vp]
     L.merlin_env_reset.argtypes = [vp, vp, vp, vp]
     L.merlin_env_step.argtypes = [vp, vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, i32, vp]
-    L.merlin_group_act.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp]
+    L.merlin_group_act.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, vp]
     L.merlin_env_act_step.argtypes = [vp, vp, i32, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp, vp, vp,
                                       vp, vp, vp, vp, vp, vp]
     L.merlin_env_set_refill_interval.argtypes = [vp, i32]
@@ -1194,13 +1194,17 @@ H3_TN_SPLITS = 32
 
 def group_act(codes, T2, b2, W3t, b3, W4p, b4, Wa, ba, Wc, bc, a3_ws=None, part=None):
     """FOMAML's acting step over G tasks with per-task weights (merlin_group_act): head partials f32[2, 8, G, 4]
-    (biases added in chunk 0) for merlin_env_act_step / act_draw with zero biases."""
+    (biases added in chunk 0) for merlin_env_act_step / act_draw with zero biases.  Weights of ONE task (T2 with 2
+    towers) with G > 1 frames: every task acts with them (shared_weights)."""
     G = int(codes.shape[0])
     A = int(Wa.shape[1])
+    W = int(T2.shape[0]) // 2  # weight sets: G, or 1 shared by every task
+    shared = W == 1 and G > 1
+    assert W == G or shared
     assert codes.dtype == torch.int32 and codes.shape == (G, OBS_WORDS) and codes.is_contiguous()
-    assert T2.shape == (2 * G, 2720, 64) and W3t.shape == (2 * G, 576, 64) and W4p.shape == (2 * G, 512, 576)
-    assert b2.numel() == 2 * G * 64 and b3.numel() == 2 * G * 64 and b4.numel() == 2 * G * 512
-    assert Wa.shape == (G, A, 512) and ba.numel() == G * A and Wc.numel() == G * 512 and bc.numel() == G
+    assert T2.shape == (2 * W, 2720, 64) and W3t.shape == (2 * W, 576, 64) and W4p.shape == (2 * W, 512, 576)
+    assert b2.numel() == 2 * W * 64 and b3.numel() == 2 * W * 64 and b4.numel() == 2 * W * 512
+    assert Wa.shape == (W, A, 512) and ba.numel() == W * A and Wc.numel() == W * 512 and bc.numel() == W
     for t in (T2, b2, W3t, b3, W4p, b4, Wa, ba, Wc, bc):
         assert t.dtype == torch.float32 and t.is_contiguous()
     if a3_ws is None:
@@ -1209,7 +1213,8 @@ def group_act(codes, T2, b2, W3t, b3, W4p, b4, Wa, ba, Wc, bc, a3_ws=None, part=
         part = torch.empty((2, 8, G, 4), dtype=torch.float32, device=codes.device)
     with KernelTimer.span("k_group_act", G * 2 * (25 * 16 * 256 + 576 * 64 * 4 + 512 * 576 * 4)):
         check(lib().merlin_group_act(ptr(codes), G, ptr(T2), ptr(b2), ptr(W3t), ptr(b3), ptr(W4p), ptr(b4), ptr(Wa),
-                                     ptr(ba), ptr(Wc), ptr(bc), A, ptr(a3_ws), ptr(part), stream_of(codes)),
+                                     ptr(ba), ptr(Wc), ptr(bc), A, ptr(a3_ws), ptr(part), int(shared),
+                                     stream_of(codes)),
               "merlin_group_act")
     return part
 

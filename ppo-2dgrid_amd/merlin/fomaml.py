@@ -118,14 +118,17 @@ class FOMAML:
         st["last"].copy_(last)
 
     @torch.no_grad()
-    def collect_trajectory(self, env: MerlinVecEnv, params, steps: int, key: str = "rollout"):
+    def collect_trajectory(self, env: MerlinVecEnv, params, steps: int, key: str = "rollout",
+                           host_stats: bool = True):
         """k steps of every task in parallel (collect_trajectory, src/fomaml.py:54-108), each task acting
         with its own weights params[name] [G, *shape] (None: the meta policy for every task).  The first
         call per key records the rollout as a HIP graph; later calls refresh the weights in place and
-        replay it."""
+        replay it.  host_stats=False: the episode lists and the env's error flags are not read back (each is a
+        host synchronisation; meta_train_step reads the query's once, after everything is queued)."""
         G = env.num_envs
-        if params is None:
-            params = {n: p.detach().unsqueeze(0).expand(G, *p.shape) for n, p in self.meta_policy.named_parameters()}
+        if params is None:  # the meta policy for every task: one weight set, read by every task's acting step
+            W = 1 if self.fused_act else G  # (merlin_group_act shared_weights; the torch path needs G copies)
+            params = {n: p.detach().unsqueeze(0).expand(W, *p.shape) for n, p in self.meta_policy.named_parameters()}
         st = self._rollout_state(key, G, steps, params)
         if st["graph"] is None:
             gp.pack_into(st["pack"], params)
@@ -147,11 +150,17 @@ class FOMAML:
         else:
             gp.pack_into(st["pack"], params)
             st["graph"].replay()
+        out = {"codes": st["codes"], "act": st["act"], "logp": st["logp"], "val": st["val"], "rew": st["rew"],
+               "done": st["done"], "last_val": st["last"]}
+        if host_stats:
+            out.update(self._episode_stats(env, st))
+        return out
+
+    @staticmethod
+    def _episode_stats(env, st):
         env.errors()
         d = st["done"] > 0
-        return {"codes": st["codes"], "act": st["act"], "logp": st["logp"], "val": st["val"], "rew": st["rew"],
-                "done": st["done"], "last_val": st["last"], "ep_rews": st["epr"][d].cpu().tolist(),
-                "ep_lens": st["epl"][d].cpu().tolist()}
+        return {"ep_rews": st["epr"][d].cpu().tolist(), "ep_lens": st["epl"][d].cpu().tolist()}
 
     # ---------------------------------------------------------------- loss
     def compute_loss(self, batch, params):
@@ -197,7 +206,8 @@ class FOMAML:
         self.meta_optimizer.zero_grad()
         names = [n for n, _ in self.meta_policy.named_parameters()]
         # inner loop: all fast policies start as the meta policy -> batched support rollout
-        support = self.collect_trajectory(env, None, k_support, key="support")
+        # the support rollout's episodes are not reported (:171-176): no host read-back between it and the inner step
+        support = self.collect_trajectory(env, None, k_support, key="support", host_stats=False)
         fast = bp.stack_params(self.meta_policy, G)
         loss_s, _ = self.compute_loss(support, fast)
         grads = dict(zip(names, torch.autograd.grad(loss_s, [fast[n] for n in names])))
@@ -205,13 +215,15 @@ class FOMAML:
         with torch.no_grad():
             adapted = {n: (fast[n] - self.lr_inner * grads[n]).detach().requires_grad_(True) for n in names}
         # outer loop: query rollouts with each task's adapted policy
-        query = self.collect_trajectory(env, adapted, k_query, key="query")
+        query = self.collect_trajectory(env, adapted, k_query, key="query", host_stats=False)
         loss_q, qstats = self.compute_loss(query, adapted)
         qgrads = torch.autograd.grad(loss_q, [adapted[n] for n in names])
         for (n, p), g in zip(self.meta_policy.named_parameters(), qgrads):
             p.grad = g.sum(dim=0) / G  # sum of the tasks' fast grads / n_tasks (:198-209)
         torch.nn.utils.clip_grad_norm_(self.meta_policy.parameters(), max_norm=0.5)
         self.meta_optimizer.step()
+        # the host reads of the meta step, once everything is queued (env error flags: both rollouts')
+        query.update(self._episode_stats(env, self._rollouts["query"]))
         avg_loss = float(qstats["loss"].mean().item())
         if query["ep_rews"]:
             avg_rew, avg_steps = float(np.mean(query["ep_rews"])), float(np.mean(query["ep_lens"]))

@@ -108,3 +108,18 @@ def test_group_act_parts_match_per_task_models(device, G):
         assert int(a[g]) == int(a2[0])
         torch.testing.assert_close(lp[g], lp2[0], rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(v[g], v2[0], rtol=1e-5, atol=1e-5)
+
+
+def test_group_act_shared_weights_equal_per_task_copies(device):
+    """merlin_group_act with ONE weight set for every task (shared_weights: FOMAML's support rollout, where each fast
+    policy is still the meta policy) gives the same bits as G stacked copies of that set."""
+    from merlin import grouped_policy as gp
+
+    G = 32
+    models, _ = _tasks(device, 1, seed=77)
+    one = {n: p.detach().unsqueeze(0) for n, p in models[0].named_parameters()}
+    copies = {n: p.expand(G, *p.shape[1:]).contiguous() for n, p in one.items()}
+    codes = _codes(device, G, seed=5)
+    a = gp.act_parts(gp.pack(one), codes)
+    b = gp.act_parts(gp.pack(copies), codes)
+    assert torch.equal(a, b)
