@@ -83,6 +83,7 @@ extern "C" {
 /* device error bits reported by merlin_env_errors */
 #define MERLIN_DEVERR_BAD_ACTION 1u  /* action not in {0,1,2}: ThreeActionWrapper IndexError */
 #define MERLIN_DEVERR_PLACE_OBJ 2u   /* place_obj max_tries exceeded: RecursionError */
+#define MERLIN_DEVERR_SLOT_EMPTY 8u  /* a reset met an empty look-ahead slot with the step fallback off */
 #define MERLIN_DEVERR_BAD_TILE 4u    /* merlin_tower_codes_conv3: a frame that is no observation (the agent tile (class
                                       * 4) missing at view cell (3, 6) or present elsewhere): merlin_tower_errors */
 
@@ -187,6 +188,12 @@ int merlin_group_act(const uint32_t *codes_dev, int32_t groups, const float *T2_
  * either way. */
 int merlin_env_set_refill_interval(merlin_env *env, int32_t every);
 int merlin_env_refill(merlin_env *env, void *stream);
+/* step_fallback (default on): with refill interval 0, single-step launches are followed by the fallback pass that
+ * generates the map of a reset whose slot was empty.  A caller that refills every used slot after EVERY step, before
+ * the next one (PPO's rollout: merlin_env_refill on a side stream, joined), can never meet an empty slot and may turn
+ * the pass off (one launch -- one graph node -- fewer per step); an empty slot then raises MERLIN_DEVERR_SLOT_EMPTY
+ * (merlin_env_errors) and that step's results are invalid. */
+int merlin_env_set_step_fallback(merlin_env *env, int32_t on);
 /* The fully observable observation (FullyObsWrapper + ImgObsWrapper, src/scenario_creator/scenario_creator.py:45-50,
  * observation.fully_observable in src/config/scenario.yaml) of every env's current state: out_dev uint8[N][size][size]
  * [3], out[i][x][y] = minigrid Grid.encode's (object, color, state) of cell (x, y), the agent's cell (10, 0, dir).

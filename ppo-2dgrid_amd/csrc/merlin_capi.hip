@@ -17,6 +17,7 @@ struct merlin_env {
     bool has_state;
     int steps_since_refill;  // merlin_env_step launches since the last look-ahead refill
     int refill_every;        // 0: the caller launches refills (merlin_env_refill)
+    bool no_fallback = false;  // merlin_env_set_step_fallback(0): with refill_every 0, no k_env_fallback pass
 };
 
 namespace {
@@ -417,6 +418,7 @@ int merlin_env_step(merlin_env *e, const int64_t *actions, int32_t n_steps, int6
     o.ep_len_out = ep_len;
     const bool refill = e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
     if (refill) e->steps_since_refill = 0;
+    o.no_fallback = e->no_fallback && e->refill_every == 0;
     HIP_TRY(merlin::launch_env_step(e->dev, o, refill, (hipStream_t)stream));
     return MERLIN_OK;
 }
@@ -447,6 +449,7 @@ int merlin_env_act_step(merlin_env *e, const float *head_part, int32_t n_parts, 
                           deterministic ? 1 : 0, seed, epoch, step, env_offset, action, logp, value};
     const bool refill = e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
     if (refill) e->steps_since_refill = 0;
+    o.no_fallback = e->no_fallback && e->refill_every == 0;
     HIP_TRY(merlin::launch_env_step(e->dev, o, refill, (hipStream_t)stream));
     return MERLIN_OK;
 }
@@ -462,6 +465,12 @@ int merlin_group_act(const uint32_t *codes, int32_t groups, const float *T2, con
         return fail(MERLIN_E_INVALID, "null argument");
     HIP_TRY(merlin::launch_group_act(codes, groups, T2, b2, W3t, b3, W4p, b4, Wa, ba, Wc, bc, act_dim, a3_ws,
                                      head_part, shared_weights != 0, (hipStream_t)stream));
+    return MERLIN_OK;
+}
+
+int merlin_env_set_step_fallback(merlin_env *e, int32_t on) {
+    if (!e) return fail(MERLIN_E_INVALID, "null env");
+    e->no_fallback = on == 0;
     return MERLIN_OK;
 }
 

@@ -854,6 +854,7 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
                 if (!take_slot<SP, SBLK>(E, i, rows, lane, g)) {
                     E.rflag[i] = 1;
                     E.bflag[blockIdx.x] = 1;
+                    if (O.no_fallback) err |= MERLIN_DEVERR_SLOT_EMPTY;  // no fallback pass follows: an error
                     if (err) atomicOr(E.err, err);
                     return;
                 }
@@ -955,7 +956,10 @@ static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t 
         hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_env_fallback<SP>, dim3((nb + BLK - 1) / BLK), dim3(BLK), 0, s, E, O.obs);
+        // (no_fallback: the caller refills every used slot after every step, before the next one -- PPO's rollout --
+        // so no reset can find its slot empty; the pass and its graph node are left out)
+        if (!O.no_fallback)
+            hipLaunchKernelGGL(k_env_fallback<SP>, dim3((nb + BLK - 1) / BLK), dim3(BLK), 0, s, E, O.obs);
     } else {
         hipLaunchKernelGGL((k_env_step<SP, false>), dim3(nb), dim3(SBLK), 0, s, E, O);
     }

@@ -63,7 +63,10 @@ typedef __attribute__((address_space(3))) p_u32x4 lds_u32x4;
 // one 16-B LDS fragment read (a plain load: the k loop is unrolled, so the compiler's waits are exact counts)
 __device__ __forceinline__ void lds_rd(p_u32x4 &d, uint32_t addr) { d = *(const lds_u32x4 *)(uintptr_t)addr; }
 
-template <int BM, int BN, int WGM, int WGN, int EPI, int NK>
+// NS: LDS stages of the DMA ring (NS - 1 k steps in flight).  3: 120 KB at 128 x 192; 4 (round 6): 160 KB, the whole
+// LDS of a CU -- a step's DMA is latency-bound (~2.5 us under load against ~1.2 us of MFMA work per step), so the
+// feed rate per CU is the bytes in flight over that latency
+template <int BM, int BN, int WGM, int WGN, int EPI, int NK, int NS = 3>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restrict__ A, const p_u32x4 *__restrict__ B,
                                                           const uint32_t *__restrict__ amaxA,
                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N, int K,
@@ -78,7 +81,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
     static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "whole DMA instructions per thread");
     constexpr int STG = (BM + BN) * 8;  // chunks per stage
     constexpr uint32_t STG_B = STG * 16;
-    __shared__ p_u32x4 lds[3 * STG];
+    static_assert(NS == 3 || NS == 4, "ring depth");
+    __shared__ p_u32x4 lds[NS * STG];
 
     const int t = blockIdx.y;
     const int L = p_xcd_tile(blockIdx.x, gridDim.x);
@@ -179,25 +183,24 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
         for (int j = 0; j < TN; j++) asm volatile("" ::"v"(f.b[j][0]), "v"(f.b[j][1]));
     };
 
-    static_assert(NK >= 2, "two k steps at least");
-    issue(0, 0);
-    issue(1, 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    static_assert(NK >= NS - 1, "the prologue's k steps");
+    constexpr int D = NS - 1;  // k steps in flight
+    static_for<D>([&](auto KT) __attribute__((always_inline)) { issue(decltype(KT)::value, decltype(KT)::value); });
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (D - 1)) : "memory");  // step 0 landed
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     Frag f0, f1;
     static_for<NR>([&](auto K_) __attribute__((always_inline)) { rd(f0, K_, 0, IC<0>{}); });
     static_for<NK>([&](auto KT) __attribute__((always_inline)) {
-        constexpr int kt = decltype(KT)::value, st = kt % 3, sn = (kt + 1) % 3;
-        if constexpr (kt + 2 < NK) issue(kt + 2, (kt + 2) % 3);  // the stage read in step kt - 1
+        constexpr int kt = decltype(KT)::value, st = kt % NS, sn = (kt + 1) % NS;
+        if constexpr (kt + D < NK) issue(kt + D, (kt + D) % NS);  // the stage read in step kt - 1
         __builtin_amdgcn_sched_barrier(0);
         half(f0, f1, (uint32_t)st * STG_B, IC<1>{}, IC<1>{});  // MFMAs of half 0, reads of half 1
         if constexpr (kt + 1 < NK) {
             touch(f1);  // the compiler's wait for f1 here, before the barrier
-            if constexpr (kt + 2 < NK)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // step kt + 1 landed: the steps issued after it (up to kt + D, those that exist) may stay in flight
+            constexpr int later = (NK - 1 < kt + D ? NK - 1 : kt + D) - (kt + 1);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * later) : "memory");
             __builtin_amdgcn_s_barrier();  // step kt + 1 published; every wave is past its reads of step kt - 1
             __builtin_amdgcn_sched_barrier(0);
             half(f1, f0, (uint32_t)sn * STG_B, IC<0>{}, IC<1>{});  // MFMAs of half 1, reads of the next half 0
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
     }
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, int NS = 3>
 hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
     if (N % BN || K % 32 || K < 64) return hipErrorInvalidValue;
@@ -239,10 +242,10 @@ hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const 
 #define PQ_K(NK)                                                                                                   \
     do {                                                                                                           \
         if (bias)                                                                                                  \
-            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 1, NK>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K,   \
+            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 1, NK, NS>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
                                sA / 4, sB / 4, bias, C, sC, tiles_n);                                              \
         else                                                                                                       \
-            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 0, NK>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K,   \
+            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 0, NK, NS>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
                                sA / 4, sB / 4, nullptr, C, sC, tiles_n);                                           \
     } while (0)
     switch (K) {  // the k loop is unrolled: one instantiation per depth (fc1's forward K = 576, input gradient 512)
@@ -782,6 +785,8 @@ hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *
         case 60: return pq_launch<128, 256, 2, 4>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 61: return pq_launch<256, 128, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 62: return pq_launch<128, 192, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        // round 6: the same with a 4-stage ring (160 KB of LDS, three k steps in flight)
+        case 63: return pq_launch<128, 192, 4, 2, 4>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -180,6 +180,7 @@ struct StepOut {
     double *ep_ret_out;
     int32_t *ep_len_out;
     ActIn act;  // act.part != null (n_steps == 1): the action of env i is drawn from the heads' partials first
+    int no_fallback;  // single-step launches: no k_env_fallback pass; an empty slot raises MERLIN_DEVERR_SLOT_EMPTY
 };
 
 // Zero `bytes` bytes at p on stream s with a kernel (vector stores).  Every zero-fill of the library goes

@@ -18,6 +18,8 @@
 // order; a destination whose entries span items gets the items' partial sums added in item
 // order by k_seg_fix.  No atomics: bitwise reproducible.
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 
 #include "merlin_internal.h"
 
@@ -417,7 +419,34 @@ __device__ __forceinline__ void seg_fix_row(const float2 *__restrict__ carry, in
         *o = acc;
     }
 }
-template <int MASK, int ROLE>
+// A64 (opt-in, MERLIN_SEG_F64=1): the per-destination partial sums of an item accumulate in f64 and are rounded to
+// fp32 once, when flushed (the carries are then added in fp32, k_seg_fix's order).  Measured in round 6: the benched
+// update's first-step gradient is within ~3e-7 of float64 either way (tests/test_gpu_update_grad.py, both runs in
+// profiles/r06c_grad*.log), and the f64 adds cost the R pass 16 us per minibatch (profiles/r06c_ab*.log), so fp32
+// accumulation stays the default.
+struct SegAcc64 {
+    double x, y, z, w;
+};
+__device__ __forceinline__ void seg_zero(float4 &a) { a = make_float4(0.0f, 0.0f, 0.0f, 0.0f); }
+__device__ __forceinline__ void seg_zero(SegAcc64 &a) { a = SegAcc64{0.0, 0.0, 0.0, 0.0}; }
+__device__ __forceinline__ void seg_add(float4 &a, const float4 v) { f4_add(a, v); }
+__device__ __forceinline__ void seg_add(SegAcc64 &a, const float4 v) {
+    a.x += (double)v.x;
+    a.y += (double)v.y;
+    a.z += (double)v.z;
+    a.w += (double)v.w;
+}
+// the two parity lanes' partials of a destination added (lanes q and q ^ 1 compute the same sum), as fp32
+__device__ __forceinline__ float4 seg_pair(const float4 a) {
+    return make_float4(a.x + __shfl_xor(a.x, 16), a.y + __shfl_xor(a.y, 16), a.z + __shfl_xor(a.z, 16),
+                       a.w + __shfl_xor(a.w, 16));
+}
+__device__ __forceinline__ float4 seg_pair(const SegAcc64 a) {
+    return make_float4((float)(a.x + __shfl_xor(a.x, 16)), (float)(a.y + __shfl_xor(a.y, 16)),
+                       (float)(a.z + __shfl_xor(a.z, 16)), (float)(a.w + __shfl_xor(a.w, 16)));
+}
+
+template <int MASK, int ROLE, bool A64 = true>
 __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__restrict__ src,
                                                            const void *__restrict__ mask, int64_t src_rows,
                                                            const int32_t *__restrict__ idx,
@@ -447,14 +476,12 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
         const bool xfirst = e0 > 0 && key[e0 - 1] == kfirst;
         const bool xlast = e1 < nnz && key[e1] == klast;
         const bool to_head_last = kfirst == klast && xlast;
-        float4 head = zero, tail = zero, acc = zero;
+        float4 head = zero, tail = zero;
+        std::conditional_t<A64, SegAcc64, float4> acc;
+        seg_zero(acc);
         int cur = -1;
         auto flush = [&]() {  // wave-uniform call sites (keys are uniform)
-            float4 o = acc;
-            o.x += __shfl_xor(acc.x, 16);
-            o.y += __shfl_xor(acc.y, 16);
-            o.z += __shfl_xor(acc.z, 16);
-            o.w += __shfl_xor(acc.w, 16);
+            const float4 o = seg_pair(acc);
             if (cur == kfirst && (xfirst || to_head_last))
                 head = o;
             else if (cur == klast && xlast)
@@ -535,16 +562,16 @@ __global__ __launch_bounds__(64 * SEG_WAVES) void k_seg_sum(const float4 *__rest
                     if (k0[u] != cur) {
                         if (cur >= 0) flush();
                         cur = k0[u];
-                        acc = zero;
+                        seg_zero(acc);
                     }
-                    if (q == 0) f4_add(acc, vq[u]);
+                    if (q == 0) seg_add(acc, vq[u]);
                     if (k1[u] < 0) break;
                     if (k1[u] != cur) {
                         flush();
                         cur = k1[u];
-                        acc = zero;
+                        seg_zero(acc);
                     }
-                    if (q == 1) f4_add(acc, vq[u]);
+                    if (q == 1) seg_add(acc, vq[u]);
                 }
             }
         }
@@ -719,6 +746,13 @@ hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, 
 }
 
 namespace {
+bool seg_f32() {  // fp32 accumulation unless MERLIN_SEG_F64=1 (read once per process)
+    static const bool v = [] {
+        const char *e = getenv("MERLIN_SEG_F64");
+        return !(e && e[0] == '1');
+    }();
+    return v;
+}
 template <int ROLE>
 hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t src_rows, const int32_t *idx,
                       const int32_t *key, int64_t nnz, const int32_t *slot, int S, int64_t L, const int32_t *fix,
@@ -731,18 +765,26 @@ hipError_t seg_launch(const float *src, const void *mask, int mask_bits, int64_t
     const int32_t *hf = cnt ? hfix : nullptr;
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
     float4 *o4 = reinterpret_cast<float4 *>(out), *c4 = reinterpret_cast<float4 *>(carry);
+#define SEG_GO(MASK_, A64_, MP_, RP_)                                                                                \
+    hipLaunchKernelGGL((k_seg_sum<MASK_, ROLE, A64_>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, MP_, src_rows, idx, \
+                       key, nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, RP_)
+#define SEG_GO2(MASK_, MP_, RP_)       \
+    do {                               \
+        if (seg_f32())                 \
+            SEG_GO(MASK_, false, MP_, RP_); \
+        else                           \
+            SEG_GO(MASK_, true, MP_, RP_);  \
+    } while (0)
     if (mask && mask_bits && mrow)
-        hipLaunchKernelGGL((k_seg_sum<3, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, mask, src_rows, idx, key,
-                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, mrow);
+        SEG_GO2(3, mask, mrow);
     else if (mask && mask_bits)
-        hipLaunchKernelGGL((k_seg_sum<2, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, mask, src_rows, idx, key,
-                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, nullptr);
+        SEG_GO2(2, mask, nullptr);
     else if (mask)
-        hipLaunchKernelGGL((k_seg_sum<1, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, mask, src_rows, idx, key,
-                           nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, nullptr);
+        SEG_GO2(1, mask, nullptr);
     else
-        hipLaunchKernelGGL((k_seg_sum<0, ROLE>), dim3(grid), dim3(64 * SEG_WAVES), 0, s, s4, nullptr, src_rows, idx,
-                           key, nnz, slot, S, L, nitems, T, o4, out_rows, c4, acc_out, mark, fx, hf, cnt, nullptr);
+        SEG_GO2(0, nullptr, nullptr);
+#undef SEG_GO2
+#undef SEG_GO
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || nfix <= 0 || cnt) return e;
     const int gfix = (int)std::min<int64_t>((nfix + 3) / 4, 256 * 8);

@@ -24,6 +24,7 @@ OBS_WORDS = 8
 DEVERR_BAD_ACTION = 1
 DEVERR_PLACE_OBJ = 2
 DEVERR_BAD_TILE = 4  # merlin_tower_codes_conv3 saw a frame that is no observation (merlin_tower_errors)
+DEVERR_SLOT_EMPTY = 8  # a reset met an empty look-ahead slot with the step fallback off (merlin_env_set_step_fallback)
 
 DIFFICULTY_IDS = {"easy": 0, "medium": 1, "mediumhard": 2, "hard": 3, "hardest": 4}
 
@@ -83,6 +84,7 @@ def lib():
     L.merlin_env_act_step.argtypes = [vp, vp, i32, vp, vp, i32, i32, C.c_uint64, vp, i64, i64, vp, vp, vp, vp, vp,
                                       vp, vp, vp, vp, vp, vp]
     L.merlin_env_set_refill_interval.argtypes = [vp, i32]
+    L.merlin_env_set_step_fallback.argtypes = [vp, i32]
     L.merlin_env_refill.argtypes = [vp, vp]
     L.merlin_env_get_state.argtypes = [vp, vp, vp, vp, vp]
     L.merlin_env_full_obs.argtypes = [vp, vp, vp]
@@ -203,7 +205,7 @@ EXPORTED_SYMBOLS = (
     "merlin_version", "merlin_last_error", "merlin_tile_atlas", "merlin_env_config_layout", "merlin_env_create",
     "merlin_env_destroy", "merlin_env_seed", "merlin_env_reset", "merlin_env_step", "merlin_env_act_step", "merlin_group_act",
     "merlin_env_set_refill_interval", "merlin_env_refill",
-    "merlin_env_get_state", "merlin_env_full_obs", "merlin_env_errors", "merlin_env_num_envs", "merlin_env_size",
+    "merlin_env_get_state", "merlin_env_full_obs", "merlin_env_errors", "merlin_env_set_step_fallback", "merlin_env_num_envs", "merlin_env_size",
     "merlin_obs_expand_f32", "merlin_obs_expand_u8", "merlin_gae", "merlin_adv_normalize",
     "merlin_conv1_lut_fwd", "merlin_conv1_lut_bwd", "merlin_tower_conv2_im2col_fwd",
     "merlin_tower_conv2_im2col_bwd", "merlin_tower_conv3_im2col_fwd", "merlin_tower_conv3_col2im_bwd",

@@ -205,6 +205,12 @@ class MerlinVecEnv:
         refills to the caller's refill() (merlin_env_set_refill_interval)."""
         nat.check(self._lib.merlin_env_set_refill_interval(self._h, int(every)), "merlin_env_set_refill_interval")
 
+    def set_step_fallback(self, on: bool) -> None:
+        """on=False: the caller refills every used look-ahead slot after every step (refill(), refill interval 0),
+        so the per-step fallback pass is not launched; a reset that meets an empty slot then raises
+        DEVERR_SLOT_EMPTY in errors() (merlin_env_set_step_fallback)."""
+        nat.check(self._lib.merlin_env_set_step_fallback(self._h, 1 if on else 0), "merlin_env_set_step_fallback")
+
     def refill(self) -> None:
         """Generate the next map of every env whose look-ahead slot was used, on the current stream
         (merlin_env_refill).  Touches only the slots and reads the envs' RNG: it may run on a side
@@ -276,6 +282,9 @@ class MerlinVecEnv:
                             "logits were non-finite, merlin_act_heads)")
             if flags.value & nat.DEVERR_PLACE_OBJ:
                 what.append("place_obj rejection sampling failed (RecursionError)")
+            if flags.value & nat.DEVERR_SLOT_EMPTY:
+                what.append("a reset met an empty look-ahead map slot with the step fallback off (refill() was not "
+                            "run after every step)")
             raise nat.MerlinNativeError("device env error: " + "; ".join(what))
         return flags.value, fb.value
 

@@ -240,6 +240,9 @@ class PPO:
         T = buf.T
         main, side = torch.cuda.current_stream(self.device), self._refill_stream
         every = max(1, int(self.refill_every))
+        # refilled after every step and joined before the next: no reset can meet an empty slot, so the step's
+        # fallback pass (a graph node per step, ~4 us + its dispatch gap) is left out; errors() would report one
+        env.set_step_fallback(side is None or every != 1)
         env.reset(out=buf.codes[0])
         with torch.no_grad():
             self._act_epoch.add_(1)
