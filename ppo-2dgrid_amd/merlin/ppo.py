@@ -75,6 +75,9 @@ ROLLOUT_SCALE_ROWS = True
 # the rollout's draw from the acting GEMM's head partials fused into the env step (merlin_env_act_step; False:
 # k_act_draw + merlin_env_step, one launch more per step)
 FUSE_ACT_STEP = True
+# the env step's fallback pass in the rollout even when the look-ahead slots are refilled after every step (False:
+# left out there, round 6 -- no reset can meet an empty slot; MerlinVecEnv.set_step_fallback)
+ROLLOUT_STEP_FALLBACK = False
 
 
 class PPO:
@@ -242,7 +245,7 @@ class PPO:
         every = max(1, int(self.refill_every))
         # refilled after every step and joined before the next: no reset can meet an empty slot, so the step's
         # fallback pass (a graph node per step, ~4 us + its dispatch gap) is left out; errors() would report one
-        env.set_step_fallback(side is None or every != 1)
+        env.set_step_fallback(ROLLOUT_STEP_FALLBACK or side is None or every != 1)
         env.reset(out=buf.codes[0])
         with torch.no_grad():
             self._act_epoch.add_(1)

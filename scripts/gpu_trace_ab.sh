@@ -1,7 +1,7 @@
 #!/bin/bash
-# round 5 (i): kernel trace of one A/B setting (per-kernel times by template instance)
+# kernel trace of one A/B setting (per-kernel times by template instance)
 R="$GRAFT_REPO_ROOT"; cd "$R"; mkdir -p gpurun_out
-L=${LOG:-r05i}
+L=${LOG:-r06t}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$R/gpurun_out/prof_$L" -o run -- \
     python3 -u "$R/scripts/ab_update.py" 1 5 ${AB:-fast} > "$R/gpurun_out/$L.log" 2>&1

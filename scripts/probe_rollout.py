@@ -20,8 +20,11 @@ def main():
     from merlin import actor_critic as AC
 
     def setting(v):
-        if v.isdigit():
-            agent.refill_every = int(v)
+        from merlin import ppo as PPO_MOD
+
+        PPO_MOD.ROLLOUT_STEP_FALLBACK = v.endswith("fb")  # e.g. 1fb: the per-step fallback pass launched anyway
+        if v.rstrip("fb").isdigit():
+            agent.refill_every = int(v.rstrip("fb"))
             return
         AC.ROLLOUT_FC1_H3 = v.startswith("h3")
         nat.H3_NT_CFG["rollout"] = next((int(t[3:]) for t in v.split("_") if t[:3] == "h3r"), 12)

@@ -57,7 +57,7 @@ def _grad64(g, agent, rec, oracle, golden, adv_n):
     entropy = -(lg.exp() * lg).sum(-1)
     old_logp = torch.from_numpy(g["logp"]).double()[idx]
     adv = adv_n.reshape(-1).double().cpu()[idx]
-    ret = agent.buf.returns.reshape(-1).double().cpu()[idx]
+    ret = rec["ret"].reshape(-1).double().cpu()[idx]
     lr, gamma, lam, clip, vf, ent = (float(v) for v in g["hparams"])
     ratio = torch.exp(new_logp - old_logp)
     pi = -torch.min(ratio * adv, torch.clamp(ratio, 1 - clip, 1 + clip) * adv).mean()
@@ -68,7 +68,7 @@ def _grad64(g, agent, rec, oracle, golden, adv_n):
     return [t * coef for t in grads]
 
 
-def _run(golden, device, ref_adv=False):
+def _run(golden, device, ref_adv=False, oracle_gae=None):
     from merlin import MerlinVecEnv
     from merlin.ppo import PPO
     from test_gpu_obs_gae import pack
@@ -111,15 +111,21 @@ def _run(golden, device, ref_adv=False):
     if ref_adv:  # the reference's normalisation (src/ppo.py:125, fp32 torch on the CPU) of the bit-exact GAE output
         adv_orig = agent._advantages
 
-        def adv_wrap(*a, **k):
-            adv_n, ret = adv_orig(*a, **k)
-            adv = agent.buf.adv.cpu()
-            rec["adv_n"] = ((adv - adv.mean()) / (adv.std() + 1e-8)).to(adv_n.device)
+        def adv_wrap(rewards, values, dones, last_value, *a, **k):
+            # the reference's GAE (the oracle's restatement is bit-exact with src/ppo.py:107-120, gae_ref.npz; with
+            # one env the benched path takes the wave-scan kernel, which reassociates) and its fp32 normalisation
+            _, ret = adv_orig(rewards, values, dones, last_value, *a, **k)
+            adv, r = oracle_gae(g["rewards"][:, None], g["values"][:, None], g["dones"][:, None],
+                                np.array([g["last_value"]], np.float32))
+            adv = torch.from_numpy(np.ascontiguousarray(adv, dtype=np.float32))
+            rec["adv_n"] = ((adv - adv.mean()) / (adv.std() + 1e-8)).to(ret.device)
+            ret.copy_(torch.from_numpy(np.ascontiguousarray(r, dtype=np.float32)).to(ret.device))
             return rec["adv_n"], ret
 
         agent._advantages = adv_wrap
     stats = agent.update(float(g["last_value"]))
     rec.setdefault("adv_n", agent.last_adv_normalized)
+    rec["ret"] = agent.buf.returns
     assert agent._wstep is not None  # the fast (benched) step ran, not the autograd fallback
     return g, agent, named, rec, stats, (B, MB, lr)
 
@@ -131,7 +137,7 @@ def _step_lr(rec, i, lr):
 def test_first_step_gradient_matches_reference(golden, oracle, device):
     """The reference's normalised advantages injected: gradient, pre-clip norm and first Adam step as the reference's;
     the epoch's statistics too."""
-    g, agent, named, rec, stats, (B, MB, lr) = _run(golden, device, ref_adv=True)
+    g, agent, named, rec, stats, (B, MB, lr) = _run(golden, device, ref_adv=True, oracle_gae=oracle.gae_tn)
     assert [n for n, _ in named] == [str(n) for n in g["param_names"]]
     assert agent.last_distinct_frac < 0.75  # the rollout repeats frames (0.52 distinct per sample): grouping exercised
     g64 = _grad64(g, agent, rec, oracle, golden, rec["adv_n"])
