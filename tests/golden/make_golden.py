@@ -379,6 +379,12 @@ def gen_update_grad():
         agent.buffer.add(torch.from_numpy(imgs[t].astype(np.float32)), torch.tensor(actions[t]), lp[t], v[t],
                          torch.tensor(rewards[t]), torch.tensor(dones[t]))
     last_value = float(v[-1].item())
+    # the advantages the update normalises, as it computes them (src/ppo.py:123-125: the reference's own
+    # compute_gae on the buffer, then the fp32 torch moments) -- stored, so a test can feed the benched path the
+    # reference's exact normalised advantages (torch's CPU reductions round by the host's vector ISA)
+    _, _, _, rw, vo, dn = agent.buffer.get()
+    adv_raw, ret_ref = agent.compute_gae(rw, vo, dn, last_value)
+    adv_norm = (adv_raw - adv_raw.mean()) / (adv_raw.std() + 1e-8)
     rec = {}
     norms = []
     clip_orig = torch.nn.utils.clip_grad_norm_
@@ -419,6 +425,7 @@ def gen_update_grad():
         stat_names=np.array(sorted(stats)), stat_vals=np.array([stats[k] for k in sorted(stats)]),
         hparams=np.array([3e-4, 0.99, 0.95, 0.2, 0.5, 0.05]), param_names=np.array(names),
         first_norm=np.float64(norms[0]), norms=np.array(norms),
+        adv_norm=adv_norm.numpy().astype(np.float32), returns=ret_ref.numpy().astype(np.float32),
     )
     for i, (g, d) in enumerate(zip(rec["grads"], rec["delta"])):
         out[f"grad{i}"] = g.numpy().astype(np.float32)  # the clipped gradient Adam consumed
