@@ -55,6 +55,19 @@
  *                        segmented sums of their backward pass (merlin/windows.py)
  *   merlin_tower_bias_relu / _relu_bwd / _head_bwd: the ReLU + bias epilogues of the
  *                        conv3 / fc1 GEMMs and the heads' backward (actor_critic.py:14-41)
+ *
+ * What the benched loop (bench.py, BASELINE cfg 2) calls, per rollout step: merlin_tower_codes_conv3_amax,
+ * merlin_h3_gemm_nt_heads (cfg 12, heads only), merlin_env_act_step, merlin_env_refill; per update:
+ * merlin_gae, merlin_adv_normalize, merlin_minibatch_patch_maps, and per optimizer step merlin_window_lut_*,
+ * merlin_window_gemm_fwd / _bwd, merlin_tower_window_conv3_planes, merlin_h3_gemm_nt_heads (cfg 60),
+ * merlin_ppo_loss*, merlin_tower_head_bwd_planes, merlin_h3_gemm_nt_planes (cfg 62),
+ * merlin_h3_gemm_tn_gather_planes_a (cfg 20), merlin_segment_sum_* (R / S / dQ / dT2), merlin_stage_*,
+ * merlin_clip_adam.  The rest serve the other drop-in paths -- the gym single env and the frame path (obs
+ * expansion, conv1 / conv2 lookups per frame, im2col), the autograd window path, FOMAML (merlin_group_act) -- or
+ * are ALTERNATE forms kept selectable for A/B and float64 precision tests: merlin_x6_* (fc1 in six bf16
+ * products, rounds 2-3), merlin_h3_gemm_nt / _tn / _tn_planes / _nt_gather with the register-staged
+ * configurations (round 4).  Probe-only configurations (kernel ablations that compute wrong results on purpose)
+ * exist only in a -DMERLIN_PROBES build.
  */
 #ifndef MERLIN_HIP_H
 #define MERLIN_HIP_H

@@ -1668,6 +1668,7 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 45: return H3_NTGQ(256, 128, 4, 2, true);
         case 46: return H3_NTGQ(256, 128, 4, 2, false);
 #undef H3_NTGQ
+#ifdef MERLIN_PROBES  // ablations (round 5): results are wrong on purpose (no DMA / no MFMA in the k loop)
 #define H3_NTGA(BM, BN, WM, WN, ABL) \
     ((a_rows || head_part) ? hipErrorInvalidValue                                                  \
             : ntg_launch<BM, BN, WM, WN, true, true, false, ABL>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s))
@@ -1675,13 +1676,16 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
         case 48: return H3_NTGA(128, 256, 2, 4, 2);
         case 49: return H3_NTGA(128, 256, 2, 4, 3);
 #undef H3_NTGA
+#endif
 #define H3_NTGO(BM, BN, WM, WN, AP, ABL) \
     ((a_rows || head_part) ? hipErrorInvalidValue                                                  \
             : ntg_launch<BM, BN, WM, WN, true, AP, false, ABL, true>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, s))
         case 50: return H3_NTGO(128, 256, 2, 4, true, 0);
         case 51: return H3_NTGO(256, 128, 4, 2, true, 0);
         case 52: return H3_NTGO(128, 192, 4, 2, true, 0);
+#ifdef MERLIN_PROBES
         case 53: return H3_NTGO(128, 256, 2, 4, true, 1);  // ablation: no DMA in the main loop
+#endif
         case 54: return H3_NTGO(128, 256, 2, 4, false, 0);  // fp32 A split at the fragment reads
 #undef H3_NTGO
         default: return hipErrorInvalidValue;

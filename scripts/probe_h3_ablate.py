@@ -1,5 +1,6 @@
 """Probe (round 5): where the plane-operand NT GEMM's time goes -- k_h3_ntg AP (cfg 42, 128 x 256) against its
 ablations: 47 no DMA in the main loop, 48 no MFMAs, 49 the DMA stream alone.  HIP-event time per launch.
+(The ablation configs are compiled only with -DMERLIN_PROBES: make -C ppo-2dgrid_amd EXTRA=-DMERLIN_PROBES.)
     python scripts/probe_h3_ablate.py [U] [reps] [cfgs...]"""
 import os
 import sys
