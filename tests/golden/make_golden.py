@@ -428,6 +428,10 @@ def gen_update_grad():
         adv_norm=adv_norm.numpy().astype(np.float32), returns=ret_ref.numpy().astype(np.float32),
     )
     for i, (g, d) in enumerate(zip(rec["grads"], rec["delta"])):
+        # the starting weights too: torch's orthogonal_ init (QR through the host's LAPACK) rounds differently on
+        # another CPU, and at the initial weights the actor tower's gradient is a near-cancelling sum that turns a
+        # 1e-7 weight difference into ~6e-4 of gradient -- the test loads these, not a re-run of the init
+        out[f"p0_{i}"] = rec["p0"][i].numpy().astype(np.float32)
         out[f"grad{i}"] = g.numpy().astype(np.float32)  # the clipped gradient Adam consumed
         out[f"step{i}"] = (d.double() / 3e-4).numpy().astype(np.float16)  # the first Adam step in units of lr
     np.savez_compressed(os.path.join(HERE, "update_grad_ref.npz"), **out)

@@ -11,7 +11,9 @@ k_h3_pq / k_h3_tq), the fused loss and the two-launch clip + Adam -- and the gra
 optimizer (p.grad at the first ClipAdam.step) is compared tensor by tensor with the reference's and with the same
 gradient in float64 (the reference's network and loss restated below on the CPU in double).
 
-One input differs by design: the reference normalises the advantages with fp32 torch moments (src/ppo.py:125), the
+The starting weights are the reference's, loaded from the fixture (torch's orthogonal_ init goes through the host's
+LAPACK, whose rounding differs between CPUs; at these weights the actor tower's gradient is a near-cancelling sum
+that turns a 1e-7 weight difference into ~6e-4 of gradient).  One input differs by design: the reference normalises the advantages with fp32 torch moments (src/ppo.py:125), the
 benched path with f64 moments (k_gae_thread + k_adv_normalize; the GAE itself is bit-exact).  At the initial weights
 the actor's gradient is a near-cancelling sum (|g| ~ 1e-5 per weight): a ~1e-8 shift of the normalised advantages
 moves it by ~6e-4 relative.  So the test runs the update twice:
@@ -85,7 +87,10 @@ def _run(golden, device, ref_adv=False):
     assert agent.conv1_from_codes and agent.dedup and agent.windows and agent.fast_step
     assert agent.ac.fc1_impl == "h3" and agent._clip_adam is not None
     for (k, t), (s, a, first) in zip(agent.ac.state_dict().items(), g["sums0"]):
-        assert abs(t.double().sum().item() - s) <= 1e-5 * max(1.0, abs(a)), k
+        assert abs(t.double().sum().item() - s) <= 1e-5 * max(1.0, abs(a)), k  # the same init (up to LAPACK rounding)
+    with torch.no_grad():  # the reference's exact starting weights (its orthogonal_ init ran on this container's CPU)
+        for i, (_, p) in enumerate(agent.ac.named_parameters()):
+            p.copy_(torch.from_numpy(g[f"p0_{i}"]).to(p.device))
     buf = agent.buf
     buf.codes[:B, 0] = torch.from_numpy(pack(g["codes"])).to(device)
     for dst, key, dt in ((buf.actions, "actions", torch.int64), (buf.logprobs, "logp", torch.float32),
