@@ -72,11 +72,6 @@ class FOMAML:
         self._env.seed_each(self._task_seeds)
         return self._env
 
-    def _refill_stream(self):
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device)
-        return self._side
-
     # ------------------------------------------------------------ rollouts
     def _rollout_state(self, key, G, steps, params):
         st = self._rollouts.get(key)
@@ -103,32 +98,20 @@ class FOMAML:
     def _rollout_body(self, env, st):
         steps = st["steps"]
         pk = st["pack"]
-        if self.fused_act:
-            # the look-ahead map slots refilled after every step on a side stream (beside the next acting step),
-            # joined before the next env step, as PPO's rollout does: no reset can meet an empty slot, so the env
-            # step's fallback pass is left out (one launch fewer per step)
-            main, side = torch.cuda.current_stream(self.device), self._refill_stream()
-            env.set_refill_interval(0)
-            env.set_step_fallback(False)
-        else:  # the library's own refills (every 16 steps) and fallback pass
-            env.set_refill_interval(16)
-            env.set_step_fallback(True)
+        # the library's own look-ahead refills (every 16 steps) and fallback pass.  (Refilling on a side stream after
+        # every step without the fallback, as PPO's rollout does, made these 32-env rollouts slower: 13.5 / 15.4
+        # against 9.7 / 11.8 ms for the support / query rollout, profiles/r06f_fomaml_phases.log -- at 32 envs the
+        # cross-stream joins cost more than the fallback launch)
         env.reset(out=st["codes"][0])  # = env.reset(seed=task_seed) for every task
         if self.fused_act:
             self._act_epoch.add_(1)  # a fresh draw on every replay
             A = int(pk["ba_r"].shape[1])
             for t in range(steps):
                 part = gp.act_parts(pk, st["codes"][t], part=st["part"], a3_ws=st["a3ws"])
-                if t > 0:
-                    main.wait_stream(side)
                 env.act_step_into(part, st["zb"][:A], st["zb"][:1], (st["act"][t], st["logp"][t], st["val"][t]),
                                   st["codes"][t + 1], st["rew"][t], None, None, st["done"][t], st["epr"][t],
                                   st["epl"][t], seed=self._act_seed, epoch=self._act_epoch, step=t)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    env.refill()
             part = gp.act_parts(pk, st["codes"][steps], part=st["part"], a3_ws=st["a3ws"])
-            main.wait_stream(side)
             st["last"].copy_(part[1, :, :, 0].sum(0))
             return
         for t in range(steps):
