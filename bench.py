@@ -121,10 +121,17 @@ def fomaml_bench(args):
                                              f"k_steps={args.k_steps}"}}), flush=True)
 
 
-def fomaml_tier(device, difficulty, tasks=32, k=256, warmup=1, steps=1):
+def wgrad_side() -> bool:
+    from merlin import fast_step as FS
+
+    return bool(FS.WGRAD_SIDE)
+
+
+def fomaml_tier(device, difficulty, tasks=32, k=256, warmup=3, steps=4):
     """BASELINE cfg 5 inside the default run: meta-iterations of 32 tasks x (256 support + 256
     query) env steps with the inner SGD step and the meta Adam step (merlin.fomaml, batched over
-    tasks); env-steps/s of the meta step."""
+    tasks); env-steps/s of the meta step, after `warmup` meta steps (the first two run eagerly, the third records
+    the inner / outer graphs: merlin.fomaml CAPTURE_AFTER)."""
     import torch
 
     from merlin import ScenarioCreator
@@ -518,6 +525,16 @@ def hard22_tier(device, N, T, epochs, minibatches, warmup=2, iters=3):
            "distinct_frames_per_sample": round(agent.last_distinct_frac, 4),
            "windows_per_update": agent.last_num_windows,
            "rollout_acting": "all-windows conv3 table" if agent.rollout_all_windows else "per-frame conv2 lookups"}
+    # the data-independent floor of this tier too (round-5 verdict): the same loop with neither the distinct-frame
+    # grouping nor the windows, on the agent's current state
+    saved = (agent.dedup, agent.windows)
+    try:
+        agent.dedup, agent.windows = False, False
+        frate, ftimes = _median_iter_rate(agent, 1, 2)
+        out["full_loop_floor"] = {"no_dedup_no_windows": round(frate, 1),
+                                  "no_dedup_no_windows_iter_ms": [round(t * 1e3, 1) for t in ftimes]}
+    finally:
+        agent.dedup, agent.windows = saved
     env.close()
     del agent
     torch.cuda.empty_cache()
@@ -692,7 +709,8 @@ def main():
         "roofline": dict(roofline_of(dominant, kernels[dominant], fc1),
                          **({"note": "in the loop the weight gradient runs on a side stream beside conv3's "
                                      "backward segmented sums, so its event time includes that sharing; "
-                                     "alone: roofline_x6_standalone"} if dominant == "gemm_wgrad" and x6 else {})),
+                                     "alone: roofline_x6_standalone"}
+                            if dominant == "gemm_wgrad" and x6 and wgrad_side() else {})),
         # dominant hand-written kernel
         "roofline_handwritten": dict(roofline_of(handwritten, kernels[handwritten]),
                                      **gather_note(handwritten, kernels[handwritten])),

@@ -34,6 +34,11 @@ from .envs import MerlinVecEnv
 
 # the rollouts' acting step through merlin_group_act + merlin_env_act_step (False: grouped_policy.act_packed)
 FUSED_ACT = True
+# after CAPTURE_AFTER eager meta steps of a (tasks, k_support, k_query) shape, its inner step (support loss, every
+# task's gradient, per-task clip, SGD) and outer step (query loss, meta gradient, clip, Adam) are recorded as two HIP
+# graphs and replayed: ~330 small launches per meta step that the host queued while the GPU idled (round 6)
+CAPTURE_STEPS = True
+CAPTURE_AFTER = 2
 
 
 class FOMAML:
@@ -46,7 +51,10 @@ class FOMAML:
         self.lr_inner = lr_inner
         self.env_kwargs = self.sc._env_kwargs(difficulty)
         self.meta_policy = CNNActorCritic((56, 56, 3), 3).to(self.device)
-        self.meta_optimizer = optim.Adam(self.meta_policy.parameters(), lr=lr_outer)
+        # capturable: the step count lives on the device, so the Adam step can be part of a captured graph
+        self.meta_optimizer = optim.Adam(self.meta_policy.parameters(), lr=lr_outer, capturable=True)
+        self.capture_steps = CAPTURE_STEPS
+        self._steps = {}  # per (tasks, k_support, k_query): eager step count, then the captured inner / outer graphs
         self.gamma, self.lam = 0.995, 0.95
         self.vf_coef, self.ent_coef, self.clip_eps = 0.5, 0.05, 0.2
         self._env = None
@@ -204,28 +212,69 @@ class FOMAML:
         return {k: g * coef.view(G, *([1] * (g.dim() - 1))) for k, g in grads.items()}, norm
 
     # ------------------------------------------------------------ meta step
-    def meta_train_step(self, task_seeds, k_support=50, k_query=50):
-        G = len(task_seeds)
-        env = self._task_env(task_seeds)
-        self.meta_optimizer.zero_grad()
-        names = [n for n, _ in self.meta_policy.named_parameters()]
-        # inner loop: all fast policies start as the meta policy -> batched support rollout
-        # the support rollout's episodes are not reported (:171-176): no host read-back between it and the inner step
-        support = self.collect_trajectory(env, None, k_support, key="support", host_stats=False)
+    def _inner(self, support, G, names):
+        """Inner loop (src/fomaml.py:164-185): every fast policy starts as the meta policy; support loss, each task's
+        gradient, clip_grad_norm_(0.5) per task, one SGD(lr_inner) step -> the adapted weights [G, *shape]."""
         fast = bp.stack_params(self.meta_policy, G)
         loss_s, _ = self.compute_loss(support, fast)
         grads = dict(zip(names, torch.autograd.grad(loss_s, [fast[n] for n in names])))
         grads, _ = self._clip_per_task(grads, 0.5)
         with torch.no_grad():
-            adapted = {n: (fast[n] - self.lr_inner * grads[n]).detach().requires_grad_(True) for n in names}
-        # outer loop: query rollouts with each task's adapted policy
-        query = self.collect_trajectory(env, adapted, k_query, key="query", host_stats=False)
-        loss_q, qstats = self.compute_loss(query, adapted)
-        qgrads = torch.autograd.grad(loss_q, [adapted[n] for n in names])
+            return {n: (fast[n] - self.lr_inner * grads[n]).detach() for n in names}
+
+    def _outer(self, query, adapted, G, names):
+        """Outer loop (:187-212): query loss with the adapted weights, the sum of the tasks' gradients / n_tasks as
+        the meta gradient, clip_grad_norm_(0.5), Adam.  Returns the query statistics per task."""
+        ad = {n: adapted[n].detach().requires_grad_(True) for n in names}
+        loss_q, qstats = self.compute_loss(query, ad)
+        qgrads = torch.autograd.grad(loss_q, [ad[n] for n in names])
         for (n, p), g in zip(self.meta_policy.named_parameters(), qgrads):
             p.grad = g.sum(dim=0) / G  # sum of the tasks' fast grads / n_tasks (:198-209)
         torch.nn.utils.clip_grad_norm_(self.meta_policy.parameters(), max_norm=0.5)
         self.meta_optimizer.step()
+        return qstats
+
+    def _phase(self, st, name, fn, *args):
+        """fn(*args) eagerly, or its captured graph (recorded on the call after CAPTURE_AFTER eager meta steps)."""
+        g = st.get(name)
+        if g is not None:
+            g.replay()
+            return st[name + "_out"]
+        if not (self.capture_steps and st["eager"] >= CAPTURE_AFTER):
+            return fn(*args)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with nat.capture_guard(), torch.cuda.graph(g):
+                out = fn(*args)
+        except Exception:  # an op this stack cannot capture: keep launching eagerly
+            self.capture_steps = False
+            torch.cuda.synchronize(self.device)
+            return fn(*args)
+        st[name], st[name + "_out"] = g, out
+        g.replay()  # the capture recorded the launches without running them
+        return out
+
+    def meta_train_step(self, task_seeds, k_support=50, k_query=50):
+        G = len(task_seeds)
+        env = self._task_env(task_seeds)
+        names = [n for n, _ in self.meta_policy.named_parameters()]
+        st = self._steps.setdefault((G, k_support, k_query), {"eager": 0})
+        if "outer" not in st:
+            self.meta_optimizer.zero_grad()
+        # inner loop: all fast policies start as the meta policy -> batched support rollout
+        # the support rollout's episodes are not reported (:171-176): no host read-back between it and the inner step
+        support = self.collect_trajectory(env, None, k_support, key="support", host_stats=False)
+        adapted = self._phase(st, "inner", self._inner, support, G, names)
+        # outer loop: query rollouts with each task's adapted policy
+        query = self.collect_trajectory(env, adapted, k_query, key="query", host_stats=False)
+        qstats = self._phase(st, "outer", self._outer, query, adapted, G, names)
+        if "outer" in st:  # the captured meta gradient is what .grad shows
+            for p, g in zip(self.meta_policy.parameters(), st.setdefault("grads", [p.grad for p in
+                                                                                  self.meta_policy.parameters()])):
+                p.grad = g
+        else:
+            st["eager"] += 1
         # the host reads of the meta step, once everything is queued (env error flags: both rollouts')
         query.update(self._episode_stats(env, self._rollouts["query"]))
         avg_loss = float(qstats["loss"].mean().item())
