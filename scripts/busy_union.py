@@ -32,6 +32,23 @@ for a, b in runs[-6:]:
 for w, bz, n in out:
     print(f"update: span {w:8.1f} ms, GPU busy (union) {bz:8.1f} ms, idle {w - bz:7.1f} ms ({(w - bz) / w * 100:.1f} %), {n} dispatches")
 
+# where the last update's idle time is: its largest gaps between the union's busy intervals, with the kernels either
+# side (a host read drains the queue: the gap after it is the host's planning / queueing time)
+if runs:
+    a, b = runs[-1]
+    seg = rows[a:b]
+    gaps, cur_e, last_k = [], None, None
+    for s, e, k in seg:
+        if cur_e is not None and s > cur_e:
+            gaps.append((s - cur_e, last_k, k, cur_e - seg[0][0]))
+        if cur_e is None or e > cur_e:
+            cur_e, last_k = e, k
+    gaps.sort(reverse=True)
+    tot = sum(g for g, *_ in gaps)
+    print(f"last update: {len(gaps)} gaps, {tot / 1e6:.2f} ms; the largest:")
+    for g, k0, k1, at in gaps[:12]:
+        print(f"    {g / 1e3:8.1f} us at +{at / 1e6:7.2f} ms  after {k0[:48]:48s} before {k1[:48]}")
+
 
 # rollout phases: from the first k_env_step of a run to the last one, plus the per-kernel means and the mean step
 # period (k_env_step start to start), so the dispatch gaps of the captured rollout graph show
