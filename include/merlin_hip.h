@@ -336,26 +336,6 @@ int merlin_tower_conv2_lut_bwd_grouped(const uint32_t *codes_dev, int64_t group_
  *               (a list split by source block into several calls sums in call order). */
 int merlin_tower_window_lut(const int32_t *rows_dev, int64_t n_windows, const float *tables_dev,
                             int32_t towers, float *Z2w_dev, void *stream);
-/* patch_compact (round 6): one minibatch's compact list of an update-wide destination-sorted plan (idx / key int32
- * [nnz], merlin/windows.py WindowPlan.patch_plan): its live entries (slot[idx / sub] >= 0) in plan order, n_live of
- * them (the caller knows the count: the minibatch's frames x sub), as ckey[ci] (the destination), crow[ci] = slot *
- * sub + idx % sub (the source row, < src_rows: pos and mask_rows hold src_rows entries), pos[crow[ci]] = ci,
- * cmrow[ci] = mask_rows[crow[ci]] (or crow[ci] with mask_rows NULL), and -- with fix / head_fix non-NULL -- the compact list's item fix-up rows for items of item_len entries
- * (fix int32 [nitems][4], head_fix int32 [nitems]: merlin_segment_sum_fused's in-launch fix-ups).  workspace: int32
- * [merlin_patch_compact_workspace(nnz)].  Three launches; a destination's entries keep their plan order, so its sum
- * adds the same rows in the same order as over the whole plan.
- * h3_gemm_nt_planes_rowmap: merlin_h3_gemm_nt_planes (cfg 62 tiles, K 512) with the output written by 64-column
- * chunk to C[t][row_map[m * N/64 + n/64]][n % 64] -- conv3's input gradient in the compact list's order, which the R
- * pass then reads front to back (merlin/fast_step.py COMPACT_R). */
-int64_t merlin_patch_compact_workspace(int64_t nnz);
-int merlin_patch_compact(const int32_t *idx_dev, const int32_t *key_dev, int64_t nnz, const int32_t *slot_dev,
-                         int32_t sub, const int32_t *mask_rows_dev, int64_t n_live, int64_t src_rows, int64_t item_len,
-                         int32_t *workspace_dev, int32_t *pos_dev, int32_t *ckey_dev, int32_t *crow_dev,
-                         int32_t *cmrow_dev, int32_t *fix_dev, int32_t *head_fix_dev, void *stream);
-int merlin_h3_gemm_nt_planes_rowmap(const void *A_planes_dev, const uint32_t *amax_a_dev, const void *B_dev,
-                                    const uint32_t *amax_b_dev, int64_t M, int32_t N, int32_t K, int32_t towers,
-                                    int64_t a_stride, int64_t b_stride, float *C_dev, int64_t c_stride,
-                                    const int32_t *row_map_dev, void *stream);
 /* The live-patch maps of every minibatch of an update (merlin/windows.py WindowPlan._bulk_minibatches): group g
  * (group_keys[g] = minibatch m * n_frames + frame; group_offsets[m] = first group of minibatch m), position p3 ->
  * patch k = kid[frame * 9 + p3]: kmap[m * n_patches + k] = k (preset to -1 by the caller), rmap[...] = one row

@@ -723,34 +723,6 @@ int merlin_tower_window_lut(const int32_t *rows, int64_t nw, const float *tables
     return MERLIN_OK;
 }
 
-int64_t merlin_patch_compact_workspace(int64_t nnz) { return nnz > 0 ? merlin::patch_compact_workspace(nnz) : 0; }
-
-int merlin_patch_compact(const int32_t *idx, const int32_t *key, int64_t nnz, const int32_t *slot, int32_t sub,
-                         const int32_t *mask_rows, int64_t n_live, int64_t src_rows, int64_t item_len,
-                         int32_t *workspace, int32_t *pos,
-                         int32_t *ckey, int32_t *crow, int32_t *cmrow, int32_t *fix, int32_t *head_fix, void *stream) {
-    if (nnz < 0 || n_live < 0 || src_rows < 0 || sub < 1 || item_len < 1) return fail(MERLIN_E_INVALID, "bad shape");
-    if (nnz > 0 && n_live > 0 && (!idx || !key || !slot || !workspace || !pos || !ckey || !crow || !cmrow))
-        return fail(MERLIN_E_INVALID, "null argument");
-    if ((fix == nullptr) != (head_fix == nullptr)) return fail(MERLIN_E_INVALID, "fix and head_fix go together");
-    if (nnz > INT32_MAX || n_live > INT32_MAX || src_rows > INT32_MAX) return fail(MERLIN_E_UNSUPPORTED, "more than 2^31 entries");
-    HIP_TRY(merlin::launch_patch_compact(idx, key, nnz, slot, sub, mask_rows, n_live, src_rows, item_len, workspace, pos, ckey,
-                                         crow, cmrow, fix, head_fix, (hipStream_t)stream));
-    return MERLIN_OK;
-}
-
-int merlin_h3_gemm_nt_planes_rowmap(const void *A_planes, const uint32_t *amax_a, const void *B,
-                                    const uint32_t *amax_b, int64_t M, int32_t N, int32_t K, int32_t towers,
-                                    int64_t a_stride, int64_t b_stride, float *C, int64_t c_stride,
-                                    const int32_t *row_map, void *stream) {
-    if (M > 0 && (!A_planes || !amax_a || !B || !amax_b || !C || !row_map)) return fail(MERLIN_E_INVALID, "null argument");
-    if (towers < 1 || towers > 2) return fail(MERLIN_E_INVALID, "towers must be 1 or 2");
-    if (N % 192 || N % 64 || K != 512) return fail(MERLIN_E_UNSUPPORTED, "row-map input gradient: N % 192, K 512");
-    HIP_TRY(merlin::launch_h3p_gemm_nt_rowmap(A_planes, amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride, C,
-                                              c_stride, row_map, (hipStream_t)stream));
-    return MERLIN_OK;
-}
-
 int merlin_minibatch_patch_maps(const int32_t *kid, const int64_t *group_keys, int64_t n_groups, int64_t n_frames,
                                 const int64_t *group_offsets, int32_t n_patches, int32_t *kmap, int32_t *rmap,
                                 int32_t *rep_row, void *stream) {

@@ -71,8 +71,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
                                                           const uint32_t *__restrict__ amaxA,
                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N, int K,
                                                           int64_t sA, int64_t sB, const float *__restrict__ bias,
-                                                          float *__restrict__ C, int64_t sC, int tiles_n,
-                                                          const int32_t *__restrict__ rmap) {
+                                                          float *__restrict__ C, int64_t sC, int tiles_n) {
     constexpr int NT = 64 * WGM * WGN;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -223,10 +222,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
                 const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
                 if (row < M) {
                     const float v = (hi[i][j][r] + lo[i][j][r] * P_LO_INV) * inv * invB;
-                    if constexpr (EPI == 2)  // 64-column chunk (row, col / 64) to its row of the map (N % 64 == 0)
-                        Ct[(int64_t)rmap[row * (N >> 6) + (col >> 6)] * 64 + (col & 63)] = v;
-                    else
-                        Ct[row * N + col] = EPI == 1 ? p_relu(v + bv) : v;
+                    Ct[row * N + col] = EPI == 1 ? p_relu(v + bv) : v;
                 }
             }
         }
@@ -235,8 +231,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
 
 template <int BM, int BN, int WGM, int WGN, int NS = 3>
 hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
-                     int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s,
-                     const int32_t *rmap = nullptr) {
+                     int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
     if (N % BN || K % 32 || K < 64) return hipErrorInvalidValue;
     const int64_t tiles_m = (M + BM - 1) / BM;
     const int tiles_n = N / BN;
@@ -246,15 +241,12 @@ hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const 
     const auto *b = static_cast<const p_u32x4 *>(B);
 #define PQ_K(NK)                                                                                                   \
     do {                                                                                                           \
-        if (rmap)                                                                                                  \
-            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 2, NK, NS>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
-                               sA / 4, sB / 4, nullptr, C, sC, tiles_n, rmap);                                     \
-        else if (bias)                                                                                             \
+        if (bias)                                                                                                  \
             hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 1, NK, NS>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
-                               sA / 4, sB / 4, bias, C, sC, tiles_n, nullptr);                                     \
+                               sA / 4, sB / 4, bias, C, sC, tiles_n);                                              \
         else                                                                                                       \
             hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 0, NK, NS>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
-                               sA / 4, sB / 4, nullptr, C, sC, tiles_n, nullptr);                                  \
+                               sA / 4, sB / 4, nullptr, C, sC, tiles_n);                                           \
     } while (0)
     switch (K) {  // the k loop is unrolled: one instantiation per depth (fc1's forward K = 576, input gradient 512)
         case 576: PQ_K(18); break;
@@ -799,16 +791,6 @@ hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *
     }
 }
 
-
-// the input gradient (cfg 62 tiles) with its output rows scattered by 64-column chunk: C[t][rmap[m * N/64 + n/64]][n %
-// 64] (conv3's input gradient written in the order of the minibatch's compact patch list, round 6)
-hipError_t launch_h3p_gemm_nt_rowmap(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB,
-                                     int64_t M, int N, int K, int T, int64_t a_stride, int64_t b_stride, float *C,
-                                     int64_t c_stride, const int32_t *rmap, hipStream_t s) {
-    if (M <= 0) return hipSuccess;
-    if (!rmap || N % 64 || K != 512 || a_stride % 4 || b_stride % 4) return hipErrorInvalidValue;
-    return pq_launch<128, 192, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, nullptr, C, c_stride, s, rmap);
-}
 
 // the weight gradient over plane operands with B's rows gathered (cfg 20: 128 x 192 tiles, 4 x 2 waves); slab as
 // merlin_h3_gemm_tn's (S slabs of [T][M][N], summed in order by the caller's fold); strides in values

@@ -235,15 +235,6 @@ hipError_t launch_conv2_lut_fwd(const uint32_t *codes, const int64_t *index, int
 hipError_t launch_conv2_lut_bwd(const uint32_t *codes, int64_t n, const float *dZ2c, const uint32_t *absmax,
                                 int towers, float *dT, void *slabs, hipStream_t s, int64_t gstride = 0);
 
-hipError_t launch_patch_compact(const int32_t *idx, const int32_t *key, int64_t nnz, const int32_t *slot, int sub,
-                                const int32_t *mrow, int64_t n_live, int64_t src_rows, int64_t item_len,
-                                int32_t *bcount, int32_t *pos,
-                                int32_t *ckey, int32_t *crow, int32_t *cmrow, int32_t *fix, int32_t *hfix,
-                                hipStream_t s);
-int64_t patch_compact_workspace(int64_t nnz);
-hipError_t launch_h3p_gemm_nt_rowmap(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB,
-                                     int64_t M, int N, int K, int T, int64_t a_stride, int64_t b_stride, float *C,
-                                     int64_t c_stride, const int32_t *rmap, hipStream_t s);
 hipError_t launch_patch_maps(const int32_t *kid, const int64_t *gkey, int64_t G, int64_t F, const int64_t *goff, int K,
                              int32_t *kmap, int32_t *rmap, int32_t *rep_row, hipStream_t s);
 hipError_t launch_window_lut(const int32_t *rows, int64_t nw, const float *tab, int T, float *Z2w, hipStream_t s,

@@ -669,145 +669,6 @@ __global__ __launch_bounds__(256) void k_patch_maps(const int32_t *__restrict__ 
 
 }  // namespace
 
-namespace {
-// One minibatch's compact patch list (round 6): the live entries (slot[idx / sub] >= 0) of an update-wide,
-// destination-sorted plan (merlin/windows.py WindowPlan.patch_plan), kept in plan order -- so every destination sums
-// the same rows in the same order as over the whole plan -- as (crow = slot * sub + idx % sub, ckey), the compact
-// index of every source row (pos[crow[ci]] = ci: conv3's input gradient can be written in this order, and the R pass
-// then reads it front to back), each compact entry's mask row (cmrow[ci] = mrow[crow[ci]], or crow[ci]) and the compact
-// list's item fix-up rows (merlin/windows.py SegmentPlan's, for merlin_segment_sum_fused).  Round 5's R pass walked the
-// whole update-wide plan for every minibatch, ~86 % of its entries skipped through the slot map, and gathered the
-// live rows in random order.
-constexpr int PC_T = 256, PC_PER = 16, PC_BLK = PC_T * PC_PER;  // plan entries per block
-
-__device__ __forceinline__ int pc_block_sum(int v, int *ws) {  // every thread gets the block's sum of v
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
-    __syncthreads();
-    int s = 0;
-#pragma unroll
-    for (int w = 0; w < PC_T / 64; w++) s += ws[w];
-    return s;
-}
-
-__global__ __launch_bounds__(PC_T) void k_pc_count(const int32_t *__restrict__ idx, int64_t nnz,
-                                                   const int32_t *__restrict__ slot, int sub,
-                                                   int32_t *__restrict__ bcount) {
-    __shared__ int ws[PC_T / 64];
-    const int64_t base = (int64_t)blockIdx.x * PC_BLK;
-    int c = 0;
-#pragma unroll 4
-    for (int j = 0; j < PC_PER; j++) {
-        const int64_t e = base + j * PC_T + threadIdx.x;
-        if (e < nnz) c += slot[idx[e] / sub] >= 0 ? 1 : 0;
-    }
-    c = pc_block_sum(c, ws);
-    if (threadIdx.x == 0) bcount[blockIdx.x] = c;
-}
-
-__global__ __launch_bounds__(PC_T) void k_pc_scatter(const int32_t *__restrict__ idx, const int32_t *__restrict__ key,
-                                                     int64_t nnz, const int32_t *__restrict__ slot, int sub,
-                                                     const int32_t *__restrict__ bcount,
-                                                     const int32_t *__restrict__ mrow, int32_t *__restrict__ pos,
-                                                     int32_t *__restrict__ ckey, int32_t *__restrict__ crow,
-                                                     int32_t *__restrict__ cmrow, int64_t cap, int64_t src_rows) {
-    __shared__ int ws[PC_T / 64];
-    int c = 0;
-    for (int b = threadIdx.x; b < (int)blockIdx.x; b += PC_T) c += bcount[b];
-    int run = pc_block_sum(c, ws);  // this block's first compact index
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    const int64_t base = (int64_t)blockIdx.x * PC_BLK;
-    for (int j = 0; j < PC_PER; j++) {
-        const int64_t e = base + j * PC_T + threadIdx.x;
-        int v = 0, sl = -1;
-        if (e < nnz) {
-            v = idx[e];
-            sl = slot[v / sub];
-        }
-        const bool live = sl >= 0;
-        const unsigned long long m = __ballot(live);
-        __syncthreads();  // every wave is done reading ws of the previous chunk
-        if (lane == 0) ws[w] = __popcll(m);
-        __syncthreads();
-        int woff = 0, tot = 0;
-#pragma unroll
-        for (int q = 0; q < PC_T / 64; q++) {
-            woff += q < w ? ws[q] : 0;
-            tot += ws[q];
-        }
-        if (live) {
-            const int ci = run + woff + __popcll(m & below);
-            const int row = sl * sub + (v - (v / sub) * sub);
-            // more live entries than the caller counted, or a slot past its rows: a bad plan, never an overrun
-            if (ci < cap && row < src_rows) {
-                pos[row] = ci;
-                ckey[ci] = key[e];
-                crow[ci] = row;
-                cmrow[ci] = mrow ? mrow[row] : row;
-            }
-        }
-        run += tot;
-    }
-}
-
-// the compact list's fix-up rows, one thread per item of L entries: (dst, j, the item its run ends in, the carry slot
-// of item j) for the destination that starts in item j and continues past it, else dst = -1; head_fix[j] = the item
-// at which item j's first destination started, when that is an earlier one, else -1 (SegmentPlan's arrays)
-__device__ __forceinline__ int64_t pc_lower(const int32_t *a, int64_t n, int32_t v) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a[mid] < v) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-__device__ __forceinline__ int64_t pc_upper(const int32_t *a, int64_t n, int32_t v) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a[mid] <= v) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-__global__ __launch_bounds__(256) void k_pc_fix(const int32_t *__restrict__ ckey, int64_t n, int64_t L, int64_t nitems,
-                                                int4 *__restrict__ fix, int32_t *__restrict__ hfix) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= nitems) return;
-    const int64_t p = std::min<int64_t>((j + 1) * L, n) - 1;
-    const int32_t kp = ckey[p];
-    const int64_t s = pc_lower(ckey, n, kp), e = pc_upper(ckey, n, kp);
-    const bool live = e > (j + 1) * L && s >= j * L;
-    fix[j] = make_int4(live ? kp : -1, (int)j, (int)((e - 1) / L), s != j * L ? 1 : 0);
-    const int64_t sf = pc_lower(ckey, n, ckey[j * L]);
-    hfix[j] = sf < j * L ? (int)(sf / L) : -1;
-}
-}  // namespace
-
-hipError_t launch_patch_compact(const int32_t *idx, const int32_t *key, int64_t nnz, const int32_t *slot, int sub,
-                                const int32_t *mrow, int64_t n_live, int64_t src_rows, int64_t item_len,
-                                int32_t *bcount, int32_t *pos,
-                                int32_t *ckey, int32_t *crow, int32_t *cmrow, int32_t *fix, int32_t *hfix,
-                                hipStream_t s) {
-    if (nnz <= 0 || n_live <= 0) return hipSuccess;
-    const int nb = (int)((nnz + PC_BLK - 1) / PC_BLK);
-    hipLaunchKernelGGL(k_pc_count, dim3(nb), dim3(PC_T), 0, s, idx, nnz, slot, sub, bcount);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pc_scatter, dim3(nb), dim3(PC_T), 0, s, idx, key, nnz, slot, sub, bcount, mrow, pos, ckey,
-                       crow, cmrow, n_live, src_rows);
-    e = hipGetLastError();
-    if (e != hipSuccess || !fix) return e;
-    const int64_t nitems = (n_live + item_len - 1) / item_len;
-    hipLaunchKernelGGL(k_pc_fix, dim3((unsigned)((nitems + 255) / 256)), dim3(256), 0, s, ckey, n_live, item_len, nitems,
-                       reinterpret_cast<int4 *>(fix), hfix);
-    return hipGetLastError();
-}
-int64_t patch_compact_workspace(int64_t nnz) { return (nnz + PC_BLK - 1) / PC_BLK; }
-
 hipError_t launch_patch_maps(const int32_t *kid, const int64_t *gkey, int64_t G, int64_t F, const int64_t *goff, int K,
                              int32_t *kmap, int32_t *rmap, int32_t *rep_row, hipStream_t s) {
     if (G <= 0) return hipSuccess;

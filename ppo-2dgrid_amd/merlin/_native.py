@@ -111,10 +111,6 @@ def lib():
     L.merlin_tower_window_conv3.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp]
     L.merlin_tower_window_lut_bias_relu.argtypes = [vp, i64, vp, i32, vp, vp, vp]
     L.merlin_minibatch_patch_maps.argtypes = [vp, vp, i64, i64, vp, i32, vp, vp, vp, vp]
-    L.merlin_patch_compact_workspace.argtypes = [i64]
-    L.merlin_patch_compact_workspace.restype = i64
-    L.merlin_patch_compact.argtypes = [vp, vp, i64, vp, i32, vp, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp]
-    L.merlin_h3_gemm_nt_planes_rowmap.argtypes = [vp, vp, vp, vp, i64, i32, i32, i32, i64, i64, vp, i64, vp, vp]
     L.merlin_tower_window_conv3_bits.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp]
     L.merlin_tower_window_conv3_reuse.argtypes = [vp, i64, vp, vp, i64, vp, i32, vp, vp, vp, vp, i32, vp]
     L.merlin_tower_all_windows.restype = i64
@@ -229,8 +225,7 @@ EXPORTED_SYMBOLS = (
     "merlin_ppo_loss_absmax", "merlin_tower_head_bwd_planes", "merlin_h3_gemm_nt_planes",
     "merlin_h3_gemm_tn_gather_planes_a", "merlin_h3_gemm_nt_heads_planes", "merlin_h3_gemm_tn_gather_planes",
     "merlin_tower_window_conv3_planes", "merlin_window_gemm_bwd_work", "merlin_window_gemm_bwd",
-    "merlin_window_gemm_fwd", "merlin_patch_compact_workspace", "merlin_patch_compact",
-    "merlin_h3_gemm_nt_planes_rowmap",
+    "merlin_window_gemm_fwd",
 )
 
 
@@ -767,74 +762,6 @@ def minibatch_patch_maps(kid, group_keys, num_frames, group_offsets, nmb, num_pa
     return kmap, rep_row
 
 
-class CompactPlan:
-    """One minibatch's compact patch list (patch_compact): the SegmentPlan attributes merlin_segment_sum reads (idx,
-    key, nnz, item_len, nitems, fix, head_fix, counters) over the minibatch's live entries only, plus pos (source row
-    -> compact index), crow (compact index -> source row) and cmrow (compact index -> mask row).  idx is crow
-    ("gather": the sum reads the rows where they are) or the identity ("scatter": the rows were written in compact
-    order, merlin_h3_gemm_nt_planes_rowmap)."""
-
-    def __init__(self, idx, key, n, L, fix, head_fix, counters, pos, crow, cmrow):
-        self.idx, self.key, self.nnz, self.item_len = idx, key, n, L
-        self.nitems = (n + L - 1) // L
-        self.fix, self.head_fix, self.counters = fix, head_fix, counters
-        self.pos, self.crow, self.cmrow = pos, crow, cmrow
-
-
-_IOTA = {}
-_ZEROS = {}
-
-
-def _iota(n: int, device) -> torch.Tensor:
-    """0 .. n-1 int32 (cached per device, grown in powers of two; read only)."""
-    d = torch.device(device)
-    t = _IOTA.get(d)
-    if t is None or t.numel() < n:
-        t = _IOTA[d] = torch.arange(max(n, 1 << (max(n, 1) - 1).bit_length()), dtype=torch.int32, device=d)
-    return t[:n]
-
-
-def _zero_counters(n: int, device) -> torch.Tensor:
-    """n int32 arrival counters, zero (merlin_segment_sum_fused leaves them zero after every launch: shared)."""
-    d = torch.device(device)
-    t = _ZEROS.get(d)
-    if t is None or t.numel() < n:
-        t = _ZEROS[d] = torch.zeros(max(n, 1 << (max(n, 1) - 1).bit_length()), dtype=torch.int32, device=d)
-    return t[:n]
-
-
-def patch_compact(plan, slot, sub: int, n_live: int, mask_rows=None, layout: str = "gather", item_len=None,
-                  src_rows: int | None = None):
-    """CompactPlan of the live entries (slot[idx // sub] >= 0) of `plan` (a destination-sorted SegmentPlan), n_live of
-    them -- the caller's count (a minibatch's frames x 9), not read back (merlin_patch_compact: three launches).  A
-    destination's entries keep their plan order: its sum adds the same rows in the same order as over the whole plan,
-    cut into items of the compact list's length (item_len: auto_item_len(n_live)).  src_rows: the source rows (pos and
-    mask_rows hold that many; default n_live, every row of the live frames in the plan, as a patch plan has them)."""
-    from .windows import auto_item_len
-
-    dev = plan.idx.device
-    n = int(n_live)
-    L = auto_item_len(n) if item_len is None else int(item_len)
-    assert slot.dtype == torch.int32 and slot.is_contiguous()
-    rows = n if src_rows is None else int(src_rows)
-    if mask_rows is not None:
-        assert mask_rows.dtype == torch.int32 and mask_rows.numel() == rows
-    nitems = (n + L - 1) // L
-    ws = torch.empty(max(int(lib().merlin_patch_compact_workspace(plan.nnz)), 1), dtype=torch.int32, device=dev)
-    pos = torch.empty(rows, dtype=torch.int32, device=dev)
-    ckey = torch.empty(n, dtype=torch.int32, device=dev)
-    crow = torch.empty(n, dtype=torch.int32, device=dev)
-    cmrow = torch.empty(n, dtype=torch.int32, device=dev)
-    fix = torch.empty((nitems, 4), dtype=torch.int32, device=dev)
-    hfix = torch.empty(nitems, dtype=torch.int32, device=dev)
-    with KernelTimer.span("k_patch_compact", plan.nnz * 16 + n * 20):
-        check(lib().merlin_patch_compact(ptr(plan.idx), ptr(plan.key), plan.nnz, ptr(slot), int(sub), ptr(mask_rows),
-                                         n, rows, L, ptr(ws), ptr(pos), ptr(ckey), ptr(crow), ptr(cmrow), ptr(fix),
-                                         ptr(hfix), stream_of(slot)), "merlin_patch_compact")
-    idx = crow if layout == "gather" else _iota(n, dev)
-    return CompactPlan(idx, ckey, n, L, fix, hfix, _zero_counters(nitems, dev), pos, crow, cmrow)
-
-
 def window_conv3_copy_masks(Y3, bits, rep_row):
     """The mask words of the rows that are not their patch's representative, copied from it (the second half of
     window_conv3(rep_row=..., copy=2), for a launch on another stream after the representatives' one)."""
@@ -1366,26 +1293,9 @@ def h3_gemm_nt(A: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: tor
 
 def h3_gemm_nt_planes(Ap: torch.Tensor, amaxA: torch.Tensor, B: torch.Tensor, amaxB: torch.Tensor,
                       bias: torch.Tensor | None = None, cfg: int = 62, out: torch.Tensor | None = None,
-                      name: str = "h3_gemm_nt", row_map: torch.Tensor | None = None) -> torch.Tensor:
+                      name: str = "h3_gemm_nt") -> torch.Tensor:
     """h3_gemm_nt with A already in plane form, Ap int16[T, M, 2K] scaled by amaxA's exponent (e.g. head_bwd's dz
-    planes): merlin_h3_gemm_nt_planes, both operands by LDS-DMA (cfg 60 / 61 / 62, K = 512 or 576).
-    row_map (int32 [M * N / 64], a permutation): out viewed as [T, M * N / 64, 64] gets 64-column chunk (m, c) at row
-    row_map[m * N / 64 + c] (merlin_h3_gemm_nt_planes_rowmap: cfg 62's tiles, K = 512, no bias)."""
-    if row_map is not None:
-        H3_SPANS.add(name)
-        T, M, K2 = (int(v) for v in Ap.shape)
-        K, N = K2 // 2, int(B.shape[1])
-        assert Ap.dtype == B.dtype == torch.int16 and B.shape == (T, N, 2 * K) and Ap.is_contiguous()
-        assert B.is_contiguous() and bias is None and cfg == 62 and N % 64 == 0
-        assert row_map.dtype == torch.int32 and row_map.numel() == M * (N // 64) and row_map.is_contiguous()
-        if out is None:
-            out = torch.empty((T, M, N), dtype=torch.float32, device=Ap.device)
-        assert out.numel() == T * M * N and out.is_contiguous()
-        with KernelTimer.span(name, 0, 2 * T * M * N * K):
-            check(lib().merlin_h3_gemm_nt_planes_rowmap(ptr(Ap), ptr(amaxA), ptr(B), ptr(amaxB), M, N, K, T, M * K,
-                                                        N * K, ptr(out), M * N, ptr(row_map), stream_of(Ap)),
-                  "merlin_h3_gemm_nt_planes_rowmap")
-        return out
+    planes): merlin_h3_gemm_nt_planes, both operands by LDS-DMA (cfg 60 / 61 / 62, K = 512 or 576)."""
     H3_SPANS.add(name)
     T, M, K2 = (int(v) for v in Ap.shape)
     K = K2 // 2

@@ -27,7 +27,6 @@ import weakref
 import torch
 
 from . import _native as nat
-from . import windows as _win
 from .actor_critic import _splitk_bmm_tn
 
 
@@ -239,10 +238,6 @@ MASK_ROWS = True
 DZ_PLANES = True
 # conv3's backward chain's fills made before the side-stream weight gradient starts (_conv3_backward_prefill)
 PREFILL = True
-# with merlin.windows.PATCH_COMPACT (the R pass over the minibatch's compact patch list) and dz's planes: the input-
-# gradient GEMM writes da3 in the compact list's order (merlin_h3_gemm_nt_planes_rowmap), so the R pass reads its rows
-# front to back instead of gathering them (False: gathered where the GEMM left them)
-COMPACT_SCATTER = True
 # with DZ_PLANES: conv3's representative rows leave k_window_conv3_reps as h3 planes too, scaled by a bound on max Y3
 # from Q's column maxima (merlin_tower_window_conv3_planes), so the forward GEMM stages a3 as copies
 # (merlin_h3_gemm_nt_heads_planes) and the weight gradient runs on both operands' planes
@@ -448,16 +443,8 @@ class WindowStep:
         # weight gradient: launched beside it, a small fill waits for a CU the GEMM's blocks free (~90 us each with
         # the LDS-DMA weight gradient, whose blocks hold a CU's LDS and VGPRs whole; profiles/r05u_* trace)
         pre = _conv3_backward_prefill(plan, int(Q.shape[1]), dz.device) if PREFILL else None
-        # the minibatch's compact patch list (merlin.windows.PATCH_COMPACT), before the input gradient that may write
-        # da3 in its order
-        scatter = dzp and COMPACT_SCATTER and nat.H3_NT_CFG["dgrad_planes"] == 62
-        cp = None
-        if _win.PATCH_COMPACT:
-            cp = nat.patch_compact(plan.patch_plan, mb.slot, 9, n * 9, mask_rows=arows,
-                                   layout="scatter" if scatter else "gather")
         if dzp:
-            da3 = nat.h3_gemm_nt_planes(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad_planes"], name="gemm_fc1_dgrad",
-                                        row_map=cp.pos if (cp is not None and scatter) else None)
+            da3 = nat.h3_gemm_nt_planes(dz, amz, P4t, amW, cfg=nat.H3_NT_CFG["dgrad_planes"], name="gemm_fc1_dgrad")
         elif h3:
             if pa3 is not None and not WGRAD_EARLY and not split_side:
                 pdz = torch.empty((2, n, 1024), dtype=torch.int16, device=dz.device)
@@ -477,7 +464,7 @@ class WindowStep:
         if masks_ready is not None:
             main.wait_event(masks_ready)
         dQ = _conv3_backward_bulk(plan, mb, bits, da3.view(2, n * 9, 64), int(Q.shape[1]),
-                                  mask_rows=arows if MASK_ROWS else None, pre=pre, cp=cp, scattered=scatter)
+                                  mask_rows=arows if MASK_ROWS else None, pre=pre)
         if wh3 or not WINDOW_BWD_HIP:  # (else summed by merlin_window_gemm_bwd below)
             nat.colsum(dQ.view(2, -1, 9, 64)[:, :, 0], out=g[3])  # db3: every (u, p3) has one window at tap 0
         dQ = dQ.view(2, -1, 576)
@@ -508,17 +495,12 @@ def _conv3_backward_prefill(plan, nw, device):
     return bslot, dq
 
 
-def _conv3_backward_bulk(plan, mb, bits, dY3, nw, mask_rows=None, pre=None, cp=None, scattered=False):
+def _conv3_backward_bulk(plan, mb, bits, dY3, nw, mask_rows=None, pre=None):
     """dQ [T, nw*9, 64] of merlin.windows._conv3_backward with the minibatch's live-patch map taken from
     the update-wide array (mb.kmap, WindowPlan.update_minibatches(bulk=True)).  pre: (bslot preset to -1, zeroed
-    dQ) from _conv3_backward_prefill.  cp: the minibatch's compact patch list (nat.patch_compact); scattered: dY3's
-    rows are in its order (the mask words then through cp.cmrow)."""
-    if cp is not None:
-        R = nat.segment_sum(dY3.contiguous(), cp, plan.num_patches, name="k_seg_sum_R", mask=bits, fill=False,
-                            mask_rows=cp.cmrow if scattered else mask_rows)
-    else:
-        R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
-                            name="k_seg_sum_R", mask=bits, fill=False, mask_rows=mask_rows)
+    dQ) from _conv3_backward_prefill."""
+    R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
+                        name="k_seg_sum_R", mask=bits, fill=False, mask_rows=mask_rows)
     # band sums over the live patches, marking the bands that got one (merlin_segment_sum_marked); dQ reads only
     # those: the dead bands' rows are never zeroed (a 128-MB fill per step) nor read
     if pre is None:

@@ -516,25 +516,14 @@ class _WindowConv3(torch.autograd.Function):
         return dQ, db3, None, None, None
 
 
-# conv3's patch sums (the R pass) over the minibatch's compact patch list (merlin_patch_compact: the update-wide
-# plan's live entries, in plan order) instead of the update-wide plan with the other minibatches' entries skipped
-# through the slot map (~7/8 of them at the bench's 8 minibatches, each wave walking its item's entries regardless).
-# The same rows per patch in the same order; the items they are cut into follow the shorter list
-PATCH_COMPACT = True
-
-
 def _conv3_backward(plan, mb, bits, dY3, nw):
     """(dQ [T, nw, 576], db3 [T, 64]) from dY3 [T, U*9, 64] (conv3's output gradient) and the ReLU bit
     words of the forward: the patch -> band -> window segmented sums of the module docstring."""
     T = bits.shape[0]
     # pass 1: per-patch sums of the ReLU-masked dY3 rows of this minibatch's frames (rows of
     # patches absent from the minibatch are left unwritten and skipped below)
-    if PATCH_COMPACT:
-        cp = nat.patch_compact(plan.patch_plan, mb.slot, 9, int(mb.groups.numel()) * 9)
-        R = nat.segment_sum(dY3.contiguous(), cp, plan.num_patches, name="k_seg_sum_R", mask=bits, fill=False)
-    else:
-        R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
-                            name="k_seg_sum_R", mask=bits, fill=False)
+    R = nat.segment_sum(dY3.contiguous(), plan.patch_plan, plan.num_patches, slot=mb.slot, sub=9,
+                        name="k_seg_sum_R", mask=bits, fill=False)
     live = plan.kid.index_select(0, mb.groups).reshape(-1)
     kmap = torch.full((plan.num_patches,), -1, dtype=torch.int32, device=bits.device)
     kmap[live] = live

@@ -74,8 +74,6 @@ def main():
             FS.MASK_ROWS = "maskcopy" not in name  # the mask-word copy instead of the R pass's row map
             FS.DZ_PLANES = "nodzp" not in name  # dz in fp32 (split by the GEMMs) instead of head_bwd's planes
             FS.A3_PLANES = "noa3p" not in name  # a3 in fp32 instead of conv3's planes
-            W.PATCH_COMPACT = "nocompact" not in name  # the R pass over the update-wide plan
-            FS.COMPACT_SCATTER = "cgather" not in name  # the compact R pass gathering da3's rows
             FS.PREFILL = "noprefill" not in name  # conv3's backward fills beside the weight gradient
             FS.WINDOW_BWD_HIP = "nowinbwd" not in name  # the window GEMM's backward on hipBLASLt + torch
             nat.H3_TN_CFG_PLANES = 0 if "tngplanes" in name else 21 if "tq21" in name else 20  # register-staged / 64-row
