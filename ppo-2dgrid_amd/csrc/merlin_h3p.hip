@@ -48,6 +48,11 @@ __device__ __forceinline__ uint32_t p_amax(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int p_swz(int r) { return (r >> 1) & 7; }
+// a lo plane fragment (8 f16 at 2^11 x their value) back at scale: v_pk_mul_f16 x 4, exact unless the result is
+// subnormal (then rounded to the f16 subnormal grid, 2^-24)
+__device__ __forceinline__ p_u32x4 p_unscale(const p_u32x4 x) {
+    return __builtin_bit_cast(p_u32x4, __builtin_bit_cast(p_f16x8, x) * (_Float16)(1.0f / 2048.0f));
+}
 
 template <int V>
 using IC = std::integral_constant<int, V>;
@@ -66,7 +71,12 @@ __device__ __forceinline__ void lds_rd(p_u32x4 &d, uint32_t addr) { d = *(const 
 // NS: LDS stages of the DMA ring (NS - 1 k steps in flight).  3: 120 KB at 128 x 192; 4 (round 6): 160 KB, the whole
 // LDS of a CU -- a step's DMA is latency-bound (~2.5 us under load against ~1.2 us of MFMA work per step), so the
 // feed rate per CU is the bytes in flight over that latency
-template <int BM, int BN, int WGM, int WGN, int EPI, int NK, int NS = 3>
+// ONE (round 6): one accumulator per tile -- the lo planes (stored 2^11 up) brought back to scale in registers
+// (v_pk_mul_f16 by 2^-11: exact while the result stays normal, f16 subnormals kept) so all three products of a k
+// step add into the same fp32 accumulator: half the accumulator registers, hence twice the tile area per byte staged.
+// Not the same bits as the two-accumulator kernels (a different summation); its error is held to float64 by
+// tests/test_gpu_h3.py like theirs.
+template <int BM, int BN, int WGM, int WGN, int EPI, int NK, int NS = 3, bool ONE = false, int ABL = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restrict__ A, const p_u32x4 *__restrict__ B,
                                                           const uint32_t *__restrict__ amaxA,
                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N, int K,
@@ -81,7 +91,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
     static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "whole DMA instructions per thread");
     constexpr int STG = (BM + BN) * 8;  // chunks per stage
     constexpr uint32_t STG_B = STG * 16;
-    static_assert(NS == 3 || NS == 4, "ring depth");
+    static_assert(NS >= 2 && NS <= 4, "ring depth");
     __shared__ p_u32x4 lds[NS * STG];
 
     const int t = blockIdx.y;
@@ -151,9 +161,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
         else
             lds_rd(g.b[(k - 2 * TM) >> 1][k & 1], adB[kh][k & 1] + so + ((k - 2 * TM) >> 1) * 32 * 128);
     };
-    auto mf = [&](const Frag &f, auto M_) __attribute__((always_inline)) {  // MFMA m: tile (i, j), product m % 3
-        constexpr int m = decltype(M_)::value, i = m / (3 * TN), j = (m / 3) % TN, pr = m % 3;
-        if constexpr (pr == 0)
+    auto mf = [&](const Frag &f, const Frag &u, auto M_) __attribute__((always_inline)) {  // MFMA m: tile (i, j),
+        constexpr int m = decltype(M_)::value, i = m / (3 * TN), j = (m / 3) % TN, pr = m % 3;  // product m % 3
+        if constexpr (ONE) {  // u: f's lo planes at scale
+            if constexpr (pr == 0)
+                hi[i][j] = p_mfma(u.a[i][1], f.b[j][0], hi[i][j]);
+            else if constexpr (pr == 1)
+                hi[i][j] = p_mfma(f.a[i][0], u.b[j][1], hi[i][j]);
+            else
+                hi[i][j] = p_mfma(f.a[i][0], f.b[j][0], hi[i][j]);
+        } else if constexpr (pr == 0)
             lo[i][j] = p_mfma(f.a[i][1], f.b[j][0], lo[i][j]);
         else if constexpr (pr == 1)
             lo[i][j] = p_mfma(f.a[i][0], f.b[j][1], lo[i][j]);
@@ -163,8 +180,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
     // half step: the 12 MFMAs on f, with the 8 reads of g (stage offset so, half KH) one behind each of the first 8
     // (sched_group_barrier: MFMA, read, MFMA, read, ...)
     auto half = [&](const Frag &f, Frag &g, uint32_t so, auto KH, auto READS) __attribute__((always_inline)) {
+        Frag u;
+        if constexpr (ONE) {
+#pragma unroll
+            for (int i = 0; i < TM; i++) u.a[i][1] = p_unscale(f.a[i][1]);
+#pragma unroll
+            for (int j = 0; j < TN; j++) u.b[j][1] = p_unscale(f.b[j][1]);
+        }
         static_for<NM>([&](auto M_) __attribute__((always_inline)) {
-            mf(f, M_);
+            mf(f, u, M_);
             if constexpr (decltype(READS)::value && decltype(M_)::value < NR) rd(g, M_, so, KH);
         });
         if constexpr (decltype(READS)::value) {
@@ -193,7 +217,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
     static_for<NR>([&](auto K_) __attribute__((always_inline)) { rd(f0, K_, 0, IC<0>{}); });
     static_for<NK>([&](auto KT) __attribute__((always_inline)) {
         constexpr int kt = decltype(KT)::value, st = kt % NS, sn = (kt + 1) % NS;
-        if constexpr (kt + D < NK) issue(kt + D, (kt + D) % NS);  // the stage read in step kt - 1
+        if constexpr (kt + D < NK && ABL != 1) issue(kt + D, (kt + D) % NS);  // the stage read in step kt - 1
+        // (ABL 1, a probe: no DMA in the loop -- the MFMA / fragment-read side alone, wrong results)
         __builtin_amdgcn_sched_barrier(0);
         half(f0, f1, (uint32_t)st * STG_B, IC<1>{}, IC<1>{});  // MFMAs of half 0, reads of half 1
         if constexpr (kt + 1 < NK) {
@@ -221,7 +246,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
             for (int r = 0; r < 16; r++) {
                 const int64_t row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
                 if (row < M) {
-                    const float v = (hi[i][j][r] + lo[i][j][r] * P_LO_INV) * inv * invB;
+                    const float v = (ONE ? hi[i][j][r] : hi[i][j][r] + lo[i][j][r] * P_LO_INV) * inv * invB;
                     Ct[row * N + col] = EPI == 1 ? p_relu(v + bv) : v;
                 }
             }
@@ -229,7 +254,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
     }
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS = 3>
+template <int BM, int BN, int WGM, int WGN, int NS = 3, bool ONE = false, int ABL = 0>
 hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
     if (N % BN || K % 32 || K < 64) return hipErrorInvalidValue;
@@ -242,10 +267,10 @@ hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const 
 #define PQ_K(NK)                                                                                                   \
     do {                                                                                                           \
         if (bias)                                                                                                  \
-            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 1, NK, NS>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
+            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 1, NK, NS, ONE, ABL>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
                                sA / 4, sB / 4, bias, C, sC, tiles_n);                                              \
         else                                                                                                       \
-            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 0, NK, NS>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
+            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 0, NK, NS, ONE, ABL>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
                                sA / 4, sB / 4, nullptr, C, sC, tiles_n);                                           \
     } while (0)
     switch (K) {  // the k loop is unrolled: one instantiation per depth (fc1's forward K = 576, input gradient 512)
@@ -787,6 +812,16 @@ hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *
         case 62: return pq_launch<128, 192, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         // round 6: the same with a 4-stage ring (160 KB of LDS, three k steps in flight)
         case 63: return pq_launch<128, 192, 4, 2, 4>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        // round 6: one accumulator per tile (ONE): 65: 256 x 192 tiles on a 2-stage ring (112 KB), 66: 62's 128 x 192
+        // tile, 68: 256 x 256 over 4 waves (one per SIMD: 512 registers each; 8 waves spill), 69: 192 x 192 over 6
+        // waves, 3 stages (144 KB)
+        case 65: return pq_launch<256, 192, 4, 2, 2, true>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 66: return pq_launch<128, 192, 4, 2, 3, true>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 68: return pq_launch<256, 256, 2, 2, 2, true>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 69: return pq_launch<192, 192, 3, 2, 3, true>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        // probes (ABL 1: no DMA in the k loop, wrong results): 64 = 65's, 67 = 62's
+        case 64: return pq_launch<256, 192, 4, 2, 2, true, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 67: return pq_launch<128, 192, 4, 2, 3, false, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         default: return hipErrorInvalidValue;
     }
 }
