@@ -18,6 +18,11 @@ struct merlin_env {
     int steps_since_refill;  // merlin_env_step launches since the last look-ahead refill
     int refill_every;        // 0: the caller launches refills (merlin_env_refill)
     bool no_fallback = false;  // merlin_env_set_step_fallback(0): with refill_every 0, no k_env_fallback pass
+    // reseed mode (every reset is reset(seed=task_seed)) after a full reset: every look-ahead slot holds its env's
+    // seed map and no reset consumes it, so the periodic refills and the fallback pass would find nothing to do and
+    // are left out (an empty slot would still raise MERLIN_DEVERR_SLOT_EMPTY); cleared when merlin_env_seed makes
+    // the slots stale (round 6: FOMAML's 32-env task rollouts, two graph nodes fewer per step)
+    bool seed_slots_full = false;
 };
 
 namespace {
@@ -381,6 +386,7 @@ int merlin_env_seed(merlin_env *e, const uint64_t *seeds, int32_t n, void *strea
         err = hipMemcpyAsync(e->dev.rng_i, inc, N * sizeof(ulonglong2), hipMemcpyHostToDevice, s);
     if (err == hipSuccess) err = merlin::zero_async(e->dev.rng_b, N * sizeof(uint2), s);
     if (err == hipSuccess) err = merlin::zero_async(e->dev.pg_valid, N, s);  // look-ahead maps are stale
+    e->seed_slots_full = false;
     if (err == hipSuccess) err = hipStreamSynchronize(s);  // host staging buffers are freed below
     delete[] st;
     delete[] inc;
@@ -392,7 +398,10 @@ int merlin_env_reset(merlin_env *e, const uint8_t *mask, uint32_t *obs, void *st
     if (!e) return fail(MERLIN_E_INVALID, "null env");
     HIP_TRY(merlin::launch_env_reset(e->dev, mask, obs, (hipStream_t)stream));  // + look-ahead refill
     e->steps_since_refill = 0;
-    if (!mask) e->has_state = true;
+    if (!mask) {
+        e->has_state = true;
+        e->seed_slots_full = e->dev.reseed != 0;  // the reset's full refill filled every slot with its seed map
+    }
     return MERLIN_OK;
 }
 
@@ -416,9 +425,9 @@ int merlin_env_step(merlin_env *e, const int64_t *actions, int32_t n_steps, int6
     o.done = done;
     o.ep_ret_out = ep_ret;
     o.ep_len_out = ep_len;
-    const bool refill = e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
+    const bool refill = !e->seed_slots_full && e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
     if (refill) e->steps_since_refill = 0;
-    o.no_fallback = e->no_fallback && e->refill_every == 0;
+    o.no_fallback = e->seed_slots_full || (e->no_fallback && e->refill_every == 0);
     HIP_TRY(merlin::launch_env_step(e->dev, o, refill, (hipStream_t)stream));
     return MERLIN_OK;
 }
@@ -447,9 +456,9 @@ int merlin_env_act_step(merlin_env *e, const float *head_part, int32_t n_parts, 
     o.ep_len_out = ep_len;
     o.act = merlin::ActIn{reinterpret_cast<const float4 *>(head_part), n_parts, b_actor, b_critic, act_dim,
                           deterministic ? 1 : 0, seed, epoch, step, env_offset, action, logp, value};
-    const bool refill = e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
+    const bool refill = !e->seed_slots_full && e->refill_every > 0 && ++e->steps_since_refill >= e->refill_every;
     if (refill) e->steps_since_refill = 0;
-    o.no_fallback = e->no_fallback && e->refill_every == 0;
+    o.no_fallback = e->seed_slots_full || (e->no_fallback && e->refill_every == 0);
     HIP_TRY(merlin::launch_env_step(e->dev, o, refill, (hipStream_t)stream));
     return MERLIN_OK;
 }
