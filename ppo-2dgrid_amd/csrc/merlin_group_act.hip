@@ -12,7 +12,7 @@
 //                  -> conv3 (9 x 64 outputs, 576 MACs each; the 4 waves split the 576-long reduction, summed in
 //                  wave order) + b3, ReLU -> a3 [tower][576] in fc1's (p3, co) column order
 //   k_group_fc1    one block per (task, tower, 64-column chunk of fc1): h = relu(b4 + W4p a3) of its 64 columns
-//                  (a wave per column, lanes over k, a fixed xor tree), then the head dot products of those 64
+//                  (16 waves of 4 columns, lanes over k, a fixed xor tree), then the head dot products of those 64
 //                  columns (actor: the task's A logits' weights, critic: its value weights) summed in wave order;
 //                  chunk 0 adds the task's head biases -> part[tower][chunk][task][4], the partial-sum layout
 //                  merlin_env_act_step / merlin_act_draw read (then called with zero biases)
@@ -40,6 +40,12 @@ __global__ __launch_bounds__(GC_T) void k_group_conv(const uint32_t *__restrict_
     const int tt = blockIdx.x, g = tt >> 1;  // tower tt = 2 g (actor) / 2 g + 1 (critic) of task g
     const int wt = shared ? (tt & 1) : tt;   // its weights' tower (one weight set for every task when shared)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // conv3's weights first (they do not depend on the frame): their load round trip overlaps the frame -> T2 chain
+    const float *w3 = W3t + (size_t)wt * GA_K * 64 + lane;
+    const int k0 = wv * GC_KW;
+    float wk[GC_KW];
+#pragma unroll
+    for (int u = 0; u < GC_KW; u++) wk[u] = w3[(size_t)(k0 + u) * 64];
     if (tid < 49) {
         const uint32_t word = codes[(size_t)g * MERLIN_OBS_WORDS + (tid >> 3)];
         cls[tid] = (uint8_t)min((word >> ((tid & 7) * 4)) & 0xfu, 4u);
@@ -88,14 +94,9 @@ __global__ __launch_bounds__(GC_T) void k_group_conv(const uint32_t *__restrict_
     // conv3: lane = output channel co, wave wv takes k = tap * 64 + ci in [36 wv, 36 wv + 36) for all 9 positions
     // (its 36 weights loaded before the FMAs: one load round trip per wave)
     const float *a2f = reinterpret_cast<const float *>(&a2[0][0]);
-    const float *w3 = W3t + (size_t)wt * GA_K * 64 + lane;
     float acc[9];
 #pragma unroll
     for (int p3 = 0; p3 < 9; p3++) acc[p3] = 0.0f;
-    const int k0 = wv * GC_KW;
-    float wk[GC_KW];
-#pragma unroll
-    for (int u = 0; u < GC_KW; u++) wk[u] = w3[(size_t)(k0 + u) * 64];
 #pragma unroll
     for (int u = 0; u < GC_KW; u++) {
         const int k = k0 + u, tap = k >> 6, ci = k & 63, ky = tap / 3, kx = tap - ky * 3;
@@ -117,53 +118,65 @@ __global__ __launch_bounds__(GC_T) void k_group_conv(const uint32_t *__restrict_
     }
 }
 
-__global__ __launch_bounds__(256) void k_group_fc1(const float *__restrict__ a3, const float *__restrict__ W4p,
-                                                   const float *__restrict__ b4, const float *__restrict__ Wa,
-                                                   const float *__restrict__ ba, const float *__restrict__ Wc,
-                                                   const float *__restrict__ bc, int G, int A,
-                                                   float *__restrict__ part, int shared) {
-    __shared__ float red[4][4];
+// 16 waves x 4 columns per 64-column chunk (round 6; 4 waves walked 16 columns in 4 dependent load rounds): each lane
+// issues its 36 fc1 weights, the columns' biases and head weights at once -- one load round trip per step
+constexpr int GF_W = 16, GF_T = 64 * GF_W;
+__global__ __launch_bounds__(GF_T) void k_group_fc1(const float *__restrict__ a3, const float *__restrict__ W4p,
+                                                    const float *__restrict__ b4, const float *__restrict__ Wa,
+                                                    const float *__restrict__ ba, const float *__restrict__ Wc,
+                                                    const float *__restrict__ bc, int G, int A,
+                                                    float *__restrict__ part, int shared) {
+    __shared__ float red[GF_W][4];
     const int j = blockIdx.x, tt = blockIdx.y, g = tt >> 1, tower = tt & 1;
     const int wt = shared ? tower : tt, wg = shared ? 0 : g;  // the weights' tower and task
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n0 = j * 64 + wv * 4;  // this wave's 4 columns
+    const float *wrow = W4p + (size_t)wt * GA_H * GA_K + (size_t)n0 * GA_K + lane;
+    float wr[4][9];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int i = 0; i < 9; i++) wr[c][i] = wrow[(size_t)c * GA_K + 64 * i];
+    float bn[4], hw[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int n = n0 + c;
+        bn[c] = b4[(size_t)wt * GA_H + n];
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+            hw[c][a] = tower == 0 ? (a < A ? Wa[((size_t)wg * A + a) * GA_H + n] : 0.0f)
+                                  : (a == 0 ? Wc[(size_t)wg * GA_H + n] : 0.0f);
+    }
     float x[9];
 #pragma unroll
     for (int i = 0; i < 9; i++) x[i] = a3[(size_t)tt * GA_K + lane + 64 * i];
-    float hp[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // this wave's head partials over its 16 columns
-    const float *wrow = W4p + (size_t)wt * GA_H * GA_K;
-    for (int n0 = j * 64 + wv * 16; n0 < j * 64 + wv * 16 + 16; n0 += 4) {
-        float d[4];
+    float d[4];
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const float *r = wrow + (size_t)(n0 + c) * GA_K + lane;
-            float s = 0.0f;
+    for (int c = 0; c < 4; c++) {
+        float s = 0.0f;
 #pragma unroll
-            for (int i = 0; i < 9; i++) s += r[64 * i] * x[i];
-            d[c] = s;
-        }
+        for (int i = 0; i < 9; i++) s += wr[c][i] * x[i];
+        d[c] = s;
+    }
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
+    for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
-            for (int c = 0; c < 4; c++) d[c] += __shfl_xor(d[c], off);
+        for (int c = 0; c < 4; c++) d[c] += __shfl_xor(d[c], off);
+    float hp[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // this wave's head partials over its 4 columns
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const int n = n0 + c;
-            const float h = fmaxf(d[c] + b4[(size_t)wt * GA_H + n], 0.0f);
-            if (tower == 0) {
+    for (int c = 0; c < 4; c++) {
+        const float h = fmaxf(d[c] + bn[c], 0.0f);
 #pragma unroll
-                for (int a = 0; a < 4; a++)
-                    if (a < A) hp[a] += h * Wa[((size_t)wg * A + a) * GA_H + n];
-            } else {
-                hp[0] += h * Wc[(size_t)wg * GA_H + n];
-            }
-        }
+        for (int a = 0; a < 4; a++) hp[a] += h * hw[c][a];
     }
     if (lane == 0)
 #pragma unroll
         for (int a = 0; a < 4; a++) red[wv][a] = hp[a];
     __syncthreads();
     if (tid < 4) {
-        float s = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+        float s = red[0][tid];
+#pragma unroll
+        for (int v = 1; v < GF_W; v++) s += red[v][tid];  // wave order
         if (j == 0) s += tower == 0 ? (tid < A ? ba[(size_t)wg * A + tid] : 0.0f) : (tid == 0 ? bc[wg] : 0.0f);
         part[(((size_t)tower * gridDim.x + j) * G + g) * 4 + tid] = s;
     }
@@ -181,7 +194,7 @@ hipError_t launch_group_act(const uint32_t *codes, int G, const float *T2, const
                        W3t, b3, a3, (int)shared);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_group_fc1, dim3(GA_H / 64, 2 * G), dim3(256), 0, s, a3, W4p, b4, Wa, ba, Wc, bc, G, A, part,
+    hipLaunchKernelGGL(k_group_fc1, dim3(GA_H / 64, 2 * G), dim3(GF_T), 0, s, a3, W4p, b4, Wa, ba, Wc, bc, G, A, part,
                        (int)shared);
     return hipGetLastError();
 }
