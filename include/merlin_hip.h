@@ -632,8 +632,11 @@ int merlin_h3_gemm_nt_heads(const float *A_dev, const uint32_t *amax_a_dev, cons
 int32_t merlin_h3_heads_parts(int32_t N, int32_t cfg);
 /* gemm_nt_planes: gemm_nt with A already in plane form too (A_planes [t][M][K/8][2][8] f16 scaled by amax_a_dev's
  *          exponent, e.g. merlin_tower_head_bwd_planes' dz), both operands staged into LDS by DMA (csrc/merlin_h3p.hip):
- *          cfg 60 128x256 / 61 256x128 / 62 128x192 tiles, K = 512 or 576, bias as gemm_nt.  Same products and
- *          order as gemm_nt on the fp32 A with the same scale: the same bits.
+ *          cfg 60 128x256 / 62 128x192 tiles, K = 512 or 576, bias as gemm_nt.  Same products and order as gemm_nt
+ *          on the fp32 A with the same scale: the same bits.  Measured alternates (round 6, not on the benched path):
+ *          63 = 62 on a 4-stage ring; 66 = 62 with its MFMAs product-major (the same bits); 65 / 68 / 69 = one
+ *          accumulator per tile (the lo planes rescaled in registers: another summation, held to float64 like the
+ *          rest) on 256x192 / 256x256 (4 waves) / 192x192 tiles.
  * gemm_tn_gather_planes_a: gemm_tn_gather with A already in plane form (strides in values). */
 int merlin_h3_gemm_nt_planes(const void *A_planes_dev, const uint32_t *amax_a_dev, const void *B_dev,
                              const uint32_t *amax_b_dev, int64_t M, int32_t N, int32_t K, int32_t towers,

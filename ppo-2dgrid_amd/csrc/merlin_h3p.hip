@@ -76,7 +76,7 @@ __device__ __forceinline__ void lds_rd(p_u32x4 &d, uint32_t addr) { d = *(const 
 // step add into the same fp32 accumulator: half the accumulator registers, hence twice the tile area per byte staged.
 // Not the same bits as the two-accumulator kernels (a different summation); its error is held to float64 by
 // tests/test_gpu_h3.py like theirs.
-template <int BM, int BN, int WGM, int WGN, int EPI, int NK, int NS = 3, bool ONE = false, int ABL = 0>
+template <int BM, int BN, int WGM, int WGN, int EPI, int NK, int NS = 3, bool ONE = false, int ABL = 0, int ORD = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restrict__ A, const p_u32x4 *__restrict__ B,
                                                           const uint32_t *__restrict__ amaxA,
                                                           const uint32_t *__restrict__ amaxB, int64_t M, int N, int K,
@@ -161,8 +161,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
         else
             lds_rd(g.b[(k - 2 * TM) >> 1][k & 1], adB[kh][k & 1] + so + ((k - 2 * TM) >> 1) * 32 * 128);
     };
-    auto mf = [&](const Frag &f, const Frag &u, auto M_) __attribute__((always_inline)) {  // MFMA m: tile (i, j),
-        constexpr int m = decltype(M_)::value, i = m / (3 * TN), j = (m / 3) % TN, pr = m % 3;  // product m % 3
+    // MFMA m: tile (i, j), product pr -- ORD 0: a tile's three products back to back (m / 3 = tile, m % 3 = pr);
+    // ORD 1: product-major (every tile's pr 0, then every tile's pr 1, ...), so consecutive MFMAs never share an
+    // accumulator; each accumulator still sums the same products in the same order (the same bits)
+    auto mf = [&](const Frag &f, const Frag &u, auto M_) __attribute__((always_inline)) {
+        constexpr int m = decltype(M_)::value, tl = ORD ? m % (TM * TN) : m / 3, pr = ORD ? m / (TM * TN) : m % 3;
+        constexpr int i = tl / TN, j = tl % TN;
         if constexpr (ONE) {  // u: f's lo planes at scale
             if constexpr (pr == 0)
                 hi[i][j] = p_mfma(u.a[i][1], f.b[j][0], hi[i][j]);
@@ -254,7 +258,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
     }
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS = 3, bool ONE = false, int ABL = 0>
+template <int BM, int BN, int WGM, int WGN, int NS = 3, bool ONE = false, int ABL = 0, int ORD = 0>
 hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const uint32_t *amaxB, int64_t M, int N,
                      int K, int T, int64_t sA, int64_t sB, const float *bias, float *C, int64_t sC, hipStream_t s) {
     if (N % BN || K % 32 || K < 64) return hipErrorInvalidValue;
@@ -267,10 +271,10 @@ hipError_t pq_launch(const void *A, const void *B, const uint32_t *amaxA, const 
 #define PQ_K(NK)                                                                                                   \
     do {                                                                                                           \
         if (bias)                                                                                                  \
-            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 1, NK, NS, ONE, ABL>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
+            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 1, NK, NS, ONE, ABL, ORD>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
                                sA / 4, sB / 4, bias, C, sC, tiles_n);                                              \
         else                                                                                                       \
-            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 0, NK, NS, ONE, ABL>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
+            hipLaunchKernelGGL((k_h3_pq<BM, BN, WGM, WGN, 0, NK, NS, ONE, ABL, ORD>), grid, block, 0, s, a, b, amaxA, amaxB, M, N, K, \
                                sA / 4, sB / 4, nullptr, C, sC, tiles_n);                                           \
     } while (0)
     switch (K) {  // the k loop is unrolled: one instantiation per depth (fc1's forward K = 576, input gradient 512)
@@ -780,7 +784,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pqg(const p_u32x4 *__rest
 
 }  // namespace
 
-// A, B: plane images (4 B per value, strides in values); cfg 60: 128 x 256 tiles (2 x 4 waves), 61: 256 x 128 (4 x 2),
+// A, B: plane images (4 B per value, strides in values); cfg 60: 128 x 256 tiles (2 x 4 waves),
 // 62: 128 x 192 (4 x 2 waves of 32 x 96: N = 576)
 hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *B, const uint32_t *amaxB, int64_t M,
                               int N, int K, int T, int64_t a_stride, int64_t b_stride, const float *bias, float *C,
@@ -808,7 +812,6 @@ hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *
     }
     switch (cfg) {
         case 60: return pq_launch<128, 256, 2, 4>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
-        case 61: return pq_launch<256, 128, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 62: return pq_launch<128, 192, 4, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         // round 6: the same with a 4-stage ring (160 KB of LDS, three k steps in flight)
         case 63: return pq_launch<128, 192, 4, 2, 4>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
@@ -816,12 +819,15 @@ hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *
         // tile, 68: 256 x 256 over 4 waves (one per SIMD: 512 registers each; 8 waves spill), 69: 192 x 192 over 6
         // waves, 3 stages (144 KB)
         case 65: return pq_launch<256, 192, 4, 2, 2, true>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
-        case 66: return pq_launch<128, 192, 4, 2, 3, true>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        // 66: 62 with the MFMAs product-major (ORD 1: no two consecutive MFMAs on one accumulator; the same bits)
+        case 66: return pq_launch<128, 192, 4, 2, 3, false, 0, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 68: return pq_launch<256, 256, 2, 2, 2, true>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 69: return pq_launch<192, 192, 3, 2, 3, true>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
-        // probes (ABL 1: no DMA in the k loop, wrong results): 64 = 65's, 67 = 62's
+#ifdef MERLIN_PROBES  // ablations (ABL 1: no DMA in the k loop -- wrong results on purpose): 64 = 65's, 67 = 62's, 61 = 66's
         case 64: return pq_launch<256, 192, 4, 2, 2, true, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 67: return pq_launch<128, 192, 4, 2, 3, false, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 61: return pq_launch<128, 192, 4, 2, 3, false, 1, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+#endif
         default: return hipErrorInvalidValue;
     }
 }

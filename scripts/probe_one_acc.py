@@ -4,7 +4,9 @@ two-accumulator kernels, at the update's shapes: the input gradient (N = 576, K 
 forward's shape (N = 512, K = 576: cfg 60 vs 64 / 67 / 68).  HIP-event time per launch (median of 3 rounds, alternating
 in one process) and each kernel's error against float64 in the units of tests/test_gpu_h3.py (max |C - C64| /
 sum_k |a_k b_k|), beside torch's fp32 GEMM on the same operands.
-    python scripts/probe_one_acc.py [U] [reps]"""
+The no-DMA ablations (cfg 61 / 64 / 67) exist only in a -DMERLIN_PROBES build (make -C ppo-2dgrid_amd
+EXTRA=-DMERLIN_PROBES); results: profiles/r06k_one_acc.log, r06r_order.log.
+    python scripts/probe_one_acc.py [U] [reps] [cfgs]"""
 import os
 import sys
 
@@ -37,9 +39,9 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     shapes = {
         # input gradient: dz [U, 512] (sparse-ish, ~1e-6) x W^T -> [U, 576]
-        "dgrad": (576, 512, [62, 65, 66, 69, 64, 67]),
+        "dgrad": (576, 512, [62, 66, 67, 61]),
         # forward's shape: a3 [U, 576] (ReLU output) x W4 [512, 576]^T -> [U, 512]
-        "fwd": (512, 576, [60, 68]),
+        "fwd": (512, 576, [60]),
     }
     for name, (N, K, cs) in shapes.items():
         if cfgs:
