@@ -257,3 +257,26 @@ def test_gemm_tn_dynamic_range(device):
     zmax = dz.abs().amax(dim=(1, 2)).double().view(2, 1, 1)
     absa = a3.abs().double().sum(dim=1).unsqueeze(1)  # [2, 1, 576]
     assert ((W.double() - W64).abs() <= tol * den + 2.0 ** -49 * zmax * absa).all()
+
+
+@pytest.mark.parametrize("N,K,cfg", [(576, 512, 62), (576, 512, 63), (576, 512, 66), (576, 512, 65), (576, 512, 69),
+                                     (512, 576, 60), (512, 576, 68)])
+@pytest.mark.parametrize("M,scale_a,ragged", [(777, 1.0, False), (20011, 1e-7, False), (9999, 1.0, True)])
+def test_gemm_nt_planes_vs_float64(device, M, N, K, cfg, scale_a, ragged):
+    """merlin_h3_gemm_nt_planes (both operands as planes, LDS-DMA staged, csrc/merlin_h3p.hip) at the update's shapes:
+    the benched tiles (60 / 62), the 4-stage ring (63) and the product-major MFMA order (66) -- 62's products in 62's
+    order, the same bits -- and the one-accumulator alternates (65 / 68 / 69: the lo planes rescaled in registers,
+    another summation) all within torch's fp32 GEMM error against float64."""
+    from merlin import _native as nat
+
+    A, B = _operands(device, M, N, K, 7 * M + cfg, scale_a, ragged)
+    C64 = torch.bmm(A.double(), B.double().transpose(1, 2))
+    den = torch.bmm(A.abs().double(), B.abs().double().transpose(1, 2))
+    tol = max(_err(torch.bmm(A, B.transpose(1, 2)), C64, den), FLOOR)
+    amA, amB = nat.h3_amax(A), nat.h3_amax(B)
+    Ap, Bp = nat.h3_split(A, amA), nat.h3_split(B, amB)
+    C = nat.h3_gemm_nt_planes(Ap, amA, Bp, amB, cfg=cfg)
+    assert _err(C, C64, den) <= tol
+    assert torch.equal(C, nat.h3_gemm_nt_planes(Ap, amA, Bp, amB, cfg=cfg))  # fixed order: the same bits every call
+    if cfg in (63, 66):
+        assert torch.equal(C, nat.h3_gemm_nt_planes(Ap, amA, Bp, amB, cfg=62))
