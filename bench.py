@@ -375,12 +375,18 @@ def pmc_traffic(kernel: str):
         stats = sorted(glob.glob(os.path.join(REPO, "profiles", "*_kernel_stats.md")))
         newest = os.path.basename(stats[-1]).split("_")[0] if stats else ""
         files = [f for f in files if os.path.basename(f).split("_")[0] >= newest]
+    def entry(dd, n):  # the exact name, else the one kernel whose template arguments extend the alias's
+        if n in dd or not n.endswith(">"):
+            return dd.get(n, {})
+        ext = [k for k in dd if k.startswith(n[:-1] + ",")]
+        return dd[ext[0]] if len(ext) == 1 else {}
+
     for f in files:
         try:
             dd = json.load(open(f))
         except Exception:
             continue
-        got = [dd.get(n, {}).get("hbm_bytes_per_launch") for n in names]
+        got = [entry(dd, n).get("hbm_bytes_per_launch") for n in names]
         if got[0]:
             return int(sum(g for g in got if g))
     return None

@@ -22,5 +22,7 @@ if [ -n "$PMC" ]; then
 fi
 cd "$R" && python scripts/prof_summary.py "${TAG:-r06}" gpurun_out/summary || exit $?
 python scripts/busy_union.py gpurun_out/prof_trace/run_kernel_trace.csv > gpurun_out/summary/${TAG:-r06}_busy_union.txt
+python scripts/kernel_sequence.py gpurun_out/prof_trace/run_kernel_trace.csv \
+    gpurun_out/summary/${TAG:-r06}_step_sequence.md || true
 cp gpurun_out/prof_trace.log gpurun_out/summary/ 2>/dev/null
 rm -f gpurun_out/prof_*/run_kernel_trace.csv gpurun_out/prof_*/run_counter_collection.csv
