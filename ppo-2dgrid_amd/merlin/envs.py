@@ -65,7 +65,7 @@ class MerlinVecEnv:
                  max_steps: int | None = None, seed: int | None = None, device="cuda",
                  stuck_penalty: bool = False, max_stay: int = 3, penalty: float = -0.1,
                  exploration_bonus: bool = False, bonus: float = 0.01, env_offset: int = 0,
-                 seeds=None, reseed_each_reset: bool = False):
+                 seeds=None, reseed_each_reset: bool = False, fully_observable: bool = False, flatten: bool = False):
         if difficulty not in nat.DIFFICULTY_IDS:
             raise ValueError(f"Unknown difficulty: {difficulty}")
         self.device = torch.device(device)
@@ -77,7 +77,14 @@ class MerlinVecEnv:
         self.max_steps = int(max_steps) if max_steps else 4 * self.size * self.size
         self.env_offset = int(env_offset)
         self.action_space = Discrete(3)
-        self.single_observation_space = Box(0, 255, (56, 56, 3), np.uint8)
+        # the observation wrappers of scenario_creator.py:45-53 (observation.fully_observable / flatten): the step
+        # always produces the RGB partial view's tile codes; flat_obs() gives the wrapped observation of a batch --
+        # the RGB view (56, 56, 3) or the encoded full grid (size, size, 3), flattened to a vector with flatten
+        self.fully_observable, self.flatten = bool(fully_observable), bool(flatten)
+        shape = (self.size, self.size, 3) if self.fully_observable else (56, 56, 3)
+        if self.flatten:
+            shape = (int(np.prod(shape)),)
+        self.single_observation_space = Box(0, 255, shape, np.uint8)
         self.observation_space = self.single_observation_space
         cfg = nat.EnvConfig(self.num_envs, self.size, nat.DIFFICULTY_IDS[difficulty], self.max_steps,
                             int(stuck_penalty), int(max_stay), float(penalty), int(exploration_bonus),
@@ -239,6 +246,13 @@ class MerlinVecEnv:
     def render_rgb(self, codes: torch.Tensor | None = None) -> torch.Tensor:
         codes = self.obs if codes is None else codes
         return nat.expand_obs_u8(codes.reshape(-1, nat.OBS_WORDS))
+
+    def flat_obs(self, codes: torch.Tensor | None = None, index: torch.Tensor | None = None) -> torch.Tensor:
+        """f32 [n, D]: FlattenObservation of the wrapped observation as the reference's MLP path takes it (src/ppo.py:
+        58-62: the uint8 values as floats, no scaling) -- the RGB partial view expanded from tile codes (rows `index`
+        of `codes`, default the current ones), D = 9,408."""
+        codes = self.obs if codes is None else codes
+        return nat.expand_obs_u8(codes.reshape(-1, nat.OBS_WORDS), index=index).view(-1, 56 * 56 * 3).float()
 
     def render_full(self, out: torch.Tensor | None = None) -> torch.Tensor:
         """uint8[N, size, size, 3]: the fully observable observation of every env's current state

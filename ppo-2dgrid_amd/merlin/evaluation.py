@@ -36,10 +36,23 @@ def evaluate_seeds(ac, seeds, difficulty: str = "mediumhard", size: int = 16, de
                    max_steps: int | None = None, record: bool = False, **env_flags):
     """One deterministic episode per seed, all at once -> (rewards list[float], steps list[int])
     [+ actions int64[T, n] when record: the actions taken, for replay checks]."""
+    from .actor_critic import MLPActorCritic
+
     seeds = [int(s) for s in seeds]
     n = len(seeds)
     env = MerlinVecEnv(n, difficulty=difficulty, size=size, device=device, max_steps=max_steps, seeds=seeds,
                        **env_flags)
+    # an MLP policy (observation.flatten) takes the flattened view its input width names: the RGB partial view
+    # (9,408) or the encoded full grid (size * size * 3, observation.fully_observable)
+    mlp = isinstance(ac, MLPActorCritic)
+    full = mlp and ac.actor[0].in_features == size * size * 3
+
+    def act(obs):
+        if not mlp:
+            return ac.act_codes(obs, deterministic=True)
+        x = env.render_full().reshape(n, -1).float() if full else env.flat_obs(obs)
+        return ac.act(x, deterministic=True)
+
     try:
         obs = env.reset().clone()
         total = torch.zeros(n, dtype=torch.float64, device=env.device)
@@ -47,7 +60,7 @@ def evaluate_seeds(ac, seeds, difficulty: str = "mediumhard", size: int = 16, de
         done = torch.zeros(n, dtype=torch.bool, device=env.device)
         acts = []
         for _ in range(env.max_steps):
-            action, _, _ = ac.act_codes(obs, deterministic=True)
+            action, _, _ = act(obs)
             obs, _, term, trunc, info = env.step(action, autoreset=False)
             if record:
                 acts.append(action.clone())

@@ -142,15 +142,31 @@ class PPO:
                 raise ValueError(f"batch_size {batch_size} must be a multiple of num_envs {N}")
             self.num_envs, self.k_steps = N, batch_size // N
             self.batch_size = batch_size
-            self.use_cnn = True
-            self.obs_shape = (56, 56, 3)
-            self.ac = CNNActorCritic(self.obs_shape, act_dim).to(self.device)
+            self._full_obs = None
+            if getattr(self.vec, "flatten", False):
+                # observation.flatten (scenario_creator.py:52-53): the reference's MLP on the flattened observation
+                # (src/ppo.py:38-41), N envs at a time -- the RGB view rebuilt from the stored tile codes per
+                # minibatch, or the encoded full grid (observation.fully_observable) stored per step
+                self.use_cnn = False
+                self.obs_shape = tuple(self.vec.observation_space.shape)
+                self.ac = MLPActorCritic(self.obs_shape[0], act_dim).to(self.device)
+                self.conv1_from_codes = False
+                if getattr(self.vec, "fully_observable", False):
+                    self._full_obs = torch.empty((self.k_steps + 1, N) + self.obs_shape, dtype=torch.uint8,
+                                                 device=self.device)
+            elif getattr(self.vec, "fully_observable", False):
+                raise ValueError("the full grid without flatten is smaller than CNNActorCritic's receptive field")
+            else:
+                self.use_cnn = True
+                self.obs_shape = (56, 56, 3)
+                self.ac = CNNActorCritic(self.obs_shape, act_dim).to(self.device)
             self.buf = CodeRolloutBuffer(self.k_steps, N, self.device)
             self._obs_step = torch.empty((N, 3, 56, 56), dtype=torch.float32, device=self.device)
             self._mb_obs = None
             # look-ahead map refills on a side stream after every step, overlapping the next act
             # (MerlinVecEnv.refill; the env's own every-16-steps refill is switched off)
-            self._refill_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+            self._refill_stream = (torch.cuda.Stream(self.device) if self.device.type == "cuda" and self.use_cnn
+                                   else None)
             if self._refill_stream is not None:
                 self.vec.set_refill_interval(0)
         else:
@@ -216,6 +232,8 @@ class PPO:
     def collect_rollouts(self):
         if self.vec is None:
             return self._collect_rollouts_single()
+        if not self.use_cnn:
+            return self._collect_rollouts_flat()
         if self._graph is not None and not self._params_on_flat():
             self._rehome_parameters()  # the graph would read the old parameter storage: re-capture
         if self._graph is not None:
@@ -346,6 +364,39 @@ class PPO:
             _, _, v = self.ac.act(self._obs_to_tensor(state))
         return v.item()
 
+    def _flat_obs_at(self, t=None, index=None):
+        """The MLP's f32 observations: step t's (all envs) or the flat samples `index` of the rollout."""
+        buf = self.buf
+        if self._full_obs is not None:
+            x = self._full_obs[t] if index is None else self._full_obs[:buf.T].reshape(buf.T * buf.N, -1)[index]
+            return x.reshape(x.shape[0], -1).float()
+        codes = buf.codes[t] if index is None else buf.flat_codes
+        return self.vec.flat_obs(codes, index=index)
+
+    @torch.no_grad()
+    def _collect_rollouts_flat(self):
+        """ppo.py:64-105 with the MLP on flattened observations (src/ppo.py:38-41), N envs per step: the act is the
+        reference's (Categorical sample with torch's RNG), the env step and the auto-reset are the HIP kernels'."""
+        buf, env = self.buf, self.vec
+        T = buf.T
+        env.reset(out=buf.codes[0])
+        if self._full_obs is not None:
+            env.render_full(out=self._full_obs[0])
+        for t in range(T):
+            action, logp, value = self.ac.act(self._flat_obs_at(t))
+            buf.actions[t].copy_(action)
+            buf.logprobs[t].copy_(logp)
+            buf.values[t].copy_(value)
+            env.step_into(buf.actions[t], buf.codes[t + 1], buf.rewards[t], None, None, buf.dones[t],
+                          buf.ep_return[t], buf.ep_length[t])
+            if self._full_obs is not None:
+                env.render_full(out=self._full_obs[t + 1])
+        _, _, last_value = self.ac.act(self._flat_obs_at(T))
+        buf.last_value.copy_(last_value)
+        self._record_episodes()
+        env.errors()
+        return buf.last_value
+
     # ---------------------------------------------------------------------- GAE
     def compute_gae(self, rewards, values, dones, last_value, stats=None):
         """ppo.py:107-120 on the HIP kernel; [T] or [T, N] device tensors."""
@@ -380,6 +431,8 @@ class PPO:
     def _minibatch_obs(self, codes, states, mb_idx):
         if codes is None:
             return states[mb_idx], False
+        if not self.use_cnn:  # the flattened observations of the batched MLP path
+            return self._flat_obs_at(index=mb_idx), False
         n = mb_idx.numel()
         if self._mb_obs is None or self._mb_obs.shape[0] < n:
             self._mb_obs = torch.empty((n, 3, 56, 56), dtype=torch.float32, device=self.device)

@@ -67,15 +67,17 @@ class ScenarioCreator:
 
     def create_vec_env(self, difficulty: str, num_envs: int, seed=None, device="cuda", env_offset: int = 0,
                        **flags) -> MerlinVecEnv:
-        """N envs for the batched trainer.  Their step produces the RGB partial view's tile codes (the only
-        observation the reference's CNNActorCritic can train on: the full grid is 16 x 16, smaller than its conv
-        stack's receptive field, and a flattened vector has no (h, w, c) shape); the full grid of any state is
-        MerlinVecEnv.render_full."""
-        if self.obs_cfg.get("fully_observable", False) or self.obs_cfg.get("flatten", False):
+        """N envs for the batched trainer.  Their step produces the RGB partial view's tile codes; with
+        observation.flatten the batched trainer takes the reference's MLP path on the flattened view (the RGB view, or
+        with observation.fully_observable the encoded full grid: MerlinVecEnv.flat_obs / render_full).  The full grid
+        unflattened is refused: it is 16 x 16, smaller than CNNActorCritic's receptive field (the reference's CNN
+        fails on it too)."""
+        full, flat = bool(self.obs_cfg.get("fully_observable", False)), bool(self.obs_cfg.get("flatten", False))
+        if full and not flat:
             raise ValueError("CNNActorCritic trains on the (56, 56, 3) RGB partial view (src/actor_critic.py:22-28); "
-                             "observation.fully_observable / flatten give observations it cannot take")
-        return MerlinVecEnv(num_envs, seed=seed, device=device, env_offset=env_offset,
-                            **self._env_kwargs(difficulty), **flags)
+                             "observation.fully_observable without flatten gives a grid smaller than its receptive field")
+        return MerlinVecEnv(num_envs, seed=seed, device=device, env_offset=env_offset, fully_observable=full,
+                            flatten=flat, **self._env_kwargs(difficulty), **flags)
 
     def sample_scenarios(self, n: int = 5, difficulty: str = "easy"):
         return [self.create_env(difficulty) for _ in range(n)]
