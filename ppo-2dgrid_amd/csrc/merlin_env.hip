@@ -774,7 +774,9 @@ __global__ __launch_bounds__(BLK) void k_env_fallback(EnvDev E, uint32_t *__rest
 // DEFER (single-step launches): a reset takes the env's look-ahead slot; when the slot is empty the env
 // is flagged (rflag, and its SBLK-env block in bflag) and k_env_fallback, launched next on the stream,
 // generates its map and writes its observation, so this kernel carries no generator (lean registers).
-template <int SP, bool DEFER>
+// ACT: the action drawn from head partials (merlin_env_act_step) -- its own instantiation, so the plain step keeps its
+// registers (the draw's partial loads in flight take ~40 more)
+template <int SP, bool DEFER, bool ACT = false>
 __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
     __shared__ uint32_t rows[SP][SBLK];
     const int lane = threadIdx.x;
@@ -796,8 +798,11 @@ __global__ __launch_bounds__(SBLK) void k_env_step(EnvDev E, StepOut O) {
     for (int t = 0; t < O.n_steps; t++) {
         // merlin_env_act_step: the action is drawn here from the acting GEMM's head partials (one launch instead of
         // k_act_draw + this kernel); otherwise read from the caller's actions
-        const int64_t a = O.act.part ? (int64_t)act_from_parts(O.act, E.n, i)
-                                     : O.actions[(size_t)t * O.action_stride + i];
+        int64_t a;
+        if constexpr (ACT)
+            a = (int64_t)act_from_parts(O.act, E.n, i);
+        else
+            a = O.actions[(size_t)t * O.action_stride + i];
         steps += 1;
         const int fx = ax + ((dir == 0) - (dir == 2));
         const int fy = ay + ((dir == 1) - (dir == 3));
@@ -953,7 +958,10 @@ static hipError_t launch_step_sp(const EnvDev &E, const StepOut &O, hipStream_t 
     } else if (O.n_steps == 1) {  // also the fused draw + step (merlin_env_act_step): the generator stays out of the
         // step kernel (k_env_step<SP, false> with it inlined takes 241 VGPRs + 92 B of scratch per lane: 15.7 against
         // 8 us per 4096-env step, profiles/r05c_kernel_stats.md)  // empty look-ahead slots reset in k_env_fallback
-        hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
+        if (O.act.part)
+            hipLaunchKernelGGL((k_env_step<SP, true, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
+        else
+            hipLaunchKernelGGL((k_env_step<SP, true>), dim3(nb), dim3(SBLK), 0, s, E, O);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         // (no_fallback: the caller refills every used slot after every step, before the next one -- PPO's rollout --

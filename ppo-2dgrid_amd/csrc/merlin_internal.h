@@ -57,6 +57,7 @@ constexpr int REFILL_EVERY = 16;
 // The acting tail shared by merlin_act.hip (k_act_heads, k_act_draw) and the fused draw + env step
 // (merlin_env.hip, merlin_env_act_step): log-softmax, argmax or the counter-keyed exponential-race draw.
 constexpr int ACT_MAXA = 8;
+constexpr int ACT_PARTS_UNROLL = 8;  // head-partial chunks summed with all loads in flight (act_from_parts)
 
 
 __device__ __forceinline__ float relu_nan(float v) { return v != v ? v : fmaxf(v, 0.0f); }  // torch.relu keeps NaN
@@ -87,9 +88,12 @@ __device__ __forceinline__ int act_finish(const float (&acc)[ACT_MAXA + 1], cons
                                            float *__restrict__ logp, float *__restrict__ value) {
     float zl[ACT_MAXA], m = -INFINITY;
     int amax = 0;
+    float bj[ACT_MAXA];  // every bias load issued before any is used (index clamped into [0, A): no load behind a branch)
+#pragma unroll
+    for (int j = 0; j < ACT_MAXA; j++) bj[j] = ba[j < A ? j : 0];
 #pragma unroll
     for (int j = 0; j < ACT_MAXA; j++) {
-        zl[j] = j < A ? acc[j] + ba[j] : -INFINITY;
+        zl[j] = j < A ? acc[j] + bj[j] : -INFINITY;
         if (zl[j] > m) {  // first maximum (torch.argmax)
             m = zl[j];
             amax = j;
@@ -146,14 +150,42 @@ struct ActIn {
 };
 
 __device__ __forceinline__ int act_from_parts(const ActIn &c, int64_t n, int64_t k) {
-    float4 a = c.part[k], v = c.part[(int64_t)c.P * n + k];
-    for (int p = 1; p < c.P; p++) {
-        const float4 x = c.part[(int64_t)p * n + k], y = c.part[(int64_t)(c.P + p) * n + k];
-        a.x += x.x;
-        a.y += x.y;
-        a.z += x.z;
-        a.w += x.w;
-        v.x += y.x;
+    float4 a, v;
+    if (c.P <= ACT_PARTS_UNROLL) {
+        // the common widths (8 chunk partials: the acting GEMM's heads epilogue, merlin_group_act): every partial's
+        // load issued first (indices clamped into [0, P): no load behind a branch, one round trip instead of P), then
+        // the same ordered sums as the loop below -- the same bits
+        float4 xs[ACT_PARTS_UNROLL];
+        float ys[ACT_PARTS_UNROLL];  // the critic's partials: only their first lane is the value's
+#pragma unroll
+        for (int p = 0; p < ACT_PARTS_UNROLL; p++) {
+            const int q = p < c.P ? p : 0;
+            xs[p] = c.part[(int64_t)q * n + k];
+            ys[p] = reinterpret_cast<const float *>(c.part + (int64_t)(c.P + q) * n + k)[0];
+        }
+        a = xs[0];
+        v = make_float4(ys[0], 0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int p = 1; p < ACT_PARTS_UNROLL; p++) {
+            if (p < c.P) {
+                a.x += xs[p].x;
+                a.y += xs[p].y;
+                a.z += xs[p].z;
+                a.w += xs[p].w;
+                v.x += ys[p];
+            }
+        }
+    } else {
+        a = c.part[k];
+        v = c.part[(int64_t)c.P * n + k];
+        for (int p = 1; p < c.P; p++) {
+            const float4 x = c.part[(int64_t)p * n + k], y = c.part[(int64_t)(c.P + p) * n + k];
+            a.x += x.x;
+            a.y += x.y;
+            a.z += x.z;
+            a.w += x.w;
+            v.x += y.x;
+        }
     }
     float acc[ACT_MAXA + 1];
 #pragma unroll
