@@ -480,7 +480,10 @@ __device__ __forceinline__ void h3_ntp_body(const float *__restrict__ A, const u
             const int col = n0 + wn * WTN + j * 32 + fr;
             bv[j] = bias[(int64_t)t * N + col];
 #pragma unroll
-            for (int o = 0; o < 4; o++) wv[o][j] = o < nh ? hw[(int64_t)o * N + col] : 0.0f;
+            for (int o = 0; o < 4; o++) {  // loaded unconditionally (row clamped into [0, nh)): no load behind a branch
+                const float x = hw[(int64_t)(o < nh ? o : 0) * N + col];
+                wv[o][j] = o < nh ? x : 0.0f;
+            }
         }
         float *part = hd.part + ((int64_t)(t * tiles_n + tn) * WGN + wn) * M * 4;
 #pragma unroll

@@ -725,7 +725,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pqg(const p_u32x4 *__rest
             const int col = n0 + wn * WTN + j * 32 + fr;
             bv[j] = bias[(int64_t)t * N + col];
 #pragma unroll
-            for (int o = 0; o < 4; o++) wv[o][j] = o < nh ? hw[(int64_t)o * N + col] : 0.0f;
+            for (int o = 0; o < 4; o++) {  // loaded unconditionally (row clamped into [0, nh)): no load behind a branch
+                const float x = hw[(int64_t)(o < nh ? o : 0) * N + col];
+                wv[o][j] = o < nh ? x : 0.0f;
+            }
         }
         float *part = hpart + ((int64_t)(t * tiles_n + tn) * WGN + wn) * M * 4;
 #pragma unroll
