@@ -138,14 +138,17 @@ __global__ __launch_bounds__(GF_T) void k_group_fc1(const float *__restrict__ a3
 #pragma unroll
         for (int i = 0; i < 9; i++) wr[c][i] = wrow[(size_t)c * GA_K + 64 * i];
     float bn[4], hw[4][4];
+    const int na = tower == 0 ? A : 1;  // the tower's head rows: the task's A logits (actor) or its value (critic)
+    const float *hsrc = tower == 0 ? Wa + (size_t)wg * A * GA_H : Wc + (size_t)wg * GA_H;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
         const int n = n0 + c;
         bn[c] = b4[(size_t)wt * GA_H + n];
 #pragma unroll
-        for (int a = 0; a < 4; a++)
-            hw[c][a] = tower == 0 ? (a < A ? Wa[((size_t)wg * A + a) * GA_H + n] : 0.0f)
-                                  : (a == 0 ? Wc[(size_t)wg * GA_H + n] : 0.0f);
+        for (int a = 0; a < 4; a++) {  // loaded unconditionally (row clamped into the tower's heads), then masked
+            const float x = hsrc[(size_t)(a < na ? a : 0) * GA_H + n];
+            hw[c][a] = a < na ? x : 0.0f;
+        }
     }
     float x[9];
 #pragma unroll

@@ -160,9 +160,15 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
     const int c = threadIdx.x % H4, r0 = threadIdx.x / H4;
     const int nw = t == 0 ? A : 1;
     float4 w[NA], accw[NA];
+    // the head-gradient source of this tower (actor: dlogits [n][A], critic: dvalue [n]): every load below is issued
+    // unconditionally from it (index clamped into [0, nw)) and masked after, so no load waits behind a branch
+    const float *dsrc = t == 0 ? dlogits : dvalue;
+    const int dstride = t == 0 ? A : 1;
+    const float4 *wsrc = t == 0 ? wa : wc;
 #pragma unroll
     for (int j = 0; j < NA; j++) {
-        w[j] = j < nw ? (t == 0 ? wa[j * H4 + c] : wc[c]) : f4_zero();
+        const float4 x = wsrc[(j < nw ? j : 0) * H4 + c];
+        w[j] = j < nw ? x : f4_zero();
         accw[j] = f4_zero();
     }
     float sc = 1.0f, sc2 = H3_LO_SCALE;
@@ -208,8 +214,10 @@ __global__ __launch_bounds__(EBLK) void k_head_bwd(const float4 *__restrict__ h,
             const int64_t rk = std::min<int64_t>(r + k * R, hi - 1);
             hv[k] = h[base + (size_t)rk * H4 + c];
 #pragma unroll
-            for (int j = 0; j < NA; j++)
-                d[k][j] = j < nw ? (t == 0 ? dlogits[rk * A + j] : dvalue[rk]) : 0.0f;
+            for (int j = 0; j < NA; j++) {
+                const float x = dsrc[rk * dstride + (j < nw ? j : 0)];
+                d[k][j] = j < nw ? x : 0.0f;
+            }
         }
 #pragma unroll
         for (int k = 0; k < HEAD_ROWS; k++) {

@@ -92,8 +92,10 @@ __global__ __launch_bounds__(LOSS_BLK) void k_ppo_loss(const float *__restrict__
         float z[MAXA], lp[MAXA], p[MAXA];
         float m = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < MAXA; j++) {
-            z[j] = j < A ? logits[u * A + j] + (bias_a ? bias_a[j] : 0.0f) : -INFINITY;
+        for (int j = 0; j < MAXA; j++) {  // every logit load issued unconditionally (index clamped), then masked
+            const int jj = j < A ? j : 0;
+            const float x = logits[u * A + jj] + (bias_a ? bias_a[jj] : 0.0f);
+            z[j] = j < A ? x : -INFINITY;
             m = fmaxf(m, z[j]);
         }
         float s = 0.0f;

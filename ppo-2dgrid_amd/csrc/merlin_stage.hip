@@ -169,14 +169,16 @@ __global__ __launch_bounds__(WT) void k_stage_bwd_w(const float *__restrict__ HT
         float rh[NH], rg[NG];
         auto load = [&](int vs) {
 #pragma unroll
-            for (int u = 0; u < NH; u++) {
-                const int q = threadIdx.x + u * WT, vl = q / C1;
-                rh[u] = vs + vl < vb ? HT[((size_t)t * NV + vs) * C1 + q] : 0.0f;
+            for (int u = 0; u < NH; u++) {  // (loads unconditional -- rows clamped into the type -- then masked)
+                const int q = threadIdx.x + u * WT, vl = q / C1, in = vs + vl < vb;
+                const float x = HT[((size_t)t * NV + (in ? vs : vb - 1 - vl)) * C1 + q];
+                rh[u] = in ? x : 0.0f;
             }
 #pragma unroll
             for (int u = 0; u < NG; u++) {
-                const int q = threadIdx.x + u * WT, vl = q / C2, co = q - vl * C2;
-                rg[u] = vs + vl < vb ? dT2[((size_t)t * NROW + 4 * (vs + vl) + j) * C2 + co] : 0.0f;
+                const int q = threadIdx.x + u * WT, vl = q / C2, co = q - vl * C2, in = vs + vl < vb;
+                const float x = dT2[((size_t)t * NROW + 4 * (in ? vs + vl : vb - 1) + j) * C2 + co];
+                rg[u] = in ? x : 0.0f;
             }
         };
         load(va);
