@@ -97,13 +97,21 @@ __global__ __launch_bounds__(GC_T) void k_group_conv(const uint32_t *__restrict_
     float acc[9];
 #pragma unroll
     for (int p3 = 0; p3 < 9; p3++) acc[p3] = 0.0f;
+    // four consecutive k (one tap, ci .. ci + 3: k0 and the tap boundaries are multiples of 4) per LDS read
+    // (ds_read_b128 instead of 4 ds_read_b32: the phase was LDS-issue-bound), each position's products added in
+    // the same order as one k at a time -- the same bits
+    static_assert(GC_KW % 4 == 0, "k in groups of 4");
 #pragma unroll
-    for (int u = 0; u < GC_KW; u++) {
+    for (int u = 0; u < GC_KW; u += 4) {
         const int k = k0 + u, tap = k >> 6, ci = k & 63, ky = tap / 3, kx = tap - ky * 3;
 #pragma unroll
         for (int p3 = 0; p3 < 9; p3++) {
             const int oy = p3 / 3, ox = p3 - oy * 3;
-            acc[p3] += a2f[((oy + ky) * 5 + ox + kx) * 64 + ci] * wk[u];
+            const float4 v = *reinterpret_cast<const float4 *>(a2f + ((oy + ky) * 5 + ox + kx) * 64 + ci);
+            acc[p3] += v.x * wk[u];
+            acc[p3] += v.y * wk[u + 1];
+            acc[p3] += v.z * wk[u + 2];
+            acc[p3] += v.w * wk[u + 3];
         }
     }
 #pragma unroll
