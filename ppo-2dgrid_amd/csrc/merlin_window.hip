@@ -279,6 +279,7 @@ constexpr int64_t ALL_WINDOWS = 458752;  // 4^9 + 3 * 4^8
 // 16 lanes of each of the 9 output rows that read them: round 4's per-lane key arithmetic (81 class lookups per lane)
 // made the kernel VALU-bound (35 us per 4096-frame step; 57 us once the compact key's slot skipping was added).
 constexpr int CC_F = 4;  // 1,024 blocks of 256 threads at 4,096 frames: ~4.5 outputs (9 row gathers each) per thread
+template <int CC_U>
 __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict__ codes, int64_t n,
                                                      const float4 *__restrict__ Q, const float4 *__restrict__ b3,
                                                      int T, float4 *__restrict__ Y3, uint32_t *__restrict__ amax,
@@ -311,28 +312,45 @@ __global__ __launch_bounds__(256) void k_codes_conv3(const uint32_t *__restrict_
         }
         __syncthreads();
         const int per_t = nf * 9 * 16;
-        for (int e = threadIdx.x; e < T * per_t; e += 256) {
-            const int t = e / per_t, r = e - t * per_t, c = r & 15, fp = r >> 4, f = fp / 9, p3 = fp - f * 9;
-            const int oy = p3 / 3, ox = p3 - oy * 3;
-            const float4 *qt = Q + (size_t)t * ALL_WINDOWS * 9 * 16 + c;
-            float4 v[9];
+        // CC_U outputs per thread and round, all their 9 CC_U row gathers issued before any is summed (outputs past
+        // the block's end gather the round's first output's rows and are dropped): ~4.5 outputs per thread took 4-5
+        // dependent gather round trips one after the other
+        for (int e0 = threadIdx.x; e0 < T * per_t; e0 += CC_U * 256) {
+            float4 v[CC_U][9];
+            int tt[CC_U], cc[CC_U], ff[CC_U], pp[CC_U];
 #pragma unroll
-            for (int tap = 0; tap < 9; tap++) {
-                const int ky = tap / 3, kx = tap - ky * 3;
-                v[tap] = qt[((size_t)keys[f][(oy + ky) * 5 + ox + kx] * 9 + tap) * 16];
+            for (int h = 0; h < CC_U; h++) {
+                const int e = e0 + h * 256 < T * per_t ? e0 + h * 256 : e0;
+                const int t = e / per_t, r = e - t * per_t, c = r & 15, fp = r >> 4, f = fp / 9, p3 = fp - f * 9;
+                const int oy = p3 / 3, ox = p3 - oy * 3;
+                const float4 *qt = Q + (size_t)t * ALL_WINDOWS * 9 * 16 + c;
+#pragma unroll
+                for (int tap = 0; tap < 9; tap++) {
+                    const int ky = tap / 3, kx = tap - ky * 3;
+                    v[h][tap] = qt[((size_t)keys[f][(oy + ky) * 5 + ox + kx] * 9 + tap) * 16];
+                }
+                tt[h] = t;
+                cc[h] = c;
+                ff[h] = f;
+                pp[h] = p3;
             }
-            float4 acc = v[0];
 #pragma unroll
-            for (int tap = 1; tap < 9; tap++) f4_add(acc, v[tap]);
-            const float4 b = b3[t * 16 + c];
-            const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
-                                         relu_nan(acc.w + b.w));
-            Y3[(((size_t)t * n + f0 + f) * 9 + p3) * 16 + c] = y;
-            if (amax) {
-                const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
-                                            std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
-                if (t == 0) mx[0] = std::max(mx[0], m);
-                else mx[1] = std::max(mx[1], m);
+            for (int h = 0; h < CC_U; h++) {
+                if (e0 + h * 256 >= T * per_t) break;
+                const int t = tt[h], c = cc[h];
+                float4 acc = v[h][0];
+#pragma unroll
+                for (int tap = 1; tap < 9; tap++) f4_add(acc, v[h][tap]);
+                const float4 b = b3[t * 16 + c];
+                const float4 y = make_float4(relu_nan(acc.x + b.x), relu_nan(acc.y + b.y), relu_nan(acc.z + b.z),
+                                             relu_nan(acc.w + b.w));
+                Y3[(((size_t)t * n + f0 + ff[h]) * 9 + pp[h]) * 16 + c] = y;
+                if (amax) {
+                    const uint32_t m = std::max(std::max(__float_as_uint(y.x) & 0x7fffffffu, __float_as_uint(y.y) & 0x7fffffffu),
+                                                std::max(__float_as_uint(y.z) & 0x7fffffffu, __float_as_uint(y.w) & 0x7fffffffu));
+                    if (t == 0) mx[0] = std::max(mx[0], m);
+                    else mx[1] = std::max(mx[1], m);
+                }
             }
         }
         __syncthreads();
@@ -740,8 +758,13 @@ hipError_t launch_codes_conv3(const uint32_t *codes, int64_t n, const float *Q, 
     const int64_t total = (int64_t)T * n * 9 * 16;
     if (total <= 0) return hipSuccess;
     const int grid = (int)std::min<int64_t>((n + CC_F - 1) / CC_F, 256 * 32);
-    hipLaunchKernelGGL(k_codes_conv3, dim3(grid), dim3(256), 0, s, codes, n, reinterpret_cast<const float4 *>(Q),
-                       reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), amax, err);
+    // 3 outputs per thread and gather round: at the bench state 20.85 ms per rollout against 21.85 for one output's
+    // gathers at a time, 21.4 for 2 and 21.7 for 5 (scripts/probe_rollout.py, profiles/r06ab_ccu*.log)
+#define CC_GO(U)                                                                                                  \
+    hipLaunchKernelGGL(k_codes_conv3<U>, dim3(grid), dim3(256), 0, s, codes, n, reinterpret_cast<const float4 *>(Q), \
+                       reinterpret_cast<const float4 *>(b3), T, reinterpret_cast<float4 *>(Y3), amax, err)
+    CC_GO(3);
+#undef CC_GO
     return hipGetLastError();
 }
 
