@@ -21,6 +21,8 @@
 //           get_pov_render tile classes (RGBImgPartialObsWrapper, scenario_creator.py:48)
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "merlin_internal.h"
 
 namespace merlin {
@@ -672,7 +674,7 @@ __global__ __launch_bounds__(BLK) void k_env_reset(EnvDev E, const uint8_t *__re
 // Fill the empty look-ahead slots: each one-wave block takes SPAN x 64 envs (SPAN 16: lane l reads the
 // slot flags of envs base + 16*l .. in one 16-B load), packs the empty ones onto consecutive lanes
 // (ballot + prefix count) and generates 64 at a time, one thread per env, from the env's RNG (which
-// stays as it is: the slot holds the state after the generation).  SPAN 16 for the few slots a step
+// stays as it is: the slot holds the state after the generation).  SPAN 4 for the few slots a step
 // uses, SPAN 1 (one wave per 64 envs, all generating at once) after a full reset used every slot.
 template <int SP>
 __device__ __forceinline__ void refill_one(const EnvDev &E, int i, uint32_t (*rows)[BLK], int lane) {
@@ -699,7 +701,7 @@ __global__ __launch_bounds__(BLK) void k_env_refill(EnvDev E) {
     __shared__ int queue[BLK];
     const int lane = threadIdx.x;
     const unsigned long long below = (1ull << lane) - 1ull;
-    static_assert(SPAN == 1 || SPAN == 16, "refill span");
+    static_assert(SPAN == 1 || SPAN == 4 || SPAN == 16, "refill span");
     const int64_t base = ((int64_t)blockIdx.x * BLK + lane) * SPAN;  // this lane's first env
     uint32_t fl[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
     if (SPAN == 16 && base + SPAN <= E.n) {
@@ -708,6 +710,8 @@ __global__ __launch_bounds__(BLK) void k_env_refill(EnvDev E) {
         fl[1] = v.y;
         fl[2] = v.z;
         fl[3] = v.w;
+    } else if (SPAN == 4 && base + SPAN <= E.n) {
+        fl[0] = *reinterpret_cast<const uint32_t *>(E.pg_valid + base);
     } else {
         for (int b = 0; b < SPAN; b++)
             if (base + b < E.n && !E.pg_valid[base + b]) fl[b >> 2] &= ~(0xffu << (8 * (b & 3)));
@@ -929,10 +933,12 @@ __global__ __launch_bounds__(256) void k_env_full_obs(EnvDev E, uint8_t *__restr
 
 template <int SP>
 static hipError_t launch_refill_sp(const EnvDev &E, bool full, hipStream_t s) {
+    // after steps: 4 envs per lane (16 one-wave blocks at 4,096 envs; 16 per lane, 4 blocks: each wave waits for the
+    // slowest of more generations) -- 20.75 / 20.91 against 21.09 / 20.97 ms per rollout (profiles/r06ad_span*.log)
     if (full)
         hipLaunchKernelGGL((k_env_refill<SP, 1>), dim3((E.n + BLK - 1) / BLK), dim3(BLK), 0, s, E);
     else
-        hipLaunchKernelGGL((k_env_refill<SP, 16>), dim3((E.n + BLK * 16 - 1) / (BLK * 16)), dim3(BLK), 0, s, E);
+        hipLaunchKernelGGL((k_env_refill<SP, 4>), dim3((E.n + BLK * 4 - 1) / (BLK * 4)), dim3(BLK), 0, s, E);
     return hipGetLastError();
 }
 
