@@ -339,6 +339,8 @@ def h3_gemm_names(nat):
     heads = nat.H3_HEADS_EPILOGUE and nat.lib().merlin_h3_heads_parts(512, nat.H3_NT_CFG["fwd"]) > 0
     fwd = H3_NT_NAMES.get(nat.H3_NT_CFG["fwd"], "?").format(2 if heads else 1)  # EPI 2: the heads in the epilogue
     out = {"gemm_fc1_dgrad": (H3_NT_NAMES.get(nat.H3_NT_CFG["dgrad"], "?").format(0),)}
+    if not FS.WINDOW_H3 and FS.WINDOW_BWD_HIP:  # conv3's per-window GEMM on the exact-f32 kernel (_native.window_gemm_fwd)
+        out["gemm_window_fwd"] = ("k_winfwd",)
     dzp = FS.DZ_PLANES and FS.PATCH_REUSE == "gather"
     if dzp:  # dz leaves the heads' backward as planes: the input gradient on the plane-operand DMA kernel (cfg 62)
         out["gemm_fc1_dgrad"] = ("k_h3_pq<128, 192, 4, 2, 0, 16>",)

@@ -82,32 +82,47 @@ def stats(tag):
         print("no step sequence:", e)
 
 
-def pmc(tag):
-    res = {}
-    # prof_pmc_*: the bench loop; prof_pmcenv_*: bench.py --env-tier-only (2M envs), whose
-    # k_env_step launches are keyed k_env_step_large (bench.py tiers.env_only_2M_envs)
-    for pre, rename in (("prof_pmc_", {}), ("prof_pmcenv_", {"k_env_step": "k_env_step_large"})):
+def env_rename(name):
+    """bench.py --env-tier-only (2M envs): every k_env_step instantiation is keyed k_env_step_large (bench.py
+    env_large_tier's roofline.traffic).  Its other kernels are dropped: they would collide with the bench loop's
+    entries of the same name."""
+    return "k_env_step_large" if name.startswith("k_env_step") else None
+
+
+# bench.py --env-tier-only launches k_env_step 1 + 16 (auto-reset on) + 16 (auto-reset off, the roofline timing)
+# times: the last 16 in dispatch order are the roofline's launches
+ENV_TIMED = 16
+
+
+def pmc(tag, merge=False):
+    out = os.path.join(DEST, f"{tag}_pmc.json")
+    res = json.load(open(out)) if merge and os.path.exists(out) else {}
+    # prof_pmc_*: the bench loop; prof_pmcenv_*: bench.py --env-tier-only
+    for pre, rename, last in (("prof_pmc_", None, None), ("prof_pmcenv_", env_rename, ENV_TIMED)):
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             src = os.path.join(OUT, f"{pre}{counter}", "run_counter_collection.csv")
             if os.path.exists(src):
-                collect(res, src, counter, rename)
+                collect(res, src, counter, rename, last)
     for k, d in res.items():
         if "fetch_size_kb" in d and "write_size_kb" in d:
             d["hbm_bytes_per_launch"] = int((2 * d["fetch_size_kb"] + d["write_size_kb"]) * 1024)
     if res:
-        json.dump(res, open(os.path.join(DEST, f"{tag}_pmc.json"), "w"), indent=1)
+        json.dump(res, open(out, "w"), indent=1)
 
 
-def collect(res, src, counter, rename):
+def collect(res, src, counter, rename=None, last=None):
     per = {}
     for r in csv.DictReader(open(src)):
         name = kname(r["Kernel_Name"])
-        name = rename.get(name, name)
+        name = rename(name) if rename else name
+        if name is None:
+            continue
         per.setdefault(name, []).append((int(r["Dispatch_Id"]), int(r["Grid_Size"]), float(r["Counter_Value"])))
     for k, vals in per.items():
-        vals = timed_tail(sorted(vals))  # dispatch order; the timed iterations' launches
+        # dispatch order; the timed iterations' launches
+        vals = sorted(vals)[-last:] if last else timed_tail(sorted(vals))
         d = res.setdefault(k, {"grid_max": max(v[1] for v in vals), "launches": len(vals),
-                               "timed_frac": TIMED_FRAC})
+                               "timed_frac": TIMED_FRAC if not last else round(len(vals) / len(per[k]), 4)})
         d[counter.lower() + "_kb"] = sum(v[2] for v in vals) / len(vals)
 
 
@@ -115,6 +130,10 @@ if __name__ == "__main__":
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     if len(sys.argv) > 2:
         DEST = os.path.abspath(sys.argv[2])
+    if os.environ.get("PMC_MERGE_ENV"):  # add the --env-tier-only passes to an existing <tag>_pmc.json
+        pmc(tag, merge=True)
+        print("merged env-tier PMC into", tag)
+        sys.exit(0)
     stats(tag)
     pmc(tag)
     print("wrote profiles for", tag)

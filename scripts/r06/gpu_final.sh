@@ -5,10 +5,10 @@
 R="$GRAFT_REPO_ROOT"; cd "$R"; mkdir -p gpurun_out
 crash() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
 timeout -k 10 800 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/ \
-    > gpurun_out/r06f2_pytest_gpu.log 2>&1; rc=$?
-tail -3 gpurun_out/r06f2_pytest_gpu.log; grep -E "FAILED|Error" gpurun_out/r06f2_pytest_gpu.log | head -10
+    > gpurun_out/r06zf_pytest_gpu.log 2>&1; rc=$?
+tail -3 gpurun_out/r06zf_pytest_gpu.log; grep -E "FAILED|Error" gpurun_out/r06zf_pytest_gpu.log | head -10
 crash $rc && exit $rc
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r06f2_smoke.log 2>&1; rc=$?
-tail -1 gpurun_out/r06f2_smoke.log; crash $rc && exit $rc
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r06zf_smoke.log 2>&1; rc=$?
+tail -1 gpurun_out/r06zf_smoke.log; crash $rc && exit $rc
 exit 0
