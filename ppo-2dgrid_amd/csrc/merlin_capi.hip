@@ -1160,7 +1160,11 @@ int merlin_h3_gemm_nt(const float *A, const uint32_t *amax_a, const void *B, con
 int merlin_h3_gemm_nt_planes(const void *A_planes, const uint32_t *amax_a, const void *B, const uint32_t *amax_b,
                              int64_t M, int32_t N, int32_t K, int32_t towers, int64_t a_stride, int64_t b_stride,
                              const float *bias, float *C, int64_t c_stride, int32_t cfg, void *stream) {
+#ifdef MERLIN_PROBES
+    if (cfg < 60 || cfg >= 80) return fail(MERLIN_E_UNSUPPORTED, "plane-operand cfgs are 60..79 (probe build)");
+#else
     if (cfg < 60 || cfg >= 70) return fail(MERLIN_E_UNSUPPORTED, "plane-operand cfgs are 60..69");
+#endif
     return h3_gemm_nt(static_cast<const float *>(A_planes), amax_a, B, amax_b, M, N, K, towers, a_stride, b_stride,
                       bias, C, c_stride, nullptr, nullptr, cfg, stream);
 }

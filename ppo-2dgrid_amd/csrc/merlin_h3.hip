@@ -1627,7 +1627,12 @@ hipError_t launch_h3_gemm_nt(const float *A, const uint32_t *amaxA, const void *
     nt_launch<BM, BN, WM, WN, PIPE>(A, b, amaxA, amaxB, M, N, K, T, a_stride, sB, bias, C, c_stride, P, a_rows, hd, s, \
                                     a_is_planes)
     if (a_is_planes && (cfg < 10 || cfg > 14) && cfg != 60) return hipErrorInvalidValue;
-    if (cfg >= 60 && cfg < 70) {  // both operands as plane images (merlin_h3p.hip)
+#ifdef MERLIN_PROBES
+    constexpr int PLANE_CFG_END = 80;  // + the probe ablations 70..74
+#else
+    constexpr int PLANE_CFG_END = 70;
+#endif
+    if (cfg >= 60 && cfg < PLANE_CFG_END) {  // both operands as plane images (merlin_h3p.hip)
         if (P || ((a_rows || head_part) && !a_is_planes)) return hipErrorInvalidValue;
         return launch_h3p_gemm_nt(A, amaxA, B, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, cfg, s, a_rows,
                                   head_w0, n_actions, head_w1, head_part);

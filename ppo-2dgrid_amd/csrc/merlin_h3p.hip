@@ -221,8 +221,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
     static_for<NR>([&](auto K_) __attribute__((always_inline)) { rd(f0, K_, 0, IC<0>{}); });
     static_for<NK>([&](auto KT) __attribute__((always_inline)) {
         constexpr int kt = decltype(KT)::value, st = kt % NS, sn = (kt + 1) % NS;
-        if constexpr (kt + D < NK && ABL != 1) issue(kt + D, (kt + D) % NS);  // the stage read in step kt - 1
-        // (ABL 1, a probe: no DMA in the loop -- the MFMA / fragment-read side alone, wrong results)
+        if constexpr (kt + D < NK && !(ABL & 1)) issue(kt + D, (kt + D) % NS);  // the stage read in step kt - 1
+        // (ABL bit 1, a probe: no DMA in the loop -- the MFMA / fragment-read side alone, wrong results)
         __builtin_amdgcn_sched_barrier(0);
         half(f0, f1, (uint32_t)st * STG_B, IC<1>{}, IC<1>{});  // MFMAs of half 0, reads of half 1
         if constexpr (kt + 1 < NK) {
@@ -240,6 +240,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_h3_pq(const p_u32x4 *__restr
 
     const float inv = p_pow2(-eA), invB = p_pow2(-eB);
     float *Ct = C + t * sC;
+    if constexpr ((ABL & 2) != 0) {  // probe: no tile stores -- one sum per wave keeps the MFMAs live (wrong results)
+        float sum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int j = 0; j < TN; j++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) sum += hi[i][j][r] + lo[i][j][r];
+        if (lane == 0 && m0 + w < M) Ct[(m0 + w) * N + n0] = sum;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < TN; j++) {
         const int col = n0 + wn * WTN + j * 32 + fr;
@@ -830,6 +841,13 @@ hipError_t launch_h3p_gemm_nt(const void *A, const uint32_t *amaxA, const void *
         case 64: return pq_launch<256, 192, 4, 2, 2, true, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 67: return pq_launch<128, 192, 4, 2, 3, false, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
         case 61: return pq_launch<128, 192, 4, 2, 3, false, 1, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        // ABL 2: no tile stores (the epilogue's share); ABL 3: neither DMA in the loop nor stores -- 70 / 71 = 62's,
+        // 72 / 73 = 60's (the forward's 128 x 256 tile)
+        case 70: return pq_launch<128, 192, 4, 2, 3, false, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 71: return pq_launch<128, 192, 4, 2, 3, false, 3>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 72: return pq_launch<128, 256, 2, 4, 3, false, 2>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 73: return pq_launch<128, 256, 2, 4, 3, false, 3>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
+        case 74: return pq_launch<128, 256, 2, 4, 3, false, 1>(A, B, amaxA, amaxB, M, N, K, T, a_stride, b_stride, bias, C, c_stride, s);
 #endif
         default: return hipErrorInvalidValue;
     }
